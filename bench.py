@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GPT-2-small local-SGD training throughput (samples/s) on N MI355X peers.
+
+BASELINE.json metric: "samples/sec GPT-2-small local-SGD at 1/2/4/8 peers; step-time under
+1-peer drop". Config 2: GPT-2-small bf16, one volunteer peer per GPU, local-SGD with H=4 local
+AdamW steps between averaging rounds over RCCL/xGMI.
+
+One "step" = one local AdamW step of every peer (fwd + bwd + fused AdamW on the full model);
+every H-th step additionally runs the averaging round, which is therefore inside the timed
+region at its real 1/H frequency. Weak scaling: per-peer batch is fixed, global batch = N x B.
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W` (N>1 under torchrun, one
+rank per GPU). Rank 0 prints ONE JSON line; `value` is the whole-job samples/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+from distributedvolunteercomputing_amd.models.gpt2 import GPT2, GPT2Config
+from distributedvolunteercomputing_amd.parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer
+from distributedvolunteercomputing_amd.parallel.peer_group import PeerGroup
+
+BF16_DENSE_PEAK = 2.5e15  # MI355X dense bf16 MFMA, no sparsity
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--batch", type=int, default=32, help="per-peer micro-batch (sequences)")
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--H", type=int, default=4)
+    ap.add_argument("--algo", default="rccl", choices=["rccl", "rs_ag", "butterfly", "ring"])
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cuda = torch.cuda.is_available()
+    if cuda:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group("nccl" if cuda else "gloo", device_id=device if cuda else None)
+    group = PeerGroup.from_default(device) if world > 1 else None
+
+    cfg = GPT2Config.preset(a.model)
+    cfg.n_ctx = max(cfg.n_ctx, a.seq)
+    torch.manual_seed(0)
+    model = GPT2(cfg).to(device=device, dtype=torch.bfloat16)
+    tcfg = LocalSGDConfig(H=a.H, algo=a.algo)
+    trainer = LocalSGDTrainer(model, tcfg, group=group, device=device)
+
+    # synthetic token stream: a pool of distinct batches per peer (different shard per rank)
+    g = torch.Generator(device=device)
+    g.manual_seed(1000 + rank)
+    pool = [torch.randint(0, cfg.vocab_size, (a.batch, a.seq + 1), device=device, generator=g) for _ in range(4)]
+
+    def batch(i):
+        b = pool[i % len(pool)]
+        return b[:, :-1], b[:, 1:]
+
+    def sync_all():
+        if cuda:
+            torch.cuda.synchronize()
+        if group is not None:
+            group.barrier()
+
+    for i in range(a.warmup):
+        trainer.step(*batch(i))
+    sync_all()
+    t0 = time.perf_counter()
+    last = None
+    for i in range(a.steps):
+        last = trainer.step(*batch(a.warmup + i))
+    sync_all()
+    dt = time.perf_counter() - t0
+    loss = float(last.extra["loss_t"]) if last is not None else float("nan")
+    if group is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    samples = world * a.batch * a.steps
+    sps = samples / dt
+    tok_s = sps * a.seq
+    flops = model.flops_per_token(a.seq) * tok_s
+    if rank == 0:
+        rec = {
+            "metric": "samples/sec GPT-2-small local-SGD",
+            "value": round(sps, 3),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random tokens, random-init weights)",
+            "config": {
+                "model": a.model,
+                "global_batch": world * a.batch,
+                "per_peer_batch": a.batch,
+                "seq_len": a.seq,
+                "parallelism": f"local-sgd dp{world} H={a.H} allreduce={a.algo}",
+            },
+            "tokens_per_s": round(tok_s, 1),
+            "model_tflops_per_gpu": round(flops / world / 1e12, 2),
+            "mfu_bf16_dense": round(flops / world / BF16_DENSE_PEAK, 4),
+            "final_loss": round(loss, 4),
+            "sync_ms": round(trainer.last_sync_ms, 3),
+        }
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,247 @@
+// Torch bindings for the gfx950 kernels. Every entry point validates shapes/dtypes on the
+// host (a wrong shape must never reach a hand-written kernel: an out-of-bounds access can
+// reset the whole node) and launches on the caller's current HIP stream, so the ops compose
+// with torch streams and hipGraph capture.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include "kernels/vcx_api.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_DT(x, dt) TORCH_CHECK((x).scalar_type() == (dt), #x " has wrong dtype ", (x).scalar_type())
+#define CHECK_IN(x, dt) \
+  CHECK_CUDA(x);        \
+  CHECK_CONTIG(x);      \
+  CHECK_DT(x, dt)
+
+const auto kBF = at::kBFloat16;
+const auto kF = at::kFloat;
+
+void* opt_ptr(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+// ------------------------------------------------------------------ optimizer / local SGD
+void grad_sumsq(at::Tensor g, at::Tensor ostate) {
+  CHECK_IN(g, kBF);
+  CHECK_IN(ostate, kF);
+  TORCH_CHECK(g.numel() % 8 == 0, "flat buffer length must be a multiple of 8");
+  vcx_grad_sumsq(g.data_ptr(), g.numel(), ostate.data_ptr<float>(), cur_stream());
+}
+
+void adam_prologue(at::Tensor ostate, double max_norm) {
+  CHECK_IN(ostate, kF);
+  TORCH_CHECK(ostate.numel() >= 4);
+  vcx_adam_prologue(ostate.data_ptr<float>(), (float)max_norm, cur_stream());
+}
+
+void adamw_flat(at::Tensor param, at::Tensor grad, at::Tensor master, at::Tensor m, at::Tensor v, int64_t n_decay,
+                at::Tensor ostate, double beta1, double beta2, double eps, double wd) {
+  CHECK_IN(param, kBF);
+  CHECK_IN(grad, kBF);
+  CHECK_IN(master, kF);
+  CHECK_IN(m, kF);
+  CHECK_IN(v, kF);
+  CHECK_IN(ostate, kF);
+  const int64_t n = param.numel();
+  TORCH_CHECK(n % 8 == 0 && grad.numel() == n && master.numel() == n && m.numel() == n && v.numel() == n,
+              "adamw_flat: buffers must share a length that is a multiple of 8");
+  TORCH_CHECK(n_decay >= 0 && n_decay <= n && n_decay % 8 == 0);
+  vcx_adamw_flat(param.data_ptr(), grad.data_ptr(), master.data_ptr<float>(), m.data_ptr<float>(),
+                 v.data_ptr<float>(), n, n_decay, ostate.data_ptr<float>(), (float)beta1, (float)beta2, (float)eps,
+                 (float)wd, cur_stream());
+}
+
+void lsgd_delta(at::Tensor master, at::Tensor anchor, at::Tensor delta) {
+  CHECK_IN(master, kF);
+  CHECK_IN(anchor, kF);
+  CHECK_IN(delta, kBF);
+  const int64_t n = master.numel();
+  TORCH_CHECK(n % 8 == 0 && anchor.numel() == n && delta.numel() == n);
+  vcx_lsgd_delta(master.data_ptr<float>(), anchor.data_ptr<float>(), delta.data_ptr(), n, cur_stream());
+}
+
+void lsgd_apply(at::Tensor avg, at::Tensor anchor, at::Tensor master, at::Tensor param,
+                c10::optional<at::Tensor> mom, double outer_lr, double mu, bool nesterov, double avg_scale) {
+  CHECK_IN(avg, kBF);
+  CHECK_IN(anchor, kF);
+  CHECK_IN(master, kF);
+  CHECK_IN(param, kBF);
+  const int64_t n = avg.numel();
+  TORCH_CHECK(n % 8 == 0 && anchor.numel() == n && master.numel() == n && param.numel() == n);
+  if (mom.has_value()) {
+    CHECK_IN((*mom), kF);
+    TORCH_CHECK(mom->numel() == n);
+  }
+  vcx_lsgd_apply(avg.data_ptr(), anchor.data_ptr<float>(), master.data_ptr<float>(), param.data_ptr(),
+                 mom.has_value() ? mom->data_ptr<float>() : nullptr, n, (float)outer_lr, (float)mu, nesterov ? 1 : 0,
+                 (float)avg_scale, cur_stream());
+}
+
+void f32_to_bf16(at::Tensor src, at::Tensor dst) {
+  CHECK_IN(src, kF);
+  CHECK_IN(dst, kBF);
+  TORCH_CHECK(src.numel() == dst.numel() && src.numel() % 8 == 0);
+  vcx_f32_to_bf16(src.data_ptr<float>(), dst.data_ptr(), src.numel(), cur_stream());
+}
+
+void axpy_bf16(at::Tensor src, at::Tensor acc, double scale) {
+  CHECK_IN(src, kBF);
+  CHECK_IN(acc, kBF);
+  TORCH_CHECK(src.numel() == acc.numel() && src.numel() % 8 == 0);
+  vcx_axpy_bf16(src.data_ptr(), acc.data_ptr(), src.numel(), (float)scale, cur_stream());
+}
+
+// ------------------------------------------------------------------ norms / activations
+std::vector<at::Tensor> ln_fwd(at::Tensor a, c10::optional<at::Tensor> b, at::Tensor w, c10::optional<at::Tensor> bias,
+                               double eps, bool rms) {
+  CHECK_IN(a, kBF);
+  CHECK_IN(w, kBF);
+  const int C = (int)a.size(-1);
+  const int64_t R = a.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 8192, "layernorm: C must be a multiple of 8 and <= 8192");
+  TORCH_CHECK(w.numel() == C);
+  TORCH_CHECK(R < INT32_MAX);
+  if (b.has_value()) {
+    CHECK_IN((*b), kBF);
+    TORCH_CHECK(b->sizes() == a.sizes());
+  }
+  if (bias.has_value()) {
+    CHECK_IN((*bias), kBF);
+    TORCH_CHECK(bias->numel() == C);
+  }
+  auto y = at::empty_like(a);
+  at::Tensor xout = b.has_value() ? at::empty_like(a) : a;
+  auto mean = at::empty({R}, a.options().dtype(kF));
+  auto rstd = at::empty({R}, a.options().dtype(kF));
+  vcx_ln_fwd(a.data_ptr(), opt_ptr(b), b.has_value() ? xout.data_ptr() : nullptr, y.data_ptr(), w.data_ptr(),
+             opt_ptr(bias), mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)R, C, (float)eps, rms ? 1 : 0,
+             cur_stream());
+  return {y, xout, mean, rstd};
+}
+
+std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Tensor mean, at::Tensor rstd,
+                               c10::optional<at::Tensor> dres, bool has_bias, bool rms) {
+  CHECK_IN(dy, kBF);
+  CHECK_IN(x, kBF);
+  CHECK_IN(w, kBF);
+  CHECK_IN(mean, kF);
+  CHECK_IN(rstd, kF);
+  const int C = (int)x.size(-1);
+  const int64_t R = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 8192 && dy.sizes() == x.sizes() && w.numel() == C);
+  TORCH_CHECK(mean.numel() == R && rstd.numel() == R);
+  if (dres.has_value()) {
+    CHECK_IN((*dres), kBF);
+    TORCH_CHECK(dres->sizes() == x.sizes());
+  }
+  const int P = vcx_ln_bwd_partials((int)R);
+  auto dx = at::empty_like(x);
+  auto dw_part = at::empty({P, C}, x.options().dtype(kF));
+  at::Tensor db_part, db;
+  auto dw = at::empty({C}, x.options());
+  if (has_bias) {
+    db_part = at::empty({P, C}, x.options().dtype(kF));
+    db = at::empty({C}, x.options());
+  }
+  vcx_ln_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+             opt_ptr(dres), dx.data_ptr(), dw_part.data_ptr<float>(), has_bias ? db_part.data_ptr<float>() : nullptr,
+             dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)R, C, rms ? 1 : 0, cur_stream());
+  if (has_bias) return {dx, dw, db};
+  return {dx, dw};
+}
+
+at::Tensor gelu_fwd(at::Tensor x) {
+  CHECK_IN(x, kBF);
+  TORCH_CHECK(x.numel() % 8 == 0);
+  auto y = at::empty_like(x);
+  vcx_gelu_fwd(x.data_ptr(), y.data_ptr(), x.numel(), cur_stream());
+  return y;
+}
+
+at::Tensor gelu_bwd(at::Tensor x, at::Tensor dy) {
+  CHECK_IN(x, kBF);
+  CHECK_IN(dy, kBF);
+  TORCH_CHECK(x.numel() % 8 == 0 && dy.numel() == x.numel());
+  auto dx = at::empty_like(x);
+  vcx_gelu_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), cur_stream());
+  return dx;
+}
+
+at::Tensor swiglu_fwd(at::Tensor gu) {
+  CHECK_IN(gu, kBF);
+  const int64_t F2 = gu.size(-1);
+  TORCH_CHECK(F2 % 16 == 0, "swiglu: feature dim must be a multiple of 16");
+  const int64_t R = gu.numel() / F2;
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F2 / 2;
+  auto y = at::empty(sizes, gu.options());
+  vcx_swiglu_fwd(gu.data_ptr(), y.data_ptr(), R, (int)(F2 / 2), cur_stream());
+  return y;
+}
+
+at::Tensor swiglu_bwd(at::Tensor gu, at::Tensor dy) {
+  CHECK_IN(gu, kBF);
+  CHECK_IN(dy, kBF);
+  const int64_t F2 = gu.size(-1);
+  TORCH_CHECK(F2 % 16 == 0 && dy.numel() * 2 == gu.numel());
+  auto dgu = at::empty_like(gu);
+  vcx_swiglu_bwd(gu.data_ptr(), dy.data_ptr(), dgu.data_ptr(), gu.numel() / F2, (int)(F2 / 2), cur_stream());
+  return dgu;
+}
+
+std::vector<at::Tensor> xent_fwd(at::Tensor logits, at::Tensor tgt, int64_t V) {
+  CHECK_IN(logits, kBF);
+  CHECK_IN(tgt, at::kLong);
+  TORCH_CHECK(logits.dim() == 2);
+  const int64_t R = logits.size(0), Vp = logits.size(1);
+  TORCH_CHECK(Vp % 8 == 0 && V <= Vp && V > 0 && tgt.numel() == R);
+  auto lse = at::empty({R}, logits.options().dtype(kF));
+  auto loss = at::empty({R}, logits.options().dtype(kF));
+  vcx_xent_fwd(logits.data_ptr(), tgt.data_ptr<int64_t>(), lse.data_ptr<float>(), loss.data_ptr<float>(), R, (int)V,
+               (int)Vp, cur_stream());
+  return {loss, lse};
+}
+
+void xent_bwd(at::Tensor logits, at::Tensor tgt, at::Tensor lse, at::Tensor gscale, at::Tensor dlogits, int64_t V) {
+  CHECK_IN(logits, kBF);
+  CHECK_IN(tgt, at::kLong);
+  CHECK_IN(lse, kF);
+  CHECK_IN(gscale, kF);
+  CHECK_IN(dlogits, kBF);
+  const int64_t R = logits.size(0), Vp = logits.size(1);
+  TORCH_CHECK(logits.dim() == 2 && dlogits.sizes() == logits.sizes() && tgt.numel() == R && lse.numel() == R);
+  TORCH_CHECK(Vp % 8 == 0 && V <= Vp && gscale.numel() >= 1);
+  vcx_xent_bwd(logits.data_ptr(), tgt.data_ptr<int64_t>(), lse.data_ptr<float>(), gscale.data_ptr<float>(),
+               dlogits.data_ptr(), R, (int)V, (int)Vp, cur_stream());
+}
+
+}  // namespace
+
+void vcx_register_vision(pybind11::module& m);
+void vcx_register_compress(pybind11::module& m);
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "gfx950 HIP kernels of distributedvolunteercomputing_amd";
+  m.def("grad_sumsq", &grad_sumsq);
+  m.def("adam_prologue", &adam_prologue);
+  m.def("adamw_flat", &adamw_flat);
+  m.def("lsgd_delta", &lsgd_delta);
+  m.def("lsgd_apply", &lsgd_apply);
+  m.def("f32_to_bf16", &f32_to_bf16);
+  m.def("axpy_bf16", &axpy_bf16);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
+  vcx_register_vision(m);
+  vcx_register_compress(m);
+}

@@ -1,0 +1,442 @@
+// LayerNorm (+ fused residual add), RMSNorm, tanh-GELU and fused softmax-cross-entropy
+// kernels for the transformer training path (gfx950).
+//
+// Shape rules (checked host-side in the binding): row length C % 8 == 0, C <= 8192.
+// One wave64 owns one row; a 256-thread block covers 4 rows. The row is held in registers
+// (CH = ceil(C/512) chunks of 8 elements per lane), so the variance is an exact two-pass
+// computation over registers with a single HBM read of the row.
+#include "vcx_common.h"
+
+namespace vcx {
+
+// ============================================================ LayerNorm forward
+// xsum = a + b (if b != nullptr, written to xout), y = LN(xsum) * w + bias
+template <int CH>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
+                                                      bf16* __restrict__ xout, bf16* __restrict__ y,
+                                                      const bf16* __restrict__ w, const bf16* __restrict__ bias,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      int R, int C, float eps, int rms) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int C8 = C >> 3;
+  const int64_t off = (int64_t)row * C;
+  float v[CH][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int c = lane + k * 64;
+    if (c < C8) {
+      bf16x8 av = *(const bf16x8*)(a + off + c * 8);
+      if (b) {
+        bf16x8 bv = *(const bf16x8*)(b + off + c * 8);
+        bf16x8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] = (bf16)((float)av[j] + (float)bv[j]);
+          v[k][j] = (float)s[j];  // normalise the rounded residual actually stored
+        }
+        *(bf16x8*)(xout + off + c * 8) = s;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = (float)av[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += v[k][j];
+    }
+  }
+  const float invC = 1.f / (float)C;
+  float mean = rms ? 0.f : wave_sum(sum) * invC;
+  float var = 0.f;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int c = lane + k * 64;
+    if (c < C8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = v[k][j] - mean;
+        var = fmaf(d, d, var);
+      }
+    }
+  }
+  var = wave_sum(var) * invC;
+  const float rstd = rsqrtf(var + eps);
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int c = lane + k * 64;
+    if (c < C8) {
+      bf16x8 wv = *(const bf16x8*)(w + c * 8);
+      bf16x8 o;
+      if (bias) {
+        bf16x8 bv = *(const bf16x8*)(bias + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)fmaf((v[k][j] - mean) * rstd, (float)wv[j], (float)bv[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)((v[k][j] - mean) * rstd * (float)wv[j]);
+      }
+      *(bf16x8*)(y + off + c * 8) = o;
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// ============================================================ LayerNorm backward
+// dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat)) + dres
+// per-wave partial dw = sum_rows dy*xhat, db = sum_rows dy -> part[(wave_global), C]
+template <int CH>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                      const bf16* __restrict__ w, const float* __restrict__ mean_in,
+                                                      const float* __restrict__ rstd_in,
+                                                      const bf16* __restrict__ dres, bf16* __restrict__ dx,
+                                                      float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                      int R, int C, int rms) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;
+  const int C8 = C >> 3;
+  const float invC = 1.f / (float)C;
+  float dwacc[CH][8], dbacc[CH][8], wreg[CH][8];
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int c = lane + k * 64;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dwacc[k][j] = 0.f;
+      dbacc[k][j] = 0.f;
+      wreg[k][j] = 0.f;
+    }
+    if (c < C8) {
+      bf16x8 wv = *(const bf16x8*)(w + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wreg[k][j] = (float)wv[j];
+    }
+  }
+  for (int row = gw; row < R; row += nw) {
+    const int64_t off = (int64_t)row * C;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[CH][8], g[CH][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int c = lane + k * 64;
+      if (c < C8) {
+        bf16x8 dv = *(const bf16x8*)(dy + off + c * 8);
+        bf16x8 xv = *(const bf16x8*)(x + off + c * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float d = (float)dv[j];
+          xh[k][j] = ((float)xv[j] - mean) * rstd;
+          g[k][j] = d * wreg[k][j];
+          s1 += g[k][j];
+          s2 = fmaf(g[k][j], xh[k][j], s2);
+          dwacc[k][j] = fmaf(d, xh[k][j], dwacc[k][j]);
+          dbacc[k][j] += d;
+        }
+      }
+    }
+    s1 = rms ? 0.f : wave_sum(s1) * invC;
+    s2 = wave_sum(s2) * invC;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int c = lane + k * 64;
+      if (c < C8) {
+        bf16x8 o;
+        if (dres) {
+          bf16x8 rv = *(const bf16x8*)(dres + off + c * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (bf16)(rstd * (g[k][j] - s1 - xh[k][j] * s2) + (float)rv[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (bf16)(rstd * (g[k][j] - s1 - xh[k][j] * s2));
+        }
+        *(bf16x8*)(dx + off + c * 8) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int c = lane + k * 64;
+    if (c < C8) {
+      float* dwp = dw_part + (int64_t)gw * C + c * 8;
+      *(f32x4*)dwp = f32x4{dwacc[k][0], dwacc[k][1], dwacc[k][2], dwacc[k][3]};
+      *(f32x4*)(dwp + 4) = f32x4{dwacc[k][4], dwacc[k][5], dwacc[k][6], dwacc[k][7]};
+      if (db_part) {
+        float* dbp = db_part + (int64_t)gw * C + c * 8;
+        *(f32x4*)dbp = f32x4{dbacc[k][0], dbacc[k][1], dbacc[k][2], dbacc[k][3]};
+        *(f32x4*)(dbp + 4) = f32x4{dbacc[k][4], dbacc[k][5], dbacc[k][6], dbacc[k][7]};
+      }
+    }
+  }
+}
+
+// Column sums of a [P, C] fp32 partial buffer -> bf16 [C]. One block per 64 columns,
+// 16 waves stride the P rows, LDS combine.
+__global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ part, int P, int C,
+                                                       bf16* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float acc = 0.f;
+  if (c < C) {
+    int p = wid;
+    for (; p + 48 < P; p += 64) {
+      float a0 = part[(int64_t)p * C + c], a1 = part[(int64_t)(p + 16) * C + c];
+      float a2 = part[(int64_t)(p + 32) * C + c], a3 = part[(int64_t)(p + 48) * C + c];
+      acc += (a0 + a1) + (a2 + a3);
+    }
+    for (; p < P; p += 16) acc += part[(int64_t)p * C + c];
+  }
+  red[wid][lane] = acc;
+  __syncthreads();
+  if (wid == 0 && c < C) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[i][lane];
+    out[c] = (bf16)s;
+  }
+}
+
+// ============================================================ tanh-GELU
+__device__ __forceinline__ float gelu_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  float du = k0 * (1.f + 3.f * k1 * x2);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
+}
+
+__global__ void __launch_bounds__(256) gelu_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                        int64_t n8) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    bf16x8 v = *(const bf16x8*)(x + i * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)gelu_f((float)v[j]);
+    *(bf16x8*)(y + i * 8) = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) gelu_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                        bf16* __restrict__ dx, int64_t n8) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    bf16x8 v = *(const bf16x8*)(x + i * 8);
+    bf16x8 g = *(const bf16x8*)(dy + i * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)g[j] * gelu_grad_f((float)v[j]));
+    *(bf16x8*)(dx + i * 8) = o;
+  }
+}
+
+// SwiGLU for the Llama MLP: y = silu(g) * u, over [R, 2F] packed as [g | u] per row.
+__global__ void __launch_bounds__(256) swiglu_fwd_kernel(const bf16* __restrict__ gu, bf16* __restrict__ y,
+                                                          int64_t R, int F) {
+  const int F8 = F >> 3;
+  const int64_t n8 = R * F8;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / F8, c = i - r * F8;
+    bf16x8 g = *(const bf16x8*)(gu + r * 2 * F + c * 8);
+    bf16x8 u = *(const bf16x8*)(gu + r * 2 * F + F + c * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float gf = (float)g[j];
+      o[j] = (bf16)(gf / (1.f + __expf(-gf)) * (float)u[j]);
+    }
+    *(bf16x8*)(y + r * F + c * 8) = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) swiglu_bwd_kernel(const bf16* __restrict__ gu, const bf16* __restrict__ dy,
+                                                          bf16* __restrict__ dgu, int64_t R, int F) {
+  const int F8 = F >> 3;
+  const int64_t n8 = R * F8;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / F8, c = i - r * F8;
+    bf16x8 g = *(const bf16x8*)(gu + r * 2 * F + c * 8);
+    bf16x8 u = *(const bf16x8*)(gu + r * 2 * F + F + c * 8);
+    bf16x8 d = *(const bf16x8*)(dy + r * F + c * 8);
+    bf16x8 dg, du;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float gf = (float)g[j], uf = (float)u[j], df = (float)d[j];
+      float sg = 1.f / (1.f + __expf(-gf));
+      float silu = gf * sg;
+      du[j] = (bf16)(df * silu);
+      dg[j] = (bf16)(df * uf * sg * (1.f + gf * (1.f - sg)));
+    }
+    *(bf16x8*)(dgu + r * 2 * F + c * 8) = dg;
+    *(bf16x8*)(dgu + r * 2 * F + F + c * 8) = du;
+  }
+}
+
+// ============================================================ cross-entropy
+// logits [R, Vp] bf16 (Vp = padded row stride, only the first V columns are real classes).
+// fwd: lse[r], loss[r] = lse - logit[target] (0 for target < 0 = ignore)
+__global__ void __launch_bounds__(256) xent_fwd_kernel(const bf16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                        float* __restrict__ lse_out, float* __restrict__ loss_out,
+                                                        int V, int Vp) {
+  __shared__ float sm[4], ss[4];
+  const int64_t row = blockIdx.x;
+  const bf16* lr = logits + row * Vp;
+  const int V8 = V >> 3;  // full chunks
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x; c < V8; c += 256) {
+    bf16x8 v = *(const bf16x8*)(lr + c * 8);
+    float f[8], cm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f[j] = (float)v[j];
+      cm = fmaxf(cm, f[j]);
+    }
+    if (cm > m) {
+      s *= __expf(m - cm);
+      m = cm;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += __expf(f[j] - m);
+  }
+  for (int c = V8 * 8 + threadIdx.x; c < V; c += 256) {  // ragged tail (V % 8)
+    float f = (float)lr[c];
+    if (f > m) {
+      s *= __expf(m - f);
+      m = f;
+    }
+    s += __expf(f - m);
+  }
+  // wave merge of (m, s)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float om = __shfl_xor(m, o, 64), os = __shfl_xor(s, o, 64);
+    float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[wid] = m;
+    ss[wid] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0];
+    for (int i = 1; i < 4; ++i) M = fmaxf(M, sm[i]);
+    float S = 0.f;
+    for (int i = 0; i < 4; ++i) S += (sm[i] == -INFINITY) ? 0.f : ss[i] * __expf(sm[i] - M);
+    const float lse = M + __logf(S);
+    lse_out[row] = lse;
+    const int64_t t = tgt[row];
+    loss_out[row] = (t >= 0 && t < V) ? (lse - (float)lr[t]) : 0.f;
+  }
+}
+
+// bwd (in place allowed: dlogits may alias logits):
+//   d[r, c] = gscale * (exp(logit - lse) - [c == target])  for c < V,  0 for V <= c < Vp
+__global__ void __launch_bounds__(256) xent_bwd_kernel(const bf16* logits, const int64_t* __restrict__ tgt,
+                                                        const float* __restrict__ lse_in,
+                                                        const float* __restrict__ gscale, bf16* dlogits, int V,
+                                                        int Vp) {
+  const int64_t row = blockIdx.x;
+  const int64_t t = tgt[row];
+  const float lse = lse_in[row];
+  const float sc = (t >= 0) ? gscale[0] : 0.f;
+  const bf16* lr = logits + row * Vp;
+  bf16* dr = dlogits + row * Vp;
+  const int Vp8 = Vp >> 3;
+  for (int c = threadIdx.x; c < Vp8; c += 256) {
+    bf16x8 v = *(const bf16x8*)(lr + c * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = c * 8 + j;
+      float p = (col < V) ? __expf((float)v[j] - lse) : 0.f;
+      if (col == t) p -= 1.f;
+      o[j] = (bf16)(p * sc);
+    }
+    *(bf16x8*)(dr + c * 8) = o;
+  }
+}
+
+}  // namespace vcx
+
+// ============================================================ launchers
+using namespace vcx;
+
+#define VCX_LN_DISPATCH(CHV, ...)                     \
+  switch (CHV) {                                      \
+    case 1: { constexpr int CH = 1; __VA_ARGS__; } break; \
+    case 2: { constexpr int CH = 2; __VA_ARGS__; } break; \
+    case 3: { constexpr int CH = 3; __VA_ARGS__; } break; \
+    case 4: { constexpr int CH = 4; __VA_ARGS__; } break; \
+    case 5: case 6: { constexpr int CH = 6; __VA_ARGS__; } break; \
+    case 7: case 8: { constexpr int CH = 8; __VA_ARGS__; } break; \
+    default: { constexpr int CH = 16; __VA_ARGS__; } break; \
+  }
+
+void vcx_ln_fwd(const void* a, const void* b, void* xout, void* y, const void* w, const void* bias, float* mean,
+                float* rstd, int R, int C, float eps, int rms, hipStream_t s) {
+  const int ch = (C / 8 + 63) / 64;
+  dim3 grid((R + 3) / 4);
+  VCX_LN_DISPATCH(ch, hipLaunchKernelGGL(ln_fwd_kernel<CH>, grid, dim3(256), 0, s, (const bf16*)a,
+                                         (const bf16*)b, (bf16*)xout, (bf16*)y, (const bf16*)w,
+                                         (const bf16*)bias, mean, rstd, R, C, eps, rms));
+}
+
+int vcx_ln_bwd_partials(int R) {
+  int g = (R + 3) / 4;
+  return (g > 256 ? 256 : g) * 4;
+}
+
+void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
+                void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, hipStream_t s) {
+  const int ch = (C / 8 + 63) / 64;
+  const int P = vcx_ln_bwd_partials(R);
+  dim3 grid(P / 4);
+  VCX_LN_DISPATCH(ch, hipLaunchKernelGGL(ln_bwd_kernel<CH>, grid, dim3(256), 0, s, (const bf16*)dy,
+                                         (const bf16*)x, (const bf16*)w, mean, rstd, (const bf16*)dres,
+                                         (bf16*)dx, dw_part, db_part, R, C, rms));
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, dw_part, P, C, (bf16*)dw);
+  if (db_part && db) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, db_part, P, C, (bf16*)db);
+}
+
+void vcx_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(gelu_fwd_kernel, dim3(stream_grid(n / 8, 256)), dim3(256), 0, s, (const bf16*)x, (bf16*)y,
+                     n / 8);
+}
+
+void vcx_gelu_bwd(const void* x, const void* dy, void* dx, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(stream_grid(n / 8, 256)), dim3(256), 0, s, (const bf16*)x,
+                     (const bf16*)dy, (bf16*)dx, n / 8);
+}
+
+void vcx_swiglu_fwd(const void* gu, void* y, int64_t R, int F, hipStream_t s) {
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(stream_grid(R * (F / 8), 256)), dim3(256), 0, s, (const bf16*)gu,
+                     (bf16*)y, R, F);
+}
+
+void vcx_swiglu_bwd(const void* gu, const void* dy, void* dgu, int64_t R, int F, hipStream_t s) {
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(stream_grid(R * (F / 8), 256)), dim3(256), 0, s, (const bf16*)gu,
+                     (const bf16*)dy, (bf16*)dgu, R, F);
+}
+
+void vcx_xent_fwd(const void* logits, const int64_t* tgt, float* lse, float* loss, int64_t R, int V, int Vp,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(xent_fwd_kernel, dim3(R), dim3(256), 0, s, (const bf16*)logits, tgt, lse, loss, V, Vp);
+}
+
+void vcx_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, const float* gscale, void* dlogits,
+                  int64_t R, int V, int Vp, hipStream_t s) {
+  hipLaunchKernelGGL(xent_bwd_kernel, dim3(R), dim3(256), 0, s, (const bf16*)logits, tgt, lse, gscale,
+                     (bf16*)dlogits, V, Vp);
+}

@@ -1,0 +1,31 @@
+// Host-side launcher declarations for every gfx950 kernel of the package. Kernel files
+// (*.hip, built by hipcc --offload-arch=gfx950) define them; the torch bindings call them.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// optim.hip
+void vcx_grad_sumsq(const void* g, int64_t n, float* ostate, hipStream_t s);
+void vcx_adam_prologue(float* ostate, float max_norm, hipStream_t s);
+void vcx_adamw_flat(void* param, const void* grad, float* master, float* m, float* v, int64_t n, int64_t n_decay,
+                    const float* ostate, float beta1, float beta2, float eps, float wd, hipStream_t s);
+void vcx_lsgd_delta(const float* master, const float* anchor, void* delta, int64_t n, hipStream_t s);
+void vcx_lsgd_apply(const void* avg, float* anchor, float* master, void* param, float* mom, int64_t n,
+                    float outer_lr, float mu, int nesterov, float avg_scale, hipStream_t s);
+void vcx_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s);
+void vcx_axpy_bf16(const void* src, void* acc, int64_t n, float scale, hipStream_t s);
+
+// norm_act.hip
+void vcx_ln_fwd(const void* a, const void* b, void* xout, void* y, const void* w, const void* bias, float* mean,
+                float* rstd, int R, int C, float eps, int rms, hipStream_t s);
+int vcx_ln_bwd_partials(int R);
+void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
+                void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, hipStream_t s);
+void vcx_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s);
+void vcx_gelu_bwd(const void* x, const void* dy, void* dx, int64_t n, hipStream_t s);
+void vcx_swiglu_fwd(const void* gu, void* y, int64_t R, int F, hipStream_t s);
+void vcx_swiglu_bwd(const void* gu, const void* dy, void* dgu, int64_t R, int F, hipStream_t s);
+void vcx_xent_fwd(const void* logits, const int64_t* tgt, float* lse, float* loss, int64_t R, int V, int Vp,
+                  hipStream_t s);
+void vcx_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, const float* gscale, void* dlogits,
+                  int64_t R, int V, int Vp, hipStream_t s);

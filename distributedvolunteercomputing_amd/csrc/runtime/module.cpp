@@ -1,0 +1,117 @@
+// pybind11 module `_native`: host runtime of the volunteer-computing framework.
+// All blocking calls release the GIL.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "scheduler.h"
+#include "transport.h"
+
+namespace py = pybind11;
+using namespace vcxrt;
+
+namespace {
+
+// A received frame whose payload is exposed through the buffer protocol without a copy
+// (numpy.frombuffer(frame, dtype) views the bytes the transport thread filled).
+struct PyFrame {
+  Frame f;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "C++ runtime: framed TCP transport, chunk scheduler, reorder index";
+
+  py::class_<PyFrame>(m, "Frame", py::buffer_protocol())
+      .def_property_readonly("header", [](const PyFrame& p) { return py::str(p.f.header); })
+      .def_property_readonly("peer", [](const PyFrame& p) { return p.f.peer; })
+      .def_property_readonly("nbytes", [](const PyFrame& p) { return p.f.payload.size(); })
+      .def_buffer([](PyFrame& p) -> py::buffer_info {
+        return py::buffer_info(p.f.payload.data(), 1, py::format_descriptor<uint8_t>::format(), 1,
+                               {(py::ssize_t)p.f.payload.size()}, {(py::ssize_t)1});
+      });
+
+  py::class_<Hub>(m, "Hub")
+      .def(py::init<const std::string&, int, size_t, bool>(), py::arg("bind_host") = "", py::arg("port") = 0,
+           py::arg("capacity") = 64, py::arg("ack") = true)
+      .def_property_readonly("port", &Hub::port)
+      .def(
+          "recv",
+          [](Hub& h, double timeout) -> py::object {
+            auto pf = std::make_unique<PyFrame>();
+            bool ok;
+            {
+              py::gil_scoped_release rel;
+              ok = h.recv(&pf->f, timeout);
+            }
+            if (!ok) return py::none();
+            return py::cast(pf.release(), py::return_value_policy::take_ownership);
+          },
+          py::arg("timeout") = -1.0)
+      .def("pending", &Hub::pending)
+      .def("close", &Hub::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("frames_received", &Hub::frames_received)
+      .def_property_readonly("bytes_received", &Hub::bytes_received);
+
+  py::class_<Sender>(m, "Sender")
+      .def(py::init<const std::string&, int, bool, double>(), py::arg("host"), py::arg("port"),
+           py::arg("ack") = true, py::arg("connect_timeout") = 10.0, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "send",
+          [](Sender& s, const std::string& header, py::buffer payload, double timeout) {
+            py::buffer_info bi = payload.request();
+            size_t n = (size_t)bi.size * (size_t)bi.itemsize;
+            // require C-contiguous bytes; the python layer makes arrays contiguous first
+            if (bi.ndim > 0) {
+              py::ssize_t expect = bi.itemsize;
+              for (int d = (int)bi.ndim - 1; d >= 0; --d) {
+                if (bi.shape[d] > 1 && bi.strides[d] != expect)
+                  throw std::invalid_argument("Sender.send: payload must be C-contiguous");
+                expect *= bi.shape[d];
+              }
+            }
+            const uint8_t* ptr = (const uint8_t*)bi.ptr;
+            py::gil_scoped_release rel;
+            return s.send(header, ptr, n, timeout);
+          },
+          py::arg("header"), py::arg("payload"), py::arg("timeout") = 60.0)
+      .def("close", &Sender::close)
+      .def_property_readonly("connected", &Sender::connected)
+      .def_property_readonly("bytes_sent", &Sender::bytes_sent);
+
+  py::class_<Assignment>(m, "Assignment")
+      .def_readonly("chunk", &Assignment::chunk)
+      .def_readonly("worker", &Assignment::worker)
+      .def_readonly("requester", &Assignment::requester)
+      .def("valid", &Assignment::valid);
+
+  py::class_<ChunkScheduler> cs(m, "ChunkScheduler");
+  py::enum_<ChunkScheduler::Policy>(cs, "Policy")
+      .value("ROUND_ROBIN", ChunkScheduler::ROUND_ROBIN)
+      .value("LEAST_LOADED", ChunkScheduler::LEAST_LOADED);
+  cs.def(py::init<int, int>(), py::arg("policy") = 0, py::arg("credits") = 2)
+      .def("add_worker", &ChunkScheduler::add_worker)
+      .def("remove_worker", &ChunkScheduler::remove_worker)
+      .def("set_available", &ChunkScheduler::set_available)
+      .def("has_worker", &ChunkScheduler::has_worker)
+      .def("workers", &ChunkScheduler::workers)
+      .def("available_workers", &ChunkScheduler::available_workers)
+      .def("heartbeat", &ChunkScheduler::heartbeat)
+      .def("expire", &ChunkScheduler::expire)
+      .def("submit", &ChunkScheduler::submit)
+      .def("requeue_front", &ChunkScheduler::requeue_front)
+      .def("next", &ChunkScheduler::next)
+      .def("complete", &ChunkScheduler::complete)
+      .def("cancel_requester", &ChunkScheduler::cancel_requester)
+      .def("queued", &ChunkScheduler::queued)
+      .def("inflight", &ChunkScheduler::inflight)
+      .def("inflight_of", &ChunkScheduler::inflight_of)
+      .def_property_readonly("dispatched", &ChunkScheduler::dispatched);
+
+  py::class_<ReorderIndex>(m, "ReorderIndex")
+      .def(py::init<int64_t>(), py::arg("first") = 1)
+      .def("push", &ReorderIndex::push)
+      .def("reset", &ReorderIndex::reset)
+      .def_property_readonly("next_expected", &ReorderIndex::next_expected)
+      .def_property_readonly("stashed", &ReorderIndex::stashed);
+}

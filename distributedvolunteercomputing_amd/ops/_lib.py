@@ -1,0 +1,62 @@
+"""Loader for the in-tree gfx950 extension ``_C``.
+
+Policy: GPU tensors ALWAYS go through the HIP kernels. If the extension is missing or fails
+to load, GPU ops raise immediately (no silent eager fallback on a GPU box). CPU tensors use
+the plain-PyTorch reference implementations in each op module; those references double as
+the numerics oracle in the tests.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+_C = None
+_ERR: Exception | None = None
+
+
+def _load():
+    global _C, _ERR
+    if _C is not None or _ERR is not None:
+        return
+    try:
+        _C = importlib.import_module("distributedvolunteercomputing_amd._C")
+    except Exception as e:  # pragma: no cover - depends on build state
+        _ERR = e
+
+
+def native():
+    """Return the compiled module or raise a loud error explaining how to build it."""
+    _load()
+    if _C is None:
+        raise RuntimeError(
+            "distributedvolunteercomputing_amd._C (gfx950 HIP kernels) is not built or failed to load: "
+            f"{_ERR!r}. Build it with `python -m distributedvolunteercomputing_amd._build`."
+        )
+    return _C
+
+
+def available() -> bool:
+    _load()
+    return _C is not None
+
+
+_FORCE_REF = [os.environ.get("VCX_FORCE_REFERENCE_OPS") == "1"]
+
+
+def use_native(t) -> bool:
+    """True when tensor `t` lives on the GPU (then the native kernel is mandatory)."""
+    if _FORCE_REF[0]:
+        return False
+    return bool(getattr(t, "is_cuda", False))
+
+
+class reference_ops:
+    """Context manager: run the plain-PyTorch reference path even for GPU tensors.
+    Used ONLY by the numerics tests to build an oracle on the same device."""
+
+    def __enter__(self):
+        self._old = _FORCE_REF[0]
+        _FORCE_REF[0] = True
+
+    def __exit__(self, *exc):
+        _FORCE_REF[0] = self._old

@@ -1,0 +1,72 @@
+"""LayerNorm / RMSNorm with an optional fused residual add (HIP on GPU, torch on CPU).
+
+``add_layernorm(a, b, w, bias)`` returns ``(y, x)`` with ``x = a + b`` (the new residual
+stream) and ``y = LN(x)``. Fusing the add saves one full read+write of the residual stream per
+sub-layer; the backward fuses the residual-gradient add into ``dx``.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import native, use_native
+
+
+def _ref_ln(x, w, b, eps, rms):
+    xf = x.float()
+    if rms:
+        var = xf.pow(2).mean(-1, keepdim=True)
+        y = xf * torch.rsqrt(var + eps)
+    else:
+        mu = xf.mean(-1, keepdim=True)
+        var = (xf - mu).pow(2).mean(-1, keepdim=True)
+        y = (xf - mu) * torch.rsqrt(var + eps)
+    y = y * w.float()
+    if b is not None:
+        y = y + b.float()
+    return y.to(x.dtype)
+
+
+class _AddLN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, w, bias, eps, rms):
+        C = native()
+        y, x, mean, rstd = C.ln_fwd(a.contiguous(), None if b is None else b.contiguous(), w, bias, eps, rms)
+        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.has_b = b is not None
+        ctx.has_bias = bias is not None
+        ctx.rms = rms
+        if b is None:
+            x = x.view_as(x)  # output aliases the input: hand autograd a view, not the input itself
+        return y, x
+
+    @staticmethod
+    def backward(ctx, dy, dx_res):
+        x, w, mean, rstd = ctx.saved_tensors
+        C = native()
+        dres = None if dx_res is None else dx_res.contiguous()
+        outs = C.ln_bwd(dy.contiguous(), x, w, mean, rstd, dres, ctx.has_bias, ctx.rms)
+        dx = outs[0]
+        dw = outs[1]
+        dbias = outs[2] if ctx.has_bias else None
+        return dx, (dx if ctx.has_b else None), dw, dbias, None, None
+
+
+def add_layernorm(a, b, weight, bias=None, eps: float = 1e-5, rms: bool = False):
+    """Returns (LN(a+b), a+b). With b=None returns (LN(a), a)."""
+    if use_native(a):
+        y, x = _AddLN.apply(a, b, weight, bias, eps, rms)
+        return y, x
+    x = a if b is None else a + b
+    return _ref_ln(x, weight, bias, eps, rms), x
+
+
+def layernorm(x, weight, bias=None, eps: float = 1e-5):
+    return add_layernorm(x, None, weight, bias, eps, False)[0]
+
+
+def rmsnorm(x, weight, eps: float = 1e-6):
+    return add_layernorm(x, None, weight, None, eps, True)[0]
+
+
+def add_rmsnorm(a, b, weight, eps: float = 1e-6):
+    return add_layernorm(a, b, weight, None, eps, True)

@@ -1,0 +1,155 @@
+"""All-reduce algorithms for averaging across volunteer peers.
+
+* ``rccl``      — the library all-reduce of the peer group (RCCL over xGMI on MI355X: it runs
+                  several rings/trees over the 7 point-to-point links at once). Default: the
+                  averaging payload is one flat buffer, so a single large collective is the
+                  per-link-bandwidth-optimal call.
+* ``rs_ag``     — reduce-scatter + all-gather (the sharded form used by optimizer-state
+                  sharding: each peer only needs its shard between the two halves).
+* ``butterfly`` — recursive halving (reduce-scatter) + recursive doubling (all-gather) over
+                  pairwise exchanges: log2(P) rounds, each with ONE partner, so every round is
+                  one xGMI link at full rate and the schedule re-forms trivially over any live
+                  set (non-power-of-two sets fold the extra peers in first).
+* ``ring``      — classic 2(P-1)-step ring over pairwise exchanges.
+
+The reductions of the hand-written algorithms run in a HIP kernel (``axpy_bf16``) for bf16
+GPU buffers. All functions SUM in place; the caller applies the 1/P scale (fused into the
+local-SGD apply kernel).
+
+No reference analog: the reference has no collectives.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from .peer_group import PeerGroup
+
+ALGOS = ("rccl", "rs_ag", "butterfly", "ring")
+
+
+def _add_(acc: torch.Tensor, src: torch.Tensor):
+    if acc.dtype == torch.bfloat16 and acc.is_cuda and acc.numel() % 8 == 0:
+        ops.axpy_bf16(src, acc, 1.0)
+    else:
+        acc.add_(src)
+
+
+def allreduce_sum_(t: torch.Tensor, group: PeerGroup, algo: str = "rccl") -> torch.Tensor:
+    if group is None or group.size == 1:
+        return t
+    if algo == "rccl":
+        return group.allreduce_(t)
+    if algo == "rs_ag":
+        return _rs_ag(t, group)
+    if algo == "butterfly":
+        return _butterfly(t, group)
+    if algo == "ring":
+        return _ring(t, group)
+    raise ValueError(f"unknown all-reduce algorithm {algo!r}; choose from {ALGOS}")
+
+
+def _pad_len(n: int, parts: int, align: int = 64) -> int:
+    q = parts * align
+    return (n + q - 1) // q * q
+
+
+def _rs_ag(t, group):
+    P = group.size
+    n = t.numel()
+    L = _pad_len(n, P)
+    buf = t if L == n else torch.cat([t, t.new_zeros(L - n)])
+    shard = buf.new_empty(L // P)
+    group.reduce_scatter_(shard, buf)
+    group.all_gather_(buf, shard)
+    if buf is not t:
+        t.copy_(buf[:n])
+    return t
+
+
+def _butterfly(t, group):
+    P, r = group.size, group.rank
+    p2 = 1
+    while p2 * 2 <= P:
+        p2 *= 2
+    n = t.numel()
+    # --- fold: peers >= p2 hand their whole buffer to (rank - p2) and wait for the result
+    extra = P - p2
+    if r >= p2:
+        group.send(t, r - p2, tag=1)
+        group.recv(t, r - p2, tag=2)
+        return t
+    if r < extra:
+        tmp = torch.empty_like(t)
+        group.recv(tmp, r + p2, tag=1)
+        _add_(t, tmp)
+    # --- recursive halving reduce-scatter among the p2 core peers
+    L = _pad_len(n, p2)
+    buf = t if L == n else torch.cat([t, t.new_zeros(L - n)])
+    lo, hi = 0, L
+    dist_ = p2 // 2
+    segs = []
+    while dist_ >= 1:
+        peer = r ^ dist_
+        mid = (lo + hi) // 2
+        if r & dist_:  # keep upper half
+            keep, give = (mid, hi), (lo, mid)
+        else:
+            keep, give = (lo, mid), (mid, hi)
+        recv = buf.new_empty(keep[1] - keep[0])
+        group.exchange(buf[give[0] : give[1]].contiguous(), recv, peer, tag=3)
+        kv = buf[keep[0] : keep[1]]
+        _add_(kv, recv)
+        segs.append((lo, hi, dist_))
+        lo, hi = keep
+        dist_ //= 2
+    # --- recursive doubling all-gather (reverse order)
+    for plo, phi, d in reversed(segs):
+        peer = r ^ d
+        mid = (plo + phi) // 2
+        mine = (lo, hi)
+        other = (mid, phi) if mine[0] == plo else (plo, mid)
+        recv = buf.new_empty(other[1] - other[0])
+        group.exchange(buf[mine[0] : mine[1]].contiguous(), recv, peer, tag=4)
+        buf[other[0] : other[1]].copy_(recv)
+        lo, hi = plo, phi
+    if buf is not t:
+        t.copy_(buf[:n])
+    # --- unfold: return the result to the folded peers
+    if r < extra:
+        group.send(t, r + p2, tag=2)
+    return t
+
+
+def _ring(t, group):
+    P, r = group.size, group.rank
+    n = t.numel()
+    L = _pad_len(n, P)
+    buf = t if L == n else torch.cat([t, t.new_zeros(L - n)])
+    cs = L // P
+    chunks = [buf[i * cs : (i + 1) * cs] for i in range(P)]
+    right, left = (r + 1) % P, (r - 1) % P
+    recv = buf.new_empty(cs)
+
+    def step(send_t, recv_t, tag):
+        # even ranks send first, odd ranks receive first: deadlock-free for blocking p2p
+        if r % 2 == 0:
+            group.send(send_t, right, tag)
+            group.recv(recv_t, left, tag)
+        else:
+            group.recv(recv_t, left, tag)
+            group.send(send_t, right, tag)
+
+    for s in range(P - 1):  # reduce-scatter
+        si = (r - s) % P
+        ri = (r - s - 1) % P
+        step(chunks[si].contiguous(), recv, tag=10)
+        _add_(chunks[ri], recv)
+    for s in range(P - 1):  # all-gather
+        si = (r + 1 - s) % P
+        ri = (r - s) % P
+        step(chunks[si].contiguous(), recv, tag=11)
+        chunks[ri].copy_(recv)
+    if buf is not t:
+        t.copy_(buf[:n])
+    return t

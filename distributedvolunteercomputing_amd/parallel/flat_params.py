@@ -1,0 +1,86 @@
+"""Flat parameter / gradient storage.
+
+Every parameter of a module is re-homed into ONE contiguous buffer (and its gradient into a
+second one) so that the optimizer, the local-SGD averaging, compression and optimizer-state
+sharding each operate on a single 1-D tensor: one kernel launch for AdamW, one collective per
+bucket, trivial sharding (contiguous slices) and trivial re-sharding when peers join/leave.
+
+Layout: [decayed params (dim >= 2) | non-decayed params (biases, norm gains)], each segment
+aligned to ``ALIGN`` elements (128 B for bf16) so vectorised 16-B accesses never straddle.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+ALIGN = 64
+
+
+def _round_up(n, a=ALIGN):
+    return (n + a - 1) // a * a
+
+
+@dataclass
+class Segment:
+    name: str
+    offset: int
+    numel: int
+    shape: tuple
+    decay: bool
+
+
+class FlatParams:
+    def __init__(self, module: torch.nn.Module, dtype=torch.bfloat16, device=None, pad_to: int = ALIGN):
+        params = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
+        seen = {}
+        uniq = []
+        for n, p in params:  # tied weights appear once
+            if id(p) in seen:
+                continue
+            seen[id(p)] = n
+            uniq.append((n, p))
+        decay = [(n, p) for n, p in uniq if p.dim() >= 2]
+        nodecay = [(n, p) for n, p in uniq if p.dim() < 2]
+        device = device or (uniq[0][1].device if uniq else torch.device("cpu"))
+        self.segments: list[Segment] = []
+        off = 0
+        for group, is_decay in ((decay, True), (nodecay, False)):
+            for n, p in group:
+                self.segments.append(Segment(n, off, p.numel(), tuple(p.shape), is_decay))
+                off = _round_up(off + p.numel())
+            if is_decay:
+                self.n_decay = off
+        self.numel = _round_up(max(off, pad_to), pad_to)
+        self.dtype = dtype
+        self.param = torch.zeros(self.numel, dtype=dtype, device=device)
+        self.grad = torch.zeros(self.numel, dtype=dtype, device=device)
+        self._params = []
+        byname = dict(uniq)
+        with torch.no_grad():
+            for s in self.segments:
+                p = byname[s.name]
+                view = self.param[s.offset : s.offset + s.numel].view(s.shape)
+                view.copy_(p.detach().to(device=device, dtype=dtype))
+                p.data = view
+                p.grad = self.grad[s.offset : s.offset + s.numel].view(s.shape)
+                self._params.append(p)
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def rebind_grads(self):
+        """Re-point .grad at the flat buffer (call if something replaced p.grad)."""
+        for s, p in zip(self.segments, self._params):
+            p.grad = self.grad[s.offset : s.offset + s.numel].view(s.shape)
+
+    def state_dict_views(self, flat: torch.Tensor):
+        """Name -> view of an arbitrary flat buffer with this layout (for checkpoints)."""
+        return {s.name: flat[s.offset : s.offset + s.numel].view(s.shape) for s in self.segments}
+
+    def shard_bounds(self, rank: int, world: int, align: int = ALIGN):
+        """Contiguous [lo, hi) slice of the flat space owned by `rank` (ZeRO-style)."""
+        per = _round_up((self.numel + world - 1) // world, align)
+        lo = min(rank * per, self.numel)
+        hi = min(lo + per, self.numel)
+        return lo, hi

@@ -1,0 +1,53 @@
+"""GPT-2 through the HIP kernels vs the same model through the PyTorch reference ops."""
+import pytest
+import torch
+
+from distributedvolunteercomputing_amd.models.gpt2 import GPT2, GPT2Config
+from distributedvolunteercomputing_amd.ops._lib import reference_ops
+from distributedvolunteercomputing_amd.parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(dev, name="gpt2-tiny"):
+    cfg = GPT2Config.preset(name)
+    return GPT2(cfg).to(device=dev, dtype=torch.bfloat16), cfg
+
+
+def test_gpt2_forward_backward_matches_reference(gpu):
+    m, cfg = _model(gpu)
+    x = torch.randint(0, cfg.vocab_size, (4, 64), device=gpu)
+    y = torch.randint(0, cfg.vocab_size, (4, 64), device=gpu)
+    loss = m(x, y)
+    loss.backward()
+    g_native = {n: p.grad.float().clone() for n, p in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    with reference_ops():
+        loss_ref = m(x, y)
+        loss_ref.backward()
+    assert abs(loss.item() - loss_ref.item()) < 2e-2
+    for n, p in m.named_parameters():
+        a, b = g_native[n], p.grad.float()
+        denom = b.norm().item() + 1e-6
+        assert (a - b).norm().item() / denom < 0.08, n
+
+
+def test_local_sgd_trains(gpu):
+    m, cfg = _model(gpu)
+    tr = LocalSGDTrainer(m, LocalSGDConfig(H=2, lr=3e-3, weight_decay=0.0), device=gpu)
+    x = torch.randint(0, cfg.vocab_size, (8, 64), device=gpu)
+    y = torch.roll(x, -1, 1)  # learnable structure
+    losses = []
+    for _ in range(30):
+        st = tr.step(x, y)
+        losses.append(float(st.extra["loss_t"]))
+    assert losses[-1] < losses[0] - 1.0, losses
+
+
+def test_gpt2_small_step_shapes(gpu):
+    m, cfg = _model(gpu, "gpt2")
+    tr = LocalSGDTrainer(m, LocalSGDConfig(H=4), device=gpu)
+    x = torch.randint(0, cfg.vocab_size, (2, 256), device=gpu)
+    st = tr.step(x, x)
+    torch.cuda.synchronize()
+    assert 9.0 < float(st.extra["loss_t"]) < 12.0  # ~ln(50257) at init

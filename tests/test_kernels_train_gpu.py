@@ -1,0 +1,165 @@
+"""Numerics of the training-path HIP kernels vs plain PyTorch fp32 references (gfx950)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributedvolunteercomputing_amd import ops
+from distributedvolunteercomputing_amd.ops import optim as optim_ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("C", [64, 768, 1024, 1600, 4096])
+@pytest.mark.parametrize("fused", [False, True])
+def test_add_layernorm_fwd_bwd(gpu, C, fused):
+    torch.manual_seed(0)
+    R = 257
+    a = _bf(torch.randn(R, C, device=gpu)).requires_grad_()
+    b = _bf(torch.randn(R, C, device=gpu)).requires_grad_() if fused else None
+    w = _bf(torch.rand(C, device=gpu) + 0.5).requires_grad_()
+    bias = _bf(torch.randn(C, device=gpu) * 0.1).requires_grad_()
+    y, x = ops.add_layernorm(a, b, w, bias)
+    # reference in fp32 on the bf16-rounded residual
+    a32 = a.detach().float().requires_grad_()
+    b32 = b.detach().float().requires_grad_() if fused else None
+    w32 = w.detach().float().requires_grad_()
+    bias32 = bias.detach().float().requires_grad_()
+    xr = a32 + b32 if fused else a32
+    yr = F.layer_norm(xr, (C,), w32, bias32, 1e-5)
+    assert torch.allclose(x.float(), xr.detach(), atol=2e-2, rtol=1e-2)
+    assert torch.allclose(y.float(), yr.detach(), atol=3e-2, rtol=2e-2)
+    dy = torch.randn(R, C, device=gpu)
+    dx_res = torch.randn(R, C, device=gpu)
+    loss = (y.float() * dy).sum() + (x.float() * dx_res).sum()
+    loss.backward()
+    lr = (yr * dy).sum() + (xr * dx_res).sum()
+    lr.backward()
+    assert torch.allclose(a.grad.float(), a32.grad, atol=5e-2, rtol=3e-2)
+    if fused:
+        assert torch.allclose(b.grad.float(), b32.grad, atol=5e-2, rtol=3e-2)
+    assert torch.allclose(w.grad.float(), w32.grad, atol=0.5, rtol=3e-2)
+    assert torch.allclose(bias.grad.float(), bias32.grad, atol=0.5, rtol=3e-2)
+
+
+def test_rmsnorm(gpu):
+    torch.manual_seed(1)
+    R, C = 100, 4096
+    x = _bf(torch.randn(R, C, device=gpu)).requires_grad_()
+    w = _bf(torch.rand(C, device=gpu) + 0.5).requires_grad_()
+    y = ops.rmsnorm(x, w)
+    x32 = x.detach().float().requires_grad_()
+    w32 = w.detach().float().requires_grad_()
+    yr = x32 * torch.rsqrt(x32.pow(2).mean(-1, keepdim=True) + 1e-6) * w32
+    assert torch.allclose(y.float(), yr, atol=3e-2, rtol=2e-2)
+    dy = torch.randn(R, C, device=gpu)
+    (y.float() * dy).sum().backward()
+    (yr * dy).sum().backward()
+    assert torch.allclose(x.grad.float(), x32.grad, atol=5e-2, rtol=3e-2)
+    assert torch.allclose(w.grad.float(), w32.grad, atol=0.5, rtol=3e-2)
+
+
+def test_gelu(gpu):
+    torch.manual_seed(2)
+    x = _bf(torch.randn(64, 3072, device=gpu) * 3).requires_grad_()
+    y = ops.gelu(x)
+    x32 = x.detach().float().requires_grad_()
+    yr = F.gelu(x32, approximate="tanh")
+    assert torch.allclose(y.float(), yr, atol=2e-2, rtol=1e-2)
+    dy = torch.randn_like(x32)
+    (y.float() * dy).sum().backward()
+    (yr * dy).sum().backward()
+    assert torch.allclose(x.grad.float(), x32.grad, atol=3e-2, rtol=2e-2)
+
+
+def test_swiglu(gpu):
+    torch.manual_seed(3)
+    gu = _bf(torch.randn(33, 2 * 512, device=gpu) * 2).requires_grad_()
+    y = ops.swiglu(gu)
+    g32 = gu.detach().float().requires_grad_()
+    g, u = g32.chunk(2, -1)
+    yr = F.silu(g) * u
+    assert torch.allclose(y.float(), yr, atol=3e-2, rtol=2e-2)
+    dy = torch.randn_like(yr)
+    (y.float() * dy).sum().backward()
+    (yr * dy).sum().backward()
+    assert torch.allclose(gu.grad.float(), g32.grad, atol=5e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("V,Vp", [(50257, 50304), (1000, 1000), (37, 40)])
+def test_cross_entropy(gpu, V, Vp):
+    torch.manual_seed(4)
+    R = 129
+    logits = _bf(torch.randn(R, Vp, device=gpu) * 3).requires_grad_()
+    tgt = torch.randint(0, V, (R,), device=gpu)
+    tgt[5] = -100
+    loss = ops.cross_entropy(logits * 1.0, tgt, vocab=V)
+    l32 = logits.detach().float().requires_grad_()
+    ref = F.cross_entropy(l32[:, :V], tgt, ignore_index=-100)
+    assert abs(loss.item() - ref.item()) < 2e-3 * max(1.0, abs(ref.item()))
+    (loss * 2.0).backward()
+    (ref * 2.0).backward()
+    assert torch.allclose(logits.grad.float(), l32.grad, atol=2e-4, rtol=2e-2)
+    assert logits.grad[:, V:].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("max_norm", [0.0, 1.0])
+def test_adamw_flat_matches_reference(gpu, max_norm):
+    torch.manual_seed(5)
+    n = 64 * 1000 + 8
+    n_decay = 64 * 600
+    p = _bf(torch.randn(n, device=gpu))
+    g = _bf(torch.randn(n, device=gpu) * 0.1)
+    master = p.float()
+    m = torch.zeros(n, device=gpu)
+    v = torch.zeros(n, device=gpu)
+    st = ops.new_ostate(gpu, 1e-2)
+    # CPU reference copies
+    pc, gc, mc, m2, v2 = p.cpu(), g.cpu(), master.cpu(), m.cpu(), v.cpu()
+    stc = st.cpu()
+    for _ in range(3):
+        ops.adamw_step(p, g, master, m, v, st, n_decay=n_decay, beta1=0.9, beta2=0.95, eps=1e-8, wd=0.1,
+                       max_norm=max_norm)
+        optim_ops.adamw_step(pc, gc, mc, m2, v2, stc, n_decay=n_decay, beta1=0.9, beta2=0.95, eps=1e-8, wd=0.1,
+                             max_norm=max_norm)
+    torch.cuda.synchronize()
+    assert st[0].item() == 3
+    assert torch.allclose(master.cpu(), mc, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(m.cpu(), m2, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(v.cpu(), v2, atol=1e-7, rtol=1e-5)
+    assert torch.allclose(p.cpu().float(), mc.to(torch.bfloat16).float(), atol=1e-2, rtol=1e-2)
+    if max_norm > 0:
+        assert abs(st[2].item() - stc[2].item()) < 1e-4
+
+
+def test_lsgd_delta_apply(gpu):
+    torch.manual_seed(6)
+    n = 64 * 77
+    master = torch.randn(n, device=gpu)
+    anchor = master + torch.randn(n, device=gpu) * 1e-2
+    delta = torch.empty(n, dtype=torch.bfloat16, device=gpu)
+    ops.lsgd_delta(master, anchor, delta)
+    assert torch.allclose(delta.float(), master - anchor, atol=1e-4, rtol=1e-2)
+    param = torch.empty(n, dtype=torch.bfloat16, device=gpu)
+    mom = torch.zeros(n, device=gpu)
+    a0 = anchor.clone()
+    ops.lsgd_apply(delta, anchor, master, param, mom, outer_lr=0.7, mu=0.9, nesterov=True, avg_scale=0.5)
+    gref = -delta.float() * 0.5
+    momr = gref
+    upd = gref + 0.9 * momr
+    ar = a0 - 0.7 * upd
+    assert torch.allclose(anchor, ar, atol=1e-6, rtol=1e-5)
+    assert torch.equal(master, anchor)
+    assert torch.equal(param, anchor.to(torch.bfloat16))
+    assert torch.allclose(mom, momr)
+
+
+def test_axpy_bf16(gpu):
+    a = _bf(torch.randn(4096, device=gpu))
+    b = _bf(torch.randn(4096, device=gpu))
+    ref = (a.float() + 0.5 * b.float()).to(torch.bfloat16)
+    ops.axpy_bf16(b, a, 0.5)
+    assert torch.equal(a, ref)
