@@ -1,0 +1,259 @@
+"""Video sources and sinks without OpenCV/ffmpeg (neither exists on this image).
+
+Reference: ``cv2.VideoCapture(0 | path)`` + ``cv2.VideoWriter(mp4v, 30 fps)``
+(/root/reference/worker.py:95-98, 110, 215, 229). Replacements:
+
+Sources (``open_source(spec)``):
+  * ``"live"``                      — a synthetic camera (moving shapes + frame counter), endless
+                                      until ``stop()``; the image has no webcam.
+  * ``"synthetic:<n>[:<W>x<H>]"``   — n synthetic frames (default 1280x720).
+  * ``*.y4m``                       — YUV4MPEG2 (C420jpeg/C420/C444) file, e.g. ``ffmpeg -i in.mp4 out.y4m``.
+  * ``*.npy``                       — uint8 array [N, H, W, 3] (BGR, like OpenCV).
+  * a directory                     — sorted image files decoded with Pillow.
+All frames are H x W x 3 uint8 in **BGR** order (OpenCV's convention, which the reference's
+drawing colours assume).
+
+Sinks (``open_sink(path, width, height, fps)``):
+  * ``*.y4m`` (default) — YUV4MPEG2 4:4:4, losslessly round-trippable; ``*.npy``; a directory of PNGs.
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+import numpy as np
+
+
+# ----------------------------------------------------------------------------- colour
+def bgr_to_yuv444(frame: np.ndarray) -> np.ndarray:
+    f = frame.astype(np.float32)
+    b, g, r = f[..., 0], f[..., 1], f[..., 2]
+    y = 0.299 * r + 0.587 * g + 0.114 * b
+    u = (b - y) * 0.564 + 128.0
+    v = (r - y) * 0.713 + 128.0
+    return np.clip(np.stack([y, u, v]) + 0.5, 0, 255).astype(np.uint8)  # [3, H, W]
+
+
+def yuv444_to_bgr(yuv: np.ndarray) -> np.ndarray:
+    y, u, v = (yuv[i].astype(np.float32) for i in range(3))
+    r = y + 1.403 * (v - 128.0)
+    g = y - 0.344 * (u - 128.0) - 0.714 * (v - 128.0)
+    b = y + 1.773 * (u - 128.0)
+    return np.clip(np.stack([b, g, r], -1) + 0.5, 0, 255).astype(np.uint8)
+
+
+# ----------------------------------------------------------------------------- sources
+class FrameSource:
+    def read(self):
+        """Returns (ok, frame) like cv2.VideoCapture.read()."""
+        raise NotImplementedError
+
+    def release(self):
+        pass
+
+    def __iter__(self):
+        while True:
+            ok, f = self.read()
+            if not ok:
+                return
+            yield f
+
+
+def synthetic_frame(i: int, width: int, height: int, seed: int = 0) -> np.ndarray:
+    """Deterministic test frame: gradient background, two moving boxes, frame-index bar."""
+    yy, xx = np.mgrid[0:height, 0:width]
+    f = np.empty((height, width, 3), np.uint8)
+    f[..., 0] = (xx * 255 // max(1, width - 1)).astype(np.uint8)
+    f[..., 1] = (yy * 255 // max(1, height - 1)).astype(np.uint8)
+    f[..., 2] = (seed * 37 + i * 3) & 255
+    bw, bh = max(4, width // 8), max(6, height // 3)
+    x0 = (i * 7) % max(1, width - bw)
+    y0 = height // 4
+    f[y0 : y0 + bh, x0 : x0 + bw] = (40, 40, 200)
+    x1 = width - bw - (i * 5) % max(1, width - bw)
+    f[height // 2 : height // 2 + bh // 2, x1 : x1 + bw // 2] = (200, 200, 40)
+    # frame index as a 16-bit bar code along the top rows (lets tests verify ordering)
+    seg = max(1, width // 16)
+    for b in range(16):
+        f[0 : max(2, height // 60), b * seg : (b + 1) * seg] = 255 if (i >> b) & 1 else 0
+    return f
+
+
+def decode_frame_index(frame: np.ndarray, width: int | None = None) -> int:
+    width = width or frame.shape[1]
+    seg = max(1, width // 16)
+    v = 0
+    for b in range(16):
+        if frame[0, b * seg + seg // 2].mean() > 127:
+            v |= 1 << b
+    return v
+
+
+class SyntheticSource(FrameSource):
+    def __init__(self, n: int | None, width: int = 1280, height: int = 720, seed: int = 0):
+        self.n, self.w, self.h, self.seed, self.i = n, width, height, seed, 0
+        self._stop = False
+
+    def read(self):
+        if self._stop or (self.n is not None and self.i >= self.n):
+            return False, None
+        f = synthetic_frame(self.i, self.w, self.h, self.seed)
+        self.i += 1
+        return True, f
+
+    def release(self):
+        self._stop = True
+
+
+class NpySource(FrameSource):
+    def __init__(self, path):
+        self.a = np.load(path, mmap_mode="r", allow_pickle=False)
+        if self.a.ndim != 4 or self.a.shape[-1] != 3 or self.a.dtype != np.uint8:
+            raise ValueError(f"{path}: expected uint8 [N,H,W,3], got {self.a.dtype} {self.a.shape}")
+        self.i = 0
+
+    def read(self):
+        if self.i >= len(self.a):
+            return False, None
+        f = np.ascontiguousarray(self.a[self.i])
+        self.i += 1
+        return True, f
+
+
+class ImageDirSource(FrameSource):
+    EXT = {".png", ".jpg", ".jpeg", ".bmp", ".ppm", ".pgm"}
+
+    def __init__(self, path):
+        self.files = sorted(p for p in Path(path).iterdir() if p.suffix.lower() in self.EXT)
+        self.i = 0
+
+    def read(self):
+        from PIL import Image
+
+        if self.i >= len(self.files):
+            return False, None
+        im = Image.open(self.files[self.i]).convert("RGB")
+        self.i += 1
+        return True, np.ascontiguousarray(np.asarray(im)[..., ::-1])
+
+
+class Y4MSource(FrameSource):
+    def __init__(self, path):
+        self.f = open(path, "rb")
+        header = self.f.readline().decode("ascii").split()
+        if not header or header[0] != "YUV4MPEG2":
+            raise ValueError(f"{path}: not a YUV4MPEG2 file")
+        self.w = self.h = 0
+        self.cs = "420jpeg"
+        for tok in header[1:]:
+            if tok[0] == "W":
+                self.w = int(tok[1:])
+            elif tok[0] == "H":
+                self.h = int(tok[1:])
+            elif tok[0] == "C":
+                self.cs = tok[1:]
+
+    def read(self):
+        line = self.f.readline()
+        if not line or not line.startswith(b"FRAME"):
+            return False, None
+        w, h = self.w, self.h
+        if self.cs.startswith("444"):
+            yuv = np.frombuffer(self.f.read(3 * w * h), np.uint8).reshape(3, h, w)
+        else:  # 4:2:0 — upsample chroma by 2x2 replication
+            y = np.frombuffer(self.f.read(w * h), np.uint8).reshape(h, w)
+            cw, ch = (w + 1) // 2, (h + 1) // 2
+            u = np.frombuffer(self.f.read(cw * ch), np.uint8).reshape(ch, cw)
+            v = np.frombuffer(self.f.read(cw * ch), np.uint8).reshape(ch, cw)
+            u = u.repeat(2, 0).repeat(2, 1)[:h, :w]
+            v = v.repeat(2, 0).repeat(2, 1)[:h, :w]
+            yuv = np.stack([y, u, v])
+        return True, yuv444_to_bgr(yuv)
+
+    def release(self):
+        self.f.close()
+
+
+def open_source(spec: str) -> FrameSource:
+    if spec == "live":
+        return SyntheticSource(None, 640, 480)
+    if spec.startswith("synthetic"):
+        parts = spec.split(":")
+        n = int(parts[1]) if len(parts) > 1 and parts[1] else 300
+        w, h = 1280, 720
+        if len(parts) > 2:
+            w, h = (int(v) for v in parts[2].lower().split("x"))
+        return SyntheticSource(n, w, h)
+    p = Path(spec)
+    if p.is_dir():
+        return ImageDirSource(p)
+    if p.suffix == ".y4m":
+        return Y4MSource(p)
+    if p.suffix == ".npy":
+        return NpySource(p)
+    raise ValueError(f"unsupported video source {spec!r} (no OpenCV/ffmpeg here: use .y4m, .npy, an image "
+                     "directory, 'live' or 'synthetic:<n>:<W>x<H>')")
+
+
+# ----------------------------------------------------------------------------- sinks
+class Y4MWriter:
+    """YUV4MPEG2 4:4:4 writer (cv2.VideoWriter replacement)."""
+
+    def __init__(self, path, width, height, fps=30):
+        self.path, self.w, self.h = str(path), int(width), int(height)
+        self.f = open(self.path, "wb")
+        self.f.write(f"YUV4MPEG2 W{self.w} H{self.h} F{int(fps)}:1 Ip A1:1 C444\n".encode())
+        self.frames = 0
+
+    def write(self, frame: np.ndarray):
+        if frame.shape[0] != self.h or frame.shape[1] != self.w:
+            raise ValueError(f"frame {frame.shape} does not match writer {self.h}x{self.w}")
+        self.f.write(b"FRAME\n")
+        self.f.write(bgr_to_yuv444(frame).tobytes())
+        self.frames += 1
+
+    def release(self):
+        if self.f and not self.f.closed:
+            self.f.close()
+
+
+class NpyWriter:
+    def __init__(self, path, width, height, fps=30):
+        self.path, self.frames_list = str(path), []
+        self.frames = 0
+
+    def write(self, frame):
+        self.frames_list.append(np.array(frame, copy=True))
+        self.frames += 1
+
+    def release(self):
+        if self.frames_list is not None:
+            np.save(self.path, np.stack(self.frames_list) if self.frames_list else np.zeros((0, 0, 0, 3), np.uint8))
+            self.frames_list = None
+
+
+class PngDirWriter:
+    def __init__(self, path, width, height, fps=30):
+        self.dir = Path(path)
+        self.dir.mkdir(parents=True, exist_ok=True)
+        self.frames = 0
+
+    def write(self, frame):
+        from PIL import Image
+
+        Image.fromarray(np.ascontiguousarray(frame[..., ::-1])).save(self.dir / f"{self.frames:06d}.png")
+        self.frames += 1
+
+    def release(self):
+        pass
+
+
+def open_sink(path, width, height, fps=30):
+    s = str(path)
+    if s.endswith(".npy"):
+        return NpyWriter(path, width, height, fps)
+    if s.endswith(".y4m"):
+        return Y4MWriter(path, width, height, fps)
+    if os.path.splitext(s)[1] == "":
+        return PngDirWriter(path, width, height, fps)
+    return Y4MWriter(s + ".y4m", width, height, fps)

@@ -103,7 +103,8 @@ def test_cross_entropy(gpu, V, Vp):
     (loss * 2.0).backward()
     (ref * 2.0).backward()
     assert torch.allclose(logits.grad.float(), l32.grad, atol=2e-4, rtol=2e-2)
-    assert logits.grad[:, V:].abs().max().item() == 0.0
+    if Vp > V:
+        assert logits.grad[:, V:].abs().max().item() == 0.0
 
 
 @pytest.mark.parametrize("max_norm", [0.0, 1.0])
