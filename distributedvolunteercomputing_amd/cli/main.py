@@ -1,0 +1,101 @@
+"""Command-line entry points with the reference's REPLs.
+
+  python server.py [server_ip] [--port 9999] ...          REPL: `quit`
+  python worker.py [server_ip own_ip] [--port 9999] ...   REPL: `request live|<path>`, `end`, anything else quits
+  python -m distributedvolunteercomputing_amd.cli.main train ...   local-SGD training peer
+
+Positional arguments keep the reference's form (server.py:166-169, worker.py:341-344);
+everything else is an optional flag with the reference default.
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+
+
+def server_main(argv=None):
+    ap = argparse.ArgumentParser(prog="server.py", description="volunteer-computing coordinator")
+    ap.add_argument("ip", nargs="?", default="localhost")
+    ap.add_argument("--port", type=int, default=9999, help="UDP control port")
+    ap.add_argument("--policy", default="round_robin", choices=["round_robin", "least_loaded"])
+    ap.add_argument("--credits", type=int, default=2, help="max chunks in flight per volunteer")
+    ap.add_argument("--lease", type=float, default=10.0, help="heartbeat lease (s)")
+    ap.add_argument("--ephemeral-ports", action="store_true", help="data ports from the OS instead of 5555..5599")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    from ..control.coordinator import coordinator
+
+    c = coordinator(a.ip, a.port, ephemeral_ports=a.ephemeral_ports, policy=a.policy, credits=a.credits,
+                    lease_s=a.lease, verbose=a.verbose)
+    print(f"\nlistening on {a.ip} port {c.control_port}", flush=True)
+    while True:
+        try:
+            line = input("\nEnter quit to exit\n")
+        except EOFError:
+            line = "quit"
+        if line.strip() == "quit":
+            c.exit_threads()
+            print("done.")
+            return 0
+        if line.strip() == "status":
+            print(c.status())
+
+
+def worker_main(argv=None):
+    ap = argparse.ArgumentParser(prog="worker.py", description="volunteer client (worker / requester)")
+    ap.add_argument("server_ip", nargs="?", default="localhost")
+    ap.add_argument("own_ip", nargs="?", default="localhost")
+    ap.add_argument("--port", type=int, default=9999, help="coordinator UDP control port")
+    ap.add_argument("--data-port", type=int, default=5554, help="own data port (0 = ephemeral)")
+    ap.add_argument("--prototxt", default=None, help="Caffe prototxt (default: built-in MobileNet-SSD)")
+    ap.add_argument("--caffemodel", default="MobileNetSSD_deploy.caffemodel",
+                    help="weights (random init when absent, as in this environment)")
+    ap.add_argument("--device", default=None, help="cuda:N or cpu (default: cuda if available)")
+    ap.add_argument("--confidence", type=float, default=0.2)
+    ap.add_argument("--chunk", type=int, default=100)
+    ap.add_argument("--out-dir", default=".")
+    ap.add_argument("--out-ext", default=".y4m", choices=[".y4m", ".npy", ""])
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    from ..control.peer import client
+    from ..jobs.video import DetectorEngine
+
+    eng = DetectorEngine(device=a.device, prototxt=a.prototxt, caffemodel=a.caffemodel, conf_thresh=a.confidence)
+    w = client(a.server_ip, a.own_ip, control_port=a.port, my_port=a.data_port, engine=eng, out_dir=a.out_dir,
+               out_ext=a.out_ext, verbose=a.verbose, chunk=a.chunk)
+    while True:
+        try:
+            line = input("\nEnter request to become requester or end to stop requesting or quit to exit\n")
+        except EOFError:
+            line = "quit"
+        if "request" in line:
+            parts = line.split(" ")
+            if len(parts) < 2:
+                print("usage: request live|<path>")
+                continue
+            w.become_requester(parts[1])
+        elif line == "end":
+            w.stop_requesting_thread()
+        else:
+            w.exit_threads()
+            print("done.")
+            return 0
+
+
+def train_main(argv=None):
+    from ..jobs.train import main as tmain
+
+    return tmain(argv)
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] not in ("server", "worker", "train"):
+        print("usage: python -m distributedvolunteercomputing_amd.cli.main {server|worker|train} ...")
+        return 2
+    cmd, rest = argv[0], argv[1:]
+    return {"server": server_main, "worker": worker_main, "train": train_main}[cmd](rest)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

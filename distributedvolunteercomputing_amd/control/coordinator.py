@@ -1,0 +1,307 @@
+"""The coordinator: membership, data-port allocation, chunk dispatch, result routing.
+
+Public API kept from the reference (/root/reference/server.py):
+``coordinator(ip='localhost')``, ``.exit_threads()``, ``.log(msg)``, class-level tunables
+``verbose``, ``req_rep``, ``max_buffer`` and the 5555..5599 data-port pool; the UDP verbs
+join/request/stop/end with ``ok||<port>`` / ``ok`` replies.
+
+What happens where:
+* UDP control thread (``manager``)      — reference C4, plus ``hb``/``status`` verbs.
+* one ingest thread per volunteer       — reference C5: a ``FrameHub`` on that volunteer's port;
+  ``request`` chunks go to the scheduler, ``processed`` chunks to the requester's router.
+* dispatcher thread                     — reference C6, but the policy/ledger is the C++
+  ``ChunkScheduler``: no dropped chunks, requester exclusion, per-worker credits, re-dispatch.
+* one outbox thread per volunteer       — owns that volunteer's ``FrameSender``; both dispatched
+  work and routed results go through it, so a socket is never used by two threads
+  (the reference shares one REQ socket between two threads).
+* lease monitor                         — expires silent volunteers, re-queues their chunks.
+
+All mutable state is per instance (the reference keeps it in class attributes shared by every
+instance, server.py:13-24).
+"""
+from __future__ import annotations
+
+import itertools
+import json
+import queue
+import socket
+import threading
+import time
+from collections import deque
+
+from .. import _native_loader
+from ..utils.metrics import Metrics
+from . import protocol
+from .transport import FrameHub, FrameSender
+
+
+class _Volunteer:
+    def __init__(self, addr, port, hub, sender):
+        self.addr = addr
+        self.port = port
+        self.hub = hub
+        self.sender = sender
+        self.outbox: queue.Queue = queue.Queue()
+        self.alive = True
+        self.threads: list[threading.Thread] = []
+
+
+class coordinator:  # noqa: N801  (reference class name)
+    verbose = False
+    req_rep = True
+    max_buffer = 40
+    port_pool = tuple(range(5555, 5600))
+    lease_s = 10.0
+
+    def log(self, message):
+        if self.verbose:
+            print(message, flush=True)
+
+    def __init__(self, ip: str = "localhost", control_port: int = protocol.DEFAULT_CONTROL_PORT, *,
+                 ephemeral_ports: bool = False, max_clients: int | None = None, policy: str = "round_robin",
+                 credits: int = 2, lease_s: float | None = None, verbose: bool | None = None):
+        if verbose is not None:
+            self.verbose = verbose
+        if lease_s is not None:
+            self.lease_s = lease_s
+        N = _native_loader.native()
+        pol = N.ChunkScheduler.Policy.LEAST_LOADED if policy == "least_loaded" else N.ChunkScheduler.Policy.ROUND_ROBIN
+        self.sched = N.ChunkScheduler(int(pol), credits)
+        self.ephemeral = ephemeral_ports
+        nports = max_clients or len(self.port_pool)
+        self.free_ports = deque([0] * nports if ephemeral_ports else list(self.port_pool)[:nports])
+        self.vols: dict[str, _Volunteer] = {}
+        self.port_to_client: dict[int, str] = {}
+        self.chunks: dict[int, tuple] = {}
+        self.requesters: set[str] = set()
+        self._ids = itertools.count(1)
+        self._lock = threading.RLock()
+        self._work = threading.Condition()
+        self.metrics = Metrics("coordinator")
+        self.continue_listening = True
+        self.continue_send_request = True
+
+        self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        self.sock.bind(("", int(control_port)))
+        self.sock.settimeout(0.25)
+        self.control_port = self.sock.getsockname()[1]
+        self.my_ip = f"{ip}:{self.control_port}"
+        self._threads = [
+            threading.Thread(target=self.manager, name="vcx-manager", daemon=True),
+            threading.Thread(target=self.send_request, name="vcx-dispatch", daemon=True),
+            threading.Thread(target=self._lease_monitor, name="vcx-lease", daemon=True),
+        ]
+        for t in self._threads:
+            t.start()
+        self.log(f"listening on {self.my_ip}")
+
+    # ------------------------------------------------------------------ control plane
+    def manager(self):
+        while self.continue_listening:
+            try:
+                data, src = self.sock.recvfrom(4096)
+            except socket.timeout:
+                continue
+            except OSError:
+                break
+            verb, addr = protocol.decode(data)
+            if verb is None:
+                continue
+            try:
+                reply = self._handle(verb, addr)
+            except Exception as e:  # never let one bad datagram kill the control loop
+                reply = f"err{protocol.SEP}{e}".encode()
+            if reply is not None:
+                try:
+                    self.sock.sendto(reply, src)
+                except OSError:
+                    pass
+        self.log("manager terminated.")
+
+    def _handle(self, verb, addr):
+        now = time.time()
+        if verb == "join":
+            return self._join(addr, now)
+        if verb == "request":
+            self.sched.set_available(addr, False)
+            with self._lock:
+                self.requesters.add(addr)
+            self.metrics.incr("requests")
+            return protocol.reply_ok()
+        if verb == "stop":
+            self.sched.set_available(addr, True)
+            self._kick()
+            return protocol.reply_ok()
+        if verb == "end":
+            self._remove(addr, reason="end")
+            return protocol.reply_ok()
+        if verb == "hb":
+            self.sched.heartbeat(addr, now)
+            return protocol.reply_ok()
+        if verb == "status":
+            return protocol.reply_ok(json.dumps(self.status()))
+        return None
+
+    def _join(self, addr, now):
+        with self._lock:
+            v = self.vols.get(addr)
+            if v is not None:  # idempotent re-join (lost ack): same port, no duplicate
+                self.sched.add_worker(addr, now)
+                return protocol.reply_ok(str(v.port))
+            if not self.free_ports:
+                return f"err{protocol.SEP}no free data port".encode()
+            port = self.free_ports.popleft()
+            hub = FrameHub(port, REQ_REP=self.req_rep, capacity=max(2, self.max_buffer))
+            port = hub.port
+            host, cport = protocol.split_addr(addr)
+            try:
+                sender = FrameSender(f"tcp://{host}:{cport}", REQ_REP=self.req_rep, connect_timeout=5.0)
+            except Exception:
+                hub.close()
+                self.free_ports.appendleft(0 if self.ephemeral else port)
+                raise
+            v = _Volunteer(addr, port, hub, sender)
+            self.vols[addr] = v
+            self.port_to_client[port] = addr
+            for fn, nm in ((self._ingest, "ingest"), (self._outbox, "outbox")):
+                t = threading.Thread(target=fn, args=(v,), name=f"vcx-{nm}-{addr}", daemon=True)
+                v.threads.append(t)
+                t.start()
+            self.sched.add_worker(addr, now)
+            self.metrics.incr("joins")
+            self.log(f"join {addr} -> data port {port}")
+        self._kick()
+        return protocol.reply_ok(str(port))
+
+    def _remove(self, addr, reason):
+        with self._lock:
+            v = self.vols.pop(addr, None)
+            self.requesters.discard(addr)
+        requeued = self.sched.remove_worker(addr)
+        self.sched.cancel_requester(addr)
+        if v is None:
+            return
+        v.alive = False
+        self.port_to_client.pop(v.port, None)
+        self.free_ports.append(0 if self.ephemeral else v.port)
+        v.outbox.put(None)
+        v.hub.close()
+        v.sender.close()
+        self.metrics.incr("leaves_" + reason)
+        if requeued:
+            self.metrics.incr("redispatched", len(requeued))
+            self.log(f"{addr} left ({reason}); re-queued chunks {requeued}")
+        self._kick()
+
+    def _lease_monitor(self):
+        while self.continue_listening:
+            time.sleep(max(0.05, self.lease_s / 4))
+            for addr in self.sched.expire(time.time(), self.lease_s):
+                self.log(f"lease expired: {addr}")
+                self._remove(addr, reason="lease")
+
+    # ------------------------------------------------------------------ data plane
+    def _ingest(self, v: _Volunteer):
+        while v.alive and self.continue_listening:
+            r = v.hub.recv_frame(timeout=0.25)
+            if r is None:
+                continue
+            hdr, arr, _ = r
+            self.sched.heartbeat(v.addr, time.time())
+            info = hdr.get("msg", "")
+            parts = info.split(protocol.SEP)
+            if len(parts) < 2:
+                continue
+            requester, command = parts[0], parts[1]
+            if command == "request":
+                while self.req_rep and self.sched.queued() > self.max_buffer and v.alive:
+                    time.sleep(0.005)  # back-pressure: the hub stops acking, TCP throttles the requester
+                cid = next(self._ids)
+                with self._lock:
+                    self.chunks[cid] = (info, arr)
+                self.sched.submit(cid, requester)
+                self.metrics.incr("chunks_in")
+                self._kick()
+            elif command == "processed":
+                cid = int(hdr.get("chunk", -1))
+                if not self.sched.complete(cid):
+                    self.metrics.incr("duplicate_results")
+                    continue  # late duplicate of a re-dispatched chunk
+                with self._lock:
+                    self.chunks.pop(cid, None)
+                    dst = self.vols.get(requester)
+                if dst is not None:
+                    dst.outbox.put((info, arr, {"chunk": cid}))
+                self.metrics.incr("chunks_done")
+                self._kick()
+
+    def _outbox(self, v: _Volunteer):
+        while v.alive:
+            item = v.outbox.get()
+            if item is None:
+                break
+            info, arr, meta = item
+            ok = v.sender.send_image(info, arr, **meta)
+            if not ok:
+                self.log(f"send to {v.addr} failed; removing")
+                self._remove(v.addr, reason="broken")
+                break
+
+    def _kick(self):
+        with self._work:
+            self._work.notify_all()
+
+    def send_request(self):
+        """Dispatcher (reference C6): FIFO chunks -> eligible volunteers (never dropped)."""
+        while self.continue_send_request:
+            a = self.sched.next()
+            if not a.valid():
+                with self._work:
+                    self._work.wait(timeout=0.05)
+                continue
+            with self._lock:
+                item = self.chunks.get(a.chunk)
+                v = self.vols.get(a.worker)
+            if item is None:
+                self.sched.complete(a.chunk)
+                continue
+            if v is None:
+                self.sched.requeue_front(a.chunk, a.requester)
+                continue
+            info, arr = item
+            v.outbox.put((info, arr, {"chunk": a.chunk}))
+            self.metrics.incr("dispatched")
+        self.log("send_request terminated.")
+
+    # ------------------------------------------------------------------ misc
+    def status(self) -> dict:
+        return {
+            "workers": self.sched.workers(),
+            "available": self.sched.available_workers(),
+            "queued": self.sched.queued(),
+            "inflight": self.sched.inflight(),
+            "dispatched": self.sched.dispatched,
+            "free_ports": len(self.free_ports),
+            "metrics": self.metrics.snapshot(),
+        }
+
+    @property
+    def clients(self):
+        """The available worker pool (reference attribute name)."""
+        return self.sched.available_workers()
+
+    def exit_threads(self):
+        self.continue_listening = False
+        self.continue_send_request = False
+        self._kick()
+        for addr in list(self.vols):
+            self._remove(addr, reason="shutdown")
+        for t in self._threads:
+            t.join(timeout=2)
+        try:
+            self.sock.close()
+        except OSError:
+            pass
+
+
+Coordinator = coordinator

@@ -1,0 +1,102 @@
+"""Control-plane wire protocol (UDP datagrams), compatible with the reference.
+
+Requests are UTF-8 datagrams ``"<verb>||<ip>:<port>"`` sent to the coordinator's control port
+(default 9999); replies are ``"ok||<port>"`` for ``join`` and ``"ok"`` otherwise
+(/root/reference/server.py:100-156, worker.py:50-68).
+
+Verbs: ``join`` (enter the worker pool, get a data port), ``request`` (become a requester,
+leave the pool), ``stop`` (stop requesting, back to the pool), ``end`` (leave). New verbs:
+``hb`` (heartbeat; renews the lease, reply ``ok``), ``status`` (reply ``ok||<json>``).
+
+Differences from the reference, by design:
+* verbs are matched EXACTLY on the field before ``||`` (the reference matches substrings, so
+  an address containing "end" would be treated as the end verb);
+* client retries are bounded (the reference retries forever on a 10 s select);
+* a repeated ``join`` from the same address is idempotent (the reference leaks a port and
+  double-inserts the client, server.py:106-109).
+"""
+from __future__ import annotations
+
+import select
+import socket
+import time
+
+VERBS = ("join", "request", "stop", "end", "hb", "status")
+SEP = "||"
+DEFAULT_CONTROL_PORT = 9999
+
+
+def encode(verb: str, addr: str) -> bytes:
+    if verb not in VERBS:
+        raise ValueError(f"unknown verb {verb!r}")
+    return f"{verb}{SEP}{addr}".encode("utf-8")
+
+
+def decode(data: bytes):
+    """-> (verb, addr) or (None, None) for a malformed datagram."""
+    try:
+        s = data.decode("utf-8")
+    except UnicodeDecodeError:
+        return None, None
+    parts = s.split(SEP, 1)
+    if len(parts) != 2 or parts[0] not in VERBS or not parts[1]:
+        return None, None
+    return parts[0], parts[1]
+
+
+def reply_ok(extra: str | None = None) -> bytes:
+    return ("ok" if extra is None else f"ok{SEP}{extra}").encode("utf-8")
+
+
+def parse_reply(data: bytes):
+    """-> (ok: bool, payload or None)"""
+    s = data.decode("utf-8", "replace")
+    if s == "ok":
+        return True, None
+    if s.startswith("ok" + SEP):
+        return True, s[len("ok" + SEP):]
+    return False, s
+
+
+def split_addr(addr: str):
+    host, _, port = addr.rpartition(":")
+    return host, int(port)
+
+
+class ControlClient:
+    """Sends verbs to the coordinator with bounded retries (reference: unbounded)."""
+
+    def __init__(self, server_host: str, server_port: int = DEFAULT_CONTROL_PORT, *, timeout_s: float = 2.0,
+                 retries: int = 30, verbose: bool = False):
+        self.addr = (server_host if server_host not in ("", "localhost") else "127.0.0.1", int(server_port))
+        self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        self.timeout_s = timeout_s
+        self.retries = retries
+        self.verbose = verbose
+
+    def call(self, verb: str, my_addr: str, *, retries: int | None = None):
+        """Send verb and wait for an `ok` reply. Returns the reply payload (or None)."""
+        msg = encode(verb, my_addr)
+        n = self.retries if retries is None else retries
+        last = None
+        for i in range(max(1, n)):
+            if self.verbose:
+                print(f"sending message trial {i}...")
+            self.sock.sendto(msg, self.addr)
+            t_end = time.time() + self.timeout_s
+            while True:
+                left = t_end - time.time()
+                if left <= 0:
+                    break
+                ready, _, _ = select.select([self.sock], [], [], left)
+                if not ready:
+                    break
+                data, _ = self.sock.recvfrom(4096)
+                ok, payload = parse_reply(data)
+                if ok:
+                    return payload
+                last = payload
+        raise TimeoutError(f"coordinator {self.addr} did not acknowledge {verb!r} (last reply: {last!r})")
+
+    def close(self):
+        self.sock.close()

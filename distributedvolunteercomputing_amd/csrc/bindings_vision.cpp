@@ -1,5 +1,148 @@
-// Torch bindings for the MobileNet-SSD inference kernels (vision.hip). Filled in as the
-// kernels land; registering an empty set keeps the module layout stable.
+// Torch bindings for the MobileNet-SSD inference kernels (kernels/vision.hip).
+// Host-side shape checks guard every launch (no hand-written kernel sees a shape it was not
+// written for).
 #include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
 
-void vcx_register_vision(pybind11::module& m) { (void)m; }
+#include "kernels/vcx_api_vision.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHK(x, dt)                                                      \
+  TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor");               \
+  TORCH_CHECK((x).is_contiguous(), #x " must be contiguous");           \
+  TORCH_CHECK((x).scalar_type() == (dt), #x " has dtype ", (x).scalar_type())
+
+at::Tensor resize_area_u8(at::Tensor src, int64_t h, int64_t w) {
+  CHK(src, at::kByte);
+  TORCH_CHECK(src.dim() == 4 && src.size(3) == 3, "expect [N,H,W,3] uint8");
+  TORCH_CHECK(h > 0 && w > 0 && w <= src.size(2) && h <= src.size(1), "area resize is a downscale");
+  auto dst = at::empty({src.size(0), h, w, 3}, src.options());
+  vcx_resize_area_u8(src.data_ptr<uint8_t>(), dst.data_ptr<uint8_t>(), (int)src.size(0), (int)src.size(1),
+                     (int)src.size(2), (int)h, (int)w, cur_stream());
+  return dst;
+}
+
+at::Tensor resize_bilinear_u8(at::Tensor src, int64_t h, int64_t w) {
+  CHK(src, at::kByte);
+  TORCH_CHECK(src.dim() == 4 && src.size(3) == 3 && h > 0 && w > 0);
+  auto dst = at::empty({src.size(0), h, w, 3}, src.options());
+  vcx_resize_bilinear_u8(src.data_ptr<uint8_t>(), dst.data_ptr<uint8_t>(), (int)src.size(0), (int)src.size(1),
+                         (int)src.size(2), (int)h, (int)w, cur_stream());
+  return dst;
+}
+
+at::Tensor blob_bilinear(at::Tensor src, int64_t S, double scale, double mean) {
+  CHK(src, at::kByte);
+  TORCH_CHECK(src.dim() == 4 && src.size(3) == 3 && S > 0);
+  auto dst = at::empty({src.size(0), S, S, 4}, src.options().dtype(at::kBFloat16));
+  vcx_blob_bilinear(src.data_ptr<uint8_t>(), dst.data_ptr(), (int)src.size(0), (int)src.size(1), (int)src.size(2),
+                    (int)S, (float)scale, (float)mean, cur_stream());
+  return dst;
+}
+
+at::Tensor im2col_nhwc(at::Tensor x, int64_t C, int64_t k, int64_t stride, int64_t pad, int64_t Kp) {
+  CHK(x, at::kBFloat16);
+  TORCH_CHECK(x.dim() == 4 && C <= x.size(3) && Kp % 32 == 0 && Kp >= k * k * C);
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2);
+  const int64_t Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0);
+  auto out = at::empty({N * Ho * Wo, Kp}, x.options());
+  vcx_im2col_nhwc(x.data_ptr(), out.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)x.size(3), (int)Ho, (int)Wo,
+                  (int)k, (int)k, (int)stride, (int)pad, (int)Kp, cur_stream());
+  return out;
+}
+
+at::Tensor dwconv3x3(at::Tensor x, at::Tensor w, at::Tensor b, int64_t stride, bool relu) {
+  CHK(x, at::kBFloat16);
+  CHK(w, at::kBFloat16);
+  CHK(b, at::kFloat);
+  TORCH_CHECK(x.dim() == 4);
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && w.numel() == 9 * C && b.numel() == C && (stride == 1 || stride == 2));
+  const int64_t Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  auto y = at::empty({N, Ho, Wo, C}, x.options());
+  vcx_dwconv3x3(x.data_ptr(), w.data_ptr(), b.data_ptr<float>(), y.data_ptr(), (int)N, (int)H, (int)W, (int)C,
+                (int)Ho, (int)Wo, (int)stride, relu ? 1 : 0, cur_stream());
+  return y;
+}
+
+at::Tensor gemm_bias_act(at::Tensor X, at::Tensor Wt, c10::optional<at::Tensor> bias, bool relu) {
+  CHK(X, at::kBFloat16);
+  CHK(Wt, at::kBFloat16);
+  TORCH_CHECK(X.dim() == 2 && Wt.dim() == 2 && X.size(1) == Wt.size(1), "X [M,K] . Wt[N,K]^T");
+  const int64_t M = X.size(0), K = X.size(1), N = Wt.size(0);
+  TORCH_CHECK(K % 32 == 0, "K must be a multiple of 32");
+  TORCH_CHECK(M < INT32_MAX && M * K < (int64_t)1 << 40);
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    CHK((*bias), at::kFloat);
+    TORCH_CHECK(bias->numel() == N);
+    bp = bias->data_ptr<float>();
+  }
+  auto Y = at::empty({M, N}, X.options());
+  vcx_gemm_bias_act(X.data_ptr(), Wt.data_ptr(), bp, Y.data_ptr(), (int)M, (int)N, (int)K, (int)N, relu ? 1 : 0,
+                    cur_stream());
+  return Y;
+}
+
+std::vector<at::Tensor> ssd_detect(at::Tensor conf, at::Tensor loc, at::Tensor pri, at::Tensor var, int64_t C,
+                                   int64_t bg, double thresh, double nms_thresh, int64_t topk, int64_t keep) {
+  CHK(conf, at::kBFloat16);
+  CHK(loc, at::kBFloat16);
+  CHK(pri, at::kFloat);
+  CHK(var, at::kFloat);
+  const int64_t N = conf.size(0);
+  const int64_t P = pri.numel() / 4;
+  TORCH_CHECK(conf.numel() == N * P * C && loc.numel() == N * P * 4 && var.numel() == P * 4);
+  TORCH_CHECK(P <= 2048, "ssd_detect: at most 2048 priors per image");
+  TORCH_CHECK(topk > 0 && topk <= 256 && keep > 0 && keep <= 4096 && C >= 2 && C <= 63 && bg >= 0 && bg < C);
+  TORCH_CHECK((C - 1) * topk <= 4096, "ssd_detect: (C-1)*topk must fit the merge sort");
+  auto fo = conf.options().dtype(at::kFloat);
+  auto io = conf.options().dtype(at::kInt);
+  auto cls_out = at::empty({N, C, topk, 5}, fo);
+  auto cls_cnt = at::zeros({N, C}, io);
+  auto out = at::zeros({N, keep, 7}, fo);
+  auto cnt = at::empty({N}, io);
+  vcx_ssd_detect(conf.data_ptr(), loc.data_ptr(), pri.data_ptr<float>(), var.data_ptr<float>(),
+                 cls_out.data_ptr<float>(), cls_cnt.data_ptr<int>(), out.data_ptr<float>(), cnt.data_ptr<int>(),
+                 (int)N, (int)P, (int)C, (int)bg, (float)thresh, (float)nms_thresh, (int)topk, (int)keep,
+                 cur_stream());
+  return {out, cnt};
+}
+
+at::Tensor annotate(at::Tensor frames, at::Tensor dets, at::Tensor det_cnt, int64_t label, double thresh,
+                    int64_t box_bgr, at::Tensor name_mask, int64_t nm_x, int64_t nm_y, int64_t name_bgr,
+                    at::Tensor lab_masks, int64_t lm_x, int64_t lm_y, int64_t lab_bgr) {
+  CHK(frames, at::kByte);
+  CHK(dets, at::kFloat);
+  CHK(det_cnt, at::kInt);
+  CHK(name_mask, at::kByte);
+  CHK(lab_masks, at::kByte);
+  TORCH_CHECK(frames.dim() == 4 && frames.size(3) == 3 && dets.dim() == 3 && dets.size(2) == 7);
+  TORCH_CHECK(dets.size(0) == frames.size(0) && det_cnt.numel() == frames.size(0));
+  TORCH_CHECK(name_mask.dim() == 2 && lab_masks.dim() == 3);
+  auto counts = at::zeros({frames.size(0)}, det_cnt.options());
+  vcx_annotate(frames.data_ptr<uint8_t>(), (int)frames.size(0), (int)frames.size(1), (int)frames.size(2),
+               dets.data_ptr<float>(), det_cnt.data_ptr<int>(), (int)dets.size(1), (int)label, (float)thresh,
+               (uint32_t)box_bgr, name_mask.data_ptr<uint8_t>(), (int)name_mask.size(0), (int)name_mask.size(1),
+               (int)nm_x, (int)nm_y, (uint32_t)name_bgr, lab_masks.data_ptr<uint8_t>(), (int)lab_masks.size(0),
+               (int)lab_masks.size(1), (int)lab_masks.size(2), (int)lm_x, (int)lm_y, (uint32_t)lab_bgr,
+               counts.data_ptr<int>(), cur_stream());
+  return counts;
+}
+
+}  // namespace
+
+void vcx_register_vision(pybind11::module& m) {
+  m.def("resize_area_u8", &resize_area_u8);
+  m.def("resize_bilinear_u8", &resize_bilinear_u8);
+  m.def("blob_bilinear", &blob_bilinear);
+  m.def("im2col_nhwc", &im2col_nhwc);
+  m.def("dwconv3x3", &dwconv3x3);
+  m.def("gemm_bias_act", &gemm_bias_act);
+  m.def("ssd_detect", &ssd_detect);
+  m.def("annotate", &annotate);
+}

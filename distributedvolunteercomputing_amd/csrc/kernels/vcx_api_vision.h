@@ -1,0 +1,22 @@
+// Launchers of kernels/vision.hip (MobileNet-SSD inference path).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+void vcx_resize_area_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int h, int w, hipStream_t s);
+void vcx_resize_bilinear_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int h, int w, hipStream_t s);
+void vcx_blob_bilinear(const uint8_t* src, void* dst, int N, int H, int W, int S, float scale, float mean,
+                       hipStream_t s);
+void vcx_im2col_nhwc(const void* x, void* out, int N, int H, int W, int C, int Cs, int Ho, int Wo, int KH, int KW,
+                     int stride, int pad, int Kp, hipStream_t s);
+void vcx_dwconv3x3(const void* x, const void* w, const float* b, void* y, int N, int H, int W, int C, int Ho, int Wo,
+                   int stride, int relu, hipStream_t s);
+void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
+                       int relu, hipStream_t s);
+void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* cls_out,
+                    int* cls_cnt, float* out, int* out_cnt, int N, int P, int C, int bg, float thresh,
+                    float nms_thresh, int topk, int keep, hipStream_t s);
+void vcx_annotate(uint8_t* frames, int N, int h, int w, const float* dets, const int* det_cnt, int keep, int label,
+                  float thresh, uint32_t box_bgr, const uint8_t* name_mask, int nm_h, int nm_w, int nm_x, int nm_y,
+                  uint32_t name_bgr, const uint8_t* lab_masks, int lm_n, int lm_h, int lm_w, int lm_x, int lm_y,
+                  uint32_t lab_bgr, int* counts_out, hipStream_t s);

@@ -1,0 +1,601 @@
+// MobileNet-SSD inference kernels for gfx950 (reference: OpenCV DNN running
+// MobileNetSSD_deploy.prototxt on CPU, /root/reference/worker.py:185-280).
+//
+// Activations are NHWC bf16 for the whole network so that
+//   * every 1x1 convolution is a plain GEMM  Y[M=N*H*W, Cout] = X[M, Cin] . W[Cout, Cin]^T,
+//     run on MFMA (v_mfma_f32_16x16x32_bf16) with a fused bias+ReLU epilogue;
+//   * the depthwise 3x3 convolutions read 16-B channel vectors (8 channels per lane);
+//   * the SSD heads' Permute(0,2,3,1)+Flatten is the identity on NHWC data.
+// A whole 100-frame chunk is one batch, which turns the per-frame GEMVs of the reference into
+// real GEMMs (M = 100*19*19 = 36100 rows for conv11).
+#include "vcx_common.h"
+
+namespace vcx {
+
+// =====================================================================================
+// K1+K2+K3: preprocessing
+// =====================================================================================
+// (a) area (box-filter) resize uint8 BGR [N,H,W,3] -> [N,h,w,3] — imutils.resize(width=400)
+//     uses cv2.INTER_AREA; for upscaling INTER_AREA behaves bilinearly, handled by (b).
+__global__ void __launch_bounds__(256) resize_area_u8_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                              int N, int H, int W, int h, int w) {
+  const int64_t total = (int64_t)N * h * w;
+  const float sx = (float)W / w, sy = (float)H / h;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int x = (int)(i % w);
+    const int y = (int)((i / w) % h);
+    const int n = (int)(i / ((int64_t)w * h));
+    const float fx0 = x * sx, fx1 = fminf((x + 1) * sx, (float)W);
+    const float fy0 = y * sy, fy1 = fminf((y + 1) * sy, (float)H);
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, wsum = 0.f;
+    const uint8_t* base = src + (int64_t)n * H * W * 3;
+    for (int yy = (int)fy0; yy < (int)ceilf(fy1) && yy < H; ++yy) {
+      const float wy = fminf(fy1, (float)(yy + 1)) - fmaxf(fy0, (float)yy);
+      if (wy <= 0.f) continue;
+      for (int xx = (int)fx0; xx < (int)ceilf(fx1) && xx < W; ++xx) {
+        const float wx = fminf(fx1, (float)(xx + 1)) - fmaxf(fx0, (float)xx);
+        if (wx <= 0.f) continue;
+        const float wgt = wx * wy;
+        const uint8_t* p = base + ((int64_t)yy * W + xx) * 3;
+        acc0 = fmaf(wgt, (float)p[0], acc0);
+        acc1 = fmaf(wgt, (float)p[1], acc1);
+        acc2 = fmaf(wgt, (float)p[2], acc2);
+        wsum += wgt;
+      }
+    }
+    const float inv = 1.f / wsum;
+    uint8_t* q = dst + i * 3;
+    q[0] = (uint8_t)fminf(255.f, fmaxf(0.f, rintf(acc0 * inv)));
+    q[1] = (uint8_t)fminf(255.f, fmaxf(0.f, rintf(acc1 * inv)));
+    q[2] = (uint8_t)fminf(255.f, fmaxf(0.f, rintf(acc2 * inv)));
+  }
+}
+
+// (b) bilinear (half-pixel centres, cv2.INTER_LINEAR) uint8 [N,H,W,3] -> uint8 [N,h,w,3]
+__global__ void __launch_bounds__(256) resize_bilinear_u8_kernel(const uint8_t* __restrict__ src,
+                                                                  uint8_t* __restrict__ dst, int N, int H, int W,
+                                                                  int h, int w) {
+  const int64_t total = (int64_t)N * h * w;
+  const float sx = (float)W / w, sy = (float)H / h;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int x = (int)(i % w), y = (int)((i / w) % h), n = (int)(i / ((int64_t)w * h));
+    float fx = fmaxf((x + 0.5f) * sx - 0.5f, 0.f), fy = fmaxf((y + 0.5f) * sy - 0.5f, 0.f);
+    int x0 = min((int)fx, W - 1), y0 = min((int)fy, H - 1);
+    int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
+    float ax = fx - x0, ay = fy - y0;
+    const uint8_t* b = src + (int64_t)n * H * W * 3;
+    for (int c = 0; c < 3; ++c) {
+      float v00 = b[((int64_t)y0 * W + x0) * 3 + c], v01 = b[((int64_t)y0 * W + x1) * 3 + c];
+      float v10 = b[((int64_t)y1 * W + x0) * 3 + c], v11 = b[((int64_t)y1 * W + x1) * 3 + c];
+      float v = (v00 * (1 - ax) + v01 * ax) * (1 - ay) + (v10 * (1 - ax) + v11 * ax) * ay;
+      dst[i * 3 + c] = (uint8_t)fminf(255.f, fmaxf(0.f, rintf(v)));
+    }
+  }
+}
+
+// (c) cv2.resize(frame, (S,S)) bilinear -> blobFromImage(scale, mean) -> NHWC bf16, channel
+//     padded to CP (=4) lanes with zeros: [N, S, S, CP]. BGR order kept (no swapRB).
+__global__ void __launch_bounds__(256) blob_bilinear_kernel(const uint8_t* __restrict__ src, bf16* __restrict__ dst,
+                                                             int N, int H, int W, int S, float scale, float mean) {
+  const int64_t total = (int64_t)N * S * S;
+  const float sx = (float)W / S, sy = (float)H / S;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int x = (int)(i % S), y = (int)((i / S) % S), n = (int)(i / ((int64_t)S * S));
+    float fx = fmaxf((x + 0.5f) * sx - 0.5f, 0.f), fy = fmaxf((y + 0.5f) * sy - 0.5f, 0.f);
+    int x0 = min((int)fx, W - 1), y0 = min((int)fy, H - 1);
+    int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
+    float ax = fx - x0, ay = fy - y0;
+    const uint8_t* b = src + (int64_t)n * H * W * 3;
+    bf16x4 o;
+    for (int c = 0; c < 3; ++c) {
+      float v00 = b[((int64_t)y0 * W + x0) * 3 + c], v01 = b[((int64_t)y0 * W + x1) * 3 + c];
+      float v10 = b[((int64_t)y1 * W + x0) * 3 + c], v11 = b[((int64_t)y1 * W + x1) * 3 + c];
+      float v = (v00 * (1 - ax) + v01 * ax) * (1 - ay) + (v10 * (1 - ax) + v11 * ax) * ay;
+      v = rintf(fminf(255.f, fmaxf(0.f, v)));  // cv2.resize output is uint8
+      o[c] = (bf16)((v - mean) * scale);
+    }
+    o[3] = (bf16)0.f;
+    *(bf16x4*)(dst + i * 4) = o;
+  }
+}
+
+// =====================================================================================
+// im2col for dense KxK convolutions on NHWC bf16 (stem conv0 and the SSD extras' 3x3 s2)
+// out[m, k] with m = (n, oy, ox), k = (ky, kx, c) for c < C (channel stride Cs), zero-padded
+// to Kp columns (Kp % 32 == 0).
+// =====================================================================================
+__global__ void __launch_bounds__(256) im2col_nhwc_kernel(const bf16* __restrict__ x, bf16* __restrict__ out, int N,
+                                                           int H, int W, int C, int Cs, int Ho, int Wo, int KH,
+                                                           int KW, int stride, int pad, int Kp) {
+  const int64_t total = (int64_t)N * Ho * Wo * Kp;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int k = (int)(i % Kp);
+    const int64_t m = i / Kp;
+    const int ox = (int)(m % Wo), oy = (int)((m / Wo) % Ho), n = (int)(m / ((int64_t)Wo * Ho));
+    bf16 v = (bf16)0.f;
+    if (k < KH * KW * C) {
+      const int c = k % C, kx = (k / C) % KW, ky = k / (C * KW);
+      const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = x[(((int64_t)n * H + iy) * W + ix) * Cs + c];
+    }
+    out[i] = v;
+  }
+}
+
+// =====================================================================================
+// K5: depthwise 3x3 conv + bias + ReLU, NHWC bf16, stride 1|2, pad 1. 8 channels per lane.
+// w: [9][C] bf16 (tap-major so the 8 channels of one tap are one 16-B load), b: [C] fp32.
+// =====================================================================================
+__global__ void __launch_bounds__(256) dwconv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                         const float* __restrict__ b, bf16* __restrict__ y, int N,
+                                                         int H, int W, int C, int Ho, int Wo, int stride, int relu) {
+  const int C8 = C >> 3;
+  const int64_t total = (int64_t)N * Ho * Wo * C8;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c8 = (int)(i % C8);
+    const int64_t p = i / C8;
+    const int ox = (int)(p % Wo), oy = (int)((p / Wo) % Ho), n = (int)(p / ((int64_t)Wo * Ho));
+    float acc[8];
+    {
+      f32x4 b0 = *(const f32x4*)(b + c8 * 8), b1 = *(const f32x4*)(b + c8 * 8 + 4);
+      acc[0] = b0[0]; acc[1] = b0[1]; acc[2] = b0[2]; acc[3] = b0[3];
+      acc[4] = b1[0]; acc[5] = b1[1]; acc[6] = b1[2]; acc[7] = b1[3];
+    }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy * stride - 1 + ky;
+      if (iy < 0 || iy >= H) continue;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ox * stride - 1 + kx;
+        if (ix < 0 || ix >= W) continue;
+        bf16x8 xv = *(const bf16x8*)(x + (((int64_t)n * H + iy) * W + ix) * C + c8 * 8);
+        bf16x8 wv = *(const bf16x8*)(w + (ky * 3 + kx) * C + c8 * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = fmaf((float)xv[j], (float)wv[j], acc[j]);
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)(relu ? fmaxf(acc[j], 0.f) : acc[j]);
+    *(bf16x8*)(y + p * C + c8 * 8) = o;
+  }
+}
+
+// =====================================================================================
+// K6/K7/K8: GEMM  Y[M, N] = act(X[M, K] . W[N, K]^T + bias[N])   (bf16 in, fp32 acc, bf16 out)
+// Block tile 128 x BN (BN = 128 | 64), BK = 32, 256 threads = 4 waves in a 2 x 2 grid; each
+// wave owns a 64 x (BN/2) sub-tile made of 16x16 MFMA tiles (v_mfma_f32_16x16x32_bf16: one
+// MFMA per 16x16 tile per K-step). LDS rows are padded to 40 bf16 (80 B) so the 16 rows a
+// ds_read_b128 lane group touches hit 16 distinct 4-bank slots (conflict-free). Global->LDS
+// staging is double-buffered through registers (load tile k+1 while tile k feeds the MFMAs).
+// Blocks are remapped so that consecutive tiles of one M panel land on the same XCD (they
+// share the X panel through that XCD's L2). Requires K % 32 == 0; M, N arbitrary.
+// =====================================================================================
+typedef short bf16x8s __attribute__((ext_vector_type(8)));
+constexpr int GBM = 128, GBK = 32, GLDK = 40;
+
+template <int BN>
+__global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
+                                                             const float* __restrict__ bias, bf16* __restrict__ Y,
+                                                             int M, int N, int K, int ldy, int relu) {
+  __shared__ __attribute__((aligned(16))) bf16 sA[2][GBM * GLDK];
+  __shared__ __attribute__((aligned(16))) bf16 sB[2][BN * GLDK];
+  constexpr int WN = BN / 2;          // per-wave N extent
+  constexpr int TN = WN / 16;         // 16x16 tiles per wave along N
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // XCD-aware, bijective block remap (cdna guide §5 T1): group label = bid % 8
+  const int ntm = (M + GBM - 1) / GBM, ntn = (N + BN - 1) / BN;
+  const int nwg = ntm * ntn;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+    if (nwg >= 8) bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int tm = bid / ntn, tn = bid % ntn;
+  const int m0 = tm * GBM, n0 = tn * BN;
+
+  // staging: A tile 128x32 bf16 = 512 x 16 B -> 2 per thread; B tile BN x 32 -> BN/128 per thread
+  constexpr int BL = BN * 4 / 256;  // 16-B loads of B per thread
+  bf16x8s ra[2], rb[BL];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * 256, row = e >> 2, kc = (e & 3) * 8;
+      const int gm = m0 + row;
+      ra[i] = gm < M ? *(const bf16x8s*)(X + (int64_t)gm * K + k0 + kc) : bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int e = tid + i * 256, row = e >> 2, kc = (e & 3) * 8;
+      const int gn = n0 + row;
+      rb[i] = gn < N ? *(const bf16x8s*)(Wt + (int64_t)gn * K + k0 + kc) : bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * 256, row = e >> 2, kc = (e & 3) * 8;
+      *(bf16x8s*)(&sA[buf][row * GLDK + kc]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+      const int e = tid + i * 256, row = e >> 2, kc = (e & 3) * 8;
+      *(bf16x8s*)(&sB[buf][row * GLDK + kc]) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][TN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / GBK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * GBK);
+    bf16x8s af[4], bfr[TN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8s*)(&sA[cur][(wm * 64 + i * 16 + fr) * GLDK + fk]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8s*)(&sB[cur][(wn * WN + j * 16 + fr) * GLDK + fk]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r  (acc[i][j] = A-tile i x B-tile j:
+  // rows from A (M), cols from B (N))
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int gn = n0 + wn * WN + j * 16 + (lane & 15);
+    const float bv = (gn < N && bias) ? bias[gn] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gm = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (gm < M && gn < N) {
+          float v = acc[i][j][r] + bv;
+          if (relu) v = fmaxf(v, 0.f);
+          Y[(int64_t)gm * ldy + gn] = (bf16)v;
+        }
+      }
+    }
+  }
+}
+
+// =====================================================================================
+// K12+K13: DetectionOutput. Stage 1: one block per (image, foreground class).
+//   softmax(conf row)[class] > thresh -> candidates -> bitonic sort (desc score, asc prior)
+//   -> top_k -> CENTER_SIZE decode -> greedy NMS -> per-class kept list.
+// conf: [N, P, C] bf16 raw logits (the softmax is fused here), loc: [N, P, 4] bf16,
+// pri: [P*4] fp32 boxes, var: [P*4] fp32.
+// cls_out: [N, C, TOPK, 5] fp32 (score, x0, y0, x1, y1), cls_cnt: [N, C] int.
+// =====================================================================================
+constexpr int DET_MAXP = 2048;
+
+__global__ void __launch_bounds__(256) ssd_class_nms_kernel(const bf16* __restrict__ conf, const bf16* __restrict__ loc,
+                                                             const float* __restrict__ pri, const float* __restrict__ var,
+                                                             float* __restrict__ cls_out, int* __restrict__ cls_cnt,
+                                                             int P, int C, int bg, float thresh, float nms_thresh,
+                                                             int topk) {
+  __shared__ float s_score[DET_MAXP];
+  __shared__ int s_idx[DET_MAXP];
+  __shared__ float s_box[DET_MAXP / 8][4];  // topk <= 256
+  __shared__ int s_keep[DET_MAXP / 8];
+  __shared__ int s_cnt;
+  const int n = blockIdx.x / (C - 1);
+  int c = blockIdx.x % (C - 1);
+  c = c >= bg ? c + 1 : c;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  const bf16* cr = conf + (int64_t)n * P * C;
+  for (int p = tid; p < P; p += 256) {
+    const bf16* row = cr + (int64_t)p * C;
+    float mx = -INFINITY;
+    for (int k = 0; k < C; ++k) mx = fmaxf(mx, (float)row[k]);
+    float s = 0.f;
+    for (int k = 0; k < C; ++k) s += __expf((float)row[k] - mx);
+    const float prob = __expf((float)row[c] - mx) / s;
+    if (prob > thresh) {
+      const int slot = atomicAdd(&s_cnt, 1);
+      s_score[slot] = prob;
+      s_idx[slot] = p;
+    }
+  }
+  __syncthreads();
+  const int ncand = s_cnt;
+  int L = 1;
+  while (L < ncand) L <<= 1;
+  for (int i = ncand + tid; i < L; i += 256) {
+    s_score[i] = -INFINITY;
+    s_idx[i] = 0x7fffffff;
+  }
+  __syncthreads();
+  // bitonic sort, descending by score, ascending by prior index on ties
+  for (int k = 2; k <= L; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < L; i += 256) {
+        const int ij = i ^ j;
+        if (ij > i) {
+          const bool desc = (i & k) == 0;
+          const float a = s_score[i], b = s_score[ij];
+          const int ia = s_idx[i], ib = s_idx[ij];
+          const bool a_first = (a > b) || (a == b && ia < ib);
+          if (desc ? !a_first : a_first) {
+            s_score[i] = b;
+            s_score[ij] = a;
+            s_idx[i] = ib;
+            s_idx[ij] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int K = min(ncand, topk);
+  const bf16* lr = loc + (int64_t)n * P * 4;
+  for (int i = tid; i < K; i += 256) {
+    const int p = s_idx[i];
+    const float px0 = pri[p * 4], py0 = pri[p * 4 + 1], px1 = pri[p * 4 + 2], py1 = pri[p * 4 + 3];
+    const float pw = px1 - px0, ph = py1 - py0, pcx = 0.5f * (px0 + px1), pcy = 0.5f * (py0 + py1);
+    const float cx = var[p * 4] * (float)lr[p * 4] * pw + pcx;
+    const float cy = var[p * 4 + 1] * (float)lr[p * 4 + 1] * ph + pcy;
+    const float bw = __expf(var[p * 4 + 2] * (float)lr[p * 4 + 2]) * pw;
+    const float bh = __expf(var[p * 4 + 3] * (float)lr[p * 4 + 3]) * ph;
+    s_box[i][0] = cx - 0.5f * bw;
+    s_box[i][1] = cy - 0.5f * bh;
+    s_box[i][2] = cx + 0.5f * bw;
+    s_box[i][3] = cy + 0.5f * bh;
+    s_keep[i] = 1;
+  }
+  __syncthreads();
+  // greedy NMS: candidate i survives if no earlier survivor overlaps it by > nms_thresh
+  for (int i = 0; i < K; ++i) {
+    if (s_keep[i]) {
+      const float ax0 = s_box[i][0], ay0 = s_box[i][1], ax1 = s_box[i][2], ay1 = s_box[i][3];
+      const float aa = fmaxf(ax1 - ax0, 0.f) * fmaxf(ay1 - ay0, 0.f);
+      for (int j = i + 1 + tid; j < K; j += 256) {
+        if (!s_keep[j]) continue;
+        const float bx0 = s_box[j][0], by0 = s_box[j][1], bx1 = s_box[j][2], by1 = s_box[j][3];
+        const float iw = fminf(ax1, bx1) - fmaxf(ax0, bx0), ih = fminf(ay1, by1) - fmaxf(ay0, by0);
+        const float inter = fmaxf(iw, 0.f) * fmaxf(ih, 0.f);
+        const float ba = fmaxf(bx1 - bx0, 0.f) * fmaxf(by1 - by0, 0.f);
+        const float uni = aa + ba - inter;
+        const float iou = uni > 0.f ? inter / uni : 0.f;
+        if (iou > nms_thresh) s_keep[j] = 0;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int w = 0;
+    float* o = cls_out + ((int64_t)n * C + c) * topk * 5;
+    for (int i = 0; i < K; ++i) {
+      if (!s_keep[i]) continue;
+      o[w * 5 + 0] = s_score[i];
+      o[w * 5 + 1] = s_box[i][0];
+      o[w * 5 + 2] = s_box[i][1];
+      o[w * 5 + 3] = s_box[i][2];
+      o[w * 5 + 4] = s_box[i][3];
+      ++w;
+    }
+    cls_cnt[n * C + c] = w;
+  }
+}
+
+// Stage 2: one block per image. Concatenate the per-class lists (class-major, as Caffe does);
+// if more than keep_top_k survive, keep the keep_top_k highest scores (sorted descending).
+// out: [N, KEEP, 7] (img, label, score, x0, y0, x1, y1), out_cnt: [N]
+__global__ void __launch_bounds__(256) ssd_merge_kernel(const float* __restrict__ cls_out,
+                                                         const int* __restrict__ cls_cnt, float* __restrict__ out,
+                                                         int* __restrict__ out_cnt, int C, int bg, int topk, int keep) {
+  __shared__ float s_score[DET_MAXP * 2];
+  __shared__ int s_key[DET_MAXP * 2];  // class * topk + slot
+  __shared__ int s_off[64];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    int o = 0;
+    for (int c = 0; c < C; ++c) {
+      s_off[c] = o;
+      if (c != bg) o += cls_cnt[n * C + c];
+    }
+    s_off[C] = o;
+  }
+  __syncthreads();
+  const int total = s_off[C];
+  const float* co = cls_out + (int64_t)n * C * topk * 5;
+  float* on = out + (int64_t)n * keep * 7;
+  if (total <= keep) {
+    for (int c = 0; c < C; ++c) {
+      if (c == bg) continue;
+      const int cnt = cls_cnt[n * C + c];
+      for (int s = tid; s < cnt; s += 256) {
+        const float* src = co + ((int64_t)c * topk + s) * 5;
+        float* d = on + (int64_t)(s_off[c] + s) * 7;
+        d[0] = (float)n; d[1] = (float)c; d[2] = src[0];
+        d[3] = src[1]; d[4] = src[2]; d[5] = src[3]; d[6] = src[4];
+      }
+    }
+    if (tid == 0) out_cnt[n] = total;
+    return;
+  }
+  int L = 1;
+  while (L < total) L <<= 1;
+  for (int c = 0; c < C; ++c) {
+    if (c == bg) continue;
+    const int cnt = cls_cnt[n * C + c];
+    for (int s = tid; s < cnt; s += 256) {
+      s_score[s_off[c] + s] = co[((int64_t)c * topk + s) * 5];
+      s_key[s_off[c] + s] = c * topk + s;
+    }
+  }
+  for (int i = total + tid; i < L; i += 256) {
+    s_score[i] = -INFINITY;
+    s_key[i] = 0x7fffffff;
+  }
+  __syncthreads();
+  for (int k = 2; k <= L; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < L; i += 256) {
+        const int ij = i ^ j;
+        if (ij > i) {
+          const bool desc = (i & k) == 0;
+          const float a = s_score[i], b = s_score[ij];
+          const int ka = s_key[i], kb = s_key[ij];
+          const bool a_first = (a > b) || (a == b && ka < kb);
+          if (desc ? !a_first : a_first) {
+            s_score[i] = b; s_score[ij] = a;
+            s_key[i] = kb; s_key[ij] = ka;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < keep; i += 256) {
+    const int key = s_key[i], c = key / topk, s = key % topk;
+    const float* src = co + ((int64_t)c * topk + s) * 5;
+    float* d = on + (int64_t)i * 7;
+    d[0] = (float)n; d[1] = (float)c; d[2] = src[0];
+    d[3] = src[1]; d[4] = src[2]; d[5] = src[3]; d[6] = src[4];
+  }
+  if (tid == 0) out_cnt[n] = keep;
+}
+
+// =====================================================================================
+// K14: annotation. One block per frame: 2-px boxes for `label` detections above `thresh`
+// (colour box_bgr), then two pre-rasterised text masks: the requester name and the
+// "person: k" label chosen by the per-frame count k (mask table indexed by k).
+// frames: [N, h, w, 3] uint8 BGR (in place); dets: [N, KEEP, 7]; det_cnt: [N]
+// =====================================================================================
+__global__ void __launch_bounds__(256) annotate_kernel(uint8_t* __restrict__ frames, int h, int w,
+                                                        const float* __restrict__ dets, const int* __restrict__ det_cnt,
+                                                        int keep, int label, float thresh, uint32_t box_bgr,
+                                                        const uint8_t* __restrict__ name_mask, int nm_h, int nm_w,
+                                                        int nm_x, int nm_y, uint32_t name_bgr,
+                                                        const uint8_t* __restrict__ lab_masks, int lm_n, int lm_h,
+                                                        int lm_w, int lm_x, int lm_y, uint32_t lab_bgr,
+                                                        int* __restrict__ counts_out) {
+  __shared__ int s_count;
+  const int n = blockIdx.x, tid = threadIdx.x;
+  uint8_t* f = frames + (int64_t)n * h * w * 3;
+  const float* dn = dets + (int64_t)n * keep * 7;
+  const int nd = det_cnt[n];
+  if (tid == 0) s_count = 0;
+  __syncthreads();
+  auto put = [&](int x, int y, uint32_t bgr) {
+    if (x >= 0 && x < w && y >= 0 && y < h) {
+      uint8_t* p = f + ((int64_t)y * w + x) * 3;
+      p[0] = bgr & 255;
+      p[1] = (bgr >> 8) & 255;
+      p[2] = (bgr >> 16) & 255;
+    }
+  };
+  for (int d = 0; d < nd; ++d) {
+    const float* det = dn + d * 7;
+    if ((int)det[1] != label || det[2] <= thresh) continue;
+    if (tid == 0) s_count++;
+    // box = det[3:7] * [w, h, w, h], truncated like ndarray.astype("int")
+    const int x0 = (int)(det[3] * w), y0 = (int)(det[4] * h), x1 = (int)(det[5] * w), y1 = (int)(det[6] * h);
+    const int bw = x1 - x0 + 1, bh = y1 - y0 + 1;
+    if (bw <= 0 || bh <= 0 || bw > 4 * w || bh > 4 * h) continue;
+    for (int t = tid; t < 2 * bw + 2 * bh; t += 256) {  // thickness 2: the line and its outer neighbour
+      int x, y;
+      if (t < bw) { x = x0 + t; y = y0; }
+      else if (t < 2 * bw) { x = x0 + t - bw; y = y1; }
+      else if (t < 2 * bw + bh) { x = x0; y = y0 + t - 2 * bw; }
+      else { x = x1; y = y0 + t - 2 * bw - bh; }
+      put(x, y, box_bgr);
+      if (y == y0) put(x, y - 1, box_bgr);
+      else if (y == y1) put(x, y + 1, box_bgr);
+      if (x == x0) put(x - 1, y, box_bgr);
+      else if (x == x1) put(x + 1, y, box_bgr);
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < nm_h * nm_w; t += 256) {
+    if (name_mask[t]) put(nm_x + t % nm_w, nm_y + t / nm_w, name_bgr);
+  }
+  const int k = min(s_count, lm_n - 1);
+  const uint8_t* lm = lab_masks + (int64_t)k * lm_h * lm_w;
+  for (int t = tid; t < lm_h * lm_w; t += 256) {
+    if (lm[t]) put(lm_x + t % lm_w, lm_y + t / lm_w, lab_bgr);
+  }
+  if (tid == 0 && counts_out) counts_out[n] = s_count;
+}
+
+}  // namespace vcx
+
+// ====================================================================================== launchers
+using namespace vcx;
+
+void vcx_resize_area_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int h, int w, hipStream_t s) {
+  hipLaunchKernelGGL(resize_area_u8_kernel, dim3(stream_grid((int64_t)N * h * w, 256)), dim3(256), 0, s, src, dst, N,
+                     H, W, h, w);
+}
+
+void vcx_resize_bilinear_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int h, int w, hipStream_t s) {
+  hipLaunchKernelGGL(resize_bilinear_u8_kernel, dim3(stream_grid((int64_t)N * h * w, 256)), dim3(256), 0, s, src, dst,
+                     N, H, W, h, w);
+}
+
+void vcx_blob_bilinear(const uint8_t* src, void* dst, int N, int H, int W, int S, float scale, float mean,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(blob_bilinear_kernel, dim3(stream_grid((int64_t)N * S * S, 256)), dim3(256), 0, s, src,
+                     (bf16*)dst, N, H, W, S, scale, mean);
+}
+
+void vcx_im2col_nhwc(const void* x, void* out, int N, int H, int W, int C, int Cs, int Ho, int Wo, int KH, int KW,
+                     int stride, int pad, int Kp, hipStream_t s) {
+  hipLaunchKernelGGL(im2col_nhwc_kernel, dim3(stream_grid((int64_t)N * Ho * Wo * Kp, 256)), dim3(256), 0, s,
+                     (const bf16*)x, (bf16*)out, N, H, W, C, Cs, Ho, Wo, KH, KW, stride, pad, Kp);
+}
+
+void vcx_dwconv3x3(const void* x, const void* w, const float* b, void* y, int N, int H, int W, int C, int Ho, int Wo,
+                   int stride, int relu, hipStream_t s) {
+  hipLaunchKernelGGL(dwconv3x3_kernel, dim3(stream_grid((int64_t)N * Ho * Wo * (C / 8), 256)), dim3(256), 0, s,
+                     (const bf16*)x, (const bf16*)w, b, (bf16*)y, N, H, W, C, Ho, Wo, stride, relu);
+}
+
+void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
+                       int relu, hipStream_t s) {
+  if (N <= 64) {
+    const int nwg = ((M + GBM - 1) / GBM) * ((N + 63) / 64);
+    hipLaunchKernelGGL(gemm_bias_act_kernel<64>, dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt, bias,
+                       (bf16*)Y, M, N, K, ldy, relu);
+  } else {
+    const int nwg = ((M + GBM - 1) / GBM) * ((N + 127) / 128);
+    hipLaunchKernelGGL(gemm_bias_act_kernel<128>, dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt, bias,
+                       (bf16*)Y, M, N, K, ldy, relu);
+  }
+}
+
+void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* cls_out,
+                    int* cls_cnt, float* out, int* out_cnt, int N, int P, int C, int bg, float thresh,
+                    float nms_thresh, int topk, int keep, hipStream_t s) {
+  hipLaunchKernelGGL(ssd_class_nms_kernel, dim3(N * (C - 1)), dim3(256), 0, s, (const bf16*)conf, (const bf16*)loc,
+                     pri, var, cls_out, cls_cnt, P, C, bg, thresh, nms_thresh, topk);
+  hipLaunchKernelGGL(ssd_merge_kernel, dim3(N), dim3(256), 0, s, cls_out, cls_cnt, out, out_cnt, C, bg, topk, keep);
+}
+
+void vcx_annotate(uint8_t* frames, int N, int h, int w, const float* dets, const int* det_cnt, int keep, int label,
+                  float thresh, uint32_t box_bgr, const uint8_t* name_mask, int nm_h, int nm_w, int nm_x, int nm_y,
+                  uint32_t name_bgr, const uint8_t* lab_masks, int lm_n, int lm_h, int lm_w, int lm_x, int lm_y,
+                  uint32_t lab_bgr, int* counts_out, hipStream_t s) {
+  hipLaunchKernelGGL(annotate_kernel, dim3(N), dim3(256), 0, s, frames, h, w, dets, det_cnt, keep, label, thresh,
+                     box_bgr, name_mask, nm_h, nm_w, nm_x, nm_y, name_bgr, lab_masks, lm_n, lm_h, lm_w, lm_x, lm_y,
+                     lab_bgr, counts_out);
+}

@@ -1,0 +1,269 @@
+"""MobileNet-SSD person detector — the reference's only model (MobileNetSSD_deploy.prototxt,
+run by OpenCV DNN on CPU at /root/reference/worker.py:194,245-249).
+
+``SSDExecutor`` compiles the Caffe ``NetDef`` into a plan of MI355X kernels over NHWC bf16
+activations for a whole chunk of frames at once:
+
+  Convolution group=C (depthwise 3x3)  -> dwconv3x3 kernel (+bias +ReLU fused)
+  Convolution 1x1                      -> MFMA GEMM  [N*H*W, Cin] x [Cout, Cin]^T (+bias +ReLU)
+  Convolution kxk (stem, SSD extras)   -> im2col + the same MFMA GEMM
+  ReLU after a convolution             -> fused into the producer's epilogue
+  Permute(0,2,3,1) + Flatten           -> free (NHWC is already that order)
+  PriorBox                             -> computed once on the host, cached on the device
+  Reshape + Softmax + DetectionOutput  -> one fused softmax/decode/top-k/NMS kernel pair
+
+On CPU the same object runs the plain-PyTorch ``CaffeNet`` interpreter (the oracle).
+"""
+from __future__ import annotations
+
+import os
+import numpy as np
+import torch
+
+from .. import ops
+from ..ops import vision as V
+from .caffe import CaffeNet, Layer, NetDef, load_caffemodel, load_prototxt, prior_boxes
+
+CLASSES = ["background", "aeroplane", "bicycle", "bird", "boat", "bottle", "bus", "car", "cat", "chair", "cow",
+           "diningtable", "dog", "horse", "motorbike", "person", "pottedplant", "sheep", "sofa", "train",
+           "tvmonitor"]
+
+def _conv(name, bottom, cout, k=1, stride=1, pad=0, group=1):
+    cp = {"num_output": [cout], "kernel_size": [k]}
+    if pad:
+        cp["pad"] = [pad]
+    if stride != 1:
+        cp["stride"] = [stride]
+    if group != 1:
+        cp["group"] = [group]
+    return Layer(name, "Convolution", [bottom], [name], {"convolution_param": [cp]})
+
+
+def mobilenet_ssd_netdef(num_classes: int = 21, size: int = 300) -> NetDef:
+    """The MobileNet-SSD graph of MobileNetSSD_deploy.prototxt (119 layers), built in code:
+    MobileNet-v1 backbone (conv0 + 13 dw/pw pairs), 4 SSD extra stages, 6 multibox heads."""
+    L = []
+
+    def relu(top):
+        L.append(Layer(top + "/relu", "ReLU", [top], [top]))
+
+    L.append(_conv("conv0", "data", 32, 3, 2, 1))
+    relu("conv0")
+    chans = [(32, 64, 1), (64, 128, 2), (128, 128, 1), (128, 256, 2), (256, 256, 1), (256, 512, 2)] + \
+        [(512, 512, 1)] * 5 + [(512, 1024, 2), (1024, 1024, 1)]
+    prev = "conv0"
+    for i, (cin, cout, s) in enumerate(chans, start=1):
+        L.append(_conv(f"conv{i}/dw", prev, cin, 3, s, 1, group=cin))
+        relu(f"conv{i}/dw")
+        L.append(_conv(f"conv{i}", f"conv{i}/dw", cout))
+        relu(f"conv{i}")
+        prev = f"conv{i}"
+    for i, (mid, out) in zip(range(14, 18), [(256, 512), (128, 256), (128, 256), (64, 128)]):
+        L.append(_conv(f"conv{i}_1", prev, mid))
+        relu(f"conv{i}_1")
+        L.append(_conv(f"conv{i}_2", f"conv{i}_1", out, 3, 2, 1))
+        relu(f"conv{i}_2")
+        prev = f"conv{i}_2"
+    sources = ["conv11", "conv13", "conv14_2", "conv15_2", "conv16_2", "conv17_2"]
+    mins = [60.0, 105.0, 150.0, 195.0, 240.0, 285.0]
+    maxs = [None, 150.0, 195.0, 240.0, 285.0, 300.0]
+    for src, mn, mx in zip(sources, mins, maxs):
+        npri = 3 if mx is None else 6
+        for kind, c in (("loc", 4 * npri), ("conf", num_classes * npri)):
+            nm = f"{src}_mbox_{kind}"
+            L.append(_conv(nm, src, c))
+            L.append(Layer(nm + "_perm", "Permute", [nm], [nm + "_perm"], {"permute_param": [{"order": [0, 2, 3, 1]}]}))
+            L.append(Layer(nm + "_flat", "Flatten", [nm + "_perm"], [nm + "_flat"], {"flatten_param": [{"axis": [1]}]}))
+        pp = {"min_size": [mn], "aspect_ratio": [2.0] if mx is None else [2.0, 3.0], "flip": [True], "clip": [False],
+              "variance": [0.1, 0.1, 0.2, 0.2], "offset": [0.5]}
+        if mx is not None:
+            pp["max_size"] = [mx]
+        L.append(Layer(f"{src}_mbox_priorbox", "PriorBox", [src, "data"], [f"{src}_mbox_priorbox"],
+                       {"prior_box_param": [pp]}))
+    for kind, ax in (("loc", 1), ("conf", 1), ("priorbox", 2)):
+        sfx = "_flat" if kind != "priorbox" else ""
+        L.append(Layer(f"mbox_{kind}", "Concat", [f"{s}_mbox_{kind}{sfx}" for s in sources], [f"mbox_{kind}"],
+                       {"concat_param": [{"axis": [ax]}]}))
+    L.append(Layer("mbox_conf_reshape", "Reshape", ["mbox_conf"], ["mbox_conf_reshape"],
+                   {"reshape_param": [{"shape": [{"dim": [0, -1, num_classes]}]}]}))
+    L.append(Layer("mbox_conf_softmax", "Softmax", ["mbox_conf_reshape"], ["mbox_conf_softmax"],
+                   {"softmax_param": [{"axis": [2]}]}))
+    L.append(Layer("mbox_conf_flatten", "Flatten", ["mbox_conf_softmax"], ["mbox_conf_flatten"],
+                   {"flatten_param": [{"axis": [1]}]}))
+    L.append(Layer("detection_out", "DetectionOutput", ["mbox_loc", "mbox_conf_flatten", "mbox_priorbox"],
+                   ["detection_out"], {"detection_output_param": [{
+                       "num_classes": [num_classes], "share_location": [True], "background_label_id": [0],
+                       "nms_param": [{"nms_threshold": [0.45], "top_k": [100]}], "code_type": ["CENTER_SIZE"],
+                       "keep_top_k": [100], "confidence_threshold": [0.25]}]}))
+    return NetDef("MobileNet-SSD", ["data"], [[1, 3, size, size]], L)
+
+
+def _round_up(n, a):
+    return (n + a - 1) // a * a
+
+
+class SSDExecutor:
+    def __init__(self, net: NetDef | str | None = None, caffemodel: str | None = None, device="cpu", seed: int = 0):
+        if net is None:
+            net = mobilenet_ssd_netdef()
+        elif isinstance(net, (str, os.PathLike)):
+            net = load_prototxt(str(net))
+        self.net = net
+        weights = load_caffemodel(caffemodel) if caffemodel and os.path.exists(caffemodel) else None
+        self.ref = CaffeNet(net, weights, seed=seed)
+        self.device = torch.device(device)
+        self.input_size = int(net.input_shapes[0][2]) if net.input_shapes else 300
+        self._prior_cache = {}
+        self._plan = self._compile() if self.device.type == "cuda" else None
+
+    # ------------------------------------------------------------------ compile
+    def _compile(self):
+        dev = self.device
+        plan = []
+        layers = self.net.layers
+        consumed = set()
+        shapes = {self.net.inputs[0]: 3}  # channels per blob
+        for i, l in enumerate(layers):
+            if i in consumed:
+                continue
+            if l.type == "Convolution":
+                w, b = self.ref.conv_weights(l.name)
+                cout, cin_g, k, _ = w.shape
+                group = int(l.p("convolution_param", "group", 1))
+                stride = int(l.p("convolution_param", "stride", 1))
+                pad = int(l.p("convolution_param", "pad", 0))
+                relu = False
+                if i + 1 < len(layers) and layers[i + 1].type == "ReLU" and layers[i + 1].bottoms[0] == l.tops[0]:
+                    relu = True
+                    consumed.add(i + 1)
+                bias = (b.detach().float() if b is not None else torch.zeros(cout)).to(dev)
+                cin = cin_g * group
+                if group > 1:
+                    if not (group == cin == cout and k == 3 and pad == 1):
+                        raise NotImplementedError(f"{l.name}: only depthwise 3x3 pad 1 grouped conv is supported")
+                    w9 = w.detach().float().permute(2, 3, 0, 1).reshape(9, cout).contiguous()
+                    plan.append(("dw", l, dict(w=w9.to(dev, torch.bfloat16), b=bias, stride=stride, relu=relu)))
+                elif k == 1 and stride == 1 and pad == 0 and cin % 32 == 0:
+                    wt = w.detach().float().reshape(cout, cin).to(dev, torch.bfloat16).contiguous()
+                    plan.append(("pw", l, dict(w=wt, b=bias, relu=relu)))
+                else:
+                    K = k * k * cin
+                    Kp = _round_up(K, 32)
+                    wt = torch.zeros(cout, Kp)
+                    wt[:, :K] = w.detach().float().permute(0, 2, 3, 1).reshape(cout, K)
+                    plan.append(("conv", l, dict(w=wt.to(dev, torch.bfloat16).contiguous(), b=bias, k=k,
+                                                 stride=stride, pad=pad, cin=cin, Kp=Kp, relu=relu)))
+                shapes[l.tops[0]] = cout
+            elif l.type == "ReLU":
+                plan.append(("relu", l, {}))
+            elif l.type == "Permute":
+                order = [int(o) for o in l.plist("permute_param", "order")]
+                if order != [0, 2, 3, 1]:
+                    raise NotImplementedError(f"{l.name}: permute {order}")
+                plan.append(("nhwc", l, {}))
+            elif l.type in ("Flatten", "Concat", "PriorBox", "Reshape", "Softmax", "DetectionOutput"):
+                plan.append((l.type.lower(), l, {}))
+            else:
+                raise NotImplementedError(f"Caffe layer type {l.type!r} ({l.name})")
+        return plan
+
+    # ------------------------------------------------------------------ helpers
+    def _priors(self, layer, fh, fw):
+        key = (layer.name, fh, fw)
+        if key not in self._prior_cache:
+            pb = prior_boxes(layer, fh, fw, self.input_size, self.input_size)
+            self._prior_cache[key] = torch.from_numpy(pb).to(self.device)
+        return self._prior_cache[key]
+
+    # ------------------------------------------------------------------ run
+    @torch.no_grad()
+    def forward_blob(self, blob: torch.Tensor) -> dict:
+        """blob: NHWC bf16 [N, S, S, 4] (from ops.vision.blob_from_frames). Returns named tensors;
+        'detection_out' -> (dets [N, keep, 7], counts [N])."""
+        if self._plan is None:
+            x = blob[..., :3].permute(0, 3, 1, 2).float()
+            t = self.ref(x)
+            d = t["detection_out"]
+            keep = 100
+            out = torch.zeros(len(d), keep, 7)
+            cnt = torch.zeros(len(d), dtype=torch.int32)
+            for n, dd in enumerate(d):
+                kk = min(len(dd), keep)
+                out[n, :kk] = dd[:kk]
+                cnt[n] = kk
+            t["detection_out"] = (out, cnt)
+            return t
+        N = blob.shape[0]
+        t = {self.net.inputs[0]: blob}
+        layout = {self.net.inputs[0]: "nhwc"}
+        hw = {self.net.inputs[0]: (blob.shape[1], blob.shape[2])}
+        chans = {self.net.inputs[0]: 3}
+        for kind, l, p in self._plan:
+            src = l.bottoms[0] if l.bottoms else None
+            x = t.get(src)
+            top = l.tops[0] if l.tops else None
+            if kind == "dw":
+                y = V.dwconv3x3(x, p["w"], p["b"], p["stride"], p["relu"])
+                t[top], layout[top], hw[top], chans[top] = y, "nhwc", (y.shape[1], y.shape[2]), y.shape[3]
+            elif kind == "pw":
+                H, W = hw[src]
+                M = N * H * W
+                y = V.gemm_bias_act(x.reshape(M, x.shape[-1]), p["w"], p["b"], p["relu"])
+                t[top], layout[top], hw[top], chans[top] = y.view(N, H, W, -1), "nhwc", (H, W), y.shape[1]
+            elif kind == "conv":
+                H, W = hw[src]
+                k, s, pd = p["k"], p["stride"], p["pad"]
+                Ho, Wo = (H + 2 * pd - k) // s + 1, (W + 2 * pd - k) // s + 1
+                cols = V.im2col_nhwc(x, p["cin"], k, s, pd, p["Kp"])
+                y = V.gemm_bias_act(cols, p["w"], p["b"], p["relu"]).view(N, Ho, Wo, -1)
+                t[top], layout[top], hw[top], chans[top] = y, "nhwc", (Ho, Wo), y.shape[3]
+            elif kind == "relu":
+                t[top] = torch.relu(x)
+                layout[top], hw[top], chans[top] = layout[src], hw.get(src), chans.get(src)
+            elif kind == "nhwc":  # Permute(0,2,3,1) of a logical NCHW tensor stored NHWC: free
+                t[top], layout[top] = x, "plain"
+            elif kind == "flatten":
+                t[top], layout[top] = x.reshape(N, -1) if x.dim() > 2 or layout[src] != "priors" else x, (
+                    "priors" if layout.get(src) == "priors" else "plain")
+            elif kind == "priorbox":
+                fh, fw = hw[src]
+                t[top], layout[top] = self._priors(l, fh, fw), "priors"
+            elif kind == "concat":
+                ax = int(l.p("concat_param", "axis", 1))
+                parts = [t[b] for b in l.bottoms]
+                if layout[l.bottoms[0]] == "priors":
+                    t[top], layout[top] = torch.cat(parts, 1), "priors"
+                else:
+                    t[top], layout[top] = torch.cat([q.reshape(N, -1) for q in parts], ax), "plain"
+            elif kind in ("reshape", "softmax"):
+                # folded into DetectionOutput: the detect kernel takes raw logits
+                t[top], layout[top] = x, "logits"
+            elif kind == "detectionoutput":
+                loc, conf, pri = (t[b] for b in l.bottoms)
+                dp = lambda k, d: l.p("detection_output_param", k, d)  # noqa: E731
+                P = pri.shape[-1] // 4
+                nc = int(dp("num_classes", 21))
+                dets, cnt = V.ssd_detect(conf.reshape(N, P * nc), loc.reshape(N, P * 4), pri[0, 0], pri[0, 1],
+                                         num_classes=nc, background=int(dp("background_label_id", 0)),
+                                         conf_thresh=float(dp("confidence_threshold", 0.01)),
+                                         nms_thresh=float(l.sub("detection_output_param", "nms_param",
+                                                                "nms_threshold", 0.45)),
+                                         top_k=int(l.sub("detection_output_param", "nms_param", "top_k", 100)),
+                                         keep_top_k=int(dp("keep_top_k", 100)))
+                t[top] = (dets, cnt)
+        return t
+
+    def detect(self, frames_u8: torch.Tensor):
+        """frames [N, H, W, 3] uint8 BGR (already at the annotation size) -> (dets, counts)."""
+        blob = V.blob_from_frames(frames_u8, self.input_size)
+        return self.forward_blob(blob)["detection_out"]
+
+
+def smoke_detect(dev):
+    """Tiny end-to-end detection on the GPU (used by __graft_entry__.smoke)."""
+    ex = SSDExecutor(device=dev)
+    frames = torch.randint(0, 255, (2, 225, 400, 3), dtype=torch.uint8, device=dev)
+    dets, cnt = ex.detect(frames)
+    V.annotate(frames, dets, cnt, "127.0.0.1:5554")
+    torch.cuda.synchronize()
+    print(f"[smoke] mobilenet-ssd detect ok, dets/frame={cnt.tolist()}")

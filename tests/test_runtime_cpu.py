@@ -1,0 +1,136 @@
+"""C++ runtime (scheduler, reorder index, transport) and control protocol, on CPU."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from distributedvolunteercomputing_amd._native_loader import native
+from distributedvolunteercomputing_amd.control import protocol
+from distributedvolunteercomputing_amd.control.transport import FrameHub, FrameSender
+
+N = native()
+
+
+def test_round_robin_excludes_requester_and_never_drops():
+    s = N.ChunkScheduler(0, 0)
+    s.submit(1, "R")
+    assert not s.next().valid()  # empty pool: the chunk waits (reference drops it)
+    for w in ("R", "A", "B"):
+        s.add_worker(w, 0.0)
+    got = []
+    for c in range(2, 8):
+        s.submit(c, "R")
+    while True:
+        a = s.next()
+        if not a.valid():
+            break
+        got.append((a.chunk, a.worker))
+        assert a.worker != "R"
+    assert [c for c, _ in got] == list(range(1, 8))
+    ws = [w for _, w in got]
+    assert ws == ["A", "B"] * 3 + ["A"]  # strict alternation at chunk granularity
+
+
+def test_credits_and_completion():
+    s = N.ChunkScheduler(0, 1)
+    s.add_worker("A", 0.0)
+    s.submit(1, "R")
+    s.submit(2, "R")
+    a = s.next()
+    assert a.valid() and a.chunk == 1
+    assert not s.next().valid()  # A is at its credit limit
+    assert s.complete(1)
+    assert not s.complete(1)  # duplicate completion is ignored
+    assert s.next().chunk == 2
+
+
+def test_worker_loss_requeues_in_order():
+    s = N.ChunkScheduler(0, 4)
+    s.add_worker("A", 0.0)
+    s.add_worker("B", 0.0)
+    for c in range(1, 5):
+        s.submit(c, "R")
+    assigned = [s.next() for _ in range(4)]
+    a_chunks = sorted(x.chunk for x in assigned if x.worker == "A")
+    back = s.remove_worker("A")
+    assert sorted(back) == a_chunks
+    again = [s.next() for _ in range(len(a_chunks))]
+    assert [x.chunk for x in again] == a_chunks and all(x.worker == "B" for x in again)
+
+
+def test_lease_expiry():
+    s = N.ChunkScheduler(0, 2)
+    s.add_worker("A", 0.0)
+    s.add_worker("B", 0.0)
+    s.heartbeat("B", 5.0)
+    assert s.expire(6.0, 3.0) == ["A"]
+    assert s.workers() == ["B"]
+
+
+def test_least_loaded_policy():
+    s = N.ChunkScheduler(1, 0)
+    for w in ("A", "B", "C"):
+        s.add_worker(w, 0)
+    for c in range(6):
+        s.submit(c, "R")
+    ws = [s.next().worker for _ in range(6)]
+    assert sorted(ws) == ["A", "A", "B", "B", "C", "C"]
+
+
+def test_reorder_index():
+    r = N.ReorderIndex(1)
+    assert r.push(3) == []
+    assert r.push(2) == []
+    assert r.push(1) == [1, 2, 3]
+    assert r.push(2) == []  # late duplicate
+    assert r.push(5) == [] and r.stashed == 1
+    assert r.push(4) == [4, 5]
+
+
+def test_transport_roundtrip_ack_and_many_senders():
+    hub = FrameHub(0, REQ_REP=True, capacity=4)
+    senders = [FrameSender(f"tcp://127.0.0.1:{hub.port}") for _ in range(3)]
+    arrs = [np.random.randint(0, 255, (5, 7, 3), dtype=np.uint8) for _ in range(3)]
+
+    def send(i):
+        assert senders[i].send_image(f"m{i}", arrs[i], chunk=i)
+
+    th = [threading.Thread(target=send, args=(i,)) for i in range(3)]
+    for t in th:
+        t.start()
+    got = {}
+    for _ in range(3):
+        hdr, a, peer = hub.recv_frame(timeout=5)
+        got[hdr["chunk"]] = (hdr["msg"], a.copy())
+    for t in th:
+        t.join()
+    for i in range(3):
+        assert got[i][0] == f"m{i}" and np.array_equal(got[i][1], arrs[i])
+    big = np.random.rand(1000, 1000).astype(np.float32)
+    assert senders[0].send_image("big", big)
+    msg, a = hub.recv_image(timeout=5)
+    assert msg == "big" and a.dtype == np.float32 and np.array_equal(a, big)
+    assert hub.recv_image(timeout=0.05) == (None, None)
+    hub.close()
+
+
+def test_transport_backpressure_and_timeout():
+    hub = FrameHub(0, REQ_REP=True, capacity=1)
+    s = FrameSender(f"tcp://127.0.0.1:{hub.port}")
+    x = np.zeros(10, np.uint8)
+    assert s.send_image("a", x, timeout=2)
+    t0 = time.time()
+    assert not s.send_image("b", x, timeout=0.5)  # queue full: no ack -> bounded wait, not a hang
+    assert time.time() - t0 < 3
+    hub.close()
+
+
+def test_protocol_exact_verbs():
+    assert protocol.decode(b"join||1.2.3.4:5554") == ("join", "1.2.3.4:5554")
+    assert protocol.decode(b"joined||x") == (None, None)  # no substring matching
+    assert protocol.decode(b"end") == (None, None)
+    assert protocol.parse_reply(b"ok||5555") == (True, "5555")
+    assert protocol.parse_reply(b"ok") == (True, None)
+    with pytest.raises(ValueError):
+        protocol.encode("bogus", "x")

@@ -1,0 +1,103 @@
+"""End-to-end volunteer video job on CPU: coordinator + volunteers over the native TCP data
+plane and the UDP control verbs (reference server.py/worker.py flow)."""
+import time
+
+import numpy as np
+import pytest
+
+from distributedvolunteercomputing_amd.control.coordinator import coordinator
+from distributedvolunteercomputing_amd.control.peer import client
+from distributedvolunteercomputing_amd.io.video import decode_frame_index
+from distributedvolunteercomputing_amd.jobs.video import AnnotateOnlyEngine, PassthroughEngine
+
+
+@pytest.fixture
+def coord():
+    c = coordinator("127.0.0.1", 0, ephemeral_ports=True, lease_s=2.0)
+    yield c
+    c.exit_threads()
+
+
+def _client(coord, tmp_path, engine, chunk=100):
+    c = client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0, engine=engine,
+               out_dir=str(tmp_path), out_ext=".npy", chunk=chunk)
+    c.heartbeat_s = 0.2
+    return c
+
+
+def test_join_request_and_inorder_output(coord, tmp_path):
+    req = _client(coord, tmp_path, PassthroughEngine())
+    w1 = _client(coord, tmp_path, PassthroughEngine(delay_s=0.05))
+    w2 = _client(coord, tmp_path, PassthroughEngine())
+    try:
+        assert len(coord.sched.workers()) == 3
+        req.preresize = False
+        req.become_requester("synthetic:250:64x48")
+        t = req.wait_job(timeout=60)
+        assert t is not None and t > 0
+        out = np.load(req.path_out)
+        assert out.shape == (250, 48, 64, 3)  # tail chunk of 50 frames is NOT dropped
+        idx = [decode_frame_index(f) for f in out]
+        assert idx == list(range(250))  # in-order reassembly, first frame kept
+        # the requester itself never received work; both workers did
+        assert w1.metrics.counters.get("frames_processed", 0) + w2.metrics.counters.get("frames_processed", 0) == 250
+        assert req.metrics.counters.get("frames_processed", 0) == 0
+        assert coord.clients and req.my_ip in coord.clients  # back in the pool after EOF (stop verb)
+    finally:
+        for c in (req, w1, w2):
+            c.exit_threads()
+
+
+def test_annotated_output_is_400_wide(coord, tmp_path):
+    req = _client(coord, tmp_path, AnnotateOnlyEngine())
+    w = _client(coord, tmp_path, AnnotateOnlyEngine())
+    try:
+        req.become_requester("synthetic:30:640x360")
+        assert req.wait_job(timeout=60) is not None
+        out = np.load(req.path_out)
+        assert out.shape == (30, 225, 400, 3)
+        # green "person: 0" label pixels exist near the bottom-left
+        g = out[0, 180:225, 0:120]
+        assert ((g[..., 1] == 255) & (g[..., 0] == 0) & (g[..., 2] == 0)).sum() > 10
+    finally:
+        req.exit_threads()
+        w.exit_threads()
+
+
+def test_dead_worker_chunks_are_redispatched(coord, tmp_path):
+    req = _client(coord, tmp_path, PassthroughEngine())
+    good = _client(coord, tmp_path, PassthroughEngine(delay_s=0.02))
+    bad = _client(coord, tmp_path, PassthroughEngine())
+    try:
+        # "crash" the bad worker: it swallows work and stops heartbeating, never says `end`
+        bad.continue_procesing = False
+        bad.continue_receiving = False
+        time.sleep(0.3)
+        req.preresize = False
+        req.become_requester("synthetic:400:32x24")
+        t = req.wait_job(timeout=90)
+        assert t is not None, "job must complete despite a dead worker"
+        out = np.load(req.path_out)
+        assert [decode_frame_index(f) for f in out] == list(range(400))
+        assert coord.metrics.counters.get("leaves_lease", 0) >= 1
+    finally:
+        for c in (req, good, bad):
+            c.exit_threads()
+
+
+def test_status_and_idempotent_join(coord, tmp_path):
+    w = _client(coord, tmp_path, PassthroughEngine())
+    try:
+        from distributedvolunteercomputing_amd.control import protocol
+
+        cc = protocol.ControlClient("127.0.0.1", coord.control_port)
+        p1 = cc.call("join", w.my_ip)
+        p2 = cc.call("join", w.my_ip)
+        assert p1 == p2 == w.connect_to_port
+        assert coord.sched.workers().count(w.my_ip) == 1
+        import json
+
+        st = json.loads(cc.call("status", w.my_ip))
+        assert w.my_ip in st["workers"]
+    finally:
+        w.exit_threads()

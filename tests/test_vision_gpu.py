@@ -1,0 +1,143 @@
+"""MobileNet-SSD HIP kernels vs PyTorch fp32 references (gfx950)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributedvolunteercomputing_amd.models.caffe import detection_output
+from distributedvolunteercomputing_amd.models.mobilenet_ssd import SSDExecutor
+from distributedvolunteercomputing_amd.ops import vision as V
+from distributedvolunteercomputing_amd.ops._lib import reference_ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,N,K,relu", [(1000, 64, 32, True), (36100, 512, 512, True), (777, 126, 512, False),
+                                        (100, 1024, 1024, True), (5, 12, 64, False), (4096, 200, 96, True)])
+def test_gemm_bias_act(gpu, M, N, K, relu):
+    torch.manual_seed(0)
+    X = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=gpu) / K**0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=gpu)
+    Y = V.gemm_bias_act(X, W, b, relu)
+    R = X.float() @ W.float().t() + b
+    if relu:
+        R = F.relu(R)
+    assert torch.allclose(Y.float(), R, atol=3e-2, rtol=2e-2), (Y.float() - R).abs().max()
+
+
+def test_gemm_asymmetric_identity(gpu):
+    """A = I, asymmetric B: catches a transposed C write (cdna guide §3)."""
+    K = 64
+    X = torch.eye(K, device=gpu).to(torch.bfloat16)
+    W = torch.arange(K * 48, device=gpu, dtype=torch.float32).view(48, K).remainder(17).to(torch.bfloat16)
+    Y = V.gemm_bias_act(X, W, None, False)
+    assert torch.equal(Y.float(), W.float().t())
+
+
+@pytest.mark.parametrize("C,stride,H", [(32, 1, 150), (64, 2, 150), (512, 1, 19), (1024, 1, 10), (256, 2, 38)])
+def test_dwconv(gpu, C, stride, H):
+    torch.manual_seed(1)
+    x = torch.randn(3, H, H, C, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(9, C, device=gpu) * 0.3).to(torch.bfloat16)
+    b = torch.randn(C, device=gpu)
+    y = V.dwconv3x3(x, w, b, stride, True)
+    with reference_ops():
+        r = V.dwconv3x3(x, w, b, stride, True)
+    assert torch.allclose(y.float(), r.float(), atol=3e-2, rtol=2e-2)
+
+
+def test_im2col(gpu):
+    x = torch.randn(2, 10, 10, 256, device=gpu).to(torch.bfloat16)
+    a = V.im2col_nhwc(x, 256, 3, 2, 1, 2304)
+    with reference_ops():
+        r = V.im2col_nhwc(x, 256, 3, 2, 1, 2304)
+    assert torch.equal(a, r)
+    x4 = torch.randn(2, 30, 30, 4, device=gpu).to(torch.bfloat16)
+    a = V.im2col_nhwc(x4, 3, 3, 2, 1, 32)
+    with reference_ops():
+        r = V.im2col_nhwc(x4, 3, 3, 2, 1, 32)
+    assert torch.equal(a, r)
+
+
+def test_preprocess(gpu):
+    torch.manual_seed(2)
+    f = torch.randint(0, 256, (3, 720, 1280, 3), dtype=torch.uint8, device=gpu)
+    a = V.resize_width(f, 400)
+    with reference_ops():
+        r = V.resize_width(f.cpu(), 400)
+    assert a.shape == (3, 225, 400, 3)
+    assert (a.cpu().int() - r.int()).abs().max() <= 1
+    b = V.blob_from_frames(a, 300)
+    with reference_ops():
+        rb = V.blob_from_frames(a.cpu(), 300)
+    assert (b.cpu().float() - rb.float()).abs().max() <= 0.0079 + 1e-3
+
+
+def _rand_det_inputs(dev, N=4, P=1917, C=21, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    conf = torch.randn(N, P * C, generator=g) * 2.5
+    conf.view(N, P, C)[:, :, 15] += 2.0  # plenty of "person" candidates
+    loc = torch.randn(N, P * 4, generator=g) * 0.5
+    cx, cy = torch.rand(P, generator=g), torch.rand(P, generator=g)
+    s = torch.rand(P, generator=g) * 0.3 + 0.05
+    pri = torch.stack([cx - s, cy - s, cx + s, cy + s], -1).reshape(-1)
+    var = torch.tensor([0.1, 0.1, 0.2, 0.2]).repeat(P)
+    bf = lambda t: t.to(torch.bfloat16)  # noqa: E731
+    return bf(conf).to(dev), bf(loc).to(dev), pri.to(dev), var.to(dev)
+
+
+def test_ssd_detect_matches_reference(gpu):
+    conf, loc, pri, var = _rand_det_inputs(gpu)
+    dets, cnt = V.ssd_detect(conf, loc, pri, var)
+    N, P = conf.shape[0], pri.numel() // 4
+    prob = torch.softmax(conf.float().cpu().view(N, P, 21), -1).view(N, -1)
+    ref = detection_output(loc.float().cpu(), prob, pri.cpu(), var.cpu())
+    for n in range(N):
+        k = int(cnt[n])
+        r = ref[n]
+        assert k == min(len(r), 100), (k, len(r))
+        got = dets[n, :k].cpu()
+        # same set of (label, box) with matching scores
+        gs = sorted(got.tolist(), key=lambda d: (-d[2], d[1]))
+        rs = sorted(r[:k].tolist(), key=lambda d: (-d[2], d[1]))
+        for a, b in zip(gs, rs):
+            assert a[1] == b[1]
+            assert abs(a[2] - b[2]) < 2e-3
+            assert max(abs(x - y) for x, y in zip(a[3:], b[3:])) < 2e-3
+
+
+def test_annotate(gpu):
+    f = torch.zeros(2, 225, 400, 3, dtype=torch.uint8, device=gpu)
+    dets = torch.zeros(2, 100, 7, device=gpu)
+    dets[0, 0] = torch.tensor([0, 15, 0.9, 0.1, 0.2, 0.5, 0.6])
+    dets[0, 1] = torch.tensor([0, 7, 0.9, 0.1, 0.2, 0.5, 0.6])  # not a person
+    cnt = torch.tensor([2, 0], dtype=torch.int32, device=gpu)
+    fc = f.cpu().clone()
+    counts = V.annotate(f, dets, cnt, "10.0.0.1:5554")
+    with reference_ops():
+        rc = V.annotate(fc, dets.cpu(), cnt.cpu(), "10.0.0.1:5554")
+    assert counts.tolist() == [1, 0] == rc.tolist()
+    assert torch.equal(f.cpu(), fc)
+    assert (f[0, :, :, 0] == 255).sum() > 100  # blue box pixels
+
+
+def test_executor_matches_caffe_reference(gpu):
+    ex = SSDExecutor(device=gpu)
+    torch.manual_seed(4)
+    frames = torch.randint(0, 256, (2, 225, 400, 3), dtype=torch.uint8, device=gpu)
+    blob = V.blob_from_frames(frames, 300)
+    out = ex.forward_blob(blob)
+    x = blob[..., :3].permute(0, 3, 1, 2).float().cpu()
+    ref = ex.ref(x)
+    for name in ["conv0", "conv1", "conv5", "conv11", "conv13", "conv14_2", "conv17_2"]:
+        a = out[name].float().cpu().permute(0, 3, 1, 2)
+        r = ref[name]
+        rel = (a - r).norm() / (r.norm() + 1e-6)
+        assert rel < 0.05, (name, float(rel))
+    for name in ["mbox_loc", "mbox_conf"]:
+        a = out[name].float().cpu()
+        r = ref[name]
+        rel = (a - r).norm() / (r.norm() + 1e-6)
+        assert rel < 0.05, (name, float(rel))
+    dets, cnt = out["detection_out"]
+    assert dets.shape == (2, 100, 7) and cnt.shape == (2,)
