@@ -172,7 +172,7 @@ class SSDExecutor:
         key = (layer.name, fh, fw)
         if key not in self._prior_cache:
             pb = prior_boxes(layer, fh, fw, self.input_size, self.input_size)
-            self._prior_cache[key] = torch.from_numpy(pb).to(self.device)
+            self._prior_cache[key] = torch.from_numpy(pb).unsqueeze(0).to(self.device)  # [1, 2, P*4]
         return self._prior_cache[key]
 
     # ------------------------------------------------------------------ run
@@ -232,7 +232,7 @@ class SSDExecutor:
                 ax = int(l.p("concat_param", "axis", 1))
                 parts = [t[b] for b in l.bottoms]
                 if layout[l.bottoms[0]] == "priors":
-                    t[top], layout[top] = torch.cat(parts, 1), "priors"
+                    t[top], layout[top] = torch.cat(parts, ax), "priors"
                 else:
                     t[top], layout[top] = torch.cat([q.reshape(N, -1) for q in parts], ax), "plain"
             elif kind in ("reshape", "softmax"):

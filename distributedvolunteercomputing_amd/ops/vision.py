@@ -51,6 +51,7 @@ def _bilinear_weights(src: int, dst: int) -> torch.Tensor:
 
 def _separable(frames_u8: torch.Tensor, wy: torch.Tensor, wx: torch.Tensor) -> torch.Tensor:
     f = frames_u8.float()
+    wy, wx = wy.to(f.device), wx.to(f.device)
     y = torch.einsum("yh,nhwc->nywc", wy, f)
     y = torch.einsum("xw,nywc->nyxc", wx, y)
     return y
@@ -88,7 +89,7 @@ def blob_from_frames(frames: torch.Tensor, size: int = 300, scale: float = 0.007
     if use_native(frames):
         return native().blob_bilinear(frames.contiguous(), size, scale, mean)
     r = resize_bilinear_u8(frames, size, size).float()
-    out = torch.zeros(frames.shape[0], size, size, 4)
+    out = torch.zeros(frames.shape[0], size, size, 4, device=frames.device)
     out[..., :3] = (r - mean) * scale
     return out.to(torch.bfloat16)
 
@@ -126,7 +127,7 @@ def im2col_nhwc(x, C, k, stride, pad, Kp):
     cols = F.unfold(xc, k, padding=pad, stride=stride)  # [N, C*k*k, L] with (c, ky, kx) order
     L = cols.shape[-1]
     cols = cols.view(N, C, k * k, L).permute(0, 3, 2, 1).reshape(N * L, k * k * C)  # (ky,kx,c)
-    out = torch.zeros(N * L, Kp)
+    out = torch.zeros(N * L, Kp, device=x.device)
     out[:, : k * k * C] = cols
     return out.to(x.dtype)
 
