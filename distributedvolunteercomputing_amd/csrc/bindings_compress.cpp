@@ -1,4 +1,112 @@
-// Torch bindings for the gradient-compression kernels (compress.hip).
+// Torch bindings for the gradient-compression kernels (kernels/compress.hip).
 #include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
 
-void vcx_register_compress(pybind11::module& m) { (void)m; }
+#include "kernels/vcx_api_compress.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHK(x)                                                  \
+  TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor");       \
+  TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+
+// state: int32[8] on device, prepared by the caller: {0, k, 0, 0, ...}; hist: int32[4096] zeros
+void topk_ef(at::Tensor g, at::Tensor e, int64_t k, at::Tensor state, at::Tensor hist, at::Tensor idx_out,
+             at::Tensor val_out) {
+  CHK(g);
+  CHK(e);
+  CHK(state);
+  CHK(hist);
+  CHK(idx_out);
+  CHK(val_out);
+  TORCH_CHECK(e.scalar_type() == at::kFloat && g.numel() == e.numel());
+  TORCH_CHECK(g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat);
+  TORCH_CHECK(state.scalar_type() == at::kInt && state.numel() >= 8 && hist.scalar_type() == at::kInt &&
+              hist.numel() >= 4096);
+  TORCH_CHECK(idx_out.scalar_type() == at::kInt && idx_out.numel() >= k && val_out.numel() >= k);
+  TORCH_CHECK(val_out.scalar_type() == at::kBFloat16 || val_out.scalar_type() == at::kFloat);
+  TORCH_CHECK(k > 0 && k <= g.numel() && g.numel() < INT32_MAX);
+  vcx_topk_ef(g.data_ptr(), g.scalar_type() == at::kBFloat16, e.data_ptr<float>(), g.numel(), (int)k,
+              state.data_ptr<int>(), (uint32_t*)hist.data_ptr<int>(), idx_out.data_ptr<int32_t>(), val_out.data_ptr(),
+              val_out.scalar_type() == at::kBFloat16, cur_stream());
+}
+
+void scatter_add(at::Tensor idx, at::Tensor val, double scale, at::Tensor dense) {
+  CHK(idx);
+  CHK(val);
+  CHK(dense);
+  TORCH_CHECK(idx.scalar_type() == at::kInt && dense.scalar_type() == at::kFloat && idx.numel() == val.numel());
+  TORCH_CHECK(val.scalar_type() == at::kBFloat16 || val.scalar_type() == at::kFloat);
+  // bounds are enforced on the host: an out-of-range index would be an OOB atomic
+  if (idx.numel()) {
+    auto mx = idx.max().item<int>();
+    auto mn = idx.min().item<int>();
+    TORCH_CHECK(mn >= 0 && mx < dense.numel(), "scatter_add: index out of range");
+  }
+  vcx_scatter_add(idx.data_ptr<int32_t>(), val.data_ptr(), val.scalar_type() == at::kBFloat16, idx.numel(),
+                  (float)scale, dense.data_ptr<float>(), cur_stream());
+}
+
+void check_desc(const at::Tensor& d, int64_t nmat) {
+  CHK(d);
+  TORCH_CHECK(d.scalar_type() == at::kByte && d.numel() == nmat * vcx_psgd_desc_size(), "bad descriptor table");
+}
+
+void psgd_mq(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::Tensor Q, at::Tensor P, int64_t rank) {
+  check_desc(desc, nmat);
+  CHK(M);
+  CHK(Q);
+  CHK(P);
+  vcx_psgd_mq(desc.data_ptr(), (int)nmat, (int)nblocks, M.data_ptr<float>(), Q.data_ptr<float>(), P.data_ptr<float>(),
+              (int)rank, cur_stream());
+}
+
+void psgd_mtp(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::Tensor P, at::Tensor Q, int64_t rank) {
+  check_desc(desc, nmat);
+  CHK(M);
+  CHK(Q);
+  CHK(P);
+  vcx_psgd_mtp(desc.data_ptr(), (int)nmat, (int)nblocks, M.data_ptr<float>(), P.data_ptr<float>(),
+               Q.data_ptr<float>(), (int)rank, cur_stream());
+}
+
+void psgd_orth(at::Tensor desc, int64_t nmat, at::Tensor P, int64_t rank) {
+  check_desc(desc, nmat);
+  CHK(P);
+  vcx_psgd_orth(desc.data_ptr(), (int)nmat, P.data_ptr<float>(), (int)rank, cur_stream());
+}
+
+void psgd_reconstruct(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::Tensor P, at::Tensor Q,
+                      at::Tensor out, int64_t rank) {
+  check_desc(desc, nmat);
+  CHK(M);
+  CHK(P);
+  CHK(Q);
+  CHK(out);
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.numel() == M.numel());
+  vcx_psgd_reconstruct(desc.data_ptr(), (int)nmat, (int)nblocks, M.data_ptr<float>(), P.data_ptr<float>(),
+                       Q.data_ptr<float>(), out.data_ptr(), (int)rank, cur_stream());
+}
+
+void ef_accum(at::Tensor g, at::Tensor e) {
+  CHK(g);
+  CHK(e);
+  TORCH_CHECK(g.scalar_type() == at::kBFloat16 && e.scalar_type() == at::kFloat && g.numel() == e.numel() &&
+              g.numel() % 8 == 0);
+  vcx_ef_accum(g.data_ptr(), e.data_ptr<float>(), g.numel(), cur_stream());
+}
+
+}  // namespace
+
+void vcx_register_compress(pybind11::module& m) {
+  m.def("topk_ef", &topk_ef);
+  m.def("scatter_add", &scatter_add);
+  m.def("psgd_mq", &psgd_mq);
+  m.def("psgd_mtp", &psgd_mtp);
+  m.def("psgd_orth", &psgd_orth);
+  m.def("psgd_reconstruct", &psgd_reconstruct);
+  m.def("ef_accum", &ef_accum);
+  m.def("psgd_desc_size", &vcx_psgd_desc_size);
+}

@@ -1,0 +1,351 @@
+// Gradient / pseudo-gradient compression kernels (gfx950): exact top-k with error feedback
+// and PowerSGD rank-r with error feedback. No reference analog (BASELINE.json
+// configs 3 and 5).
+//
+// Top-k: the k-th largest |g + e| is found EXACTLY by a 3-pass radix select on the IEEE bit
+// pattern of |x| (monotonic for non-negative floats): 12 + 12 + 7 bits, each pass a per-block
+// LDS histogram merged with one global atomic per bin, then a 1-block scan that narrows the
+// prefix. All state stays on the device (no host sync; graph-capturable). Selection then
+// compacts the winners with a per-wave ballot prefix + one atomic per wave.
+//
+// PowerSGD (Vogels et al. 2019): M <- g + e; P = M Q; allreduce(P); P = orth(P);
+// Q = M^T P; allreduce(Q); out = P Q^T; e = M - out. For rank r <= 8 the two products are
+// HBM-bound (2r FLOP per 4-B element), so they are single-pass streaming kernels with the
+// small Q/P operands served from L2; all matrices of a model are processed by ONE launch per
+// stage through a device-side descriptor table (grouped kernels).
+#include "vcx_common.h"
+
+namespace vcx {
+
+// =====================================================================================
+// top-k
+// =====================================================================================
+// state layout (int32): [0] prefix bits, [1] remaining k, [2] selected count, [3] threshold bits,
+//                       [4] n_greater (elements strictly above threshold)
+constexpr int TK_BINS = 4096;
+
+__device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
+
+// acc = g + e (written to e, fp32), histogram pass 0 of |acc| (bits 30..19 -> 12 bits)
+template <typename GT>
+__global__ void __launch_bounds__(256) topk_accum_hist_kernel(const GT* __restrict__ g, float* __restrict__ e,
+                                                               int64_t n, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[TK_BINS];
+  for (int i = threadIdx.x; i < TK_BINS; i += 256) h[i] = 0;
+  __syncthreads();
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float a = (float)g[i] + e[i];
+    e[i] = a;
+    atomicAdd(&h[absbits(a) >> 19], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < TK_BINS; i += 256)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// histogram of the next bit field for elements whose higher bits equal the current prefix
+__global__ void __launch_bounds__(256) topk_hist_kernel(const float* __restrict__ x, int64_t n,
+                                                         const int* __restrict__ st, int shift_hi, int shift,
+                                                         int nbits, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[TK_BINS];
+  const int nb = 1 << nbits;
+  for (int i = threadIdx.x; i < nb; i += 256) h[i] = 0;
+  __syncthreads();
+  const uint32_t prefix = (uint32_t)st[0];
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint32_t b = absbits(x[i]);
+    if ((b >> shift_hi) == prefix) atomicAdd(&h[(b >> shift) & (nb - 1)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += 256)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// one block: walk the histogram from the top bin down until the cumulative count reaches
+// the remaining k; extend the prefix by that bin; update remaining k; zero the histogram.
+__global__ void __launch_bounds__(256) topk_scan_kernel(uint32_t* __restrict__ hist, int nbits, int* __restrict__ st,
+                                                         int last) {
+  __shared__ uint32_t h[TK_BINS];
+  const int nb = 1 << nbits;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    h[i] = hist[i];
+    hist[i] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int rem = st[1];
+    uint32_t cum = 0;
+    int bin = 0;
+    for (int b = nb - 1; b >= 0; --b) {
+      if (cum + h[b] >= (uint32_t)rem) {
+        bin = b;
+        break;
+      }
+      cum += h[b];
+    }
+    st[0] = (int)(((uint32_t)st[0] << nbits) | (uint32_t)bin);
+    st[1] = rem - (int)cum;  // how many elements equal to the final prefix we still need
+    if (last) {
+      st[3] = st[0];  // full 31-bit pattern of the k-th largest magnitude
+      st[2] = 0;
+    }
+  }
+}
+
+// compact: |x| > thr always selected; |x| == thr selected while the tie budget lasts.
+// Selected entries are removed from the error buffer (error feedback keeps the rest).
+template <typename VT>
+__global__ void __launch_bounds__(256) topk_select_kernel(float* __restrict__ x, int64_t n, int* __restrict__ st,
+                                                           int k, int32_t* __restrict__ idx_out,
+                                                           VT* __restrict__ val_out) {
+  const uint32_t thr = (uint32_t)st[3];
+  int* ties = st + 1;
+  int* count = st + 2;
+  const int lane = threadIdx.x & 63;
+  for (int64_t base = blockIdx.x * 256ll; base < n; base += (int64_t)gridDim.x * 256) {
+    const int64_t i = base + threadIdx.x;
+    bool sel = false;
+    float v = 0.f;
+    if (i < n) {
+      v = x[i];
+      const uint32_t b = absbits(v);
+      if (b > thr) sel = true;
+      else if (b == thr && b != 0u) sel = atomicSub(ties, 1) > 0;
+    }
+    const unsigned long long mask = __ballot(sel);
+    const int wcount = __popcll(mask);
+    int wbase = 0;
+    if (lane == 0 && wcount) wbase = atomicAdd(count, wcount);
+    wbase = __shfl(wbase, 0, 64);
+    if (sel) {
+      const int pos = wbase + __popcll(mask & ((1ull << lane) - 1ull));
+      if (pos < k) {
+        idx_out[pos] = (int32_t)i;
+        val_out[pos] = (VT)v;
+        x[i] = 0.f;
+      }
+    }
+  }
+}
+
+// dense[idx[j]] += scale * val[j]  (fp32 accumulation of gathered sparse contributions)
+template <typename VT>
+__global__ void __launch_bounds__(256) scatter_add_kernel(const int32_t* __restrict__ idx, const VT* __restrict__ val,
+                                                           int64_t m, float scale, float* __restrict__ dense) {
+  for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < m; j += (int64_t)gridDim.x * 256)
+    atomicAdd(&dense[idx[j]], scale * (float)val[j]);
+}
+
+// =====================================================================================
+// PowerSGD (grouped over matrices)
+// =====================================================================================
+struct MatDesc {
+  int64_t off;   // element offset of M in the flat fp32 buffer
+  int64_t poff;  // element offset of P [rows, R]
+  int64_t qoff;  // element offset of Q [cols, R]
+  int rows, cols;
+  int blk0;      // first block of this matrix in the current launch's block numbering
+  int pad;
+};
+
+__device__ __forceinline__ int find_mat(const MatDesc* __restrict__ d, int nmat, int b, int stage) {
+  // blk0 for stage s is stored in descriptor table s (caller passes the table for the stage)
+  int lo = 0, hi = nmat - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].blk0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// P[row, :] = M[row, :] . Q   — 4 rows per block (one per wave)
+template <int R>
+__global__ void __launch_bounds__(256) psgd_mq_kernel(const MatDesc* __restrict__ d, int nmat,
+                                                       const float* __restrict__ M, const float* __restrict__ Q,
+                                                       float* __restrict__ P) {
+  const int mi = find_mat(d, nmat, blockIdx.x, 0);
+  const MatDesc md = d[mi];
+  const int row = (blockIdx.x - md.blk0) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= md.rows) return;
+  const float* mr = M + md.off + (int64_t)row * md.cols;
+  const float* q = Q + md.qoff;
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+  for (int c = lane; c < md.cols; c += 64) {
+    const float mv = mr[c];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = fmaf(mv, q[(int64_t)c * R + r], acc[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const float s = wave_sum(acc[r]);
+    if (lane == 0) P[md.poff + (int64_t)row * R + r] = s;
+  }
+}
+
+// Q[c, :] += sum over a 64-row slab of M[row, c] * P[row, :]   (Q zeroed beforehand)
+// block = (matrix, row slab of 64, column chunk of 256)
+template <int R>
+__global__ void __launch_bounds__(256) psgd_mtp_kernel(const MatDesc* __restrict__ d, int nmat,
+                                                        const float* __restrict__ M, const float* __restrict__ P,
+                                                        float* __restrict__ Q) {
+  const int mi = find_mat(d, nmat, blockIdx.x, 1);
+  const MatDesc md = d[mi];
+  const int local = blockIdx.x - md.blk0;
+  const int nck = (md.cols + 255) / 256;
+  const int slab = local / nck, ck = local % nck;
+  const int c = ck * 256 + threadIdx.x;
+  const int r0 = slab * 64, r1 = min(r0 + 64, md.rows);
+  __shared__ float sp[64][R];
+  for (int i = threadIdx.x; i < 64 * R; i += 256) {
+    const int rr = r0 + i / R;
+    sp[i / R][i % R] = rr < md.rows ? P[md.poff + (int64_t)rr * R + (i % R)] : 0.f;
+  }
+  __syncthreads();
+  if (c >= md.cols) return;
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+  const float* mb = M + md.off + c;
+  for (int row = r0; row < r1; ++row) {
+    const float mv = mb[(int64_t)row * md.cols];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = fmaf(mv, sp[row - r0][r], acc[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) atomicAdd(&Q[md.qoff + (int64_t)c * R + r], acc[r]);
+}
+
+// modified Gram-Schmidt on the R columns of each P (one block per matrix)
+template <int R>
+__global__ void __launch_bounds__(256) psgd_orth_kernel(const MatDesc* __restrict__ d, float* __restrict__ P) {
+  __shared__ float scratch[4];
+  const MatDesc md = d[blockIdx.x];
+  float* p = P + md.poff;
+  for (int i = 0; i < R; ++i) {
+    for (int j = 0; j < i; ++j) {
+      float s = 0.f;
+      for (int row = threadIdx.x; row < md.rows; row += 256) s = fmaf(p[(int64_t)row * R + i], p[(int64_t)row * R + j], s);
+      s = block_sum<256>(s, scratch);
+      for (int row = threadIdx.x; row < md.rows; row += 256) p[(int64_t)row * R + i] -= s * p[(int64_t)row * R + j];
+      __syncthreads();
+    }
+    float s = 0.f;
+    for (int row = threadIdx.x; row < md.rows; row += 256) {
+      const float v = p[(int64_t)row * R + i];
+      s = fmaf(v, v, s);
+    }
+    s = block_sum<256>(s, scratch);
+    const float inv = 1.f / (sqrtf(s) + 1e-8f);
+    for (int row = threadIdx.x; row < md.rows; row += 256) p[(int64_t)row * R + i] *= inv;
+    __syncthreads();
+  }
+}
+
+// out = P Q^T (bf16, into the flat output buffer at md.off), e = M - P Q^T (in place on M)
+template <int R>
+__global__ void __launch_bounds__(256) psgd_reconstruct_kernel(const MatDesc* __restrict__ d, int nmat,
+                                                                float* __restrict__ M, const float* __restrict__ P,
+                                                                const float* __restrict__ Q, bf16* __restrict__ out) {
+  const int mi = find_mat(d, nmat, blockIdx.x, 2);
+  const MatDesc md = d[mi];
+  const int64_t e0 = (int64_t)(blockIdx.x - md.blk0) * 2048;
+  const int64_t total = (int64_t)md.rows * md.cols;
+  for (int64_t t = e0 + threadIdx.x; t < min(e0 + 2048, total); t += 256) {
+    const int row = (int)(t / md.cols), c = (int)(t % md.cols);
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v = fmaf(P[md.poff + (int64_t)row * R + r], Q[md.qoff + (int64_t)c * R + r], v);
+    const int64_t gi = md.off + t;
+    M[gi] -= v;
+    out[gi] = (bf16)v;
+  }
+}
+
+// e = e + g  (fp32 += bf16) over a flat range; used before PowerSGD
+__global__ void __launch_bounds__(256) ef_accum_kernel(const bf16* __restrict__ g, float* __restrict__ e, int64_t n8) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    bf16x8 gv = *(const bf16x8*)(g + i * 8);
+    f32x4 a = *(const f32x4*)(e + i * 8), b = *(const f32x4*)(e + i * 8 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a[j] += (float)gv[j];
+      b[j] += (float)gv[j + 4];
+    }
+    *(f32x4*)(e + i * 8) = a;
+    *(f32x4*)(e + i * 8 + 4) = b;
+  }
+}
+
+}  // namespace vcx
+
+// ====================================================================================== launchers
+using namespace vcx;
+
+void vcx_topk_ef(const void* g, int g_is_bf16, float* e, int64_t n, int k, int* st, uint32_t* hist,
+                 int32_t* idx_out, void* val_out, int val_is_bf16, hipStream_t s) {
+  const int grid = stream_grid(n, 256, 1024);
+  // st[0] = prefix 0, st[1] = k (set by the caller with a memset-free init kernel below)
+  if (g_is_bf16)
+    hipLaunchKernelGGL(topk_accum_hist_kernel<bf16>, dim3(grid), dim3(256), 0, s, (const bf16*)g, e, n, hist);
+  else
+    hipLaunchKernelGGL(topk_accum_hist_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)g, e, n, hist);
+  hipLaunchKernelGGL(topk_scan_kernel, dim3(1), dim3(256), 0, s, hist, 12, st, 0);
+  hipLaunchKernelGGL(topk_hist_kernel, dim3(grid), dim3(256), 0, s, e, n, st, 19, 7, 12, hist);
+  hipLaunchKernelGGL(topk_scan_kernel, dim3(1), dim3(256), 0, s, hist, 12, st, 0);
+  hipLaunchKernelGGL(topk_hist_kernel, dim3(grid), dim3(256), 0, s, e, n, st, 7, 0, 7, hist);
+  hipLaunchKernelGGL(topk_scan_kernel, dim3(1), dim3(256), 0, s, hist, 7, st, 1);
+  if (val_is_bf16)
+    hipLaunchKernelGGL(topk_select_kernel<bf16>, dim3(grid), dim3(256), 0, s, e, n, st, k, idx_out, (bf16*)val_out);
+  else
+    hipLaunchKernelGGL(topk_select_kernel<float>, dim3(grid), dim3(256), 0, s, e, n, st, k, idx_out, (float*)val_out);
+}
+
+void vcx_scatter_add(const int32_t* idx, const void* val, int val_is_bf16, int64_t m, float scale, float* dense,
+                     hipStream_t s) {
+  const int grid = stream_grid(m, 256, 1024);
+  if (val_is_bf16)
+    hipLaunchKernelGGL(scatter_add_kernel<bf16>, dim3(grid), dim3(256), 0, s, idx, (const bf16*)val, m, scale, dense);
+  else
+    hipLaunchKernelGGL(scatter_add_kernel<float>, dim3(grid), dim3(256), 0, s, idx, (const float*)val, m, scale,
+                       dense);
+}
+
+#define PSGD_R_DISPATCH(RV, ...)                              \
+  switch (RV) {                                               \
+    case 1: { constexpr int R = 1; __VA_ARGS__; } break;      \
+    case 2: { constexpr int R = 2; __VA_ARGS__; } break;      \
+    case 4: { constexpr int R = 4; __VA_ARGS__; } break;      \
+    default: { constexpr int R = 8; __VA_ARGS__; } break;     \
+  }
+
+void vcx_psgd_mq(const void* desc, int nmat, int nblocks, const float* M, const float* Q, float* P, int rank,
+                 hipStream_t s) {
+  PSGD_R_DISPATCH(rank, hipLaunchKernelGGL(psgd_mq_kernel<R>, dim3(nblocks), dim3(256), 0, s, (const MatDesc*)desc,
+                                           nmat, M, Q, P));
+}
+
+void vcx_psgd_mtp(const void* desc, int nmat, int nblocks, const float* M, const float* P, float* Q, int rank,
+                  hipStream_t s) {
+  PSGD_R_DISPATCH(rank, hipLaunchKernelGGL(psgd_mtp_kernel<R>, dim3(nblocks), dim3(256), 0, s, (const MatDesc*)desc,
+                                           nmat, M, P, Q));
+}
+
+void vcx_psgd_orth(const void* desc, int nmat, float* P, int rank, hipStream_t s) {
+  PSGD_R_DISPATCH(rank, hipLaunchKernelGGL(psgd_orth_kernel<R>, dim3(nmat), dim3(256), 0, s, (const MatDesc*)desc, P));
+}
+
+void vcx_psgd_reconstruct(const void* desc, int nmat, int nblocks, float* M, const float* P, const float* Q,
+                          void* out, int rank, hipStream_t s) {
+  PSGD_R_DISPATCH(rank, hipLaunchKernelGGL(psgd_reconstruct_kernel<R>, dim3(nblocks), dim3(256), 0, s,
+                                           (const MatDesc*)desc, nmat, M, P, Q, (bf16*)out));
+}
+
+void vcx_ef_accum(const void* g, float* e, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(ef_accum_kernel, dim3(stream_grid(n / 8, 256)), dim3(256), 0, s, (const bf16*)g, e, n / 8);
+}
+
+int vcx_psgd_desc_size() { return (int)sizeof(MatDesc); }

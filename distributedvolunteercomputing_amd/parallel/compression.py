@@ -1,0 +1,227 @@
+"""Communication compression with error feedback for averaging rounds / gradient steps.
+
+* ``TopKCompressor``   — exact global top-k of |g + e| (radix select on the GPU), sparse
+  all-gather of (index, value) pairs, scatter-add into a dense buffer. The unsent remainder
+  stays in the error-feedback buffer ``e`` (BASELINE.json config 3: "top-k sparsified
+  gradients + error feedback").
+* ``PowerSGDCompressor`` — rank-r PowerSGD (Vogels et al., 2019) with warm-started Q and
+  error feedback over every matrix of a ``FlatParams`` layout; vectors go uncompressed
+  (BASELINE.json config 5: "PowerSGD rank-4 compression").
+
+Both expose ``allreduce_mean(buf_bf16, group) -> averaged bf16 buffer`` so they plug into
+``LocalSGDTrainer`` (compressing the pseudo-gradient) and the sharded data-parallel trainer
+(compressing gradients). GPU tensors use the HIP kernels of ``compress.hip``; CPU tensors
+use the torch reference below (same math).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..ops._lib import native, use_native
+from .flat_params import FlatParams
+
+
+class TopKCompressor:
+    def __init__(self, numel: int, ratio: float, device, value_dtype=torch.bfloat16):
+        self.n = int(numel)
+        self.k = max(1, int(math.ceil(numel * ratio)))
+        self.device = torch.device(device)
+        self.e = torch.zeros(self.n, dtype=torch.float32, device=self.device)
+        self.idx = torch.zeros(self.k, dtype=torch.int32, device=self.device)
+        self.val = torch.zeros(self.k, dtype=value_dtype, device=self.device)
+        self.state = torch.zeros(8, dtype=torch.int32, device=self.device)
+        self.state_init = torch.tensor([0, self.k, 0, 0, 0, 0, 0, 0], dtype=torch.int32, device=self.device)
+        self.hist = torch.zeros(4096, dtype=torch.int32, device=self.device)
+        self.bytes_sent = 0
+
+    @property
+    def ratio(self) -> float:
+        return self.k / self.n
+
+    def compress(self, g: torch.Tensor):
+        """(idx int32 [k], val [k]) of the k largest |g + e|; e keeps the rest."""
+        if use_native(g):
+            self.state.copy_(self.state_init)
+            self.val.zero_()
+            self.idx.zero_()
+            native().topk_ef(g.contiguous(), self.e, self.k, self.state, self.hist, self.idx, self.val)
+            return self.idx, self.val
+        self.e.add_(g.float())
+        _, i = torch.topk(self.e.abs(), self.k, sorted=False)
+        self.idx.copy_(i.to(torch.int32))
+        self.val.copy_(self.e[i].to(self.val.dtype))
+        self.e[i] = 0.0
+        return self.idx, self.val
+
+    def allreduce_mean(self, g: torch.Tensor, group) -> torch.Tensor:
+        idx, val = self.compress(g)
+        P = 1 if group is None else group.size
+        if P > 1:
+            all_idx = torch.empty(P * self.k, dtype=idx.dtype, device=idx.device)
+            all_val = torch.empty(P * self.k, dtype=val.dtype, device=val.device)
+            group.all_gather_(all_idx, idx)
+            group.all_gather_(all_val, val)
+        else:
+            all_idx, all_val = idx, val
+        self.bytes_sent += self.k * (idx.element_size() + val.element_size())
+        dense = torch.zeros(self.n, dtype=torch.float32, device=g.device)
+        if use_native(dense):
+            native().scatter_add(all_idx, all_val, 1.0 / P, dense)
+        else:
+            dense.index_add_(0, all_idx.long(), all_val.float() / P)
+        return dense.to(torch.bfloat16)
+
+
+class PowerSGDCompressor:
+    DESC_BYTES = 40  # sizeof(MatDesc) in compress.hip
+
+    def __init__(self, flat: FlatParams, rank: int = 4, device=None, seed: int = 0, min_ratio: float = 2.0):
+        assert rank in (1, 2, 4, 8), "rank must be 1, 2, 4 or 8"
+        self.flat = flat
+        self.rank = rank
+        self.device = torch.device(device or flat.param.device)
+        self.mats = []  # (offset, rows, cols)
+        for s in flat.segments:
+            if len(s.shape) < 2:
+                continue
+            rows = s.shape[0]
+            cols = s.numel // rows
+            if rows * cols < min_ratio * rank * (rows + cols):
+                continue  # not worth compressing: sent dense
+            self.mats.append((s.offset, rows, cols))
+        self.dense_ranges = self._dense_ranges()
+        R = rank
+        self.p_off, self.q_off = [], []
+        pt = qt = 0
+        for off, r, c in self.mats:
+            self.p_off.append(pt)
+            self.q_off.append(qt)
+            pt += r * R
+            qt += c * R
+        self.P = torch.zeros(max(pt, 1), dtype=torch.float32, device=self.device)
+        g = torch.Generator().manual_seed(seed)  # identical warm-start Q on every peer
+        self.Q = torch.randn(max(qt, 1), generator=g).to(self.device)
+        self.e = torch.zeros(flat.numel, dtype=torch.float32, device=self.device)
+        self.out = torch.zeros(flat.numel, dtype=torch.bfloat16, device=self.device)
+        self.bytes_sent = 0
+        if self.device.type == "cuda":
+            self._build_desc()
+
+    def _dense_ranges(self):
+        covered = np.zeros(0)
+        ranges = []
+        mats = sorted(self.mats)
+        pos = 0
+        for off, r, c in mats:
+            if off > pos:
+                ranges.append((pos, off))
+            pos = off + r * c
+        if pos < self.flat.numel:
+            ranges.append((pos, self.flat.numel))
+        del covered
+        return ranges
+
+    def _build_desc(self):
+        def table(blocks_of):
+            recs = np.zeros(len(self.mats), dtype=np.dtype([("off", "<i8"), ("poff", "<i8"), ("qoff", "<i8"),
+                                                            ("rows", "<i4"), ("cols", "<i4"), ("blk0", "<i4"),
+                                                            ("pad", "<i4")]))
+            b = 0
+            for i, (off, r, c) in enumerate(self.mats):
+                recs[i] = (off, self.p_off[i], self.q_off[i], r, c, b, 0)
+                b += blocks_of(r, c)
+            return torch.from_numpy(recs.view(np.uint8).copy()).to(self.device), b
+
+        self.d_mq, self.nb_mq = table(lambda r, c: (r + 3) // 4)
+        self.d_mtp, self.nb_mtp = table(lambda r, c: ((r + 63) // 64) * ((c + 255) // 256))
+        self.d_rec, self.nb_rec = table(lambda r, c: (r * c + 2047) // 2048)
+        self.d_orth = self.d_mq
+
+    @property
+    def compression_ratio(self) -> float:
+        dense = sum(b - a for a, b in self.dense_ranges)
+        sent = self.P.numel() + self.Q.numel() + dense
+        return self.flat.numel / max(1, sent)
+
+    def allreduce_mean(self, g: torch.Tensor, group) -> torch.Tensor:
+        Pn = 1 if group is None else group.size
+        nm = len(self.mats)
+        R = self.rank
+        native_path = use_native(g)
+        if native_path:
+            C = native()
+            C.ef_accum(g, self.e)
+        else:
+            self.e.add_(g.float())
+        if nm:
+            if native_path:
+                C.psgd_mq(self.d_mq, nm, self.nb_mq, self.e, self.Q, self.P, R)
+            else:
+                self._ref_mq()
+            if Pn > 1:
+                group.allreduce_(self.P)
+                self.P.div_(Pn)
+            if native_path:
+                C.psgd_orth(self.d_orth, nm, self.P, R)
+            else:
+                self._ref_orth()
+            self.Q.zero_()
+            if native_path:
+                C.psgd_mtp(self.d_mtp, nm, self.nb_mtp, self.e, self.P, self.Q, R)
+            else:
+                self._ref_mtp()
+            if Pn > 1:
+                group.allreduce_(self.Q)
+                self.Q.div_(Pn)
+            if native_path:
+                C.psgd_reconstruct(self.d_rec, nm, self.nb_rec, self.e, self.P, self.Q, self.out, R)
+            else:
+                self._ref_reconstruct()
+        # vectors / small matrices: plain average, no error feedback needed
+        for a, b in self.dense_ranges:
+            seg = self.e[a:b]
+            if Pn > 1:
+                group.allreduce_(seg)
+                seg.div_(Pn)
+            self.out[a:b].copy_(seg.to(torch.bfloat16))
+            seg.zero_()
+        self.bytes_sent += 4 * (self.P.numel() + self.Q.numel() + sum(b - a for a, b in self.dense_ranges))
+        return self.out
+
+    # ------------------------------------------------------------------ torch reference
+    def _views(self, i):
+        off, r, c = self.mats[i]
+        R = self.rank
+        M = self.e[off : off + r * c].view(r, c)
+        P = self.P[self.p_off[i] : self.p_off[i] + r * R].view(r, R)
+        Q = self.Q[self.q_off[i] : self.q_off[i] + c * R].view(c, R)
+        return M, P, Q
+
+    def _ref_mq(self):
+        for i in range(len(self.mats)):
+            M, P, Q = self._views(i)
+            P.copy_(M @ Q)
+
+    def _ref_orth(self):
+        for i in range(len(self.mats)):
+            _, P, _ = self._views(i)
+            for a in range(self.rank):
+                for b in range(a):
+                    P[:, a] -= (P[:, a] @ P[:, b]) * P[:, b]
+                P[:, a] /= P[:, a].norm() + 1e-8
+
+    def _ref_mtp(self):
+        for i in range(len(self.mats)):
+            M, P, Q = self._views(i)
+            Q.copy_(M.t() @ P)
+
+    def _ref_reconstruct(self):
+        for i in range(len(self.mats)):
+            off, r, c = self.mats[i]
+            M, P, Q = self._views(i)
+            approx = P @ Q.t()
+            M.sub_(approx)
+            self.out[off : off + r * c].copy_(approx.reshape(-1).to(torch.bfloat16))

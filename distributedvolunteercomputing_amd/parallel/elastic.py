@@ -43,6 +43,8 @@ class ElasticMembership:
         self.poll_s = poll_s
         self.gen = -1
         self.members: list[int] = []
+        self.prev_members: list[int] = []
+        self.newcomers: list[int] = []
         self.group: PeerGroup | None = None
         self.round = 0
         self.joins_seen = 0
@@ -186,6 +188,12 @@ class ElasticMembership:
             self.group.shutdown()
         self.gen = g
         self.members = list(members)
+        pk = f"{_P}gen/{g - 1}/members"
+        if g > 0 and self.store.check([pk]):
+            self.prev_members = [int(x) for x in _s(self.store.get(pk)).split(",") if x]
+        else:
+            self.prev_members = list(members)
+        self.newcomers = [m for m in members if m not in self.prev_members]
         self.round = 0
         js = f"{_P}gen/{g}/joins"
         self.joins_seen = int(_s(self.store.get(js))) if self.store.check([js]) else self._njoin()

@@ -15,6 +15,9 @@ from dataclasses import dataclass
 import torch
 
 ALIGN = 64
+# total length is padded to a multiple of ALIGN * lcm(1..8) so that the flat space splits into
+# equal, 128-B-aligned shards for ANY peer count 1..8 (elastic re-sharding never re-pads)
+SHARD_PAD = ALIGN * 840
 
 
 def _round_up(n, a=ALIGN):
@@ -31,7 +34,7 @@ class Segment:
 
 
 class FlatParams:
-    def __init__(self, module: torch.nn.Module, dtype=torch.bfloat16, device=None, pad_to: int = ALIGN):
+    def __init__(self, module: torch.nn.Module, dtype=torch.bfloat16, device=None, pad_to: int = SHARD_PAD):
         params = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
         seen = {}
         uniq = []
@@ -79,8 +82,12 @@ class FlatParams:
         return {s.name: flat[s.offset : s.offset + s.numel].view(s.shape) for s in self.segments}
 
     def shard_bounds(self, rank: int, world: int, align: int = ALIGN):
-        """Contiguous [lo, hi) slice of the flat space owned by `rank` (ZeRO-style)."""
-        per = _round_up((self.numel + world - 1) // world, align)
+        """Contiguous [lo, hi) slice of the flat space owned by `rank` (ZeRO-style). For world
+        sizes dividing 840 all shards have the same, aligned length."""
+        if (self.numel // align) % world == 0:
+            per = self.numel // world
+        else:
+            per = _round_up((self.numel + world - 1) // world, align)
         lo = min(rank * per, self.numel)
         hi = min(lo + per, self.numel)
         return lo, hi

@@ -109,32 +109,49 @@ class LocalSGDTrainer:
         if self.membership is not None:
             self.group, changed, newcomers = self.membership.sync_round()
             if changed and newcomers:
-                self._admit_newcomers()
+                self._admit_newcomers(newcomers)
+        self._average(newcomers)
+        self.sync_count += 1
+        self.last_sync_ms = (time.perf_counter() - t0) * 1e3
+
+    def _average(self, newcomers=()):
         g = self.group
         if g is not None and g.size > 1:
             ops.lsgd_delta(self.master, self.anchor, self.delta)
+            contributors = g.size - len(newcomers)  # newcomers hold delta == 0
             if self.compressor is not None:
                 avg = self.compressor.allreduce_mean(self.delta, g)
-                scale = 1.0
+                scale = g.size / contributors
             else:
                 allreduce_sum_(self.delta, g, self.cfg.algo)
-                avg, scale = self.delta, 1.0 / g.size
+                avg, scale = self.delta, 1.0 / contributors
             c = self.cfg
             ops.lsgd_apply(avg, self.anchor, self.master, self.flat.param, self.outer_mom, outer_lr=c.outer_lr,
                            mu=c.outer_momentum, nesterov=c.nesterov, avg_scale=scale)
         else:
             self.anchor.copy_(self.master)
-        self.sync_count += 1
-        self.last_sync_ms = (time.perf_counter() - t0) * 1e3
 
-    def _admit_newcomers(self):
-        """New generation contains peers without the current model: rank 0 broadcasts it."""
+    def _admit_newcomers(self, newcomers):
+        """The new generation contains peers without the model: the first continuing member
+        broadcasts the anchor (identical on all continuing members); newcomers adopt it as
+        their weights. Continuing members keep their un-averaged local progress."""
         g = self.group
-        g.broadcast_(self.anchor, root=0)
-        self.master.copy_(self.anchor)
-        ops.f32_to_bf16(self.anchor, self.flat.param)
+        members = g.members
+        root = next(i for i, m in enumerate(members) if m not in newcomers)
+        g.broadcast_(self.anchor, root=root)
         if self.outer_mom is not None:
-            g.broadcast_(self.outer_mom, root=0)
+            g.broadcast_(self.outer_mom, root=root)
+        me = self.membership.pid if self.membership is not None else None
+        if me in newcomers:
+            self.master.copy_(self.anchor)
+            ops.f32_to_bf16(self.anchor, self.flat.param)
+
+    def join_running_job(self):
+        """Called by a peer that was just admitted (``membership.join()``): receive the model
+        and take part in the round that admitted it."""
+        nc = self.membership.newcomers
+        self._admit_newcomers(nc)
+        self._average(nc)
 
     # ------------------------------------------------------------------ state
     def state_tensors(self):

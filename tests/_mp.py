@@ -45,12 +45,12 @@ def run(fn, world: int, *args, timeout: float = 120.0, expect_exit=()):
     for p in procs:
         p.start()
     out, errs = {}, []
-    need = world - len(expect_exit)
+    need = set(range(world)) - set(expect_exit)
     import queue as _q
     import time
 
     t0 = time.time()
-    while len(out) + len(errs) < need and time.time() - t0 < timeout:
+    while not need.issubset(set(out) | {r for r, _ in errs}) and time.time() - t0 < timeout:
         try:
             r, st, res = q.get(timeout=1.0)
         except _q.Empty:
@@ -65,6 +65,6 @@ def run(fn, world: int, *args, timeout: float = 120.0, expect_exit=()):
             p.kill()
     if errs:
         raise AssertionError("worker failures:\n" + "\n".join(f"[rank {r}] {e}" for r, e in errs))
-    if len(out) < need:
+    if not need.issubset(out):
         raise AssertionError(f"timeout: only ranks {sorted(out)} finished")
     return out
