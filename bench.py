@@ -20,7 +20,11 @@ import os
 import sys
 import time
 
-import torch
+from distributedvolunteercomputing_amd.utils.tuning import enable_tuned_gemms
+
+TUNED_GEMMS = enable_tuned_gemms(int(os.environ.get("LOCAL_RANK", "0")))  # before torch's first GEMM
+
+import torch  # noqa: E402
 import torch.distributed as dist
 
 from distributedvolunteercomputing_amd.models.gpt2 import GPT2, GPT2Config
@@ -36,7 +40,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--model", default="gpt2")
-    ap.add_argument("--batch", type=int, default=32, help="per-peer micro-batch (sequences)")
+    ap.add_argument("--batch", type=int, default=64, help="per-peer micro-batch (sequences)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--H", type=int, default=4)
     ap.add_argument("--algo", default="rccl", choices=["rccl", "rs_ag", "butterfly", "ring"])
@@ -125,6 +129,7 @@ def main():
             "mfu_bf16_dense": round(flops / world / BF16_DENSE_PEAK, 4),
             "final_loss": round(loss, 4),
             "sync_ms": round(trainer.last_sync_ms, 3),
+            "tuned_gemms": TUNED_GEMMS,
         }
         line = json.dumps(rec)
         print(line, flush=True)

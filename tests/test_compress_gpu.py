@@ -84,8 +84,10 @@ def test_powersgd_error_feedback_converges(gpu):
     c = PowerSGDCompressor(flat, rank=4, device=gpu)
     g = (torch.randn(flat.numel, device=gpu) * 0.01).to(torch.bfloat16)
     total = torch.zeros(flat.numel, device=gpu)
-    T = 40
-    for _ in range(T):
+    rels = {}
+    for t in range(1, 81):
         total += c.allreduce_mean(g, None).float()
-    rel = (total / T - g.float()).norm() / g.float().norm()
-    assert rel < 0.25, float(rel)
+        if t in (10, 80):
+            rels[t] = float((total / t - g.float()).norm() / g.float().norm())
+    # e stays bounded, so the time-averaged transmitted gradient converges to g
+    assert rels[80] < 0.5 * rels[10], rels
