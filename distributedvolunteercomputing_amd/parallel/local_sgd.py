@@ -156,3 +156,30 @@ class LocalSGDTrainer:
     # ------------------------------------------------------------------ state
     def state_tensors(self):
         return {"master": self.master, "m": self.m, "v": self.v, "anchor": self.anchor, "ostate": self.ostate}
+
+    def checkpoint_slice(self):
+        """This peer's 1/P share of the (synchronised) state: call right after a sync round,
+        when master == anchor on every peer. Moments are per-peer; each peer contributes its
+        own slice of them."""
+        P = 1 if self.group is None else self.group.size
+        r = 0 if self.group is None else self.group.rank
+        lo, hi = self.flat.shard_bounds(r, P)
+        t = {"master": self.anchor[lo:hi], "m": self.m[lo:hi], "v": self.v[lo:hi]}
+        if self.outer_mom is not None:
+            t["outer_mom"] = self.outer_mom[lo:hi]
+        return lo, hi, t
+
+    def restore(self, reader):
+        reader.check_layout(self.flat)
+        n = self.flat.numel
+        dev = self.device
+        self.master.copy_(reader.read_range("master", 0, n).to(dev))
+        self.anchor.copy_(self.master)
+        self.m.copy_(reader.read_range("m", 0, n).to(dev))
+        self.v.copy_(reader.read_range("v", 0, n).to(dev))
+        if self.outer_mom is not None:
+            self.outer_mom.copy_(reader.read_range("outer_mom", 0, n).to(dev))
+        _, ost = reader.params()
+        self.ostate.copy_(ost.to(dev))
+        ops.f32_to_bf16(self.master, self.flat.param)
+        self.t = reader.step

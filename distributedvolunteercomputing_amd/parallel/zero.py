@@ -89,6 +89,28 @@ class ShardedDPTrainer:
         else:
             self.b_master = self.b_m = self.b_v = None
 
+    def checkpoint_slice(self):
+        lo, hi = self.prim
+        return lo, hi, {"master": self.master, "m": self.m, "v": self.v}
+
+    def restore(self, reader):
+        """Load a checkpoint written by any number of peers into the CURRENT layout."""
+        reader.check_layout(self.flat)
+        dev = self.device
+        param, ost = reader.params()
+        self.flat.param.copy_(param.to(dev))
+        self.ostate.copy_(ost.to(dev))
+        lo, hi = self.prim
+        self.master.copy_(reader.read_range("master", lo, hi).to(dev))
+        self.m.copy_(reader.read_range("m", lo, hi).to(dev))
+        self.v.copy_(reader.read_range("v", lo, hi).to(dev))
+        if self.back is not None:
+            a, b = self.back
+            self.b_master.copy_(reader.read_range("master", a, b).to(dev))
+            self.b_m.copy_(reader.read_range("m", a, b).to(dev))
+            self.b_v.copy_(reader.read_range("v", a, b).to(dev))
+        self.t = reader.step
+
     def state_bytes(self) -> int:
         n = self.master.numel() + (self.b_master.numel() if self.b_master is not None else 0)
         return 12 * n
