@@ -220,6 +220,35 @@ void xent_bwd(at::Tensor logits, at::Tensor tgt, at::Tensor lse, at::Tensor gsca
                dlogits.data_ptr(), R, (int)V, (int)Vp, cur_stream());
 }
 
+// ------------------------------------------------------------------ attention (head dim 64)
+std::vector<at::Tensor> attn_fwd(at::Tensor qkv, double scale) {
+  CHECK_IN(qkv, kBF);
+  TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.size(4) == 64, "attn_fwd: qkv must be [B, T, 3, H, 64]");
+  const int64_t B = qkv.size(0), T = qkv.size(1), H = qkv.size(3);
+  TORCH_CHECK(B * H * ((T + 127) / 128) < INT32_MAX && T > 0);
+  auto out = at::empty({B, T, H, 64}, qkv.options());
+  auto lse = at::empty({B, H, T}, qkv.options().dtype(kF));
+  vcx_attn_fwd_d64(qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T, (int)H, (float)scale,
+                   cur_stream());
+  return {out, lse};
+}
+
+at::Tensor attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse, double scale) {
+  CHECK_IN(qkv, kBF);
+  CHECK_IN(out, kBF);
+  CHECK_IN(dout, kBF);
+  CHECK_IN(lse, kF);
+  TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.size(4) == 64);
+  const int64_t B = qkv.size(0), T = qkv.size(1), H = qkv.size(3);
+  TORCH_CHECK(out.sizes() == at::IntArrayRef({B, T, H, 64}) && dout.sizes() == out.sizes());
+  TORCH_CHECK(lse.numel() == B * H * T);
+  auto dqkv = at::empty_like(qkv);
+  auto delta = at::empty({B, H, T}, lse.options());
+  vcx_attn_bwd_d64(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+                   dqkv.data_ptr(), (int)B, (int)T, (int)H, (float)scale, cur_stream());
+  return dqkv;
+}
+
 }  // namespace
 
 void vcx_register_vision(pybind11::module& m);
@@ -242,6 +271,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
   vcx_register_vision(m);
   vcx_register_compress(m);
 }

@@ -1,0 +1,471 @@
+// Causal flash attention for head dim 64 on gfx950 (GPT-2 family), bf16 in/out, fp32 softmax.
+//
+// Layouts (no permute/copy kernels around attention):
+//   qkv  : [B, T, 3, H, 64] bf16 — exactly the output of the fused QKV projection GEMM
+//   o    : [B, T, H, 64]    bf16 — exactly the input of the output projection GEMM
+//   lse  : [B, H, T]        fp32 — log2-domain row log-sum-exp saved for the backward
+//   dqkv : [B, T, 3, H, 64] bf16 — written directly by the backward kernels (no torch.cat)
+//
+// MFMA structure (v_mfma_f32_32x32x16_bf16, wave64): the score tile is computed TRANSPOSED,
+// S^T[key, query] = K . Q^T, so every lane owns one query column and holds 16 of its 32 key
+// scores in registers (its partner lane l^32 holds the other 16): the softmax row statistics
+// need one cross-lane exchange, and the bf16-converted P^T accumulator is directly the B
+// operand of O^T += V^T . P^T (cdna guide §3 "accumulator tile as the next MFMA's operand").
+// The A operand V^T is read from the row-major V tile in LDS with ds_read_b64_tr_b16, in the
+// permuted key order that the accumulator layout implies.
+//
+// LDS tiles: K rows padded to 72 bf16 (144 B: 16 consecutive rows of a ds_read_b128 land in
+// 16 distinct 4-bank slots); V rows padded to 96 bf16 (192 B: the 4 rows x 32 columns of a
+// half-wave ds_read_b64_tr_b16 hit disjoint banks). K/V tiles are double-buffered and staged
+// through registers (issue next tile's global loads before the MFMAs, write LDS after).
+#include "vcx_common.h"
+
+namespace vcx {
+
+typedef short sx8 __attribute__((ext_vector_type(8)));
+typedef short sx4 __attribute__((ext_vector_type(4)));
+
+constexpr int AD = 64;         // head dim
+constexpr int A_BQ = 128;      // queries per block (4 waves x 32)
+constexpr int A_BK = 64;       // keys per LDS tile
+constexpr int KLD = 72;        // K tile row stride (elements)
+constexpr int VLD = 96;        // V tile row stride (elements)
+constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ sx4 lds_tr_b64(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sx4*)(p));
+}
+
+__device__ __forceinline__ f32x16 mfma32(sx8 a, sx8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ short bf16_bits(float f) {
+  bf16 b = (bf16)f;
+  return *(short*)&b;
+}
+
+// A operand of X^T . P^T-style products: rows = d (lane&31 within the 32-wide d tile),
+// k = 16 keys of k-step `s`, in the accumulator's permuted order
+// (element j <-> key 16s + 8(j>>2) + 4h + (j&3)), read from a row-major [key][d] LDS tile.
+__device__ __forceinline__ sx8 vt_frag(const bf16* tile, int ld, int key0, int dtile, int s, int lane) {
+  const int h = lane >> 5, g = lane >> 4, lig = lane & 15;
+  const int cb = dtile * 32 + (g & 1) * 16 + 4 * (lig & 3);
+  const int rb = key0 + 16 * s + 4 * h + (lig >> 2);
+  sx4 lo = lds_tr_b64(tile + rb * ld + cb);
+  sx4 hi = lds_tr_b64(tile + (rb + 8) * ld + cb);
+  return sx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// ============================================================================ forward
+__global__ void __launch_bounds__(256) attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+                                                            float* __restrict__ lse, int B, int T, int H,
+                                                            float scale_log2) {
+  __shared__ __attribute__((aligned(16))) bf16 sK[2][A_BK * KLD];
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][A_BK * VLD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
+  const int nqt = (T + A_BQ - 1) / A_BQ;
+  // heaviest (last) query tiles first: better tail under the causal triangle
+  const int qt = nqt - 1 - (blockIdx.x % nqt);
+  const int bh = blockIdx.x / nqt;
+  const int b = bh / H, hh = bh % H;
+  const int64_t tok = 3ll * H * AD;  // token stride in qkv
+  const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
+  const bf16* Kg = base + H * AD;
+  const bf16* Vg = base + 2 * H * AD;
+  const int q0 = qt * A_BQ;
+  const int qw = q0 + w * 32;      // this wave's first query
+  const int q = qw + col;          // this lane's query
+  const int qc = min(q, T - 1);
+
+  // Q^T fragments (B operand): lane holds Q[q][16s + 8h + j]
+  sx8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *(const sx8*)(base + (int64_t)qc * tok + 16 * s + 8 * h2);
+
+  f32x16 o0 = {}, o1 = {};
+  float m = -INFINITY, l = 0.f;
+
+  const int kend = min(T, q0 + A_BQ);  // keys needed by this block (causal)
+  const int nkt = (kend + A_BK - 1) / A_BK;
+
+  // staging: a 64x64 tile = 512 16-B chunks -> 2 per thread for K and for V
+  sx8 rk[2], rv[2];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
+      const int key = min(kt * A_BK + r, T - 1);
+      rk[i] = *(const sx8*)(Kg + (int64_t)key * tok + c);
+      rv[i] = *(const sx8*)(Vg + (int64_t)key * tok + c);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
+      *(sx8*)(&sK[buf][r * KLD + c]) = rk[i];
+      *(sx8*)(&sV[buf][r * VLD + c]) = rv[i];
+    }
+  };
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload(kt + 1);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb = kt * A_BK + sub * 32;
+      if (kb > qw + 31) continue;  // wave-uniform: every query of this wave is before these keys
+      const bf16* kt_lds = &sK[cur][(sub * 32) * KLD];
+      f32x16 st = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        sx8 a = *(const sx8*)(kt_lds + col * KLD + 16 * s + 8 * h2);
+        st = mfma32(a, qf[s], st);
+      }
+      // scale (log2 domain) + causal mask; key of register r
+      float mx = -INFINITY;
+      const bool diag = kb + 31 > qw;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float x = st[r] * scale_log2;
+        if (diag) {
+          const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
+          if (key > q || key >= T) x = -INFINITY;
+        }
+        st[r] = x;
+        mx = fmaxf(mx, x);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float alpha = exp2f(m - mnew);  // m = -inf on the first tile -> 0
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(st[r] - mnew);
+        st[r] = p;
+        ps += p;
+      }
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * alpha + ps;
+      m = mnew;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        o0[r] *= alpha;
+        o1[r] *= alpha;
+      }
+      // P^T (bf16) as the B operand, k-steps s = 0, 1 (registers 8s .. 8s+7)
+      const bf16* vt_lds = &sV[cur][0];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sx8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = bf16_bits(st[8 * s + j]);
+        o0 = mfma32(vt_frag(vt_lds, VLD, sub * 32, 0, s, lane), pb, o0);
+        o1 = mfma32(vt_frag(vt_lds, VLD, sub * 32, 1, s, lane), pb, o1);
+      }
+    }
+    if (kt + 1 < nkt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  if (q < T) {
+    const float inv = 1.f / l;
+    bf16* orow = out + ((int64_t)b * T + q) * H * AD + hh * AD;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * h2;
+      bf16x4 v0 = {(bf16)(o0[4 * g] * inv), (bf16)(o0[4 * g + 1] * inv), (bf16)(o0[4 * g + 2] * inv),
+                   (bf16)(o0[4 * g + 3] * inv)};
+      bf16x4 v1 = {(bf16)(o1[4 * g] * inv), (bf16)(o1[4 * g + 1] * inv), (bf16)(o1[4 * g + 2] * inv),
+                   (bf16)(o1[4 * g + 3] * inv)};
+      *(bf16x4*)(orow + d) = v0;
+      *(bf16x4*)(orow + 32 + d) = v1;
+    }
+    if (h2 == 0) lse[((int64_t)b * H + hh) * T + q] = m + __log2f(l);
+  }
+}
+
+// ============================================================================ backward
+// delta[b, h, q] = sum_d dO[b, q, h, d] * O[b, q, h, d]   (8 lanes x 8 elements per row)
+__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const bf16* __restrict__ o, const bf16* __restrict__ dout,
+                                                              float* __restrict__ delta, int B, int T, int H) {
+  const int64_t rows = (int64_t)B * T * H;
+  const int64_t row = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  if (row >= rows) return;
+  const int sub = threadIdx.x & 7;
+  bf16x8 a = *(const bf16x8*)(o + row * AD + sub * 8);
+  bf16x8 g = *(const bf16x8*)(dout + row * AD + sub * 8);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s = fmaf((float)a[j], (float)g[j], s);
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if (sub == 0) {
+    const int hh = (int)(row % H);
+    const int64_t bt = row / H;
+    const int tq = (int)(bt % T), b = (int)(bt / T);
+    delta[((int64_t)b * H + hh) * T + tq] = s;
+  }
+}
+
+// dQ (query-parallel; same tiling as the forward): per 32-key sub-tile
+//   S^T = K Q^T, P^T = exp2(S^T c - lse), dP^T = V dO^T, dS^T = P^T (dP^T - delta),
+//   dQ^T += K^T dS^T  (A = K^T through ds_read_b64_tr_b16, B = dS^T from the accumulator)
+__global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                               int B, int T, int H, float scale, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) bf16 sK[2][A_BK * KLD];
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][A_BK * KLD];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
+  const int nqt = (T + A_BQ - 1) / A_BQ;
+  const int qt = nqt - 1 - (blockIdx.x % nqt);
+  const int bh = blockIdx.x / nqt;
+  const int b = bh / H, hh = bh % H;
+  const int64_t tok = 3ll * H * AD;
+  const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
+  const bf16* Kg = base + H * AD;
+  const bf16* Vg = base + 2 * H * AD;
+  const int64_t otok = (int64_t)H * AD;
+  const bf16* dOb = dout + (int64_t)b * T * otok + hh * AD;
+  const int q0 = qt * A_BQ, qw = q0 + w * 32, q = qw + col, qc = min(q, T - 1);
+  sx8 qf[4], df[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = *(const sx8*)(base + (int64_t)qc * tok + 16 * s + 8 * h2);
+    df[s] = *(const sx8*)(dOb + (int64_t)qc * otok + 16 * s + 8 * h2);
+  }
+  const float lq = lse[((int64_t)b * H + hh) * T + qc];
+  const float dq_delta = delta[((int64_t)b * H + hh) * T + qc];
+  f32x16 a0 = {}, a1 = {};
+  const int kend = min(T, q0 + A_BQ);
+  const int nkt = (kend + A_BK - 1) / A_BK;
+  sx8 rk[2], rv[2];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
+      const int key = min(kt * A_BK + r, T - 1);
+      rk[i] = *(const sx8*)(Kg + (int64_t)key * tok + c);
+      rv[i] = *(const sx8*)(Vg + (int64_t)key * tok + c);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
+      *(sx8*)(&sK[buf][r * KLD + c]) = rk[i];
+      *(sx8*)(&sV[buf][r * KLD + c]) = rv[i];
+    }
+  };
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload(kt + 1);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb = kt * A_BK + sub * 32;
+      if (kb > qw + 31) continue;
+      const bf16* kl = &sK[cur][(sub * 32) * KLD];
+      const bf16* vl = &sV[cur][(sub * 32) * KLD];
+      f32x16 st = {}, dp = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        st = mfma32(*(const sx8*)(kl + col * KLD + 16 * s + 8 * h2), qf[s], st);
+        dp = mfma32(*(const sx8*)(vl + col * KLD + 16 * s + 8 * h2), df[s], dp);
+      }
+      const bool diag = kb + 31 > qw;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = exp2f(st[r] * scale_log2 - lq);
+        if (diag) {
+          const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
+          if (key > q || key >= T) p = 0.f;
+        }
+        st[r] = p * (dp[r] - dq_delta);  // dS^T
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sx8 db;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) db[j] = bf16_bits(st[8 * s + j]);
+        a0 = mfma32(vt_frag(&sK[cur][0], KLD, sub * 32, 0, s, lane), db, a0);
+        a1 = mfma32(vt_frag(&sK[cur][0], KLD, sub * 32, 1, s, lane), db, a1);
+      }
+    }
+    if (kt + 1 < nkt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  if (q < T) {
+    bf16* row = dqkv + ((int64_t)b * T + q) * tok + hh * AD;  // slot 0 = dQ
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * h2;
+      bf16x4 v0 = {(bf16)(a0[4 * g] * scale), (bf16)(a0[4 * g + 1] * scale), (bf16)(a0[4 * g + 2] * scale),
+                   (bf16)(a0[4 * g + 3] * scale)};
+      bf16x4 v1 = {(bf16)(a1[4 * g] * scale), (bf16)(a1[4 * g + 1] * scale), (bf16)(a1[4 * g + 2] * scale),
+                   (bf16)(a1[4 * g + 3] * scale)};
+      *(bf16x4*)(row + d) = v0;
+      *(bf16x4*)(row + 32 + d) = v1;
+    }
+  }
+}
+
+// dK, dV (key-parallel, "key on the lane"): per 32-query sub-tile
+//   S = Q K^T, P = exp2(S c - lse[q]), dP = dO V^T, dS = P (dP - delta[q]),
+//   dV^T += dO^T P,  dK^T += Q^T dS   (A operands through ds_read_b64_tr_b16 on the Q/dO tiles,
+//   B operands = the bf16-converted accumulators; the keys stay on the lanes throughout)
+constexpr int B_BQ = 64;  // queries per LDS tile
+
+__global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __restrict__ qkv,
+                                                                 const bf16* __restrict__ dout,
+                                                                 const float* __restrict__ lse,
+                                                                 const float* __restrict__ delta,
+                                                                 bf16* __restrict__ dqkv, int B, int T, int H,
+                                                                 float scale, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) bf16 sQ[2][B_BQ * KLD];
+  __shared__ __attribute__((aligned(16))) bf16 sD[2][B_BQ * KLD];
+  __shared__ float sL[2][B_BQ], sDel[2][B_BQ];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
+  const int nkb = (T + 127) / 128;
+  const int kbi = blockIdx.x % nkb;  // light (late) key blocks last
+  const int bh = blockIdx.x / nkb;
+  const int b = bh / H, hh = bh % H;
+  const int64_t tok = 3ll * H * AD;
+  const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
+  const int64_t otok = (int64_t)H * AD;
+  const bf16* dOb = dout + (int64_t)b * T * otok + hh * AD;
+  const float* lrow = lse + ((int64_t)b * H + hh) * T;
+  const float* drow = delta + ((int64_t)b * H + hh) * T;
+  const int k0 = kbi * 128, kw = k0 + w * 32, key = kw + col, kc = min(key, T - 1);
+  sx8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = *(const sx8*)(base + H * AD + (int64_t)kc * tok + 16 * s + 8 * h2);
+    vf[s] = *(const sx8*)(base + 2 * H * AD + (int64_t)kc * tok + 16 * s + 8 * h2);
+  }
+  f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
+  const int qstart = k0 / B_BQ;  // first query tile that can see these keys
+  const int nqt = (T + B_BQ - 1) / B_BQ;
+  sx8 rq[2], rd[2];
+  float rl = 0.f, rdl = 0.f;
+  auto gload = [&](int qt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
+      const int qq = min(qt * B_BQ + r, T - 1);
+      rq[i] = *(const sx8*)(base + (int64_t)qq * tok + c);
+      rd[i] = *(const sx8*)(dOb + (int64_t)qq * otok + c);
+    }
+    if (tid < B_BQ) {
+      const int qq = min(qt * B_BQ + tid, T - 1);
+      rl = lrow[qq];
+      rdl = drow[qq];
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
+      *(sx8*)(&sQ[buf][r * KLD + c]) = rq[i];
+      *(sx8*)(&sD[buf][r * KLD + c]) = rd[i];
+    }
+    if (tid < B_BQ) {
+      sL[buf][tid] = rl;
+      sDel[buf][tid] = rdl;
+    }
+  };
+  gload(qstart);
+  sstore(0);
+  __syncthreads();
+  for (int qt = qstart; qt < nqt; ++qt) {
+    const int cur = (qt - qstart) & 1;
+    if (qt + 1 < nqt) gload(qt + 1);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int qb = qt * B_BQ + sub * 32;
+      if (qb + 31 < kw) continue;  // every query before this wave's first key
+      const bf16* ql = &sQ[cur][(sub * 32) * KLD];
+      const bf16* dl = &sD[cur][(sub * 32) * KLD];
+      f32x16 st = {}, dp = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        st = mfma32(*(const sx8*)(ql + col * KLD + 16 * s + 8 * h2), kf[s], st);
+        dp = mfma32(*(const sx8*)(dl + col * KLD + 16 * s + 8 * h2), vf[s], dp);
+      }
+      const bool diag = qb < kw + 31;
+      f32x16 pp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = (r & 3) + 8 * (r >> 2) + 4 * h2;  // row of S = query qb + qi
+        const int qq = qb + qi;
+        float p = exp2f(st[r] * scale_log2 - sL[cur][sub * 32 + qi]);
+        if ((diag && key > qq) || qq >= T || key >= T) p = 0.f;
+        pp[r] = p;
+        st[r] = p * (dp[r] - sDel[cur][sub * 32 + qi]);  // dS
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sx8 pb, sb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pb[j] = bf16_bits(pp[8 * s + j]);
+          sb[j] = bf16_bits(st[8 * s + j]);
+        }
+        dv0 = mfma32(vt_frag(&sD[cur][0], KLD, sub * 32, 0, s, lane), pb, dv0);
+        dv1 = mfma32(vt_frag(&sD[cur][0], KLD, sub * 32, 1, s, lane), pb, dv1);
+        dk0 = mfma32(vt_frag(&sQ[cur][0], KLD, sub * 32, 0, s, lane), sb, dk0);
+        dk1 = mfma32(vt_frag(&sQ[cur][0], KLD, sub * 32, 1, s, lane), sb, dk1);
+      }
+    }
+    if (qt + 1 < nqt) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  if (key < T) {
+    bf16* rowk = dqkv + ((int64_t)b * T + key) * tok + H * AD + hh * AD;      // slot 1 = dK
+    bf16* rowv = dqkv + ((int64_t)b * T + key) * tok + 2 * H * AD + hh * AD;  // slot 2 = dV
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * h2;
+      bf16x4 k0v = {(bf16)(dk0[4 * g] * scale), (bf16)(dk0[4 * g + 1] * scale), (bf16)(dk0[4 * g + 2] * scale),
+                    (bf16)(dk0[4 * g + 3] * scale)};
+      bf16x4 k1v = {(bf16)(dk1[4 * g] * scale), (bf16)(dk1[4 * g + 1] * scale), (bf16)(dk1[4 * g + 2] * scale),
+                    (bf16)(dk1[4 * g + 3] * scale)};
+      bf16x4 v0 = {(bf16)dv0[4 * g], (bf16)dv0[4 * g + 1], (bf16)dv0[4 * g + 2], (bf16)dv0[4 * g + 3]};
+      bf16x4 v1 = {(bf16)dv1[4 * g], (bf16)dv1[4 * g + 1], (bf16)dv1[4 * g + 2], (bf16)dv1[4 * g + 3]};
+      *(bf16x4*)(rowk + d) = k0v;
+      *(bf16x4*)(rowk + 32 + d) = k1v;
+      *(bf16x4*)(rowv + d) = v0;
+      *(bf16x4*)(rowv + 32 + d) = v1;
+    }
+  }
+}
+
+}  // namespace vcx
+
+using namespace vcx;
+
+void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
+                      int B, int T, int H, float scale, hipStream_t s) {
+  const int64_t rows = (int64_t)B * T * H;
+  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 31) / 32), dim3(256), 0, s, (const bf16*)out,
+                     (const bf16*)dout, delta, B, T, H);
+  const int nkb = (T + 127) / 128;
+  hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel, dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
+                     (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+  const int nqt = (T + A_BQ - 1) / A_BQ;
+  hipLaunchKernelGGL(attn_bwd_dq_d64_kernel, dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
+                     lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+}
+
+void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s) {
+  const int nqt = (T + A_BQ - 1) / A_BQ;
+  hipLaunchKernelGGL(attn_fwd_d64_kernel, dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B,
+                     T, H, scale * LOG2E);
+}

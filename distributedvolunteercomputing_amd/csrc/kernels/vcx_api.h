@@ -29,3 +29,8 @@ void vcx_xent_fwd(const void* logits, const int64_t* tgt, float* lse, float* los
                   hipStream_t s);
 void vcx_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, const float* gscale, void* dlogits,
                   int64_t R, int V, int Vp, hipStream_t s);
+
+// attention.hip (causal flash attention, head dim 64, packed qkv)
+void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s);
+void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
+                      int B, int T, int H, float scale, hipStream_t s);
