@@ -57,6 +57,15 @@ __device__ __forceinline__ sx8 vt_frag(const bf16* tile, int ld, int key0, int d
   return sx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// Bijective XCD-aware block remap (cdna guide §5 T1): hardware block b runs on XCD group b % 8;
+// give each group a CONTIGUOUS range of logical blocks so all query tiles of one (batch, head)
+// share that XCD's L2 copy of K/V.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  if (nwg < 8) return b;
+  const int q = nwg / 8, r = nwg % 8, x = b % 8, i = b / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 // ============================================================================ forward
 __global__ void __launch_bounds__(256) attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                             float* __restrict__ lse, int B, int T, int H,
@@ -66,8 +75,9 @@ __global__ void __launch_bounds__(256) attn_fwd_d64_kernel(const bf16* __restric
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
   const int nqt = (T + A_BQ - 1) / A_BQ;
   // heaviest (last) query tiles first: better tail under the causal triangle
-  const int qt = nqt - 1 - (blockIdx.x % nqt);
-  const int bh = blockIdx.x / nqt;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = nqt - 1 - (lb % nqt);
+  const int bh = lb / nqt;
   const int b = bh / H, hh = bh % H;
   const int64_t tok = 3ll * H * AD;  // token stride in qkv
   const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
@@ -115,57 +125,63 @@ __global__ void __launch_bounds__(256) attn_fwd_d64_kernel(const bf16* __restric
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nkt) gload(kt + 1);
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      const int kb = kt * A_BK + sub * 32;
-      if (kb > qw + 31) continue;  // wave-uniform: every query of this wave is before these keys
-      const bf16* kt_lds = &sK[cur][(sub * 32) * KLD];
-      f32x16 st = {};
+    const int kb = kt * A_BK;
+    if (kb <= qw + 31) {  // wave-uniform: otherwise every query of this wave precedes these keys
+      const bf16* kl = &sK[cur][0];
+      // two independent 32-key score tiles (interleaved MFMA chains)
+      f32x16 s0 = {}, s1 = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        sx8 a = *(const sx8*)(kt_lds + col * KLD + 16 * s + 8 * h2);
-        st = mfma32(a, qf[s], st);
+        s0 = mfma32(*(const sx8*)(kl + col * KLD + 16 * s + 8 * h2), qf[s], s0);
+        s1 = mfma32(*(const sx8*)(kl + (32 + col) * KLD + 16 * s + 8 * h2), qf[s], s1);
       }
-      // scale (log2 domain) + causal mask; key of register r
       float mx = -INFINITY;
-      const bool diag = kb + 31 > qw;
+      const bool diag = kb + 63 > qw;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float x = st[r] * scale_log2;
+        float x0 = s0[r] * scale_log2, x1 = s1[r] * scale_log2;
         if (diag) {
           const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
-          if (key > q || key >= T) x = -INFINITY;
+          if (key > q || key >= T) x0 = -INFINITY;
+          if (key + 32 > q || key + 32 >= T) x1 = -INFINITY;
         }
-        st[r] = x;
-        mx = fmaxf(mx, x);
+        s0[r] = x0;
+        s1[r] = x1;
+        mx = fmaxf(mx, fmaxf(x0, x1));
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
-      const float alpha = exp2f(m - mnew);  // m = -inf on the first tile -> 0
+      // deferred rescale (cdna guide T13): keep the running max unless it grew by > 8 (P <= 2^8,
+      // safe in fp32 accumulation and bf16 P), saving the O-wide multiply on most tiles
+      if (!__all(mx - m <= 8.f)) {
+        const float mnew = fmaxf(m, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);  // m = -inf on the first tile -> 0
+        l *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          o0[r] *= alpha;
+          o1[r] *= alpha;
+        }
+        m = mnew;
+      }
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(st[r] - mnew);
-        st[r] = p;
-        ps += p;
+        const float p0 = __builtin_amdgcn_exp2f(s0[r] - m), p1 = __builtin_amdgcn_exp2f(s1[r] - m);
+        s0[r] = p0;
+        s1[r] = p1;
+        ps += p0 + p1;
       }
-      ps += __shfl_xor(ps, 32, 64);
-      l = l * alpha + ps;
-      m = mnew;
+      l += ps + __shfl_xor(ps, 32, 64);
+      // P^T (bf16) as the B operand: 4 k-steps of 16 keys (registers 8s .. 8s+7 of s0 / s1)
+      const bf16* vl = &sV[cur][0];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        o0[r] *= alpha;
-        o1[r] *= alpha;
-      }
-      // P^T (bf16) as the B operand, k-steps s = 0, 1 (registers 8s .. 8s+7)
-      const bf16* vt_lds = &sV[cur][0];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < 4; ++s) {
+        const f32x16& sp = (s < 2) ? s0 : s1;
         sx8 pb;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = bf16_bits(st[8 * s + j]);
-        o0 = mfma32(vt_frag(vt_lds, VLD, sub * 32, 0, s, lane), pb, o0);
-        o1 = mfma32(vt_frag(vt_lds, VLD, sub * 32, 1, s, lane), pb, o1);
+        for (int j = 0; j < 8; ++j) pb[j] = bf16_bits(sp[8 * (s & 1) + j]);
+        o0 = mfma32(vt_frag(vl, VLD, (s >> 1) * 32, 0, s & 1, lane), pb, o0);
+        o1 = mfma32(vt_frag(vl, VLD, (s >> 1) * 32, 1, s & 1, lane), pb, o1);
       }
     }
     if (kt + 1 < nkt) sstore(cur ^ 1);
@@ -223,8 +239,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __rest
   __shared__ __attribute__((aligned(16))) bf16 sV[2][A_BK * KLD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
   const int nqt = (T + A_BQ - 1) / A_BQ;
-  const int qt = nqt - 1 - (blockIdx.x % nqt);
-  const int bh = blockIdx.x / nqt;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = nqt - 1 - (lb % nqt);
+  const int bh = lb / nqt;
   const int b = bh / H, hh = bh % H;
   const int64_t tok = 3ll * H * AD;
   const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
@@ -283,7 +300,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __rest
       const bool diag = kb + 31 > qw;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = exp2f(st[r] * scale_log2 - lq);
+        float p = __builtin_amdgcn_exp2f(st[r] * scale_log2 - lq);
         if (diag) {
           const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
           if (key > q || key >= T) p = 0.f;
@@ -331,11 +348,13 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __re
                                                                  float scale, float scale_log2) {
   __shared__ __attribute__((aligned(16))) bf16 sQ[2][B_BQ * KLD];
   __shared__ __attribute__((aligned(16))) bf16 sD[2][B_BQ * KLD];
-  __shared__ float sL[2][B_BQ], sDel[2][B_BQ];
+  __shared__ __attribute__((aligned(16))) float sL[2][B_BQ];
+  __shared__ __attribute__((aligned(16))) float sDel[2][B_BQ];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
   const int nkb = (T + 127) / 128;
-  const int kbi = blockIdx.x % nkb;  // light (late) key blocks last
-  const int bh = blockIdx.x / nkb;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int kbi = lb % nkb;  // light (late) key blocks last
+  const int bh = lb / nkb;
   const int b = bh / H, hh = bh % H;
   const int64_t tok = 3ll * H * AD;
   const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
@@ -402,13 +421,19 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __re
       const bool diag = qb < kw + 31;
       f32x16 pp;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = (r & 3) + 8 * (r >> 2) + 4 * h2;  // row of S = query qb + qi
-        const int qq = qb + qi;
-        float p = exp2f(st[r] * scale_log2 - sL[cur][sub * 32 + qi]);
-        if ((diag && key > qq) || qq >= T || key >= T) p = 0.f;
-        pp[r] = p;
-        st[r] = p * (dp[r] - sDel[cur][sub * 32 + qi]);  // dS
+      for (int g = 0; g < 4; ++g) {
+        // rows 8g + 4h + (0..3) of S are 4 consecutive queries: one 16-B LDS read each
+        const f32x4 lv = *(const f32x4*)(&sL[cur][sub * 32 + 8 * g + 4 * h2]);
+        const f32x4 dv = *(const f32x4*)(&sDel[cur][sub * 32 + 8 * g + 4 * h2]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * g + i;
+          const int qq = qb + 8 * g + 4 * h2 + i;
+          float p = __builtin_amdgcn_exp2f(st[r] * scale_log2 - lv[i]);
+          if ((diag && key > qq) || qq >= T || key >= T) p = 0.f;
+          pp[r] = p;
+          st[r] = p * (dp[r] - dv[i]);  // dS
+        }
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
