@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Reference-parity benchmark: the volunteer video-analytics job on MI355X.
+
+The reference's only performance output is "final frame time taken for the job = <sec>"
+(/root/reference/worker.py:219,234): a requester streams a video, the coordinator deals
+100-frame chunks round-robin to the other volunteers, each runs MobileNet-SSD person detection
+per frame, and the requester reassembles the annotated frames in order.
+
+Two measurements (synthetic 1280x720 BGR frames, random-init MobileNet-SSD weights — the
+caffemodel is not available here):
+  * engine : frames/s of one volunteer's chunk pipeline on the GPU (H2D, resize to 400 px,
+             blob, batched MobileNet-SSD forward, fused NMS, annotation kernel, D2H) for 100-frame chunks;
+  * job    : the full job through the real coordinator/client stack (UDP verbs, C++ TCP data
+             plane, scheduler, in-order sink) with 1 requester + N worker volunteers in this
+             process sharing the GPU; reports the reference's job wall time and frames/s.
+Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+
+def bench_engine(args, dev):
+    from distributedvolunteercomputing_amd.io.video import synthetic_frame
+    from distributedvolunteercomputing_amd.jobs.video import DetectorEngine
+
+    eng = DetectorEngine(device=dev)
+    frames = np.stack([synthetic_frame(i, args.width, args.height) for i in range(args.chunk)])
+    for _ in range(args.warmup):
+        eng.process(frames, "127.0.0.1:5554")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.iters):
+        out, counts = eng.process(frames, "127.0.0.1:5554")
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # device-only time of the batched network (no H2D/D2H, no host work)
+    small = torch.from_numpy(frames).to(dev)
+    from distributedvolunteercomputing_amd.ops import vision as V
+
+    small = V.resize_width(small, 400).contiguous()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.iters):
+        eng.exec.detect(small)
+    e1.record()
+    torch.cuda.synchronize()
+    net_ms = e0.elapsed_time(e1) / args.iters
+    gflop = 2.30 * args.chunk
+    return {"engine_frames_per_s": round(args.chunk * args.iters / dt, 1),
+            "engine_chunk_ms": round(dt / args.iters * 1e3, 2),
+            "net_only_chunk_ms": round(net_ms, 3),
+            "net_only_frames_per_s": round(args.chunk / net_ms * 1e3, 1),
+            "net_tflops": round(gflop / net_ms, 2), "out_shape": list(out.shape)}
+
+
+def bench_job(args, dev):
+    from distributedvolunteercomputing_amd.control.coordinator import coordinator
+    from distributedvolunteercomputing_amd.control.peer import client
+    from distributedvolunteercomputing_amd.jobs.video import DetectorEngine
+
+    coord = coordinator("127.0.0.1", 0, ephemeral_ports=True, credits=2)
+    eng = DetectorEngine(device=dev)  # one GPU: volunteers share one engine (serialised by a lock)
+    tmp = tempfile.mkdtemp(prefix="vcx_video_")
+    req = client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0, engine=eng, out_dir=tmp,
+                 out_ext=".npy")
+    workers = [client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0, engine=eng,
+                      out_dir=tmp, out_ext=".npy") for _ in range(args.workers)]
+    try:
+        req.become_requester(f"synthetic:{args.frames}:{args.width}x{args.height}")
+        t = req.wait_job(timeout=600)
+        n = int(np.load(req.path_out, mmap_mode="r").shape[0]) if t else 0
+    finally:
+        for c in [req] + workers:
+            c.exit_threads()
+        coord.exit_threads()
+    return {"job_time_s": round(t, 3) if t else None, "job_frames": n,
+            "job_frames_per_s": round(n / t, 1) if t else None, "workers": args.workers}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chunk", type=int, default=100)
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=1000)
+    ap.add_argument("--workers", type=int, default=2)
+    ap.add_argument("--no-job", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    rec = {"metric": "MobileNet-SSD video job (reference parity)", "unit": "frames/s", "dtype": "bf16",
+           "data": "synthetic 1280x720 frames, random-init weights", "chunk": a.chunk}
+    rec.update(bench_engine(a, dev))
+    if not a.no_job:
+        rec.update(bench_job(a, dev))
+    rec["value"] = rec.get("job_frames_per_s") or rec["engine_frames_per_s"]
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -18,6 +18,7 @@ Sinks (``open_sink(path, width, height, fps)``):
 """
 from __future__ import annotations
 
+import functools
 import os
 from pathlib import Path
 
@@ -59,12 +60,19 @@ class FrameSource:
             yield f
 
 
-def synthetic_frame(i: int, width: int, height: int, seed: int = 0) -> np.ndarray:
-    """Deterministic test frame: gradient background, two moving boxes, frame-index bar."""
+@functools.lru_cache(maxsize=8)
+def _gradient(width: int, height: int) -> np.ndarray:
     yy, xx = np.mgrid[0:height, 0:width]
     f = np.empty((height, width, 3), np.uint8)
     f[..., 0] = (xx * 255 // max(1, width - 1)).astype(np.uint8)
     f[..., 1] = (yy * 255 // max(1, height - 1)).astype(np.uint8)
+    f[..., 2] = 0
+    return f
+
+
+def synthetic_frame(i: int, width: int, height: int, seed: int = 0) -> np.ndarray:
+    """Deterministic test frame: gradient background, two moving boxes, frame-index bar."""
+    f = _gradient(width, height).copy()
     f[..., 2] = (seed * 37 + i * 3) & 255
     bw, bh = max(4, width // 8), max(6, height // 3)
     x0 = (i * 7) % max(1, width - bw)
