@@ -98,7 +98,7 @@ void axpy_bf16(at::Tensor src, at::Tensor acc, double scale) {
 
 // ------------------------------------------------------------------ norms / activations
 std::vector<at::Tensor> ln_fwd(at::Tensor a, c10::optional<at::Tensor> b, at::Tensor w, c10::optional<at::Tensor> bias,
-                               double eps, bool rms) {
+                               double eps, bool rms, c10::optional<at::Tensor> bb) {
   CHECK_IN(a, kBF);
   CHECK_IN(w, kBF);
   const int C = (int)a.size(-1);
@@ -114,18 +114,23 @@ std::vector<at::Tensor> ln_fwd(at::Tensor a, c10::optional<at::Tensor> b, at::Te
     CHECK_IN((*bias), kBF);
     TORCH_CHECK(bias->numel() == C);
   }
+  if (bb.has_value()) {
+    CHECK_IN((*bb), kBF);
+    TORCH_CHECK(bb->numel() == C && b.has_value(), "branch bias needs a branch tensor");
+  }
   auto y = at::empty_like(a);
   at::Tensor xout = b.has_value() ? at::empty_like(a) : a;
   auto mean = at::empty({R}, a.options().dtype(kF));
   auto rstd = at::empty({R}, a.options().dtype(kF));
   vcx_ln_fwd(a.data_ptr(), opt_ptr(b), b.has_value() ? xout.data_ptr() : nullptr, y.data_ptr(), w.data_ptr(),
              opt_ptr(bias), mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)R, C, (float)eps, rms ? 1 : 0,
-             cur_stream());
+             opt_ptr(bb), cur_stream());
   return {y, xout, mean, rstd};
 }
 
+// returns {dx, dw, db or None, dbb or None}
 std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Tensor mean, at::Tensor rstd,
-                               c10::optional<at::Tensor> dres, bool has_bias, bool rms) {
+                               c10::optional<at::Tensor> dres, bool has_bias, bool rms, bool has_bb) {
   CHECK_IN(dy, kBF);
   CHECK_IN(x, kBF);
   CHECK_IN(w, kBF);
@@ -148,11 +153,40 @@ std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Te
     db_part = at::empty({P, C}, x.options().dtype(kF));
     db = at::empty({C}, x.options());
   }
+  at::Tensor dbb_part, dbb;
+  if (has_bb) {
+    dbb_part = at::empty({P, C}, x.options().dtype(kF));
+    dbb = at::empty({C}, x.options());
+  }
   vcx_ln_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
              opt_ptr(dres), dx.data_ptr(), dw_part.data_ptr<float>(), has_bias ? db_part.data_ptr<float>() : nullptr,
-             dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)R, C, rms ? 1 : 0, cur_stream());
-  if (has_bias) return {dx, dw, db};
-  return {dx, dw};
+             dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)R, C, rms ? 1 : 0,
+             has_bb ? dbb_part.data_ptr<float>() : nullptr, has_bb ? dbb.data_ptr() : nullptr, cur_stream());
+  return {dx, dw, db, dbb};
+}
+
+at::Tensor bias_gelu_fwd(at::Tensor x, at::Tensor b) {
+  CHECK_IN(x, kBF);
+  CHECK_IN(b, kBF);
+  const int64_t F = x.size(-1), R = x.numel() / F;
+  TORCH_CHECK(F % 8 == 0 && b.numel() == F && R < INT32_MAX);
+  auto y = at::empty_like(x);
+  vcx_bias_gelu_fwd(x.data_ptr(), b.data_ptr(), y.data_ptr(), (int)R, (int)F, cur_stream());
+  return y;
+}
+
+std::vector<at::Tensor> bias_gelu_bwd(at::Tensor x, at::Tensor b, at::Tensor dy) {
+  CHECK_IN(x, kBF);
+  CHECK_IN(b, kBF);
+  CHECK_IN(dy, kBF);
+  const int64_t F = x.size(-1), R = x.numel() / F;
+  TORCH_CHECK(F % 8 == 0 && b.numel() == F && dy.sizes() == x.sizes() && R < INT32_MAX);
+  auto dx = at::empty_like(x);
+  auto part = at::empty({vcx_bias_gelu_partials((int)R), F}, x.options().dtype(kF));
+  auto db = at::empty({F}, x.options());
+  vcx_bias_gelu_bwd(x.data_ptr(), b.data_ptr(), dy.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), db.data_ptr(),
+                    (int)R, (int)F, cur_stream());
+  return {dx, db};
 }
 
 at::Tensor gelu_fwd(at::Tensor x) {
@@ -266,6 +300,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
   m.def("gelu_fwd", &gelu_fwd);
+  m.def("bias_gelu_fwd", &bias_gelu_fwd);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);

@@ -10,13 +10,15 @@
 namespace vcx {
 
 // ============================================================ LayerNorm forward
-// xsum = a + b (if b != nullptr, written to xout), y = LN(xsum) * w + bias
+// xsum = a + b [+ bb] (if b != nullptr, written to xout), y = LN(xsum) * w + bias
+// bb is the bias of the GEMM that produced b (its epilogue add is moved here for free; the
+// matching bias gradient falls out of the backward's column sums)
 template <int CH>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
                                                       bf16* __restrict__ xout, bf16* __restrict__ y,
                                                       const bf16* __restrict__ w, const bf16* __restrict__ bias,
                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                      int R, int C, float eps, int rms) {
+                                                      int R, int C, float eps, int rms, const bf16* __restrict__ bb) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
@@ -32,9 +34,15 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16* __restrict__ a,
       if (b) {
         bf16x8 bv = *(const bf16x8*)(b + off + c * 8);
         bf16x8 s;
+        float bias_b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (bb) {
+          bf16x8 t = *(const bf16x8*)(bb + c * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bias_b[j] = (float)t[j];
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          s[j] = (bf16)((float)av[j] + (float)bv[j]);
+          s[j] = (bf16)((float)av[j] + ((float)bv[j] + bias_b[j]));
           v[k][j] = (float)s[j];  // normalise the rounded residual actually stored
         }
         *(bf16x8*)(xout + off + c * 8) = s;
@@ -94,13 +102,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
                                                       const float* __restrict__ rstd_in,
                                                       const bf16* __restrict__ dres, bf16* __restrict__ dx,
                                                       float* __restrict__ dw_part, float* __restrict__ db_part,
-                                                      int R, int C, int rms) {
+                                                      int R, int C, int rms, float* __restrict__ dbb_part) {
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int nw = gridDim.x * 4;
   const int C8 = C >> 3;
   const float invC = 1.f / (float)C;
-  float dwacc[CH][8], dbacc[CH][8], wreg[CH][8];
+  float dwacc[CH][8], dbacc[CH][8], wreg[CH][8], dxacc[CH][8];
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     const int c = lane + k * 64;
@@ -109,6 +117,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
       dwacc[k][j] = 0.f;
       dbacc[k][j] = 0.f;
       wreg[k][j] = 0.f;
+      dxacc[k][j] = 0.f;
     }
     if (c < C8) {
       bf16x8 wv = *(const bf16x8*)(w + c * 8);
@@ -146,13 +155,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
       const int c = lane + k * 64;
       if (c < C8) {
         bf16x8 o;
+        float rvf[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         if (dres) {
           bf16x8 rv = *(const bf16x8*)(dres + off + c * 8);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = (bf16)(rstd * (g[k][j] - s1 - xh[k][j] * s2) + (float)rv[j]);
-        } else {
+          for (int j = 0; j < 8; ++j) rvf[j] = (float)rv[j];
+        }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = (bf16)(rstd * (g[k][j] - s1 - xh[k][j] * s2));
+        for (int j = 0; j < 8; ++j) {
+          const float v = rstd * (g[k][j] - s1 - xh[k][j] * s2) + rvf[j];
+          o[j] = (bf16)v;
+          dxacc[k][j] += v;
         }
         *(bf16x8*)(dx + off + c * 8) = o;
       }
@@ -170,8 +183,62 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
         *(f32x4*)dbp = f32x4{dbacc[k][0], dbacc[k][1], dbacc[k][2], dbacc[k][3]};
         *(f32x4*)(dbp + 4) = f32x4{dbacc[k][4], dbacc[k][5], dbacc[k][6], dbacc[k][7]};
       }
+      if (dbb_part) {  // gradient of the branch bias = column sums of dx
+        float* p = dbb_part + (int64_t)gw * C + c * 8;
+        *(f32x4*)p = f32x4{dxacc[k][0], dxacc[k][1], dxacc[k][2], dxacc[k][3]};
+        *(f32x4*)(p + 4) = f32x4{dxacc[k][4], dxacc[k][5], dxacc[k][6], dxacc[k][7]};
+      }
     }
   }
+}
+
+// ============================================================ bias + tanh-GELU over [R, F]
+// fwd: y = gelu(x + b). bwd: dx = dy * gelu'(x + b) and per-block column partials of dx
+// (the bias gradient) — the GEMM before it runs without a bias epilogue and no separate
+// bias-gradient reduction is needed. grid = (ceil(F/8/256), row groups).
+__device__ __forceinline__ float gelu_f(float x);
+__device__ __forceinline__ float gelu_grad_f(float x);
+
+__global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ b,
+                                                             bf16* __restrict__ y, int R, int F) {
+  const int F8 = F >> 3;
+  const int c8 = blockIdx.x * 256 + threadIdx.x;
+  if (c8 >= F8) return;
+  bf16x8 bv = *(const bf16x8*)(b + c8 * 8);
+  for (int r = blockIdx.y; r < R; r += gridDim.y) {
+    const int64_t off = (int64_t)r * F + c8 * 8;
+    bf16x8 v = *(const bf16x8*)(x + off);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)gelu_f((float)v[j] + (float)bv[j]);
+    *(bf16x8*)(y + off) = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ b,
+                                                             const bf16* __restrict__ dy, bf16* __restrict__ dx,
+                                                             float* __restrict__ dbias_part, int R, int F) {
+  const int F8 = F >> 3;
+  const int c8 = blockIdx.x * 256 + threadIdx.x;
+  if (c8 >= F8) return;
+  bf16x8 bv = *(const bf16x8*)(b + c8 * 8);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = blockIdx.y; r < R; r += gridDim.y) {
+    const int64_t off = (int64_t)r * F + c8 * 8;
+    bf16x8 v = *(const bf16x8*)(x + off);
+    bf16x8 g = *(const bf16x8*)(dy + off);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = (float)g[j] * gelu_grad_f((float)v[j] + (float)bv[j]);
+      o[j] = (bf16)d;
+      acc[j] += d;
+    }
+    *(bf16x8*)(dx + off) = o;
+  }
+  float* p = dbias_part + (int64_t)blockIdx.y * F + c8 * 8;
+  *(f32x4*)p = f32x4{acc[0], acc[1], acc[2], acc[3]};
+  *(f32x4*)(p + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
 }
 
 // Column sums of a [P, C] fp32 partial buffer -> bf16 [C]. One block per 64 columns,
@@ -385,29 +452,52 @@ using namespace vcx;
   }
 
 void vcx_ln_fwd(const void* a, const void* b, void* xout, void* y, const void* w, const void* bias, float* mean,
-                float* rstd, int R, int C, float eps, int rms, hipStream_t s) {
+                float* rstd, int R, int C, float eps, int rms, const void* bb, hipStream_t s) {
   const int ch = (C / 8 + 63) / 64;
   dim3 grid((R + 3) / 4);
   VCX_LN_DISPATCH(ch, hipLaunchKernelGGL(ln_fwd_kernel<CH>, grid, dim3(256), 0, s, (const bf16*)a,
                                          (const bf16*)b, (bf16*)xout, (bf16*)y, (const bf16*)w,
-                                         (const bf16*)bias, mean, rstd, R, C, eps, rms));
+                                         (const bf16*)bias, mean, rstd, R, C, eps, rms, (const bf16*)bb));
+}
+
+static int bias_gelu_groups(int R) { return R < 256 ? (R > 0 ? R : 1) : 256; }
+
+int vcx_bias_gelu_partials(int R) { return bias_gelu_groups(R); }
+
+void vcx_bias_gelu_fwd(const void* x, const void* b, void* y, int R, int F, hipStream_t s) {
+  dim3 grid((F / 8 + 255) / 256, R < 1024 ? (R > 0 ? R : 1) : 1024);
+  hipLaunchKernelGGL(bias_gelu_fwd_kernel, grid, dim3(256), 0, s, (const bf16*)x, (const bf16*)b, (bf16*)y, R, F);
+}
+
+void vcx_bias_gelu_bwd(const void* x, const void* b, const void* dy, void* dx, float* part, void* db, int R, int F,
+                       hipStream_t s) {
+  const int G = bias_gelu_groups(R);
+  dim3 grid((F / 8 + 255) / 256, G);
+  hipLaunchKernelGGL(bias_gelu_bwd_kernel, grid, dim3(256), 0, s, (const bf16*)x, (const bf16*)b, (const bf16*)dy,
+                     (bf16*)dx, part, R, F);
+  hipLaunchKernelGGL(colsum_kernel, dim3((F + 63) / 64), dim3(1024), 0, s, part, G, F, (bf16*)db);
 }
 
 int vcx_ln_bwd_partials(int R) {
+  // enough waves to keep every SIMD busy with several rows in flight (each wave streams
+  // ~16 rows); the [P, C] fp32 partials cost one extra small read in colsum_kernel
   int g = (R + 3) / 4;
-  return (g > 256 ? 256 : g) * 4;
+  return (g > 1024 ? 1024 : g) * 4;
 }
 
 void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
-                void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, hipStream_t s) {
+                void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, float* dbb_part,
+                void* dbb, hipStream_t s) {
   const int ch = (C / 8 + 63) / 64;
   const int P = vcx_ln_bwd_partials(R);
   dim3 grid(P / 4);
   VCX_LN_DISPATCH(ch, hipLaunchKernelGGL(ln_bwd_kernel<CH>, grid, dim3(256), 0, s, (const bf16*)dy,
                                          (const bf16*)x, (const bf16*)w, mean, rstd, (const bf16*)dres,
-                                         (bf16*)dx, dw_part, db_part, R, C, rms));
+                                         (bf16*)dx, dw_part, db_part, R, C, rms, dbb_part));
   hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, dw_part, P, C, (bf16*)dw);
   if (db_part && db) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, db_part, P, C, (bf16*)db);
+  if (dbb_part && dbb)
+    hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, dbb_part, P, C, (bf16*)dbb);
 }
 
 void vcx_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s) {

@@ -17,10 +17,15 @@ void vcx_axpy_bf16(const void* src, void* acc, int64_t n, float scale, hipStream
 
 // norm_act.hip
 void vcx_ln_fwd(const void* a, const void* b, void* xout, void* y, const void* w, const void* bias, float* mean,
-                float* rstd, int R, int C, float eps, int rms, hipStream_t s);
+                float* rstd, int R, int C, float eps, int rms, const void* bb, hipStream_t s);
+int vcx_bias_gelu_partials(int R);
+void vcx_bias_gelu_fwd(const void* x, const void* b, void* y, int R, int F, hipStream_t s);
+void vcx_bias_gelu_bwd(const void* x, const void* b, const void* dy, void* dx, float* part, void* db, int R, int F,
+                       hipStream_t s);
 int vcx_ln_bwd_partials(int R);
 void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
-                void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, hipStream_t s);
+                void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, float* dbb_part,
+                void* dbb, hipStream_t s);
 void vcx_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s);
 void vcx_gelu_bwd(const void* x, const void* dy, void* dx, int64_t n, hipStream_t s);
 void vcx_swiglu_fwd(const void* gu, void* y, int64_t R, int F, hipStream_t s);

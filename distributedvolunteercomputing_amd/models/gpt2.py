@@ -84,10 +84,13 @@ class Block(nn.Module):
             with sdpa_kernel(_SDPA_BACKENDS):
                 y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
             y = y.transpose(1, 2)
-        return F.linear(y.reshape(B, T, C), self.proj_w, self.proj_b)
+        # no bias here: proj_b is added (and its gradient reduced) by the following fused
+        # residual-add + LayerNorm kernel
+        return F.linear(y.reshape(B, T, C), self.proj_w)
 
     def mlp(self, h):
-        return F.linear(ops.gelu(F.linear(h, self.fc_w, self.fc_b)), self.fc2_w, self.fc2_b)
+        # fc bias fused into the GELU kernel; fc2 bias fused into the next add+LayerNorm
+        return F.linear(ops.bias_gelu(F.linear(h, self.fc_w), self.fc_b), self.fc2_w)
 
 
 class GPT2(nn.Module):
@@ -142,13 +145,13 @@ class GPT2(nn.Module):
         h, resid = ops.add_layernorm(x, None, blocks[0].ln1_w, blocks[0].ln1_b, eps)
         for i, blk in enumerate(blocks):
             a = blk.attn(h)
-            h, resid = ops.add_layernorm(resid, a, blk.ln2_w, blk.ln2_b, eps)
+            h, resid = ops.add_layernorm(resid, a, blk.ln2_w, blk.ln2_b, eps, branch_bias=blk.proj_b)
             m = blk.mlp(h)
             if i + 1 < len(blocks):
                 nxt = blocks[i + 1]
-                h, resid = ops.add_layernorm(resid, m, nxt.ln1_w, nxt.ln1_b, eps)
+                h, resid = ops.add_layernorm(resid, m, nxt.ln1_w, nxt.ln1_b, eps, branch_bias=blk.fc2_b)
             else:
-                h, resid = ops.add_layernorm(resid, m, self.lnf_w, self.lnf_b, eps)
+                h, resid = ops.add_layernorm(resid, m, self.lnf_w, self.lnf_b, eps, branch_bias=blk.fc2_b)
         logits = F.linear(h, self.wte)  # tied LM head, [B, T, Vp]
         if targets is None:
             return logits[..., : cfg.vocab_size]

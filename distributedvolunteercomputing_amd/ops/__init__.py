@@ -1,7 +1,7 @@
 """Hot ops. On GPU every op here runs a hand-written gfx950 HIP kernel from ``_C``;
 on CPU the same call runs the plain-PyTorch reference (used by tests and CPU volunteers)."""
 from ._lib import available as native_available, native  # noqa: F401
-from .activations import gelu, swiglu  # noqa: F401
+from .activations import bias_gelu, gelu, swiglu  # noqa: F401
 from .attention import causal_attention  # noqa: F401
 from .loss import cross_entropy  # noqa: F401
 from .norm import add_layernorm, add_rmsnorm, layernorm, rmsnorm  # noqa: F401

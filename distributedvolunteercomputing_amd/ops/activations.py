@@ -26,6 +26,27 @@ def gelu(x):
     return F.gelu(x.float(), approximate="tanh").to(x.dtype)
 
 
+class _BiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, b):
+        x = x.contiguous()
+        ctx.save_for_backward(x, b)
+        return native().bias_gelu_fwd(x, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, b = ctx.saved_tensors
+        dx, db = native().bias_gelu_bwd(x, b, dy.contiguous())
+        return dx, db
+
+
+def bias_gelu(x, b):
+    """gelu_tanh(x + b) with the bias gradient reduced inside the backward kernel."""
+    if use_native(x):
+        return _BiasGelu.apply(x, b)
+    return F.gelu((x + b).float(), approximate="tanh").to(x.dtype)
+
+
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, gu):

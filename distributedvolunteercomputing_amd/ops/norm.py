@@ -1,8 +1,11 @@
 """LayerNorm / RMSNorm with an optional fused residual add (HIP on GPU, torch on CPU).
 
-``add_layernorm(a, b, w, bias)`` returns ``(y, x)`` with ``x = a + b`` (the new residual
-stream) and ``y = LN(x)``. Fusing the add saves one full read+write of the residual stream per
-sub-layer; the backward fuses the residual-gradient add into ``dx``.
+``add_layernorm(a, b, w, bias, branch_bias=bb)`` returns ``(y, x)`` with ``x = a + b + bb``
+(the new residual stream) and ``y = LN(x)``. Fusing the add saves one full read+write of the
+residual stream per sub-layer; ``bb`` is the bias of the GEMM that produced ``b`` (the GEMM
+then runs without a bias epilogue and its bias gradient comes out of this kernel's backward
+as the column sums of dx, replacing a separate reduction). The backward also fuses the
+residual-gradient add into ``dx``.
 """
 from __future__ import annotations
 
@@ -28,12 +31,13 @@ def _ref_ln(x, w, b, eps, rms):
 
 class _AddLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, b, w, bias, eps, rms):
+    def forward(ctx, a, b, w, bias, eps, rms, bb):
         C = native()
-        y, x, mean, rstd = C.ln_fwd(a.contiguous(), None if b is None else b.contiguous(), w, bias, eps, rms)
+        y, x, mean, rstd = C.ln_fwd(a.contiguous(), None if b is None else b.contiguous(), w, bias, eps, rms, bb)
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.has_b = b is not None
         ctx.has_bias = bias is not None
+        ctx.has_bb = bb is not None
         ctx.rms = rms
         if b is None:
             x = x.view_as(x)  # output aliases the input: hand autograd a view, not the input itself
@@ -44,19 +48,19 @@ class _AddLN(torch.autograd.Function):
         x, w, mean, rstd = ctx.saved_tensors
         C = native()
         dres = None if dx_res is None else dx_res.contiguous()
-        outs = C.ln_bwd(dy.contiguous(), x, w, mean, rstd, dres, ctx.has_bias, ctx.rms)
-        dx = outs[0]
-        dw = outs[1]
-        dbias = outs[2] if ctx.has_bias else None
-        return dx, (dx if ctx.has_b else None), dw, dbias, None, None
+        dx, dw, dbias, dbb = C.ln_bwd(dy.contiguous(), x, w, mean, rstd, dres, ctx.has_bias, ctx.rms, ctx.has_bb)
+        return dx, (dx if ctx.has_b else None), dw, dbias, None, None, dbb
 
 
-def add_layernorm(a, b, weight, bias=None, eps: float = 1e-5, rms: bool = False):
-    """Returns (LN(a+b), a+b). With b=None returns (LN(a), a)."""
+def add_layernorm(a, b, weight, bias=None, eps: float = 1e-5, rms: bool = False, branch_bias=None):
+    """Returns (LN(a+b[+branch_bias]), a+b[+branch_bias]). With b=None returns (LN(a), a)."""
     if use_native(a):
-        y, x = _AddLN.apply(a, b, weight, bias, eps, rms)
+        y, x = _AddLN.apply(a, b, weight, bias, eps, rms, branch_bias)
         return y, x
-    x = a if b is None else a + b
+    if b is None:
+        x = a
+    else:
+        x = a + (b if branch_bias is None else b + branch_bias)
     return _ref_ln(x, weight, bias, eps, rms), x
 
 

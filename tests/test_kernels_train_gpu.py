@@ -164,3 +164,37 @@ def test_axpy_bf16(gpu):
     ref = (a.float() + 0.5 * b.float()).to(torch.bfloat16)
     ops.axpy_bf16(b, a, 0.5)
     assert torch.equal(a, ref)
+
+
+def test_add_layernorm_branch_bias(gpu):
+    torch.manual_seed(7)
+    R, C = 300, 768
+    a = _bf(torch.randn(R, C, device=gpu)).requires_grad_()
+    b = _bf(torch.randn(R, C, device=gpu)).requires_grad_()
+    bb = _bf(torch.randn(C, device=gpu)).requires_grad_()
+    w = _bf(torch.rand(C, device=gpu) + 0.5).requires_grad_()
+    y, x = ops.add_layernorm(a, b, w, None, branch_bias=bb)
+    a32, b32, bb32, w32 = (t.detach().float().requires_grad_() for t in (a, b, bb, w))
+    xr = a32 + b32 + bb32
+    yr = F.layer_norm(xr, (C,), w32, None, 1e-5)
+    assert torch.allclose(y.float(), yr, atol=3e-2, rtol=2e-2)
+    dy, dxr = torch.randn(R, C, device=gpu), torch.randn(R, C, device=gpu)
+    ((y.float() * dy).sum() + (x.float() * dxr).sum()).backward()
+    ((yr * dy).sum() + (xr * dxr).sum()).backward()
+    assert torch.allclose(bb.grad.float(), bb32.grad, atol=0.5, rtol=3e-2)
+    assert torch.allclose(b.grad.float(), b32.grad, atol=5e-2, rtol=3e-2)
+
+
+def test_bias_gelu(gpu):
+    torch.manual_seed(8)
+    x = _bf(torch.randn(1000, 3072, device=gpu) * 2).requires_grad_()
+    b = _bf(torch.randn(3072, device=gpu)).requires_grad_()
+    y = ops.bias_gelu(x, b)
+    x32, b32 = x.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    yr = F.gelu(x32 + b32, approximate="tanh")
+    assert torch.allclose(y.float(), yr, atol=3e-2, rtol=2e-2)
+    dy = torch.randn_like(yr)
+    (y.float() * dy).sum().backward()
+    (yr * dy).sum().backward()
+    assert torch.allclose(x.grad.float(), x32.grad, atol=5e-2, rtol=3e-2)
+    assert torch.allclose(b.grad.float(), b32.grad, atol=1.0, rtol=3e-2)
