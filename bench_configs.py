@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Per-config throughput of the BASELINE.json training configs on ONE MI355X peer.
+
+Config 2 (GPT-2-small local-SGD) is bench.py. Here, on a single GPU (the multi-peer
+collective is then a no-op, everything else — compression kernels, sharded optimizer,
+fused AdamW — runs in full):
+  3: ResNet-50, synthetic ImageNet, local-SGD H=4 + top-k (1%) error-feedback compression
+  4: GPT-2-medium local-SGD H=4
+  5: Llama-3-8B sharded-optimizer trainer + PowerSGD rank 4 (HBM sizing check on 288 GB)
+Prints one JSON line per config.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+from distributedvolunteercomputing_amd.utils.tuning import enable_tuned_gemms
+
+enable_tuned_gemms(0)
+
+import torch  # noqa: E402
+
+
+def _time(step, warmup, steps):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps, out
+
+
+def cfg3(a, dev):
+    from distributedvolunteercomputing_amd.models.resnet import resnet50
+    from distributedvolunteercomputing_amd.parallel.compression import TopKCompressor
+    from distributedvolunteercomputing_amd.parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer
+
+    m = resnet50().to(dev, torch.bfloat16).to(memory_format=torch.channels_last)
+    tr = LocalSGDTrainer(m, LocalSGDConfig(H=4, lr=1e-3, weight_decay=0.0), device=dev)
+    tr.compressor = TopKCompressor(tr.flat.numel, 0.01, dev)
+    B = a.resnet_batch
+    x = torch.randn(B, 3, 224, 224, device=dev).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (B,), device=dev)
+    dt, st = _time(lambda: tr.step(x, y), 4, a.steps)
+    # cost of one compressed averaging round on its own
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr.compressor.allreduce_mean(tr.delta, None)
+    torch.cuda.synchronize()
+    return {"config": 3, "model": "resnet50", "images_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 2),
+            "batch": B, "topk_ratio": 0.01, "topk_round_ms": round((time.perf_counter() - t0) * 1e3, 2),
+            "params": tr.flat.numel}
+
+
+def cfg4(a, dev):
+    from distributedvolunteercomputing_amd.models.gpt2 import GPT2, GPT2Config
+    from distributedvolunteercomputing_amd.parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer
+
+    cfg = GPT2Config.preset("gpt2-medium")
+    m = GPT2(cfg).to(dev, torch.bfloat16)
+    tr = LocalSGDTrainer(m, LocalSGDConfig(H=4), device=dev)
+    B, T = a.medium_batch, 1024
+    x = torch.randint(0, cfg.vocab_size, (B, T + 1), device=dev)
+    dt, _ = _time(lambda: tr.step(x[:, :-1], x[:, 1:]), 4, a.steps)
+    return {"config": 4, "model": "gpt2-medium", "samples_per_s": round(B / dt, 2), "tokens_per_s": round(B * T / dt),
+            "ms_per_step": round(dt * 1e3, 2), "batch": B, "mfu_bf16_dense": round(m.flops_per_token(T) * B * T / dt /
+                                                                                    2.5e15, 4)}
+
+
+def cfg5(a, dev):
+    from distributedvolunteercomputing_amd.models.llama import Llama, LlamaConfig
+    from distributedvolunteercomputing_amd.parallel.compression import PowerSGDCompressor
+    from distributedvolunteercomputing_amd.parallel.zero import ShardedConfig, ShardedDPTrainer
+
+    name = a.llama
+    cfg = LlamaConfig.preset(name)
+    with torch.device("meta"):
+        m = Llama(cfg, init=False)
+    m = m.to_empty(device=dev).to(torch.bfloat16)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.normal_(0.0, 0.02) if p.dim() >= 2 else p.fill_(1.0)
+    torch.cuda.reset_peak_memory_stats()
+    tr = ShardedDPTrainer(m, ShardedConfig(lr=1e-4), device=dev)
+    tr.compressor = PowerSGDCompressor(tr.flat, rank=4, device=dev)
+    B, T = a.llama_batch, a.llama_seq
+    x = torch.randint(0, cfg.vocab_size, (B, T + 1), device=dev)
+    dt, loss = _time(lambda: tr.step(x[:, :-1], x[:, 1:]), 2, max(2, a.steps // 2))
+    return {"config": 5, "model": name, "params": m.num_params(), "tokens_per_s": round(B * T / dt, 1),
+            "ms_per_step": round(dt * 1e3, 1), "batch": B, "seq": T, "loss": round(float(loss), 3),
+            "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+            "powersgd_compression_ratio": round(tr.compressor.compression_ratio, 1),
+            "mfu_bf16_dense": round(m.flops_per_token(T) * B * T / dt / 2.5e15, 4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="3,4,5")
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--resnet-batch", type=int, default=128)
+    ap.add_argument("--medium-batch", type=int, default=32)
+    ap.add_argument("--llama", default="llama3-8b")
+    ap.add_argument("--llama-batch", type=int, default=2)
+    ap.add_argument("--llama-seq", type=int, default=2048)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    fns = {"3": cfg3, "4": cfg4, "5": cfg5}
+    rc = 0
+    for c in a.configs.split(","):
+        try:
+            rec = fns[c](a, dev)
+        except Exception as e:  # report and continue with the next config
+            rec = {"config": int(c), "error": repr(e)[:500]}
+            rc = 1
+        print(json.dumps(rec), flush=True)
+        torch.cuda.empty_cache()
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(main())
