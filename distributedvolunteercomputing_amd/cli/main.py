@@ -88,13 +88,52 @@ def train_main(argv=None):
     return tmain(argv)
 
 
+def video_main(argv=None):
+    """Video job on the RCCL/xGMI data plane: run under torchrun, one rank per GPU; rank 0 is
+    the requester, every other rank a worker volunteer."""
+    import datetime
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    ap = argparse.ArgumentParser(prog="video", description=video_main.__doc__)
+    ap.add_argument("--source", default="synthetic:1000:1280x720")
+    ap.add_argument("--out", default="video0.y4m")
+    ap.add_argument("--chunk", type=int, default=100)
+    ap.add_argument("--store-port", type=int, default=int(os.environ.get("VCX_STORE_PORT", "29612")))
+    a = ap.parse_args(argv)
+    from ..jobs.video import DetectorEngine
+    from ..jobs.video_dist import run_requester, run_worker
+    from ..parallel.peer_group import PeerGroup
+
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cuda = torch.cuda.is_available()
+    dev = torch.device("cuda", local) if cuda else torch.device("cpu")
+    if cuda:
+        torch.cuda.set_device(dev)
+    store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), a.store_port, None, rank == 0,
+                          timeout=datetime.timedelta(seconds=300), wait_for_workers=False)
+    g = PeerGroup(store, rank, world, "nccl" if cuda else "gloo", device=dev) if world > 1 else None
+    eng = DetectorEngine(device=dev)
+    if rank == 0:
+        st = run_requester(g, a.source, a.out, dev, chunk=a.chunk, engine=eng)
+        print(st, flush=True)
+    else:
+        run_worker(g, eng, dev)
+    if g is not None:
+        g.barrier()
+    return 0
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
-    if not argv or argv[0] not in ("server", "worker", "train"):
-        print("usage: python -m distributedvolunteercomputing_amd.cli.main {server|worker|train} ...")
+    if not argv or argv[0] not in ("server", "worker", "train", "video"):
+        print("usage: python -m distributedvolunteercomputing_amd.cli.main {server|worker|train|video} ...")
         return 2
     cmd, rest = argv[0], argv[1:]
-    return {"server": server_main, "worker": worker_main, "train": train_main}[cmd](rest)
+    return {"server": server_main, "worker": worker_main, "train": train_main, "video": video_main}[cmd](rest)
 
 
 if __name__ == "__main__":

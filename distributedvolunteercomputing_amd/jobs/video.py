@@ -30,6 +30,12 @@ class Engine:
         """frames [n, H, W, 3] uint8 BGR -> (annotated [n, h, 400, 3] uint8, per-frame counts)."""
         raise NotImplementedError
 
+    def process_tensor(self, frames: torch.Tensor, requester: str) -> torch.Tensor:
+        """Device-resident variant used by the RCCL data plane: the chunk arrives in this
+        peer's memory and the annotated chunk leaves from it. Default: host round trip."""
+        out, _ = self.process(frames.cpu().numpy(), requester)
+        return torch.from_numpy(np.ascontiguousarray(out)).to(frames.device)
+
 
 class DetectorEngine(Engine):
     def __init__(self, device=None, prototxt=None, caffemodel=None, conf_thresh: float = 0.2, width: int = 400,
@@ -58,10 +64,32 @@ class DetectorEngine(Engine):
                 out, counts = self._run(frames, requester)
             return out.cpu().numpy(), counts.cpu().tolist()
 
+    @torch.no_grad()
+    def process_tensor(self, frames, requester):
+        with self._lock:
+            out, _ = self._run(frames, requester)
+            return out
+
+    def _staging(self, nbytes):
+        """Reusable pinned host buffer: one DMA-able copy per chunk instead of pin_memory()."""
+        buf = getattr(self, "_pinned", None)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+            self._pinned = buf
+        return buf[:nbytes]
+
     def _run(self, frames, requester):
-        x = torch.from_numpy(np.ascontiguousarray(frames))
-        if self.device.type == "cuda":
-            x = x.pin_memory().to(self.device, non_blocking=True)
+        if isinstance(frames, torch.Tensor):
+            x = frames.to(self.device)
+        else:
+            a = np.ascontiguousarray(frames)
+            if self.device.type == "cuda":
+                st = self._staging(a.nbytes)
+                torch.cuda.current_stream().synchronize()  # previous chunk's H2D done before reuse
+                st.numpy()[:] = a.reshape(-1)
+                x = st.view(a.shape).to(self.device, non_blocking=True)
+            else:
+                x = torch.from_numpy(a)
         small = V.resize_width(x, self.width).contiguous()
         dets, cnt = self.exec.detect(small)
         counts = V.annotate(small, dets, cnt, requester, label=self.label, cls_name=self.consider,
