@@ -26,6 +26,21 @@ constexpr int TK_BINS = 4096;
 
 __device__ __forceinline__ uint32_t absbits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
 
+// Wave-aggregated LDS histogram increment. Gradient magnitudes crowd into a handful of
+// exponent bins, so a plain per-lane LDS atomic serialises up to 64 lanes on one address;
+// here each distinct bin present in the wave costs ONE atomic (leader + ballot popcount).
+__device__ __forceinline__ void wave_hist_add(uint32_t* h, int bin, bool valid) {
+  unsigned long long todo = __ballot(valid);
+  const int lane = threadIdx.x & 63;
+  while (todo) {
+    const int leader = __ffsll((long long)todo) - 1;
+    const int lb = __shfl(bin, leader, 64);
+    const unsigned long long same = __ballot(valid && bin == lb) & todo;
+    if (lane == leader) atomicAdd(&h[lb], (uint32_t)__popcll(same));
+    todo &= ~same;
+  }
+}
+
 // acc = g + e (written to e, fp32), histogram pass 0 of |acc| (bits 30..19 -> 12 bits)
 template <typename GT>
 __global__ void __launch_bounds__(256) topk_accum_hist_kernel(const GT* __restrict__ g, float* __restrict__ e,
@@ -33,10 +48,16 @@ __global__ void __launch_bounds__(256) topk_accum_hist_kernel(const GT* __restri
   __shared__ uint32_t h[TK_BINS];
   for (int i = threadIdx.x; i < TK_BINS; i += 256) h[i] = 0;
   __syncthreads();
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    float a = (float)g[i] + e[i];
-    e[i] = a;
-    atomicAdd(&h[absbits(a) >> 19], 1u);
+  // the loop bound is wave-uniform (whole-block strides) so every lane joins the ballots
+  for (int64_t base = blockIdx.x * 256ll; base < n; base += (int64_t)gridDim.x * 256) {
+    const int64_t i = base + threadIdx.x;
+    int bin = 0;
+    if (i < n) {
+      float a = (float)g[i] + e[i];
+      e[i] = a;
+      bin = (int)(absbits(a) >> 19);
+    }
+    wave_hist_add(h, bin, i < n);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < TK_BINS; i += 256)
@@ -52,9 +73,16 @@ __global__ void __launch_bounds__(256) topk_hist_kernel(const float* __restrict_
   for (int i = threadIdx.x; i < nb; i += 256) h[i] = 0;
   __syncthreads();
   const uint32_t prefix = (uint32_t)st[0];
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const uint32_t b = absbits(x[i]);
-    if ((b >> shift_hi) == prefix) atomicAdd(&h[(b >> shift) & (nb - 1)], 1u);
+  for (int64_t base = blockIdx.x * 256ll; base < n; base += (int64_t)gridDim.x * 256) {
+    const int64_t i = base + threadIdx.x;
+    bool hit = false;
+    int bin = 0;
+    if (i < n) {
+      const uint32_t b = absbits(x[i]);
+      hit = (b >> shift_hi) == prefix;
+      bin = (int)((b >> shift) & (nb - 1));
+    }
+    wave_hist_add(h, bin, hit);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nb; i += 256)
