@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--H", type=int, default=4)
     ap.add_argument("--algo", default="rccl", choices=["rccl", "rs_ag", "butterfly", "ring"])
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--graph", type=int, default=0, help="1: replay each local step as one hipGraph")
     return ap.parse_args()
 
 
@@ -85,7 +86,11 @@ def main():
         if group is not None:
             group.barrier()
 
-    for i in range(a.warmup):
+    w0 = 0
+    if a.graph and cuda:
+        w0 = min(3, a.warmup)
+        trainer.capture(*batch(0), warmup=w0)  # w0 real steps, then hipGraph capture
+    for i in range(w0, a.warmup):
         trainer.step(*batch(i))
     sync_all()
     t0 = time.perf_counter()
@@ -130,6 +135,7 @@ def main():
             "final_loss": round(loss, 4),
             "sync_ms": round(trainer.last_sync_ms, 3),
             "tuned_gemms": TUNED_GEMMS,
+            "hipgraph": bool(a.graph and cuda),
         }
         line = json.dumps(rec)
         print(line, flush=True)

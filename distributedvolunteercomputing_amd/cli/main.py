@@ -21,12 +21,14 @@ def server_main(argv=None):
     ap.add_argument("--credits", type=int, default=2, help="max chunks in flight per volunteer")
     ap.add_argument("--lease", type=float, default=10.0, help="heartbeat lease (s)")
     ap.add_argument("--ephemeral-ports", action="store_true", help="data ports from the OS instead of 5555..5599")
+    ap.add_argument("--train-store-port", type=int, default=None,
+                    help="also host the rendezvous store for training peers on this TCP port")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
     from ..control.coordinator import coordinator
 
     c = coordinator(a.ip, a.port, ephemeral_ports=a.ephemeral_ports, policy=a.policy, credits=a.credits,
-                    lease_s=a.lease, verbose=a.verbose)
+                    lease_s=a.lease, verbose=a.verbose, train_store_port=a.train_store_port)
     print(f"\nlistening on {a.ip} port {c.control_port}", flush=True)
     while True:
         try:

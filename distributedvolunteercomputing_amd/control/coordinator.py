@@ -59,9 +59,21 @@ class coordinator:  # noqa: N801  (reference class name)
 
     def __init__(self, ip: str = "localhost", control_port: int = protocol.DEFAULT_CONTROL_PORT, *,
                  ephemeral_ports: bool = False, max_clients: int | None = None, policy: str = "round_robin",
-                 credits: int = 2, lease_s: float | None = None, verbose: bool | None = None):
+                 credits: int = 2, lease_s: float | None = None, verbose: bool | None = None,
+                 train_store_port: int | None = None):
         if verbose is not None:
             self.verbose = verbose
+        # Rendezvous store for training peers (heartbeats, generations, RCCL bootstrap). Hosted
+        # here so that ANY training peer may die without taking the membership state with it.
+        self.train_store = None
+        if train_store_port is not None:
+            import datetime
+
+            import torch.distributed as dist
+
+            self.train_store = dist.TCPStore("0.0.0.0", int(train_store_port), None, True,
+                                             timeout=datetime.timedelta(seconds=300), wait_for_workers=False)
+            self.train_store_port = self.train_store.port
         if lease_s is not None:
             self.lease_s = lease_s
         N = _native_loader.native()
@@ -140,6 +152,8 @@ class coordinator:  # noqa: N801  (reference class name)
             return protocol.reply_ok()
         if verb == "status":
             return protocol.reply_ok(json.dumps(self.status()))
+        if verb == "store":  # where training peers rendezvous
+            return protocol.reply_ok(str(self.train_store_port) if self.train_store is not None else "")
         return None
 
     def _join(self, addr, now):

@@ -21,7 +21,7 @@ import select
 import socket
 import time
 
-VERBS = ("join", "request", "stop", "end", "hb", "status")
+VERBS = ("join", "request", "stop", "end", "hb", "status", "store")
 SEP = "||"
 DEFAULT_CONTROL_PORT = 9999
 

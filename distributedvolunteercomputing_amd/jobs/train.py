@@ -98,6 +98,8 @@ def parse(argv=None):
     ap.add_argument("--world", type=int, default=None)
     ap.add_argument("--store-host", default=os.environ.get("MASTER_ADDR", "127.0.0.1"))
     ap.add_argument("--store-port", type=int, default=int(os.environ.get("VCX_STORE_PORT", "29611")))
+    ap.add_argument("--coordinator", default=None,
+                    help="host:control_port of a coordinator that hosts the rendezvous store (no peer is special)")
     ap.add_argument("--join", action="store_true", help="join a running job instead of bootstrapping")
     ap.add_argument("--drop-at", type=int, default=-1, help="fault injection: crash this peer at that step")
     ap.add_argument("--ckpt-dir", default=None)
@@ -120,7 +122,13 @@ def main(argv=None):
     backend = a.backend or ("nccl" if cuda else "gloo")
     from ..parallel.peer_group import PeerGroup
 
-    store = dist.TCPStore(a.store_host, a.store_port, None, rank == 0 and not a.join,
+    if a.coordinator:  # the coordinator hosts the rendezvous store: ask it where
+        from ..control.protocol import ControlClient
+
+        host, _, cport = a.coordinator.rpartition(":")
+        a.store_host = host
+        a.store_port = int(ControlClient(host, int(cport)).call("store", f"train-peer-{rank}"))
+    store = dist.TCPStore(a.store_host, a.store_port, None, rank == 0 and not a.join and not a.coordinator,
                           timeout=datetime.timedelta(seconds=300), wait_for_workers=False)
     membership = group = None
     if a.elastic:

@@ -91,9 +91,39 @@ class LocalSGDTrainer:
                        n_decay=self.flat.n_decay, beta1=c.betas[0], beta2=c.betas[1], eps=c.eps,
                        wd=c.weight_decay, max_norm=c.max_grad_norm)
 
+    # ------------------------------------------------------------------ hipGraph capture
+    def capture(self, x, y, warmup: int = 3):
+        """Capture zero-grad + forward + backward + fused AdamW of one local step into a
+        hipGraph (torch.cuda.graph). Replays then cost one graph launch instead of ~300
+        kernel launches; the averaging round stays outside the graph (collective,
+        membership). x/y shapes are fixed from here on. Runs `warmup` real steps first."""
+        assert x.is_cuda, "graph capture needs GPU tensors"
+        self._gx = x.clone()
+        self._gy = y.clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.forward_backward(self._gx, self._gy)
+                self.optimizer_step()
+                self.t += 1
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._gloss = self.forward_backward(self._gx, self._gy)
+            self.optimizer_step()
+        return self
+
     def step(self, x, y) -> StepStats:
-        loss = self.forward_backward(x, y)
-        self.optimizer_step()
+        if getattr(self, "graph", None) is not None:
+            if x.data_ptr() != self._gx.data_ptr():
+                self._gx.copy_(x, non_blocking=True)
+                self._gy.copy_(y, non_blocking=True)
+            self.graph.replay()
+            loss = self._gloss
+        else:
+            loss = self.forward_backward(x, y)
+            self.optimizer_step()
         self.t += 1
         synced = False
         if self.t % self.cfg.H == 0:

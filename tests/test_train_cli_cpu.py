@@ -88,3 +88,29 @@ def test_localsgd_cli_peer_crash_survivors_continue(tmp_path):
     for r in (0, 1):
         recs = _records(outs[r][0])
         assert recs[-1]["step"] == 16 and recs[-1]["members"] == 2 and recs[-1]["gen"] == 1
+
+
+def test_coordinator_hosted_store_survives_peer0_crash():
+    """With the coordinator hosting the rendezvous store, even peer 0 may crash."""
+    from distributedvolunteercomputing_amd.control.coordinator import coordinator
+
+    c = coordinator("127.0.0.1", 0, ephemeral_ports=True, train_store_port=0)
+    try:
+        env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+        procs = []
+        for r in range(3):
+            args = ["--model", "mlp", "--steps", "16", "--H", "2", "--batch", "32", "--elastic", "--lease", "1.0",
+                    "--log-every", "2", "--coordinator", f"127.0.0.1:{c.control_port}"]
+            if r == 0:
+                args += ["--drop-at", "5"]
+            procs.append(subprocess.Popen([sys.executable, "-m", "distributedvolunteercomputing_amd.cli.main",
+                                           "train", "--peer-id", str(r), "--world", "3", *args], cwd=ROOT, env=env,
+                                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+        outs = [p.communicate(timeout=180)[0] for p in procs]
+        for out, p in zip(outs, procs):
+            assert p.returncode == 0, out[-3000:]
+        for r in (1, 2):
+            recs = _records(outs[r])
+            assert recs[-1]["step"] == 16 and recs[-1]["members"] == 2, recs[-1]
+    finally:
+        c.exit_threads()
