@@ -254,6 +254,36 @@ void xent_bwd(at::Tensor logits, at::Tensor tgt, at::Tensor lse, at::Tensor gsca
                dlogits.data_ptr(), R, (int)V, (int)Vp, cur_stream());
 }
 
+// ------------------------------------------------------------------ embedding
+at::Tensor embed_fwd(at::Tensor idx, at::Tensor wte, c10::optional<at::Tensor> wpe, int64_t T) {
+  CHECK_IN(idx, at::kLong);
+  CHECK_IN(wte, kBF);
+  TORCH_CHECK(wte.dim() == 2 && wte.size(1) % 8 == 0);
+  const int64_t R = idx.numel(), V = wte.size(0), C = wte.size(1);
+  TORCH_CHECK(T > 0 && R % T == 0);
+  if (wpe.has_value()) {
+    CHECK_IN((*wpe), kBF);
+    TORCH_CHECK(wpe->dim() == 2 && wpe->size(1) == C && wpe->size(0) >= T, "position table too short");
+  }
+  auto out = at::empty({R, C}, wte.options());
+  vcx_embed_fwd(idx.data_ptr<int64_t>(), wte.data_ptr(), opt_ptr(wpe), out.data_ptr(), R, (int)T, (int)C, (int)V,
+                cur_stream());
+  return out;
+}
+
+std::vector<at::Tensor> embed_bwd(at::Tensor idx, at::Tensor dx, int64_t V, int64_t T, int64_t Tpos) {
+  CHECK_IN(idx, at::kLong);
+  CHECK_IN(dx, kBF);
+  const int64_t R = idx.numel(), C = dx.size(-1);
+  TORCH_CHECK(dx.numel() == R * C && C % 8 == 0 && T > 0 && R % T == 0 && Tpos >= 0);
+  auto dwte = at::zeros({V, C}, dx.options().dtype(kF));
+  at::Tensor dwpe;
+  if (Tpos > 0) dwpe = at::zeros({Tpos, C}, dx.options().dtype(kF));
+  vcx_embed_bwd(idx.data_ptr<int64_t>(), dx.data_ptr(), dwte.data_ptr<float>(),
+                Tpos > 0 ? dwpe.data_ptr<float>() : nullptr, R, (int)T, (int)C, (int)V, cur_stream());
+  return {dwte.to(at::kBFloat16), Tpos > 0 ? dwpe.to(at::kBFloat16) : at::Tensor()};
+}
+
 // ------------------------------------------------------------------ attention (head dim 64)
 std::vector<at::Tensor> attn_fwd(at::Tensor qkv, double scale) {
   CHECK_IN(qkv, kBF);
@@ -307,6 +337,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   vcx_register_vision(m);

@@ -39,3 +39,9 @@ void vcx_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, cons
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s);
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
                       int B, int T, int H, float scale, hipStream_t s);
+
+// embed.hip
+void vcx_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int64_t R, int T, int C, int V,
+                   hipStream_t s);
+void vcx_embed_bwd(const int64_t* idx, const void* dx, float* dwte, float* dwpe, int64_t R, int T, int C, int V,
+                   hipStream_t s);

@@ -50,7 +50,7 @@ class GPT2Config:
             "gpt2-medium": dict(n_layer=24, n_head=16, n_embd=1024),  # 350M
             "gpt2-large": dict(n_layer=36, n_head=20, n_embd=1280),  # 774M
             "gpt2-xl": dict(n_layer=48, n_head=25, n_embd=1600),  # 1.56B
-            "gpt2-tiny": dict(n_layer=2, n_head=4, n_embd=128, n_ctx=128, vocab_size=512, padded_vocab=512),
+            "gpt2-tiny": dict(n_layer=2, n_head=2, n_embd=128, n_ctx=128, vocab_size=512, padded_vocab=512),
         }
         return GPT2Config(**table[name])
 
@@ -138,8 +138,7 @@ class GPT2(nn.Module):
     def forward(self, idx, targets=None):
         B, T = idx.shape
         cfg = self.cfg
-        pos = torch.arange(T, device=idx.device)
-        x = F.embedding(idx, self.wte) + F.embedding(pos, self.wpe)
+        x = ops.embed(idx, self.wte, self.wpe)  # fused token + position gather (HIP)
         eps = cfg.ln_eps
         blocks = self.blocks
         h, resid = ops.add_layernorm(x, None, blocks[0].ln1_w, blocks[0].ln1_b, eps)

@@ -120,7 +120,7 @@ class Llama(nn.Module):
         B, T = idx.shape
         c = self.c
         cos, sin = rope_tables(T, c.dim // c.n_heads, c.rope_theta, idx.device)
-        x = F.embedding(idx, self.tok)
+        x = ops.embed(idx, self.tok)
         h, resid = ops.add_rmsnorm(x, None, self.layers[0].attn_norm, c.norm_eps)
         for i, L in enumerate(self.layers):
             a = L.attn(h, cos, sin)

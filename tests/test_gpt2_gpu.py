@@ -71,4 +71,4 @@ def test_hipgraph_step_matches_eager(gpu):
         sb = tb.step(x, y)
     torch.cuda.synchronize()
     assert abs(float(sa.extra["loss_t"]) - float(sb.extra["loss_t"])) < 1e-2
-    assert torch.allclose(ta.master, tb.master, atol=1e-4, rtol=1e-3)
+    assert ((ta.master - tb.master).norm() / ta.master.norm()).item() < 1e-3

@@ -198,3 +198,20 @@ def test_bias_gelu(gpu):
     (yr * dy).sum().backward()
     assert torch.allclose(x.grad.float(), x32.grad, atol=5e-2, rtol=3e-2)
     assert torch.allclose(b.grad.float(), b32.grad, atol=1.0, rtol=3e-2)
+
+
+def test_embedding_fwd_bwd(gpu):
+    torch.manual_seed(9)
+    V, C, B, T = 1000, 768, 4, 100
+    idx = torch.randint(0, V, (B, T), device=gpu)
+    wte = _bf(torch.randn(V, C, device=gpu)).requires_grad_()
+    wpe = _bf(torch.randn(128, C, device=gpu)).requires_grad_()
+    x = ops.embed(idx, wte, wpe)
+    w32, p32 = wte.detach().float().requires_grad_(), wpe.detach().float().requires_grad_()
+    xr = F.embedding(idx, w32) + p32[:T]
+    assert torch.allclose(x.float(), xr, atol=2e-2, rtol=1e-2)
+    dy = torch.randn_like(xr)
+    (x.float() * dy).sum().backward()
+    (xr * dy).sum().backward()
+    assert torch.allclose(wte.grad.float(), w32.grad, atol=5e-2, rtol=2e-2)
+    assert torch.allclose(wpe.grad.float(), p32.grad, atol=5e-2, rtol=2e-2)
