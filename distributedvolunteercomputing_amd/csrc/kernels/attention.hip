@@ -57,6 +57,30 @@ __device__ __forceinline__ sx8 vt_frag(const bf16* tile, int ld, int key0, int d
   return sx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// XOR-swizzled [rows][64] bf16 LDS tile (no padding): 16-B chunk c of row r is stored at chunk
+// c ^ g((r >> 1) & 7), g(k) = ((k & 1) << 2) | (k >> 1). Even and odd rows fall in opposite
+// 128-B halves of the 256-B bank row; g is a bijection on 0..7 (16 consecutive rows of one
+// chunk -> 16 distinct 4-bank slots: ds_read_b128 row reads conflict-free) and g(2m), g(2m+1)
+// differ in bit 2 (the 4 rows x 4 chunks of a half-wave ds_read_b64_tr_b16 hit 64 distinct
+// banks). One image serves both the row-operand reads and the transposed reads.
+__device__ __forceinline__ int swz(int r, int chunk) {
+  const int k = (r >> 1) & 7;
+  return r * 64 + ((chunk ^ (((k & 1) << 2) | (k >> 1))) << 3);
+}
+
+__device__ __forceinline__ sx8 row_frag_swz(const bf16* tile, int row, int s, int h) {
+  return *(const sx8*)(tile + swz(row, 2 * s + h));
+}
+
+__device__ __forceinline__ sx8 vt_frag_swz(const bf16* tile, int key0, int dtile, int s, int lane) {
+  const int h = lane >> 5, g = lane >> 4, lig = lane & 15, p = lig & 3;
+  const int chunk = dtile * 4 + (g & 1) * 2 + (p >> 1);
+  const int rb = key0 + 16 * s + 4 * h + (lig >> 2);
+  sx4 lo = lds_tr_b64(tile + swz(rb, chunk) + 4 * (p & 1));
+  sx4 hi = lds_tr_b64(tile + swz(rb + 8, chunk) + 4 * (p & 1));
+  return sx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 // Bijective XCD-aware block remap (cdna guide §5 T1): hardware block b runs on XCD group b % 8;
 // give each group a CONTIGUOUS range of logical blocks so all query tiles of one (batch, head)
 // share that XCD's L2 copy of K/V.
@@ -235,8 +259,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __rest
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                                int B, int T, int H, float scale, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 sK[2][A_BK * KLD];
-  __shared__ __attribute__((aligned(16))) bf16 sV[2][A_BK * KLD];
+  __shared__ __attribute__((aligned(16))) bf16 sK[2][A_BK * AD];  // swizzled (swz)
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][A_BK * AD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
   const int nqt = (T + A_BQ - 1) / A_BQ;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -275,8 +299,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __rest
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
-      *(sx8*)(&sK[buf][r * KLD + c]) = rk[i];
-      *(sx8*)(&sV[buf][r * KLD + c]) = rv[i];
+      (void)c;
+      *(sx8*)(&sK[buf][swz(r, e & 7)]) = rk[i];
+      *(sx8*)(&sV[buf][swz(r, e & 7)]) = rv[i];
     }
   };
   gload(0);
@@ -289,13 +314,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __rest
     for (int sub = 0; sub < 2; ++sub) {
       const int kb = kt * A_BK + sub * 32;
       if (kb > qw + 31) continue;
-      const bf16* kl = &sK[cur][(sub * 32) * KLD];
-      const bf16* vl = &sV[cur][(sub * 32) * KLD];
       f32x16 st = {}, dp = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        st = mfma32(*(const sx8*)(kl + col * KLD + 16 * s + 8 * h2), qf[s], st);
-        dp = mfma32(*(const sx8*)(vl + col * KLD + 16 * s + 8 * h2), df[s], dp);
+        st = mfma32(row_frag_swz(&sK[cur][0], sub * 32 + col, s, h2), qf[s], st);
+        dp = mfma32(row_frag_swz(&sV[cur][0], sub * 32 + col, s, h2), df[s], dp);
       }
       const bool diag = kb + 31 > qw;
 #pragma unroll
@@ -312,8 +335,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __rest
         sx8 db;
 #pragma unroll
         for (int j = 0; j < 8; ++j) db[j] = bf16_bits(st[8 * s + j]);
-        a0 = mfma32(vt_frag(&sK[cur][0], KLD, sub * 32, 0, s, lane), db, a0);
-        a1 = mfma32(vt_frag(&sK[cur][0], KLD, sub * 32, 1, s, lane), db, a1);
+        a0 = mfma32(vt_frag_swz(&sK[cur][0], sub * 32, 0, s, lane), db, a0);
+        a1 = mfma32(vt_frag_swz(&sK[cur][0], sub * 32, 1, s, lane), db, a1);
       }
     }
     if (kt + 1 < nkt) sstore(cur ^ 1);
@@ -346,8 +369,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __re
                                                                  const float* __restrict__ delta,
                                                                  bf16* __restrict__ dqkv, int B, int T, int H,
                                                                  float scale, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 sQ[2][B_BQ * KLD];
-  __shared__ __attribute__((aligned(16))) bf16 sD[2][B_BQ * KLD];
+  __shared__ __attribute__((aligned(16))) bf16 sQ[2][B_BQ * AD];  // swizzled (swz)
+  __shared__ __attribute__((aligned(16))) bf16 sD[2][B_BQ * AD];
   __shared__ __attribute__((aligned(16))) float sL[2][B_BQ];
   __shared__ __attribute__((aligned(16))) float sDel[2][B_BQ];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
@@ -392,8 +415,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __re
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
-      *(sx8*)(&sQ[buf][r * KLD + c]) = rq[i];
-      *(sx8*)(&sD[buf][r * KLD + c]) = rd[i];
+      (void)c;
+      *(sx8*)(&sQ[buf][swz(r, e & 7)]) = rq[i];
+      *(sx8*)(&sD[buf][swz(r, e & 7)]) = rd[i];
     }
     if (tid < B_BQ) {
       sL[buf][tid] = rl;
@@ -410,13 +434,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __re
     for (int sub = 0; sub < 2; ++sub) {
       const int qb = qt * B_BQ + sub * 32;
       if (qb + 31 < kw) continue;  // every query before this wave's first key
-      const bf16* ql = &sQ[cur][(sub * 32) * KLD];
-      const bf16* dl = &sD[cur][(sub * 32) * KLD];
       f32x16 st = {}, dp = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        st = mfma32(*(const sx8*)(ql + col * KLD + 16 * s + 8 * h2), kf[s], st);
-        dp = mfma32(*(const sx8*)(dl + col * KLD + 16 * s + 8 * h2), vf[s], dp);
+        st = mfma32(row_frag_swz(&sQ[cur][0], sub * 32 + col, s, h2), kf[s], st);
+        dp = mfma32(row_frag_swz(&sD[cur][0], sub * 32 + col, s, h2), vf[s], dp);
       }
       const bool diag = qb < kw + 31;
       f32x16 pp;
@@ -443,10 +465,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __re
           pb[j] = bf16_bits(pp[8 * s + j]);
           sb[j] = bf16_bits(st[8 * s + j]);
         }
-        dv0 = mfma32(vt_frag(&sD[cur][0], KLD, sub * 32, 0, s, lane), pb, dv0);
-        dv1 = mfma32(vt_frag(&sD[cur][0], KLD, sub * 32, 1, s, lane), pb, dv1);
-        dk0 = mfma32(vt_frag(&sQ[cur][0], KLD, sub * 32, 0, s, lane), sb, dk0);
-        dk1 = mfma32(vt_frag(&sQ[cur][0], KLD, sub * 32, 1, s, lane), sb, dk1);
+        dv0 = mfma32(vt_frag_swz(&sD[cur][0], sub * 32, 0, s, lane), pb, dv0);
+        dv1 = mfma32(vt_frag_swz(&sD[cur][0], sub * 32, 1, s, lane), pb, dv1);
+        dk0 = mfma32(vt_frag_swz(&sQ[cur][0], sub * 32, 0, s, lane), sb, dk0);
+        dk1 = mfma32(vt_frag_swz(&sQ[cur][0], sub * 32, 1, s, lane), sb, dk1);
       }
     }
     if (qt + 1 < nqt) sstore(cur ^ 1);

@@ -6,12 +6,13 @@ north-star training model.
 
 MI355X-first choices:
 * bf16 weights/activations, fp32 master weights live in the optimizer (flat buffers);
-* every LayerNorm is fused with the residual add that precedes it (one HIP kernel reads the
-  residual stream once and writes both the new residual and the normalised activations);
-* tanh-GELU and the vocab-wide softmax cross-entropy are HIP kernels; the cross-entropy
-  backward writes the logit gradient in place;
-* GEMMs are plain library GEMMs (hipBLASLt via torch.nn.functional.linear) and attention is
-  torch's fused SDPA kernel;
+* every LayerNorm is fused with the residual add that precedes it AND with the bias of the
+  GEMM that produced the branch (one HIP kernel reads the residual stream once and writes
+  the new residual and the normalised activations; its backward also emits that bias's grad);
+* fc bias + tanh-GELU, the token+position embedding, and the vocab-wide softmax
+  cross-entropy are HIP kernels; the cross-entropy backward writes the logit gradient in place;
+* causal attention (head dim 64) is the HIP flash-attention kernel on the packed qkv layout
+  (no permute/cat copies); GEMMs are library GEMMs (hipBLASLt/rocBLAS via TunableOp tables);
 * vocabulary padded to a multiple of 128 (50257 -> 50304) so the LM-head GEMM tiles cleanly;
   padded logits are masked inside the loss kernel.
 """
