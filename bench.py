@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--H", type=int, default=4)
     ap.add_argument("--algo", default="rccl", choices=["rccl", "rs_ag", "butterfly", "ring"])
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--graph", type=int, default=0, help="1: replay each local step as one hipGraph")
+    ap.add_argument("--graph", type=int, default=1, help="1: replay each local step as one hipGraph, 0: eager")
     return ap.parse_args()
 
 
@@ -87,9 +87,15 @@ def main():
             group.barrier()
 
     w0 = 0
+    graphed = False
     if a.graph and cuda:
         w0 = min(3, a.warmup)
-        trainer.capture(*batch(0), warmup=w0)  # w0 real steps, then hipGraph capture
+        try:
+            trainer.capture(*batch(0), warmup=w0)  # w0 real steps, then hipGraph capture
+            graphed = True
+        except Exception as e:  # stay correct if capture is refused: eager steps instead
+            print(f"[bench] hipGraph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
+            trainer.graph = None
     for i in range(w0, a.warmup):
         trainer.step(*batch(i))
     sync_all()
@@ -135,7 +141,7 @@ def main():
             "final_loss": round(loss, 4),
             "sync_ms": round(trainer.last_sync_ms, 3),
             "tuned_gemms": TUNED_GEMMS,
-            "hipgraph": bool(a.graph and cuda),
+            "hipgraph": graphed,
         }
         line = json.dumps(rec)
         print(line, flush=True)

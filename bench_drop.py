@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Step time under a 1-peer drop: the second half of the BASELINE.json metric
+("samples/sec GPT-2-small local-SGD at 1/2/4/8 peers; step-time under 1-peer drop").
+
+    python bench_drop.py --peers P [--model gpt2] [--batch 64] [--steps 24] [--warmup 8] [--lease 1.0]
+
+This process plays the coordinator: it hosts the rendezvous store (so no peer is special and
+any peer may die) and starts P peer processes, one per visible GPU (round-robin when P exceeds
+the GPUs; RCCL does not run two ranks on one device, so peers sharing a GPU use gloo). Every
+peer runs the elastic local-SGD trainer (parallel/elastic.py + parallel/local_sgd.py). At step
+``--drop-at`` (default: mid-window, between two averaging rounds) peer ``--drop-peer`` crashes
+without a goodbye (heartbeat stops, process exits). The survivors notice at their next
+averaging round (lease expiry), agree on the next generation, build a fresh process group and
+go on. Every peer times each step (device-synchronised); the launcher prints ONE JSON line
+with the step time before the drop, across the window that contains it, after it, and the
+stall of the round that absorbed the detection and regroup.
+
+Reference analog: the reference has no failure handling (a dead volunteer hangs the job,
+SURVEY.md §5.3); this measures the replacement.
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--peers", type=int, default=2)
+    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--H", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=24, help="timed window (contains the drop)")
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--drop-at", type=int, default=None, help="step at which the peer dies (default: mid-window)")
+    ap.add_argument("--drop-peer", type=int, default=None, help="default: the last peer")
+    ap.add_argument("--lease", type=float, default=1.0, help="heartbeat lease (s) after which a silent peer is dead")
+    ap.add_argument("--backend", default=None, choices=[None, "nccl", "gloo"])
+    ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--timeout", type=float, default=900.0)
+    ap.add_argument("--json-out", default=None)
+    # internal (peer processes)
+    ap.add_argument("--peer", type=int, default=None)
+    ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("--out", default=None)
+    return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------- peer
+def peer_main(a):
+    from distributedvolunteercomputing_amd.utils.tuning import enable_tuned_gemms
+
+    ngpu = int(os.environ.get("VCX_DROP_NGPU", "0"))
+    local = a.peer % ngpu if ngpu else 0
+    enable_tuned_gemms(local)
+    import torch
+    import torch.distributed as dist
+
+    from distributedvolunteercomputing_amd.models.gpt2 import GPT2, GPT2Config
+    from distributedvolunteercomputing_amd.parallel.elastic import ElasticMembership
+    from distributedvolunteercomputing_amd.parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer
+
+    cuda = ngpu > 0
+    device = torch.device("cuda", local) if cuda else torch.device("cpu")
+    if cuda:
+        torch.cuda.set_device(device)
+    backend = a.backend or ("nccl" if cuda and ngpu >= a.peers else "gloo")
+    store = dist.TCPStore("127.0.0.1", a.port, None, False, timeout=datetime.timedelta(seconds=300),
+                          wait_for_workers=False)
+    mem = ElasticMembership(store, a.peer, backend=backend, device=device, lease_s=a.lease,
+                            heartbeat_s=max(a.lease / 10, 0.02))
+    mem.bootstrap(list(range(a.peers)))
+    cfg = GPT2Config.preset(a.model)
+    cfg.n_ctx = max(cfg.n_ctx, a.seq)
+    torch.manual_seed(0)
+    dtype = torch.bfloat16 if cuda else torch.float32
+    model = GPT2(cfg).to(device=device, dtype=dtype)
+    tcfg = LocalSGDConfig(H=a.H, comm_dtype=dtype)
+    tr = LocalSGDTrainer(model, tcfg, membership=mem, device=device)
+    g = torch.Generator(device=device).manual_seed(1000 + a.peer)
+    pool = [torch.randint(0, cfg.vocab_size, (a.batch, a.seq + 1), device=device, generator=g) for _ in range(4)]
+
+    def batch(i):
+        b = pool[i % len(pool)]
+        return b[:, :-1], b[:, 1:]
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    w0 = 0
+    if a.graph and cuda:
+        w0 = min(3, a.warmup)
+        tr.capture(*batch(0), warmup=w0)
+    for i in range(w0, a.warmup):
+        tr.step(*batch(i))
+    sync()
+    mem.group.barrier()
+    timeline = []
+    for i in range(a.warmup, a.warmup + a.steps):
+        if a.peer == a.drop_peer and i == a.drop_at:
+            print(f"[peer {a.peer}] fault injection: crashing at step {i}", flush=True)
+            mem.stop_heartbeat()
+            os._exit(0)  # no leave(): the survivors must detect the silence
+        t0 = time.perf_counter()
+        st = tr.step(*batch(i))
+        sync()
+        timeline.append({"step": i, "ms": (time.perf_counter() - t0) * 1e3, "synced": bool(st.synced),
+                         "members": st.members, "gen": mem.gen, "sync_ms": st.sync_ms if st.synced else 0.0})
+    with open(os.path.join(a.out, f"peer{a.peer}.json"), "w") as f:
+        json.dump({"peer": a.peer, "backend": backend, "timeline": timeline, "events": mem.events}, f)
+    mem.stop_heartbeat()
+    return 0
+
+
+# ----------------------------------------------------------------------------- launcher
+def launcher(a):
+    import torch
+    import torch.distributed as dist
+
+    ngpu = torch.cuda.device_count()  # does not initialise the GPU in this process
+    if a.drop_peer is None:
+        a.drop_peer = a.peers - 1
+    if a.drop_at is None:
+        a.drop_at = a.warmup + a.steps // 2 + (1 if a.H > 1 else 0)
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    store = dist.TCPStore("127.0.0.1", port, None, True, timeout=datetime.timedelta(seconds=300),
+                          wait_for_workers=False)
+    out = tempfile.mkdtemp(prefix="vcx_drop_")
+    env = dict(os.environ, VCX_DROP_NGPU=str(ngpu), PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    common = [sys.executable, os.path.abspath(__file__), "--peers", str(a.peers), "--model", a.model,
+              "--batch", str(a.batch), "--seq", str(a.seq), "--H", str(a.H), "--steps", str(a.steps),
+              "--warmup", str(a.warmup), "--drop-at", str(a.drop_at), "--drop-peer", str(a.drop_peer),
+              "--lease", str(a.lease), "--graph", str(a.graph), "--port", str(port), "--out", out]
+    if a.backend:
+        common += ["--backend", a.backend]
+    procs = [subprocess.Popen(common + ["--peer", str(r)], env=env) for r in range(a.peers)]
+    t_end = time.time() + a.timeout
+    rc = {}
+    while len(rc) < len(procs) and time.time() < t_end:
+        for r, p in enumerate(procs):
+            if r not in rc and p.poll() is not None:
+                rc[r] = p.returncode
+        time.sleep(0.2)
+    for r, p in enumerate(procs):
+        if r not in rc:
+            p.kill()
+            rc[r] = "timeout"
+    bad = {r: c for r, c in rc.items() if c != 0}
+    if bad:
+        print(f"[bench_drop] peers failed: {bad}", file=sys.stderr)
+        return 1
+    survivors = [r for r in range(a.peers) if r != a.drop_peer]
+    tl = {}
+    backend = None
+    for r in survivors:
+        with open(os.path.join(out, f"peer{r}.json")) as f:
+            d = json.load(f)
+        backend = d["backend"]
+        for e in d["timeline"]:
+            cur = tl.setdefault(e["step"], dict(e))
+            cur["ms"] = max(cur["ms"], e["ms"])  # a step ends when its slowest survivor is done
+    steps = sorted(tl)
+    before = [tl[s]["ms"] for s in steps if s < a.drop_at]
+    regroup = next((s for s in steps if s >= a.drop_at and tl[s]["members"] == a.peers - 1 and tl[s]["synced"]), None)
+    after = [tl[s]["ms"] for s in steps if regroup is not None and s > regroup]
+    window = [tl[s]["ms"] for s in steps]
+    mean = lambda xs: sum(xs) / len(xs) if xs else float("nan")  # noqa: E731
+    # the stall: the averaging call that detected the silent peer (lease wait + agreement + new
+    # process group + first collective on it) against a steady averaging call before the drop
+    steady_sync = mean([tl[s]["sync_ms"] for s in steps if s < a.drop_at and tl[s]["synced"]])
+    regroup_sync = tl[regroup]["sync_ms"] if regroup is not None else float("nan")
+    rec = {
+        "metric": "step-time under 1-peer drop, GPT-2-small local-SGD",
+        "value": round(mean(window), 3),
+        "unit": "ms/step",
+        "n_gpus": min(ngpu, a.peers) if ngpu else 0,
+        "peers": a.peers,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "higher_is_better": False,
+        "dtype": "bf16" if ngpu else "fp32",
+        "data": "synthetic (random tokens, random-init weights)",
+        "config": {"model": a.model, "per_peer_batch": a.batch, "seq_len": a.seq, "H": a.H,
+                   "backend": backend, "lease_s": a.lease, "drop_at": a.drop_at, "drop_peer": a.drop_peer},
+        "ms_per_step_before": round(mean(before), 3),
+        "ms_per_step_after": round(mean(after), 3),
+        "regroup_step": regroup,
+        "steady_sync_ms": round(steady_sync, 3),
+        "regroup_sync_ms": round(regroup_sync, 3),
+        "drop_stall_ms": round(regroup_sync - steady_sync, 3),
+        "samples_per_s_before": round(a.peers * a.batch / mean(before) * 1e3, 2),
+        "samples_per_s_after": round((a.peers - 1) * a.batch / mean(after) * 1e3, 2) if after else None,
+    }
+    line = json.dumps(rec)
+    print(line, flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(line + "\n")
+    del store
+    return 0
+
+
+def main(argv=None):
+    a = parse(argv)
+    if a.peer is not None:
+        return peer_main(a)
+    return launcher(a)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

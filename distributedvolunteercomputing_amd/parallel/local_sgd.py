@@ -98,20 +98,23 @@ class LocalSGDTrainer:
         kernel launches; the averaging round stays outside the graph (collective,
         membership). x/y shapes are fixed from here on. Runs `warmup` real steps first."""
         assert x.is_cuda, "graph capture needs GPU tensors"
+        self.graph = None
         self._gx = x.clone()
         self._gy = y.clone()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for _ in range(warmup):
-                self.forward_backward(self._gx, self._gy)
-                self.optimizer_step()
-                self.t += 1
+            for _ in range(warmup):  # real steps (eager; an H boundary still averages)
+                self.step(self._gx, self._gy)
         torch.cuda.current_stream().wait_stream(s)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        # thread_local: a process-group watchdog thread querying its events during capture
+        # must not invalidate it
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             self._gloss = self.forward_backward(self._gx, self._gy)
             self.optimizer_step()
+        self.graph = graph
         return self
 
     def step(self, x, y) -> StepStats:

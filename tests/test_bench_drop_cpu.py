@@ -1,0 +1,23 @@
+"""bench_drop.py end to end on CPU/gloo: 3 peers, one crashes mid-window, the survivors
+detect it by lease expiry, regroup and finish; the launcher reports the drop metrics."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_drop_three_peers_one_crash(tmp_path):
+    out = tmp_path / "drop.json"
+    env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, os.path.join(ROOT, "bench_drop.py"), "--peers", "3", "--model", "gpt2-tiny", "--batch", "2",
+           "--seq", "32", "--steps", "14", "--warmup", "2", "--lease", "0.5", "--json-out", str(out), "--timeout", "240"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads(out.read_text())
+    assert rec["peers"] == 3 and rec["higher_is_better"] is False
+    assert rec["regroup_step"] is not None and rec["regroup_step"] >= rec["config"]["drop_at"]
+    # the regroup waited at least one lease for the silent peer
+    assert rec["regroup_sync_ms"] >= 0.5 * 1e3 * 0.9
+    assert rec["ms_per_step_after"] > 0 and rec["samples_per_s_after"] > 0
