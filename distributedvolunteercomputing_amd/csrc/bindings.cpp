@@ -96,6 +96,14 @@ void axpy_bf16(at::Tensor src, at::Tensor acc, double scale) {
   vcx_axpy_bf16(src.data_ptr(), acc.data_ptr(), src.numel(), (float)scale, cur_stream());
 }
 
+void splitk_reduce(at::Tensor part, at::Tensor acc, bool accumulate) {
+  CHECK_IN(part, kBF);
+  CHECK_IN(acc, kBF);
+  const int64_t n = acc.numel();
+  TORCH_CHECK(n % 8 == 0 && part.numel() % n == 0, "splitk_reduce: part must be [S, acc.numel()], numel % 8 == 0");
+  vcx_splitk_reduce(part.data_ptr(), acc.data_ptr(), (int)(part.numel() / n), n, accumulate ? 1 : 0, cur_stream());
+}
+
 // ------------------------------------------------------------------ norms / activations
 std::vector<at::Tensor> ln_fwd(at::Tensor a, c10::optional<at::Tensor> b, at::Tensor w, c10::optional<at::Tensor> bias,
                                double eps, bool rms, c10::optional<at::Tensor> bb) {
@@ -327,6 +335,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lsgd_apply", &lsgd_apply);
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("axpy_bf16", &axpy_bf16);
+  m.def("splitk_reduce", &splitk_reduce);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
   m.def("gelu_fwd", &gelu_fwd);

@@ -18,6 +18,8 @@
 // 16 distinct 4-bank slots); V rows padded to 96 bf16 (192 B: the 4 rows x 32 columns of a
 // half-wave ds_read_b64_tr_b16 hit disjoint banks). K/V tiles are double-buffered and staged
 // through registers (issue next tile's global loads before the MFMAs, write LDS after).
+#include <type_traits>
+
 #include "vcx_common.h"
 
 namespace vcx {
@@ -31,6 +33,9 @@ constexpr int A_BK = 64;       // keys per LDS tile
 constexpr int KLD = 72;        // K tile row stride (elements)
 constexpr int VLD = 96;        // V tile row stride (elements)
 constexpr float LOG2E = 1.4426950408889634f;
+
+using I0 = std::integral_constant<int, 0>;
+using I1 = std::integral_constant<int, 1>;
 
 __device__ __forceinline__ sx4 lds_tr_b64(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sx4*)(p));
@@ -91,7 +96,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 }
 
 // ============================================================================ forward
-__global__ void __launch_bounds__(256) attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                             float* __restrict__ lse, int B, int T, int H,
                                                             float scale_log2) {
   __shared__ __attribute__((aligned(16))) bf16 sK[2][A_BK * KLD];
@@ -143,73 +148,95 @@ __global__ void __launch_bounds__(256) attn_fwd_d64_kernel(const bf16* __restric
     }
   };
 
+  // one 64-key tile; MASK only on the (at most two) tiles that cross this block's diagonal.
+  // Keys >= T need no test of their own: for every stored query q < T they satisfy key > q.
+  auto tile = [&](int kt, auto cur_c, auto mask_c) {
+    constexpr int cur = decltype(cur_c)::value;  // LDS buffer: compile-time -> immediate offsets
+    constexpr bool MASK = decltype(mask_c)::value;
+    const int kb = kt * A_BK;
+    if (MASK && kb > qw + 31) return;  // wave-uniform: every query of this wave precedes these keys
+    const bf16* kl = &sK[cur][0];
+    // two independent 32-key score tiles (interleaved MFMA chains)
+    f32x16 s0 = {}, s1 = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s0 = mfma32(*(const sx8*)(kl + col * KLD + 16 * s + 8 * h2), qf[s], s0);
+      s1 = mfma32(*(const sx8*)(kl + (32 + col) * KLD + 16 * s + 8 * h2), qf[s], s1);
+    }
+    if (MASK) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
+        s0[r] = key > q ? -INFINITY : s0[r];
+        s1[r] = key + 32 > q ? -INFINITY : s1[r];
+      }
+    }
+    // raw-score max (scale > 0 commutes with max); the scale is folded into one FMA per score
+    float mx = fmaxf(s0[0], s1[0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
+    // deferred rescale (cdna guide T13): keep the running max unless it grew by > 8 (P <= 2^8,
+    // safe in fp32 accumulation and bf16 P), saving the O-wide multiply on most tiles
+    if (!__all(mx - m <= 8.f)) {
+      const float mnew = fmaxf(m, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);  // m = -inf on the first tile -> 0
+      l *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        o0[r] *= alpha;
+        o1[r] *= alpha;
+      }
+      m = mnew;
+    }
+    const float mneg = -m;
+    float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p0 = __builtin_amdgcn_exp2f(fmaf(s0[r], scale_log2, mneg));
+      const float p1 = __builtin_amdgcn_exp2f(fmaf(s1[r], scale_log2, mneg));
+      s0[r] = p0;
+      s1[r] = p1;
+      ps0 += p0;
+      ps1 += p1;
+    }
+    const float ps = ps0 + ps1;
+    l += ps + __shfl_xor(ps, 32, 64);
+    // P^T (bf16) as the B operand: 4 k-steps of 16 keys (registers 8s .. 8s+7 of s0 / s1)
+    const bf16* vl = &sV[cur][0];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const f32x16& sp = (s < 2) ? s0 : s1;
+      sx8 pb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[j] = bf16_bits(sp[8 * (s & 1) + j]);
+      o0 = mfma32(vt_frag(vl, VLD, (s >> 1) * 32, 0, s & 1, lane), pb, o0);
+      o1 = mfma32(vt_frag(vl, VLD, (s >> 1) * 32, 1, s & 1, lane), pb, o1);
+    }
+  };
+
   gload(0);
   sstore(0);
   __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
+  const int kdiag = q0 / A_BK;  // first tile that can hold a key > some query of this block
+  auto step = [&](int kt, auto cur_c, auto mask_c) {
+    constexpr int cur = decltype(cur_c)::value;
     if (kt + 1 < nkt) gload(kt + 1);
-    const int kb = kt * A_BK;
-    if (kb <= qw + 31) {  // wave-uniform: otherwise every query of this wave precedes these keys
-      const bf16* kl = &sK[cur][0];
-      // two independent 32-key score tiles (interleaved MFMA chains)
-      f32x16 s0 = {}, s1 = {};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        s0 = mfma32(*(const sx8*)(kl + col * KLD + 16 * s + 8 * h2), qf[s], s0);
-        s1 = mfma32(*(const sx8*)(kl + (32 + col) * KLD + 16 * s + 8 * h2), qf[s], s1);
-      }
-      float mx = -INFINITY;
-      const bool diag = kb + 63 > qw;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float x0 = s0[r] * scale_log2, x1 = s1[r] * scale_log2;
-        if (diag) {
-          const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
-          if (key > q || key >= T) x0 = -INFINITY;
-          if (key + 32 > q || key + 32 >= T) x1 = -INFINITY;
-        }
-        s0[r] = x0;
-        s1[r] = x1;
-        mx = fmaxf(mx, fmaxf(x0, x1));
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      // deferred rescale (cdna guide T13): keep the running max unless it grew by > 8 (P <= 2^8,
-      // safe in fp32 accumulation and bf16 P), saving the O-wide multiply on most tiles
-      if (!__all(mx - m <= 8.f)) {
-        const float mnew = fmaxf(m, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m - mnew);  // m = -inf on the first tile -> 0
-        l *= alpha;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          o0[r] *= alpha;
-          o1[r] *= alpha;
-        }
-        m = mnew;
-      }
-      float ps = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p0 = __builtin_amdgcn_exp2f(s0[r] - m), p1 = __builtin_amdgcn_exp2f(s1[r] - m);
-        s0[r] = p0;
-        s1[r] = p1;
-        ps += p0 + p1;
-      }
-      l += ps + __shfl_xor(ps, 32, 64);
-      // P^T (bf16) as the B operand: 4 k-steps of 16 keys (registers 8s .. 8s+7 of s0 / s1)
-      const bf16* vl = &sV[cur][0];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const f32x16& sp = (s < 2) ? s0 : s1;
-        sx8 pb;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pb[j] = bf16_bits(sp[8 * (s & 1) + j]);
-        o0 = mfma32(vt_frag(vl, VLD, (s >> 1) * 32, 0, s & 1, lane), pb, o0);
-        o1 = mfma32(vt_frag(vl, VLD, (s >> 1) * 32, 1, s & 1, lane), pb, o1);
-      }
-    }
+    tile(kt, cur_c, mask_c);
     if (kt + 1 < nkt) sstore(cur ^ 1);
     __syncthreads();
+  };
+  int kt = 0;
+  for (; kt + 1 < kdiag; kt += 2) {  // unrolled by two so the LDS buffer is a constant
+    step(kt, I0{}, std::false_type{});
+    step(kt + 1, I1{}, std::false_type{});
+  }
+  if (kt < kdiag) step(kt++, I0{}, std::false_type{});
+  for (; kt < nkt; ++kt) {  // the (at most two) diagonal tiles
+    if (kt & 1)
+      step(kt, I1{}, std::true_type{});
+    else
+      step(kt, I0{}, std::true_type{});
   }
   if (q < T) {
     const float inv = 1.f / l;
@@ -255,7 +282,7 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const bf16* __restr
 // dQ (query-parallel; same tiling as the forward): per 32-key sub-tile
 //   S^T = K Q^T, P^T = exp2(S^T c - lse), dP^T = V dO^T, dS^T = P^T (dP^T - delta),
 //   dQ^T += K^T dS^T  (A = K^T through ds_read_b64_tr_b16, B = dS^T from the accumulator)
-__global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_bwd_dq_d64_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                                int B, int T, int H, float scale, float scale_log2) {
@@ -280,7 +307,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __rest
     qf[s] = *(const sx8*)(base + (int64_t)qc * tok + 16 * s + 8 * h2);
     df[s] = *(const sx8*)(dOb + (int64_t)qc * otok + 16 * s + 8 * h2);
   }
-  const float lq = lse[((int64_t)b * H + hh) * T + qc];
+  const float nlq = -lse[((int64_t)b * H + hh) * T + qc];
   const float dq_delta = delta[((int64_t)b * H + hh) * T + qc];
   f32x16 a0 = {}, a1 = {};
   const int kend = min(T, q0 + A_BQ);
@@ -304,29 +331,26 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __rest
       *(sx8*)(&sV[buf][swz(r, e & 7)]) = rv[i];
     }
   };
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nkt) gload(kt + 1);
+  // one 64-key tile (two 32-key sub-tiles); MASK only on the tiles crossing the diagonal
+  auto tile = [&](int kt, auto cur_c, auto mask_c) {
+    constexpr int cur = decltype(cur_c)::value;  // LDS buffer: compile-time -> immediate offsets
+    constexpr bool MASK = decltype(mask_c)::value;
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const int kb = kt * A_BK + sub * 32;
-      if (kb > qw + 31) continue;
+      if (MASK && kb > qw + 31) continue;
       f32x16 st = {}, dp = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         st = mfma32(row_frag_swz(&sK[cur][0], sub * 32 + col, s, h2), qf[s], st);
         dp = mfma32(row_frag_swz(&sV[cur][0], sub * 32 + col, s, h2), df[s], dp);
       }
-      const bool diag = kb + 31 > qw;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = __builtin_amdgcn_exp2f(st[r] * scale_log2 - lq);
-        if (diag) {
+        float p = __builtin_amdgcn_exp2f(fmaf(st[r], scale_log2, nlq));
+        if (MASK) {
           const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
-          if (key > q || key >= T) p = 0.f;
+          p = key > q ? 0.f : p;
         }
         st[r] = p * (dp[r] - dq_delta);  // dS^T
       }
@@ -339,8 +363,29 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __rest
         a1 = mfma32(vt_frag_swz(&sK[cur][0], sub * 32, 1, s, lane), db, a1);
       }
     }
+  };
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int kdiag = q0 / A_BK;
+  auto step = [&](int kt, auto cur_c, auto mask_c) {
+    constexpr int cur = decltype(cur_c)::value;
+    if (kt + 1 < nkt) gload(kt + 1);
+    tile(kt, cur_c, mask_c);
     if (kt + 1 < nkt) sstore(cur ^ 1);
     __syncthreads();
+  };
+  int kt = 0;
+  for (; kt + 1 < kdiag; kt += 2) {  // unrolled by two so the LDS buffer is a constant
+    step(kt, I0{}, std::false_type{});
+    step(kt + 1, I1{}, std::false_type{});
+  }
+  if (kt < kdiag) step(kt++, I0{}, std::false_type{});
+  for (; kt < nkt; ++kt) {  // the (at most two) diagonal tiles
+    if (kt & 1)
+      step(kt, I1{}, std::true_type{});
+    else
+      step(kt, I0{}, std::true_type{});
   }
   if (q < T) {
     bf16* row = dqkv + ((int64_t)b * T + q) * tok + hh * AD;  // slot 0 = dQ
@@ -363,7 +408,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_d64_kernel(const bf16* __rest
 //   B operands = the bf16-converted accumulators; the keys stay on the lanes throughout)
 constexpr int B_BQ = 64;  // queries per LDS tile
 
-__global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __restrict__ qkv,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_bwd_dkdv_d64_kernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ lse,
                                                                  const float* __restrict__ delta,
@@ -405,10 +450,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __re
       rq[i] = *(const sx8*)(base + (int64_t)qq * tok + c);
       rd[i] = *(const sx8*)(dOb + (int64_t)qq * otok + c);
     }
-    if (tid < B_BQ) {
-      const int qq = min(qt * B_BQ + tid, T - 1);
-      rl = lrow[qq];
-      rdl = drow[qq];
+    if (tid < B_BQ) {  // -lse (so P = exp2(S c + nl)); -inf for rows past T: their P is 0
+      const int qq = qt * B_BQ + tid;
+      rl = qq < T ? -lrow[qq] : -INFINITY;
+      rdl = drow[min(qq, T - 1)];
     }
   };
   auto sstore = [&](int buf) {
@@ -424,23 +469,21 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __re
       sDel[buf][tid] = rdl;
     }
   };
-  gload(qstart);
-  sstore(0);
-  __syncthreads();
-  for (int qt = qstart; qt < nqt; ++qt) {
-    const int cur = (qt - qstart) & 1;
-    if (qt + 1 < nqt) gload(qt + 1);
+  // one 64-query tile (two 32-query sub-tiles); MASK only on the two tiles that cross this
+  // block's diagonal. Rows past T carry -inf in sL (P = 0) and keys past T are never stored.
+  auto tile = [&](int qt, auto cur_c, auto mask_c) {
+    constexpr int cur = decltype(cur_c)::value;
+    constexpr bool MASK = decltype(mask_c)::value;
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const int qb = qt * B_BQ + sub * 32;
-      if (qb + 31 < kw) continue;  // every query before this wave's first key
+      if (MASK && qb + 31 < kw) continue;  // every query before this wave's first key
       f32x16 st = {}, dp = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         st = mfma32(row_frag_swz(&sQ[cur][0], sub * 32 + col, s, h2), kf[s], st);
         dp = mfma32(row_frag_swz(&sD[cur][0], sub * 32 + col, s, h2), vf[s], dp);
       }
-      const bool diag = qb < kw + 31;
       f32x16 pp;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -450,9 +493,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __re
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * g + i;
-          const int qq = qb + 8 * g + 4 * h2 + i;
-          float p = __builtin_amdgcn_exp2f(st[r] * scale_log2 - lv[i]);
-          if ((diag && key > qq) || qq >= T || key >= T) p = 0.f;
+          float p = __builtin_amdgcn_exp2f(fmaf(st[r], scale_log2, lv[i]));
+          if (MASK) {
+            const int qq = qb + 8 * g + 4 * h2 + i;
+            p = key > qq ? 0.f : p;
+          }
           pp[r] = p;
           st[r] = p * (dp[r] - dv[i]);  // dS
         }
@@ -471,9 +516,26 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_d64_kernel(const bf16* __re
         dk1 = mfma32(vt_frag_swz(&sQ[cur][0], sub * 32, 1, s, lane), sb, dk1);
       }
     }
+  };
+  gload(qstart);
+  sstore(0);
+  __syncthreads();
+  auto step = [&](int qt, auto cur_c, auto mask_c) {
+    constexpr int cur = decltype(cur_c)::value;
+    if (qt + 1 < nqt) gload(qt + 1);
+    tile(qt, cur_c, mask_c);
     if (qt + 1 < nqt) sstore(cur ^ 1);
     __syncthreads();
+  };
+  // queries k0 .. k0+127 (tiles qstart, qstart+1) cross the diagonal; later tiles are unmasked
+  step(qstart, I0{}, std::true_type{});
+  if (qstart + 1 < nqt) step(qstart + 1, I1{}, std::true_type{});
+  int qt = qstart + 2;
+  for (; qt + 1 < nqt; qt += 2) {  // unrolled by two so the LDS buffer is a constant
+    step(qt, I0{}, std::false_type{});
+    step(qt + 1, I1{}, std::false_type{});
   }
+  if (qt < nqt) step(qt, I0{}, std::false_type{});
   if (key < T) {
     bf16* rowk = dqkv + ((int64_t)b * T + key) * tok + H * AD + hh * AD;      // slot 1 = dK
     bf16* rowv = dqkv + ((int64_t)b * T + key) * tok + 2 * H * AD + hh * AD;  // slot 2 = dV

@@ -185,6 +185,35 @@ __global__ void __launch_bounds__(256) axpy_bf16_kernel(const bf16* __restrict__
   }
 }
 
+// acc[i] (+)= sum_s part[s * n + i]: the split-M weight-gradient reduction. The S partial
+// products come from ONE batched GEMM over S token chunks (more output tiles in flight than the
+// single K = tokens GEMM); they are summed in fp32 straight into the flat gradient buffer.
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const bf16* __restrict__ part, bf16* __restrict__ acc,
+                                                            int S, int64_t n8, int accumulate) {
+  const int64_t n = n8 * 8;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i * 8;
+    float t[8];
+    if (accumulate) {
+      bf16x8 a = *(const bf16x8*)(acc + b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = (float)a[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = 0.f;
+    }
+    for (int k = 0; k < S; ++k) {
+      bf16x8 v = *(const bf16x8*)(part + k * n + b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] += (float)v[j];
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)t[j];
+    *(bf16x8*)(acc + b) = o;
+  }
+}
+
 }  // namespace vcx
 
 // ---------------------------------------------------------------- launchers
@@ -229,4 +258,10 @@ void vcx_axpy_bf16(const void* src, void* acc, int64_t n, float scale, hipStream
   const int64_t n8 = n / 8;
   hipLaunchKernelGGL(axpy_bf16_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, s, (const bf16*)src,
                      (bf16*)acc, n8, scale);
+}
+
+void vcx_splitk_reduce(const void* part, void* acc, int S, int64_t n, int accumulate, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, s, (const bf16*)part,
+                     (bf16*)acc, S, n8, accumulate);
 }

@@ -14,7 +14,9 @@ MI355X-first choices:
 * causal attention (head dim 64) is the HIP flash-attention kernel on the packed qkv layout
   (no permute/cat copies); GEMMs are library GEMMs (hipBLASLt/rocBLAS via TunableOp tables);
 * vocabulary padded to a multiple of 128 (50257 -> 50304) so the LM-head GEMM tiles cleanly;
-  padded logits are masked inside the loss kernel.
+  padded logits are masked inside the loss kernel;
+* weight gradients are split-M batched GEMMs reduced by a HIP kernel straight into the flat
+  gradient buffer (ops/linear.py).
 """
 from __future__ import annotations
 
@@ -77,7 +79,7 @@ class Block(nn.Module):
     def attn(self, h):
         B, T, C = h.shape
         H = self.n_head
-        qkv = F.linear(h, self.attn_w, self.attn_b).view(B, T, 3, H, C // H)
+        qkv = ops.linear(h, self.attn_w, self.attn_b).view(B, T, 3, H, C // H)
         if C // H == 64 and qkv.is_cuda:
             y = ops.causal_attention(qkv)  # HIP flash attention on the packed layout
         else:
@@ -87,11 +89,11 @@ class Block(nn.Module):
             y = y.transpose(1, 2)
         # no bias here: proj_b is added (and its gradient reduced) by the following fused
         # residual-add + LayerNorm kernel
-        return F.linear(y.reshape(B, T, C), self.proj_w)
+        return ops.linear(y.reshape(B, T, C), self.proj_w)
 
     def mlp(self, h):
         # fc bias fused into the GELU kernel; fc2 bias fused into the next add+LayerNorm
-        return F.linear(ops.bias_gelu(F.linear(h, self.fc_w), self.fc_b), self.fc2_w)
+        return ops.linear(ops.bias_gelu(ops.linear(h, self.fc_w), self.fc_b), self.fc2_w)
 
 
 class GPT2(nn.Module):
@@ -152,7 +154,7 @@ class GPT2(nn.Module):
                 h, resid = ops.add_layernorm(resid, m, nxt.ln1_w, nxt.ln1_b, eps, branch_bias=blk.fc2_b)
             else:
                 h, resid = ops.add_layernorm(resid, m, self.lnf_w, self.lnf_b, eps, branch_bias=blk.fc2_b)
-        logits = F.linear(h, self.wte)  # tied LM head, [B, T, Vp]
+        logits = ops.linear(h, self.wte)  # tied LM head, [B, T, Vp]
         if targets is None:
             return logits[..., : cfg.vocab_size]
         return ops.cross_entropy(logits.view(B * T, -1), targets.reshape(-1), vocab=cfg.vocab_size)

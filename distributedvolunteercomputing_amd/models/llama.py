@@ -73,7 +73,7 @@ class LlamaBlock(nn.Module):
         c = self.c
         B, T, D = h.shape
         hd = D // c.n_heads
-        qkv = F.linear(h, self.wqkv)
+        qkv = ops.linear(h, self.wqkv)
         q, k, v = qkv.split([c.n_heads * hd, c.n_kv_heads * hd, c.n_kv_heads * hd], -1)
         q = apply_rope(q.view(B, T, c.n_heads, hd).transpose(1, 2), cos, sin)
         k = apply_rope(k.view(B, T, c.n_kv_heads, hd).transpose(1, 2), cos, sin)
@@ -83,10 +83,10 @@ class LlamaBlock(nn.Module):
             k = k.repeat_interleave(rep, dim=1)
             v = v.repeat_interleave(rep, dim=1)
         y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        return F.linear(y.transpose(1, 2).reshape(B, T, D), self.wo)
+        return ops.linear(y.transpose(1, 2).reshape(B, T, D), self.wo)
 
     def mlp(self, h):
-        return F.linear(ops.swiglu(F.linear(h, self.w13)), self.w2)
+        return ops.linear(ops.swiglu(ops.linear(h, self.w13)), self.w2)
 
 
 class Llama(nn.Module):
@@ -128,7 +128,7 @@ class Llama(nn.Module):
             m = L.mlp(h)
             nw = self.layers[i + 1].attn_norm if i + 1 < len(self.layers) else self.norm
             h, resid = ops.add_rmsnorm(resid, m, nw, c.norm_eps)
-        logits = F.linear(h, self.out)
+        logits = ops.linear(h, self.out)
         if targets is None:
             return logits
         return ops.cross_entropy(logits.view(B * T, -1), targets.reshape(-1), vocab=c.vocab_size)

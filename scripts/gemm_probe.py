@@ -36,6 +36,7 @@ def bench(fn, cold, it=10):
 
 
 tag = os.environ.get("PROBE_TAG", "")
+SPLITS = [int(v) for v in os.environ.get("PROBE_SPLITS", "").split(",") if v]
 tot = {False: 0.0, True: 0.0}
 for name, N, K, has_bias in SHAPES:
     x = torch.randn(M, K, device=dev, dtype=bf)
@@ -43,10 +44,13 @@ for name, N, K, has_bias in SHAPES:
     b = torch.zeros(N, device=dev, dtype=bf) if has_bias else None
     dy = torch.randn(M, N, device=dev, dtype=bf)
     ops = {"fwd": lambda: F.linear(x, w, b), "dgrad": lambda: dy.mm(w), "wgrad": lambda: dy.t().mm(x)}
+    for S in SPLITS:  # split-M wgrad: batched partial products, then a sum over the splits
+        ops[f"wg/{S}"] = (lambda S=S: torch.bmm(dy.view(S, M // S, N).transpose(1, 2), x.view(S, M // S, K))
+                          .sum(0, dtype=torch.float32))
     for op, fn in ops.items():
         fl = 2.0 * M * N * K
         h, c = bench(fn, False), bench(fn, True)
-        n = 1 if name == "lm" else 12
+        n = (1 if name == "lm" else 12) * (op in ("fwd", "dgrad", "wgrad"))
         tot[False] += h * n
         tot[True] += c * n
         print(f"{tag:8s} {name:5s} {op:5s} N={N:5d} K={K:4d}  hot {h:8.1f} us ({fl / h / 1e6:6.0f} TF)  "

@@ -215,3 +215,30 @@ def test_embedding_fwd_bwd(gpu):
     (xr * dy).sum().backward()
     assert torch.allclose(wte.grad.float(), w32.grad, atol=5e-2, rtol=2e-2)
     assert torch.allclose(wpe.grad.float(), p32.grad, atol=5e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K,bias", [(8192, 768, 768, True), (65536, 2304, 768, False), (4096, 512, 96, False)])
+@pytest.mark.parametrize("preset_grad", [False, True])
+def test_linear_splitm_wgrad(gpu, M, N, K, bias, preset_grad):
+    """ops.linear: split-M batched weight gradient (HIP fp32 reduction into .grad) against an
+    fp32 reference; with a preset .grad (the flat-buffer case) the gradient is accumulated."""
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(N, K, device=gpu) * 0.05).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(N, device=gpu).to(torch.bfloat16).requires_grad_() if bias else None
+    g0 = torch.randn(N, K, device=gpu).to(torch.bfloat16)
+    if preset_grad:
+        w.grad = g0.clone()
+    dy = torch.randn(M, N, device=gpu).to(torch.bfloat16)
+    y = ops.linear(x, w, b)
+    y.backward(dy)
+    xr, wr = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    br = b.detach().float().requires_grad_() if bias else None
+    F.linear(xr, wr, br).backward(dy.float())
+    ref_w = wr.grad + (g0.float() if preset_grad else 0)
+    rel = lambda a, r: float((a.float() - r).norm() / r.norm())  # noqa: E731
+    assert rel(y, F.linear(xr, wr, br)) < 1e-2
+    assert rel(x.grad, xr.grad) < 1e-2
+    assert rel(w.grad, ref_w) < 1e-2, rel(w.grad, ref_w)
+    if bias:
+        assert rel(b.grad, br.grad) < 1e-2
