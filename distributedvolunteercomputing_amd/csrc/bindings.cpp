@@ -169,7 +169,8 @@ std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Te
   vcx_ln_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
              opt_ptr(dres), dx.data_ptr(), dw_part.data_ptr<float>(), has_bias ? db_part.data_ptr<float>() : nullptr,
              dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)R, C, rms ? 1 : 0,
-             has_bb ? dbb_part.data_ptr<float>() : nullptr, has_bb ? dbb.data_ptr() : nullptr, cur_stream());
+             has_bb ? dbb_part.data_ptr<float>() : nullptr, has_bb ? dbb.data_ptr() : nullptr,
+             at::empty({3 * VCX_COLSUM_NB * C}, x.options().dtype(kF)).data_ptr<float>(), cur_stream());
   return {dx, dw, db, dbb};
 }
 
@@ -192,8 +193,9 @@ std::vector<at::Tensor> bias_gelu_bwd(at::Tensor x, at::Tensor b, at::Tensor dy)
   auto dx = at::empty_like(x);
   auto part = at::empty({vcx_bias_gelu_partials((int)R), F}, x.options().dtype(kF));
   auto db = at::empty({F}, x.options());
+  auto stage = at::empty({VCX_COLSUM_NB * F}, x.options().dtype(kF));
   vcx_bias_gelu_bwd(x.data_ptr(), b.data_ptr(), dy.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), db.data_ptr(),
-                    (int)R, (int)F, cur_stream());
+                    (int)R, (int)F, stage.data_ptr<float>(), cur_stream());
   return {dx, db};
 }
 
@@ -260,6 +262,28 @@ void xent_bwd(at::Tensor logits, at::Tensor tgt, at::Tensor lse, at::Tensor gsca
   TORCH_CHECK(Vp % 8 == 0 && V <= Vp && gscale.numel() >= 1);
   vcx_xent_bwd(logits.data_ptr(), tgt.data_ptr<int64_t>(), lse.data_ptr<float>(), gscale.data_ptr<float>(),
                dlogits.data_ptr(), R, (int)V, (int)Vp, cur_stream());
+}
+
+// fused loss + gradient; returns per-row losses or None if the row does not fit (caller falls back)
+c10::optional<at::Tensor> xent_fused(at::Tensor logits, at::Tensor tgt, at::Tensor nvalid, int64_t V) {
+  CHECK_IN(logits, kBF);
+  CHECK_IN(tgt, at::kLong);
+  CHECK_IN(nvalid, kF);
+  TORCH_CHECK(logits.dim() == 2);
+  const int64_t R = logits.size(0), Vp = logits.size(1);
+  TORCH_CHECK(Vp % 8 == 0 && V <= Vp && V > 0 && tgt.numel() == R && nvalid.numel() >= 1);
+  auto loss = at::empty({R}, logits.options().dtype(kF));
+  if (!vcx_xent_fused(logits.data_ptr(), tgt.data_ptr<int64_t>(), nvalid.data_ptr<float>(), loss.data_ptr<float>(), R,
+                      (int)V, (int)Vp, cur_stream()))
+    return c10::nullopt;
+  return loss;
+}
+
+void xent_rescale(at::Tensor d, at::Tensor dloss) {
+  CHECK_IN(d, kBF);
+  CHECK_IN(dloss, kF);
+  TORCH_CHECK(d.numel() % 8 == 0 && dloss.numel() >= 1);
+  vcx_xent_rescale(d.data_ptr(), dloss.data_ptr<float>(), d.numel(), cur_stream());
 }
 
 // ------------------------------------------------------------------ embedding
@@ -346,6 +370,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("xent_fused", &xent_fused);
+  m.def("xent_rescale", &xent_rescale);
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("attn_fwd", &attn_fwd);

@@ -41,6 +41,14 @@ __device__ __forceinline__ sx4 lds_tr_b64(const bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sx4*)(p));
 }
 
+// v_max3_f32 without the canonicalising v_max_f32 the compiler puts in front of fmaxf on MFMA
+// results (scores are never NaN here)
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ __forceinline__ f32x16 mfma32(sx8 a, sx8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -172,9 +180,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       }
     }
     // raw-score max (scale > 0 commutes with max); the scale is folded into one FMA per score
-    float mx = fmaxf(s0[0], s1[0]);
+    float mx0 = max3(s0[0], s0[1], s1[0]), mx1 = max3(s1[1], s0[2], s1[2]);  // two chains
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+    for (int r = 3; r < 15; r += 2) {
+      mx0 = max3(mx0, s0[r], s1[r]);
+      mx1 = max3(mx1, s0[r + 1], s1[r + 1]);
+    }
+    float mx = max3(mx0, mx1, fmaxf(s0[15], s1[15]));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
     // deferred rescale (cdna guide T13): keep the running max unless it grew by > 8 (P <= 2^8,
     // safe in fp32 accumulation and bf16 P), saving the O-wide multiply on most tiles

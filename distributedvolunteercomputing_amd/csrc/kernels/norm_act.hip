@@ -5,6 +5,7 @@
 // One wave64 owns one row; a 256-thread block covers 4 rows. The row is held in registers
 // (CH = ceil(C/512) chunks of 8 elements per lane), so the variance is an exact two-pass
 // computation over registers with a single HBM read of the row.
+#include "vcx_api.h"
 #include "vcx_common.h"
 
 namespace vcx {
@@ -199,38 +200,84 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
 __device__ __forceinline__ float gelu_f(float x);
 __device__ __forceinline__ float gelu_grad_f(float x);
 
-__global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ b,
-                                                             bf16* __restrict__ y, int R, int F) {
-  const int F8 = F >> 3;
-  const int c8 = blockIdx.x * 256 + threadIdx.x;
-  if (c8 >= F8) return;
+// bias + GELU over [R, F] row-major: a block is TPB threads x 8 columns; each thread walks rows
+// r = blockIdx.y + k * gridDim.y with 4 rows' loads in flight (16-B vectors)
+template <int TPB>
+__global__ void __launch_bounds__(TPB) bias_gelu_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ b,
+                                                            bf16* __restrict__ y, int R, int F) {
+  const int c8 = blockIdx.x * TPB + threadIdx.x;
+  if (c8 * 8 >= F) return;
   bf16x8 bv = *(const bf16x8*)(b + c8 * 8);
-  for (int r = blockIdx.y; r < R; r += gridDim.y) {
+  float bf[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bf[j] = (float)bv[j];
+  const int G = gridDim.y;
+  int r = blockIdx.y;
+  for (; r + 3 * G < R; r += 4 * G) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *(const bf16x8*)(x + (int64_t)(r + u * G) * F + c8 * 8);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)gelu_f((float)v[u][j] + bf[j]);
+      *(bf16x8*)(y + (int64_t)(r + u * G) * F + c8 * 8) = o;
+    }
+  }
+  for (; r < R; r += G) {
     const int64_t off = (int64_t)r * F + c8 * 8;
     bf16x8 v = *(const bf16x8*)(x + off);
     bf16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (bf16)gelu_f((float)v[j] + (float)bv[j]);
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)gelu_f((float)v[j] + bf[j]);
     *(bf16x8*)(y + off) = o;
   }
 }
 
-__global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ b,
-                                                             const bf16* __restrict__ dy, bf16* __restrict__ dx,
-                                                             float* __restrict__ dbias_part, int R, int F) {
-  const int F8 = F >> 3;
-  const int c8 = blockIdx.x * 256 + threadIdx.x;
-  if (c8 >= F8) return;
+template <int TPB>
+__global__ void __launch_bounds__(TPB) bias_gelu_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ b,
+                                                            const bf16* __restrict__ dy, bf16* __restrict__ dx,
+                                                            float* __restrict__ dbias_part, int R, int F) {
+  const int c8 = blockIdx.x * TPB + threadIdx.x;
+  if (c8 * 8 >= F) return;
   bf16x8 bv = *(const bf16x8*)(b + c8 * 8);
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int r = blockIdx.y; r < R; r += gridDim.y) {
+  float bf[8], acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bf[j] = (float)bv[j];
+    acc[j] = 0.f;
+  }
+  const int G = gridDim.y;
+  int r = blockIdx.y;
+  for (; r + 3 * G < R; r += 4 * G) {
+    bf16x8 v[4], g[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t off = (int64_t)(r + u * G) * F + c8 * 8;
+      v[u] = *(const bf16x8*)(x + off);
+      g[u] = *(const bf16x8*)(dy + off);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (float)g[u][j] * gelu_grad_f((float)v[u][j] + bf[j]);
+        o[j] = (bf16)d;
+        acc[j] += d;
+      }
+      *(bf16x8*)(dx + (int64_t)(r + u * G) * F + c8 * 8) = o;
+    }
+  }
+  for (; r < R; r += G) {
     const int64_t off = (int64_t)r * F + c8 * 8;
     bf16x8 v = *(const bf16x8*)(x + off);
     bf16x8 g = *(const bf16x8*)(dy + off);
     bf16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float d = (float)g[j] * gelu_grad_f((float)v[j] + (float)bv[j]);
+      const float d = (float)g[j] * gelu_grad_f((float)v[j] + bf[j]);
       o[j] = (bf16)d;
       acc[j] += d;
     }
@@ -241,46 +288,64 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const bf16* __restri
   *(f32x4*)(p + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
 }
 
-// Column sums of a [P, C] fp32 partial buffer -> bf16 [C]. One block per 64 columns,
-// 16 waves stride the P rows, LDS combine.
-__global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ part, int P, int C,
-                                                       bf16* __restrict__ out) {
-  __shared__ float red[16][64];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+
+
+// Two-stage column sums of up to three [P, C] fp32 partial buffers -> bf16 [C] each, in two
+// launches for all outputs together. Stage 1: grid (C/64, NB, nout) -- every block reduces
+// P/NB rows of 64 columns (4 waves, LDS combine) into stage[out][NB][C]; stage 2: NB rows -> bf16.
+// (A single-stage sum had only C/64 blocks -- 12 for C = 768 -- and ran latency-bound.)
+__global__ void __launch_bounds__(256) colsum_stage1_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                            const float* __restrict__ p2, float* __restrict__ stage,
+                                                            int P, int C) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int out = blockIdx.z, NB = gridDim.y, by = blockIdx.y;
+  const float* part = out == 0 ? p0 : (out == 1 ? p1 : p2);
   const int c = blockIdx.x * 64 + lane;
+  const int r0 = (int)((int64_t)P * by / NB), r1 = (int)((int64_t)P * (by + 1) / NB);
   float acc = 0.f;
   if (c < C) {
-    int p = wid;
-    for (; p + 48 < P; p += 64) {
-      float a0 = part[(int64_t)p * C + c], a1 = part[(int64_t)(p + 16) * C + c];
-      float a2 = part[(int64_t)(p + 32) * C + c], a3 = part[(int64_t)(p + 48) * C + c];
+    int r = r0 + w;
+    for (; r + 12 < r1; r += 16) {
+      const float a0 = part[(int64_t)r * C + c], a1 = part[(int64_t)(r + 4) * C + c];
+      const float a2 = part[(int64_t)(r + 8) * C + c], a3 = part[(int64_t)(r + 12) * C + c];
       acc += (a0 + a1) + (a2 + a3);
     }
-    for (; p < P; p += 16) acc += part[(int64_t)p * C + c];
+    for (; r < r1; r += 4) acc += part[(int64_t)r * C + c];
   }
-  red[wid][lane] = acc;
+  red[w][lane] = acc;
   __syncthreads();
-  if (wid == 0 && c < C) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s += red[i][lane];
-    out[c] = (bf16)s;
-  }
+  if (w == 0 && c < C) stage[((int64_t)out * NB + by) * C + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+__global__ void __launch_bounds__(64) colsum_stage2_kernel(const float* __restrict__ stage, int NB, int C,
+                                                           bf16* __restrict__ o0, bf16* __restrict__ o1,
+                                                           bf16* __restrict__ o2) {
+  const int out = blockIdx.y;
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= C) return;
+  const float* st = stage + (int64_t)out * NB * C + c;
+  float acc = 0.f;
+  for (int i = 0; i < NB; ++i) acc += st[(int64_t)i * C];
+  bf16* o = out == 0 ? o0 : (out == 1 ? o1 : o2);
+  o[c] = (bf16)acc;
 }
 
 // ============================================================ tanh-GELU
+// 0.5 x (1 + tanh(u)) == x * sigmoid(2u): one exp2 and one reciprocal instead of a libm tanhf
 __device__ __forceinline__ float gelu_f(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  const float c0 = -2.f * 0.7978845608028654f * 1.4426950408889634f, k1 = 0.044715f;
+  const float e = __builtin_amdgcn_exp2f(c0 * fmaf(k1 * x, x * x, x));  // exp(-2u)
+  return x * __builtin_amdgcn_rcpf(1.f + e);
 }
 __device__ __forceinline__ float gelu_grad_f(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
-  float du = k0 * (1.f + 3.f * k1 * x2);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
+  const float c0 = -2.f * k0 * 1.4426950408889634f;
+  const float x2 = x * x;
+  const float e = __builtin_amdgcn_exp2f(c0 * fmaf(k1 * x, x2, x));
+  const float sg = __builtin_amdgcn_rcpf(1.f + e);  // sigmoid(2u)
+  const float du2 = 2.f * k0 * fmaf(3.f * k1, x2, 1.f);
+  return fmaf(x * sg * (1.f - sg), du2, sg);
 }
 
 __global__ void __launch_bounds__(256) gelu_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
@@ -435,6 +500,96 @@ __global__ void __launch_bounds__(256) xent_bwd_kernel(const bf16* logits, const
   }
 }
 
+// Fused softmax cross-entropy forward + backward, one row per block with the whole row held in
+// registers (TPB threads x NV 16-B vectors): ONE read of the logits and ONE write of the gradient
+// (softmax - onehot) / nvalid over the same buffer, versus a read for the loss plus a read and a
+// write for the gradient. The loss backward's incoming scalar is applied afterwards only if it is
+// not 1 (xent_rescale_kernel). Rows with a negative target contribute neither loss nor gradient.
+template <int TPB, int NV>
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) xent_fused_kernel(
+    bf16* __restrict__ logits, const int64_t* __restrict__ tgt, const float* __restrict__ nvalid,
+    float* __restrict__ loss_out, int V, int Vp) {
+  constexpr int NW = TPB / 64;
+  __shared__ float red[2][NW];
+  __shared__ float tlogit;
+  const int64_t row = blockIdx.x;
+  bf16* lr = logits + row * Vp;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int Vp8 = Vp >> 3;
+  const int64_t t = tgt[row];
+  if (tid == 0) tlogit = (t >= 0 && t < V) ? (float)lr[t] : 0.f;
+  constexpr float L2E = 1.4426950408889634f;
+  bf16x8 v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = tid + k * TPB;
+    if (c < Vp8) v[k] = *(const bf16x8*)(lr + c * 8);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = tid + k * TPB;
+    if (c < Vp8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c * 8 + j < V) m = fmaxf(m, (float)v[k][j]);
+    }
+  }
+  m = wave_max(m);
+  if (lane == 0) red[0][wid] = m;
+  __syncthreads();
+  float M = red[0][0];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) M = fmaxf(M, red[0][i]);
+  const float M2 = M * L2E;
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = tid + k * TPB;
+    if (c < Vp8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c * 8 + j < V) sum += __builtin_amdgcn_exp2f(fmaf((float)v[k][j], L2E, -M2));
+    }
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) red[1][wid] = sum;
+  __syncthreads();
+  float S = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) S += red[1][i];
+  const float lse2 = M2 + __builtin_amdgcn_logf(S);  // log2-domain lse (v_log_f32 is log2)
+  const float sc = (t >= 0) ? 1.f / nvalid[0] : 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = tid + k * TPB;
+    if (c < Vp8) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = c * 8 + j;
+        float p = (col < V) ? __builtin_amdgcn_exp2f(fmaf((float)v[k][j], L2E, -lse2)) : 0.f;
+        if (col == t) p -= 1.f;
+        o[j] = (bf16)(p * sc);
+      }
+      *(bf16x8*)(lr + c * 8) = o;
+    }
+  }
+  if (tid == 0) loss_out[row] = (t >= 0) ? lse2 * (1.f / L2E) - tlogit : 0.f;
+}
+
+__global__ void __launch_bounds__(256) xent_rescale_kernel(bf16* __restrict__ d, const float* __restrict__ dloss,
+                                                           int64_t n8) {
+  const float g = dloss[0];
+  if (g == 1.f) return;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    bf16x8 v = *(const bf16x8*)(d + i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] * g);
+    *(bf16x8*)(d + i * 8) = v;
+  }
+}
+
 }  // namespace vcx
 
 // ============================================================ launchers
@@ -460,44 +615,85 @@ void vcx_ln_fwd(const void* a, const void* b, void* xout, void* y, const void* w
                                          (const bf16*)bias, mean, rstd, R, C, eps, rms, (const bf16*)bb));
 }
 
-static int bias_gelu_groups(int R) { return R < 256 ? (R > 0 ? R : 1) : 256; }
+
+static void colsums(const float* p0, const float* p1, const float* p2, void* o0, void* o1, void* o2, int nout, int P,
+                    int C, float* stage, hipStream_t s) {
+  hipLaunchKernelGGL(colsum_stage1_kernel, dim3((C + 63) / 64, VCX_COLSUM_NB, nout), dim3(256), 0, s, p0, p1, p2,
+                     stage, P, C);
+  hipLaunchKernelGGL(colsum_stage2_kernel, dim3((C + 63) / 64, nout), dim3(64), 0, s, stage, VCX_COLSUM_NB, C,
+                     (bf16*)o0, (bf16*)o1, (bf16*)o2);
+}
+
+static int bias_gelu_groups(int R) { return R < 1024 ? (R > 0 ? R : 1) : 1024; }
 
 int vcx_bias_gelu_partials(int R) { return bias_gelu_groups(R); }
 
+// threads per block: the largest of 256/128/64 that tiles the F/8 column vectors exactly
+static int bias_gelu_tpb(int F) {
+  const int F8 = F / 8;
+  return F8 % 256 == 0 ? 256 : F8 % 128 == 0 ? 128 : 64;
+}
+
+#define VCX_TPB_DISPATCH(tpb, ...) \
+  do {                               \
+    if (tpb == 256) {                \
+      constexpr int TPB = 256;       \
+      __VA_ARGS__;                   \
+    } else if (tpb == 128) {         \
+      constexpr int TPB = 128;       \
+      __VA_ARGS__;                   \
+    } else {                         \
+      constexpr int TPB = 64;        \
+      __VA_ARGS__;                   \
+    }                                \
+  } while (0)
+
 void vcx_bias_gelu_fwd(const void* x, const void* b, void* y, int R, int F, hipStream_t s) {
-  dim3 grid((F / 8 + 255) / 256, R < 1024 ? (R > 0 ? R : 1) : 1024);
-  hipLaunchKernelGGL(bias_gelu_fwd_kernel, grid, dim3(256), 0, s, (const bf16*)x, (const bf16*)b, (bf16*)y, R, F);
+  const int tpb = bias_gelu_tpb(F);
+  dim3 grid((F / 8 + tpb - 1) / tpb, R < 1024 ? (R > 0 ? R : 1) : 1024);
+  VCX_TPB_DISPATCH(tpb, hipLaunchKernelGGL(bias_gelu_fwd_kernel<TPB>, grid, dim3(TPB), 0, s, (const bf16*)x,
+                                           (const bf16*)b, (bf16*)y, R, F));
 }
 
 void vcx_bias_gelu_bwd(const void* x, const void* b, const void* dy, void* dx, float* part, void* db, int R, int F,
-                       hipStream_t s) {
+                       float* stage, hipStream_t s) {
   const int G = bias_gelu_groups(R);
-  dim3 grid((F / 8 + 255) / 256, G);
-  hipLaunchKernelGGL(bias_gelu_bwd_kernel, grid, dim3(256), 0, s, (const bf16*)x, (const bf16*)b, (const bf16*)dy,
-                     (bf16*)dx, part, R, F);
-  hipLaunchKernelGGL(colsum_kernel, dim3((F + 63) / 64), dim3(1024), 0, s, part, G, F, (bf16*)db);
+  const int tpb = bias_gelu_tpb(F);
+  dim3 grid((F / 8 + tpb - 1) / tpb, G);
+  VCX_TPB_DISPATCH(tpb, hipLaunchKernelGGL(bias_gelu_bwd_kernel<TPB>, grid, dim3(TPB), 0, s, (const bf16*)x,
+                                           (const bf16*)b, (const bf16*)dy, (bf16*)dx, part, R, F));
+  colsums(part, nullptr, nullptr, db, nullptr, nullptr, 1, G, F, stage, s);
 }
 
 int vcx_ln_bwd_partials(int R) {
   // enough waves to keep every SIMD busy with several rows in flight (each wave streams
-  // ~16 rows); the [P, C] fp32 partials cost one extra small read in colsum_kernel
+  // ~16 rows); the [P, C] fp32 partials cost one extra small read in the column sums
   int g = (R + 3) / 4;
   return (g > 1024 ? 1024 : g) * 4;
 }
 
 void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
                 void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, float* dbb_part,
-                void* dbb, hipStream_t s) {
+                void* dbb, float* stage, hipStream_t s) {
   const int ch = (C / 8 + 63) / 64;
   const int P = vcx_ln_bwd_partials(R);
   dim3 grid(P / 4);
   VCX_LN_DISPATCH(ch, hipLaunchKernelGGL(ln_bwd_kernel<CH>, grid, dim3(256), 0, s, (const bf16*)dy,
                                          (const bf16*)x, (const bf16*)w, mean, rstd, (const bf16*)dres,
                                          (bf16*)dx, dw_part, db_part, R, C, rms, dbb_part));
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, dw_part, P, C, (bf16*)dw);
-  if (db_part && db) hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, db_part, P, C, (bf16*)db);
-  if (dbb_part && dbb)
-    hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, s, dbb_part, P, C, (bf16*)dbb);
+  // dw, then db and dbb when present, in one pair of launches
+  const float* ps[3] = {dw_part, nullptr, nullptr};
+  void* os[3] = {dw, nullptr, nullptr};
+  int n = 1;
+  if (db_part && db) {
+    ps[n] = db_part;
+    os[n++] = db;
+  }
+  if (dbb_part && dbb) {
+    ps[n] = dbb_part;
+    os[n++] = dbb;
+  }
+  colsums(ps[0], ps[1], ps[2], os[0], os[1], os[2], n, P, C, stage, s);
 }
 
 void vcx_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s) {
@@ -529,4 +725,24 @@ void vcx_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, cons
                   int64_t R, int V, int Vp, hipStream_t s) {
   hipLaunchKernelGGL(xent_bwd_kernel, dim3(R), dim3(256), 0, s, (const bf16*)logits, tgt, lse, gscale,
                      (bf16*)dlogits, V, Vp);
+}
+
+// returns 0 if the row does not fit the register-resident fused kernel (caller falls back)
+int vcx_xent_fused(void* logits, const int64_t* tgt, const float* nvalid, float* loss, int64_t R, int V, int Vp,
+                   hipStream_t s) {
+  // two rows in flight per CU (12 waves each at <= 85 VGPRs): one row's loads overlap the
+  // other's reductions and stores
+  const int Vp8 = Vp / 8;
+  dim3 grid(R);
+  if (Vp8 <= 768 * 4)
+    hipLaunchKernelGGL((xent_fused_kernel<768, 4>), grid, dim3(768), 0, s, (bf16*)logits, tgt, nvalid, loss, V, Vp);
+  else if (Vp8 <= 768 * 9)
+    hipLaunchKernelGGL((xent_fused_kernel<768, 9>), grid, dim3(768), 0, s, (bf16*)logits, tgt, nvalid, loss, V, Vp);
+  else
+    return 0;
+  return 1;
+}
+
+void vcx_xent_rescale(void* d, const float* dloss, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(xent_rescale_kernel, dim3(stream_grid(n / 8, 256)), dim3(256), 0, s, (bf16*)d, dloss, n / 8);
 }

@@ -21,18 +21,22 @@ void vcx_ln_fwd(const void* a, const void* b, void* xout, void* y, const void* w
                 float* rstd, int R, int C, float eps, int rms, const void* bb, hipStream_t s);
 int vcx_bias_gelu_partials(int R);
 void vcx_bias_gelu_fwd(const void* x, const void* b, void* y, int R, int F, hipStream_t s);
+constexpr int VCX_COLSUM_NB = 32;  // stage-1 row chunks of the two-stage column sums (stage: 3 * NB * C fp32)
 void vcx_bias_gelu_bwd(const void* x, const void* b, const void* dy, void* dx, float* part, void* db, int R, int F,
-                       hipStream_t s);
+                       float* stage, hipStream_t s);
 int vcx_ln_bwd_partials(int R);
 void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
                 void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, float* dbb_part,
-                void* dbb, hipStream_t s);
+                void* dbb, float* stage, hipStream_t s);
 void vcx_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s);
 void vcx_gelu_bwd(const void* x, const void* dy, void* dx, int64_t n, hipStream_t s);
 void vcx_swiglu_fwd(const void* gu, void* y, int64_t R, int F, hipStream_t s);
 void vcx_swiglu_bwd(const void* gu, const void* dy, void* dgu, int64_t R, int F, hipStream_t s);
 void vcx_xent_fwd(const void* logits, const int64_t* tgt, float* lse, float* loss, int64_t R, int V, int Vp,
                   hipStream_t s);
+int vcx_xent_fused(void* logits, const int64_t* tgt, const float* nvalid, float* loss, int64_t R, int V, int Vp,
+                   hipStream_t s);
+void vcx_xent_rescale(void* d, const float* dloss, int64_t n, hipStream_t s);
 void vcx_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, const float* gscale, void* dlogits,
                   int64_t R, int V, int Vp, hipStream_t s);
 

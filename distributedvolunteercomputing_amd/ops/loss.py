@@ -1,9 +1,13 @@
 """Fused softmax cross-entropy over a (possibly padded) vocabulary.
 
-Forward: one block per row computes an online max/sum (one HBM read of the logits) and
-returns per-row losses; the mean is taken by torch. Backward: writes the logit gradient IN
-PLACE over the logits buffer (the logits are dead after the loss), scaled by a device-side
-scalar, so no host sync and no second logits-sized allocation (3.3 GB at 32k tokens x 50k).
+Rows that fit in registers (vocab <= 57344, e.g. GPT-2's 50304): ONE kernel per step reads
+each logits row once, returns the row loss and overwrites the row IN PLACE with the gradient
+(softmax - onehot) / n_valid (the logits are dead after the loss). The backward then only
+rescales if the incoming gradient is not 1 (a device-side test, no host sync). 13.2 GB of HBM
+traffic at the GPT-2 bench shape instead of 19.8 GB.
+
+Larger vocabularies (Llama-3: 128256): forward = online max/sum per row (one read), backward =
+in-place gradient scaled by a device-side scalar.
 """
 from __future__ import annotations
 
@@ -11,6 +15,20 @@ import torch
 import torch.nn.functional as F
 
 from ._lib import native, use_native
+
+
+class _XEntFused(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets, vocab, ignore_index, nvalid, loss_rows):
+        ctx.logits = logits  # holds the gradient now
+        return loss_rows.sum() / nvalid
+
+    @staticmethod
+    def backward(ctx, dloss):
+        d = ctx.logits
+        ctx.logits = None
+        native().xent_rescale(d, dloss.float().reshape(1).contiguous())
+        return d, None, None, None, None, None
 
 
 class _XEnt(torch.autograd.Function):
@@ -41,5 +59,12 @@ def cross_entropy(logits, targets, vocab: int | None = None, ignore_index: int =
     logits = logits.reshape(-1, logits.shape[-1])
     targets = targets.reshape(-1)
     if use_native(logits):
-        return _XEnt.apply(logits.contiguous(), targets.contiguous().long(), vocab, ignore_index)
+        logits, targets = logits.contiguous(), targets.contiguous().long()
+        if logits.requires_grad and ignore_index < 0:  # the kernel treats target < 0 as ignored
+            nvalid = ((targets != ignore_index) & (targets >= 0)).sum().clamp_min(1).to(torch.float32).reshape(1)
+            with torch.no_grad():
+                rows = native().xent_fused(logits.detach(), targets, nvalid, vocab)
+            if rows is not None:
+                return _XEntFused.apply(logits, targets, vocab, ignore_index, nvalid, rows)
+        return _XEnt.apply(logits, targets, vocab, ignore_index)
     return F.cross_entropy(logits[:, :vocab].float(), targets.long(), ignore_index=ignore_index)

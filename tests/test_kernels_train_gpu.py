@@ -89,7 +89,7 @@ def test_swiglu(gpu):
     assert torch.allclose(gu.grad.float(), g32.grad, atol=5e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("V,Vp", [(50257, 50304), (1000, 1000), (37, 40)])
+@pytest.mark.parametrize("V,Vp", [(50257, 50304), (1000, 1000), (37, 40), (128256, 128256)])
 def test_cross_entropy(gpu, V, Vp):
     torch.manual_seed(4)
     R = 129
