@@ -118,7 +118,9 @@ def build_C(nproc: int = 8, force: bool = False) -> Path:
     n = _compile_all(jobs, nproc)
     out = PKG / f"_C{EXT}"
     if n or not out.exists():
-        libs = ["-ltorch", "-ltorch_cpu", "-lc10", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64"]
+        # hipBLASLt: torch's own bundled copy (same library instance torch's GEMMs use)
+        libs = ["-ltorch", "-ltorch_cpu", "-lc10", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64",
+                "-lhipblaslt"]
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out),
               f"-L{libdir}", *libs, f"-Wl,-rpath,{libdir}"], "link _C")
         print(f"[vcx build] linked {out.name}", flush=True)

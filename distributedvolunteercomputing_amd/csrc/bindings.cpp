@@ -136,9 +136,23 @@ std::vector<at::Tensor> ln_fwd(at::Tensor a, c10::optional<at::Tensor> b, at::Te
   return {y, xout, mean, rstd};
 }
 
+// Grad outputs that the caller may pass in (views of the flat gradient buffer): the column sums
+// are then ADDED into them (no separate autograd accumulation pass); otherwise fresh tensors.
+at::Tensor grad_out(const c10::optional<at::Tensor>& given, int64_t n, const at::Tensor& like, int* mask, int bit) {
+  if (given.has_value()) {
+    CHECK_IN((*given), kBF);
+    TORCH_CHECK(given->numel() == n, "gradient output has the wrong size");
+    *mask |= 1 << bit;
+    return *given;
+  }
+  return at::empty({n}, like.options());
+}
+
 // returns {dx, dw, db or None, dbb or None}
 std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Tensor mean, at::Tensor rstd,
-                               c10::optional<at::Tensor> dres, bool has_bias, bool rms, bool has_bb) {
+                               c10::optional<at::Tensor> dres, bool has_bias, bool rms, bool has_bb,
+                               c10::optional<at::Tensor> dw_out, c10::optional<at::Tensor> db_out,
+                               c10::optional<at::Tensor> dbb_out) {
   CHECK_IN(dy, kBF);
   CHECK_IN(x, kBF);
   CHECK_IN(w, kBF);
@@ -155,23 +169,38 @@ std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Te
   const int P = vcx_ln_bwd_partials((int)R);
   auto dx = at::empty_like(x);
   auto dw_part = at::empty({P, C}, x.options().dtype(kF));
+  int mask = 0;
+  at::Tensor dw = grad_out(dw_out, C, x, &mask, 0);
   at::Tensor db_part, db;
-  auto dw = at::empty({C}, x.options());
   if (has_bias) {
     db_part = at::empty({P, C}, x.options().dtype(kF));
-    db = at::empty({C}, x.options());
+    db = grad_out(db_out, C, x, &mask, 1);
   }
   at::Tensor dbb_part, dbb;
   if (has_bb) {
     dbb_part = at::empty({P, C}, x.options().dtype(kF));
-    dbb = at::empty({C}, x.options());
+    dbb = grad_out(dbb_out, C, x, &mask, 2);
   }
   vcx_ln_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
              opt_ptr(dres), dx.data_ptr(), dw_part.data_ptr<float>(), has_bias ? db_part.data_ptr<float>() : nullptr,
              dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)R, C, rms ? 1 : 0,
              has_bb ? dbb_part.data_ptr<float>() : nullptr, has_bb ? dbb.data_ptr() : nullptr,
-             at::empty({3 * VCX_COLSUM_NB * C}, x.options().dtype(kF)).data_ptr<float>(), cur_stream());
+             at::empty({3 * VCX_COLSUM_NB * C}, x.options().dtype(kF)).data_ptr<float>(), mask, cur_stream());
   return {dx, dw, db, dbb};
+}
+
+// out[F] (+)= column sums of y [.., F] (bias gradient of a token-major GEMM output)
+at::Tensor colsum_bf16(at::Tensor y, c10::optional<at::Tensor> out) {
+  CHECK_IN(y, kBF);
+  const int64_t F = y.size(-1), R = y.numel() / F;
+  TORCH_CHECK(F % 8 == 0 && R > 0 && R < INT32_MAX, "colsum_bf16: last dim must be a multiple of 8");
+  int mask = 0;
+  at::Tensor o = grad_out(out, F, y, &mask, 0);
+  auto part = at::empty({vcx_bias_gelu_partials((int)R), F}, y.options().dtype(kF));
+  auto stage = at::empty({VCX_COLSUM_NB * F}, y.options().dtype(kF));
+  vcx_colsum_bf16(y.data_ptr(), part.data_ptr<float>(), o.data_ptr(), (int)R, (int)F, mask, stage.data_ptr<float>(),
+                  cur_stream());
+  return o;
 }
 
 at::Tensor bias_gelu_fwd(at::Tensor x, at::Tensor b) {
@@ -184,7 +213,7 @@ at::Tensor bias_gelu_fwd(at::Tensor x, at::Tensor b) {
   return y;
 }
 
-std::vector<at::Tensor> bias_gelu_bwd(at::Tensor x, at::Tensor b, at::Tensor dy) {
+std::vector<at::Tensor> bias_gelu_bwd(at::Tensor x, at::Tensor b, at::Tensor dy, c10::optional<at::Tensor> db_out) {
   CHECK_IN(x, kBF);
   CHECK_IN(b, kBF);
   CHECK_IN(dy, kBF);
@@ -192,10 +221,11 @@ std::vector<at::Tensor> bias_gelu_bwd(at::Tensor x, at::Tensor b, at::Tensor dy)
   TORCH_CHECK(F % 8 == 0 && b.numel() == F && dy.sizes() == x.sizes() && R < INT32_MAX);
   auto dx = at::empty_like(x);
   auto part = at::empty({vcx_bias_gelu_partials((int)R), F}, x.options().dtype(kF));
-  auto db = at::empty({F}, x.options());
+  int mask = 0;
+  auto db = grad_out(db_out, F, x, &mask, 0);
   auto stage = at::empty({VCX_COLSUM_NB * F}, x.options().dtype(kF));
   vcx_bias_gelu_bwd(x.data_ptr(), b.data_ptr(), dy.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), db.data_ptr(),
-                    (int)R, (int)F, stage.data_ptr<float>(), cur_stream());
+                    (int)R, (int)F, stage.data_ptr<float>(), mask, cur_stream());
   return {dx, db};
 }
 
@@ -303,17 +333,38 @@ at::Tensor embed_fwd(at::Tensor idx, at::Tensor wte, c10::optional<at::Tensor> w
   return out;
 }
 
-std::vector<at::Tensor> embed_bwd(at::Tensor idx, at::Tensor dx, int64_t V, int64_t T, int64_t Tpos) {
+// returns {dwte, dwpe or None}; with wte_grad / wpe_grad given (flat .grad views) the gradients
+// are added into them and those same tensors are returned
+std::vector<at::Tensor> embed_bwd(at::Tensor idx, at::Tensor dx, int64_t V, int64_t T, int64_t Tpos,
+                                  c10::optional<at::Tensor> wte_grad, c10::optional<at::Tensor> wpe_grad) {
   CHECK_IN(idx, at::kLong);
   CHECK_IN(dx, kBF);
   const int64_t R = idx.numel(), C = dx.size(-1);
-  TORCH_CHECK(dx.numel() == R * C && C % 8 == 0 && T > 0 && R % T == 0 && Tpos >= 0);
-  auto dwte = at::zeros({V, C}, dx.options().dtype(kF));
-  at::Tensor dwpe;
-  if (Tpos > 0) dwpe = at::zeros({Tpos, C}, dx.options().dtype(kF));
-  vcx_embed_bwd(idx.data_ptr<int64_t>(), dx.data_ptr(), dwte.data_ptr<float>(),
-                Tpos > 0 ? dwpe.data_ptr<float>() : nullptr, R, (int)T, (int)C, (int)V, cur_stream());
-  return {dwte.to(at::kBFloat16), Tpos > 0 ? dwpe.to(at::kBFloat16) : at::Tensor()};
+  TORCH_CHECK(dx.numel() == R * C && C % 8 == 0 && C <= 8192 && T > 0 && R % T == 0 && Tpos >= 0 && Tpos >= (Tpos ? T : 0));
+  auto scratch = at::zeros({V, C}, dx.options().dtype(kF));
+  at::Tensor dwte, dwpe;
+  int acc_wte = 0, acc_wpe = 0;
+  if (wte_grad.has_value()) {
+    CHECK_IN((*wte_grad), kBF);
+    TORCH_CHECK(wte_grad->numel() == V * C);
+    dwte = *wte_grad;
+    acc_wte = 1;
+  } else {
+    dwte = at::empty({V, C}, dx.options());
+  }
+  if (Tpos > 0) {
+    if (wpe_grad.has_value()) {
+      CHECK_IN((*wpe_grad), kBF);
+      TORCH_CHECK(wpe_grad->numel() == Tpos * C);
+      dwpe = *wpe_grad;
+      acc_wpe = 1;
+    } else {
+      dwpe = at::zeros({Tpos, C}, dx.options());  // rows >= T get no gradient
+    }
+  }
+  vcx_embed_bwd(idx.data_ptr<int64_t>(), dx.data_ptr(), scratch.data_ptr<float>(), dwte.data_ptr(), acc_wte,
+                Tpos > 0 ? dwpe.data_ptr() : nullptr, acc_wpe, R, (int)T, (int)C, (int)V, cur_stream());
+  return {dwte, dwpe};
 }
 
 // ------------------------------------------------------------------ attention (head dim 64)
@@ -349,6 +400,7 @@ at::Tensor attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor 
 
 void vcx_register_vision(pybind11::module& m);
 void vcx_register_compress(pybind11::module& m);
+void vcx_register_lt(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels of distributedvolunteercomputing_amd";
@@ -361,10 +413,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("axpy_bf16", &axpy_bf16);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("ln_fwd", &ln_fwd);
-  m.def("ln_bwd", &ln_bwd);
+  m.def("ln_bwd", &ln_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("mean"),
+        pybind11::arg("rstd"), pybind11::arg("dres"), pybind11::arg("has_bias"), pybind11::arg("rms"),
+        pybind11::arg("has_bb"), pybind11::arg("dw_out") = pybind11::none(), pybind11::arg("db_out") = pybind11::none(),
+        pybind11::arg("dbb_out") = pybind11::none());
+  m.def("colsum_bf16", &colsum_bf16, pybind11::arg("y"), pybind11::arg("out") = pybind11::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
-  m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd, pybind11::arg("x"), pybind11::arg("b"), pybind11::arg("dy"),
+        pybind11::arg("db_out") = pybind11::none());
   m.def("gelu_bwd", &gelu_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
@@ -373,9 +430,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("xent_fused", &xent_fused);
   m.def("xent_rescale", &xent_rescale);
   m.def("embed_fwd", &embed_fwd);
-  m.def("embed_bwd", &embed_bwd);
+  m.def("embed_bwd", &embed_bwd, pybind11::arg("idx"), pybind11::arg("dx"), pybind11::arg("V"), pybind11::arg("T"),
+        pybind11::arg("Tpos"), pybind11::arg("wte_grad") = pybind11::none(), pybind11::arg("wpe_grad") = pybind11::none());
   m.def("attn_fwd", &attn_fwd);
+  m.def("attn_set_variant", &vcx_attn_set_variant);
   m.def("attn_bwd", &attn_bwd);
   vcx_register_vision(m);
   vcx_register_compress(m);
+  vcx_register_lt(m);
 }

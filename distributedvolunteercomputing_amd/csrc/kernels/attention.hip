@@ -14,10 +14,10 @@
 // The A operand V^T is read from the row-major V tile in LDS with ds_read_b64_tr_b16, in the
 // permuted key order that the accumulator layout implies.
 //
-// LDS tiles: K rows padded to 72 bf16 (144 B: 16 consecutive rows of a ds_read_b128 land in
-// 16 distinct 4-bank slots); V rows padded to 96 bf16 (192 B: the 4 rows x 32 columns of a
-// half-wave ds_read_b64_tr_b16 hit disjoint banks). K/V tiles are double-buffered and staged
-// through registers (issue next tile's global loads before the MFMAs, write LDS after).
+// LDS tiles: unpadded [rows][64] bf16 images with an XOR swizzle (swz below) that keeps both the
+// ds_read_b128 row reads and the ds_read_b64_tr_b16 transposed reads conflict-free. K/V (Q/dO)
+// tiles are double-buffered and staged through registers (issue next tile's global loads before
+// the MFMAs, write LDS after).
 #include <type_traits>
 
 #include "vcx_common.h"
@@ -30,8 +30,6 @@ typedef short sx4 __attribute__((ext_vector_type(4)));
 constexpr int AD = 64;         // head dim
 constexpr int A_BQ = 128;      // queries per block (4 waves x 32)
 constexpr int A_BK = 64;       // keys per LDS tile
-constexpr int KLD = 72;        // K tile row stride (elements)
-constexpr int VLD = 96;        // V tile row stride (elements)
 constexpr float LOG2E = 1.4426950408889634f;
 
 using I0 = std::integral_constant<int, 0>;
@@ -56,18 +54,6 @@ __device__ __forceinline__ f32x16 mfma32(sx8 a, sx8 b, f32x16 c) {
 __device__ __forceinline__ short bf16_bits(float f) {
   bf16 b = (bf16)f;
   return *(short*)&b;
-}
-
-// A operand of X^T . P^T-style products: rows = d (lane&31 within the 32-wide d tile),
-// k = 16 keys of k-step `s`, in the accumulator's permuted order
-// (element j <-> key 16s + 8(j>>2) + 4h + (j&3)), read from a row-major [key][d] LDS tile.
-__device__ __forceinline__ sx8 vt_frag(const bf16* tile, int ld, int key0, int dtile, int s, int lane) {
-  const int h = lane >> 5, g = lane >> 4, lig = lane & 15;
-  const int cb = dtile * 32 + (g & 1) * 16 + 4 * (lig & 3);
-  const int rb = key0 + 16 * s + 4 * h + (lig >> 2);
-  sx4 lo = lds_tr_b64(tile + rb * ld + cb);
-  sx4 hi = lds_tr_b64(tile + (rb + 8) * ld + cb);
-  return sx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
 // XOR-swizzled [rows][64] bf16 LDS tile (no padding): 16-B chunk c of row r is stored at chunk
@@ -103,40 +89,52 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
+// value of lane l combined with lane l ^ 32 by ONE v_permlane32_swap (VALU, no LDS round trip;
+// __shfl_xor(v, 32) lowers to ds_bpermute on gfx950, ~100+ cycles in the softmax's serial chain)
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float xhalf_max(float v) {
+  const i32x2 r = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float v) {
+  const i32x2 r = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(r[0]) + __int_as_float(r[1]);
+}
+
 // ============================================================================ forward
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                            float* __restrict__ lse, int B, int T, int H,
-                                                            float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 sK[2][A_BK * KLD];
-  __shared__ __attribute__((aligned(16))) bf16 sV[2][A_BK * VLD];
+// Forward, occupancy-templated: the same tile algorithm with both K and V in XOR-swizzled
+// UNPADDED images (2 buffers x (8 + 8) KB = 32 KB per block, vs 42 KB padded) and the row max /
+// row sum combined across the lane halves by v_permlane32_swap. With WPE = 4 the kernel is held
+// to 128 VGPRs so FOUR blocks (16 waves, 4 per SIMD) share a CU: the per-tile chain (K reads ->
+// S MFMAs -> max -> exp -> P -> V^T reads -> PV MFMAs -> barrier) is serial inside a wave, so the
+// SIMD needs more waves to overlap one wave's softmax with another's MFMAs.
+template <int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
+attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int B, int T, int H,
+                    float scale_log2) {
+  __shared__ __attribute__((aligned(16))) bf16 sK[2][A_BK * AD];  // swizzled (swz)
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][A_BK * AD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
   const int nqt = (T + A_BQ - 1) / A_BQ;
-  // heaviest (last) query tiles first: better tail under the causal triangle
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int qt = nqt - 1 - (lb % nqt);
+  const int qt = nqt - 1 - (lb % nqt);  // heaviest (last) query tiles first
   const int bh = lb / nqt;
   const int b = bh / H, hh = bh % H;
-  const int64_t tok = 3ll * H * AD;  // token stride in qkv
+  const int64_t tok = 3ll * H * AD;
   const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
   const bf16* Kg = base + H * AD;
   const bf16* Vg = base + 2 * H * AD;
   const int q0 = qt * A_BQ;
-  const int qw = q0 + w * 32;      // this wave's first query
-  const int q = qw + col;          // this lane's query
+  const int qw = q0 + w * 32;
+  const int q = qw + col;
   const int qc = min(q, T - 1);
-
-  // Q^T fragments (B operand): lane holds Q[q][16s + 8h + j]
   sx8 qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = *(const sx8*)(base + (int64_t)qc * tok + 16 * s + 8 * h2);
-
   f32x16 o0 = {}, o1 = {};
   float m = -INFINITY, l = 0.f;
-
-  const int kend = min(T, q0 + A_BQ);  // keys needed by this block (causal)
+  const int kend = min(T, q0 + A_BQ);
   const int nkt = (kend + A_BK - 1) / A_BK;
-
-  // staging: a 64x64 tile = 512 16-B chunks -> 2 per thread for K and for V
   sx8 rk[2], rv[2];
   auto gload = [&](int kt) {
 #pragma unroll
@@ -150,26 +148,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
-      *(sx8*)(&sK[buf][r * KLD + c]) = rk[i];
-      *(sx8*)(&sV[buf][r * VLD + c]) = rv[i];
+      const int e = tid + i * 256, r = e >> 3;
+      *(sx8*)(&sK[buf][swz(r, e & 7)]) = rk[i];
+      *(sx8*)(&sV[buf][swz(r, e & 7)]) = rv[i];
     }
   };
-
-  // one 64-key tile; MASK only on the (at most two) tiles that cross this block's diagonal.
-  // Keys >= T need no test of their own: for every stored query q < T they satisfy key > q.
   auto tile = [&](int kt, auto cur_c, auto mask_c) {
-    constexpr int cur = decltype(cur_c)::value;  // LDS buffer: compile-time -> immediate offsets
+    constexpr int cur = decltype(cur_c)::value;
     constexpr bool MASK = decltype(mask_c)::value;
     const int kb = kt * A_BK;
-    if (MASK && kb > qw + 31) return;  // wave-uniform: every query of this wave precedes these keys
-    const bf16* kl = &sK[cur][0];
-    // two independent 32-key score tiles (interleaved MFMA chains)
+    if (MASK && kb > qw + 31) return;
     f32x16 s0 = {}, s1 = {};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      s0 = mfma32(*(const sx8*)(kl + col * KLD + 16 * s + 8 * h2), qf[s], s0);
-      s1 = mfma32(*(const sx8*)(kl + (32 + col) * KLD + 16 * s + 8 * h2), qf[s], s1);
+      s0 = mfma32(row_frag_swz(&sK[cur][0], col, s, h2), qf[s], s0);
+      s1 = mfma32(row_frag_swz(&sK[cur][0], 32 + col, s, h2), qf[s], s1);
     }
     if (MASK) {
 #pragma unroll
@@ -179,20 +172,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         s1[r] = key + 32 > q ? -INFINITY : s1[r];
       }
     }
-    // raw-score max (scale > 0 commutes with max); the scale is folded into one FMA per score
-    float mx0 = max3(s0[0], s0[1], s1[0]), mx1 = max3(s1[1], s0[2], s1[2]);  // two chains
+    float mx0 = max3(s0[0], s0[1], s1[0]), mx1 = max3(s1[1], s0[2], s1[2]);
 #pragma unroll
     for (int r = 3; r < 15; r += 2) {
       mx0 = max3(mx0, s0[r], s1[r]);
       mx1 = max3(mx1, s0[r + 1], s1[r + 1]);
     }
-    float mx = max3(mx0, mx1, fmaxf(s0[15], s1[15]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
-    // deferred rescale (cdna guide T13): keep the running max unless it grew by > 8 (P <= 2^8,
-    // safe in fp32 accumulation and bf16 P), saving the O-wide multiply on most tiles
-    if (!__all(mx - m <= 8.f)) {
+    const float mx = xhalf_max(max3(mx0, mx1, fmaxf(s0[15], s1[15]))) * scale_log2;
+    if (!__all(mx - m <= 8.f)) {  // deferred rescale (T13), threshold 2^8
       const float mnew = fmaxf(m, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m - mnew);  // m = -inf on the first tile -> 0
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       l *= alpha;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -212,25 +201,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       ps0 += p0;
       ps1 += p1;
     }
-    const float ps = ps0 + ps1;
-    l += ps + __shfl_xor(ps, 32, 64);
-    // P^T (bf16) as the B operand: 4 k-steps of 16 keys (registers 8s .. 8s+7 of s0 / s1)
-    const bf16* vl = &sV[cur][0];
+    l += xhalf_sum(ps0 + ps1);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const f32x16& sp = (s < 2) ? s0 : s1;
       sx8 pb;
 #pragma unroll
       for (int j = 0; j < 8; ++j) pb[j] = bf16_bits(sp[8 * (s & 1) + j]);
-      o0 = mfma32(vt_frag(vl, VLD, (s >> 1) * 32, 0, s & 1, lane), pb, o0);
-      o1 = mfma32(vt_frag(vl, VLD, (s >> 1) * 32, 1, s & 1, lane), pb, o1);
+      o0 = mfma32(vt_frag_swz(&sV[cur][0], (s >> 1) * 32, 0, s & 1, lane), pb, o0);
+      o1 = mfma32(vt_frag_swz(&sV[cur][0], (s >> 1) * 32, 1, s & 1, lane), pb, o1);
     }
   };
-
   gload(0);
   sstore(0);
   __syncthreads();
-  const int kdiag = q0 / A_BK;  // first tile that can hold a key > some query of this block
+  const int kdiag = q0 / A_BK;
   auto step = [&](int kt, auto cur_c, auto mask_c) {
     constexpr int cur = decltype(cur_c)::value;
     if (kt + 1 < nkt) gload(kt + 1);
@@ -239,12 +224,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     __syncthreads();
   };
   int kt = 0;
-  for (; kt + 1 < kdiag; kt += 2) {  // unrolled by two so the LDS buffer is a constant
+  for (; kt + 1 < kdiag; kt += 2) {
     step(kt, I0{}, std::false_type{});
     step(kt + 1, I1{}, std::false_type{});
   }
   if (kt < kdiag) step(kt++, I0{}, std::false_type{});
-  for (; kt < nkt; ++kt) {  // the (at most two) diagonal tiles
+  for (; kt < nkt; ++kt) {
     if (kt & 1)
       step(kt, I1{}, std::true_type{});
     else
@@ -294,7 +279,8 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const bf16* __restr
 // dQ (query-parallel; same tiling as the forward): per 32-key sub-tile
 //   S^T = K Q^T, P^T = exp2(S^T c - lse), dP^T = V dO^T, dS^T = P^T (dP^T - delta),
 //   dQ^T += K^T dS^T  (A = K^T through ds_read_b64_tr_b16, B = dS^T from the accumulator)
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_bwd_dq_d64_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+template <int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) attn_bwd_dq_d64_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                                int B, int T, int H, float scale, float scale_log2) {
@@ -420,7 +406,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 //   B operands = the bf16-converted accumulators; the keys stay on the lanes throughout)
 constexpr int B_BQ = 64;  // queries per LDS tile
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_bwd_dkdv_d64_kernel(const bf16* __restrict__ qkv,
+template <int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) attn_bwd_dkdv_d64_kernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ lse,
                                                                  const float* __restrict__ delta,
@@ -572,21 +559,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 
 using namespace vcx;
 
+// Occupancy: forward 3 waves per SIMD (measured at the GPT-2 bench shape B=64 H=12 T=1024, one
+// process, interleaved rounds: 0.228 ms vs 0.244 at 2 and 0.312 at 4, where the 128-VGPR cap
+// spills); both backward kernels 2 (at 3-4 they spill: dq 0.87-1.25 ms vs 0.64 for the pair).
+static int g_fwd_wpe = 3;
+
+void vcx_attn_set_variant(int fwd_wpe) {
+  if (fwd_wpe == 2 || fwd_wpe == 3) g_fwd_wpe = fwd_wpe;
+}
+
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
                       int B, int T, int H, float scale, hipStream_t s) {
   const int64_t rows = (int64_t)B * T * H;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 31) / 32), dim3(256), 0, s, (const bf16*)out,
                      (const bf16*)dout, delta, B, T, H);
   const int nkb = (T + 127) / 128;
-  hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel, dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
+  hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel<2>, dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
                      (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
   const int nqt = (T + A_BQ - 1) / A_BQ;
-  hipLaunchKernelGGL(attn_bwd_dq_d64_kernel, dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv, (const bf16*)dout,
-                     lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+  hipLaunchKernelGGL(attn_bwd_dq_d64_kernel<2>, dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
+                     (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
 }
 
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s) {
   const int nqt = (T + A_BQ - 1) / A_BQ;
-  hipLaunchKernelGGL(attn_fwd_d64_kernel, dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B,
-                     T, H, scale * LOG2E);
+  const dim3 g(B * H * nqt);
+  if (g_fwd_wpe == 2)
+    hipLaunchKernelGGL(attn_fwd_d64_kernel<2>, g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H,
+                       scale * LOG2E);
+  else
+    hipLaunchKernelGGL(attn_fwd_d64_kernel<3>, g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H,
+                       scale * LOG2E);
 }

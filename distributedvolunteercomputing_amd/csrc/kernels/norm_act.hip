@@ -97,7 +97,11 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16* __restrict__ a,
 // ============================================================ LayerNorm backward
 // dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat)) + dres
 // per-wave partial dw = sum_rows dy*xhat, db = sum_rows dy -> part[(wave_global), C]
-template <int CH>
+// Each wave walks rows gw, gw + nw, ... with a one-row software pipeline: the next row's dy, x,
+// dres, mean and rstd loads are issued before this row's two cross-lane reductions, so every
+// lane keeps (2 or 3) x CH 16-B loads in flight through the shuffles (the row loop is otherwise
+// latency-bound at ~3.5 TB/s). RES is a template flag so no load sits behind a runtime branch.
+template <int CH, bool RES>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                       const bf16* __restrict__ w, const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in,
@@ -126,21 +130,38 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
       for (int j = 0; j < 8; ++j) wreg[k][j] = (float)wv[j];
     }
   }
-  for (int row = gw; row < R; row += nw) {
+  bf16x8 cd[CH], cx[CH], cr[CH];
+  float cmean = 0.f, crstd = 0.f;
+  auto load = [&](int row, bf16x8(&d)[CH], bf16x8(&xv)[CH], bf16x8(&rv)[CH], float& mu, float& rs) {
     const int64_t off = (int64_t)row * C;
-    const float mean = mean_in[row], rstd = rstd_in[row];
+    mu = mean_in[row];
+    rs = rstd_in[row];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int c = lane + k * 64;
+      if (c < C8) {
+        d[k] = *(const bf16x8*)(dy + off + c * 8);
+        xv[k] = *(const bf16x8*)(x + off + c * 8);
+        if (RES) rv[k] = *(const bf16x8*)(dres + off + c * 8);
+      }
+    }
+  };
+  if (gw < R) load(gw, cd, cx, cr, cmean, crstd);
+  for (int row = gw; row < R; row += nw) {
+    bf16x8 nd[CH], nx[CH], nr[CH];
+    float nmean = 0.f, nrstd = 0.f;
+    if (row + nw < R) load(row + nw, nd, nx, nr, nmean, nrstd);
+    const int64_t off = (int64_t)row * C;
     float xh[CH][8], g[CH][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       const int c = lane + k * 64;
       if (c < C8) {
-        bf16x8 dv = *(const bf16x8*)(dy + off + c * 8);
-        bf16x8 xv = *(const bf16x8*)(x + off + c * 8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float d = (float)dv[j];
-          xh[k][j] = ((float)xv[j] - mean) * rstd;
+          const float d = (float)cd[k][j];
+          xh[k][j] = ((float)cx[k][j] - cmean) * crstd;
           g[k][j] = d * wreg[k][j];
           s1 += g[k][j];
           s2 = fmaf(g[k][j], xh[k][j], s2);
@@ -156,21 +177,23 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
       const int c = lane + k * 64;
       if (c < C8) {
         bf16x8 o;
-        float rvf[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (dres) {
-          bf16x8 rv = *(const bf16x8*)(dres + off + c * 8);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) rvf[j] = (float)rv[j];
-        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float v = rstd * (g[k][j] - s1 - xh[k][j] * s2) + rvf[j];
+          const float v = crstd * (g[k][j] - s1 - xh[k][j] * s2) + (RES ? (float)cr[k][j] : 0.f);
           o[j] = (bf16)v;
           dxacc[k][j] += v;
         }
         *(bf16x8*)(dx + off + c * 8) = o;
       }
     }
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      cd[k] = nd[k];
+      cx[k] = nx[k];
+      if (RES) cr[k] = nr[k];
+    }
+    cmean = nmean;
+    crstd = nrstd;
   }
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
@@ -290,6 +313,35 @@ __global__ void __launch_bounds__(TPB) bias_gelu_bwd_kernel(const bf16* __restri
 
 
 
+// Column partial sums of a bf16 [R, F] matrix (the bias gradient of a token-major GEMM output):
+// same geometry as bias_gelu_bwd without the GELU, 4 rows' 16-B loads in flight per thread.
+template <int TPB>
+__global__ void __launch_bounds__(TPB) colsum_part_bf16_kernel(const bf16* __restrict__ y, float* __restrict__ part,
+                                                               int R, int F) {
+  const int c8 = blockIdx.x * TPB + threadIdx.x;
+  if (c8 * 8 >= F) return;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int G = gridDim.y;
+  int r = blockIdx.y;
+  for (; r + 3 * G < R; r += 4 * G) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *(const bf16x8*)(y + (int64_t)(r + u * G) * F + c8 * 8);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (float)v[u][j];
+  }
+  for (; r < R; r += G) {
+    bf16x8 v = *(const bf16x8*)(y + (int64_t)r * F + c8 * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+  }
+  float* p = part + (int64_t)blockIdx.y * F + c8 * 8;
+  *(f32x4*)p = f32x4{acc[0], acc[1], acc[2], acc[3]};
+  *(f32x4*)(p + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+}
+
 // Two-stage column sums of up to three [P, C] fp32 partial buffers -> bf16 [C] each, in two
 // launches for all outputs together. Stage 1: grid (C/64, NB, nout) -- every block reduces
 // P/NB rows of 64 columns (4 waves, LDS combine) into stage[out][NB][C]; stage 2: NB rows -> bf16.
@@ -320,14 +372,21 @@ __global__ void __launch_bounds__(256) colsum_stage1_kernel(const float* __restr
 
 __global__ void __launch_bounds__(64) colsum_stage2_kernel(const float* __restrict__ stage, int NB, int C,
                                                            bf16* __restrict__ o0, bf16* __restrict__ o1,
-                                                           bf16* __restrict__ o2) {
+                                                           bf16* __restrict__ o2, int accum_mask) {
   const int out = blockIdx.y;
   const int c = blockIdx.x * 64 + threadIdx.x;
   if (c >= C) return;
   const float* st = stage + (int64_t)out * NB * C + c;
+  // NB is always VCX_COLSUM_NB: fully unrolled so all loads are in flight at once instead of a
+  // chain of dependent L2 round trips
+  float v[VCX_COLSUM_NB];
+#pragma unroll
+  for (int i = 0; i < VCX_COLSUM_NB; ++i) v[i] = st[(int64_t)i * C];
   float acc = 0.f;
-  for (int i = 0; i < NB; ++i) acc += st[(int64_t)i * C];
+#pragma unroll
+  for (int i = 0; i < VCX_COLSUM_NB; ++i) acc += v[i];
   bf16* o = out == 0 ? o0 : (out == 1 ? o1 : o2);
+  if ((accum_mask >> out) & 1) acc += (float)o[c];  // add into an existing (flat) gradient
   o[c] = (bf16)acc;
 }
 
@@ -617,11 +676,11 @@ void vcx_ln_fwd(const void* a, const void* b, void* xout, void* y, const void* w
 
 
 static void colsums(const float* p0, const float* p1, const float* p2, void* o0, void* o1, void* o2, int nout, int P,
-                    int C, float* stage, hipStream_t s) {
+                    int C, float* stage, hipStream_t s, int accum_mask = 0) {
   hipLaunchKernelGGL(colsum_stage1_kernel, dim3((C + 63) / 64, VCX_COLSUM_NB, nout), dim3(256), 0, s, p0, p1, p2,
                      stage, P, C);
   hipLaunchKernelGGL(colsum_stage2_kernel, dim3((C + 63) / 64, nout), dim3(64), 0, s, stage, VCX_COLSUM_NB, C,
-                     (bf16*)o0, (bf16*)o1, (bf16*)o2);
+                     (bf16*)o0, (bf16*)o1, (bf16*)o2, accum_mask);
 }
 
 static int bias_gelu_groups(int R) { return R < 1024 ? (R > 0 ? R : 1) : 1024; }
@@ -656,13 +715,13 @@ void vcx_bias_gelu_fwd(const void* x, const void* b, void* y, int R, int F, hipS
 }
 
 void vcx_bias_gelu_bwd(const void* x, const void* b, const void* dy, void* dx, float* part, void* db, int R, int F,
-                       float* stage, hipStream_t s) {
+                       float* stage, int accumulate, hipStream_t s) {
   const int G = bias_gelu_groups(R);
   const int tpb = bias_gelu_tpb(F);
   dim3 grid((F / 8 + tpb - 1) / tpb, G);
   VCX_TPB_DISPATCH(tpb, hipLaunchKernelGGL(bias_gelu_bwd_kernel<TPB>, grid, dim3(TPB), 0, s, (const bf16*)x,
                                            (const bf16*)b, (const bf16*)dy, (bf16*)dx, part, R, F));
-  colsums(part, nullptr, nullptr, db, nullptr, nullptr, 1, G, F, stage, s);
+  colsums(part, nullptr, nullptr, db, nullptr, nullptr, 1, G, F, stage, s, accumulate ? 1 : 0);
 }
 
 int vcx_ln_bwd_partials(int R) {
@@ -674,26 +733,46 @@ int vcx_ln_bwd_partials(int R) {
 
 void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
                 void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, float* dbb_part,
-                void* dbb, float* stage, hipStream_t s) {
+                void* dbb, float* stage, int accum_mask, hipStream_t s) {
   const int ch = (C / 8 + 63) / 64;
   const int P = vcx_ln_bwd_partials(R);
   dim3 grid(P / 4);
-  VCX_LN_DISPATCH(ch, hipLaunchKernelGGL(ln_bwd_kernel<CH>, grid, dim3(256), 0, s, (const bf16*)dy,
-                                         (const bf16*)x, (const bf16*)w, mean, rstd, (const bf16*)dres,
-                                         (bf16*)dx, dw_part, db_part, R, C, rms, dbb_part));
-  // dw, then db and dbb when present, in one pair of launches
+  if (dres) {
+    VCX_LN_DISPATCH(ch, hipLaunchKernelGGL((ln_bwd_kernel<CH, true>), grid, dim3(256), 0, s, (const bf16*)dy,
+                                           (const bf16*)x, (const bf16*)w, mean, rstd, (const bf16*)dres,
+                                           (bf16*)dx, dw_part, db_part, R, C, rms, dbb_part));
+  } else {
+    VCX_LN_DISPATCH(ch, hipLaunchKernelGGL((ln_bwd_kernel<CH, false>), grid, dim3(256), 0, s, (const bf16*)dy,
+                                           (const bf16*)x, (const bf16*)w, mean, rstd, (const bf16*)nullptr,
+                                           (bf16*)dx, dw_part, db_part, R, C, rms, dbb_part));
+  }
+  // dw, then db and dbb when present, in one pair of launches; accum_mask bit 0/1/2 = add dw/db/dbb
+  // into the existing output (a view of the flat gradient buffer) instead of overwriting it
   const float* ps[3] = {dw_part, nullptr, nullptr};
   void* os[3] = {dw, nullptr, nullptr};
+  int slot_mask = accum_mask & 1;
   int n = 1;
   if (db_part && db) {
+    slot_mask |= ((accum_mask >> 1) & 1) << n;
     ps[n] = db_part;
     os[n++] = db;
   }
   if (dbb_part && dbb) {
+    slot_mask |= ((accum_mask >> 2) & 1) << n;
     ps[n] = dbb_part;
     os[n++] = dbb;
   }
-  colsums(ps[0], ps[1], ps[2], os[0], os[1], os[2], n, P, C, stage, s);
+  colsums(ps[0], ps[1], ps[2], os[0], os[1], os[2], n, P, C, stage, s, slot_mask);
+}
+
+void vcx_colsum_bf16(const void* y, float* part, void* out, int R, int F, int accumulate, float* stage,
+                     hipStream_t s) {
+  const int G = bias_gelu_groups(R);
+  const int tpb = bias_gelu_tpb(F);
+  dim3 grid((F / 8 + tpb - 1) / tpb, G);
+  VCX_TPB_DISPATCH(tpb, hipLaunchKernelGGL(colsum_part_bf16_kernel<TPB>, grid, dim3(TPB), 0, s, (const bf16*)y, part,
+                                           R, F));
+  colsums(part, nullptr, nullptr, out, nullptr, nullptr, 1, G, F, stage, s, accumulate ? 1 : 0);
 }
 
 void vcx_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s) {

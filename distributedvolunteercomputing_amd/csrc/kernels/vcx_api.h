@@ -23,11 +23,14 @@ int vcx_bias_gelu_partials(int R);
 void vcx_bias_gelu_fwd(const void* x, const void* b, void* y, int R, int F, hipStream_t s);
 constexpr int VCX_COLSUM_NB = 32;  // stage-1 row chunks of the two-stage column sums (stage: 3 * NB * C fp32)
 void vcx_bias_gelu_bwd(const void* x, const void* b, const void* dy, void* dx, float* part, void* db, int R, int F,
-                       float* stage, hipStream_t s);
+                       float* stage, int accumulate, hipStream_t s);
+// column sums of a bf16 [R, F] matrix into out[F] (bf16; added to it when accumulate != 0)
+void vcx_colsum_bf16(const void* y, float* part, void* out, int R, int F, int accumulate, float* stage,
+                     hipStream_t s);
 int vcx_ln_bwd_partials(int R);
 void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
                 void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, float* dbb_part,
-                void* dbb, float* stage, hipStream_t s);
+                void* dbb, float* stage, int accum_mask, hipStream_t s);
 void vcx_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t s);
 void vcx_gelu_bwd(const void* x, const void* dy, void* dx, int64_t n, hipStream_t s);
 void vcx_swiglu_fwd(const void* gu, void* y, int64_t R, int F, hipStream_t s);
@@ -42,11 +45,15 @@ void vcx_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, cons
 
 // attention.hip (causal flash attention, head dim 64, packed qkv)
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s);
+// forward occupancy variant: 2 or 3 waves per SIMD (default 3)
+void vcx_attn_set_variant(int fwd_wpe);
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
                       int B, int T, int H, float scale, hipStream_t s);
 
 // embed.hip
 void vcx_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int64_t R, int T, int C, int V,
                    hipStream_t s);
-void vcx_embed_bwd(const int64_t* idx, const void* dx, float* dwte, float* dwpe, int64_t R, int T, int C, int V,
-                   hipStream_t s);
+// dwte (+)= scatter of dx over idx (fp32 atomics into the zeroed dwte_scratch, then added into the
+// bf16 dwte); dwpe (+)= per-position sums of dx over the batch (nullptr: no position table)
+void vcx_embed_bwd(const int64_t* idx, const void* dx, float* dwte_scratch, void* dwte, int accum_wte, void* dwpe,
+                   int accum_wpe, int64_t R, int T, int C, int V, hipStream_t s);

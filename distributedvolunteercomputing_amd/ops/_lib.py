@@ -50,6 +50,16 @@ def use_native(t) -> bool:
     return bool(getattr(t, "is_cuda", False))
 
 
+def grad_buffer(p):
+    """p.grad when it is a preset contiguous gradient buffer of p's shape/dtype (the flat-buffer
+    view installed by parallel/flat_params.py): backward kernels then ADD their result straight
+    into it and hand autograd ``None`` for that input, which skips autograd's accumulation pass."""
+    g = getattr(p, "grad", None) if p is not None else None
+    if g is not None and g.dtype == p.dtype and g.is_contiguous() and g.shape == p.shape and g.is_cuda:
+        return g
+    return None
+
+
 class reference_ops:
     """Context manager: run the plain-PyTorch reference path even for GPU tensors.
     Used ONLY by the numerics tests to build an oracle on the same device."""

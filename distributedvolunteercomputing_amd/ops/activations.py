@@ -4,7 +4,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from ._lib import native, use_native
+from ._lib import grad_buffer, native, use_native
 
 
 class _Gelu(torch.autograd.Function):
@@ -31,13 +31,16 @@ class _BiasGelu(torch.autograd.Function):
     def forward(ctx, x, b):
         x = x.contiguous()
         ctx.save_for_backward(x, b)
+        ctx.bias = b
         return native().bias_gelu_fwd(x, b)
 
     @staticmethod
     def backward(ctx, dy):
         x, b = ctx.saved_tensors
-        dx, db = native().bias_gelu_bwd(x, b, dy.contiguous())
-        return dx, db
+        gb = grad_buffer(ctx.bias)
+        ctx.bias = None
+        dx, db = native().bias_gelu_bwd(x, b, dy.contiguous(), gb)
+        return dx, (None if gb is not None else db)
 
 
 def bias_gelu(x, b):

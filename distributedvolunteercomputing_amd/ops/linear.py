@@ -18,7 +18,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from ._lib import native, use_native
+from ._lib import grad_buffer, native, use_native
 
 MIN_ROWS_PER_SPLIT = 2048
 
@@ -60,6 +60,7 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        ctx.bias = b
         return F.linear(x, w, b)
 
     @staticmethod
@@ -77,7 +78,14 @@ class _Linear(torch.autograd.Function):
             else:
                 dw = wgrad(dy2, x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy2.sum(0, dtype=torch.float32).to(dy.dtype)
+            gb = grad_buffer(ctx.bias)
+            if gb is not None and (N % 8) == 0:
+                native().colsum_bf16(dy2.contiguous(), gb)  # HIP column sums added into the flat .grad
+            elif (N % 8) == 0:
+                db = native().colsum_bf16(dy2.contiguous())
+            else:
+                db = dy2.sum(0, dtype=torch.float32).to(dy.dtype)
+        ctx.bias = None
         return dx, dw, db
 
 

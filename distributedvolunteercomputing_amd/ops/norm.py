@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import torch
 
-from ._lib import native, use_native
+from ._lib import grad_buffer, native, use_native
 
 
 def _ref_ln(x, w, b, eps, rms):
@@ -35,6 +35,7 @@ class _AddLN(torch.autograd.Function):
         C = native()
         y, x, mean, rstd = C.ln_fwd(a.contiguous(), None if b is None else b.contiguous(), w, bias, eps, rms, bb)
         ctx.save_for_backward(x, w, mean, rstd)
+        ctx.params = (w, bias, bb)  # for their preset .grad buffers (not saved tensors: never modified)
         ctx.has_b = b is not None
         ctx.has_bias = bias is not None
         ctx.has_bb = bb is not None
@@ -48,7 +49,14 @@ class _AddLN(torch.autograd.Function):
         x, w, mean, rstd = ctx.saved_tensors
         C = native()
         dres = None if dx_res is None else dx_res.contiguous()
-        dx, dw, dbias, dbb = C.ln_bwd(dy.contiguous(), x, w, mean, rstd, dres, ctx.has_bias, ctx.rms, ctx.has_bb)
+        pw, pbias, pbb = ctx.params
+        gw, gb, gbb = grad_buffer(pw), grad_buffer(pbias) if ctx.has_bias else None, grad_buffer(pbb) if ctx.has_bb else None
+        dx, dw, dbias, dbb = C.ln_bwd(dy.contiguous(), x, w, mean, rstd, dres, ctx.has_bias, ctx.rms, ctx.has_bb,
+                                      gw, gb, gbb)
+        # parameter gradients already added into preset buffers are not handed to autograd again
+        dw = None if gw is not None else dw
+        dbias = None if gb is not None else dbias
+        dbb = None if gbb is not None else dbb
         return dx, (dx if ctx.has_b else None), dw, dbias, None, None, dbb
 
 

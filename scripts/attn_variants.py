@@ -1,0 +1,54 @@
+"""A/B of the attention forward occupancy variants (2 vs 3 waves per SIMD) plus the backward in ONE process (GPT-2-small bench shape:
+B=64, H=12, T=1024, D=64), interleaved rounds, median times; outputs checked against the
+default variant."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from distributedvolunteercomputing_amd import ops  # noqa: E402
+from distributedvolunteercomputing_amd.ops import native  # noqa: E402
+
+C = native()
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+H, T, D = 12, 1024, 64
+dev = "cuda"
+torch.manual_seed(0)
+qkv = torch.randn(B, T, 3, H, D, device=dev, dtype=torch.bfloat16)
+dO = torch.randn(B, T, H, D, device=dev, dtype=torch.bfloat16)
+scale = D ** -0.5
+fl = 4 * B * H * T * T * D / 2
+
+
+def tm(fn, it=10):
+    ts = []
+    for _ in range(it):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return sorted(ts)[len(ts) // 2]
+
+
+C.attn_set_variant(2)
+o_ref, lse_ref = C.attn_fwd(qkv, scale)
+g_ref = C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)
+torch.cuda.synchronize()
+res = {}
+for rnd in range(3):
+    for fv in (2, 3):
+        C.attn_set_variant(fv)
+        o, l = C.attn_fwd(qkv, scale)
+        if rnd == 0:
+            err = (o.float() - o_ref.float()).abs().max().item()
+            print(f"fwd variant {fv}: max|o - o_ref| = {err:.3e}", flush=True)
+        res.setdefault(("fwd", fv), []).append(tm(lambda: C.attn_fwd(qkv, scale)))
+    C.attn_set_variant(3)
+    res.setdefault(("bwd",), []).append(tm(lambda: C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)))
+for k, v in res.items():
+    ms = sorted(v)[len(v) // 2]
+    f = fl if k[0] == "fwd" else 2.5 * fl
+    print(f"{str(k):16s} {ms:7.3f} ms  {f / ms / 1e9:7.1f} TF/s   rounds {['%.3f' % x for x in v]}", flush=True)

@@ -242,3 +242,79 @@ def test_linear_splitm_wgrad(gpu, M, N, K, bias, preset_grad):
     assert rel(w.grad, ref_w) < 1e-2, rel(w.grad, ref_w)
     if bias:
         assert rel(b.grad, br.grad) < 1e-2
+
+
+def test_layernorm_grads_accumulate_into_preset_buffers(gpu):
+    """With preset .grad buffers (the flat-buffer case) the LN parameter gradients are ADDED into
+    them by the HIP column sums (autograd gets None for those inputs)."""
+    torch.manual_seed(11)
+    R, C = 513, 768
+    a = _bf(torch.randn(R, C, device=gpu)).requires_grad_()
+    b = _bf(torch.randn(R, C, device=gpu)).requires_grad_()
+    w = _bf(torch.rand(C, device=gpu) + 0.5).requires_grad_()
+    bias = _bf(torch.randn(C, device=gpu) * 0.1).requires_grad_()
+    bb = _bf(torch.randn(C, device=gpu)).requires_grad_()
+    g0 = {n: _bf(torch.randn(C, device=gpu)) for n in ("w", "bias", "bb")}
+    w.grad, bias.grad, bb.grad = g0["w"].clone(), g0["bias"].clone(), g0["bb"].clone()
+    y, x = ops.add_layernorm(a, b, w, bias, branch_bias=bb)
+    dy, dxr = torch.randn(R, C, device=gpu), torch.randn(R, C, device=gpu)
+    ((y.float() * dy).sum() + (x.float() * dxr).sum()).backward()
+    a32, b32, w32, bias32, bb32 = (t.detach().float().requires_grad_() for t in (a, b, w, bias, bb))
+    xr = a32 + b32 + bb32
+    yr = F.layer_norm(xr, (C,), w32, bias32, 1e-5)
+    ((yr * dy).sum() + (xr * dxr).sum()).backward()
+    for p, r, n in ((w, w32, "w"), (bias, bias32, "bias"), (bb, bb32, "bb")):
+        ref = r.grad + g0[n].float()
+        assert float((p.grad.float() - ref).norm() / ref.norm()) < 1e-2, n
+    assert float((a.grad.float() - a32.grad).norm() / a32.grad.norm()) < 2e-2
+
+
+@pytest.mark.parametrize("R,F_", [(65536, 2304), (1000, 768), (7, 64)])
+def test_colsum_bf16(gpu, R, F_):
+    torch.manual_seed(12)
+    y = _bf(torch.randn(R, F_, device=gpu))
+    C = ops.native()
+    out = C.colsum_bf16(y)
+    ref = y.float().sum(0)
+    assert float((out.float() - ref).norm() / ref.norm()) < 1e-2
+    acc = _bf(torch.randn(F_, device=gpu))
+    ref2 = ref + acc.float()
+    C.colsum_bf16(y, acc)
+    assert float((acc.float() - ref2).norm() / ref2.norm()) < 1e-2
+
+
+def test_embedding_grads_accumulate_into_preset_buffers(gpu):
+    torch.manual_seed(13)
+    V, C, B, T = 1000, 768, 8, 100
+    idx = torch.randint(0, V, (B, T), device=gpu)
+    wte = _bf(torch.randn(V, C, device=gpu)).requires_grad_()
+    wpe = _bf(torch.randn(128, C, device=gpu)).requires_grad_()
+    g_te, g_pe = _bf(torch.randn(V, C, device=gpu)), _bf(torch.randn(128, C, device=gpu))
+    wte.grad, wpe.grad = g_te.clone(), g_pe.clone()
+    x = ops.embed(idx, wte, wpe)
+    dy = torch.randn(B, T, C, device=gpu)
+    (x.float() * dy).sum().backward()
+    w32, p32 = wte.detach().float().requires_grad_(), wpe.detach().float().requires_grad_()
+    (((F.embedding(idx, w32) + p32[:T]) * dy).sum()).backward()
+    assert torch.allclose(wte.grad.float(), w32.grad + g_te.float(), atol=6e-2, rtol=2e-2)
+    assert torch.allclose(wpe.grad.float(), p32.grad + g_pe.float(), atol=2e-1, rtol=2e-2)
+
+
+def test_gelu_mlp_matches_reference(gpu):
+    """ops.gelu_mlp (hipBLASLt GELU epilogues when available, else GEMM + HIP bias-GELU) vs fp32."""
+    torch.manual_seed(14)
+    M, C, Fd = 2048, 256, 1024
+    h = _bf(torch.randn(M, C, device=gpu)).requires_grad_()
+    w1 = _bf(torch.randn(Fd, C, device=gpu) * 0.05).requires_grad_()
+    b1 = _bf(torch.randn(Fd, device=gpu) * 0.5).requires_grad_()
+    w2 = _bf(torch.randn(C, Fd, device=gpu) * 0.05).requires_grad_()
+    y = ops.gelu_mlp(h, w1, b1, w2)
+    dy = torch.randn(M, C, device=gpu)
+    (y.float() * dy).sum().backward()
+    h32, w132, b132, w232 = (t.detach().float().requires_grad_() for t in (h, w1, b1, w2))
+    yr = F.linear(F.gelu(F.linear(h32, w132, b132), approximate="tanh"), w232)
+    (yr * dy).sum().backward()
+    rel = lambda a, r: float((a.float() - r).norm() / r.norm())  # noqa: E731
+    assert rel(y, yr) < 2e-2
+    for p, r in ((h, h32), (w1, w132), (b1, b132), (w2, w232)):
+        assert rel(p.grad, r.grad) < 3e-2
