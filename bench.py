@@ -28,6 +28,7 @@ import torch  # noqa: E402
 import torch.distributed as dist
 
 from distributedvolunteercomputing_amd.models.gpt2 import GPT2, GPT2Config
+from distributedvolunteercomputing_amd.ops.linear import gemm_choices
 from distributedvolunteercomputing_amd.parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer
 from distributedvolunteercomputing_amd.parallel.peer_group import PeerGroup
 
@@ -142,6 +143,8 @@ def main():
             "sync_ms": round(trainer.last_sync_ms, 3),
             "tuned_gemms": TUNED_GEMMS,
             "hipgraph": graphed,
+            "gemm_lt_shapes": sum(1 for v in gemm_choices().values() if v == "lt"),
+            "gemm_shapes": len(gemm_choices()),
         }
         line = json.dumps(rec)
         print(line, flush=True)

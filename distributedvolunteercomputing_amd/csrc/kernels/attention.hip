@@ -41,10 +41,21 @@ __device__ __forceinline__ sx4 lds_tr_b64(const bf16* p) {
 
 // v_max3_f32 without the canonicalising v_max_f32 the compiler puts in front of fmaxf on MFMA
 // results (scores are never NaN here)
+// CAUTION: hipcc pads hazards only around instructions it generates itself, never for an asm
+// statement (guide §5.7 item 2). Reading an MFMA's D from inside asm without the MFMA->VALU wait
+// states returns stale partial sums on some waves of some launches (seen as run-to-run 1-ulp
+// output differences: a wrong running max only changes the rounding). Every max3 over raw score
+// accumulators is therefore preceded by mfma_read_fence.
 __device__ __forceinline__ float max3(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
+}
+
+// 18 wait states (a 16-pass v_mfma_f32_32x32x16_bf16's D -> VALU read); the "+v" operands order
+// this statement after both score MFMA chains and before the asm max3 that read them
+__device__ __forceinline__ void mfma_read_fence(f32x16& a, f32x16& b) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 1" : "+v"(a), "+v"(b));
 }
 
 __device__ __forceinline__ f32x16 mfma32(sx8 a, sx8 b, f32x16 c) {
@@ -108,12 +119,20 @@ __device__ __forceinline__ float xhalf_sum(float v) {
 // to 128 VGPRs so FOUR blocks (16 waves, 4 per SIMD) share a CU: the per-tile chain (K reads ->
 // S MFMAs -> max -> exp -> P -> V^T reads -> PV MFMAs -> barrier) is serial inside a wave, so the
 // SIMD needs more waves to overlap one wave's softmax with another's MFMAs.
-template <int WPE>
+//
+// DMA = true stages K/V with LDS-DMA (global_load_lds_dwordx4: no staging registers, no ds_write
+// pass; the swizzle moves to the per-lane SOURCE address since the DMA writes each wave's 1-KB
+// piece linearly) instead of global_load -> VGPR -> ds_write.
+template <int WPE, bool DMA>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int B, int T, int H,
                     float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 sK[2][A_BK * AD];  // swizzled (swz)
-  __shared__ __attribute__((aligned(16))) bf16 sV[2][A_BK * AD];
+  // one shared object per buffer, so the compiler can tell that the LDS-DMA into one buffer
+  // does not alias the reads of the other (else it waits vmcnt(0) before every V^T read)
+  __shared__ __attribute__((aligned(16))) bf16 sKV0[2][A_BK * AD];  // [K | V], swizzled (swz)
+  __shared__ __attribute__((aligned(16))) bf16 sKV1[2][A_BK * AD];
+#define sK_(b) ((b) ? &sKV1[0][0] : &sKV0[0][0])
+#define sV_(b) ((b) ? &sKV1[1][0] : &sKV0[1][0])
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
   const int nqt = (T + A_BQ - 1) / A_BQ;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -136,21 +155,41 @@ attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
   const int kend = min(T, q0 + A_BQ);
   const int nkt = (kend + A_BK - 1) / A_BK;
   sx8 rk[2], rv[2];
-  auto gload = [&](int kt) {
+  // register staging: load tile kt into rk/rv (sstore writes them to buffer buf later);
+  // DMA staging: tile kt goes straight into buffer buf (sstore is a no-op)
+  auto gload = [&](int kt, int buf) {
+    if constexpr (DMA) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
-      const int key = min(kt * A_BK + r, T - 1);
-      rk[i] = *(const sx8*)(Kg + (int64_t)key * tok + c);
-      rv[i] = *(const sx8*)(Vg + (int64_t)key * tok + c);
+      for (int i = 0; i < 2; ++i) {
+        const int piece = w * 2 + i;               // wave-uniform 1-KB piece of the 8-KB image
+        const int p = piece * 64 + lane;           // this lane's 16-B slot in the image
+        const int r = p >> 3, k = (r >> 1) & 7;
+        const int chunk = (p & 7) ^ (((k & 1) << 2) | (k >> 1));  // global chunk stored in slot p
+        const int key = min(kt * A_BK + r, T - 1);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(Kg + (int64_t)key * tok + chunk * 8),
+                                         (__attribute__((address_space(3))) void*)(sK_(buf) + piece * 512), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(Vg + (int64_t)key * tok + chunk * 8),
+                                         (__attribute__((address_space(3))) void*)(sV_(buf) + piece * 512), 16, 0, 0);
+      }
+    } else {
+      (void)buf;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
+        const int key = min(kt * A_BK + r, T - 1);
+        rk[i] = *(const sx8*)(Kg + (int64_t)key * tok + c);
+        rv[i] = *(const sx8*)(Vg + (int64_t)key * tok + c);
+      }
     }
   };
   auto sstore = [&](int buf) {
+    if constexpr (!DMA) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = tid + i * 256, r = e >> 3;
-      *(sx8*)(&sK[buf][swz(r, e & 7)]) = rk[i];
-      *(sx8*)(&sV[buf][swz(r, e & 7)]) = rv[i];
+      for (int i = 0; i < 2; ++i) {
+        const int e = tid + i * 256, r = e >> 3;
+        *(sx8*)(sK_(buf) + swz(r, e & 7)) = rk[i];
+        *(sx8*)(sV_(buf) + swz(r, e & 7)) = rv[i];
+      }
     }
   };
   auto tile = [&](int kt, auto cur_c, auto mask_c) {
@@ -161,9 +200,10 @@ attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
     f32x16 s0 = {}, s1 = {};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      s0 = mfma32(row_frag_swz(&sK[cur][0], col, s, h2), qf[s], s0);
-      s1 = mfma32(row_frag_swz(&sK[cur][0], 32 + col, s, h2), qf[s], s1);
+      s0 = mfma32(row_frag_swz(sK_(cur), col, s, h2), qf[s], s0);
+      s1 = mfma32(row_frag_swz(sK_(cur), 32 + col, s, h2), qf[s], s1);
     }
+    mfma_read_fence(s0, s1);
     if (MASK) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -208,17 +248,26 @@ attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
       sx8 pb;
 #pragma unroll
       for (int j = 0; j < 8; ++j) pb[j] = bf16_bits(sp[8 * (s & 1) + j]);
-      o0 = mfma32(vt_frag_swz(&sV[cur][0], (s >> 1) * 32, 0, s & 1, lane), pb, o0);
-      o1 = mfma32(vt_frag_swz(&sV[cur][0], (s >> 1) * 32, 1, s & 1, lane), pb, o1);
+      o0 = mfma32(vt_frag_swz(sV_(cur), (s >> 1) * 32, 0, s & 1, lane), pb, o0);
+      o1 = mfma32(vt_frag_swz(sV_(cur), (s >> 1) * 32, 1, s & 1, lane), pb, o1);
     }
   };
-  gload(0);
+  gload(0, 0);
   sstore(0);
   __syncthreads();
+  // Retire EVERY outstanding global load (the per-lane Q/dO/K/V fragments loaded at kernel entry
+  // included) before the tile loop. hipcc issues those fragment loads after the first tile's
+  // staging loads and does not wait for them in the prologue; the waitcnt pass then merges that
+  // pending state into the loop header and makes every iteration wait vmcnt(3..0) for its own
+  // next-tile prefetch before the first MFMA that reads a fragment register — serialising the
+  // prefetch with the compute (seen in the forward's ISA). The builtin (not inline asm: the
+  // waitcnt pass cannot see into an asm statement) is vmcnt(0) with expcnt/lgkmcnt at their
+  // maxima in the gfx9 encoding: vmcnt[3:0] = 0, expcnt[6:4] = 7, lgkmcnt[11:8] = 15.
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   const int kdiag = q0 / A_BK;
   auto step = [&](int kt, auto cur_c, auto mask_c) {
     constexpr int cur = decltype(cur_c)::value;
-    if (kt + 1 < nkt) gload(kt + 1);
+    if (kt + 1 < nkt) gload(kt + 1, cur ^ 1);
     tile(kt, cur_c, mask_c);
     if (kt + 1 < nkt) sstore(cur ^ 1);
     __syncthreads();
@@ -250,6 +299,8 @@ attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
     }
     if (h2 == 0) lse[((int64_t)b * H + hh) * T + q] = m + __log2f(l);
   }
+#undef sK_
+#undef sV_
 }
 
 // ============================================================================ backward
@@ -365,6 +416,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   gload(0);
   sstore(0);
   __syncthreads();
+  // Retire EVERY outstanding global load (the per-lane Q/dO/K/V fragments loaded at kernel entry
+  // included) before the tile loop. hipcc issues those fragment loads after the first tile's
+  // staging loads and does not wait for them in the prologue; the waitcnt pass then merges that
+  // pending state into the loop header and makes every iteration wait vmcnt(3..0) for its own
+  // next-tile prefetch before the first MFMA that reads a fragment register — serialising the
+  // prefetch with the compute (seen in the forward's ISA). The builtin (not inline asm: the
+  // waitcnt pass cannot see into an asm statement) is vmcnt(0) with expcnt/lgkmcnt at their
+  // maxima in the gfx9 encoding: vmcnt[3:0] = 0, expcnt[6:4] = 7, lgkmcnt[11:8] = 15.
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   const int kdiag = q0 / A_BK;
   auto step = [&](int kt, auto cur_c, auto mask_c) {
     constexpr int cur = decltype(cur_c)::value;
@@ -519,6 +579,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   gload(qstart);
   sstore(0);
   __syncthreads();
+  // Retire EVERY outstanding global load (the per-lane Q/dO/K/V fragments loaded at kernel entry
+  // included) before the tile loop. hipcc issues those fragment loads after the first tile's
+  // staging loads and does not wait for them in the prologue; the waitcnt pass then merges that
+  // pending state into the loop header and makes every iteration wait vmcnt(3..0) for its own
+  // next-tile prefetch before the first MFMA that reads a fragment register — serialising the
+  // prefetch with the compute (seen in the forward's ISA). The builtin (not inline asm: the
+  // waitcnt pass cannot see into an asm statement) is vmcnt(0) with expcnt/lgkmcnt at their
+  // maxima in the gfx9 encoding: vmcnt[3:0] = 0, expcnt[6:4] = 7, lgkmcnt[11:8] = 15.
+  __builtin_amdgcn_s_waitcnt(0x0F70);
   auto step = [&](int qt, auto cur_c, auto mask_c) {
     constexpr int cur = decltype(cur_c)::value;
     if (qt + 1 < nqt) gload(qt + 1);
@@ -559,13 +628,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
 
 using namespace vcx;
 
-// Occupancy: forward 3 waves per SIMD (measured at the GPT-2 bench shape B=64 H=12 T=1024, one
-// process, interleaved rounds: 0.228 ms vs 0.244 at 2 and 0.312 at 4, where the 128-VGPR cap
-// spills); both backward kernels 2 (at 3-4 they spill: dq 0.87-1.25 ms vs 0.64 for the pair).
-static int g_fwd_wpe = 3;
+// Forward default: LDS-DMA staging at 3 waves per SIMD. Measured at the GPT-2 bench shape
+// (B=64 H=12 T=1024, one process, interleaved rounds; scripts/attn_variants.py): 0.211 ms, vs
+// 0.223 DMA at 2 waves/SIMD, 0.237 register staging at 2 and 0.266 register staging at 3 (spills).
+// Backward kernels: 2 waves per SIMD (at 3-4 they spill: dq 0.87-1.25 ms vs 0.64 for the pair).
+static int g_fwd_wpe = 3, g_fwd_dma = 1;
 
-void vcx_attn_set_variant(int fwd_wpe) {
+void vcx_attn_set_variant(int fwd_wpe, int fwd_dma) {
   if (fwd_wpe == 2 || fwd_wpe == 3) g_fwd_wpe = fwd_wpe;
+  if (fwd_dma == 0 || fwd_dma == 1) g_fwd_dma = fwd_dma;
 }
 
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
@@ -584,10 +655,13 @@ void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const 
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s) {
   const int nqt = (T + A_BQ - 1) / A_BQ;
   const dim3 g(B * H * nqt);
-  if (g_fwd_wpe == 2)
-    hipLaunchKernelGGL(attn_fwd_d64_kernel<2>, g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H,
-                       scale * LOG2E);
-  else
-    hipLaunchKernelGGL(attn_fwd_d64_kernel<3>, g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H,
-                       scale * LOG2E);
+#define VCX_FWD(W, D)                                                                                      \
+  hipLaunchKernelGGL((attn_fwd_d64_kernel<W, D>), g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H, \
+                     scale * LOG2E)
+  if (g_fwd_dma) {
+    if (g_fwd_wpe == 2) VCX_FWD(2, true); else VCX_FWD(3, true);
+  } else {
+    if (g_fwd_wpe == 2) VCX_FWD(2, false); else VCX_FWD(3, false);
+  }
+#undef VCX_FWD
 }

@@ -45,8 +45,8 @@ void vcx_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, cons
 
 // attention.hip (causal flash attention, head dim 64, packed qkv)
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s);
-// forward occupancy variant: 2 or 3 waves per SIMD (default 3)
-void vcx_attn_set_variant(int fwd_wpe);
+// forward variant: 2 or 3 waves per SIMD (default 3); K/V staging through registers (0) or LDS-DMA (1)
+void vcx_attn_set_variant(int fwd_wpe, int fwd_dma);
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
                       int B, int T, int H, float scale, hipStream_t s);
 

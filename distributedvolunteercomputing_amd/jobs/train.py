@@ -107,6 +107,8 @@ def parse(argv=None):
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--log-every", type=int, default=10)
     ap.add_argument("--metrics", default=None, help="JSONL metrics file")
+    ap.add_argument("--trace-dir", default=os.environ.get("VCX_TRACE_DIR"),
+                    help="write per-stage device-time spans (HIP events) as JSONL here")
     return ap.parse_args(argv)
 
 
@@ -177,6 +179,11 @@ def main(argv=None):
             tr.restore(ShardReader(d))
             print(f"[peer {rank}] resumed from {d} at step {tr.t}", flush=True)
 
+    tracer = None
+    if a.trace_dir and hasattr(tr, "tracer"):
+        from ..utils.trace import SpanTracer
+
+        tracer = tr.tracer = SpanTracer(f"peer{rank}", path=os.path.join(a.trace_dir, f"peer{rank}.jsonl"))
     data = SyntheticData(a.model, model, a.batch, a.seq, device, seed=1000 + rank)
     log = open(a.metrics, "a") if a.metrics else None
     t_last = time.perf_counter()
@@ -189,6 +196,8 @@ def main(argv=None):
             os._exit(0)
         x, y = data(step)
         out = tr.step(x, y)
+        if tracer is not None and (step + 1) % a.log_every == 0:
+            tracer.flush(step=step + 1, peer=rank)
         loss = out.extra["loss_t"] if hasattr(out, "extra") else out
         step += 1
         if a.ckpt_dir and a.ckpt_every and step % a.ckpt_every == 0 and (

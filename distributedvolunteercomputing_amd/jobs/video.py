@@ -19,6 +19,7 @@ import torch
 
 from .. import _native_loader
 from ..ops import vision as V
+from ..utils.trace import NULL_TRACER
 
 PERSON = 15
 
@@ -52,6 +53,7 @@ class DetectorEngine(Engine):
         self.consider = consider
         self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self._lock = threading.Lock()
+        self.tracer = NULL_TRACER  # set a utils.trace.SpanTracer for per-stage device times
 
     @torch.no_grad()
     def process(self, frames, requester):
@@ -79,21 +81,26 @@ class DetectorEngine(Engine):
         return buf[:nbytes]
 
     def _run(self, frames, requester):
-        if isinstance(frames, torch.Tensor):
-            x = frames.to(self.device)
-        else:
-            a = np.ascontiguousarray(frames)
-            if self.device.type == "cuda":
-                st = self._staging(a.nbytes)
-                torch.cuda.current_stream().synchronize()  # previous chunk's H2D done before reuse
-                st.numpy()[:] = a.reshape(-1)
-                x = st.view(a.shape).to(self.device, non_blocking=True)
+        tr = self.tracer
+        with tr.span("h2d"):
+            if isinstance(frames, torch.Tensor):
+                x = frames.to(self.device)
             else:
-                x = torch.from_numpy(a)
-        small = V.resize_width(x, self.width).contiguous()
-        dets, cnt = self.exec.detect(small)
-        counts = V.annotate(small, dets, cnt, requester, label=self.label, cls_name=self.consider,
-                            thresh=self.conf_thresh)
+                a = np.ascontiguousarray(frames)
+                if self.device.type == "cuda":
+                    st = self._staging(a.nbytes)
+                    torch.cuda.current_stream().synchronize()  # previous chunk's H2D done before reuse
+                    st.numpy()[:] = a.reshape(-1)
+                    x = st.view(a.shape).to(self.device, non_blocking=True)
+                else:
+                    x = torch.from_numpy(a)
+        with tr.span("resize"):
+            small = V.resize_width(x, self.width).contiguous()
+        with tr.span("detect"):  # preprocess + MobileNet-SSD forward + decode/NMS
+            dets, cnt = self.exec.detect(small)
+        with tr.span("annotate"):
+            counts = V.annotate(small, dets, cnt, requester, label=self.label, cls_name=self.consider,
+                                thresh=self.conf_thresh)
         return small, counts
 
 

@@ -21,6 +21,7 @@ from dataclasses import dataclass, field
 import torch
 
 from .. import ops
+from ..utils.trace import NULL_TRACER
 from .collectives import allreduce_sum_
 from .flat_params import FlatParams
 
@@ -55,7 +56,7 @@ class StepStats:
 
 class LocalSGDTrainer:
     def __init__(self, model: torch.nn.Module, cfg: LocalSGDConfig, *, group=None, membership=None,
-                 device=None, compressor=None):
+                 device=None, compressor=None, tracer=None):
         self.model = model
         self.cfg = cfg
         self.device = device or next(model.parameters()).device
@@ -71,6 +72,7 @@ class LocalSGDTrainer:
         self.membership = membership
         self.group = membership.group if membership is not None else group
         self.compressor = compressor
+        self.tracer = tracer or NULL_TRACER  # utils/trace.py stage spans (HIP events)
         self.t = 0
         self.sync_count = 0
         self.last_sync_ms = 0.0
@@ -118,19 +120,24 @@ class LocalSGDTrainer:
         return self
 
     def step(self, x, y) -> StepStats:
+        tr = self.tracer
         if getattr(self, "graph", None) is not None:
             if x.data_ptr() != self._gx.data_ptr():
                 self._gx.copy_(x, non_blocking=True)
                 self._gy.copy_(y, non_blocking=True)
-            self.graph.replay()
+            with tr.span("local_step_graph"):
+                self.graph.replay()
             loss = self._gloss
         else:
-            loss = self.forward_backward(x, y)
-            self.optimizer_step()
+            with tr.span("fwd_bwd"):
+                loss = self.forward_backward(x, y)
+            with tr.span("adamw"):
+                self.optimizer_step()
         self.t += 1
         synced = False
         if self.t % self.cfg.H == 0:
-            self.sync()
+            with tr.span("average"):
+                self.sync()
             synced = True
         return StepStats(self.t, None, synced, self.last_sync_ms, self.group.size if self.group else 1,
                          {"loss_t": loss.detach()})

@@ -33,20 +33,20 @@ def tm(fn, it=10):
     return sorted(ts)[len(ts) // 2]
 
 
-C.attn_set_variant(2)
+C.attn_set_variant(2, 0)
 o_ref, lse_ref = C.attn_fwd(qkv, scale)
 g_ref = C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)
 torch.cuda.synchronize()
 res = {}
 for rnd in range(3):
-    for fv in (2, 3):
-        C.attn_set_variant(fv)
+    for fv in ((2, 0), (3, 0), (2, 1), (3, 1)):
+        C.attn_set_variant(*fv)
         o, l = C.attn_fwd(qkv, scale)
         if rnd == 0:
             err = (o.float() - o_ref.float()).abs().max().item()
             print(f"fwd variant {fv}: max|o - o_ref| = {err:.3e}", flush=True)
         res.setdefault(("fwd", fv), []).append(tm(lambda: C.attn_fwd(qkv, scale)))
-    C.attn_set_variant(3)
+    C.attn_set_variant(3, 1)
     res.setdefault(("bwd",), []).append(tm(lambda: C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)))
 for k, v in res.items():
     ms = sorted(v)[len(v) // 2]

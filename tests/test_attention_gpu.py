@@ -48,3 +48,27 @@ def test_attention_matches_sdpa_at_bench_shape(gpu):
     ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2)
     rel = (out.float() - ref.float()).norm() / ref.float().norm()
     assert rel < 1e-2, float(rel)
+
+
+@pytest.mark.parametrize("variant", [(2, 0), (3, 0), (2, 1), (3, 1)])
+def test_attention_deterministic(gpu, variant):
+    """Same inputs, same kernel -> bitwise identical outputs (a race on the double-buffered LDS
+    tiles would show up here as run-to-run differences)."""
+    C = ops.native()
+    torch.manual_seed(5)
+    B, T, H = 8, 1024, 12
+    qkv = torch.randn(B, T, 3, H, 64, device=gpu).to(torch.bfloat16)
+    C.attn_set_variant(*variant)
+    try:
+        outs = [C.attn_fwd(qkv, 0.125) for _ in range(4)]
+        torch.cuda.synchronize()
+        for o, l in outs[1:]:
+            nd = int((o != outs[0][0]).sum())
+            assert nd == 0, f"{nd} output elements differ between identical launches"
+            assert torch.equal(l, outs[0][1])
+        dO = torch.randn_like(outs[0][0])
+        gs = [C.attn_bwd(qkv, outs[0][0], dO, outs[0][1], 0.125) for _ in range(3)]
+        for g in gs[1:]:
+            assert torch.equal(g, gs[0])
+    finally:
+        C.attn_set_variant(3, 1)

@@ -134,3 +134,27 @@ def test_protocol_exact_verbs():
     assert protocol.parse_reply(b"ok") == (True, None)
     with pytest.raises(ValueError):
         protocol.encode("bogus", "x")
+
+
+def test_span_tracer_jsonl(tmp_path):
+    """utils/trace.py: spans become JSONL records with durations; disabled tracers record nothing."""
+    import json
+
+    from distributedvolunteercomputing_amd.utils.trace import NULL_TRACER, SpanTracer
+
+    p = tmp_path / "t" / "peer0.jsonl"
+    tr = SpanTracer("peer0", path=str(p))
+    for _ in range(2):
+        with tr.span("a"):
+            sum(range(1000))
+        with tr.span("b"):
+            pass
+    recs = tr.flush(step=3)
+    assert [r["span"] for r in recs] == ["a", "b", "a", "b"]
+    assert all(r["ms"] >= 0 and r["step"] == 3 for r in recs)
+    lines = [json.loads(x) for x in p.read_text().splitlines()]
+    assert len(lines) == 4 and lines[0]["component"] == "peer0"
+    assert tr.summary()["a"]["n"] == 2
+    with NULL_TRACER.span("x"):
+        pass
+    assert NULL_TRACER.flush() == []
