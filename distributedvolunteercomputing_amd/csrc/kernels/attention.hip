@@ -112,6 +112,25 @@ __device__ __forceinline__ float xhalf_sum(float v) {
   return __int_as_float(r[0]) + __int_as_float(r[1]);
 }
 
+// LDS-DMA of a 64-row x 64-column bf16 tile — rows r0 .. r0+63 of a row-major matrix with row
+// stride `ld` elements, row indices clamped to rmax — into the XOR-swizzled image `img` (swz
+// layout). Each of the 4 waves moves two 1-KB pieces with global_load_lds_dwordx4; the DMA writes a
+// wave-instruction's 64 x 16 B linearly, so the swizzle is applied to each lane's SOURCE address:
+// LDS slot p (row p/8, stored chunk p%8) receives global chunk (p%8) ^ g(row).
+__device__ __forceinline__ void dma_tile_swz(const bf16* g, int64_t ld, int r0, int rmax, bf16* img, int w,
+                                             int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = w * 2 + i;  // wave-uniform
+    const int p = piece * 64 + lane;
+    const int r = p >> 3, k = (r >> 1) & 7;
+    const int chunk = (p & 7) ^ (((k & 1) << 2) | (k >> 1));
+    const int row = min(r0 + r, rmax);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + (int64_t)row * ld + chunk * 8),
+                                     (__attribute__((address_space(3))) void*)(img + piece * 512), 16, 0, 0);
+  }
+}
+
 // ============================================================================ forward
 // Forward, occupancy-templated: the same tile algorithm with both K and V in XOR-swizzled
 // UNPADDED images (2 buffers x (8 + 8) KB = 32 KB per block, vs 42 KB padded) and the row max /
@@ -159,18 +178,8 @@ attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
   // DMA staging: tile kt goes straight into buffer buf (sstore is a no-op)
   auto gload = [&](int kt, int buf) {
     if constexpr (DMA) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int piece = w * 2 + i;               // wave-uniform 1-KB piece of the 8-KB image
-        const int p = piece * 64 + lane;           // this lane's 16-B slot in the image
-        const int r = p >> 3, k = (r >> 1) & 7;
-        const int chunk = (p & 7) ^ (((k & 1) << 2) | (k >> 1));  // global chunk stored in slot p
-        const int key = min(kt * A_BK + r, T - 1);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(Kg + (int64_t)key * tok + chunk * 8),
-                                         (__attribute__((address_space(3))) void*)(sK_(buf) + piece * 512), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(Vg + (int64_t)key * tok + chunk * 8),
-                                         (__attribute__((address_space(3))) void*)(sV_(buf) + piece * 512), 16, 0, 0);
-      }
+      dma_tile_swz(Kg, tok, kt * A_BK, T - 1, sK_(buf), w, lane);
+      dma_tile_swz(Vg, tok, kt * A_BK, T - 1, sV_(buf), w, lane);
     } else {
       (void)buf;
 #pragma unroll
@@ -330,13 +339,16 @@ __global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const bf16* __restr
 // dQ (query-parallel; same tiling as the forward): per 32-key sub-tile
 //   S^T = K Q^T, P^T = exp2(S^T c - lse), dP^T = V dO^T, dS^T = P^T (dP^T - delta),
 //   dQ^T += K^T dS^T  (A = K^T through ds_read_b64_tr_b16, B = dS^T from the accumulator)
-template <int WPE>
+template <int WPE, bool DMA>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) attn_bwd_dq_d64_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                                int B, int T, int H, float scale, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 sK[2][A_BK * AD];  // swizzled (swz)
-  __shared__ __attribute__((aligned(16))) bf16 sV[2][A_BK * AD];
+  // one shared object per buffer (see the forward): [K | V] tiles, swizzled (swz)
+  __shared__ __attribute__((aligned(16))) bf16 sKV0[2][A_BK * AD];
+  __shared__ __attribute__((aligned(16))) bf16 sKV1[2][A_BK * AD];
+#define sK_(b) ((b) ? &sKV1[0][0] : &sKV0[0][0])
+#define sV_(b) ((b) ? &sKV1[1][0] : &sKV0[1][0])
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
   const int nqt = (T + A_BQ - 1) / A_BQ;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -362,22 +374,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   const int kend = min(T, q0 + A_BQ);
   const int nkt = (kend + A_BK - 1) / A_BK;
   sx8 rk[2], rv[2];
-  auto gload = [&](int kt) {
+  auto gload = [&](int kt, int buf) {
+    if constexpr (DMA) {
+      dma_tile_swz(Kg, tok, kt * A_BK, T - 1, sK_(buf), w, lane);
+      dma_tile_swz(Vg, tok, kt * A_BK, T - 1, sV_(buf), w, lane);
+    } else {
+      (void)buf;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
-      const int key = min(kt * A_BK + r, T - 1);
-      rk[i] = *(const sx8*)(Kg + (int64_t)key * tok + c);
-      rv[i] = *(const sx8*)(Vg + (int64_t)key * tok + c);
+      for (int i = 0; i < 2; ++i) {
+        const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
+        const int key = min(kt * A_BK + r, T - 1);
+        rk[i] = *(const sx8*)(Kg + (int64_t)key * tok + c);
+        rv[i] = *(const sx8*)(Vg + (int64_t)key * tok + c);
+      }
     }
   };
   auto sstore = [&](int buf) {
+    if constexpr (!DMA) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
-      (void)c;
-      *(sx8*)(&sK[buf][swz(r, e & 7)]) = rk[i];
-      *(sx8*)(&sV[buf][swz(r, e & 7)]) = rv[i];
+      for (int i = 0; i < 2; ++i) {
+        const int e = tid + i * 256, r = e >> 3;
+        *(sx8*)(sK_(buf) + swz(r, e & 7)) = rk[i];
+        *(sx8*)(sV_(buf) + swz(r, e & 7)) = rv[i];
+      }
     }
   };
   // one 64-key tile (two 32-key sub-tiles); MASK only on the tiles crossing the diagonal
@@ -391,8 +410,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       f32x16 st = {}, dp = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        st = mfma32(row_frag_swz(&sK[cur][0], sub * 32 + col, s, h2), qf[s], st);
-        dp = mfma32(row_frag_swz(&sV[cur][0], sub * 32 + col, s, h2), df[s], dp);
+        st = mfma32(row_frag_swz(sK_(cur), sub * 32 + col, s, h2), qf[s], st);
+        dp = mfma32(row_frag_swz(sV_(cur), sub * 32 + col, s, h2), df[s], dp);
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -408,12 +427,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
         sx8 db;
 #pragma unroll
         for (int j = 0; j < 8; ++j) db[j] = bf16_bits(st[8 * s + j]);
-        a0 = mfma32(vt_frag_swz(&sK[cur][0], sub * 32, 0, s, lane), db, a0);
-        a1 = mfma32(vt_frag_swz(&sK[cur][0], sub * 32, 1, s, lane), db, a1);
+        a0 = mfma32(vt_frag_swz(sK_(cur), sub * 32, 0, s, lane), db, a0);
+        a1 = mfma32(vt_frag_swz(sK_(cur), sub * 32, 1, s, lane), db, a1);
       }
     }
   };
-  gload(0);
+  gload(0, 0);
   sstore(0);
   __syncthreads();
   // Retire EVERY outstanding global load (the per-lane Q/dO/K/V fragments loaded at kernel entry
@@ -428,7 +447,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   const int kdiag = q0 / A_BK;
   auto step = [&](int kt, auto cur_c, auto mask_c) {
     constexpr int cur = decltype(cur_c)::value;
-    if (kt + 1 < nkt) gload(kt + 1);
+    if (kt + 1 < nkt) gload(kt + 1, cur ^ 1);
     tile(kt, cur_c, mask_c);
     if (kt + 1 < nkt) sstore(cur ^ 1);
     __syncthreads();
@@ -458,6 +477,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       *(bf16x4*)(row + 32 + d) = v1;
     }
   }
+#undef sK_
+#undef sV_
 }
 
 // dK, dV (key-parallel, "key on the lane"): per 32-query sub-tile
@@ -466,15 +487,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
 //   B operands = the bf16-converted accumulators; the keys stay on the lanes throughout)
 constexpr int B_BQ = 64;  // queries per LDS tile
 
-template <int WPE>
+template <int WPE, bool DMA>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) attn_bwd_dkdv_d64_kernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ lse,
                                                                  const float* __restrict__ delta,
                                                                  bf16* __restrict__ dqkv, int B, int T, int H,
                                                                  float scale, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) bf16 sQ[2][B_BQ * AD];  // swizzled (swz)
-  __shared__ __attribute__((aligned(16))) bf16 sD[2][B_BQ * AD];
+  // one shared object per buffer (see the forward): [Q | dO] tiles, swizzled (swz)
+  __shared__ __attribute__((aligned(16))) bf16 sQD0[2][B_BQ * AD];
+  __shared__ __attribute__((aligned(16))) bf16 sQD1[2][B_BQ * AD];
+#define sQ_(b) ((b) ? &sQD1[0][0] : &sQD0[0][0])
+#define sD_(b) ((b) ? &sQD1[1][0] : &sQD0[1][0])
   __shared__ __attribute__((aligned(16))) float sL[2][B_BQ];
   __shared__ __attribute__((aligned(16))) float sDel[2][B_BQ];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
@@ -501,13 +525,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   const int nqt = (T + B_BQ - 1) / B_BQ;
   sx8 rq[2], rd[2];
   float rl = 0.f, rdl = 0.f;
-  auto gload = [&](int qt) {
+  auto gload = [&](int qt, int buf) {
+    if constexpr (DMA) {
+      dma_tile_swz(base, tok, qt * B_BQ, T - 1, sQ_(buf), w, lane);
+      dma_tile_swz(dOb, otok, qt * B_BQ, T - 1, sD_(buf), w, lane);
+    } else {
+      (void)buf;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
-      const int qq = min(qt * B_BQ + r, T - 1);
-      rq[i] = *(const sx8*)(base + (int64_t)qq * tok + c);
-      rd[i] = *(const sx8*)(dOb + (int64_t)qq * otok + c);
+      for (int i = 0; i < 2; ++i) {
+        const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
+        const int qq = min(qt * B_BQ + r, T - 1);
+        rq[i] = *(const sx8*)(base + (int64_t)qq * tok + c);
+        rd[i] = *(const sx8*)(dOb + (int64_t)qq * otok + c);
+      }
     }
     if (tid < B_BQ) {  // -lse (so P = exp2(S c + nl)); -inf for rows past T: their P is 0
       const int qq = qt * B_BQ + tid;
@@ -516,12 +546,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     }
   };
   auto sstore = [&](int buf) {
+    if constexpr (!DMA) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = tid + i * 256, r = e >> 3, c = (e & 7) * 8;
-      (void)c;
-      *(sx8*)(&sQ[buf][swz(r, e & 7)]) = rq[i];
-      *(sx8*)(&sD[buf][swz(r, e & 7)]) = rd[i];
+      for (int i = 0; i < 2; ++i) {
+        const int e = tid + i * 256, r = e >> 3;
+        *(sx8*)(sQ_(buf) + swz(r, e & 7)) = rq[i];
+        *(sx8*)(sD_(buf) + swz(r, e & 7)) = rd[i];
+      }
     }
     if (tid < B_BQ) {
       sL[buf][tid] = rl;
@@ -540,8 +571,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       f32x16 st = {}, dp = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        st = mfma32(row_frag_swz(&sQ[cur][0], sub * 32 + col, s, h2), kf[s], st);
-        dp = mfma32(row_frag_swz(&sD[cur][0], sub * 32 + col, s, h2), vf[s], dp);
+        st = mfma32(row_frag_swz(sQ_(cur), sub * 32 + col, s, h2), kf[s], st);
+        dp = mfma32(row_frag_swz(sD_(cur), sub * 32 + col, s, h2), vf[s], dp);
       }
       f32x16 pp;
 #pragma unroll
@@ -569,14 +600,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
           pb[j] = bf16_bits(pp[8 * s + j]);
           sb[j] = bf16_bits(st[8 * s + j]);
         }
-        dv0 = mfma32(vt_frag_swz(&sD[cur][0], sub * 32, 0, s, lane), pb, dv0);
-        dv1 = mfma32(vt_frag_swz(&sD[cur][0], sub * 32, 1, s, lane), pb, dv1);
-        dk0 = mfma32(vt_frag_swz(&sQ[cur][0], sub * 32, 0, s, lane), sb, dk0);
-        dk1 = mfma32(vt_frag_swz(&sQ[cur][0], sub * 32, 1, s, lane), sb, dk1);
+        dv0 = mfma32(vt_frag_swz(sD_(cur), sub * 32, 0, s, lane), pb, dv0);
+        dv1 = mfma32(vt_frag_swz(sD_(cur), sub * 32, 1, s, lane), pb, dv1);
+        dk0 = mfma32(vt_frag_swz(sQ_(cur), sub * 32, 0, s, lane), sb, dk0);
+        dk1 = mfma32(vt_frag_swz(sQ_(cur), sub * 32, 1, s, lane), sb, dk1);
       }
     }
   };
-  gload(qstart);
+  gload(qstart, 0);
   sstore(0);
   __syncthreads();
   // Retire EVERY outstanding global load (the per-lane Q/dO/K/V fragments loaded at kernel entry
@@ -590,7 +621,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   __builtin_amdgcn_s_waitcnt(0x0F70);
   auto step = [&](int qt, auto cur_c, auto mask_c) {
     constexpr int cur = decltype(cur_c)::value;
-    if (qt + 1 < nqt) gload(qt + 1);
+    if (qt + 1 < nqt) gload(qt + 1, cur ^ 1);
     tile(qt, cur_c, mask_c);
     if (qt + 1 < nqt) sstore(cur ^ 1);
     __syncthreads();
@@ -622,6 +653,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       *(bf16x4*)(rowv + 32 + d) = v1;
     }
   }
+#undef sQ_
+#undef sD_
 }
 
 }  // namespace vcx
@@ -631,12 +664,15 @@ using namespace vcx;
 // Forward default: LDS-DMA staging at 3 waves per SIMD. Measured at the GPT-2 bench shape
 // (B=64 H=12 T=1024, one process, interleaved rounds; scripts/attn_variants.py): 0.211 ms, vs
 // 0.223 DMA at 2 waves/SIMD, 0.237 register staging at 2 and 0.266 register staging at 3 (spills).
-// Backward kernels: 2 waves per SIMD (at 3-4 they spill: dq 0.87-1.25 ms vs 0.64 for the pair).
-static int g_fwd_wpe = 3, g_fwd_dma = 1;
+// Backward kernels: 2 waves per SIMD (at 3-4 they spill: dq 0.87-1.25 ms vs 0.64 for the pair);
+// dQ with LDS-DMA staging (264 vs 275 us), dK/dV with register staging (381 vs 383 us: the DMA
+// build of that kernel hits the 256-VGPR cap and spills).
+static int g_fwd_wpe = 3, g_fwd_dma = 1, g_bwd_dma = 1;  // g_bwd_dma bit 0: dQ kernel, bit 1: dK/dV kernel
 
-void vcx_attn_set_variant(int fwd_wpe, int fwd_dma) {
+void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma) {
   if (fwd_wpe == 2 || fwd_wpe == 3) g_fwd_wpe = fwd_wpe;
   if (fwd_dma == 0 || fwd_dma == 1) g_fwd_dma = fwd_dma;
+  if (bwd_dma >= 0 && bwd_dma <= 3) g_bwd_dma = bwd_dma;
 }
 
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
@@ -645,11 +681,19 @@ void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const 
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 31) / 32), dim3(256), 0, s, (const bf16*)out,
                      (const bf16*)dout, delta, B, T, H);
   const int nkb = (T + 127) / 128;
-  hipLaunchKernelGGL(attn_bwd_dkdv_d64_kernel<2>, dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
-                     (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
   const int nqt = (T + A_BQ - 1) / A_BQ;
-  hipLaunchKernelGGL(attn_bwd_dq_d64_kernel<2>, dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
-                     (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+  if (g_bwd_dma & 2)
+    hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, true>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+  else
+    hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, false>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+  if (g_bwd_dma & 1)
+    hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, true>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, false>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
 }
 
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s) {

@@ -33,21 +33,25 @@ def tm(fn, it=10):
     return sorted(ts)[len(ts) // 2]
 
 
-C.attn_set_variant(2, 0)
+C.attn_set_variant(2, 0, 0)
 o_ref, lse_ref = C.attn_fwd(qkv, scale)
 g_ref = C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)
 torch.cuda.synchronize()
 res = {}
 for rnd in range(3):
     for fv in ((2, 0), (3, 0), (2, 1), (3, 1)):
-        C.attn_set_variant(*fv)
+        C.attn_set_variant(*fv, 1)
         o, l = C.attn_fwd(qkv, scale)
         if rnd == 0:
             err = (o.float() - o_ref.float()).abs().max().item()
             print(f"fwd variant {fv}: max|o - o_ref| = {err:.3e}", flush=True)
         res.setdefault(("fwd", fv), []).append(tm(lambda: C.attn_fwd(qkv, scale)))
-    C.attn_set_variant(3, 1)
-    res.setdefault(("bwd",), []).append(tm(lambda: C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)))
+    for bd in (0, 1):
+        C.attn_set_variant(3, 1, bd)
+        if rnd == 0:
+            g = C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)
+            print(f"bwd dma {bd}: max|dqkv - ref| = {(g.float() - g_ref.float()).abs().max().item():.3e}", flush=True)
+        res.setdefault(("bwd", bd), []).append(tm(lambda: C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)))
 for k, v in res.items():
     ms = sorted(v)[len(v) // 2]
     f = fl if k[0] == "fwd" else 2.5 * fl
