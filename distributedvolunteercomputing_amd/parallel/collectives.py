@@ -67,6 +67,16 @@ def _rs_ag(t, group):
     return t
 
 
+def _swap(group, send_t, recv_t, peer, tag, all_ranks: bool):
+    """Pairwise swap of one butterfly round. When EVERY rank of the group takes part in the round
+    (power-of-two groups) it is one full-duplex alltoall (grouped send/recv); otherwise (folded
+    peers are waiting outside the round) ordered blocking point-to-point."""
+    if all_ranks:
+        group.exchange_all(send_t, recv_t, peer)
+    else:
+        group.exchange(send_t, recv_t, peer, tag=tag)
+
+
 def _butterfly(t, group):
     P, r = group.size, group.rank
     p2 = 1
@@ -97,7 +107,7 @@ def _butterfly(t, group):
         else:
             keep, give = (lo, mid), (mid, hi)
         recv = buf.new_empty(keep[1] - keep[0])
-        group.exchange(buf[give[0] : give[1]].contiguous(), recv, peer, tag=3)
+        _swap(group, buf[give[0] : give[1]].contiguous(), recv, peer, 3, extra == 0)
         kv = buf[keep[0] : keep[1]]
         _add_(kv, recv)
         segs.append((lo, hi, dist_))
@@ -110,7 +120,7 @@ def _butterfly(t, group):
         mine = (lo, hi)
         other = (mid, phi) if mine[0] == plo else (plo, mid)
         recv = buf.new_empty(other[1] - other[0])
-        group.exchange(buf[mine[0] : mine[1]].contiguous(), recv, peer, tag=4)
+        _swap(group, buf[mine[0] : mine[1]].contiguous(), recv, peer, 4, extra == 0)
         buf[other[0] : other[1]].copy_(recv)
         lo, hi = plo, phi
     if buf is not t:
@@ -132,6 +142,9 @@ def _ring(t, group):
     recv = buf.new_empty(cs)
 
     def step(send_t, recv_t, tag):
+        if P > 2:  # every rank sends right and receives left in the same round: one grouped alltoall
+            group.exchange_all(send_t, recv_t, right, left)
+            return
         # even ranks send first, odd ranks receive first: deadlock-free for blocking p2p
         if r % 2 == 0:
             group.send(send_t, right, tag)

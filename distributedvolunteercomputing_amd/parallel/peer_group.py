@@ -128,6 +128,18 @@ class PeerGroup:
             self.recv(recv_t, peer, tag)
             self.send(send_t, peer, tag)
 
+    def exchange_all(self, send_t: torch.Tensor, recv_t: torch.Tensor, send_to: int, recv_from: int | None = None):
+        """One round in which EVERY rank of the group sends `send_t` to `send_to` and receives
+        `recv_t` from `recv_from` (default: the same peer). Issued as ONE alltoall whose only
+        non-empty splits are those two, so RCCL runs it as grouped send/recv: both directions of
+        the xGMI link at once (the blocking `exchange` above serialises them)."""
+        recv_from = send_to if recv_from is None else recv_from
+        ins = [0] * self.size
+        outs = [0] * self.size
+        ins[send_to] = send_t.numel()
+        outs[recv_from] = recv_t.numel()
+        self.pg.alltoall_base(recv_t.view(-1), send_t.view(-1), outs, ins, dist.AllToAllOptions()).wait()
+
     def barrier(self):
         if self.pg is None:
             return

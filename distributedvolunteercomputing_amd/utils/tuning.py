@@ -7,7 +7,7 @@ are committed in ``tuning/tunableop_gfx950.csv``. At run time we only LOOK UP th
 (tuning disabled), so a fresh box gets the tuned kernels with no tuning cost.
 
 Must be called before torch issues its first GEMM (it only sets environment variables).
-Set VCX_TUNABLEOP=off to disable.
+Set VCX_TUNABLEOP=off to disable; VCX_TUNABLEOP_FILE=<csv> to use another results file.
 """
 from __future__ import annotations
 
@@ -22,11 +22,12 @@ RESULTS = os.path.join(ROOT, "tuning", "tunableop_gfx950.csv")
 def enable_tuned_gemms(local_rank: int = 0) -> bool:
     if os.environ.get("VCX_TUNABLEOP", "on") == "off" or "PYTORCH_TUNABLEOP_ENABLED" in os.environ:
         return False
-    if not os.path.exists(RESULTS):
+    results = os.environ.get("VCX_TUNABLEOP_FILE", RESULTS)
+    if not os.path.exists(results):
         return False
     d = tempfile.mkdtemp(prefix="vcx_tunableop_")
     # TunableOp keys its results file by device ordinal; give this rank its own copy
-    shutil.copyfile(RESULTS, os.path.join(d, f"results{local_rank}.csv"))
+    shutil.copyfile(results, os.path.join(d, f"results{local_rank}.csv"))
     os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "1"
     os.environ["PYTORCH_TUNABLEOP_TUNING"] = "0"
     os.environ["PYTORCH_TUNABLEOP_FILENAME"] = os.path.join(d, "results%d.csv")
