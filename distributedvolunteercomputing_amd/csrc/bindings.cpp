@@ -166,7 +166,7 @@ std::vector<at::Tensor> ln_bwd(at::Tensor dy, at::Tensor x, at::Tensor w, at::Te
     CHECK_IN((*dres), kBF);
     TORCH_CHECK(dres->sizes() == x.sizes());
   }
-  const int P = vcx_ln_bwd_partials((int)R);
+  const int P = vcx_ln_bwd_partials((int)R, C);
   auto dx = at::empty_like(x);
   auto dw_part = at::empty({P, C}, x.options().dtype(kF));
   int mask = 0;

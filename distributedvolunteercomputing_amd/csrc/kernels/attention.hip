@@ -313,36 +313,13 @@ attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
 }
 
 // ============================================================================ backward
-// delta[b, h, q] = sum_d dO[b, q, h, d] * O[b, q, h, d]   (8 lanes x 8 elements per row)
-__global__ void __launch_bounds__(256) attn_bwd_delta_kernel(const bf16* __restrict__ o, const bf16* __restrict__ dout,
-                                                              float* __restrict__ delta, int B, int T, int H) {
-  const int64_t rows = (int64_t)B * T * H;
-  const int64_t row = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
-  if (row >= rows) return;
-  const int sub = threadIdx.x & 7;
-  bf16x8 a = *(const bf16x8*)(o + row * AD + sub * 8);
-  bf16x8 g = *(const bf16x8*)(dout + row * AD + sub * 8);
-  float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s = fmaf((float)a[j], (float)g[j], s);
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  s += __shfl_xor(s, 4, 64);
-  if (sub == 0) {
-    const int hh = (int)(row % H);
-    const int64_t bt = row / H;
-    const int tq = (int)(bt % T), b = (int)(bt / T);
-    delta[((int64_t)b * H + hh) * T + tq] = s;
-  }
-}
-
 // dQ (query-parallel; same tiling as the forward): per 32-key sub-tile
 //   S^T = K Q^T, P^T = exp2(S^T c - lse), dP^T = V dO^T, dS^T = P^T (dP^T - delta),
 //   dQ^T += K^T dS^T  (A = K^T through ds_read_b64_tr_b16, B = dS^T from the accumulator)
 template <int WPE, bool DMA>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) attn_bwd_dq_d64_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                               const float* __restrict__ lse,
-                                                               const float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                               const bf16* __restrict__ out, const float* __restrict__ lse,
+                                                               float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                                int B, int T, int H, float scale, float scale_log2) {
   // one shared object per buffer (see the forward): [K | V] tiles, swizzled (swz)
   __shared__ __attribute__((aligned(16))) bf16 sKV0[2][A_BK * AD];
@@ -369,7 +346,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     df[s] = *(const sx8*)(dOb + (int64_t)qc * otok + 16 * s + 8 * h2);
   }
   const float nlq = -lse[((int64_t)b * H + hh) * T + qc];
-  const float dq_delta = delta[((int64_t)b * H + hh) * T + qc];
+  // delta[q] = sum_d dO[q, d] * O[q, d], computed here from the dO fragments already in registers
+  // (this lane holds 32 of the 64 d, its partner lane l ^ 32 the rest) instead of by a separate
+  // kernel; written out for the dK/dV kernel, which runs after this one
+  float dq_delta;
+  {
+    const bf16* Ob = out + ((int64_t)b * T + qc) * otok + hh * AD;
+    float acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const sx8 ov = *(const sx8*)(Ob + 16 * s + 8 * h2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const short ob = ov[j], db = df[s][j];
+        acc = fmaf((float)*(const bf16*)&ob, (float)*(const bf16*)&db, acc);
+      }
+    }
+    dq_delta = xhalf_sum(acc);
+    if (h2 == 0 && q < T) delta[((int64_t)b * H + hh) * T + q] = dq_delta;
+  }
   f32x16 a0 = {}, a1 = {};
   const int kend = min(T, q0 + A_BQ);
   const int nkt = (kend + A_BK - 1) / A_BK;
@@ -677,22 +672,20 @@ void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma) {
 
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
                       int B, int T, int H, float scale, hipStream_t s) {
-  const int64_t rows = (int64_t)B * T * H;
-  hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 31) / 32), dim3(256), 0, s, (const bf16*)out,
-                     (const bf16*)dout, delta, B, T, H);
+  // dQ first: it also computes delta = rowsum(dO * O) for the dK/dV kernel
   const int nkb = (T + 127) / 128;
   const int nqt = (T + A_BQ - 1) / A_BQ;
+  if (g_bwd_dma & 1)
+    hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, true>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, false>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
   if (g_bwd_dma & 2)
     hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, true>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
   else
     hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, false>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
-                       (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
-  if (g_bwd_dma & 1)
-    hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, true>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
-                       (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
-  else
-    hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, false>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
 }
 

@@ -27,7 +27,7 @@ void vcx_bias_gelu_bwd(const void* x, const void* b, const void* dy, void* dx, f
 // column sums of a bf16 [R, F] matrix into out[F] (bf16; added to it when accumulate != 0)
 void vcx_colsum_bf16(const void* y, float* part, void* out, int R, int F, int accumulate, float* stage,
                      hipStream_t s);
-int vcx_ln_bwd_partials(int R);
+int vcx_ln_bwd_partials(int R, int C);
 void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
                 void* dx, float* dw_part, float* db_part, void* dw, void* db, int R, int C, int rms, float* dbb_part,
                 void* dbb, float* stage, int accum_mask, hipStream_t s);
