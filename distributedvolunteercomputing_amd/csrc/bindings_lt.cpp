@@ -1,12 +1,10 @@
-// hipBLASLt GEMMs with fused epilogues for the transformer layers (gfx950).
+// hipBLASLt GEMMs with an in-process per-shape algorithm search and optional epilogues (gfx950).
 //
-// Plain GEMMs stay library GEMMs; what this file adds over torch.matmul is the epilogues that
-// hipBLASLt can fuse into the GEMM's store phase:
-//   * GELU_AUX_BIAS  — fc forward: out = gelu(x W^T + b) and the pre-activation as an aux output
-//                      (replaces the separate bias+GELU forward kernel: one fewer 400 MB pass);
-//   * DGELU_BGRAD    — fc2 input-gradient GEMM: out = (dy W) * gelu'(aux) and the fc bias gradient
-//                      (replaces the bias+GELU backward kernel and its column sums);
-//   * BIAS / DEFAULT — everything else.
+// Used by ops/linear.py's per-shape library selection (VCX_GEMM_SELECT=1) and by the probes in
+// scripts/. Measured on this image's hipBLASLt (scripts/lt_probe3.py): BIAS / GELU / GELU_BIAS /
+// DGELU have bf16 algorithms at the GPT-2 MLP shapes, GELU_AUX(_BIAS) / DGELU_BGRAD / BGRADB do
+// not, and DGELU does not compute the tanh-GELU derivative the model needs — so the MLP keeps its
+// GEMM + HIP bias-GELU kernels, and the selection layer stays opt-in (A/B: no in-step gain).
 //
 // Row-major API: out[M, N] = alpha * op(A) op(B) (+ beta * out) with A [M, K] ([K, M] if trans_a)
 // and B [K, N] ([N, K] if trans_b). hipBLASLt is column-major, so the call is issued as
