@@ -367,6 +367,42 @@ std::vector<at::Tensor> embed_bwd(at::Tensor idx, at::Tensor dx, int64_t V, int6
   return {dwte, dwpe};
 }
 
+// ------------------------------------------------------------------ rotary embedding (Llama)
+std::vector<at::Tensor> rope_qkv_fwd(at::Tensor qkv, at::Tensor cosv, at::Tensor sinv, int64_t Hq, int64_t Hkv) {
+  CHECK_IN(qkv, kBF);
+  CHECK_IN(cosv, kF);
+  CHECK_IN(sinv, kF);
+  TORCH_CHECK(qkv.dim() == 3, "rope_qkv: qkv must be [B, T, (Hq + 2 Hkv) * D]");
+  const int64_t B = qkv.size(0), T = qkv.size(1), W = qkv.size(2);
+  TORCH_CHECK(Hq > 0 && Hkv > 0 && W % (Hq + 2 * Hkv) == 0);
+  const int64_t D = W / (Hq + 2 * Hkv);
+  TORCH_CHECK(D % 8 == 0, "rope_qkv: head dim must be a multiple of 8");
+  TORCH_CHECK(cosv.dim() == 2 && cosv.size(0) >= T && cosv.size(1) == D / 2 && sinv.sizes() == cosv.sizes(),
+              "rope_qkv: cos/sin tables must be [>= T, D/2]");
+  auto q = at::empty({B, Hq, T, D}, qkv.options());
+  auto k = at::empty({B, Hkv, T, D}, qkv.options());
+  auto v = at::empty({B, Hkv, T, D}, qkv.options());
+  vcx_rope_qkv(qkv.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), cosv.data_ptr<float>(),
+               sinv.data_ptr<float>(), (int)B, (int)T, (int)Hq, (int)Hkv, (int)D, 0, cur_stream());
+  return {q, k, v};
+}
+
+at::Tensor rope_qkv_bwd(at::Tensor dq, at::Tensor dk, at::Tensor dv, at::Tensor cosv, at::Tensor sinv) {
+  CHECK_IN(dq, kBF);
+  CHECK_IN(dk, kBF);
+  CHECK_IN(dv, kBF);
+  CHECK_IN(cosv, kF);
+  CHECK_IN(sinv, kF);
+  TORCH_CHECK(dq.dim() == 4 && dk.dim() == 4 && dk.sizes() == dv.sizes());
+  const int64_t B = dq.size(0), Hq = dq.size(1), T = dq.size(2), D = dq.size(3), Hkv = dk.size(1);
+  TORCH_CHECK(dk.size(0) == B && dk.size(2) == T && dk.size(3) == D && D % 8 == 0);
+  TORCH_CHECK(cosv.size(0) >= T && cosv.size(1) == D / 2 && sinv.sizes() == cosv.sizes());
+  auto dqkv = at::empty({B, T, (Hq + 2 * Hkv) * D}, dq.options());
+  vcx_rope_qkv(dqkv.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), cosv.data_ptr<float>(),
+               sinv.data_ptr<float>(), (int)B, (int)T, (int)Hq, (int)Hkv, (int)D, 1, cur_stream());
+  return dqkv;
+}
+
 // ------------------------------------------------------------------ attention (head dim 64)
 std::vector<at::Tensor> attn_fwd(at::Tensor qkv, double scale) {
   CHECK_IN(qkv, kBF);
@@ -434,6 +470,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("Tpos"), pybind11::arg("wte_grad") = pybind11::none(), pybind11::arg("wpe_grad") = pybind11::none());
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_set_variant", &vcx_attn_set_variant);
+  m.def("rope_qkv_fwd", &rope_qkv_fwd);
+  m.def("rope_qkv_bwd", &rope_qkv_bwd);
   m.def("attn_bwd", &attn_bwd);
   vcx_register_vision(m);
   vcx_register_compress(m);

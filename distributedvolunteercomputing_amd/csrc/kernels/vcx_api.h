@@ -51,6 +51,10 @@ void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma);
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
                       int B, int T, int H, float scale, hipStream_t s);
 
+// rope.hip: rotary embedding fused with the QKV split into head-major q/k/v (and its inverse)
+void vcx_rope_qkv(void* qkv, void* q, void* k, void* v, const float* cosv, const float* sinv, int B, int T, int Hq,
+                  int Hkv, int D, int backward, hipStream_t s);
+
 // embed.hip
 void vcx_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int64_t R, int T, int C, int V,
                    hipStream_t s);

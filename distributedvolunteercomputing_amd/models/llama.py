@@ -1,8 +1,9 @@
 """Llama-3 family (BASELINE.json config 5: "Llama-3-8B, optimizer-state shard across 8
 volunteer peers (288 GB HBM per GPU sizing), PowerSGD rank-4 compression").
 
-RMSNorm (with the residual add fused) and SwiGLU are HIP kernels; GEMMs are library GEMMs;
-attention is torch SDPA with grouped-query heads; RoPE uses precomputed cos/sin tables.
+RMSNorm (with the residual add fused), SwiGLU and the rotary embedding (fused with the QKV split
+into head-major q/k/v, ops/rope.py) are HIP kernels; GEMMs are library GEMMs; attention (head dim
+128, grouped-query) is torch SDPA with enable_gqa.
 
 Memory sizing for 8B on one MI355X peer (288 GB HBM): bf16 params 16 GB + bf16 grads 16 GB,
 plus fp32 master/m/v = 96 GB for the whole model -> 12 GB per peer when sharded over 8
@@ -43,18 +44,21 @@ class LlamaConfig:
         return LlamaConfig(**t[name])
 
 
-def rope_tables(T: int, hd: int, theta: float, device):
-    inv = 1.0 / (theta ** (torch.arange(0, hd, 2, device=device, dtype=torch.float32) / hd))
-    f = torch.outer(torch.arange(T, device=device, dtype=torch.float32), inv)
-    return f.cos(), f.sin()
+from ..ops.rope import apply_rope, rope_tables  # noqa: E402,F401  (re-exported for callers)
+
+_GQA_SDPA = [True]  # SDPA's enable_gqa (no repeat_interleave copies); falls back if unsupported
 
 
-def apply_rope(x, cos, sin):
-    """x [B, H, T, hd] (interleaved-pair convention of the Llama reference)."""
-    x2 = x.float().unflatten(-1, (-1, 2))
-    a, b = x2[..., 0], x2[..., 1]
-    c, s = cos[None, None], sin[None, None]
-    return torch.stack([a * c - b * s, a * s + b * c], -1).flatten(-2).to(x.dtype)
+def _sdpa_gqa(q, k, v, rep):
+    if rep > 1 and _GQA_SDPA[0]:
+        try:
+            return F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
+        except (RuntimeError, TypeError):
+            _GQA_SDPA[0] = False
+    if rep > 1:
+        k = k.repeat_interleave(rep, dim=1)
+        v = v.repeat_interleave(rep, dim=1)
+    return F.scaled_dot_product_attention(q, k, v, is_causal=True)
 
 
 class LlamaBlock(nn.Module):
@@ -72,17 +76,9 @@ class LlamaBlock(nn.Module):
     def attn(self, h, cos, sin):
         c = self.c
         B, T, D = h.shape
-        hd = D // c.n_heads
-        qkv = ops.linear(h, self.wqkv)
-        q, k, v = qkv.split([c.n_heads * hd, c.n_kv_heads * hd, c.n_kv_heads * hd], -1)
-        q = apply_rope(q.view(B, T, c.n_heads, hd).transpose(1, 2), cos, sin)
-        k = apply_rope(k.view(B, T, c.n_kv_heads, hd).transpose(1, 2), cos, sin)
-        v = v.view(B, T, c.n_kv_heads, hd).transpose(1, 2)
-        rep = c.n_heads // c.n_kv_heads
-        if rep > 1:
-            k = k.repeat_interleave(rep, dim=1)
-            v = v.repeat_interleave(rep, dim=1)
-        y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        # fused QKV projection -> one HIP kernel: split, rotary embedding on q/k, head-major q/k/v
+        q, k, v = ops.rope_qkv(ops.linear(h, self.wqkv), cos, sin, c.n_heads, c.n_kv_heads)
+        y = _sdpa_gqa(q, k, v, c.n_heads // c.n_kv_heads)
         return ops.linear(y.transpose(1, 2).reshape(B, T, D), self.wo)
 
     def mlp(self, h):

@@ -7,4 +7,5 @@ from .embedding import embed  # noqa: F401
 from .linear import linear, wgrad  # noqa: F401
 from .loss import cross_entropy  # noqa: F401
 from .norm import add_layernorm, add_rmsnorm, layernorm, rmsnorm  # noqa: F401
+from .rope import rope_qkv  # noqa: F401
 from .optim import adamw_step, axpy_bf16, f32_to_bf16, lsgd_apply, lsgd_delta, new_ostate  # noqa: F401

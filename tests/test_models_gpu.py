@@ -51,3 +51,28 @@ def test_resnet_tiny_step(gpu):
         st = tr.step(x, y)
     torch.cuda.synchronize()
     assert torch.isfinite(st.extra["loss_t"]).item()
+
+
+def test_rope_qkv_matches_reference(gpu):
+    """HIP rotary embedding fused with the QKV split vs the torch reference (fwd + bwd)."""
+    from distributedvolunteercomputing_amd import ops
+    from distributedvolunteercomputing_amd.ops.rope import apply_rope, rope_tables
+
+    torch.manual_seed(0)
+    B, T, Hq, Hkv, hd = 2, 100, 8, 2, 128
+    qkv = torch.randn(B, T, (Hq + 2 * Hkv) * hd, device=gpu).to(torch.bfloat16).requires_grad_()
+    cos, sin = rope_tables(T, hd, 500000.0, gpu)
+    q, k, v = ops.rope_qkv(qkv, cos, sin, Hq, Hkv)
+    x32 = qkv.detach().float().requires_grad_()
+    qr, kr, vr = x32.split([Hq * hd, Hkv * hd, Hkv * hd], -1)
+    qr = apply_rope(qr.reshape(B, T, Hq, hd).transpose(1, 2), cos, sin)
+    kr = apply_rope(kr.reshape(B, T, Hkv, hd).transpose(1, 2), cos, sin)
+    vr = vr.reshape(B, T, Hkv, hd).transpose(1, 2)
+    for a, r in ((q, qr), (k, kr), (v, vr)):
+        assert a.shape == r.shape
+        assert torch.allclose(a.float(), r, atol=3e-2, rtol=2e-2)
+    gs = [torch.randn_like(r) for r in (qr, kr, vr)]
+    sum((a.float() * g).sum() for a, g in zip((q, k, v), gs)).backward()
+    sum((r * g).sum() for r, g in zip((qr, kr, vr), gs)).backward()
+    rel = float((qkv.grad.float() - x32.grad).norm() / x32.grad.norm())
+    assert rel < 1e-2, rel
