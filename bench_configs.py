@@ -47,13 +47,17 @@ def cfg3(a, dev):
     x = torch.randn(B, 3, 224, 224, device=dev).to(torch.bfloat16).to(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (B,), device=dev)
     dt, st = _time(lambda: tr.step(x, y), 4, a.steps)
-    # cost of one compressed averaging round on its own
+    # cost of one compressed averaging round on its own (warmed up: the first call loads the
+    # compression kernels' code objects; mean of 10 rounds)
+    for _ in range(2):
+        tr.compressor.allreduce_mean(tr.delta, None)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tr.compressor.allreduce_mean(tr.delta, None)
+    for _ in range(10):
+        tr.compressor.allreduce_mean(tr.delta, None)
     torch.cuda.synchronize()
     return {"config": 3, "model": "resnet50", "images_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 2),
-            "batch": B, "topk_ratio": 0.01, "topk_round_ms": round((time.perf_counter() - t0) * 1e3, 2),
+            "batch": B, "topk_ratio": 0.01, "topk_round_ms": round((time.perf_counter() - t0) * 1e3 / 10, 3),
             "params": tr.flat.numel}
 
 
