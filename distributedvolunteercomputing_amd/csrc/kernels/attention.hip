@@ -67,6 +67,27 @@ __device__ __forceinline__ short bf16_bits(float f) {
   return *(short*)&b;
 }
 
+// bf16 fragment times c, rounded back to bf16: the score scale (1/sqrt(D) * log2 e) is folded into
+// the register-resident operand of S = Q K^T once per kernel instead of one v_fma per score (dQ
+// kernel; the same change measured no faster in the forward, which then spills more, and slower in
+// dK/dV, where the row constants come from LDS and their reads then precede the S MFMAs)
+__device__ __forceinline__ sx8 prescale(sx8 v, float c) {
+  sx8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const short sv = v[j];
+    r[j] = bf16_bits((float)*(const bf16*)&sv * c);
+  }
+  return r;
+}
+
+__device__ __forceinline__ f32x16 splat16(float v) {
+  f32x16 r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r[i] = v;
+  return r;
+}
+
 // XOR-swizzled [rows][64] bf16 LDS tile (no padding): 16-B chunk c of row r is stored at chunk
 // c ^ g((r >> 1) & 7), g(k) = ((k & 1) << 2) | (k >> 1). Even and odd rows fall in opposite
 // 128-B halves of the 256-B bank row; g is a bijection on 0..7 (16 consecutive rows of one
@@ -346,6 +367,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     df[s] = *(const sx8*)(dOb + (int64_t)qc * otok + 16 * s + 8 * h2);
   }
   const float nlq = -lse[((int64_t)b * H + hh) * T + qc];
+  // row constants as the initial accumulators: S' = (c Q) K^T - lse and dP' = dO V^T - delta,
+  // so p = exp2(S') and dS = p * dP' need no per-score fma / subtract
+  const f32x16 lq16 = splat16(nlq);
   // delta[q] = sum_d dO[q, d] * O[q, d], computed here from the dO fragments already in registers
   // (this lane holds 32 of the 64 d, its partner lane l ^ 32 the rest) instead of by a separate
   // kernel; written out for the dK/dV kernel, which runs after this one
@@ -365,6 +389,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     dq_delta = xhalf_sum(acc);
     if (h2 == 0 && q < T) delta[((int64_t)b * H + hh) * T + q] = dq_delta;
   }
+  const f32x16 dl16 = splat16(-dq_delta);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = prescale(qf[s], scale_log2);
   f32x16 a0 = {}, a1 = {};
   const int kend = min(T, q0 + A_BQ);
   const int nkt = (kend + A_BK - 1) / A_BK;
@@ -402,7 +429,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     for (int sub = 0; sub < 2; ++sub) {
       const int kb = kt * A_BK + sub * 32;
       if (MASK && kb > qw + 31) continue;
-      f32x16 st = {}, dp = {};
+      f32x16 st = lq16, dp = dl16;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         st = mfma32(row_frag_swz(sK_(cur), sub * 32 + col, s, h2), qf[s], st);
@@ -410,12 +437,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p = __builtin_amdgcn_exp2f(fmaf(st[r], scale_log2, nlq));
+        float p = __builtin_amdgcn_exp2f(st[r]);
         if (MASK) {
           const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
           p = key > q ? 0.f : p;
         }
-        st[r] = p * (dp[r] - dq_delta);  // dS^T
+        st[r] = p * dp[r];  // dS^T
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {

@@ -5,6 +5,8 @@
 // One wave64 owns one row; a 256-thread block covers 4 rows. The row is held in registers
 // (CH = ceil(C/512) chunks of 8 elements per lane), so the variance is an exact two-pass
 // computation over registers with a single HBM read of the row.
+#include <type_traits>
+
 #include "vcx_api.h"
 #include "vcx_common.h"
 
@@ -101,8 +103,12 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16* __restrict__ a,
 // dres, mean and rstd loads are issued before this row's two cross-lane reductions, so every
 // lane keeps (2 or 3) x CH 16-B loads in flight through the shuffles (the row loop is otherwise
 // latency-bound at ~3.5 TB/s). RES is a template flag so no load sits behind a runtime branch.
-template <int CH, bool RES>
-__global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+// VEC = elements per lane access: 8 (16-B loads) in general; 4 (8-B loads) when the row is a
+// multiple of 256 but not of 512 elements (C = 768: 3 chunks on every lane instead of 2 on half
+// the lanes and 1 on the rest; 140 instead of 182 VGPRs: 3 instead of 2 waves per SIMD, so 1.5x the
+// bytes in flight per CU). Forcing 4 waves per SIMD spills.
+template <int CH, bool RES, int VEC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VEC == 4 ? 3 : 1))) ln_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                       const bf16* __restrict__ w, const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in,
                                                       const bf16* __restrict__ dres, bf16* __restrict__ dx,
@@ -111,28 +117,29 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int nw = gridDim.x * 4;
-  const int C8 = C >> 3;
+  using BV = std::conditional_t<VEC == 8, bf16x8, bf16x4>;
+  const int C8 = C / VEC;  // VEC-element chunks per row
   const float invC = 1.f / (float)C;
-  float dwacc[CH][8], dbacc[CH][8], wreg[CH][8], dxacc[CH][8];
+  float dwacc[CH][VEC], dbacc[CH][VEC], wreg[CH][VEC], dxacc[CH][VEC];
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     const int c = lane + k * 64;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < VEC; ++j) {
       dwacc[k][j] = 0.f;
       dbacc[k][j] = 0.f;
       wreg[k][j] = 0.f;
       dxacc[k][j] = 0.f;
     }
     if (c < C8) {
-      bf16x8 wv = *(const bf16x8*)(w + c * 8);
+      BV wv = *(const BV*)(w + c * VEC);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) wreg[k][j] = (float)wv[j];
+      for (int j = 0; j < VEC; ++j) wreg[k][j] = (float)wv[j];
     }
   }
-  bf16x8 cd[CH], cx[CH], cr[CH];
+  BV cd[CH], cx[CH], cr[CH];
   float cmean = 0.f, crstd = 0.f;
-  auto load = [&](int row, bf16x8(&d)[CH], bf16x8(&xv)[CH], bf16x8(&rv)[CH], float& mu, float& rs) {
+  auto load = [&](int row, BV(&d)[CH], BV(&xv)[CH], BV(&rv)[CH], float& mu, float& rs) {
     const int64_t off = (int64_t)row * C;
     mu = mean_in[row];
     rs = rstd_in[row];
@@ -140,50 +147,54 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
     for (int k = 0; k < CH; ++k) {
       const int c = lane + k * 64;
       if (c < C8) {
-        d[k] = *(const bf16x8*)(dy + off + c * 8);
-        xv[k] = *(const bf16x8*)(x + off + c * 8);
-        if (RES) rv[k] = *(const bf16x8*)(dres + off + c * 8);
+        d[k] = *(const BV*)(dy + off + c * VEC);
+        xv[k] = *(const BV*)(x + off + c * VEC);
+        if (RES) rv[k] = *(const BV*)(dres + off + c * VEC);
       }
     }
   };
   if (gw < R) load(gw, cd, cx, cr, cmean, crstd);
   for (int row = gw; row < R; row += nw) {
-    bf16x8 nd[CH], nx[CH], nr[CH];
+    BV nd[CH], nx[CH], nr[CH];
     float nmean = 0.f, nrstd = 0.f;
     if (row + nw < R) load(row + nw, nd, nx, nr, nmean, nrstd);
     const int64_t off = (int64_t)row * C;
-    float xh[CH][8], g[CH][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       const int c = lane + k * 64;
       if (c < C8) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < VEC; ++j) {
           const float d = (float)cd[k][j];
-          xh[k][j] = ((float)cx[k][j] - cmean) * crstd;
-          g[k][j] = d * wreg[k][j];
-          s1 += g[k][j];
-          s2 = fmaf(g[k][j], xh[k][j], s2);
-          dwacc[k][j] = fmaf(d, xh[k][j], dwacc[k][j]);
+          const float xh = ((float)cx[k][j] - cmean) * crstd;
+          const float g = d * wreg[k][j];
+          s1 += g;
+          s2 = fmaf(g, xh, s2);
+          dwacc[k][j] = fmaf(d, xh, dwacc[k][j]);
           dbacc[k][j] += d;
         }
       }
     }
     s1 = rms ? 0.f : wave_sum(s1) * invC;
     s2 = wave_sum(s2) * invC;
+    // dx = rstd*(g - s1) - xhat*rstd*s2 with g and xhat recomputed from the loaded bf16 row (written
+    // as different expressions so they are not merged with the first pass's values and kept alive:
+    // 2 x CH x VEC fewer live registers through the reductions)
+    const float k2 = crstd * crstd * s2, mk2 = cmean * k2;
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       const int c = lane + k * 64;
       if (c < C8) {
-        bf16x8 o;
+        BV o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = crstd * (g[k][j] - s1 - xh[k][j] * s2) + (RES ? (float)cr[k][j] : 0.f);
+        for (int j = 0; j < VEC; ++j) {
+          const float gs = fmaf((float)cd[k][j], wreg[k][j], -s1);
+          const float v = fmaf(crstd, gs, -fmaf((float)cx[k][j], k2, -mk2)) + (RES ? (float)cr[k][j] : 0.f);
           o[j] = (bf16)v;
           dxacc[k][j] += v;
         }
-        *(bf16x8*)(dx + off + c * 8) = o;
+        *(BV*)(dx + off + c * VEC) = o;
       }
     }
 #pragma unroll
@@ -195,18 +206,19 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
     cmean = nmean;
     crstd = nrstd;
   }
-  if constexpr (CH <= 4) {
+  if constexpr (CH * VEC <= 32) {
     // sum the 4 waves' column partials in LDS: ONE partial row per block (4x less partial traffic
     // for the column-sum kernels: 9 instead of 38 MB per call at the GPT-2 bench shape)
-    __shared__ __attribute__((aligned(16))) float red[4][CH * 512];
+    __shared__ __attribute__((aligned(16))) float red[4][CH * 64 * VEC];
     const int w = threadIdx.x >> 6;
-    auto reduce_out = [&](float(&acc)[CH][8], float* part) {
+    auto reduce_out = [&](float(&acc)[CH][VEC], float* part) {
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
         const int c = lane + k * 64;
         if (c < C8) {
-          *(f32x4*)(&red[w][c * 8]) = f32x4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
-          *(f32x4*)(&red[w][c * 8 + 4]) = f32x4{acc[k][4], acc[k][5], acc[k][6], acc[k][7]};
+#pragma unroll
+          for (int j = 0; j < VEC; j += 4)
+            *(f32x4*)(&red[w][c * VEC + j]) = f32x4{acc[k][j], acc[k][j + 1], acc[k][j + 2], acc[k][j + 3]};
         }
       }
       __syncthreads();
@@ -218,6 +230,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16* __restrict__ dy
     if (db_part) reduce_out(dbacc, db_part);
     if (dbb_part) reduce_out(dxacc, dbb_part);  // gradient of the branch bias = column sums of dx
   } else {
+    static_assert(VEC == 8, "per-wave partial rows are written as 8-column chunks");
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
       const int c = lane + k * 64;
@@ -748,17 +761,19 @@ void vcx_bias_gelu_bwd(const void* x, const void* b, const void* dy, void* dx, f
   colsums(part, nullptr, nullptr, db, nullptr, nullptr, 1, G, F, stage, s, accumulate ? 1 : 0);
 }
 
-static int ln_bwd_blocks(int R) {
-  // enough waves to keep every SIMD busy with several rows in flight (each wave streams ~16 rows)
+static int ln_bwd_blocks(int R, int C) {
+  // enough waves to keep every SIMD busy with several rows in flight (each wave streams ~16 rows);
+  // the C = 768 variant holds 3 blocks per CU (140 VGPRs): one full round of 768 blocks, no tail
+  const int cap = C == 768 ? 768 : 1024;
   const int g = (R + 3) / 4;
-  return g > 1024 ? 1024 : g;
+  return g > cap ? cap : g;
 }
 
 int vcx_ln_bwd_partials(int R, int C) {
   // [P, C] fp32 partial rows: one per block when the row fits the LDS reduction (C <= 2048),
   // else one per wave
   const int ch = (C / 8 + 63) / 64;
-  return ch <= 4 ? ln_bwd_blocks(R) : ln_bwd_blocks(R) * 4;
+  return ch <= 4 ? ln_bwd_blocks(R, C) : ln_bwd_blocks(R, C) * 4;
 }
 
 void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, const void* dres,
@@ -766,13 +781,22 @@ void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean,
                 void* dbb, float* stage, int accum_mask, hipStream_t s) {
   const int ch = (C / 8 + 63) / 64;
   const int P = vcx_ln_bwd_partials(R, C);
-  dim3 grid(ln_bwd_blocks(R));
-  if (dres) {
-    VCX_LN_DISPATCH(ch, hipLaunchKernelGGL((ln_bwd_kernel<CH, true>), grid, dim3(256), 0, s, (const bf16*)dy,
+  dim3 grid(ln_bwd_blocks(R, C));
+  if (C == 768) {  // GPT-2-small width: 8-B accesses, 3 per lane (see the kernel)
+    if (dres)
+      hipLaunchKernelGGL((ln_bwd_kernel<3, true, 4>), grid, dim3(256), 0, s, (const bf16*)dy, (const bf16*)x,
+                         (const bf16*)w, mean, rstd, (const bf16*)dres, (bf16*)dx, dw_part, db_part, R, C, rms,
+                         dbb_part);
+    else
+      hipLaunchKernelGGL((ln_bwd_kernel<3, false, 4>), grid, dim3(256), 0, s, (const bf16*)dy, (const bf16*)x,
+                         (const bf16*)w, mean, rstd, (const bf16*)nullptr, (bf16*)dx, dw_part, db_part, R, C, rms,
+                         dbb_part);
+  } else if (dres) {
+    VCX_LN_DISPATCH(ch, hipLaunchKernelGGL((ln_bwd_kernel<CH, true, 8>), grid, dim3(256), 0, s, (const bf16*)dy,
                                            (const bf16*)x, (const bf16*)w, mean, rstd, (const bf16*)dres,
                                            (bf16*)dx, dw_part, db_part, R, C, rms, dbb_part));
   } else {
-    VCX_LN_DISPATCH(ch, hipLaunchKernelGGL((ln_bwd_kernel<CH, false>), grid, dim3(256), 0, s, (const bf16*)dy,
+    VCX_LN_DISPATCH(ch, hipLaunchKernelGGL((ln_bwd_kernel<CH, false, 8>), grid, dim3(256), 0, s, (const bf16*)dy,
                                            (const bf16*)x, (const bf16*)w, mean, rstd, (const bf16*)nullptr,
                                            (bf16*)dx, dw_part, db_part, R, C, rms, dbb_part));
   }

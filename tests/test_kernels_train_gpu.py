@@ -13,11 +13,11 @@ def _bf(x):
     return x.to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("C", [64, 768, 1024, 1600, 4096])
+@pytest.mark.parametrize("C,R", [(64, 257), (768, 257), (768, 24577), (1024, 257), (1600, 257), (4096, 257)])
 @pytest.mark.parametrize("fused", [False, True])
-def test_add_layernorm_fwd_bwd(gpu, C, fused):
+def test_add_layernorm_fwd_bwd(gpu, C, R, fused):
+    """R = 24577 at C = 768: every wave of the 768-block backward grid walks many rows."""
     torch.manual_seed(0)
-    R = 257
     a = _bf(torch.randn(R, C, device=gpu)).requires_grad_()
     b = _bf(torch.randn(R, C, device=gpu)).requires_grad_() if fused else None
     w = _bf(torch.rand(C, device=gpu) + 0.5).requires_grad_()
@@ -32,8 +32,9 @@ def test_add_layernorm_fwd_bwd(gpu, C, fused):
     yr = F.layer_norm(xr, (C,), w32, bias32, 1e-5)
     assert torch.allclose(x.float(), xr.detach(), atol=2e-2, rtol=1e-2)
     assert torch.allclose(y.float(), yr.detach(), atol=3e-2, rtol=2e-2)
-    dy = torch.randn(R, C, device=gpu)
-    dx_res = torch.randn(R, C, device=gpu)
+    # bf16-representable upstream gradients: the kernel and the reference see the same values
+    dy = _bf(torch.randn(R, C, device=gpu)).float()
+    dx_res = _bf(torch.randn(R, C, device=gpu)).float()
     loss = (y.float() * dy).sum() + (x.float() * dx_res).sum()
     loss.backward()
     lr = (yr * dy).sum() + (xr * dx_res).sum()
@@ -41,8 +42,10 @@ def test_add_layernorm_fwd_bwd(gpu, C, fused):
     assert torch.allclose(a.grad.float(), a32.grad, atol=5e-2, rtol=3e-2)
     if fused:
         assert torch.allclose(b.grad.float(), b32.grad, atol=5e-2, rtol=3e-2)
-    assert torch.allclose(w.grad.float(), w32.grad, atol=0.5, rtol=3e-2)
-    assert torch.allclose(bias.grad.float(), bias32.grad, atol=0.5, rtol=3e-2)
+    # column sums over R rows: the bf16 rounding of x / y in the forward adds noise ~ sqrt(R)
+    tol = 0.5 * max(1.0, (R / 257) ** 0.5)
+    assert torch.allclose(w.grad.float(), w32.grad, atol=tol, rtol=3e-2)
+    assert torch.allclose(bias.grad.float(), bias32.grad, atol=tol, rtol=3e-2)
 
 
 def test_rmsnorm(gpu):
