@@ -428,8 +428,34 @@ at::Tensor attn_bwd(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor 
   auto dqkv = at::empty_like(qkv);
   auto delta = at::empty({B, H, T}, lse.options());
   vcx_attn_bwd_d64(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
-                   dqkv.data_ptr(), (int)B, (int)T, (int)H, (float)scale, cur_stream());
+                   dqkv.data_ptr(), nullptr, (int)B, (int)T, (int)H, (float)scale, cur_stream());
   return dqkv;
+}
+
+// attn_bwd plus the gradient of a bias added to qkv ([3 * H * 64]: the fused QKV projection's
+// bias), reduced from per-block column sums the backward kernels emit — no separate pass over
+// dqkv. db_out: the preset (flat) gradient buffer to add into; returned otherwise.
+std::vector<at::Tensor> attn_bwd_bias(at::Tensor qkv, at::Tensor out, at::Tensor dout, at::Tensor lse, double scale,
+                                      c10::optional<at::Tensor> db_out) {
+  CHECK_IN(qkv, kBF);
+  CHECK_IN(out, kBF);
+  CHECK_IN(dout, kBF);
+  CHECK_IN(lse, kF);
+  TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.size(4) == 64);
+  const int64_t B = qkv.size(0), T = qkv.size(1), H = qkv.size(3), F = 3 * H * 64;
+  TORCH_CHECK(out.sizes() == at::IntArrayRef({B, T, H, 64}) && dout.sizes() == out.sizes());
+  TORCH_CHECK(lse.numel() == B * H * T);
+  auto dqkv = at::empty_like(qkv);
+  auto delta = at::empty({B, H, T}, lse.options());
+  const int P = vcx_attn_bias_partials((int)B, (int)T);
+  auto part = at::empty({P, F}, lse.options());
+  int mask = 0;
+  at::Tensor db = grad_out(db_out, F, qkv, &mask, 0);
+  auto stage = at::empty({VCX_COLSUM_NB * F}, lse.options());
+  vcx_attn_bwd_d64(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(),
+                   dqkv.data_ptr(), part.data_ptr<float>(), (int)B, (int)T, (int)H, (float)scale, cur_stream());
+  vcx_colsum_f32(part.data_ptr<float>(), db.data_ptr(), P, (int)F, mask, stage.data_ptr<float>(), cur_stream());
+  return {dqkv, db};
 }
 
 }  // namespace
@@ -473,6 +499,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_qkv_fwd", &rope_qkv_fwd);
   m.def("rope_qkv_bwd", &rope_qkv_bwd);
   m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd_bias", &attn_bwd_bias, pybind11::arg("qkv"), pybind11::arg("out"), pybind11::arg("dout"),
+        pybind11::arg("lse"), pybind11::arg("scale"), pybind11::arg("db_out") = pybind11::none());
   vcx_register_vision(m);
   vcx_register_compress(m);
   vcx_register_lt(m);

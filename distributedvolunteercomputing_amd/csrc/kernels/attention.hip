@@ -133,6 +133,37 @@ __device__ __forceinline__ float xhalf_sum(float v) {
   return __int_as_float(r[0]) + __int_as_float(r[1]);
 }
 
+// Column sums of a wave's accumulator tile for the fused QKV-bias gradient. v holds the 32 values
+// of one lane (= one row; the two 32-lane halves hold different columns); each step exchanges
+// half of the live registers with lane l ^ K (ds_swizzle, 32-lane groups) and adds, so the live
+// set halves: 31 swizzles in all. Afterwards v[0] of lane c of a half = the sum over the half's
+// 32 rows of register c.
+template <int K>
+__device__ __forceinline__ float swz_xor(float x) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), (K << 10) | 0x1F));
+}
+template <int K>
+__device__ __forceinline__ void fold_step(float (&v)[32], int col) {
+  const bool hi = (col & K) != 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const float keep = hi ? v[j + K] : v[j];
+    const float send = hi ? v[j] : v[j + K];
+    v[j] = keep + swz_xor<K>(send);
+  }
+}
+__device__ __forceinline__ float half_colsum32(float (&v)[32], int col) {
+  fold_step<16>(v, col);
+  fold_step<8>(v, col);
+  fold_step<4>(v, col);
+  fold_step<2>(v, col);
+  fold_step<1>(v, col);
+  return v[0];
+}
+// head-dim column of register c (0..31) of the pair of 32x32 accumulators (c < 16: first, d < 32)
+// in the lane half h2: registers 4g + i hold d = 8g + 4 h2 + i
+__device__ __forceinline__ int acc_pair_col(int c, int h2) { return (c & 16) * 2 + 8 * ((c & 15) >> 2) + 4 * h2 + (c & 3); }
+
 // LDS-DMA of a 64-row x 64-column bf16 tile — rows r0 .. r0+63 of a row-major matrix with row
 // stride `ld` elements, row indices clamped to rmax — into the XOR-swizzled image `img` (swz
 // layout). Each of the 4 waves moves two 1-KB pieces with global_load_lds_dwordx4; the DMA writes a
@@ -341,6 +372,7 @@ template <int WPE, bool DMA>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) attn_bwd_dq_d64_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
                                                                const bf16* __restrict__ out, const float* __restrict__ lse,
                                                                float* __restrict__ delta, bf16* __restrict__ dqkv,
+                                                               float* __restrict__ bpart,
                                                                int B, int T, int H, float scale, float scale_log2) {
   // one shared object per buffer (see the forward): [K | V] tiles, swizzled (swz)
   __shared__ __attribute__((aligned(16))) bf16 sKV0[2][A_BK * AD];
@@ -499,6 +531,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       *(bf16x4*)(row + 32 + d) = v1;
     }
   }
+  if (bpart) {  // column sums of this block's dQ rows: one partial row of the QKV bias gradient
+    float v[32];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      v[r] = q < T ? a0[r] * scale : 0.f;
+      v[16 + r] = q < T ? a1[r] * scale : 0.f;
+    }
+    const float cs = half_colsum32(v, col);
+    float* red = (float*)&sKV0[0][0];  // the K/V tiles are dead after the last barrier of the loop
+    red[w * AD + acc_pair_col(col, h2)] = cs;
+    __syncthreads();
+    if (tid < AD)
+      bpart[((int64_t)b * nqt + qt) * 3 * H * AD + hh * AD + tid] =
+          (red[tid] + red[AD + tid]) + (red[2 * AD + tid] + red[3 * AD + tid]);
+  }
 #undef sK_
 #undef sV_
 }
@@ -514,8 +561,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ lse,
                                                                  const float* __restrict__ delta,
-                                                                 bf16* __restrict__ dqkv, int B, int T, int H,
-                                                                 float scale, float scale_log2) {
+                                                                 bf16* __restrict__ dqkv, float* __restrict__ bpart,
+                                                                 int B, int T, int H, float scale, float scale_log2) {
   // one shared object per buffer (see the forward): [Q | dO] tiles, swizzled (swz)
   __shared__ __attribute__((aligned(16))) bf16 sQD0[2][B_BQ * AD];
   __shared__ __attribute__((aligned(16))) bf16 sQD1[2][B_BQ * AD];
@@ -675,6 +722,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       *(bf16x4*)(rowv + 32 + d) = v1;
     }
   }
+  if (bpart) {  // column sums of this block's dK and dV rows: slots 1 and 2 of a QKV-bias partial row
+    float* red = (float*)&sQD0[0][0];  // the Q/dO tiles are dead after the last barrier of the loop
+    float v[32];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      v[r] = key < T ? dk0[r] * scale : 0.f;
+      v[16 + r] = key < T ? dk1[r] * scale : 0.f;
+    }
+    red[w * AD + acc_pair_col(col, h2)] = half_colsum32(v, col);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      v[r] = key < T ? dv0[r] : 0.f;
+      v[16 + r] = key < T ? dv1[r] : 0.f;
+    }
+    red[4 * AD + w * AD + acc_pair_col(col, h2)] = half_colsum32(v, col);
+    __syncthreads();
+    if (tid < 2 * AD) {
+      const int sl = tid >> 6, d = tid & 63;
+      const float* rr = red + sl * 4 * AD;
+      bpart[((int64_t)b * nkb + kbi) * 3 * H * AD + (1 + sl) * H * AD + hh * AD + d] =
+          (rr[d] + rr[AD + d]) + (rr[2 * AD + d] + rr[3 * AD + d]);
+    }
+  }
 #undef sQ_
 #undef sD_
 }
@@ -697,23 +767,27 @@ void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma) {
   if (bwd_dma >= 0 && bwd_dma <= 3) g_bwd_dma = bwd_dma;
 }
 
+int vcx_attn_bias_partials(int B, int T) { return B * ((T + 127) / 128); }
+
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
-                      int B, int T, int H, float scale, hipStream_t s) {
+                      float* bias_part, int B, int T, int H, float scale, hipStream_t s) {
   // dQ first: it also computes delta = rowsum(dO * O) for the dK/dV kernel
   const int nkb = (T + 127) / 128;
   const int nqt = (T + A_BQ - 1) / A_BQ;
   if (g_bwd_dma & 1)
     hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, true>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
-                       (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+                       (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale,
+                       scale * LOG2E);
   else
     hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, false>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
-                       (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+                       (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale,
+                       scale * LOG2E);
   if (g_bwd_dma & 2)
     hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, true>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
-                       (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E);
   else
     hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, false>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
-                       (const bf16*)dout, lse, delta, (bf16*)dqkv, B, T, H, scale, scale * LOG2E);
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E);
 }
 
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s) {

@@ -819,6 +819,10 @@ void vcx_ln_bwd(const void* dy, const void* x, const void* w, const float* mean,
   colsums(ps[0], ps[1], ps[2], os[0], os[1], os[2], n, P, C, stage, s, slot_mask);
 }
 
+void vcx_colsum_f32(const float* part, void* out, int P, int C, int accumulate, float* stage, hipStream_t s) {
+  colsums(part, nullptr, nullptr, out, nullptr, nullptr, 1, P, C, stage, s, accumulate ? 1 : 0);
+}
+
 void vcx_colsum_bf16(const void* y, float* part, void* out, int R, int F, int accumulate, float* stage,
                      hipStream_t s) {
   const int G = bias_gelu_groups(R);

@@ -25,6 +25,8 @@ constexpr int VCX_COLSUM_NB = 32;  // stage-1 row chunks of the two-stage column
 void vcx_bias_gelu_bwd(const void* x, const void* b, const void* dy, void* dx, float* part, void* db, int R, int F,
                        float* stage, int accumulate, hipStream_t s);
 // column sums of a bf16 [R, F] matrix into out[F] (bf16; added to it when accumulate != 0)
+// out[C] (+)= column sums of fp32 partial rows part[P, C] (bf16 out; stage: VCX_COLSUM_NB * C fp32)
+void vcx_colsum_f32(const float* part, void* out, int P, int C, int accumulate, float* stage, hipStream_t s);
 void vcx_colsum_bf16(const void* y, float* part, void* out, int R, int F, int accumulate, float* stage,
                      hipStream_t s);
 int vcx_ln_bwd_partials(int R, int C);
@@ -48,8 +50,11 @@ void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int 
 // variants: forward 2 or 3 waves per SIMD (default 3); K/V (Q/dO) tile staging through registers
 // (0) or LDS-DMA (1) for the forward (default 1) and the backward (bit 0: dQ, bit 1: dK/dV; default 1)
 void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma);
+// bias_part (nullable): [B * ceil(T/128), 3 * H * 64] fp32, one row of column sums of dqkv per
+// 128-row block (the gradient of a bias added to qkv: reduce with vcx_colsum_f32)
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
-                      int B, int T, int H, float scale, hipStream_t s);
+                      float* bias_part, int B, int T, int H, float scale, hipStream_t s);
+int vcx_attn_bias_partials(int B, int T);
 
 // rope.hip: rotary embedding fused with the QKV split into head-major q/k/v (and its inverse)
 void vcx_rope_qkv(void* qkv, void* q, void* k, void* v, const float* cosv, const float* sinv, int B, int T, int Hq,

@@ -79,9 +79,13 @@ class Block(nn.Module):
     def attn(self, h):
         B, T, C = h.shape
         H = self.n_head
-        qkv = ops.linear(h, self.attn_w, self.attn_b).view(B, T, 3, H, C // H)
+        # on the native path the QKV bias gradient comes out of the attention backward kernels
+        # (column sums of dqkv per block) instead of a separate pass over dqkv
+        fuse = (C // H == 64 and h.dtype == torch.bfloat16 and ops.native_linear_ok(self.attn_w)
+                and self.attn_b.requires_grad)
+        qkv = ops.linear(h, self.attn_w, self.attn_b, bias_grad_elsewhere=fuse).view(B, T, 3, H, C // H)
         if C // H == 64 and qkv.is_cuda:
-            y = ops.causal_attention(qkv)  # HIP flash attention on the packed layout
+            y = ops.causal_attention(qkv, bias=self.attn_b if fuse else None)  # HIP flash attention, packed layout
         else:
             q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
             with sdpa_kernel(_SDPA_BACKENDS):

@@ -2,9 +2,9 @@
 on CPU the same call runs the plain-PyTorch reference (used by tests and CPU volunteers)."""
 from ._lib import available as native_available, native  # noqa: F401
 from .activations import bias_gelu, gelu, swiglu  # noqa: F401
-from .attention import causal_attention  # noqa: F401
+from .attention import causal_attention, fused_bias_grad_ok  # noqa: F401
 from .embedding import embed  # noqa: F401
-from .linear import linear, wgrad  # noqa: F401
+from .linear import linear, native_linear_ok, wgrad  # noqa: F401
 from .loss import cross_entropy  # noqa: F401
 from .norm import add_layernorm, add_rmsnorm, layernorm, rmsnorm  # noqa: F401
 from .rope import rope_qkv  # noqa: F401

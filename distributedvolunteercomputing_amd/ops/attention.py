@@ -12,22 +12,31 @@ import math
 import torch
 import torch.nn.functional as F
 
-from ._lib import native, use_native
+from ._lib import grad_buffer, native, use_native
 
 
 class _Attn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, scale):
+    def forward(ctx, qkv, scale, bias):
         C = native()
         out, lse = C.attn_fwd(qkv, scale)
         ctx.save_for_backward(qkv, out, lse)
         ctx.scale = scale
+        ctx.bias = bias  # not used by the forward: only its gradient is produced here
         return out
 
     @staticmethod
     def backward(ctx, dout):
         qkv, out, lse = ctx.saved_tensors
-        return native().attn_bwd(qkv, out, dout.contiguous(), lse, ctx.scale), None
+        C = native()
+        bias, ctx.bias = ctx.bias, None
+        if bias is None or not ctx.needs_input_grad[2]:
+            return C.attn_bwd(qkv, out, dout.contiguous(), lse, ctx.scale), None, None
+        # the backward kernels also emit per-block column sums of dqkv = the gradient of the bias
+        # the QKV projection added (linear(..., bias_grad_elsewhere=True)): no pass over dqkv
+        gb = grad_buffer(bias)
+        dqkv, db = C.attn_bwd_bias(qkv, out, dout.contiguous(), lse, ctx.scale, gb)
+        return dqkv, None, (None if gb is not None else db.view_as(bias))
 
 
 def _ref(qkv, scale):
@@ -36,10 +45,20 @@ def _ref(qkv, scale):
     return y.transpose(1, 2)
 
 
-def causal_attention(qkv: torch.Tensor, scale: float | None = None) -> torch.Tensor:
-    """qkv [B, T, 3, H, D] -> out [B, T, H, D] (causal)."""
+def fused_bias_grad_ok(qkv: torch.Tensor) -> bool:
+    """True when causal_attention(qkv, bias=...) computes the QKV-bias gradient in its kernels."""
+    return use_native(qkv) and qkv.shape[-1] == 64 and qkv.dtype == torch.bfloat16
+
+
+def causal_attention(qkv: torch.Tensor, scale: float | None = None, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """qkv [B, T, 3, H, D] -> out [B, T, H, D] (causal).
+
+    bias: the [3*H*D] bias already added into qkv by the projection, whose gradient this op then
+    returns (only valid with ``linear(..., bias_grad_elsewhere=True)`` and when
+    ``fused_bias_grad_ok(qkv)``; otherwise leave it None)."""
     D = qkv.shape[-1]
     scale = 1.0 / math.sqrt(D) if scale is None else scale
-    if use_native(qkv) and D == 64 and qkv.dtype == torch.bfloat16:
-        return _Attn.apply(qkv.contiguous(), scale)
+    if fused_bias_grad_ok(qkv):
+        return _Attn.apply(qkv.contiguous(), scale, bias)
+    assert bias is None, "bias gradient fusion needs the native hd64 bf16 attention path"
     return _ref(qkv, scale)

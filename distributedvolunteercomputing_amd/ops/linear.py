@@ -174,9 +174,11 @@ def _param_grads(dy2, x2, w, bias, want_w, want_b):
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, bias_grad_elsewhere=False):
         ctx.save_for_backward(x, w)
-        ctx.has_bias = b is not None
+        # bias_grad_elsewhere: the sole consumer of y computes the bias gradient itself (column
+        # sums it already has at hand) and returns it for the same bias tensor
+        ctx.has_bias = b is not None and not bias_grad_elsewhere
         ctx.bias = b
         x2 = x.reshape(-1, x.shape[-1])
         return mm(x2, w, trans_b=True, bias=b).view(*x.shape[:-1], w.shape[0])
@@ -204,13 +206,21 @@ class _Linear(torch.autograd.Function):
             dy2.record_stream(side)  # keep the inputs' memory until the side stream is done with it
             x2.record_stream(side)
             _queue_join(main, side, dy2.device)
-            return dx, None, None
+            return dx, None, None, None
         dw, db = _param_grads(dy2, x2, w, bias, want_w, want_b)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
-    """y = x @ w^T (+ b), x [..., K], w [N, K]."""
-    if use_native(w) and w.dtype == torch.bfloat16 and torch.is_grad_enabled() and w.requires_grad:
-        return _Linear.apply(x, w, b)
+def native_linear_ok(w: torch.Tensor) -> bool:
+    """True when linear(x, w, ...) runs the native autograd path (where bias_grad_elsewhere applies)."""
+    return use_native(w) and w.dtype == torch.bfloat16 and torch.is_grad_enabled() and w.requires_grad
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
+           bias_grad_elsewhere: bool = False) -> torch.Tensor:
+    """y = x @ w^T (+ b), x [..., K], w [N, K]. With bias_grad_elsewhere the backward leaves the
+    bias gradient to y's consumer (e.g. ``causal_attention(qkv, bias=b)``), which must then be
+    y's only consumer and return d(loss)/d(b) = column sums of dy for the same tensor."""
+    if native_linear_ok(w):
+        return _Linear.apply(x, w, b, bias_grad_elsewhere)
     return F.linear(x, w, b)

@@ -39,6 +39,29 @@ def test_attention_fwd_bwd(gpu, B, T, H):
         assert rel < 2e-2, (nm, float(rel))
 
 
+@pytest.mark.parametrize("B,T,H", [(2, 200, 3), (1, 1024, 12), (3, 77, 2)])
+@pytest.mark.parametrize("preset", [False, True])
+def test_attention_fused_qkv_bias_grad(gpu, B, T, H, preset):
+    """linear(..., bias_grad_elsewhere=True) + causal_attention(qkv, bias=b): the bias gradient is
+    reduced from the backward kernels' per-block column sums (T not a multiple of 128: padded
+    query/key rows must not contribute) and equals the column sums of dqkv."""
+    torch.manual_seed(2)
+    C = H * 64
+    x = torch.randn(B, T, C, device=gpu).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(3 * C, C, device=gpu) * C ** -0.5).to(torch.bfloat16).requires_grad_()
+    b = (torch.randn(3 * C, device=gpu) * 0.1).to(torch.bfloat16).requires_grad_()
+    if preset:  # flat-buffer style: the gradient is added into the existing .grad
+        b.grad = torch.full_like(b, 0.5)
+    qkv = ops.linear(x, w, b, bias_grad_elsewhere=True).view(B, T, 3, H, 64)
+    qkv.retain_grad()
+    out = ops.causal_attention(qkv, bias=b)
+    do = torch.randn_like(out)
+    (out.float() * do.float()).sum().backward()
+    ref = qkv.grad.float().reshape(-1, 3 * C).sum(0) + (0.5 if preset else 0.0)
+    rel = (b.grad.float() - ref).norm() / ref.norm()
+    assert rel < 1e-2, float(rel)
+
+
 def test_attention_matches_sdpa_at_bench_shape(gpu):
     torch.manual_seed(1)
     B, T, H = 4, 1024, 12
