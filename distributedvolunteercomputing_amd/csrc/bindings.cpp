@@ -495,7 +495,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("embed_bwd", &embed_bwd, pybind11::arg("idx"), pybind11::arg("dx"), pybind11::arg("V"), pybind11::arg("T"),
         pybind11::arg("Tpos"), pybind11::arg("wte_grad") = pybind11::none(), pybind11::arg("wpe_grad") = pybind11::none());
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_set_variant", &vcx_attn_set_variant);
+  m.def("attn_set_variant", &vcx_attn_set_variant, pybind11::arg("fwd_wpe"), pybind11::arg("fwd_dma"),
+        pybind11::arg("bwd_dma"), pybind11::arg("stage_epi") = -1);
   m.def("rope_qkv_fwd", &rope_qkv_fwd);
   m.def("rope_qkv_bwd", &rope_qkv_bwd);
   m.def("attn_bwd", &attn_bwd);

@@ -164,6 +164,47 @@ __device__ __forceinline__ float half_colsum32(float (&v)[32], int col) {
 // in the lane half h2: registers 4g + i hold d = 8g + 4 h2 + i
 __device__ __forceinline__ int acc_pair_col(int c, int h2) { return (c & 16) * 2 + 8 * ((c & 15) >> 2) + 4 * h2 + (c & 3); }
 
+// Stores a wave's 32-row x 64-column accumulator pair (a0: columns 0-31, a1: 32-63; lane = row
+// `col`, registers 4g + i = column 8g + 4 h2 + i) times `mul` (per lane = per row) as bf16 rows of
+// a row-major matrix (dst = row 0, row stride ld; rows >= nrows are skipped). staged: through a
+// wave-private, chunk-swizzled 32 x 64 LDS image `img`, then 4 fully coalesced 16-B stores per lane
+// (whole 128-B rows) instead of 8 half-row 8-B stores.
+__device__ __forceinline__ void store_acc_tile(const f32x16& a0, const f32x16& a1, float mul, bf16* dst, int64_t ld,
+                                               int nrows, bf16* img, bool staged, int lane) {
+  const int col = lane & 31, h2 = lane >> 5;
+  if (staged) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 v0 = {(bf16)(a0[4 * g] * mul), (bf16)(a0[4 * g + 1] * mul), (bf16)(a0[4 * g + 2] * mul),
+                   (bf16)(a0[4 * g + 3] * mul)};
+      bf16x4 v1 = {(bf16)(a1[4 * g] * mul), (bf16)(a1[4 * g + 1] * mul), (bf16)(a1[4 * g + 2] * mul),
+                   (bf16)(a1[4 * g + 3] * mul)};
+      *(bf16x4*)(img + col * AD + ((g ^ (col & 7)) << 3) + 4 * h2) = v0;
+      *(bf16x4*)(img + col * AD + (((g + 4) ^ (col & 7)) << 3) + 4 * h2) = v1;
+    }
+    __builtin_amdgcn_wave_barrier();  // the wave reads back only its own image
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = i * 8 + (lane >> 3), c = lane & 7;
+      const bf16x8 v = *(const bf16x8*)(img + r * AD + ((c ^ (r & 7)) << 3));
+      if (r < nrows) *(bf16x8*)(dst + r * ld + c * 8) = v;
+    }
+  } else if (col < nrows) {
+    bf16* row = dst + col * ld;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * h2;
+      bf16x4 v0 = {(bf16)(a0[4 * g] * mul), (bf16)(a0[4 * g + 1] * mul), (bf16)(a0[4 * g + 2] * mul),
+                   (bf16)(a0[4 * g + 3] * mul)};
+      bf16x4 v1 = {(bf16)(a1[4 * g] * mul), (bf16)(a1[4 * g + 1] * mul), (bf16)(a1[4 * g + 2] * mul),
+                   (bf16)(a1[4 * g + 3] * mul)};
+      *(bf16x4*)(row + d) = v0;
+      *(bf16x4*)(row + 32 + d) = v1;
+    }
+  }
+}
+
 // LDS-DMA of a 64-row x 64-column bf16 tile — rows r0 .. r0+63 of a row-major matrix with row
 // stride `ld` elements, row indices clamped to rmax — into the XOR-swizzled image `img` (swz
 // layout). Each of the 4 waves moves two 1-KB pieces with global_load_lds_dwordx4; the DMA writes a
@@ -197,7 +238,7 @@ __device__ __forceinline__ void dma_tile_swz(const bf16* g, int64_t ld, int r0, 
 template <int WPE, bool DMA>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int B, int T, int H,
-                    float scale_log2) {
+                    float scale_log2, int staged_epi) {  // staged_epi: store_acc_tile
   // one shared object per buffer, so the compiler can tell that the LDS-DMA into one buffer
   // does not alias the reads of the other (else it waits vmcnt(0) before every V^T read)
   __shared__ __attribute__((aligned(16))) bf16 sKV0[2][A_BK * AD];  // [K | V], swizzled (swz)
@@ -345,21 +386,10 @@ attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
     else
       step(kt, I0{}, std::true_type{});
   }
-  if (q < T) {
-    const float inv = 1.f / l;
-    bf16* orow = out + ((int64_t)b * T + q) * H * AD + hh * AD;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * h2;
-      bf16x4 v0 = {(bf16)(o0[4 * g] * inv), (bf16)(o0[4 * g + 1] * inv), (bf16)(o0[4 * g + 2] * inv),
-                   (bf16)(o0[4 * g + 3] * inv)};
-      bf16x4 v1 = {(bf16)(o1[4 * g] * inv), (bf16)(o1[4 * g + 1] * inv), (bf16)(o1[4 * g + 2] * inv),
-                   (bf16)(o1[4 * g + 3] * inv)};
-      *(bf16x4*)(orow + d) = v0;
-      *(bf16x4*)(orow + 32 + d) = v1;
-    }
-    if (h2 == 0) lse[((int64_t)b * H + hh) * T + q] = m + __log2f(l);
-  }
+  const float inv = 1.f / l;
+  store_acc_tile(o0, o1, inv, out + ((int64_t)b * T + qw) * H * AD + hh * AD, (int64_t)H * AD, T - qw,
+                 &sKV0[0][0] + w * 32 * AD, staged_epi, lane);
+  if (q < T && h2 == 0) lse[((int64_t)b * H + hh) * T + q] = m + __log2f(l);
 #undef sK_
 #undef sV_
 }
@@ -373,7 +403,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
                                                                const bf16* __restrict__ out, const float* __restrict__ lse,
                                                                float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                                float* __restrict__ bpart,
-                                                               int B, int T, int H, float scale, float scale_log2) {
+                                                               int B, int T, int H, float scale, float scale_log2,
+                                                               int staged_epi) {
   // one shared object per buffer (see the forward): [K | V] tiles, swizzled (swz)
   __shared__ __attribute__((aligned(16))) bf16 sKV0[2][A_BK * AD];
   __shared__ __attribute__((aligned(16))) bf16 sKV1[2][A_BK * AD];
@@ -518,19 +549,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     else
       step(kt, I0{}, std::true_type{});
   }
-  if (q < T) {
-    bf16* row = dqkv + ((int64_t)b * T + q) * tok + hh * AD;  // slot 0 = dQ
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * h2;
-      bf16x4 v0 = {(bf16)(a0[4 * g] * scale), (bf16)(a0[4 * g + 1] * scale), (bf16)(a0[4 * g + 2] * scale),
-                   (bf16)(a0[4 * g + 3] * scale)};
-      bf16x4 v1 = {(bf16)(a1[4 * g] * scale), (bf16)(a1[4 * g + 1] * scale), (bf16)(a1[4 * g + 2] * scale),
-                   (bf16)(a1[4 * g + 3] * scale)};
-      *(bf16x4*)(row + d) = v0;
-      *(bf16x4*)(row + 32 + d) = v1;
-    }
-  }
+  store_acc_tile(a0, a1, scale, dqkv + ((int64_t)b * T + qw) * tok + hh * AD, tok, T - qw,  // slot 0 = dQ
+                 &sKV0[0][0] + w * 32 * AD, staged_epi, lane);
   if (bpart) {  // column sums of this block's dQ rows: one partial row of the QKV bias gradient
     float v[32];
 #pragma unroll
@@ -539,7 +559,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       v[16 + r] = q < T ? a1[r] * scale : 0.f;
     }
     const float cs = half_colsum32(v, col);
-    float* red = (float*)&sKV0[0][0];  // the K/V tiles are dead after the last barrier of the loop
+    float* red = (float*)&sKV1[0][0];  // the K/V tiles are dead after the loop (sKV0 holds the dQ images)
     red[w * AD + acc_pair_col(col, h2)] = cs;
     __syncthreads();
     if (tid < AD)
@@ -562,7 +582,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
                                                                  const float* __restrict__ lse,
                                                                  const float* __restrict__ delta,
                                                                  bf16* __restrict__ dqkv, float* __restrict__ bpart,
-                                                                 int B, int T, int H, float scale, float scale_log2) {
+                                                                 int B, int T, int H, float scale, float scale_log2,
+                                                                 int staged_epi) {
   // one shared object per buffer (see the forward): [Q | dO] tiles, swizzled (swz)
   __shared__ __attribute__((aligned(16))) bf16 sQD0[2][B_BQ * AD];
   __shared__ __attribute__((aligned(16))) bf16 sQD1[2][B_BQ * AD];
@@ -704,24 +725,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
     step(qt + 1, I1{}, std::false_type{});
   }
   if (qt < nqt) step(qt, I0{}, std::false_type{});
-  if (key < T) {
-    bf16* rowk = dqkv + ((int64_t)b * T + key) * tok + H * AD + hh * AD;      // slot 1 = dK
-    bf16* rowv = dqkv + ((int64_t)b * T + key) * tok + 2 * H * AD + hh * AD;  // slot 2 = dV
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * h2;
-      bf16x4 k0v = {(bf16)(dk0[4 * g] * scale), (bf16)(dk0[4 * g + 1] * scale), (bf16)(dk0[4 * g + 2] * scale),
-                    (bf16)(dk0[4 * g + 3] * scale)};
-      bf16x4 k1v = {(bf16)(dk1[4 * g] * scale), (bf16)(dk1[4 * g + 1] * scale), (bf16)(dk1[4 * g + 2] * scale),
-                    (bf16)(dk1[4 * g + 3] * scale)};
-      bf16x4 v0 = {(bf16)dv0[4 * g], (bf16)dv0[4 * g + 1], (bf16)dv0[4 * g + 2], (bf16)dv0[4 * g + 3]};
-      bf16x4 v1 = {(bf16)dv1[4 * g], (bf16)dv1[4 * g + 1], (bf16)dv1[4 * g + 2], (bf16)dv1[4 * g + 3]};
-      *(bf16x4*)(rowk + d) = k0v;
-      *(bf16x4*)(rowk + 32 + d) = k1v;
-      *(bf16x4*)(rowv + d) = v0;
-      *(bf16x4*)(rowv + 32 + d) = v1;
-    }
-  }
   if (bpart) {  // column sums of this block's dK and dV rows: slots 1 and 2 of a QKV-bias partial row
     float* red = (float*)&sQD0[0][0];  // the Q/dO tiles are dead after the last barrier of the loop
     float v[32];
@@ -744,7 +747,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       bpart[((int64_t)b * nkb + kbi) * 3 * H * AD + (1 + sl) * H * AD + hh * AD + d] =
           (rr[d] + rr[AD + d]) + (rr[2 * AD + d] + rr[3 * AD + d]);
     }
+    __syncthreads();  // red is overwritten by the dK images below
   }
+  bf16* dk_row0 = dqkv + ((int64_t)b * T + kw) * tok + H * AD + hh * AD;  // slot 1 = dK, slot 2 = dV
+  store_acc_tile(dk0, dk1, scale, dk_row0, tok, T - kw, &sQD0[0][0] + w * 32 * AD, staged_epi, lane);
+  store_acc_tile(dv0, dv1, 1.f, dk_row0 + H * AD, tok, T - kw, &sQD1[0][0] + w * 32 * AD, staged_epi, lane);
 #undef sQ_
 #undef sD_
 }
@@ -760,11 +767,16 @@ using namespace vcx;
 // dQ with LDS-DMA staging (264 vs 275 us), dK/dV with register staging (381 vs 383 us: the DMA
 // build of that kernel hits the 256-VGPR cap and spills).
 static int g_fwd_wpe = 3, g_fwd_dma = 1, g_bwd_dma = 1;  // g_bwd_dma bit 0: dQ kernel, bit 1: dK/dV kernel
+// output tiles (O, dQ, dK, dV): 1 = staged through LDS, whole-row 16-B stores; 0 = per-lane half-row
+// stores. Bench shape, same box (profiles/r1_attn_variants.log): backward 0.589 vs 0.614 ms, forward
+// within noise (0.201-0.212 vs 0.206-0.208)
+static int g_stage_epi = 1;
 
-void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma) {
+void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma, int stage_epi) {
   if (fwd_wpe == 2 || fwd_wpe == 3) g_fwd_wpe = fwd_wpe;
   if (fwd_dma == 0 || fwd_dma == 1) g_fwd_dma = fwd_dma;
   if (bwd_dma >= 0 && bwd_dma <= 3) g_bwd_dma = bwd_dma;
+  if (stage_epi == 0 || stage_epi == 1) g_stage_epi = stage_epi;
 }
 
 int vcx_attn_bias_partials(int B, int T) { return B * ((T + 127) / 128); }
@@ -777,17 +789,19 @@ void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const 
   if (g_bwd_dma & 1)
     hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, true>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale,
-                       scale * LOG2E);
+                       scale * LOG2E, g_stage_epi);
   else
     hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, false>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale,
-                       scale * LOG2E);
+                       scale * LOG2E, g_stage_epi);
   if (g_bwd_dma & 2)
     hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, true>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
-                       (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E);
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E,
+                       g_stage_epi);
   else
     hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, false>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
-                       (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E);
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E,
+                       g_stage_epi);
 }
 
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s) {
@@ -795,7 +809,7 @@ void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int 
   const dim3 g(B * H * nqt);
 #define VCX_FWD(W, D)                                                                                      \
   hipLaunchKernelGGL((attn_fwd_d64_kernel<W, D>), g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H, \
-                     scale * LOG2E)
+                     scale * LOG2E, g_stage_epi)
   if (g_fwd_dma) {
     if (g_fwd_wpe == 2) VCX_FWD(2, true); else VCX_FWD(3, true);
   } else {

@@ -49,7 +49,7 @@ void vcx_xent_bwd(const void* logits, const int64_t* tgt, const float* lse, cons
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s);
 // variants: forward 2 or 3 waves per SIMD (default 3); K/V (Q/dO) tile staging through registers
 // (0) or LDS-DMA (1) for the forward (default 1) and the backward (bit 0: dQ, bit 1: dK/dV; default 1)
-void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma);
+void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma, int stage_epi);  // stage_epi: LDS-staged output stores (-1 = unchanged)
 // bias_part (nullable): [B * ceil(T/128), 3 * H * 64] fp32, one row of column sums of dqkv per
 // 128-row block (the gradient of a bias added to qkv: reduce with vcx_colsum_f32)
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,

@@ -33,21 +33,21 @@ def tm(fn, it=10):
     return sorted(ts)[len(ts) // 2]
 
 
-C.attn_set_variant(2, 0, 0)
+C.attn_set_variant(2, 0, 0, 0)  # reference outputs: the simplest variant
 o_ref, lse_ref = C.attn_fwd(qkv, scale)
 g_ref = C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)
 torch.cuda.synchronize()
 res = {}
 for rnd in range(3):
-    for fv in ((2, 0), (3, 0), (2, 1), (3, 1)):
-        C.attn_set_variant(*fv, 1)
+    for fv in ((2, 0, 1), (3, 0, 1), (2, 1, 1), (3, 1, 0), (3, 1, 1)):  # (waves/SIMD, DMA, LDS-staged output stores)
+        C.attn_set_variant(fv[0], fv[1], 1, fv[2])
         o, l = C.attn_fwd(qkv, scale)
         if rnd == 0:
             err = (o.float() - o_ref.float()).abs().max().item()
             print(f"fwd variant {fv}: max|o - o_ref| = {err:.3e}", flush=True)
         res.setdefault(("fwd", fv), []).append(tm(lambda: C.attn_fwd(qkv, scale)))
-    for bd in (0, 1):
-        C.attn_set_variant(3, 1, bd)
+    for bd in ((0, 1), (1, 0), (1, 1)):  # (backward LDS-DMA mask, LDS-staged output stores)
+        C.attn_set_variant(3, 1, *bd)
         if rnd == 0:
             g = C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)
             print(f"bwd dma {bd}: max|dqkv - ref| = {(g.float() - g_ref.float()).abs().max().item():.3e}", flush=True)

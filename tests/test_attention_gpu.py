@@ -73,7 +73,7 @@ def test_attention_matches_sdpa_at_bench_shape(gpu):
     assert rel < 1e-2, float(rel)
 
 
-@pytest.mark.parametrize("variant", [(2, 0, 0), (3, 0, 3), (2, 1, 2), (3, 1, 1)])
+@pytest.mark.parametrize("variant", [(2, 0, 0, 0), (3, 0, 3, 1), (2, 1, 2, 1), (3, 1, 1, 0), (3, 1, 1, 1)])
 def test_attention_deterministic(gpu, variant):
     """Same inputs, same kernel -> bitwise identical outputs (a race on the double-buffered LDS
     tiles would show up here as run-to-run differences)."""
@@ -94,4 +94,4 @@ def test_attention_deterministic(gpu, variant):
         for g in gs[1:]:
             assert torch.equal(g, gs[0])
     finally:
-        C.attn_set_variant(3, 1, 1)
+        C.attn_set_variant(3, 1, 1, 1)
