@@ -310,14 +310,22 @@ __global__ void __launch_bounds__(TPB) bias_gelu_bwd_kernel(const bf16* __restri
   }
   const int G = gridDim.y;
   int r = blockIdx.y;
-  for (; r + 3 * G < R; r += 4 * G) {
-    bf16x8 v[4], g[4];
+  // 4 rows per step, software-pipelined: the next step's 8 loads are issued before this step's
+  // math and stores, so each lane keeps 16 loads in flight across the step boundary
+  bf16x8 v[4], g[4];
+  auto load4 = [&](int r0, bf16x8(&vv)[4], bf16x8(&gg)[4]) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int64_t off = (int64_t)(r + u * G) * F + c8 * 8;
-      v[u] = *(const bf16x8*)(x + off);
-      g[u] = *(const bf16x8*)(dy + off);
+      const int64_t off = (int64_t)(r0 + u * G) * F + c8 * 8;
+      vv[u] = *(const bf16x8*)(x + off);
+      gg[u] = *(const bf16x8*)(dy + off);
     }
+  };
+  if (r + 3 * G < R) load4(r, v, g);
+  for (; r + 3 * G < R; r += 4 * G) {
+    bf16x8 nv[4], ng[4];
+    const bool more = r + 7 * G < R;
+    if (more) load4(r + 4 * G, nv, ng);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       bf16x8 o;
@@ -329,15 +337,22 @@ __global__ void __launch_bounds__(TPB) bias_gelu_bwd_kernel(const bf16* __restri
       }
       *(bf16x8*)(dx + (int64_t)(r + u * G) * F + c8 * 8) = o;
     }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = nv[u];
+        g[u] = ng[u];
+      }
+    }
   }
   for (; r < R; r += G) {
     const int64_t off = (int64_t)r * F + c8 * 8;
-    bf16x8 v = *(const bf16x8*)(x + off);
-    bf16x8 g = *(const bf16x8*)(dy + off);
+    bf16x8 v1 = *(const bf16x8*)(x + off);
+    bf16x8 g1 = *(const bf16x8*)(dy + off);
     bf16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float d = (float)g[j] * gelu_grad_f((float)v[j] + bf[j]);
+      const float d = (float)g1[j] * gelu_grad_f((float)v1[j] + bf[j]);
       o[j] = (bf16)d;
       acc[j] += d;
     }

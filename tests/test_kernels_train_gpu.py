@@ -188,19 +188,21 @@ def test_add_layernorm_branch_bias(gpu):
     assert torch.allclose(b.grad.float(), b32.grad, atol=5e-2, rtol=3e-2)
 
 
-def test_bias_gelu(gpu):
+@pytest.mark.parametrize("R", [1000, 9001])
+def test_bias_gelu(gpu, R):
+    """R = 9001: each row group runs the pipelined 4-row steps and the row tail."""
     torch.manual_seed(8)
-    x = _bf(torch.randn(1000, 3072, device=gpu) * 2).requires_grad_()
+    x = _bf(torch.randn(R, 3072, device=gpu) * 2).requires_grad_()
     b = _bf(torch.randn(3072, device=gpu)).requires_grad_()
     y = ops.bias_gelu(x, b)
     x32, b32 = x.detach().float().requires_grad_(), b.detach().float().requires_grad_()
     yr = F.gelu(x32 + b32, approximate="tanh")
     assert torch.allclose(y.float(), yr, atol=3e-2, rtol=2e-2)
-    dy = torch.randn_like(yr)
+    dy = _bf(torch.randn_like(yr)).float()
     (y.float() * dy).sum().backward()
     (yr * dy).sum().backward()
     assert torch.allclose(x.grad.float(), x32.grad, atol=5e-2, rtol=3e-2)
-    assert torch.allclose(b.grad.float(), b32.grad, atol=1.0, rtol=3e-2)
+    assert torch.allclose(b.grad.float(), b32.grad, atol=1.0 * max(1.0, (R / 1000) ** 0.5), rtol=3e-2)
 
 
 def test_embedding_fwd_bwd(gpu):
