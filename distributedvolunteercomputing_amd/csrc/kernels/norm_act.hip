@@ -273,10 +273,18 @@ __global__ void __launch_bounds__(TPB) bias_gelu_fwd_kernel(const bf16* __restri
   for (int j = 0; j < 8; ++j) bf[j] = (float)bv[j];
   const int G = gridDim.y;
   int r = blockIdx.y;
-  for (; r + 3 * G < R; r += 4 * G) {
-    bf16x8 v[4];
+  // 4 rows per step, software-pipelined like the backward: the next step's loads are in flight
+  // during this step's math and stores
+  bf16x8 v[4];
+  auto load4 = [&](int r0, bf16x8(&vv)[4]) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = *(const bf16x8*)(x + (int64_t)(r + u * G) * F + c8 * 8);
+    for (int u = 0; u < 4; ++u) vv[u] = *(const bf16x8*)(x + (int64_t)(r0 + u * G) * F + c8 * 8);
+  };
+  if (r + 3 * G < R) load4(r, v);
+  for (; r + 3 * G < R; r += 4 * G) {
+    bf16x8 nv[4];
+    const bool more = r + 7 * G < R;
+    if (more) load4(r + 4 * G, nv);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       bf16x8 o;
@@ -284,13 +292,17 @@ __global__ void __launch_bounds__(TPB) bias_gelu_fwd_kernel(const bf16* __restri
       for (int j = 0; j < 8; ++j) o[j] = (bf16)gelu_f((float)v[u][j] + bf[j]);
       *(bf16x8*)(y + (int64_t)(r + u * G) * F + c8 * 8) = o;
     }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = nv[u];
+    }
   }
   for (; r < R; r += G) {
     const int64_t off = (int64_t)r * F + c8 * 8;
-    bf16x8 v = *(const bf16x8*)(x + off);
+    bf16x8 v1 = *(const bf16x8*)(x + off);
     bf16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (bf16)gelu_f((float)v[j] + bf[j]);
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)gelu_f((float)v1[j] + bf[j]);
     *(bf16x8*)(y + off) = o;
   }
 }
