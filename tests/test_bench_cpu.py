@@ -1,0 +1,52 @@
+"""bench.py under the driver's contract, on CPU/gloo with a tiny model: the single-process run and
+the torchrun launch with world_size 2 (the multi-GPU command line, RCCL replaced by gloo). Checks
+the one JSON line rank 0 prints: whole-job value, N, steps/warmup echo, weak scaling."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--steps", "4", "--warmup", "2", "--model", "gpt2-tiny", "--batch", "2", "--seq", "32", "--H", "2"]
+
+
+def _env():
+    return dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+
+
+def _json_line(stdout: str) -> dict:
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def _check(rec: dict, n: int):
+    assert rec["n_gpus"] == n and rec["steps"] == 4 and rec["warmup"] == 2
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0 and rec["higher_is_better"] is True
+    assert rec["scaling"] == "weak" and rec["config"]["global_batch"] == 2 * n
+    # value is the whole-job rate: N x per-peer batch x steps / max-over-ranks time
+    assert abs(rec["value"] - n * 2 * 4 / (rec["ms_per_step"] * 4 / 1e3)) / rec["value"] < 1e-2
+
+
+def test_bench_single_process():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", *ARGS], cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check(_json_line(r.stdout), 1)
+
+
+@pytest.mark.slow
+def test_bench_torchrun_two_ranks():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", *ARGS]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    _check(rec, 2)
+    assert "dp2" in rec["config"]["parallelism"]
