@@ -458,6 +458,44 @@ std::vector<at::Tensor> attn_bwd_bias(at::Tensor qkv, at::Tensor out, at::Tensor
   return {dqkv, db};
 }
 
+// head-major GQA attention (Llama family): q [B, Hq, T, D], k / v [B, Hkv, T, D], D in {64, 128}
+static void check_hm(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
+  CHECK_IN(q, kBF);
+  CHECK_IN(k, kBF);
+  CHECK_IN(v, kBF);
+  TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && k.sizes() == v.sizes(), "attn_hm: q [B,Hq,T,D], k/v [B,Hkv,T,D]");
+  TORCH_CHECK(q.size(0) == k.size(0) && q.size(2) == k.size(2) && q.size(3) == k.size(3));
+  TORCH_CHECK(q.size(3) == 64 || q.size(3) == 128, "attn_hm: head dim must be 64 or 128");
+  TORCH_CHECK(q.size(1) % k.size(1) == 0, "attn_hm: Hq must be a multiple of Hkv");
+}
+
+std::vector<at::Tensor> attn_hm_fwd(at::Tensor q, at::Tensor k, at::Tensor v, double scale) {
+  check_hm(q, k, v);
+  const int64_t B = q.size(0), Hq = q.size(1), T = q.size(2), D = q.size(3), Hkv = k.size(1);
+  auto out = at::empty({B, T, Hq, D}, q.options());
+  auto lse = at::empty({B, Hq, T}, q.options().dtype(kF));
+  vcx_attn_hm_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T,
+                  (int)Hq, (int)Hkv, (int)D, (float)scale, cur_stream());
+  return {out, lse};
+}
+
+std::vector<at::Tensor> attn_hm_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor out, at::Tensor dout,
+                                    at::Tensor lse, double scale) {
+  check_hm(q, k, v);
+  CHECK_IN(out, kBF);
+  CHECK_IN(dout, kBF);
+  CHECK_IN(lse, kF);
+  const int64_t B = q.size(0), Hq = q.size(1), T = q.size(2), D = q.size(3), Hkv = k.size(1);
+  TORCH_CHECK(out.sizes() == at::IntArrayRef({B, T, Hq, D}) && dout.sizes() == out.sizes());
+  TORCH_CHECK(lse.numel() == B * Hq * T);
+  auto dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  auto delta = at::empty({B, Hq, T}, lse.options());
+  vcx_attn_hm_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                  delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)T, (int)Hq,
+                  (int)Hkv, (int)D, (float)scale, cur_stream());
+  return {dq, dk, dv};
+}
+
 }  // namespace
 
 void vcx_register_vision(pybind11::module& m);
@@ -500,6 +538,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_qkv_fwd", &rope_qkv_fwd);
   m.def("rope_qkv_bwd", &rope_qkv_bwd);
   m.def("attn_bwd", &attn_bwd);
+  m.def("attn_hm_fwd", &attn_hm_fwd);
+  m.def("attn_hm_bwd", &attn_hm_bwd);
   m.def("attn_bwd_bias", &attn_bwd_bias, pybind11::arg("qkv"), pybind11::arg("out"), pybind11::arg("dout"),
         pybind11::arg("lse"), pybind11::arg("scale"), pybind11::arg("db_out") = pybind11::none());
   vcx_register_vision(m);

@@ -55,6 +55,14 @@ void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma, int stage_epi);
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
                       float* bias_part, int B, int T, int H, float scale, hipStream_t s);
 int vcx_attn_bias_partials(int B, int T);
+// attention_hm.hip (causal flash attention, head-major GQA layout, head dim 64 or 128):
+// q [B, Hq, T, D], k / v [B, Hkv, T, D], out / dout [B, T, Hq, D], lse / delta [B, Hq, T] fp32,
+// dq [B, Hq, T, D], dk / dv [B, Hkv, T, D]
+void vcx_attn_hm_fwd(const void* q, const void* k, const void* v, void* out, float* lse, int B, int T, int Hq, int Hkv,
+                     int D, float scale, hipStream_t s);
+void vcx_attn_hm_bwd(const void* q, const void* k, const void* v, const void* out, const void* dout, const float* lse,
+                     float* delta, void* dq, void* dk, void* dv, int B, int T, int Hq, int Hkv, int D, float scale,
+                     hipStream_t s);
 
 // rope.hip: rotary embedding fused with the QKV split into head-major q/k/v (and its inverse)
 void vcx_rope_qkv(void* qkv, void* q, void* k, void* v, const float* cosv, const float* sinv, int B, int T, int Hq,

@@ -3,7 +3,8 @@ volunteer peers (288 GB HBM per GPU sizing), PowerSGD rank-4 compression").
 
 RMSNorm (with the residual add fused), SwiGLU and the rotary embedding (fused with the QKV split
 into head-major q/k/v, ops/rope.py) are HIP kernels; GEMMs are library GEMMs; attention (head dim
-128, grouped-query) is torch SDPA with enable_gqa.
+128, grouped-query) is the head-major GQA flash attention of attention_hm.hip (ops.gqa_attention),
+which writes its output token-major for the o-projection.
 
 Memory sizing for 8B on one MI355X peer (288 GB HBM): bf16 params 16 GB + bf16 grads 16 GB,
 plus fp32 master/m/v = 96 GB for the whole model -> 12 GB per peer when sharded over 8
@@ -46,21 +47,6 @@ class LlamaConfig:
 
 from ..ops.rope import apply_rope, rope_tables  # noqa: E402,F401  (re-exported for callers)
 
-_GQA_SDPA = [True]  # SDPA's enable_gqa (no repeat_interleave copies); falls back if unsupported
-
-
-def _sdpa_gqa(q, k, v, rep):
-    if rep > 1 and _GQA_SDPA[0]:
-        try:
-            return F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
-        except (RuntimeError, TypeError):
-            _GQA_SDPA[0] = False
-    if rep > 1:
-        k = k.repeat_interleave(rep, dim=1)
-        v = v.repeat_interleave(rep, dim=1)
-    return F.scaled_dot_product_attention(q, k, v, is_causal=True)
-
-
 class LlamaBlock(nn.Module):
     def __init__(self, c: LlamaConfig):
         super().__init__()
@@ -78,8 +64,8 @@ class LlamaBlock(nn.Module):
         B, T, D = h.shape
         # fused QKV projection -> one HIP kernel: split, rotary embedding on q/k, head-major q/k/v
         q, k, v = ops.rope_qkv(ops.linear(h, self.wqkv), cos, sin, c.n_heads, c.n_kv_heads)
-        y = _sdpa_gqa(q, k, v, c.n_heads // c.n_kv_heads)
-        return ops.linear(y.transpose(1, 2).reshape(B, T, D), self.wo)
+        y = ops.gqa_attention(q, k, v)  # HIP flash attention (GQA, head-major in, token-major out)
+        return ops.linear(y.reshape(B, T, D), self.wo)
 
     def mlp(self, h):
         return ops.linear(ops.swiglu(ops.linear(h, self.w13)), self.w2)

@@ -2,7 +2,7 @@
 on CPU the same call runs the plain-PyTorch reference (used by tests and CPU volunteers)."""
 from ._lib import available as native_available, native  # noqa: F401
 from .activations import bias_gelu, gelu, swiglu  # noqa: F401
-from .attention import causal_attention, fused_bias_grad_ok  # noqa: F401
+from .attention import causal_attention, fused_bias_grad_ok, gqa_attention  # noqa: F401
 from .embedding import embed  # noqa: F401
 from .linear import linear, native_linear_ok, wgrad  # noqa: F401
 from .loss import cross_entropy  # noqa: F401

@@ -62,3 +62,46 @@ def causal_attention(qkv: torch.Tensor, scale: float | None = None, bias: torch.
         return _Attn.apply(qkv.contiguous(), scale, bias)
     assert bias is None, "bias gradient fusion needs the native hd64 bf16 attention path"
     return _ref(qkv, scale)
+
+
+# ------------------------------------------------------------------ head-major GQA (Llama family)
+class _AttnHM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        out, lse = native().attn_hm_fwd(q, k, v, scale)
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.scale = scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse = ctx.saved_tensors
+        dq, dk, dv = native().attn_hm_bwd(q, k, v, out, dout.contiguous(), lse, ctx.scale)
+        return dq, dk, dv, None
+
+
+_GQA_SDPA = [True]  # SDPA's enable_gqa (no repeat_interleave copies); falls back if unsupported
+
+
+def _ref_gqa(q, k, v, scale):
+    rep = q.shape[1] // k.shape[1]
+    if rep > 1 and _GQA_SDPA[0]:
+        try:
+            return F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale, enable_gqa=True).transpose(1, 2)
+        except (RuntimeError, TypeError):
+            _GQA_SDPA[0] = False
+    if rep > 1:
+        k = k.repeat_interleave(rep, dim=1)
+        v = v.repeat_interleave(rep, dim=1)
+    return F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale).transpose(1, 2)
+
+
+def gqa_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None) -> torch.Tensor:
+    """Causal grouped-query attention, q [B, Hq, T, D], k / v [B, Hkv, T, D] (head-major, as
+    ``rope_qkv`` returns them) -> out [B, T, Hq, D] (token-major: the output projection's input).
+    GPU bf16 with D in (64, 128): the HIP kernels of attention_hm.hip; otherwise torch SDPA."""
+    D = q.shape[-1]
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if use_native(q) and q.dtype == torch.bfloat16 and D in (64, 128) and q.shape[1] % k.shape[1] == 0:
+        return _AttnHM.apply(q.contiguous(), k.contiguous(), v.contiguous(), scale)
+    return _ref_gqa(q, k, v, scale)

@@ -95,3 +95,53 @@ def test_attention_deterministic(gpu, variant):
             assert torch.equal(g, gs[0])
     finally:
         C.attn_set_variant(3, 1, 1, 1)
+
+
+def _ref_gqa32(q, k, v, scale):
+    rep = q.shape[1] // k.shape[1]
+    k = k.repeat_interleave(rep, dim=1)
+    v = v.repeat_interleave(rep, dim=1)
+    T = q.shape[2]
+    s = (q @ k.transpose(-1, -2)) * scale
+    mask = torch.triu(torch.ones(T, T, dtype=torch.bool, device=q.device), 1)
+    p = torch.softmax(s.masked_fill(mask, float("-inf")), -1)
+    return (p @ v).transpose(1, 2)  # [B, T, Hq, D]
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,T,D", [(2, 4, 2, 200, 128), (1, 8, 2, 1024, 128), (2, 4, 4, 77, 64),
+                                          (1, 32, 8, 256, 128), (1, 6, 1, 130, 64)])
+def test_gqa_attention_fwd_bwd(gpu, B, Hq, Hkv, T, D):
+    """Head-major GQA flash attention (Llama layout, attention_hm.hip) vs an fp32 reference:
+    output [B, T, Hq, D] and the gradients of q, k, v (k/v summed over each group's query heads)."""
+    torch.manual_seed(3)
+    q = torch.randn(B, Hq, T, D, device=gpu).to(torch.bfloat16).requires_grad_()
+    k = torch.randn(B, Hkv, T, D, device=gpu).to(torch.bfloat16).requires_grad_()
+    v = torch.randn(B, Hkv, T, D, device=gpu).to(torch.bfloat16).requires_grad_()
+    scale = 1 / math.sqrt(D)
+    out = ops.gqa_attention(q, k, v)
+    assert out.shape == (B, T, Hq, D)
+    q32, k32, v32 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    ref = _ref_gqa32(q32, k32, v32, scale)
+    err = (out.float() - ref).abs().max().item()
+    assert err < 2e-2, err
+    do = torch.randn_like(ref).to(torch.bfloat16).float()
+    (out.float() * do).sum().backward()
+    (ref * do).sum().backward()
+    for nm, a, r in (("q", q.grad, q32.grad), ("k", k.grad, k32.grad), ("v", v.grad, v32.grad)):
+        rel = (a.float() - r).norm() / (r.norm() + 1e-6)
+        assert rel < 2e-2, (nm, float(rel))
+
+
+def test_gqa_attention_deterministic(gpu):
+    C = ops.native()
+    torch.manual_seed(6)
+    q = torch.randn(2, 8, 512, 128, device=gpu).to(torch.bfloat16)
+    k = torch.randn(2, 2, 512, 128, device=gpu).to(torch.bfloat16)
+    v = torch.randn(2, 2, 512, 128, device=gpu).to(torch.bfloat16)
+    outs = [C.attn_hm_fwd(q, k, v, 128 ** -0.5) for _ in range(3)]
+    for o, l in outs[1:]:
+        assert torch.equal(o, outs[0][0]) and torch.equal(l, outs[0][1])
+    do = torch.randn_like(outs[0][0])
+    gs = [C.attn_hm_bwd(q, k, v, outs[0][0], do, outs[0][1], 128 ** -0.5) for _ in range(3)]
+    for g in gs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(g, gs[0]))
