@@ -540,6 +540,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_hm_fwd", &attn_hm_fwd);
   m.def("attn_hm_bwd", &attn_hm_bwd);
+  m.def("attn_hm_set_variant", &vcx_attn_hm_set_variant);
   m.def("attn_bwd_bias", &attn_bwd_bias, pybind11::arg("qkv"), pybind11::arg("out"), pybind11::arg("dout"),
         pybind11::arg("lse"), pybind11::arg("scale"), pybind11::arg("db_out") = pybind11::none());
   vcx_register_vision(m);

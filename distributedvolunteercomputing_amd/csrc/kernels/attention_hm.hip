@@ -281,8 +281,12 @@ attn_hm_dq_kernel(const bf16* __restrict__ qg, const bf16* __restrict__ kg, cons
 // stay in registers while it streams the Q / dO tiles of every query head of the group in turn
 // (one flattened tile sequence, so the double-buffered prefetch runs across head boundaries).
 // MODE 0: dK and dV; 1: dK only; 2: dV only.
+// waves per SIMD of the key-parallel kernel: D = 64 both gradients at 2; D = 128 dK (and dK + dV)
+// needs the 512-register budget of 1 wave per SIMD, dV alone fits 3
+constexpr int hm_dkv_wpe(int D, int MODE) { return D == 64 ? 2 : (MODE == 2 ? 3 : 1); }
+
 template <int D, int MODE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 128 && MODE == 1 ? 1 : 2, D == 128 && MODE == 1 ? 1 : 2)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(hm_dkv_wpe(D, MODE), hm_dkv_wpe(D, MODE))))
 attn_hm_dkv_kernel(const bf16* __restrict__ qg, const bf16* __restrict__ kg, const bf16* __restrict__ vg,
                    const bf16* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
                    bf16* __restrict__ dk, bf16* __restrict__ dv, int T, int Hq, int Hkv, float scale,
@@ -451,6 +455,11 @@ void vcx_attn_hm_fwd(const void* q, const void* k, const void* v, void* out, flo
                        (bf16*)out, lse, T, Hq, Hkv, scale * LOG2E);
 }
 
+static int g_hm_dkv_split = 0;  // D = 128: dK and dV as two launches (1) or one 1-wave/SIMD launch (0)
+void vcx_attn_hm_set_variant(int dkv_split) {
+  if (dkv_split == 0 || dkv_split == 1) g_hm_dkv_split = dkv_split;
+}
+
 void vcx_attn_hm_bwd(const void* q, const void* k, const void* v, const void* out, const void* dout, const float* lse,
                      float* delta, void* dq, void* dk, void* dv, int B, int T, int Hq, int Hkv, int D, float scale,
                      hipStream_t s) {
@@ -460,10 +469,15 @@ void vcx_attn_hm_bwd(const void* q, const void* k, const void* v, const void* ou
   if (D == 128) {
     hipLaunchKernelGGL(attn_hm_dq_kernel<128>, gq, dim3(256), 0, s, VCX_HM_ARGS_Q, (const bf16*)out, (const bf16*)dout,
                        lse, delta, (bf16*)dq, T, Hq, Hkv, scale, sl);
-    hipLaunchKernelGGL((attn_hm_dkv_kernel<128, 1>), gk, dim3(256), 0, s, VCX_HM_ARGS_Q, (const bf16*)dout, lse, delta,
-                       (bf16*)dk, (bf16*)dv, T, Hq, Hkv, scale, sl);
-    hipLaunchKernelGGL((attn_hm_dkv_kernel<128, 2>), gk, dim3(256), 0, s, VCX_HM_ARGS_Q, (const bf16*)dout, lse, delta,
-                       (bf16*)dk, (bf16*)dv, T, Hq, Hkv, scale, sl);
+    if (g_hm_dkv_split) {
+      hipLaunchKernelGGL((attn_hm_dkv_kernel<128, 1>), gk, dim3(256), 0, s, VCX_HM_ARGS_Q, (const bf16*)dout, lse,
+                         delta, (bf16*)dk, (bf16*)dv, T, Hq, Hkv, scale, sl);
+      hipLaunchKernelGGL((attn_hm_dkv_kernel<128, 2>), gk, dim3(256), 0, s, VCX_HM_ARGS_Q, (const bf16*)dout, lse,
+                         delta, (bf16*)dk, (bf16*)dv, T, Hq, Hkv, scale, sl);
+    } else {
+      hipLaunchKernelGGL((attn_hm_dkv_kernel<128, 0>), gk, dim3(256), 0, s, VCX_HM_ARGS_Q, (const bf16*)dout, lse,
+                         delta, (bf16*)dk, (bf16*)dv, T, Hq, Hkv, scale, sl);
+    }
   } else {
     hipLaunchKernelGGL(attn_hm_dq_kernel<64>, gq, dim3(256), 0, s, VCX_HM_ARGS_Q, (const bf16*)out, (const bf16*)dout,
                        lse, delta, (bf16*)dq, T, Hq, Hkv, scale, sl);

@@ -60,6 +60,7 @@ int vcx_attn_bias_partials(int B, int T);
 // dq [B, Hq, T, D], dk / dv [B, Hkv, T, D]
 void vcx_attn_hm_fwd(const void* q, const void* k, const void* v, void* out, float* lse, int B, int T, int Hq, int Hkv,
                      int D, float scale, hipStream_t s);
+void vcx_attn_hm_set_variant(int dkv_split);  // D = 128: 1 = dK and dV in two launches, 0 = one
 void vcx_attn_hm_bwd(const void* q, const void* k, const void* v, const void* out, const void* dout, const float* lse,
                      float* delta, void* dq, void* dk, void* dv, int B, int T, int Hq, int Hkv, int D, float scale,
                      hipStream_t s);

@@ -38,8 +38,12 @@ def sdpa():
     return F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True).transpose(1, 2)
 
 
-for name, fn in (("hip", lambda: ops.gqa_attention(q, k, v)), ("sdpa", sdpa)):
+C = ops.native()
+for name, fn, var in (("hip/split", lambda: ops.gqa_attention(q, k, v), 1),
+                      ("hip/fused", lambda: ops.gqa_attention(q, k, v), 0), ("sdpa", sdpa, None)):
+    if var is not None:
+        C.attn_hm_set_variant(var)
     f = tm(lambda: fn())
     fb = tm(lambda: torch.autograd.grad(fn(), (q, k, v), do))
-    print(f"{name:5s} fwd {f:7.3f} ms ({fl / f / 1e9:6.1f} TF)  fwd+bwd {fb:7.3f} ms ({3.5 * fl / fb / 1e9:6.1f} TF)",
+    print(f"{name:9s} fwd {f:7.3f} ms ({fl / f / 1e9:6.1f} TF)  fwd+bwd {fb:7.3f} ms ({3.5 * fl / fb / 1e9:6.1f} TF)",
           flush=True)
