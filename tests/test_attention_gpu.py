@@ -132,6 +132,26 @@ def test_gqa_attention_fwd_bwd(gpu, B, Hq, Hkv, T, D):
         assert rel < 2e-2, (nm, float(rel))
 
 
+def test_gqa_attention_dkv_split_variant(gpu):
+    """D = 128 backward with dK and dV as two launches (the non-default variant) matches the
+    default single-launch kernel."""
+    C = ops.native()
+    torch.manual_seed(8)
+    q = torch.randn(1, 8, 300, 128, device=gpu).to(torch.bfloat16)
+    k = torch.randn(1, 2, 300, 128, device=gpu).to(torch.bfloat16)
+    v = torch.randn(1, 2, 300, 128, device=gpu).to(torch.bfloat16)
+    o, lse = C.attn_hm_fwd(q, k, v, 128 ** -0.5)
+    do = torch.randn_like(o)
+    g_fused = C.attn_hm_bwd(q, k, v, o, do, lse, 128 ** -0.5)
+    C.attn_hm_set_variant(1)
+    try:
+        g_split = C.attn_hm_bwd(q, k, v, o, do, lse, 128 ** -0.5)
+    finally:
+        C.attn_hm_set_variant(0)
+    for a, b in zip(g_fused, g_split):
+        assert (a.float() - b.float()).abs().max().item() < 1e-2
+
+
 def test_gqa_attention_deterministic(gpu):
     C = ops.native()
     torch.manual_seed(6)
