@@ -54,13 +54,21 @@ void check_desc(const at::Tensor& d, int64_t nmat) {
   TORCH_CHECK(d.scalar_type() == at::kByte && d.numel() == nmat * vcx_psgd_desc_size(), "bad descriptor table");
 }
 
-void psgd_mq(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::Tensor Q, at::Tensor P, int64_t rank) {
+// M += G (error feedback, skipped when G is None) fused with P = M Q over every matrix
+void psgd_mq(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::Tensor Q, at::Tensor P, int64_t rank,
+             std::optional<at::Tensor> G) {
   check_desc(desc, nmat);
   CHK(M);
   CHK(Q);
   CHK(P);
-  vcx_psgd_mq(desc.data_ptr(), (int)nmat, (int)nblocks, M.data_ptr<float>(), Q.data_ptr<float>(), P.data_ptr<float>(),
-              (int)rank, cur_stream());
+  const void* g = nullptr;
+  if (G.has_value()) {
+    CHK((*G));
+    TORCH_CHECK(G->scalar_type() == at::kBFloat16 && G->numel() == M.numel(), "psgd_mq: G must be bf16 like M");
+    g = G->data_ptr();
+  }
+  vcx_psgd_mq(desc.data_ptr(), (int)nmat, (int)nblocks, M.data_ptr<float>(), g, Q.data_ptr<float>(),
+              P.data_ptr<float>(), (int)rank, cur_stream());
 }
 
 void psgd_mtp(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::Tensor P, at::Tensor Q, int64_t rank) {
@@ -103,10 +111,15 @@ void ef_accum(at::Tensor g, at::Tensor e) {
 void vcx_register_compress(pybind11::module& m) {
   m.def("topk_ef", &topk_ef);
   m.def("scatter_add", &scatter_add);
-  m.def("psgd_mq", &psgd_mq);
+  m.def("psgd_mq", &psgd_mq, pybind11::arg("desc"), pybind11::arg("nmat"), pybind11::arg("nblocks"),
+        pybind11::arg("M"), pybind11::arg("Q"), pybind11::arg("P"), pybind11::arg("rank"),
+        pybind11::arg("G") = pybind11::none());
   m.def("psgd_mtp", &psgd_mtp);
   m.def("psgd_orth", &psgd_orth);
   m.def("psgd_reconstruct", &psgd_reconstruct);
   m.def("ef_accum", &ef_accum);
   m.def("psgd_desc_size", &vcx_psgd_desc_size);
+  m.def("psgd_rows_per_block", &vcx_psgd_rows_per_block);
+  m.def("psgd_mtp_rows", &vcx_psgd_mtp_rows);
+  m.def("psgd_mtp_cols", &vcx_psgd_mtp_cols);
 }

@@ -187,35 +187,115 @@ __device__ __forceinline__ int find_mat(const MatDesc* __restrict__ d, int nmat,
   return lo;
 }
 
-// P[row, :] = M[row, :] . Q   — 4 rows per block (one per wave)
+// R consecutive fp32 values (a row of P or Q) — 16-B loads when R is a multiple of 4 (P / Q
+// offsets are multiples of R, so those rows are 16-B aligned)
 template <int R>
-__global__ void __launch_bounds__(256) psgd_mq_kernel(const MatDesc* __restrict__ d, int nmat,
-                                                       const float* __restrict__ M, const float* __restrict__ Q,
-                                                       float* __restrict__ P) {
-  const int mi = find_mat(d, nmat, blockIdx.x, 0);
-  const MatDesc md = d[mi];
-  const int row = (blockIdx.x - md.blk0) * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= md.rows) return;
-  const float* mr = M + md.off + (int64_t)row * md.cols;
-  const float* q = Q + md.qoff;
-  float acc[R];
+__device__ __forceinline__ void load_rv(const float* __restrict__ p, float (&v)[R]) {
+  if constexpr (R % 4 == 0) {
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.f;
-  for (int c = lane; c < md.cols; c += 64) {
-    const float mv = mr[c];
+    for (int i = 0; i < R; i += 4) {
+      const f32x4 t = *(const f32x4*)(p + i);
+      v[i] = t[0];
+      v[i + 1] = t[1];
+      v[i + 2] = t[2];
+      v[i + 3] = t[3];
+    }
+  } else {
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = fmaf(mv, q[(int64_t)c * R + r], acc[r]);
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const float s = wave_sum(acc[r]);
-    if (lane == 0) P[md.poff + (int64_t)row * R + r] = s;
+    for (int i = 0; i < R; ++i) v[i] = p[i];
   }
 }
 
-// Q[c, :] += sum over a 64-row slab of M[row, c] * P[row, :]   (Q zeroed beforehand)
-// block = (matrix, row slab of 64, column chunk of 256)
+// matrices whose flat offset and row length are multiples of 4 take the 16-B paths below
+__device__ __forceinline__ bool psgd_vec(const MatDesc& md) { return ((md.off | (int64_t)md.cols) & 3) == 0; }
+
+// psgd_mq / psgd_reconstruct: each wave owns PSGD_ROWS consecutive rows of a matrix (16 per block)
+// and sweeps their columns, so every Q fragment it loads serves PSGD_ROWS rows (one row per wave
+// read R floats of Q per element of M: 4x the M traffic at R = 4, through L2).
+constexpr int PSGD_ROWS = 4;
+
+// P[row, :] = M[row, :] . Q with the error-feedback accumulation M += G fused into this first pass
+// over M (G == nullptr: no accumulation). On the 16-B path each lane takes 4 consecutive columns
+// per step (f32x4 M load/store, 8-B G load per row).
+template <int R>
+__global__ void __launch_bounds__(256) psgd_mq_kernel(const MatDesc* __restrict__ d, int nmat, float* __restrict__ M,
+                                                       const bf16* __restrict__ G, const float* __restrict__ Q,
+                                                       float* __restrict__ P) {
+  const int mi = find_mat(d, nmat, blockIdx.x, 0);
+  const MatDesc md = d[mi];
+  const int rw = ((blockIdx.x - md.blk0) * 4 + (threadIdx.x >> 6)) * PSGD_ROWS;
+  const int lane = threadIdx.x & 63;
+  if (rw >= md.rows) return;
+  const int nr = min(PSGD_ROWS, md.rows - rw);  // wave-uniform
+  const int64_t rb = md.off + (int64_t)rw * md.cols;
+  const float* q = Q + md.qoff;
+  float acc[PSGD_ROWS][R];
+#pragma unroll
+  for (int i = 0; i < PSGD_ROWS; ++i)
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[i][r] = 0.f;
+  if (psgd_vec(md)) {
+    for (int c = 4 * lane; c < md.cols; c += 256) {
+      float qv[4][R];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) load_rv<R>(q + (int64_t)(c + j) * R, qv[j]);
+#pragma unroll
+      for (int i = 0; i < PSGD_ROWS; ++i) {
+        if (i < nr) {
+          const int64_t e = rb + (int64_t)i * md.cols + c;
+          f32x4 mv = *(const f32x4*)(M + e);
+          if (G) {
+            const bf16x4 gv = *(const bf16x4*)(G + e);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mv[j] += (float)gv[j];
+            *(f32x4*)(M + e) = mv;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[i][r] = fmaf(mv[j], qv[j][r], acc[i][r]);
+        }
+      }
+    }
+  } else {
+    for (int c = lane; c < md.cols; c += 64) {
+      float qv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) qv[r] = q[(int64_t)c * R + r];
+#pragma unroll
+      for (int i = 0; i < PSGD_ROWS; ++i) {
+        if (i < nr) {
+          const int64_t e = rb + (int64_t)i * md.cols + c;
+          float mv = M[e];
+          if (G) {
+            mv += (float)G[e];
+            M[e] = mv;
+          }
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[i][r] = fmaf(mv, qv[r], acc[i][r]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PSGD_ROWS; ++i) {
+    if (i < nr) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float s = wave_sum(acc[i][r]);
+        if (lane == 0) P[md.poff + (int64_t)(rw + i) * R + r] = s;
+      }
+    }
+  }
+}
+
+// Q[c, :] += sum over a 256-row slab of M[row, c] * P[row, :]   (Q zeroed beforehand)
+// block = (matrix, row slab of 256, column chunk of 256): each wave sweeps 64 rows of the slab for
+// 4 consecutive columns per lane (one f32x4 M load per row on the 16-B path, P's slab broadcast
+// from LDS); the 4 waves' partials are summed in LDS and added to Q with coalesced atomics
+// (consecutive lanes -> consecutive Q words, R / 256 atomics per element of M).
+constexpr int PSGD_MTP_ROWS = 256, PSGD_MTP_COLS = 256;
+
 template <int R>
 __global__ void __launch_bounds__(256) psgd_mtp_kernel(const MatDesc* __restrict__ d, int nmat,
                                                         const float* __restrict__ M, const float* __restrict__ P,
@@ -223,28 +303,54 @@ __global__ void __launch_bounds__(256) psgd_mtp_kernel(const MatDesc* __restrict
   const int mi = find_mat(d, nmat, blockIdx.x, 1);
   const MatDesc md = d[mi];
   const int local = blockIdx.x - md.blk0;
-  const int nck = (md.cols + 255) / 256;
+  const int nck = (md.cols + PSGD_MTP_COLS - 1) / PSGD_MTP_COLS;
   const int slab = local / nck, ck = local % nck;
-  const int c = ck * 256 + threadIdx.x;
-  const int r0 = slab * 64, r1 = min(r0 + 64, md.rows);
-  __shared__ float sp[64][R];
-  for (int i = threadIdx.x; i < 64 * R; i += 256) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r0 = slab * PSGD_MTP_ROWS;
+  __shared__ float sp[PSGD_MTP_ROWS][R];
+  __shared__ float red[4][PSGD_MTP_COLS * R];
+  for (int i = threadIdx.x; i < PSGD_MTP_ROWS * R; i += 256) {
     const int rr = r0 + i / R;
     sp[i / R][i % R] = rr < md.rows ? P[md.poff + (int64_t)rr * R + (i % R)] : 0.f;
   }
   __syncthreads();
-  if (c >= md.cols) return;
-  float acc[R];
+  const int c = ck * PSGD_MTP_COLS + 4 * lane;
+  const int wr0 = r0 + 64 * w, wr1 = min(wr0 + 64, md.rows);
+  float acc[4][R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.f;
-  const float* mb = M + md.off + c;
-  for (int row = r0; row < r1; ++row) {
-    const float mv = mb[(int64_t)row * md.cols];
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = fmaf(mv, sp[row - r0][r], acc[r]);
+    for (int r = 0; r < R; ++r) acc[j][r] = 0.f;
+  if (c < md.cols) {
+    const float* mb = M + md.off + c;
+    if (psgd_vec(md)) {  // cols % 4 == 0: all 4 columns are in range
+#pragma unroll 8
+      for (int row = wr0; row < wr1; ++row) {
+        const f32x4 mv = *(const f32x4*)(mb + (int64_t)row * md.cols);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[j][r] = fmaf(mv[j], sp[row - r0][r], acc[j][r]);
+      }
+    } else {
+      for (int row = wr0; row < wr1; ++row) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float mv = c + j < md.cols ? mb[(int64_t)row * md.cols + j] : 0.f;
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[j][r] = fmaf(mv, sp[row - r0][r], acc[j][r]);
+        }
+      }
+    }
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) atomicAdd(&Q[md.qoff + (int64_t)c * R + r], acc[r]);
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < R; ++r) red[w][(4 * lane + j) * R + r] = acc[j][r];
+  __syncthreads();
+  float* qc = Q + md.qoff + (int64_t)ck * PSGD_MTP_COLS * R;
+  for (int i = threadIdx.x; i < PSGD_MTP_COLS * R; i += 256)
+    if (ck * PSGD_MTP_COLS + i / R < md.cols) atomicAdd(qc + i, red[0][i] + red[1][i] + red[2][i] + red[3][i]);
 }
 
 // modified Gram-Schmidt on the R columns of each P (one block per matrix)
@@ -273,23 +379,73 @@ __global__ void __launch_bounds__(256) psgd_orth_kernel(const MatDesc* __restric
   }
 }
 
-// out = P Q^T (bf16, into the flat output buffer at md.off), e = M - P Q^T (in place on M)
+// out = P Q^T (bf16, into the flat output buffer at md.off), e = M - P Q^T (in place on M).
+// Same row ownership as psgd_mq (PSGD_ROWS rows per wave, P rows held in registers, each Q
+// fragment used for all of them); 16-B M load/store and 8-B out store per row on the vector path.
 template <int R>
 __global__ void __launch_bounds__(256) psgd_reconstruct_kernel(const MatDesc* __restrict__ d, int nmat,
                                                                 float* __restrict__ M, const float* __restrict__ P,
                                                                 const float* __restrict__ Q, bf16* __restrict__ out) {
   const int mi = find_mat(d, nmat, blockIdx.x, 2);
   const MatDesc md = d[mi];
-  const int64_t e0 = (int64_t)(blockIdx.x - md.blk0) * 2048;
-  const int64_t total = (int64_t)md.rows * md.cols;
-  for (int64_t t = e0 + threadIdx.x; t < min(e0 + 2048, total); t += 256) {
-    const int row = (int)(t / md.cols), c = (int)(t % md.cols);
-    float v = 0.f;
+  const int rw = ((blockIdx.x - md.blk0) * 4 + (threadIdx.x >> 6)) * PSGD_ROWS;
+  const int lane = threadIdx.x & 63;
+  if (rw >= md.rows) return;
+  const int nr = min(PSGD_ROWS, md.rows - rw);
+  const int64_t rb = md.off + (int64_t)rw * md.cols;
+  const float* q = Q + md.qoff;
+  float pv[PSGD_ROWS][R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) v = fmaf(P[md.poff + (int64_t)row * R + r], Q[md.qoff + (int64_t)c * R + r], v);
-    const int64_t gi = md.off + t;
-    M[gi] -= v;
-    out[gi] = (bf16)v;
+  for (int i = 0; i < PSGD_ROWS; ++i) {
+    if (i < nr) {
+      load_rv<R>(P + md.poff + (int64_t)(rw + i) * R, pv[i]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) pv[i][r] = 0.f;
+    }
+  }
+  if (psgd_vec(md)) {
+    for (int c = 4 * lane; c < md.cols; c += 256) {
+      float qv[4][R];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) load_rv<R>(q + (int64_t)(c + j) * R, qv[j]);
+#pragma unroll
+      for (int i = 0; i < PSGD_ROWS; ++i) {
+        if (i < nr) {
+          f32x4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float s = 0.f;
+#pragma unroll
+            for (int r = 0; r < R; ++r) s = fmaf(pv[i][r], qv[j][r], s);
+            v[j] = s;
+          }
+          const int64_t e = rb + (int64_t)i * md.cols + c;
+          f32x4 mv = *(const f32x4*)(M + e);
+          mv -= v;
+          *(f32x4*)(M + e) = mv;
+          const bf16x4 ov = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          *(bf16x4*)(out + e) = ov;
+        }
+      }
+    }
+  } else {
+    for (int c = lane; c < md.cols; c += 64) {
+      float qv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) qv[r] = q[(int64_t)c * R + r];
+#pragma unroll
+      for (int i = 0; i < PSGD_ROWS; ++i) {
+        if (i < nr) {
+          float v = 0.f;
+#pragma unroll
+          for (int r = 0; r < R; ++r) v = fmaf(pv[i][r], qv[r], v);
+          const int64_t e = rb + (int64_t)i * md.cols + c;
+          M[e] -= v;
+          out[e] = (bf16)v;
+        }
+      }
+    }
   }
 }
 
@@ -350,10 +506,10 @@ void vcx_scatter_add(const int32_t* idx, const void* val, int val_is_bf16, int64
     default: { constexpr int R = 8; __VA_ARGS__; } break;     \
   }
 
-void vcx_psgd_mq(const void* desc, int nmat, int nblocks, const float* M, const float* Q, float* P, int rank,
+void vcx_psgd_mq(const void* desc, int nmat, int nblocks, float* M, const void* G, const float* Q, float* P, int rank,
                  hipStream_t s) {
   PSGD_R_DISPATCH(rank, hipLaunchKernelGGL(psgd_mq_kernel<R>, dim3(nblocks), dim3(256), 0, s, (const MatDesc*)desc,
-                                           nmat, M, Q, P));
+                                           nmat, M, (const bf16*)G, Q, P));
 }
 
 void vcx_psgd_mtp(const void* desc, int nmat, int nblocks, const float* M, const float* P, float* Q, int rank,
@@ -377,3 +533,6 @@ void vcx_ef_accum(const void* g, float* e, int64_t n, hipStream_t s) {
 }
 
 int vcx_psgd_desc_size() { return (int)sizeof(MatDesc); }
+int vcx_psgd_rows_per_block() { return 4 * PSGD_ROWS; }
+int vcx_psgd_mtp_rows() { return PSGD_MTP_ROWS; }
+int vcx_psgd_mtp_cols() { return PSGD_MTP_COLS; }

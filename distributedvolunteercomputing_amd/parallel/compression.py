@@ -135,9 +135,12 @@ class PowerSGDCompressor:
                 b += blocks_of(r, c)
             return torch.from_numpy(recs.view(np.uint8).copy()).to(self.device), b
 
-        self.d_mq, self.nb_mq = table(lambda r, c: (r + 3) // 4)
-        self.d_mtp, self.nb_mtp = table(lambda r, c: ((r + 63) // 64) * ((c + 255) // 256))
-        self.d_rec, self.nb_rec = table(lambda r, c: (r * c + 2047) // 2048)
+        C = native()
+        rb, mr, mc = C.psgd_rows_per_block(), C.psgd_mtp_rows(), C.psgd_mtp_cols()
+        self.d_mq, self.nb_mq = table(lambda r, c: (r + rb - 1) // rb)
+        self.d_mtp, self.nb_mtp = table(lambda r, c: ((r + mr - 1) // mr) * ((c + mc - 1) // mc))
+        self.d_rec = self.d_mq  # same row-block numbering
+        self.nb_rec = self.nb_mq
         self.d_orth = self.d_mq
 
     @property
@@ -152,13 +155,14 @@ class PowerSGDCompressor:
         R = self.rank
         native_path = use_native(g)
         if native_path:
+            # the error-feedback accumulation e += g of the matrices runs inside psgd_mq (one pass
+            # over e instead of two); the dense ranges accumulate in the loop at the end
             C = native()
-            C.ef_accum(g, self.e)
         else:
             self.e.add_(g.float())
         if nm:
             if native_path:
-                C.psgd_mq(self.d_mq, nm, self.nb_mq, self.e, self.Q, self.P, R)
+                C.psgd_mq(self.d_mq, nm, self.nb_mq, self.e, self.Q, self.P, R, g)
             else:
                 self._ref_mq()
             if Pn > 1:
@@ -183,6 +187,8 @@ class PowerSGDCompressor:
         # vectors / small matrices: plain average, no error feedback needed
         for a, b in self.dense_ranges:
             seg = self.e[a:b]
+            if native_path:
+                seg.add_(g[a:b])
             if Pn > 1:
                 group.allreduce_(seg)
                 seg.div_(Pn)

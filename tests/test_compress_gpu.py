@@ -91,3 +91,25 @@ def test_powersgd_error_feedback_converges(gpu):
             rels[t] = float((total / t - g.float()).norm() / g.float().norm())
     # e stays bounded, so the time-averaged transmitted gradient converges to g
     assert rels[80] < 0.5 * rels[10], rels
+
+
+@pytest.mark.parametrize("rank", [1, 4, 8])
+def test_powersgd_odd_shapes_match_reference(gpu, rank):
+    """Matrices whose row length is not a multiple of 4 take the scalar paths of the fused
+    e += g / P = e Q, Q = e^T P and reconstruct kernels; 4-aligned ones the 16-B paths (with a
+    row count that is not a multiple of the 64-row slab and columns past one 1024-column chunk)."""
+    torch.manual_seed(4)
+    m = torch.nn.Sequential(torch.nn.Linear(67, 131), torch.nn.Linear(131, 1100), torch.nn.Linear(1100, 97))
+    m = m.to(gpu, torch.bfloat16)
+    flat = FlatParams(m)
+    c_gpu = PowerSGDCompressor(flat, rank=rank, device=gpu, seed=5)
+    c_ref = PowerSGDCompressor(flat, rank=rank, device=gpu, seed=5)
+    assert len(c_gpu.mats) == 3 and any(cc % 4 for _, _, cc in c_gpu.mats)
+    for step in range(3):
+        g = (torch.randn(flat.numel, device=gpu) * 0.01).to(torch.bfloat16)
+        out = c_gpu.allreduce_mean(g, None).float().clone()
+        with reference_ops():
+            ref = c_ref.allreduce_mean(g, None).float().clone()
+        rel = (out - ref).norm() / ref.norm()
+        assert rel < 2e-2, (step, float(rel))
+        assert (c_gpu.e - c_ref.e).norm() / (c_ref.e.norm() + 1e-9) < 2e-2
