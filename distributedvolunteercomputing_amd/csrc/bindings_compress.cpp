@@ -54,9 +54,10 @@ void check_desc(const at::Tensor& d, int64_t nmat) {
   TORCH_CHECK(d.scalar_type() == at::kByte && d.numel() == nmat * vcx_psgd_desc_size(), "bad descriptor table");
 }
 
-// M += G (error feedback, skipped when G is None) fused with P = M Q over every matrix
+// M += G (error feedback, skipped when G is None) fused with P = M Q over every matrix; lazy: the
+// previous reconstruct ran with update_m=false, so M -= P_prev Q^T is applied first
 void psgd_mq(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::Tensor Q, at::Tensor P, int64_t rank,
-             std::optional<at::Tensor> G) {
+             std::optional<at::Tensor> G, bool lazy) {
   check_desc(desc, nmat);
   CHK(M);
   CHK(Q);
@@ -68,7 +69,7 @@ void psgd_mq(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::T
     g = G->data_ptr();
   }
   vcx_psgd_mq(desc.data_ptr(), (int)nmat, (int)nblocks, M.data_ptr<float>(), g, Q.data_ptr<float>(),
-              P.data_ptr<float>(), (int)rank, cur_stream());
+              P.data_ptr<float>(), (int)rank, lazy ? 1 : 0, cur_stream());
 }
 
 void psgd_mtp(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::Tensor P, at::Tensor Q, int64_t rank) {
@@ -87,7 +88,7 @@ void psgd_orth(at::Tensor desc, int64_t nmat, at::Tensor P, int64_t rank) {
 }
 
 void psgd_reconstruct(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::Tensor P, at::Tensor Q,
-                      at::Tensor out, int64_t rank) {
+                      at::Tensor out, int64_t rank, bool update_m) {
   check_desc(desc, nmat);
   CHK(M);
   CHK(P);
@@ -95,7 +96,7 @@ void psgd_reconstruct(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor
   CHK(out);
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.numel() == M.numel());
   vcx_psgd_reconstruct(desc.data_ptr(), (int)nmat, (int)nblocks, M.data_ptr<float>(), P.data_ptr<float>(),
-                       Q.data_ptr<float>(), out.data_ptr(), (int)rank, cur_stream());
+                       Q.data_ptr<float>(), out.data_ptr(), (int)rank, update_m ? 1 : 0, cur_stream());
 }
 
 void ef_accum(at::Tensor g, at::Tensor e) {
@@ -113,10 +114,12 @@ void vcx_register_compress(pybind11::module& m) {
   m.def("scatter_add", &scatter_add);
   m.def("psgd_mq", &psgd_mq, pybind11::arg("desc"), pybind11::arg("nmat"), pybind11::arg("nblocks"),
         pybind11::arg("M"), pybind11::arg("Q"), pybind11::arg("P"), pybind11::arg("rank"),
-        pybind11::arg("G") = pybind11::none());
+        pybind11::arg("G") = pybind11::none(), pybind11::arg("lazy") = false);
   m.def("psgd_mtp", &psgd_mtp);
   m.def("psgd_orth", &psgd_orth);
-  m.def("psgd_reconstruct", &psgd_reconstruct);
+  m.def("psgd_reconstruct", &psgd_reconstruct, pybind11::arg("desc"), pybind11::arg("nmat"), pybind11::arg("nblocks"),
+        pybind11::arg("M"), pybind11::arg("P"), pybind11::arg("Q"), pybind11::arg("out"), pybind11::arg("rank"),
+        pybind11::arg("update_m") = true);
   m.def("ef_accum", &ef_accum);
   m.def("psgd_desc_size", &vcx_psgd_desc_size);
   m.def("psgd_rows_per_block", &vcx_psgd_rows_per_block);

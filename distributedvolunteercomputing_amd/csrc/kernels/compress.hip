@@ -217,7 +217,12 @@ constexpr int PSGD_ROWS = 4;
 // P[row, :] = M[row, :] . Q with the error-feedback accumulation M += G fused into this first pass
 // over M (G == nullptr: no accumulation). On the 16-B path each lane takes 4 consecutive columns
 // per step (f32x4 M load/store, 8-B G load per row).
-template <int R>
+// LAZY: the previous round's reconstruct left M = e + P Q^T (it only wrote the output), so this
+// pass first subtracts P_prev Q^T from each element (P_prev = this wave's P rows as they stand, Q =
+// the warm-start Q, i.e. exactly the pair the previous reconstruct used): e = M - P_prev Q^T + G.
+// That moves the error-feedback update out of reconstruct, whose pass then never touches M
+// (2 x 4 B per element less HBM traffic per round), at R extra FMAs per element here.
+template <int R, bool LAZY>
 __global__ void __launch_bounds__(256) psgd_mq_kernel(const MatDesc* __restrict__ d, int nmat, float* __restrict__ M,
                                                        const bf16* __restrict__ G, const float* __restrict__ Q,
                                                        float* __restrict__ P) {
@@ -230,10 +235,13 @@ __global__ void __launch_bounds__(256) psgd_mq_kernel(const MatDesc* __restrict_
   const int64_t rb = md.off + (int64_t)rw * md.cols;
   const float* q = Q + md.qoff;
   float acc[PSGD_ROWS][R];
+  float pold[PSGD_ROWS][R];
 #pragma unroll
-  for (int i = 0; i < PSGD_ROWS; ++i)
+  for (int i = 0; i < PSGD_ROWS; ++i) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[i][r] = 0.f;
+    for (int r = 0; r < R; ++r) acc[i][r] = pold[i][r] = 0.f;
+    if (LAZY && i < nr) load_rv<R>(P + md.poff + (int64_t)(rw + i) * R, pold[i]);
+  }
   if (psgd_vec(md)) {
     for (int c = 4 * lane; c < md.cols; c += 256) {
       float qv[4][R];
@@ -244,12 +252,21 @@ __global__ void __launch_bounds__(256) psgd_mq_kernel(const MatDesc* __restrict_
         if (i < nr) {
           const int64_t e = rb + (int64_t)i * md.cols + c;
           f32x4 mv = *(const f32x4*)(M + e);
+          if (LAZY) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float s = 0.f;
+#pragma unroll
+              for (int r = 0; r < R; ++r) s = fmaf(pold[i][r], qv[j][r], s);
+              mv[j] -= s;
+            }
+          }
           if (G) {
             const bf16x4 gv = *(const bf16x4*)(G + e);
 #pragma unroll
             for (int j = 0; j < 4; ++j) mv[j] += (float)gv[j];
-            *(f32x4*)(M + e) = mv;
           }
+          if (LAZY || G) *(f32x4*)(M + e) = mv;
 #pragma unroll
           for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -267,10 +284,14 @@ __global__ void __launch_bounds__(256) psgd_mq_kernel(const MatDesc* __restrict_
         if (i < nr) {
           const int64_t e = rb + (int64_t)i * md.cols + c;
           float mv = M[e];
-          if (G) {
-            mv += (float)G[e];
-            M[e] = mv;
+          if (LAZY) {
+            float s = 0.f;
+#pragma unroll
+            for (int r = 0; r < R; ++r) s = fmaf(pold[i][r], qv[r], s);
+            mv -= s;
           }
+          if (G) mv += (float)G[e];
+          if (LAZY || G) M[e] = mv;
 #pragma unroll
           for (int r = 0; r < R; ++r) acc[i][r] = fmaf(mv, qv[r], acc[i][r]);
         }
@@ -379,10 +400,11 @@ __global__ void __launch_bounds__(256) psgd_orth_kernel(const MatDesc* __restric
   }
 }
 
-// out = P Q^T (bf16, into the flat output buffer at md.off), e = M - P Q^T (in place on M).
+// out = P Q^T (bf16, into the flat output buffer at md.off), e = M - P Q^T (in place on M; with
+// UPDATE_M false M is left alone and the next psgd_mq<LAZY> applies the subtraction).
 // Same row ownership as psgd_mq (PSGD_ROWS rows per wave, P rows held in registers, each Q
 // fragment used for all of them); 16-B M load/store and 8-B out store per row on the vector path.
-template <int R>
+template <int R, bool UPDATE_M>
 __global__ void __launch_bounds__(256) psgd_reconstruct_kernel(const MatDesc* __restrict__ d, int nmat,
                                                                 float* __restrict__ M, const float* __restrict__ P,
                                                                 const float* __restrict__ Q, bf16* __restrict__ out) {
@@ -421,9 +443,11 @@ __global__ void __launch_bounds__(256) psgd_reconstruct_kernel(const MatDesc* __
             v[j] = s;
           }
           const int64_t e = rb + (int64_t)i * md.cols + c;
-          f32x4 mv = *(const f32x4*)(M + e);
-          mv -= v;
-          *(f32x4*)(M + e) = mv;
+          if (UPDATE_M) {
+            f32x4 mv = *(const f32x4*)(M + e);
+            mv -= v;
+            *(f32x4*)(M + e) = mv;
+          }
           const bf16x4 ov = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
           *(bf16x4*)(out + e) = ov;
         }
@@ -441,7 +465,7 @@ __global__ void __launch_bounds__(256) psgd_reconstruct_kernel(const MatDesc* __
 #pragma unroll
           for (int r = 0; r < R; ++r) v = fmaf(pv[i][r], qv[r], v);
           const int64_t e = rb + (int64_t)i * md.cols + c;
-          M[e] -= v;
+          if (UPDATE_M) M[e] -= v;
           out[e] = (bf16)v;
         }
       }
@@ -507,9 +531,14 @@ void vcx_scatter_add(const int32_t* idx, const void* val, int val_is_bf16, int64
   }
 
 void vcx_psgd_mq(const void* desc, int nmat, int nblocks, float* M, const void* G, const float* Q, float* P, int rank,
-                 hipStream_t s) {
-  PSGD_R_DISPATCH(rank, hipLaunchKernelGGL(psgd_mq_kernel<R>, dim3(nblocks), dim3(256), 0, s, (const MatDesc*)desc,
-                                           nmat, M, (const bf16*)G, Q, P));
+                 int lazy, hipStream_t s) {
+  if (lazy) {
+    PSGD_R_DISPATCH(rank, hipLaunchKernelGGL((psgd_mq_kernel<R, true>), dim3(nblocks), dim3(256), 0, s,
+                                             (const MatDesc*)desc, nmat, M, (const bf16*)G, Q, P));
+  } else {
+    PSGD_R_DISPATCH(rank, hipLaunchKernelGGL((psgd_mq_kernel<R, false>), dim3(nblocks), dim3(256), 0, s,
+                                             (const MatDesc*)desc, nmat, M, (const bf16*)G, Q, P));
+  }
 }
 
 void vcx_psgd_mtp(const void* desc, int nmat, int nblocks, const float* M, const float* P, float* Q, int rank,
@@ -523,9 +552,14 @@ void vcx_psgd_orth(const void* desc, int nmat, float* P, int rank, hipStream_t s
 }
 
 void vcx_psgd_reconstruct(const void* desc, int nmat, int nblocks, float* M, const float* P, const float* Q,
-                          void* out, int rank, hipStream_t s) {
-  PSGD_R_DISPATCH(rank, hipLaunchKernelGGL(psgd_reconstruct_kernel<R>, dim3(nblocks), dim3(256), 0, s,
-                                           (const MatDesc*)desc, nmat, M, P, Q, (bf16*)out));
+                          void* out, int rank, int update_m, hipStream_t s) {
+  if (update_m) {
+    PSGD_R_DISPATCH(rank, hipLaunchKernelGGL((psgd_reconstruct_kernel<R, true>), dim3(nblocks), dim3(256), 0, s,
+                                             (const MatDesc*)desc, nmat, M, P, Q, (bf16*)out));
+  } else {
+    PSGD_R_DISPATCH(rank, hipLaunchKernelGGL((psgd_reconstruct_kernel<R, false>), dim3(nblocks), dim3(256), 0, s,
+                                             (const MatDesc*)desc, nmat, M, P, Q, (bf16*)out));
+  }
 }
 
 void vcx_ef_accum(const void* g, float* e, int64_t n, hipStream_t s) {

@@ -7,14 +7,14 @@ void vcx_topk_ef(const void* g, int g_is_bf16, float* e, int64_t n, int k, int* 
                  int32_t* idx_out, void* val_out, int val_is_bf16, hipStream_t s);
 void vcx_scatter_add(const int32_t* idx, const void* val, int val_is_bf16, int64_t m, float scale, float* dense,
                      hipStream_t s);
-// M += G (bf16, G may be null) fused with P = M Q
+// M += G (bf16, G may be null) fused with P = M Q; lazy: first M -= P_prev Q^T (P_prev = P on entry)
 void vcx_psgd_mq(const void* desc, int nmat, int nblocks, float* M, const void* G, const float* Q, float* P, int rank,
-                 hipStream_t s);
+                 int lazy, hipStream_t s);
 void vcx_psgd_mtp(const void* desc, int nmat, int nblocks, const float* M, const float* P, float* Q, int rank,
                   hipStream_t s);
 void vcx_psgd_orth(const void* desc, int nmat, float* P, int rank, hipStream_t s);
 void vcx_psgd_reconstruct(const void* desc, int nmat, int nblocks, float* M, const float* P, const float* Q,
-                          void* out, int rank, hipStream_t s);
+                          void* out, int rank, int update_m, hipStream_t s);
 void vcx_ef_accum(const void* g, float* e, int64_t n, hipStream_t s);
 int vcx_psgd_desc_size();
 // block tables: psgd_mq / psgd_reconstruct take rows_per_block rows per block; psgd_mtp blocks are

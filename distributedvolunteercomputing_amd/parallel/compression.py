@@ -107,6 +107,10 @@ class PowerSGDCompressor:
         self.e = torch.zeros(flat.numel, dtype=torch.float32, device=self.device)
         self.out = torch.zeros(flat.numel, dtype=torch.bfloat16, device=self.device)
         self.bytes_sent = 0
+        # lazy error feedback (HIP path): reconstruct writes only the output and leaves the matrices
+        # of `e` holding M = e_true + P Q^T; the next psgd_mq subtracts P Q^T in its own pass over M.
+        # `ef()` returns the materialised error-feedback buffer.
+        self._lazy_pending = False
         if self.device.type == "cuda":
             self._build_desc()
 
@@ -162,8 +166,9 @@ class PowerSGDCompressor:
             self.e.add_(g.float())
         if nm:
             if native_path:
-                C.psgd_mq(self.d_mq, nm, self.nb_mq, self.e, self.Q, self.P, R, g)
+                C.psgd_mq(self.d_mq, nm, self.nb_mq, self.e, self.Q, self.P, R, g, self._lazy_pending)
             else:
+                self._materialise()
                 self._ref_mq()
             if Pn > 1:
                 group.allreduce_(self.P)
@@ -181,9 +186,11 @@ class PowerSGDCompressor:
                 group.allreduce_(self.Q)
                 self.Q.div_(Pn)
             if native_path:
-                C.psgd_reconstruct(self.d_rec, nm, self.nb_rec, self.e, self.P, self.Q, self.out, R)
+                C.psgd_reconstruct(self.d_rec, nm, self.nb_rec, self.e, self.P, self.Q, self.out, R, False)
+                self._lazy_pending = True
             else:
                 self._ref_reconstruct()
+                self._lazy_pending = False
         # vectors / small matrices: plain average, no error feedback needed
         for a, b in self.dense_ranges:
             seg = self.e[a:b]
@@ -196,6 +203,25 @@ class PowerSGDCompressor:
             seg.zero_()
         self.bytes_sent += 4 * (self.P.numel() + self.Q.numel() + sum(b - a for a, b in self.dense_ranges))
         return self.out
+
+    def _approx_sub(self, e):
+        for i in range(len(self.mats)):
+            off, r, c = self.mats[i]
+            _, P, Q = self._views(i)
+            e[off : off + r * c].view(r, c).sub_(P @ Q.t())
+
+    def ef(self) -> torch.Tensor:
+        """The error-feedback buffer e (a copy with the pending P Q^T subtracted if lazy)."""
+        if not self._lazy_pending:
+            return self.e
+        e = self.e.clone()
+        self._approx_sub(e)
+        return e
+
+    def _materialise(self):
+        if self._lazy_pending:
+            self._approx_sub(self.e)
+            self._lazy_pending = False
 
     # ------------------------------------------------------------------ torch reference
     def _views(self, i):

@@ -68,7 +68,7 @@ def test_powersgd_matches_reference(gpu):
             ref = c_ref.allreduce_mean(g, None).float().clone()
         rel = (out - ref).norm() / ref.norm()
         assert rel < 2e-2, (step, float(rel))
-        assert (c_gpu.e - c_ref.e).norm() / (c_ref.e.norm() + 1e-9) < 2e-2
+        assert (c_gpu.ef() - c_ref.ef()).norm() / (c_ref.ef().norm() + 1e-9) < 2e-2
     # P columns orthonormal after orth
     off, r, cc = c_gpu.mats[0]
     P = c_gpu.P[: r * 4].view(r, 4)
@@ -112,4 +112,4 @@ def test_powersgd_odd_shapes_match_reference(gpu, rank):
             ref = c_ref.allreduce_mean(g, None).float().clone()
         rel = (out - ref).norm() / ref.norm()
         assert rel < 2e-2, (step, float(rel))
-        assert (c_gpu.e - c_ref.e).norm() / (c_ref.e.norm() + 1e-9) < 2e-2
+        assert (c_gpu.ef() - c_ref.ef()).norm() / (c_ref.ef().norm() + 1e-9) < 2e-2
