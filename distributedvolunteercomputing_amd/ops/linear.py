@@ -86,8 +86,15 @@ def gemm_choices() -> dict:
     return dict(_CHOICE)
 
 
+# Big outputs (N*K >= 16M elements) with fewer tokens than this take ONE GEMM that accumulates
+# straight into the bf16 .grad (beta = 1) instead of a split-M batch + fp32 partial reduction
+_BIG_SPLIT_MIN_M = int(os.environ.get("VCX_WGRAD_BIG_SPLIT_MIN_M", "16384"))
+
+
 def _splits(M: int, N: int, K: int) -> int:
     if N * K >= 16 * 1024 * 1024:  # big outputs (LM head) already fill the GPU
+        if M < _BIG_SPLIT_MIN_M:
+            return 1
         s = 4
     else:
         s = 16
@@ -102,13 +109,12 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor | None = None, 
     K = x2.shape[1]
     S = _splits(M, N, K)
     if S == 1 or not use_native(dy2) or (N * K) % 8:
-        g = dy2.t().mm(x2)
         if out is None:
-            return g
+            return dy2.t().mm(x2)
         if accumulate:
-            out.add_(g)
+            out.addmm_(dy2.t(), x2)  # one GEMM with beta = 1: no separate product tensor + add pass
         else:
-            out.copy_(g)
+            torch.mm(dy2.t(), x2, out=out)
         return out
     part = torch.bmm(dy2.view(S, M // S, N).transpose(1, 2), x2.view(S, M // S, K))  # [S, N, K]
     if out is None:

@@ -222,7 +222,10 @@ def test_embedding_fwd_bwd(gpu):
     assert torch.allclose(wpe.grad.float(), p32.grad, atol=5e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M,N,K,bias", [(8192, 768, 768, True), (65536, 2304, 768, False), (4096, 512, 96, False)])
+# (4096, 4096, 4096): a big output at few tokens (the Llama-3-8B shape) takes the single
+# beta = 1 GEMM into .grad instead of the split-M batch
+@pytest.mark.parametrize("M,N,K,bias", [(8192, 768, 768, True), (65536, 2304, 768, False), (4096, 512, 96, False),
+                                        (4096, 4096, 4096, False)])
 @pytest.mark.parametrize("preset_grad", [False, True])
 def test_linear_splitm_wgrad(gpu, M, N, K, bias, preset_grad):
     """ops.linear: split-M batched weight gradient (HIP fp32 reduction into .grad) against an
