@@ -10,7 +10,7 @@ from distributedvolunteercomputing_amd.parallel.flat_params import FlatParams
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n,ratio", [(1_000_003, 0.01), (65536, 0.1), (4096, 0.5), (777, 0.01)])
+@pytest.mark.parametrize("n,ratio", [(1_000_003, 0.01), (65536, 0.1), (4096, 0.5), (777, 0.01), (16_777_219, 0.01)])
 def test_topk_exact(gpu, n, ratio):
     torch.manual_seed(0)
     c = TopKCompressor(n, ratio, gpu)
