@@ -214,8 +214,12 @@ __global__ void __launch_bounds__(256) topk_select_kernel(float* __restrict__ x,
 template <typename VT>
 __global__ void __launch_bounds__(256) scatter_add_kernel(const int32_t* __restrict__ idx, const VT* __restrict__ val,
                                                            int64_t m, float scale, float* __restrict__ dense) {
-  for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < m; j += (int64_t)gridDim.x * 256)
-    atomicAdd(&dense[idx[j]], scale * (float)val[j]);
+  // zero values are skipped: slots the selection left unfilled (fewer than k nonzero candidates)
+  // hold idx 0 / val 0, and thousands of no-op atomics on dense[0] serialised the kernel (3.2 ms)
+  for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < m; j += (int64_t)gridDim.x * 256) {
+    const float v = (float)val[j];
+    if (v != 0.f) atomicAdd(&dense[idx[j]], scale * v);
+  }
 }
 
 // =====================================================================================
