@@ -44,7 +44,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=64, help="per-peer micro-batch (sequences)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--H", type=int, default=4)
-    ap.add_argument("--algo", default="rccl", choices=["rccl", "rs_ag", "butterfly", "ring"])
+    ap.add_argument("--algo", default="direct", choices=["rccl", "rs_ag", "butterfly", "ring", "direct"],
+                    help="averaging all-reduce: direct = one-shot all-to-all reduce-scatter/all-gather over "
+                         "all 7 xGMI links (parallel/collectives.py); rccl = the library all-reduce")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--graph", type=int, default=1, help="1: replay each local step as one hipGraph, 0: eager")
     return ap.parse_args()

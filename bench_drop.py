@@ -3,6 +3,14 @@
 ("samples/sec GPT-2-small local-SGD at 1/2/4/8 peers; step-time under 1-peer drop").
 
     python bench_drop.py --peers P [--model gpt2] [--batch 64] [--steps 24] [--warmup 8] [--lease 1.0]
+                         [--fault step|collective|stop] [--drop-peers 3,4]
+
+Faults: ``step`` — the victim exits between two steps (heartbeat stops); ``collective`` — the
+victim SIGKILLs itself from INSIDE the averaging all-reduce of the first round at or after
+``--drop-at`` (the other peers are blocked in that collective: their watchdog or the failed
+transport aborts it, they recover to a new generation and redo the round); ``stop`` — the
+victim SIGSTOPs itself inside the collective (no socket error anywhere: only the lease-based
+watchdog can tell), and stays frozen until the launcher kills it at the end.
 
 This process plays the coordinator: it hosts the rendezvous store (so no peer is special and
 any peer may die) and starts P peer processes, one per visible GPU (round-robin when P exceeds
@@ -44,6 +52,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--drop-at", type=int, default=None, help="step at which the peer dies (default: mid-window)")
     ap.add_argument("--drop-peer", type=int, default=None, help="default: the last peer")
+    ap.add_argument("--drop-peers", default=None, help="comma-separated victims (overrides --drop-peer)")
+    ap.add_argument("--fault", default="step", choices=["step", "collective", "stop"])
     ap.add_argument("--lease", type=float, default=1.0, help="heartbeat lease (s) after which a silent peer is dead")
     ap.add_argument("--backend", default=None, choices=[None, "nccl", "gloo"])
     ap.add_argument("--graph", type=int, default=1)
@@ -66,6 +76,8 @@ def peer_main(a):
     import torch
     import torch.distributed as dist
 
+    import signal
+
     from distributedvolunteercomputing_amd.models.gpt2 import GPT2, GPT2Config
     from distributedvolunteercomputing_amd.parallel.elastic import ElasticMembership
     from distributedvolunteercomputing_amd.parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer
@@ -79,6 +91,16 @@ def peer_main(a):
                           wait_for_workers=False)
     mem = ElasticMembership(store, a.peer, backend=backend, device=device, lease_s=a.lease,
                             heartbeat_s=max(a.lease / 10, 0.02))
+    victims = [int(v) for v in a.drop_peers.split(",")]
+    armed = {"on": False}
+    if a.peer in victims and a.fault != "step":
+        sig = signal.SIGKILL if a.fault == "collective" else signal.SIGSTOP
+
+        def hook(grp, op):  # fires after the op was issued: the other peers are inside it
+            if armed["on"] and op in ("allreduce", "alltoall", "all_gather"):
+                print(f"[peer {a.peer}] fault injection: {signal.Signals(sig).name} inside {op}", flush=True)
+                os.kill(os.getpid(), sig)
+        mem.fault_hook = hook
     mem.bootstrap(list(range(a.peers)))
     cfg = GPT2Config.preset(a.model)
     cfg.n_ctx = max(cfg.n_ctx, a.seq)
@@ -108,17 +130,20 @@ def peer_main(a):
     mem.group.barrier()
     timeline = []
     for i in range(a.warmup, a.warmup + a.steps):
-        if a.peer == a.drop_peer and i == a.drop_at:
-            print(f"[peer {a.peer}] fault injection: crashing at step {i}", flush=True)
-            mem.stop_heartbeat()
-            os._exit(0)  # no leave(): the survivors must detect the silence
+        if a.peer in victims and i == a.drop_at:
+            if a.fault == "step":
+                print(f"[peer {a.peer}] fault injection: crashing at step {i}", flush=True)
+                mem.stop_heartbeat()
+                os._exit(0)  # no leave(): the survivors must detect the silence
+            armed["on"] = True  # die inside the next averaging collective
         t0 = time.perf_counter()
         st = tr.step(*batch(i))
         sync()
         timeline.append({"step": i, "ms": (time.perf_counter() - t0) * 1e3, "synced": bool(st.synced),
                          "members": st.members, "gen": mem.gen, "sync_ms": st.sync_ms if st.synced else 0.0})
     with open(os.path.join(a.out, f"peer{a.peer}.json"), "w") as f:
-        json.dump({"peer": a.peer, "backend": backend, "timeline": timeline, "events": mem.events}, f)
+        json.dump({"peer": a.peer, "backend": backend, "timeline": timeline, "events": mem.events,
+                   "failed_rounds": tr.failed_rounds}, f)
     mem.stop_heartbeat()
     return 0
 
@@ -131,6 +156,9 @@ def launcher(a):
     ngpu = torch.cuda.device_count()  # does not initialise the GPU in this process
     if a.drop_peer is None:
         a.drop_peer = a.peers - 1
+    if a.drop_peers is None:
+        a.drop_peers = str(a.drop_peer)
+    victims = [int(v) for v in a.drop_peers.split(",")]
     if a.drop_at is None:
         a.drop_at = a.warmup + a.steps // 2 + (1 if a.H > 1 else 0)
     sk = socket.socket()
@@ -143,39 +171,44 @@ def launcher(a):
     env = dict(os.environ, VCX_DROP_NGPU=str(ngpu), PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     common = [sys.executable, os.path.abspath(__file__), "--peers", str(a.peers), "--model", a.model,
               "--batch", str(a.batch), "--seq", str(a.seq), "--H", str(a.H), "--steps", str(a.steps),
-              "--warmup", str(a.warmup), "--drop-at", str(a.drop_at), "--drop-peer", str(a.drop_peer),
+              "--warmup", str(a.warmup), "--drop-at", str(a.drop_at), "--drop-peers", a.drop_peers,
+              "--fault", a.fault,
               "--lease", str(a.lease), "--graph", str(a.graph), "--port", str(port), "--out", out]
     if a.backend:
         common += ["--backend", a.backend]
     procs = [subprocess.Popen(common + ["--peer", str(r)], env=env) for r in range(a.peers)]
     t_end = time.time() + a.timeout
     rc = {}
-    while len(rc) < len(procs) and time.time() < t_end:
+    survivors = [r for r in range(a.peers) if r not in victims]
+    while not all(r in rc for r in survivors) and time.time() < t_end:
         for r, p in enumerate(procs):
             if r not in rc and p.poll() is not None:
                 rc[r] = p.returncode
         time.sleep(0.2)
     for r, p in enumerate(procs):
         if r not in rc:
-            p.kill()
-            rc[r] = "timeout"
-    bad = {r: c for r, c in rc.items() if c != 0}
+            p.kill()  # timeout, or a SIGSTOPped victim still frozen
+            p.wait()
+            rc[r] = "timeout" if r in survivors else "killed"
+    bad = {r: c for r, c in rc.items() if r in survivors and c != 0}
     if bad:
         print(f"[bench_drop] peers failed: {bad}", file=sys.stderr)
         return 1
-    survivors = [r for r in range(a.peers) if r != a.drop_peer]
     tl = {}
     backend = None
+    failed_rounds = 0
     for r in survivors:
         with open(os.path.join(out, f"peer{r}.json")) as f:
             d = json.load(f)
         backend = d["backend"]
+        failed_rounds = max(failed_rounds, d.get("failed_rounds", 0))
         for e in d["timeline"]:
             cur = tl.setdefault(e["step"], dict(e))
             cur["ms"] = max(cur["ms"], e["ms"])  # a step ends when its slowest survivor is done
     steps = sorted(tl)
     before = [tl[s]["ms"] for s in steps if s < a.drop_at]
-    regroup = next((s for s in steps if s >= a.drop_at and tl[s]["members"] == a.peers - 1 and tl[s]["synced"]), None)
+    regroup = next((s for s in steps if s >= a.drop_at and tl[s]["members"] == len(survivors) and tl[s]["synced"]),
+                   None)
     after = [tl[s]["ms"] for s in steps if regroup is not None and s > regroup]
     window = [tl[s]["ms"] for s in steps]
     mean = lambda xs: sum(xs) / len(xs) if xs else float("nan")  # noqa: E731
@@ -195,7 +228,9 @@ def launcher(a):
         "dtype": "bf16" if ngpu else "fp32",
         "data": "synthetic (random tokens, random-init weights)",
         "config": {"model": a.model, "per_peer_batch": a.batch, "seq_len": a.seq, "H": a.H,
-                   "backend": backend, "lease_s": a.lease, "drop_at": a.drop_at, "drop_peer": a.drop_peer},
+                   "backend": backend, "lease_s": a.lease, "drop_at": a.drop_at, "drop_peers": victims,
+                   "fault": a.fault},
+        "rounds_aborted_and_redone": failed_rounds,
         "ms_per_step_before": round(mean(before), 3),
         "ms_per_step_after": round(mean(after), 3),
         "regroup_step": regroup,
@@ -203,7 +238,7 @@ def launcher(a):
         "regroup_sync_ms": round(regroup_sync, 3),
         "drop_stall_ms": round(regroup_sync - steady_sync, 3),
         "samples_per_s_before": round(a.peers * a.batch / mean(before) * 1e3, 2),
-        "samples_per_s_after": round((a.peers - 1) * a.batch / mean(after) * 1e3, 2) if after else None,
+        "samples_per_s_after": round(len(survivors) * a.batch / mean(after) * 1e3, 2) if after else None,
     }
     line = json.dumps(rec)
     print(line, flush=True)

@@ -32,7 +32,7 @@ from collections import deque
 from .. import _native_loader
 from ..utils.metrics import Metrics
 from . import protocol
-from .transport import FrameHub, FrameSender
+from .transport import BadFrame, FrameHub, FrameSender
 
 
 class _Volunteer:
@@ -120,7 +120,7 @@ class coordinator:  # noqa: N801  (reference class name)
             if verb is None:
                 continue
             try:
-                reply = self._handle(verb, addr)
+                reply = self._handle(verb, addr, src)
             except Exception as e:  # never let one bad datagram kill the control loop
                 reply = f"err{protocol.SEP}{e}".encode()
             if reply is not None:
@@ -130,10 +130,19 @@ class coordinator:  # noqa: N801  (reference class name)
                     pass
         self.log("manager terminated.")
 
-    def _handle(self, verb, addr):
+    def _handle(self, verb, addr, src=None):
         now = time.time()
         if verb == "join":
+            if src is not None and not protocol.addr_matches(addr, src[0]):
+                self.metrics.incr("spoofed_datagrams")
+                return f"err{protocol.SEP}address {addr} does not match sender {src[0]}".encode()
             return self._join(addr, now)
+        if verb in ("request", "stop", "end", "hb"):
+            with self._lock:
+                known = addr in self.vols
+            if not known or (src is not None and not protocol.addr_matches(addr, src[0])):
+                self.metrics.incr("unknown_datagrams")
+                return f"err{protocol.SEP}{addr} has not joined".encode()
         if verb == "request":
             self.sched.set_available(addr, False)
             with self._lock:
@@ -192,7 +201,12 @@ class coordinator:  # noqa: N801  (reference class name)
             v = self.vols.pop(addr, None)
             self.requesters.discard(addr)
         requeued = self.sched.remove_worker(addr)
-        self.sched.cancel_requester(addr)
+        dropped = self.sched.cancel_requester(addr)
+        if dropped:  # its queued chunks will never be dispatched: free their frames
+            with self._lock:
+                for cid in dropped:
+                    self.chunks.pop(cid, None)
+            self.metrics.incr("chunks_cancelled", len(dropped))
         if v is None:
             return
         v.alive = False
@@ -217,7 +231,12 @@ class coordinator:  # noqa: N801  (reference class name)
     # ------------------------------------------------------------------ data plane
     def _ingest(self, v: _Volunteer):
         while v.alive and self.continue_listening:
-            r = v.hub.recv_frame(timeout=0.25)
+            try:
+                r = v.hub.recv_frame(timeout=0.25)
+            except BadFrame as e:  # a malformed frame costs its sender the frame, not the thread
+                self.metrics.incr("bad_frames")
+                self.log(f"bad frame from {v.addr}: {e}")
+                continue
             if r is None:
                 continue
             hdr, arr, _ = r

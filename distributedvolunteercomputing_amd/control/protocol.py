@@ -63,6 +63,24 @@ def split_addr(addr: str):
     return host, int(port)
 
 
+def addr_matches(addr: str, src_ip: str) -> bool:
+    """Does a datagram from `src_ip` plausibly come from the volunteer that claims `addr`?
+    Datagrams from this machine (loopback) are trusted; otherwise the claimed host must resolve
+    to the sender's IP (a volunteer cannot act — join, request, end — on another one's behalf)."""
+    if src_ip.startswith("127.") or src_ip == "::1":
+        return True
+    try:
+        host, _ = split_addr(addr)
+    except ValueError:
+        return False
+    if host == src_ip:
+        return True
+    try:
+        return socket.gethostbyname(host) == src_ip
+    except OSError:
+        return False
+
+
 class ControlClient:
     """Sends verbs to the coordinator with bounded retries (reference: unbounded)."""
 

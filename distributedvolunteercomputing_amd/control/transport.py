@@ -9,6 +9,11 @@ control); ``REQ_REP=False`` streams (the reference's PUB/SUB mode).
 
 The byte moving is C++ (``_native.Hub`` / ``_native.Sender``): one listening socket per hub
 accepts any number of senders, receive queues are bounded, all blocking I/O drops the GIL.
+
+Frames come from untrusted volunteers: the native hub drops a connection whose frame announces
+more than ``max_payload`` / ``max_header`` bytes before allocating anything, and
+``recv_frame`` raises ``BadFrame`` for a header that is not a JSON object, names a dtype outside
+the plain numeric ones, or has a shape that does not match the payload size.
 """
 from __future__ import annotations
 
@@ -17,6 +22,44 @@ import json
 import numpy as np
 
 from .. import _native_loader
+
+
+class BadFrame(ValueError):
+    """A received frame whose header is malformed or disagrees with its payload."""
+
+
+# plain numeric dtypes only: no object / void / string dtypes from the wire
+_DTYPES = {np.dtype(t).str for t in (np.uint8, np.int8, np.uint16, np.int16, np.uint32, np.int32, np.uint64,
+                                     np.int64, np.float16, np.float32, np.float64, np.bool_)}
+_MAX_DIMS = 8
+
+
+def decode_frame(header: str, nbytes: int):
+    """-> (header dict, dtype, shape or None), validated against the payload size."""
+    try:
+        hdr = json.loads(header)
+    except (ValueError, UnicodeDecodeError) as e:
+        raise BadFrame(f"header is not JSON: {e}") from None
+    if not isinstance(hdr, dict):
+        raise BadFrame("header is not a JSON object")
+    if not isinstance(hdr.get("msg", ""), str):
+        raise BadFrame("msg must be a string")
+    try:
+        dt = np.dtype(hdr.get("dtype", "uint8"))
+    except TypeError:
+        raise BadFrame(f"unknown dtype {hdr.get('dtype')!r}") from None
+    if dt.str not in _DTYPES:
+        raise BadFrame(f"dtype {dt.str!r} not allowed")
+    shape = hdr.get("shape")
+    if shape is not None:
+        if (not isinstance(shape, list) or len(shape) > _MAX_DIMS
+                or not all(isinstance(d, int) and not isinstance(d, bool) and d >= 0 for d in shape)):
+            raise BadFrame(f"bad shape {shape!r}")
+        if int(np.prod(shape, dtype=np.int64)) * dt.itemsize != nbytes:
+            raise BadFrame(f"shape {shape} x {dt.itemsize} B != payload {nbytes} B")
+    elif nbytes % dt.itemsize:
+        raise BadFrame(f"payload {nbytes} B is not a multiple of {dt.itemsize}")
+    return hdr, dt, shape
 
 
 def _port_of(spec) -> int:
@@ -34,9 +77,10 @@ def _host_of(spec) -> str:
 
 
 class FrameHub:
-    def __init__(self, open_port="tcp://*:5555", REQ_REP: bool = True, capacity: int = 64, bind_host: str = ""):
+    def __init__(self, open_port="tcp://*:5555", REQ_REP: bool = True, capacity: int = 64, bind_host: str = "",
+                 max_payload: int = 2 << 30, max_header: int = 64 << 10):
         N = _native_loader.native()
-        self.hub = N.Hub(bind_host, _port_of(open_port), capacity, REQ_REP)
+        self.hub = N.Hub(bind_host, _port_of(open_port), capacity, REQ_REP, int(max_payload), int(max_header))
         self.req_rep = REQ_REP
 
     @property
@@ -48,9 +92,9 @@ class FrameHub:
         f = self.hub.recv(-1.0 if timeout is None else float(timeout))
         if f is None:
             return None
-        hdr = json.loads(f.header)
-        arr = np.frombuffer(f, dtype=np.dtype(hdr.get("dtype", "uint8")))
-        shape = hdr.get("shape")
+        view = memoryview(f)
+        hdr, dt, shape = decode_frame(f.header, view.nbytes)
+        arr = np.frombuffer(f, dtype=dt)
         if shape is not None:
             arr = arr.reshape(shape)
         return hdr, arr, f.peer
@@ -67,6 +111,10 @@ class FrameHub:
 
     def pending(self) -> int:
         return self.hub.pending()
+
+    @property
+    def frames_rejected(self) -> int:
+        return self.hub.frames_rejected
 
     def close(self):
         self.hub.close()

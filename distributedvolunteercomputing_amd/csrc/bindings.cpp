@@ -89,6 +89,18 @@ void f32_to_bf16(at::Tensor src, at::Tensor dst) {
   vcx_f32_to_bf16(src.data_ptr<float>(), dst.data_ptr(), src.numel(), cur_stream());
 }
 
+void reduce_bcast_bf16(at::Tensor in, c10::optional<at::Tensor> out, c10::optional<at::Tensor> mine, int64_t P) {
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kBFloat16 && in.is_contiguous(), "reduce_bcast: bf16 cuda in");
+  const int64_t n = in.numel() / P;
+  TORCH_CHECK(P > 0 && n * P == in.numel() && n % 8 == 0, "reduce_bcast: numel must be P * n with n % 8 == 0");
+  if (out) TORCH_CHECK(out->numel() == in.numel() && out->is_contiguous() && out->scalar_type() == at::kBFloat16,
+                       "reduce_bcast: out must match in");
+  if (mine) TORCH_CHECK(mine->numel() == n && mine->is_contiguous() && mine->scalar_type() == at::kBFloat16,
+                        "reduce_bcast: mine must hold n bf16");
+  vcx_reduce_bcast_bf16(in.data_ptr(), out ? out->data_ptr() : nullptr, mine ? mine->data_ptr() : nullptr, (int)P, n,
+                        cur_stream());
+}
+
 void axpy_bf16(at::Tensor src, at::Tensor acc, double scale) {
   CHECK_IN(src, kBF);
   CHECK_IN(acc, kBF);
@@ -511,6 +523,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lsgd_apply", &lsgd_apply);
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("axpy_bf16", &axpy_bf16);
+  m.def("reduce_bcast_bf16", &reduce_bcast_bf16);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("mean"),

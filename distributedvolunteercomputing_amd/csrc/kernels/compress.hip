@@ -224,9 +224,10 @@ __global__ void __launch_bounds__(256) topk_select_kernel(float* __restrict__ x,
       if ((selm >> j) & 1ull) {
         const int64_t i = base + (int64_t)(j >> 2) * 1024 + 4 * threadIdx.x + (j & 3);
         if (pos < k) {
+          const VT sent = (VT)v[j];
           idx_out[pos] = (int32_t)i;
-          val_out[pos] = (VT)v[j];
-          x[i] = 0.f;
+          val_out[pos] = sent;
+          x[i] = v[j] - (float)sent;  // the wire-dtype rounding residual stays in error feedback
         }
         ++pos;
       }

@@ -254,6 +254,38 @@ void vcx_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s) {
   hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, s, src, (bf16*)dst, n8);
 }
 
+// Direct all-reduce, middle step: this peer received its shard from all P peers (rows of
+// `in`, row stride n); sum them in fp32 and write the sum to all P rows of `out` (the send
+// buffer of the all-gather all-to-all, one row per destination) and to `mine` (this peer's
+// shard of the averaged buffer). One pass: reads P*n, writes (P+1)*n bf16.
+__global__ void __launch_bounds__(256) reduce_bcast_bf16_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
+                                                               bf16* __restrict__ mine, int P, int64_t n8) {
+  const int64_t n = n8 * 8;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i * 8;
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = 0.f;
+    for (int k = 0; k < P; ++k) {
+      bf16x8 v = *(const bf16x8*)(in + k * n + b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] += (float)v[j];
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)t[j];
+    if (out)
+      for (int k = 0; k < P; ++k) *(bf16x8*)(out + k * n + b) = o;
+    if (mine) *(bf16x8*)(mine + b) = o;
+  }
+}
+
+void vcx_reduce_bcast_bf16(const void* in, void* out, void* mine, int P, int64_t n, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(reduce_bcast_bf16_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, s, (const bf16*)in,
+                     (bf16*)out, (bf16*)mine, P, n8);
+}
+
 void vcx_axpy_bf16(const void* src, void* acc, int64_t n, float scale, hipStream_t s) {
   const int64_t n8 = n / 8;
   hipLaunchKernelGGL(axpy_bf16_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, s, (const bf16*)src,

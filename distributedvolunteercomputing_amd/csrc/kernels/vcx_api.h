@@ -14,6 +14,7 @@ void vcx_lsgd_apply(const void* avg, float* anchor, float* master, void* param, 
                     float outer_lr, float mu, int nesterov, float avg_scale, hipStream_t s);
 void vcx_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s);
 void vcx_axpy_bf16(const void* src, void* acc, int64_t n, float scale, hipStream_t s);
+void vcx_reduce_bcast_bf16(const void* in, void* out, void* mine, int P, int64_t n, hipStream_t s);
 void vcx_splitk_reduce(const void* part, void* acc, int S, int64_t n, int accumulate, hipStream_t s);
 
 // norm_act.hip

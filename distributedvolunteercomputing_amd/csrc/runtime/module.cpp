@@ -32,8 +32,9 @@ PYBIND11_MODULE(_native, m) {
       });
 
   py::class_<Hub>(m, "Hub")
-      .def(py::init<const std::string&, int, size_t, bool>(), py::arg("bind_host") = "", py::arg("port") = 0,
-           py::arg("capacity") = 64, py::arg("ack") = true)
+      .def(py::init<const std::string&, int, size_t, bool, uint64_t, uint32_t>(), py::arg("bind_host") = "",
+           py::arg("port") = 0, py::arg("capacity") = 64, py::arg("ack") = true,
+           py::arg("max_payload") = Hub::kDefaultMaxPayload, py::arg("max_header") = Hub::kDefaultMaxHeader)
       .def_property_readonly("port", &Hub::port)
       .def(
           "recv",
@@ -51,7 +52,8 @@ PYBIND11_MODULE(_native, m) {
       .def("pending", &Hub::pending)
       .def("close", &Hub::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("frames_received", &Hub::frames_received)
-      .def_property_readonly("bytes_received", &Hub::bytes_received);
+      .def_property_readonly("bytes_received", &Hub::bytes_received)
+      .def_property_readonly("frames_rejected", &Hub::frames_rejected);
 
   py::class_<Sender>(m, "Sender")
       .def(py::init<const std::string&, int, bool, double>(), py::arg("host"), py::arg("port"),

@@ -146,10 +146,14 @@ bool ChunkScheduler::complete(int64_t chunk) {
   return true;
 }
 
-void ChunkScheduler::cancel_requester(const std::string& requester) {
+std::vector<int64_t> ChunkScheduler::cancel_requester(const std::string& requester) {
   std::lock_guard<std::mutex> g(mu_);
+  std::vector<int64_t> dropped;
+  for (const Pending& p : q_)
+    if (p.requester == requester) dropped.push_back(p.chunk);
   q_.erase(std::remove_if(q_.begin(), q_.end(), [&](const Pending& p) { return p.requester == requester; }),
            q_.end());
+  return dropped;  // the caller frees the payloads it holds for these chunks
 }
 
 size_t ChunkScheduler::queued() {

@@ -53,7 +53,7 @@ class ChunkScheduler {
   void requeue_front(int64_t chunk, const std::string& requester);
   Assignment next();  // invalid Assignment when nothing is dispatchable
   bool complete(int64_t chunk);  // returns false for an unknown / duplicate completion
-  void cancel_requester(const std::string& requester);  // drop queued chunks of a requester
+  std::vector<int64_t> cancel_requester(const std::string& requester);  // drop (and return) its queued chunks
 
   size_t queued();
   size_t inflight();

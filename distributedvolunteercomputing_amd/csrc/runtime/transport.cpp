@@ -97,7 +97,8 @@ void tune_socket(int fd) {
 }  // namespace
 
 // ============================================================================ Hub
-Hub::Hub(const std::string& bind_host, int port, size_t capacity, bool ack) : capacity_(capacity ? capacity : 1), ack_(ack) {
+Hub::Hub(const std::string& bind_host, int port, size_t capacity, bool ack, uint64_t max_payload, uint32_t max_header)
+    : capacity_(capacity ? capacity : 1), ack_(ack), max_payload_(max_payload), max_header_(max_header) {
   listen_fd_ = ::socket(AF_INET, SOCK_STREAM, 0);
   if (listen_fd_ < 0) throw std::runtime_error("Hub: socket() failed");
   int one = 1;
@@ -168,10 +169,25 @@ void Hub::accept_loop() {
 }
 
 void Hub::conn_loop(int fd, std::string peer) {
+  // Everything on this socket comes from an untrusted volunteer: lengths are checked against
+  // the configured caps BEFORE anything is allocated, and no exception may escape the thread
+  // (std::terminate would take the whole coordinator down).
+  try {
+    conn_frames(fd, peer);
+  } catch (const std::exception&) {
+    rejected_ += 1;
+  }
+  ::shutdown(fd, SHUT_RDWR);
+}
+
+void Hub::conn_frames(int fd, const std::string& peer) {
   while (!closed_.load()) {
     WireHeader wh{};
     if (!read_all(fd, &wh, sizeof(wh), &closed_)) break;
-    if (wh.magic != kMagic || wh.header_len > (1u << 20)) break;  // protocol error: drop the connection
+    if (wh.magic != kMagic || wh.header_len > max_header_ || wh.payload_len > max_payload_) {
+      rejected_ += 1;  // protocol error or oversized frame: drop the connection, allocate nothing
+      break;
+    }
     Frame f;
     f.peer = peer;
     f.header.resize(wh.header_len);

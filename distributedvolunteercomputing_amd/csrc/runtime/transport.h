@@ -34,7 +34,12 @@ struct Frame {
 
 class Hub {
  public:
-  Hub(const std::string& bind_host, int port, size_t capacity, bool ack);
+  // max_payload / max_header bound what ONE frame from an untrusted volunteer may make this
+  // process allocate; a frame announcing more drops its connection before any allocation.
+  Hub(const std::string& bind_host, int port, size_t capacity, bool ack, uint64_t max_payload = kDefaultMaxPayload,
+      uint32_t max_header = kDefaultMaxHeader);
+  static constexpr uint64_t kDefaultMaxPayload = 2ull << 30;  // 2 GiB: a raw 100-frame 1440p chunk
+  static constexpr uint32_t kDefaultMaxHeader = 64u << 10;
   ~Hub();
   int port() const { return port_; }
   // Blocks up to timeout_s (<0: forever). Returns false on timeout / closed.
@@ -43,14 +48,18 @@ class Hub {
   void close();
   uint64_t frames_received() const { return frames_; }
   uint64_t bytes_received() const { return bytes_; }
+  uint64_t frames_rejected() const { return rejected_; }
 
  private:
   void accept_loop();
   void conn_loop(int fd, std::string peer);
+  void conn_frames(int fd, const std::string& peer);
   int listen_fd_ = -1;
   int port_ = 0;
   size_t capacity_;
   bool ack_;
+  uint64_t max_payload_;
+  uint32_t max_header_;
   std::atomic<bool> closed_{false};
   std::mutex mu_;
   std::condition_variable cv_not_empty_, cv_not_full_;
@@ -59,7 +68,7 @@ class Hub {
   std::mutex conn_mu_;
   std::vector<std::thread> conns_;
   std::vector<int> conn_fds_;
-  std::atomic<uint64_t> frames_{0}, bytes_{0};
+  std::atomic<uint64_t> frames_{0}, bytes_{0}, rejected_{0};
 };
 
 class Sender {

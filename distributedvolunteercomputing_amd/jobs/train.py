@@ -85,7 +85,10 @@ def parse(argv=None):
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--lr", type=float, default=6e-4)
     ap.add_argument("--H", type=int, default=4)
-    ap.add_argument("--algo", default="rccl", choices=["rccl", "rs_ag", "butterfly", "ring"])
+    ap.add_argument("--algo", default=None, choices=["rccl", "rs_ag", "butterfly", "ring", "direct", "rs"],
+                    help="averaging collective (default: direct for localsgd, rs = reduce-scatter + replica "
+                         "shifts for sharded)")
+    ap.add_argument("--replicas", type=int, default=2, help="sharded: extra holders of every optimizer shard")
     ap.add_argument("--compression", default="none", choices=["none", "topk", "powersgd"])
     ap.add_argument("--topk-ratio", type=float, default=0.01)
     ap.add_argument("--powersgd-rank", type=int, default=4)
@@ -153,14 +156,15 @@ def main(argv=None):
     if a.trainer == "localsgd":
         from ..parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer
 
-        cfg = LocalSGDConfig(lr=a.lr, H=a.H, algo=a.algo, outer_lr=a.outer_lr, outer_momentum=a.outer_momentum,
+        cfg = LocalSGDConfig(lr=a.lr, H=a.H, algo=a.algo or "direct", outer_lr=a.outer_lr,
+                             outer_momentum=a.outer_momentum,
                              comm_dtype=torch.bfloat16 if cuda else torch.float32)
         tr = LocalSGDTrainer(model, cfg, group=group, membership=membership, device=device)
     else:
         from ..parallel.zero import ShardedConfig, ShardedDPTrainer
 
-        tr = ShardedDPTrainer(model, ShardedConfig(lr=a.lr, algo=a.algo), group=group, membership=membership,
-                              device=device)
+        tr = ShardedDPTrainer(model, ShardedConfig(lr=a.lr, algo=a.algo or "rs", replicas=a.replicas), group=group,
+                              membership=membership, device=device)
     if a.compression == "topk":
         from ..parallel.compression import TopKCompressor
 
@@ -202,13 +206,17 @@ def main(argv=None):
         step += 1
         if a.ckpt_dir and a.ckpt_every and step % a.ckpt_every == 0 and (
                 a.trainer == "sharded" or step % a.H == 0):
+            from ..parallel.peer_group import PeerFailure
             from ..utils.checkpoint import save_checkpoint
 
             g = tr.group
-            save_checkpoint(tr, a.ckpt_dir, step, peer_id=rank, is_writer=(g is None or g.rank == 0),
-                            members=(g.members if g is not None else [rank]),
-                            generation=(membership.gen if membership else 0), model_config=mcfg,
-                            barrier=(g.barrier if g is not None else None))
+            try:
+                save_checkpoint(tr, a.ckpt_dir, step, peer_id=rank, is_writer=(g is None or g.rank == 0),
+                                members=(g.members if g is not None else [rank]),
+                                generation=(membership.gen if membership else 0), model_config=mcfg,
+                                barrier=(g.barrier if g is not None else None))
+            except PeerFailure as e:  # a peer died mid-checkpoint: skip it, the next round regroups
+                print(f"[peer {rank}] checkpoint at step {step} skipped: {e}", flush=True)
         if step % a.log_every == 0 or step == a.steps:
             if cuda:
                 torch.cuda.synchronize()

@@ -8,4 +8,5 @@ from .linear import linear, native_linear_ok, wgrad  # noqa: F401
 from .loss import cross_entropy  # noqa: F401
 from .norm import add_layernorm, add_rmsnorm, layernorm, rmsnorm  # noqa: F401
 from .rope import rope_qkv  # noqa: F401
-from .optim import adamw_step, axpy_bf16, f32_to_bf16, lsgd_apply, lsgd_delta, new_ostate  # noqa: F401
+from .optim import (adamw_step, axpy_bf16, f32_to_bf16, lsgd_apply, lsgd_delta, new_ostate,  # noqa: F401
+                    reduce_bcast_bf16)

@@ -85,3 +85,16 @@ def axpy_bf16(src, acc, scale=1.0):
         native().axpy_bf16(src, acc, scale)
     else:
         acc.copy_((acc.float() + scale * src.float()).to(acc.dtype))
+
+
+def reduce_bcast_bf16(inp, out, mine, P: int):
+    """Direct all-reduce middle step: sum the P rows of `inp`; write the sum to every row of
+    `out` (may alias `inp`: each element is read before it is written) and to `mine`."""
+    if use_native(inp):
+        native().reduce_bcast_bf16(inp, out, mine, P)
+        return
+    red = inp.view(P, -1).float().sum(0).to(inp.dtype)
+    if out is not None:
+        out.view(P, -1).copy_(red.unsqueeze(0).expand(P, -1))
+    if mine is not None:
+        mine.copy_(red)

@@ -11,6 +11,14 @@
                   one xGMI link at full rate and the schedule re-forms trivially over any live
                   set (non-power-of-two sets fold the extra peers in first).
 * ``ring``      — classic 2(P-1)-step ring over pairwise exchanges.
+* ``direct``    — one-shot reduce-scatter + all-gather over the full xGMI mesh: ONE all-to-all
+                  in which every peer sends shard j of its buffer to peer j (P-1 links at once),
+                  a fused HIP reduce that sums the P received copies of its own shard and writes
+                  the sum once per destination, and ONE all-to-all that returns the reduced
+                  shards. Each peer moves 2(P-1)/P of the buffer, spread over its P-1 = 7 links
+                  concurrently: ~2·(S/8)/153 GB/s ≈ 0.4 ms for GPT-2-small's 248 MB of bf16
+                  pseudo-gradient, against ~2.8 ms for a single ring on one link.
+                  Works for any P (no power-of-two folding).
 
 The reductions of the hand-written algorithms run in a HIP kernel (``axpy_bf16``) for bf16
 GPU buffers. All functions SUM in place; the caller applies the 1/P scale (fused into the
@@ -25,7 +33,7 @@ import torch
 from .. import ops
 from .peer_group import PeerGroup
 
-ALGOS = ("rccl", "rs_ag", "butterfly", "ring")
+ALGOS = ("rccl", "rs_ag", "butterfly", "ring", "direct")
 
 
 def _add_(acc: torch.Tensor, src: torch.Tensor):
@@ -46,6 +54,8 @@ def allreduce_sum_(t: torch.Tensor, group: PeerGroup, algo: str = "rccl") -> tor
         return _butterfly(t, group)
     if algo == "ring":
         return _ring(t, group)
+    if algo == "direct":
+        return _direct(t, group)
     raise ValueError(f"unknown all-reduce algorithm {algo!r}; choose from {ALGOS}")
 
 
@@ -54,11 +64,22 @@ def _pad_len(n: int, parts: int, align: int = 64) -> int:
     return (n + q - 1) // q * q
 
 
+def _padded(t, L):
+    """t itself when it already has length L (flat buffers are padded for P | 840), else a
+    zero-padded copy."""
+    n = t.numel()
+    if L == n:
+        return t
+    buf = t.new_zeros(L)
+    buf[:n].copy_(t)
+    return buf
+
+
 def _rs_ag(t, group):
     P = group.size
     n = t.numel()
     L = _pad_len(n, P)
-    buf = t if L == n else torch.cat([t, t.new_zeros(L - n)])
+    buf = _padded(t, L)
     shard = buf.new_empty(L // P)
     group.reduce_scatter_(shard, buf)
     group.all_gather_(buf, shard)
@@ -95,7 +116,7 @@ def _butterfly(t, group):
         _add_(t, tmp)
     # --- recursive halving reduce-scatter among the p2 core peers
     L = _pad_len(n, p2)
-    buf = t if L == n else torch.cat([t, t.new_zeros(L - n)])
+    buf = _padded(t, L)
     lo, hi = 0, L
     dist_ = p2 // 2
     segs = []
@@ -135,7 +156,7 @@ def _ring(t, group):
     P, r = group.size, group.rank
     n = t.numel()
     L = _pad_len(n, P)
-    buf = t if L == n else torch.cat([t, t.new_zeros(L - n)])
+    buf = _padded(t, L)
     cs = L // P
     chunks = [buf[i * cs : (i + 1) * cs] for i in range(P)]
     right, left = (r + 1) % P, (r - 1) % P
@@ -163,6 +184,29 @@ def _ring(t, group):
         ri = (r - s) % P
         step(chunks[si].contiguous(), recv, tag=11)
         chunks[ri].copy_(recv)
+    if buf is not t:
+        t.copy_(buf[:n])
+    return t
+
+
+def _direct(t, group):
+    P, r = group.size, group.rank
+    n = t.numel()
+    L = _pad_len(n, P, 8 if t.dtype == torch.bfloat16 else 1)
+    buf = _padded(t, L)
+    m = L // P
+    split = [m] * P
+    recv = torch.empty_like(buf)  # [P, m]: row j = peer j's copy of MY shard
+    group.alltoall_(recv, buf, split, split)
+    send = recv  # reused: row j = the reduced shard, sent back to peer j
+    mine = buf[r * m : (r + 1) * m]
+    if buf.is_cuda and buf.dtype == torch.bfloat16:
+        ops.reduce_bcast_bf16(recv, send, mine, P)
+    else:
+        red = recv.view(P, m).sum(0, dtype=torch.float32 if buf.dtype != torch.float64 else None).to(buf.dtype)
+        mine.copy_(red)
+        send = red.unsqueeze(0).expand(P, m).contiguous().view(-1)
+    group.alltoall_(buf, send, split, split)
     if buf is not t:
         t.copy_(buf[:n])
     return t

@@ -53,8 +53,25 @@ class TopKCompressor:
         _, i = torch.topk(self.e.abs(), self.k, sorted=False)
         self.idx.copy_(i.to(torch.int32))
         self.val.copy_(self.e[i].to(self.val.dtype))
-        self.e[i] = 0.0
+        self.e[i] = self.e[i] - self.val.float()  # wire-dtype rounding residual stays in e
         return self.idx, self.val
+
+    # ------------------------------------------------------------------ state
+    def snapshot(self) -> dict:
+        """Pre-round state for an elastic round that may be aborted and redone."""
+        return {"e": self.e.clone()}
+
+    def restore(self, snap: dict):
+        # fresh tensors: an abandoned (gloo) op of the aborted round may still hold the old ones
+        self.e = snap["e"]
+        self.idx = torch.zeros_like(self.idx)
+        self.val = torch.zeros_like(self.val)
+
+    def state_dict(self) -> dict:
+        return {"ef": self.e}
+
+    def load_state_dict(self, d: dict):
+        self.e.copy_(d["ef"].to(self.e.device))
 
     def allreduce_mean(self, g: torch.Tensor, group) -> torch.Tensor:
         idx, val = self.compress(g)
@@ -203,6 +220,26 @@ class PowerSGDCompressor:
             seg.zero_()
         self.bytes_sent += 4 * (self.P.numel() + self.Q.numel() + sum(b - a for a, b in self.dense_ranges))
         return self.out
+
+    # ------------------------------------------------------------------ state
+    def snapshot(self) -> dict:
+        """Pre-round state for an elastic round that may be aborted and redone."""
+        return {"e": self.e.clone(), "P": self.P.clone(), "Q": self.Q.clone(), "lazy": self._lazy_pending}
+
+    def restore(self, snap: dict):
+        # fresh tensors: an abandoned (gloo) op of the aborted round may still hold the old ones
+        self.e, self.P, self.Q = snap["e"], snap["P"], snap["Q"]
+        self._lazy_pending = snap["lazy"]
+        self.out = torch.zeros_like(self.out)
+
+    def state_dict(self) -> dict:
+        """Error feedback (materialised: the pending lazy P Q^T subtracted) and the warm-start Q."""
+        return {"ef": self.ef(), "Q": self.Q}
+
+    def load_state_dict(self, d: dict):
+        self.e.copy_(d["ef"].to(self.e.device))
+        self.Q.copy_(d["Q"].to(self.Q.device))
+        self._lazy_pending = False
 
     def _approx_sub(self, e):
         for i in range(len(self.mats)):

@@ -1,36 +1,70 @@
-"""Elastic membership for the training job: heartbeats, leases, generations, (re)join.
+"""Elastic membership for the training job: heartbeats, leases, agreed rounds, mid-collective
+abort, generations, (re)join.
 
-Reference behaviour generalised: the reference coordinator tracks
-its volunteer pool through explicit ``join``/``end`` verbs only (server.py:104-154) and never
-notices a crashed client. Here every peer
+Reference behaviour generalised: the reference coordinator tracks its
+volunteer pool through explicit ``join``/``end`` verbs only (server.py:104-154), never notices
+a crashed client, and its dispatcher blocks forever in a send to a dead one (server.py:89).
+Here every peer
 
-* heartbeats a counter in the rendezvous store (``hb/<pid>``) from a background thread;
-* at each averaging round posts an arrival key and waits for the other members;
-* a member that has not arrived and whose heartbeat counter has not moved for ``lease_s``
-  seconds is declared dead; a member that announced ``leave`` is dropped immediately;
-* the survivors agree on the next generation's member list through ONE ``compare_set``
-  (first proposal wins, everyone adopts it), then build a fresh ``PeerGroup`` for it —
-  no collective is ever issued to a dead peer, so RCCL never hangs on one;
-* a new or returning peer registers under ``join/<seq>`` and is admitted at the next round;
-  the new generation's rank 0 then broadcasts the averaged model to it.
+* heartbeats a counter in the rendezvous store (``hb/<pid>``) from a background thread, which
+  is also the **collective watchdog**: while this peer is inside a guarded collective it
+  watches the other members' heartbeats and the generation's abort key; a member silent for
+  ``lease_s`` (crashed, SIGSTOPped, partitioned) makes it post ``abort/<gen>`` and abort its
+  communicator (RCCL: ``ncclCommAbort``), which unblocks the collective on every survivor;
+* runs each averaging round as: arrive -> ONE agreed outcome -> guarded collectives -> ONE
+  agreed verdict. The outcome of round k of generation g is a single ``compare_set`` on
+  ``out/<g>/<k>`` (``same`` or ``next:<members>|<newcomers>|<joins>``) that every peer follows,
+  so two peers can never disagree about whether the group changed (a joiner registering
+  mid-round or a lease expiring on one peer only). The verdict (``verdict/<g>/<tag>``) is
+  ``commit`` once every member reported success, or ``abort``; results are applied only on
+  ``commit``, so a round that some peers finished and others did not is redone by all;
+* recovers from an aborted generation with a recovery round (``out/<g>/R``): the survivors
+  (members that arrive; silent ones are dropped by lease) plus pending joiners form g+1;
+  the trainer restores its pre-round state and redoes the round on the new group;
+* a member that arrives after it was voted out (it was stopped, or just slow) finds itself
+  outside the next generation and rejoins transparently as a newcomer;
+* a new or returning peer registers under ``join/<seq>`` and is admitted at the next round's
+  outcome; newcomers (and any member that has not yet completed a committed round since it
+  joined) receive the model inside the admission round.
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
+from contextlib import contextmanager
 
-from .peer_group import PeerGroup
+from .peer_group import PeerFailure, PeerGroup
 
 _P = "vcx/el/"
+_DEBUG = bool(os.environ.get("VCX_ELASTIC_DEBUG"))
+
+
+def _dbg(pid, msg):
+    if _DEBUG:
+        print(f"[elastic {pid} {time.time() % 1000:8.3f}] {msg}", flush=True)
 
 
 def _s(v) -> str:
     return v.decode() if isinstance(v, (bytes, bytearray)) else str(v)
 
 
+def _csv(xs) -> str:
+    return ",".join(str(int(x)) for x in xs)
+
+
+def _ints(s: str) -> list[int]:
+    return [int(x) for x in s.split(",") if x]
+
+
+def _parse_gen(rec: str):
+    members, newcomers, njoin = rec.split("|")
+    return _ints(members), _ints(newcomers), int(njoin)
+
+
 class ElasticMembership:
     def __init__(self, store, peer_id: int, *, backend: str = "gloo", device=None, lease_s: float = 3.0,
-                 heartbeat_s: float = 0.2, arrive_timeout_s: float = 600.0, pg_timeout_s: float = 300.0,
+                 heartbeat_s: float = 0.2, arrive_timeout_s: float = 600.0, pg_timeout_s: float | None = None,
                  poll_s: float = 0.002):
         self.store = store
         self.pid = int(peer_id)
@@ -39,7 +73,8 @@ class ElasticMembership:
         self.lease_s = lease_s
         self.heartbeat_s = heartbeat_s
         self.arrive_timeout_s = arrive_timeout_s
-        self.pg_timeout_s = pg_timeout_s
+        # a gloo op blocked on a stopped peer is only freed by this timeout (gloo cannot cancel)
+        self.pg_timeout_s = pg_timeout_s if pg_timeout_s is not None else max(60.0, 30.0 * lease_s)
         self.poll_s = poll_s
         self.gen = -1
         self.members: list[int] = []
@@ -48,22 +83,39 @@ class ElasticMembership:
         self.group: PeerGroup | None = None
         self.round = 0
         self.joins_seen = 0
+        self.has_model = True
+        self.fault_hook = None  # passed to every generation's PeerGroup (fault-injection tests)
+        self.failures = 0
+        self.events: list[dict] = []  # membership change log (for metrics / tests)
         self._hb_stop = threading.Event()
         self._hb_thread = None
-        self.events: list[dict] = []  # membership change log (for metrics / tests)
+        self._lock = threading.RLock()
+        self._armed = False
+        self._abort = threading.Event()
+        self._abort_reason = ""
+        self._watch_seen: dict[int, tuple[int, float]] = {}
+        if backend == "nccl":
+            # abortable (non-blocking) RCCL communicator init for every generation's group
+            os.environ.setdefault("TORCH_NCCL_USE_COMM_NONBLOCKING", "1")
 
-    # ------------------------------------------------------------------ heartbeat
+    # ------------------------------------------------------------------ heartbeat + watchdog
     def start_heartbeat(self):
         if self._hb_thread is not None:
             return
+        self._hb_stop.clear()
 
         def loop():
             key = f"{_P}hb/{self.pid}"
             while not self._hb_stop.wait(self.heartbeat_s):
                 try:
                     self.store.add(key, 1)
-                except Exception:
+                except Exception:  # noqa: BLE001 — the store is gone: nothing left to do
                     return
+                if self._armed:
+                    try:
+                        self._watch()
+                    except Exception as e:  # noqa: BLE001
+                        self._trip(f"watchdog error: {e!r}")
 
         self.store.add(f"{_P}hb/{self.pid}", 1)
         self._hb_thread = threading.Thread(target=loop, name=f"vcx-hb-{self.pid}", daemon=True)
@@ -75,29 +127,81 @@ class ElasticMembership:
             self._hb_thread.join(timeout=2)
         self._hb_thread = None
 
-    # ------------------------------------------------------------------ bootstrap
+    def _watch(self):
+        """One watchdog tick while a guarded collective is in flight."""
+        if self._abort.is_set():
+            return
+        g = self.gen
+        ak = f"{_P}abort/{g}"
+        if self.store.check([ak]):
+            self._trip(_s(self.store.get(ak)))
+            return
+        now = time.time()
+        for m in list(self.members):
+            if m == self.pid:
+                continue
+            hb = self._hb(m)
+            last = self._watch_seen.get(m)
+            if last is None or hb != last[0]:
+                self._watch_seen[m] = (hb, now)
+            elif now - last[1] > self.lease_s:
+                self.declare_abort(f"peer {m} silent for {now - last[1]:.2f}s inside a collective of gen {g}")
+                return
+
+    def declare_abort(self, reason: str):
+        """Abort the current generation for everyone: post the abort key, trip locally."""
+        try:
+            self.store.compare_set(f"{_P}abort/{self.gen}", "", reason)
+        except Exception:  # noqa: BLE001
+            pass
+        self._trip(reason)
+
+    def _trip(self, reason: str):
+        with self._lock:
+            if self._abort.is_set():
+                return
+            self._abort_reason = reason
+            self._abort.set()
+            grp = self.group
+        self.events.append({"event": "abort", "gen": self.gen, "reason": reason, "t": time.time()})
+        _dbg(self.pid, f"trip gen {self.gen}: {reason}")
+        if grp is not None:
+            grp.abort()  # RCCL: ncclCommAbort — kernels blocked on the dead peer exit
+
+    def tripped(self) -> bool:
+        return self._abort.is_set()
+
+    def abort_reason(self) -> str:
+        return self._abort_reason
+
+    # ------------------------------------------------------------------ bootstrap / join / leave
     def bootstrap(self, members: list[int]):
         """Generation 0 with a known member list (e.g. all torchrun ranks)."""
         members = sorted(int(m) for m in members)
-        self.store.compare_set(f"{_P}gen/0/members", "", ",".join(map(str, members)))
-        self.store.compare_set(f"{_P}gen/0/joins", "", "0")
-        self._adopt(0, members)
+        rec = _s(self.store.compare_set(f"{_P}gen/0", "", f"{_csv(members)}||0"))
+        m0, nc0, nj0 = _parse_gen(rec)
+        self._adopt(0, m0, nc0, nj0)
         self.start_heartbeat()
         return self.group
 
     def join(self, timeout_s: float = 600.0):
         """Ask to be admitted; blocks until a generation that contains this peer forms."""
         self.start_heartbeat()
-        seq = self.store.add(f"{_P}njoin", 1)
+        try:
+            self.store.delete_key(f"{_P}leave/{self.pid}")
+        except Exception:  # noqa: BLE001
+            pass
+        self.has_model = False
+        seq = int(self.store.add(f"{_P}njoin", 1))
         self.store.set(f"{_P}join/{seq}", str(self.pid))
+        g = self._latest_gen(max(self.gen, 0))
         t0 = time.time()
-        g = max(self._latest_gen(), 0)
         while time.time() - t0 < timeout_s:
-            key = f"{_P}gen/{g + 1}/members"
+            key = f"{_P}gen/{g + 1}"
             if self.store.check([key]):
-                members = [int(x) for x in _s(self.store.get(key)).split(",") if x]
-                if self.pid in members:
-                    self._adopt(g + 1, members)
+                members, newcomers, njoin = _parse_gen(_s(self.store.get(key)))
+                if self.pid in members and njoin >= seq:
+                    self._adopt(g + 1, members, newcomers, njoin)
                     self.events.append({"event": "joined", "gen": self.gen, "members": members})
                     return self.group
                 g += 1
@@ -107,36 +211,117 @@ class ElasticMembership:
 
     def leave(self):
         """Graceful leave: survivors drop this peer at their next round without a lease wait."""
-        self.store.set(f"{_P}leave/{self.pid}", "1")
+        self.store.set(f"{_P}leave/{self.pid}", str(self.gen))
         self.stop_heartbeat()
-        if self.group is not None:
-            self.group.shutdown()
-        self.group = None
+        self._drop_group()
 
     # ------------------------------------------------------------------ rounds
     def sync_round(self):
-        """Barrier of the current generation. Returns (group, changed, newcomers).
-        If this peer was voted out (arrived too late), it rejoins transparently."""
+        """Start the next averaging round of the current generation. Returns
+        (group, changed, newcomers); if this peer was voted out it rejoins transparently."""
+        if self._abort.is_set() or self.store.check([f"{_P}abort/{self.gen}"]):
+            return self.recover()
         self.round += 1
-        k = self.round
+        return self._round(str(self.round), recovery=False)
+
+    def recover(self):
+        """After a PeerFailure: leave the aborted generation and form the next one from the
+        members that arrive (silent ones are dropped by lease) plus pending joiners."""
         g = self.gen
-        self.store.set(f"{_P}arrive/{g}/{k}/{self.pid}", "1")
-        missing = [m for m in self.members if m != self.pid]
-        hb_seen = {m: (self._hb(m), time.time()) for m in missing}
-        dead, left = set(), set()
-        t0 = time.time()
-        nkey = f"{_P}gen/{g + 1}/members"
+        self.failures += 1
+        try:
+            self.store.compare_set(f"{_P}abort/{g}", "", f"recovery requested by peer {self.pid}")
+        except Exception:  # noqa: BLE001
+            pass
+        self._trip(f"recovery of gen {g}")
+        return self._round("R", recovery=True)
+
+    @contextmanager
+    def guard(self, phase: str = ""):
+        """Arm the watchdog around the collectives of one round, then agree on the verdict.
+        Raises PeerFailure (after voting abort) if any member failed; the caller restores its
+        pre-round state and calls ``recover()``. Nothing may be applied before this exits."""
+        grp = self.group
+        if grp is None or grp.size == 1:
+            yield
+            if grp is not None:
+                self.has_model = True
+            return
+        tag = f"{self.round}{phase}"
+        with self._lock:
+            if self._abort.is_set():
+                raise PeerFailure(f"gen {self.gen}: aborted ({self._abort_reason})")
+            self._watch_seen = {}
+            self._armed = True
+        try:
+            _dbg(self.pid, f"guard {self.gen}/{tag}: connect")
+            grp.connect()
+            _dbg(self.pid, f"guard {self.gen}/{tag}: body")
+            yield
+            _dbg(self.pid, f"guard {self.gen}/{tag}: commit")
+            self._commit(tag)
+        except PeerFailure:
+            self._vote(tag, "abort")
+            raise
+        finally:
+            self._armed = False
+
+    def _vote(self, tag, v):
+        try:
+            return _s(self.store.compare_set(f"{_P}verdict/{self.gen}/{tag}", "", v))
+        except Exception:  # noqa: BLE001
+            return "abort"
+
+    def _commit(self, tag):
+        g, P = self.gen, len(self.members)
+        okk, vk = f"{_P}ok/{g}/{tag}", f"{_P}verdict/{g}/{tag}"
+        self.store.add(okk, 1)
         while True:
-            if self.store.check([nkey]):  # someone already decided the next generation
-                return self._follow(g + 1, k)
-            still = []
-            for m in missing:
-                if m in dead or m in left:
+            if self.store.check([vk]):
+                v = _s(self.store.get(vk))
+                break
+            if int(self.store.add(okk, 0)) >= P:
+                v = self._vote(tag, "commit")
+                break
+            if self._abort.is_set():
+                v = self._vote(tag, "abort")
+                break
+            time.sleep(self.poll_s)
+        _dbg(self.pid, f"verdict {g}/{tag}: {v}")
+        if v != "commit":
+            self._trip(f"round {g}/{tag} voted abort")
+            raise PeerFailure(f"gen {g}: round {tag} aborted ({self._abort_reason})")
+        self.has_model = True
+
+    def _round(self, k: str, recovery: bool):
+        g = self.gen
+        self.store.set(f"{_P}arr/{g}/{k}/{self.pid}", "1" if self.has_model else "0")
+        okey = f"{_P}out/{g}/{k}"
+        others = [m for m in self.members if m != self.pid]
+        now = time.time()
+        hb_seen = {m: (self._hb(m), now) for m in others}
+        arrived = {self.pid: self.has_model}
+        dead, left = set(), set()
+        t0 = now
+        nj_cached, joiners = -1, []
+        while True:
+            if self.store.check([okey]):
+                return self._follow(okey)
+            if not recovery and self.store.check([f"{_P}abort/{g}"]):
+                return self.recover()
+            njoin = self._njoin()
+            if njoin != nj_cached:
+                joiners, nj_cached = self._pending_joiners(njoin), njoin
+            missing = []
+            for m in others:
+                if m in arrived or m in dead or m in left:
                     continue
-                if self.store.check([f"{_P}arrive/{g}/{k}/{m}"]):
+                ak = f"{_P}arr/{g}/{k}/{m}"
+                if self.store.check([ak]):
+                    arrived[m] = _s(self.store.get(ak)) == "1"
                     continue
-                if self.store.check([f"{_P}leave/{m}"]):
-                    left.add(m)
+                if m in joiners or self.store.check([f"{_P}leave/{m}"]):
+                    left.add(m)  # announced leave, or restarted and re-registered as a joiner
                     continue
                 hb = self._hb(m)
                 last, seen_at = hb_seen[m]
@@ -145,60 +330,74 @@ class ElasticMembership:
                 elif time.time() - seen_at > self.lease_s:
                     dead.add(m)
                     continue
-                still.append(m)
-            missing_now = still
-            njoin = self._njoin()
-            if not missing_now:
-                if not dead and not left and njoin <= self.joins_seen:
-                    return self.group, False, []
+                missing.append(m)
+            if not missing:
                 break
             if time.time() - t0 > self.arrive_timeout_s:
-                dead.update(missing_now)
+                dead.update(missing)
                 break
             time.sleep(self.poll_s)
-        # ---- propose the next generation: arrived members + pending joiners
-        survivors = [m for m in self.members if m not in dead and m not in left]
-        joiners = self._pending_joiners(njoin)
-        proposal = sorted(set(survivors) | set(joiners))
-        self.store.compare_set(f"{_P}gen/{g + 1}/joins", "", str(njoin))
-        self.store.compare_set(nkey, "", ",".join(map(str, proposal)))
-        return self._follow(g + 1, k)
+        if not recovery and not dead and not left and njoin <= self.joins_seen:
+            decision = "same"
+        else:
+            survivors = sorted(arrived)
+            new_ids = [j for j in joiners if j not in arrived]
+            members = sorted(set(survivors) | set(new_ids))
+            newcomers = sorted(set([m for m in survivors if not arrived[m]] + new_ids))
+            decision = f"next:{_csv(members)}|{_csv(newcomers)}|{njoin}"
+        won = _s(self.store.compare_set(okey, "", decision))
+        _dbg(self.pid, f"round {g}/{k}: proposed {decision!r} (dead={sorted(dead)} left={sorted(left)}), agreed {won!r}")
+        return self._follow(okey)
 
     # ------------------------------------------------------------------ internals
-    def _follow(self, g, k):
-        members = [int(x) for x in _s(self.store.get(f"{_P}gen/{g}/members")).split(",") if x]
-        old = set(self.members)
+    def _follow(self, okey):
+        v = _s(self.store.get(okey))
+        if v == "same":
+            return self.group, False, []
+        g = self.gen + 1
+        # every follower proposes the same record; the first write fixes generation g
+        rec = _s(self.store.compare_set(f"{_P}gen/{g}", "", v.split(":", 1)[1]))
+        members, newcomers, njoin = _parse_gen(rec)
+        old = list(self.members)
+        k = okey.rsplit("/", 1)[1]
         if self.pid not in members:
-            # voted out (late arrival): rejoin as a newcomer
-            self.events.append({"event": "evicted", "gen": g})
-            if self.group is not None:
-                self.group.shutdown()
-            self.group = None
+            # voted out (stopped, partitioned or late): rejoin as a newcomer
+            self.events.append({"event": "evicted", "gen": g, "round": k})
+            self._drop_group()
             self.gen = g
             self.join()
-            return self.group, True, [self.pid]
-        self._adopt(g, members)
-        newcomers = [m for m in members if m not in old]
+            return self.group, True, list(self.newcomers)
+        self._adopt(g, members, newcomers, njoin)
         self.events.append({"event": "regroup", "gen": g, "members": members, "round": k,
-                            "dropped": sorted(old - set(members)), "joined": newcomers})
+                            "dropped": sorted(set(old) - set(members)), "joined": newcomers,
+                            "t": time.time()})
         return self.group, True, newcomers
 
-    def _adopt(self, g, members):
-        if self.group is not None:
-            self.group.shutdown()
+    def _drop_group(self):
+        with self._lock:
+            grp, self.group = self.group, None
+            self._armed = False
+        if grp is not None:
+            grp.shutdown()
+
+    def _adopt(self, g, members, newcomers, njoin):
+        self._drop_group()
+        with self._lock:
+            self._abort.clear()
+            self._abort_reason = ""
+        self.prev_members = list(self.members) if self.gen >= 0 else list(members)
         self.gen = g
         self.members = list(members)
-        pk = f"{_P}gen/{g - 1}/members"
-        if g > 0 and self.store.check([pk]):
-            self.prev_members = [int(x) for x in _s(self.store.get(pk)).split(",") if x]
-        else:
-            self.prev_members = list(members)
-        self.newcomers = [m for m in members if m not in self.prev_members]
+        self.newcomers = list(newcomers)
         self.round = 0
-        js = f"{_P}gen/{g}/joins"
-        self.joins_seen = int(_s(self.store.get(js))) if self.store.check([js]) else self._njoin()
-        self.group = PeerGroup(self.store, members.index(self.pid), len(members), self.backend, generation=g,
-                               members=members, timeout_s=self.pg_timeout_s, device=self.device)
+        self.joins_seen = max(self.joins_seen, int(njoin))
+        if self.pid in newcomers:
+            self.has_model = False
+        grp = PeerGroup(self.store, members.index(self.pid), len(members), self.backend, generation=g,
+                        members=members, timeout_s=self.pg_timeout_s, device=self.device, watch=self)
+        grp.fault_hook = self.fault_hook
+        with self._lock:
+            self.group = grp
 
     def _hb(self, m) -> int:
         return int(self.store.add(f"{_P}hb/{m}", 0))
@@ -211,11 +410,13 @@ class ElasticMembership:
         for seq in range(self.joins_seen + 1, njoin + 1):
             key = f"{_P}join/{seq}"
             if self.store.check([key]):
-                out.append(int(_s(self.store.get(key))))
+                pid = int(_s(self.store.get(key)))
+                if pid not in out:
+                    out.append(pid)
         return out
 
-    def _latest_gen(self) -> int:
-        g = 0
-        while self.store.check([f"{_P}gen/{g + 1}/members"]):
+    def _latest_gen(self, start: int = 0) -> int:
+        g = start
+        while self.store.check([f"{_P}gen/{g + 1}"]):
             g += 1
-        return g if self.store.check([f"{_P}gen/{g}/members"]) else -1
+        return g

@@ -91,3 +91,51 @@ class FlatParams:
         lo = min(rank * per, self.numel)
         hi = min(lo + per, self.numel)
         return lo, hi
+
+
+class FlatBuffers:
+    """Floating-point module buffers (BatchNorm running mean/var) gathered into one flat fp32
+    vector, so the trainers average them with ONE small collective per synchronisation, hand
+    them to newcomers and store them in checkpoints (BASELINE.json config 3, ResNet-50).
+    Integer buffers (``num_batches_tracked``) are left alone."""
+
+    def __init__(self, module: torch.nn.Module):
+        self.entries = []  # (owner module, buffer name, qualified name, numel, shape)
+        for qn, b in module.named_buffers():
+            if b is None or not b.dtype.is_floating_point:
+                continue
+            mod_name, _, bname = qn.rpartition(".")
+            owner = module.get_submodule(mod_name) if mod_name else module
+            self.entries.append((owner, bname, qn, b.numel(), tuple(b.shape)))
+        self.numel = sum(e[3] for e in self.entries)
+
+    def __bool__(self):
+        return self.numel > 0
+
+    def as_fp32(self) -> torch.Tensor:
+        """All buffers in one fp32 vector (a copy), in entry order."""
+        if not self.entries:
+            return torch.zeros(0)
+        return torch.cat([owner._buffers[bn].detach().float().reshape(-1) for owner, bn, *_ in self.entries])
+
+    def load_fp32(self, vec: torch.Tensor):
+        pos = 0
+        for owner, bn, qn, n, shape in self.entries:
+            b = owner._buffers[bn]
+            b.copy_(vec[pos : pos + n].view(shape).to(device=b.device, dtype=b.dtype))
+            pos += n
+
+    def names(self):
+        return [qn for _, _, qn, *_ in self.entries]
+
+    def average_(self, group):
+        """Mean over the group's peers (collective on a scratch copy: an aborted op of an
+        elastic round can never write into the live buffers)."""
+        if not self.entries or group is None or group.size == 1:
+            return
+        v = self.as_fp32()
+        dev = group.device if group.backend == "nccl" else "cpu"
+        v = v.to(dev)
+        group.allreduce_(v)
+        v.div_(group.size)
+        self.load_fp32(v)

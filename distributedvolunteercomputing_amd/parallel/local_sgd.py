@@ -23,7 +23,8 @@ import torch
 from .. import ops
 from ..utils.trace import NULL_TRACER
 from .collectives import allreduce_sum_
-from .flat_params import FlatParams
+from .flat_params import FlatBuffers, FlatParams
+from .peer_group import PeerFailure
 
 
 @dataclass
@@ -34,7 +35,7 @@ class LocalSGDConfig:
     weight_decay: float = 0.1
     max_grad_norm: float = 1.0
     H: int = 4  # local steps between averaging rounds
-    algo: str = "rccl"  # rccl | rs_ag | butterfly | ring
+    algo: str = "direct"  # direct | rccl | rs_ag | butterfly | ring (parallel/collectives.py)
     outer_lr: float = 1.0
     outer_momentum: float = 0.0
     nesterov: bool = False
@@ -61,6 +62,7 @@ class LocalSGDTrainer:
         self.cfg = cfg
         self.device = device or next(model.parameters()).device
         self.flat = FlatParams(model, dtype=torch.bfloat16, device=self.device)
+        self.buffers = FlatBuffers(model)  # BN running stats: averaged at every sync
         n = self.flat.numel
         self.master = self.flat.param.float()
         self.m = torch.zeros(n, dtype=torch.float32, device=self.device)
@@ -76,6 +78,7 @@ class LocalSGDTrainer:
         self.t = 0
         self.sync_count = 0
         self.last_sync_ms = 0.0
+        self.failed_rounds = 0  # elastic rounds aborted mid-collective and redone
 
     # ------------------------------------------------------------------ per step
     def set_lr(self, lr: float):
@@ -145,53 +148,126 @@ class LocalSGDTrainer:
     # ------------------------------------------------------------------ averaging
     def sync(self):
         t0 = time.perf_counter()
-        newcomers = []
-        if self.membership is not None:
-            self.group, changed, newcomers = self.membership.sync_round()
-            if changed and newcomers:
-                self._admit_newcomers(newcomers)
-        self._average(newcomers)
+        if self.membership is None:
+            res = self._reduce(())
+            self._apply(res)
+            self.buffers.average_(self.group)
+        else:
+            self._sync_elastic()
         self.sync_count += 1
         self.last_sync_ms = (time.perf_counter() - t0) * 1e3
 
-    def _average(self, newcomers=()):
+    def _sync_elastic(self):
+        """One elastic averaging round: agreed outcome -> guarded admission + reduction ->
+        agreed verdict -> apply. A member dying inside the collectives aborts the round on
+        every survivor; they restore the pre-round state (anchor/master were never touched,
+        the pseudo-gradient is recomputed, the compressor state is rolled back) and redo the
+        round on the next generation."""
+        mem = self.membership
+        grp, _, newcomers = mem.sync_round()
+        while True:
+            self.group = grp
+            snap = self.compressor.snapshot() if (self.compressor is not None and grp.size > 1) else None
+            try:
+                with mem.guard():
+                    if newcomers:
+                        self._admit_newcomers(newcomers)
+                    res = self._reduce(newcomers)
+                    self.buffers.average_(grp)
+                self._apply(res)
+                return
+            except PeerFailure:
+                if snap is not None:
+                    self.compressor.restore(snap)
+                # an abandoned gloo op may still own the old pseudo-gradient buffer
+                self.delta = torch.zeros_like(self.delta)
+                self.failed_rounds += 1
+                grp, _, newcomers = mem.recover()
+
+    def _reduce(self, newcomers=()):
+        """Pseudo-gradient + collective. Returns what `_apply` needs; touches no model state."""
         g = self.group
-        if g is not None and g.size > 1:
-            ops.lsgd_delta(self.master, self.anchor, self.delta)
-            contributors = g.size - len(newcomers)  # newcomers hold delta == 0
-            if self.compressor is not None:
-                avg = self.compressor.allreduce_mean(self.delta, g)
-                scale = g.size / contributors
-            else:
-                allreduce_sum_(self.delta, g, self.cfg.algo)
-                avg, scale = self.delta, 1.0 / contributors
-            c = self.cfg
-            ops.lsgd_apply(avg, self.anchor, self.master, self.flat.param, self.outer_mom, outer_lr=c.outer_lr,
-                           mu=c.outer_momentum, nesterov=c.nesterov, avg_scale=scale)
-        else:
+        if g is None or g.size == 1:
+            return None
+        ops.lsgd_delta(self.master, self.anchor, self.delta)
+        contributors = max(1, g.size - len(newcomers))  # newcomers hold delta == 0
+        if self.compressor is not None:
+            avg = self.compressor.allreduce_mean(self.delta, g)
+            return avg, g.size / contributors
+        allreduce_sum_(self.delta, g, self.cfg.algo)
+        return self.delta, 1.0 / contributors
+
+    def _apply(self, res):
+        if res is None:
             self.anchor.copy_(self.master)
+            return
+        avg, scale = res
+        c = self.cfg
+        ops.lsgd_apply(avg, self.anchor, self.master, self.flat.param, self.outer_mom, outer_lr=c.outer_lr,
+                       mu=c.outer_momentum, nesterov=c.nesterov, avg_scale=scale)
+
+    def _average(self, newcomers=()):
+        self._apply(self._reduce(newcomers))
 
     def _admit_newcomers(self, newcomers):
-        """The new generation contains peers without the model: the first continuing member
-        broadcasts the anchor (identical on all continuing members); newcomers adopt it as
-        their weights. Continuing members keep their un-averaged local progress."""
+        """The generation contains peers without the model (joiners, or members whose earlier
+        admission was aborted): the first continuing member sends them the anchor (identical on
+        all continuing members), the outer momentum and the BN buffers, point-to-point, so a
+        failed transfer can never corrupt a continuing member. Newcomers receive into scratch
+        buffers and adopt the model only when the transfer completed."""
         g = self.group
         members = g.members
-        root = next(i for i, m in enumerate(members) if m not in newcomers)
-        g.broadcast_(self.anchor, root=root)
-        if self.outer_mom is not None:
-            g.broadcast_(self.outer_mom, root=root)
-        me = self.membership.pid if self.membership is not None else None
-        if me in newcomers:
+        cont = [i for i, m in enumerate(members) if m not in newcomers]
+        if not cont:
+            return  # nobody holds a model yet: everyone starts from its own (identical) init
+        root = cont[0]
+        new_ranks = [i for i, m in enumerate(members) if m in newcomers]
+        dev = self.anchor.device
+        if g.rank == root:
+            bufs = [self.anchor] + ([self.outer_mom] if self.outer_mom is not None else [])
+            if self.buffers:
+                bufs.append(self.buffers.as_fp32().to(dev))
+            for r in new_ranks:
+                for b in bufs:
+                    g.send(b, r, tag=7)
+        elif g.rank in new_ranks:
+            anchor = torch.empty_like(self.anchor)
+            g.recv(anchor, root, tag=7)
+            mom = None
+            if self.outer_mom is not None:
+                mom = torch.empty_like(self.outer_mom)
+                g.recv(mom, root, tag=7)
+            bv = None
+            if self.buffers:
+                bv = torch.empty(self.buffers.numel, dtype=torch.float32, device=dev)
+                g.recv(bv, root, tag=7)
+            self.anchor.copy_(anchor)
+            if mom is not None:
+                self.outer_mom.copy_(mom)
+            if bv is not None:
+                self.buffers.load_fp32(bv)
             self.master.copy_(self.anchor)
             ops.f32_to_bf16(self.anchor, self.flat.param)
 
     def join_running_job(self):
         """Called by a peer that was just admitted (``membership.join()``): receive the model
-        and take part in the round that admitted it."""
-        nc = self.membership.newcomers
-        self._admit_newcomers(nc)
-        self._average(nc)
+        and take part in the round that admitted it (retried on the next generation if a
+        member dies during it)."""
+        mem = self.membership
+        grp, newcomers = mem.group, mem.newcomers
+        while True:
+            self.group = grp
+            try:
+                with mem.guard():
+                    self._admit_newcomers(newcomers)
+                    res = self._reduce(newcomers)
+                    self.buffers.average_(grp)
+                self._apply(res)
+                return
+            except PeerFailure:
+                self.delta = torch.zeros_like(self.delta)
+                self.failed_rounds += 1
+                grp, _, newcomers = mem.recover()
 
     # ------------------------------------------------------------------ state
     def state_tensors(self):
@@ -199,15 +275,30 @@ class LocalSGDTrainer:
 
     def checkpoint_slice(self):
         """This peer's 1/P share of the (synchronised) state: call right after a sync round,
-        when master == anchor on every peer. Moments are per-peer; each peer contributes its
-        own slice of them."""
+        when master == anchor on every peer. Adam moments and the compressor's error feedback
+        are per-peer; the checkpoint stores their mean over the peers (one reduce-scatter each,
+        so every peer writes the averaged slice it owns) — a restore onto any peer count then
+        starts every peer from the same coherent moments, and from the mean unsent residual
+        (exactly what the next averaging round would have delivered)."""
         P = 1 if self.group is None else self.group.size
         r = 0 if self.group is None else self.group.rank
         lo, hi = self.flat.shard_bounds(r, P)
-        t = {"master": self.anchor[lo:hi], "m": self.m[lo:hi], "v": self.v[lo:hi]}
+        t = {"master": self.anchor[lo:hi], "m": mean_slice(self.group, self.m, lo, hi),
+             "v": mean_slice(self.group, self.v, lo, hi)}
         if self.outer_mom is not None:
-            t["outer_mom"] = self.outer_mom[lo:hi]
+            t["outer_mom"] = self.outer_mom[lo:hi]  # identical on every peer (updated from the average)
+        if self.compressor is not None:
+            t["ef"] = mean_slice(self.group, self.compressor.state_dict()["ef"], lo, hi)
         return lo, hi, t
+
+    def checkpoint_global(self) -> dict:
+        """Tensors written once (by the writer peer) next to the parameters."""
+        out = {}
+        if self.buffers:
+            out["buffers"] = self.buffers.as_fp32()
+        if self.compressor is not None and "Q" in self.compressor.state_dict():
+            out["psgd_Q"] = self.compressor.state_dict()["Q"]  # identical on every peer (all-reduced)
+        return out
 
     def restore(self, reader):
         reader.check_layout(self.flat)
@@ -222,4 +313,36 @@ class LocalSGDTrainer:
         _, ost = reader.params()
         self.ostate.copy_(ost.to(dev))
         ops.f32_to_bf16(self.master, self.flat.param)
+        restore_extras(self, reader)
         self.t = reader.step
+
+
+def mean_slice(group, buf, lo, hi):
+    """[lo, hi) of the peers' mean of `buf` (this peer's shard): one reduce-scatter."""
+    if group is None or group.size == 1:
+        return buf[lo:hi]
+    P = group.size
+    if buf.numel() % P == 0 and hi - lo == buf.numel() // P:
+        out = torch.empty(hi - lo, dtype=buf.dtype, device=buf.device)
+        group.reduce_scatter_(out, buf)
+    else:
+        tmp = buf.clone()
+        group.allreduce_(tmp)
+        out = tmp[lo:hi]
+    return out.div_(P)
+
+
+def restore_extras(trainer, reader):
+    """BN buffers and compressor state (error feedback, PowerSGD's Q) if the checkpoint has them."""
+    bufs = reader.global_tensor("buffers")
+    if bufs is not None and trainer.buffers:
+        trainer.buffers.load_fp32(bufs)
+    comp = trainer.compressor
+    if comp is not None and reader.has_key("ef"):
+        d = {"ef": reader.read_range("ef", 0, trainer.flat.numel)}
+        q = reader.global_tensor("psgd_Q")
+        if q is not None:
+            d["Q"] = q
+        elif "Q" in comp.state_dict():
+            d["Q"] = comp.state_dict()["Q"]
+        comp.load_state_dict(d)

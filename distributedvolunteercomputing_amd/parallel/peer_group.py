@@ -1,4 +1,5 @@
-"""A group of volunteer peers that can be rebuilt on membership change.
+"""A group of volunteer peers that can be rebuilt on membership change — and abandoned
+mid-collective when one of them dies.
 
 Each generation of the training membership gets its OWN raw c10d process group, created
 directly from a (prefixed) store with ``ProcessGroupNCCL`` (RCCL on ROCm, over xGMI) or
@@ -6,16 +7,37 @@ directly from a (prefixed) store with ``ProcessGroupNCCL`` (RCCL on ROCm, over x
 every member of the *previous* generation to take part, so survivors can re-form a group
 after a peer has died (SURVEY.md §5.3 "(N) dropout-tolerant averaging").
 
+Guarded collectives. When a ``watch`` (the elastic membership) is attached, no collective is
+waited on blindly: the issuing thread polls ``work.is_completed()`` and the watch's abort flag.
+The watch's heartbeat thread trips that flag when a member's lease expires while a collective
+is in flight, or when another member posted an abort for this generation; the waiting peer
+then aborts its communicator (``ProcessGroupNCCL.abort()`` = ``ncclCommAbort``: the RCCL
+kernels spinning on the dead peer's xGMI link exit) and raises ``PeerFailure``. Gloo cannot
+cancel an in-flight op (its ``abort`` returns but the pending pair read stays), so an aborted
+gloo group is parked in ``_GRAVEYARD`` (never destroyed: its destructor would join the blocked
+worker thread) and its buffers are abandoned by the caller.
+
 Reference analog: the coordinator's ``clients`` pool mutated by join/end verbs
-(/root/reference/server.py:104-154) — here the pool is a generation-numbered member list.
+(/root/reference/server.py:104-154) — here the pool is a generation-numbered member list — and
+the blocking send to a dead volunteer that stalls the reference's dispatcher forever
+(/root/reference/server.py:89), which the guarded wait replaces.
 """
 from __future__ import annotations
 
 import datetime as _dt
 import os
+import threading
+import time
 
 import torch
 import torch.distributed as dist
+
+
+class PeerFailure(RuntimeError):
+    """A collective of this generation cannot complete: a member died, stopped or aborted."""
+
+
+_GRAVEYARD: list = []  # aborted gloo groups with possibly blocked ops (see module docstring)
 
 
 def _gloo_pg(store, rank, size, timeout):
@@ -27,28 +49,39 @@ def _gloo_pg(store, rank, size, timeout):
 
 
 def _nccl_pg(store, rank, size, timeout):
-    return dist.ProcessGroupNCCL(store, rank, size, timeout)
+    opts = dist.ProcessGroupNCCL.Options()
+    opts._timeout = timeout
+    return dist.ProcessGroupNCCL(store, rank, size, opts)
 
 
 class PeerGroup:
     """One generation of live peers: rank/size are positions in ``members``."""
 
     def __init__(self, store, rank: int, size: int, backend: str = "gloo", *, generation: int = 0,
-                 members=None, timeout_s: float = 300.0, device=None):
+                 members=None, timeout_s: float = 300.0, device=None, watch=None):
         self.generation = generation
         self.members = list(members) if members is not None else list(range(size))
         self.rank = rank
         self.size = size
         self.backend = backend
         self.device = device
+        self.watch = watch  # ElasticMembership (or None: plain blocking collectives)
+        self.aborted = False
+        self.fault_hook = None  # test hook: called inside every guarded collective (after issue)
+        self.poll_s = 2e-4
+        self._pending = None  # deferred gloo rendezvous (watched groups connect in connect())
         timeout = _dt.timedelta(seconds=timeout_s)
         prefixed = dist.PrefixStore(f"vcx/pg/{generation}", store)
+        self.pg = None
         if size == 1:
-            self.pg = None
+            pass
         elif backend == "nccl":
             self.pg = _nccl_pg(prefixed, rank, size, timeout)
         elif backend == "gloo":
-            self.pg = _gloo_pg(prefixed, rank, size, timeout)
+            if watch is None:
+                self.pg = _gloo_pg(prefixed, rank, size, timeout)
+            else:  # the full-mesh connect blocks until every member shows up: make it abortable
+                self._pending = (prefixed, rank, size, timeout)
         else:
             raise ValueError(f"unknown backend {backend!r}")
 
@@ -56,67 +89,193 @@ class PeerGroup:
     def from_default(cls, device=None) -> "PeerGroup":
         """Wrap torch.distributed's default process group (e.g. the torchrun world)."""
         self = cls.__new__(cls)
+        self._pending = None
         self.generation = 0
         self.size = dist.get_world_size()
         self.rank = dist.get_rank()
         self.members = list(range(self.size))
         self.backend = dist.get_backend()
         self.device = device
+        self.watch = None
+        self.aborted = False
+        self.fault_hook = None
+        self.poll_s = 2e-4
         self.pg = dist.distributed_c10d._get_default_group() if self.size > 1 else None
         return self
 
+    def connect(self):
+        """Create the RCCL communicator now, bound to this peer's GPU (every member calls this
+        right after adopting the generation, with the watchdog armed), instead of lazily inside
+        the first collective. With ``TORCH_NCCL_USE_COMM_NONBLOCKING=1`` (set by the elastic
+        membership) the init is non-blocking, so a member dying during it is aborted like any
+        collective. No-op for gloo (connected in the constructor)."""
+        if self._pending is not None:
+            self._connect_gloo()
+            return
+        if self.pg is None or self.backend != "nccl" or self.device is None:
+            return
+        dev = torch.device(self.device)
+        if dev.type == "cuda":
+            self._check()
+            self.pg.eager_connect_single_device(dev)
+
+    def _connect_gloo(self):
+        args, self._pending = self._pending, None
+        box = {}
+
+        def build():
+            try:
+                box["pg"] = _gloo_pg(*args)
+            except Exception as e:  # noqa: BLE001
+                box["err"] = e
+
+        th = threading.Thread(target=build, name=f"vcx-pg{self.generation}-connect", daemon=True)
+        th.start()
+        while th.is_alive():
+            if self.watch.tripped():
+                self.aborted = True
+                raise PeerFailure(f"gen {self.generation}: connect aborted ({self.watch.abort_reason()})")
+            th.join(0.01)
+        if "err" in box:
+            self.watch.declare_abort(f"gen {self.generation} connect failed on peer {self.watch.pid}: {box['err']}")
+            self.aborted = True
+            raise PeerFailure(f"gen {self.generation}: connect failed: {box['err']}")
+        self.pg = box["pg"]
+        if self.aborted:  # the watchdog aborted us while the rendezvous was finishing
+            pg, self.pg = self.pg, None
+            _GRAVEYARD.append(pg)
+            raise PeerFailure(f"gen {self.generation}: aborted during connect")
+
+    # ------------------------------------------------------------------ guarded wait
+    def _wait(self, work, op: str):
+        w = self.watch
+        if w is None:
+            work.wait()
+            return
+        if self.fault_hook is not None:
+            self.fault_hook(self, op)
+        if self.backend == "gloo" and op in ("send", "recv"):
+            # gloo point-to-point work reports completion only from inside wait() (and a wait
+            # with a timeout closes the pair), so the blocking wait runs on a helper thread that
+            # is abandoned if the generation aborts
+            box = {}
+
+            def waiter():
+                try:
+                    work.wait()
+                    box["ok"] = True
+                except Exception as e:  # noqa: BLE001
+                    box["err"] = e
+
+            th = threading.Thread(target=waiter, name=f"vcx-p2p-{op}", daemon=True)
+            th.start()
+            while th.is_alive():
+                if w.tripped():
+                    self.abort()
+                    raise PeerFailure(f"gen {self.generation}: {op} aborted ({w.abort_reason()})")
+                th.join(self.poll_s * 5)
+            if "err" in box:
+                e = box["err"]
+                w.declare_abort(f"{op} failed on peer {w.pid}: {type(e).__name__}: {str(e)[:120]}")
+                self.abort()
+                raise PeerFailure(f"gen {self.generation}: {op} failed: {e}") from e
+            return
+        t0 = time.perf_counter()
+        while not work.is_completed():
+            if w.tripped():
+                self.abort()
+                raise PeerFailure(f"gen {self.generation}: {op} aborted ({w.abort_reason()})")
+            # spin briefly (GPU collectives finish in ~ms), then yield the GIL to the watchdog
+            time.sleep(0 if time.perf_counter() - t0 < 2e-4 else self.poll_s)
+        try:
+            work.wait()
+        except Exception as e:  # noqa: BLE001 — gloo: "Connection closed by peer", NCCL: aborted comm
+            w.declare_abort(f"{op} failed on peer {w.pid}: {type(e).__name__}: {str(e)[:120]}")
+            self.abort()
+            raise PeerFailure(f"gen {self.generation}: {op} failed: {e}") from e
+
+    def _check(self):
+        if self._pending is not None:
+            self.connect()
+        if self.aborted or self.pg is None and self.size > 1:
+            raise PeerFailure(f"gen {self.generation}: group aborted or never connected")
+        if self.watch is not None and self.watch.tripped():
+            self.abort()
+            raise PeerFailure(f"gen {self.generation}: aborted ({self.watch.abort_reason()})")
+
+    def abort(self):
+        """Tear down this generation's communicator; safe to call from the watchdog thread."""
+        if self.aborted:
+            return
+        self.aborted = True
+        pg, self.pg = self.pg, None
+        if pg is None:
+            return
+        try:
+            pg.abort()  # RCCL: ncclCommAbort unblocks kernels waiting on a dead peer
+        except Exception:  # noqa: BLE001
+            pass
+        if self.backend != "nccl":
+            _GRAVEYARD.append(pg)
+
     # ------------------------------------------------------------------ collectives
     def allreduce_(self, t: torch.Tensor):
-        if self.pg is None:
+        if self.size == 1:
             return t
-        self.pg.allreduce([t]).wait()
+        self._check()
+        self._wait(self.pg.allreduce([t]), "allreduce")
         return t
 
     def broadcast_(self, t: torch.Tensor, root: int = 0):
-        if self.pg is None:
+        if self.size == 1:
             return t
+        self._check()
         opts = dist.BroadcastOptions()
         opts.rootRank = root
         opts.rootTensor = 0
-        self.pg.broadcast([t], opts).wait()
+        self._wait(self.pg.broadcast([t], opts), "broadcast")
         return t
 
     def reduce_scatter_(self, out: torch.Tensor, inp: torch.Tensor):
         """out (numel = inp.numel()/size) <- sum over peers of this peer's slice of inp."""
-        if self.pg is None:
+        if self.size == 1:
             out.copy_(inp)
             return out
+        self._check()
         if self.backend == "gloo":  # gloo lacks reduce_scatter_base: all-reduce then slice
             tmp = inp.clone()
-            self.pg.allreduce([tmp]).wait()
+            self._wait(self.pg.allreduce([tmp]), "reduce_scatter")
             n = out.numel()
             out.copy_(tmp[self.rank * n : (self.rank + 1) * n])
             return out
-        self.pg._reduce_scatter_base(out, inp).wait()
+        self._wait(self.pg._reduce_scatter_base(out, inp), "reduce_scatter")
         return out
 
     def all_gather_(self, out: torch.Tensor, inp: torch.Tensor):
-        if self.pg is None:
+        if self.size == 1:
             out.copy_(inp)
             return out
-        self.pg._allgather_base(out, inp).wait()
+        self._check()
+        self._wait(self.pg._allgather_base(out, inp), "all_gather")
         return out
 
     def all_gather_object_sizes(self, n: int):
         """All-gather one int per peer (small metadata exchange)."""
+        if self.size == 1:
+            return [n]
         dev = self.device if self.backend == "nccl" else "cpu"
         t = torch.tensor([n], dtype=torch.int64, device=dev)
         out = torch.zeros(self.size, dtype=torch.int64, device=dev)
-        if self.pg is None:
-            return [n]
-        self.pg._allgather_base(out, t).wait()
+        self.all_gather_(out, t)
         return out.tolist()
 
     def send(self, t: torch.Tensor, dst: int, tag: int = 0):
-        self.pg.send([t], dst, tag).wait()
+        self._check()
+        self._wait(self.pg.send([t], dst, tag), "send")
 
     def recv(self, t: torch.Tensor, src: int, tag: int = 0):
-        self.pg.recv([t], src, tag).wait()
+        self._check()
+        self._wait(self.pg.recv([t], src, tag), "recv")
 
     def exchange(self, send_t: torch.Tensor, recv_t: torch.Tensor, peer: int, tag: int = 0):
         """Pairwise swap with `peer`. The lower rank sends first, the higher receives first,
@@ -128,6 +287,13 @@ class PeerGroup:
             self.recv(recv_t, peer, tag)
             self.send(send_t, peer, tag)
 
+    def alltoall_(self, recv_t: torch.Tensor, send_t: torch.Tensor, recv_splits, send_splits):
+        """Generic variable-split all-to-all over flat buffers (RCCL: one grouped send/recv
+        launch that drives every xGMI link of this GPU at once)."""
+        self._check()
+        self._wait(self.pg.alltoall_base(recv_t.view(-1), send_t.view(-1), list(recv_splits), list(send_splits),
+                                         dist.AllToAllOptions()), "alltoall")
+
     def exchange_all(self, send_t: torch.Tensor, recv_t: torch.Tensor, send_to: int, recv_from: int | None = None):
         """One round in which EVERY rank of the group sends `send_t` to `send_to` and receives
         `recv_t` from `recv_from` (default: the same peer). Issued as ONE alltoall whose only
@@ -138,21 +304,24 @@ class PeerGroup:
         outs = [0] * self.size
         ins[send_to] = send_t.numel()
         outs[recv_from] = recv_t.numel()
-        self.pg.alltoall_base(recv_t.view(-1), send_t.view(-1), outs, ins, dist.AllToAllOptions()).wait()
+        self.alltoall_(recv_t, send_t, outs, ins)
 
     def barrier(self):
-        if self.pg is None:
+        if self.size == 1:
             return
         dev = self.device if self.backend == "nccl" else "cpu"
         t = torch.zeros(1, device=dev)
-        self.pg.allreduce([t]).wait()
+        self.allreduce_(t)
         if self.backend == "nccl":
             torch.cuda.synchronize()
 
     def shutdown(self):
+        """Release the communicator after its last use (a new generation replaces it)."""
+        if self.aborted:
+            return
         pg, self.pg = self.pg, None
         if pg is not None and self.backend == "nccl":
             try:
                 pg.shutdown()
-            except Exception:
+            except Exception:  # noqa: BLE001
                 pass

@@ -1,18 +1,27 @@
 """Sharded data-parallel training: ZeRO-1 optimizer-state sharding across volunteer peers,
-buddy replication of every shard, optional gradient compression, elastic re-shard.
+R-fold replication of every shard, optional gradient compression, elastic re-shard, and
+mid-collective failure recovery.
 
 Per step (all on the GPU stream):
-  fwd/bwd -> flat bf16 grads -> average over live peers (RCCL all-reduce, or PowerSGD /
-  top-k with error feedback) -> grad-norm kernel -> fused AdamW on MY shard and on my
-  left neighbour's shard (the buddy replica) -> all-gather of the updated bf16 param shards.
+  fwd/bwd -> flat bf16 grads -> averaged gradient of the shards this peer holds
+  (uncompressed: ONE reduce-scatter + R ring-shifts of the averaged shard to its replica
+  holders — 1.125x the gradient bytes at P=8, R=2, instead of an all-reduce's 1.75x;
+  compressed: PowerSGD / top-k with error feedback) -> grad-norm kernel -> fused AdamW on MY
+  shard and on the R shards I replicate -> all-gather of the updated bf16 param shards.
 
-Fault tolerance: shard j is held by peer j (primary) and peer j+1 (buddy). Because every
-peer has the full averaged gradient after the all-reduce, the buddy applies the very same
-AdamW update to its replica — no extra traffic per step; only 2x the (HBM-bound) optimizer
-work on 2/P of the model. When a peer drops, its shard survives on its buddy; when the
-membership changes the survivors re-shard by rebuilding the full fp32 optimizer state once
-(affordable inside 288 GB of HBM: 12 B/param, 96 GB for an 8B model) from the live holders
-and slicing the new primary/buddy ranges out of it.
+Fault tolerance: shard j is held by peer j (primary) and peers j+1 .. j+R (replicas, default
+R = 2, so BASELINE.json config 4's "kill 2 mid-training" — any two peers, adjacent or not —
+never loses fp32 optimizer state). Replicas apply the very same AdamW update from the same
+averaged gradient: no extra traffic per step beyond the ring-shifts; only (1+R)x the
+HBM-bound optimizer work on (1+R)/P of the model. When the membership changes the survivors
+re-shard: every live holder of an old shard broadcasts it, every peer rebuilds the full fp32
+state (12 B/param: 96 GB at 8B parameters, inside 288 GB of HBM) and cuts its new primary and
+replica slices. If a shard has no live holder left the re-shard fails loudly (StateLost)
+unless ``allow_state_loss`` is set. Under elastic membership every collective phase runs
+guarded (parallel/elastic.py): a peer dying inside the gradient reduction or the parameter
+gather aborts the phase on all survivors, which recover to a new generation, re-shard, and
+redo the reduction (the local gradients are intact: collectives never write into them) or
+rebuild the parameters from the re-sharded fp32 masters.
 
 No reference analog: SURVEY.md §2.7 "Optimizer-state sharding (ZeRO-like)" and §2.9
 "Optimizer-state sharding + elastic re-shard" (BASELINE.json configs 4 and 5).
@@ -27,7 +36,13 @@ import torch
 from .. import ops
 from ..ops.optim import OS_SUMSQ
 from .collectives import allreduce_sum_
-from .flat_params import FlatParams
+from .flat_params import FlatBuffers, FlatParams
+from .local_sgd import mean_slice, restore_extras
+from .peer_group import PeerFailure
+
+
+class StateLost(RuntimeError):
+    """Every holder of some optimizer-state shard left the job at once."""
 
 
 @dataclass
@@ -37,8 +52,10 @@ class ShardedConfig:
     eps: float = 1e-8
     weight_decay: float = 0.1
     max_grad_norm: float = 1.0
-    replicate: bool = True  # keep a buddy replica of the left neighbour's shard
-    algo: str = "rccl"
+    replicas: int = 2  # extra holders of every shard (peers r+1 .. r+replicas)
+    replicate: bool = True  # False: no replicas (replicas = 0)
+    algo: str = "rs"  # rs (reduce-scatter + replica shifts) | rccl | rs_ag | butterfly | ring | direct
+    allow_state_loss: bool = False  # restart a lost shard from the bf16 params instead of raising
 
 
 class ShardedDPTrainer:
@@ -47,12 +64,17 @@ class ShardedDPTrainer:
         self.cfg = cfg
         self.device = torch.device(device or next(model.parameters()).device)
         self.flat = FlatParams(model, device=self.device)
+        self.buffers = FlatBuffers(model)
         self.membership = membership
         self.group = membership.group if membership is not None else group
         self.compressor = compressor
         self.ostate = ops.new_ostate(self.device, cfg.lr)
         self.t = 0
         self.reshard_events = []
+        self.failed_phases = 0
+        self._skip_round = False
+        self._sumsq = None  # global squared gradient norm from the reduce-scatter path
+        self._layout_members = list(self.group.members) if self.group is not None else [0]
         self._layout(full_master=self.flat.param.float(), full_m=None, full_v=None)
 
     # ------------------------------------------------------------------ layout
@@ -64,16 +86,16 @@ class ShardedDPTrainer:
     def rank(self):
         return 0 if self.group is None else self.group.rank
 
-    def _slices(self):
-        P, r = self.world, self.rank
-        prim = self.flat.shard_bounds(r, P)
-        back = self.flat.shard_bounds((r - 1) % P, P) if (self.cfg.replicate and P > 1) else None
-        return prim, back
+    @property
+    def n_replicas(self):
+        if not self.cfg.replicate:
+            return 0
+        return max(0, min(self.cfg.replicas, self.world - 1))
 
     def _layout(self, full_master, full_m, full_v):
-        (lo, hi), back = self._slices()
+        P, r = self.world, self.rank
+        lo, hi = self.flat.shard_bounds(r, P)
         self.prim = (lo, hi)
-        self.back = back
 
         def cut(full, a, b):
             if full is None:
@@ -83,15 +105,31 @@ class ShardedDPTrainer:
         self.master = cut(full_master, lo, hi)
         self.m = cut(full_m, lo, hi)
         self.v = cut(full_v, lo, hi)
-        if back is not None:
-            a, b = back
-            self.b_master, self.b_m, self.b_v = cut(full_master, a, b), cut(full_m, a, b), cut(full_v, a, b)
-        else:
-            self.b_master = self.b_m = self.b_v = None
+        self.reps = []  # replicas: shards (r-1) .. (r-R) of the current layout
+        for i in range(1, self.n_replicas + 1):
+            j = (r - i) % P
+            a, b = self.flat.shard_bounds(j, P)
+            self.reps.append({"shard": j, "range": (a, b), "master": cut(full_master, a, b),
+                              "m": cut(full_m, a, b), "v": cut(full_v, a, b)})
+
+    @property
+    def back(self):  # first replica's range (compat)
+        return self.reps[0]["range"] if self.reps else None
 
     def checkpoint_slice(self):
         lo, hi = self.prim
-        return lo, hi, {"master": self.master, "m": self.m, "v": self.v}
+        t = {"master": self.master, "m": self.m, "v": self.v}
+        if self.compressor is not None:
+            t["ef"] = mean_slice(self.group, self.compressor.state_dict()["ef"], lo, hi)
+        return lo, hi, t
+
+    def checkpoint_global(self) -> dict:
+        out = {}
+        if self.buffers:
+            out["buffers"] = self.buffers.as_fp32()
+        if self.compressor is not None and "Q" in self.compressor.state_dict():
+            out["psgd_Q"] = self.compressor.state_dict()["Q"]
+        return out
 
     def restore(self, reader):
         """Load a checkpoint written by any number of peers into the CURRENT layout."""
@@ -104,45 +142,94 @@ class ShardedDPTrainer:
         self.master.copy_(reader.read_range("master", lo, hi).to(dev))
         self.m.copy_(reader.read_range("m", lo, hi).to(dev))
         self.v.copy_(reader.read_range("v", lo, hi).to(dev))
-        if self.back is not None:
-            a, b = self.back
-            self.b_master.copy_(reader.read_range("master", a, b).to(dev))
-            self.b_m.copy_(reader.read_range("m", a, b).to(dev))
-            self.b_v.copy_(reader.read_range("v", a, b).to(dev))
+        for rep in self.reps:
+            a, b = rep["range"]
+            for k in ("master", "m", "v"):
+                rep[k].copy_(reader.read_range(k, a, b).to(dev))
+        restore_extras(self, reader)
         self.t = reader.step
 
     def state_bytes(self) -> int:
-        n = self.master.numel() + (self.b_master.numel() if self.b_master is not None else 0)
+        n = self.master.numel() + sum(rep["master"].numel() for rep in self.reps)
         return 12 * n
 
     # ------------------------------------------------------------------ step
     def step(self, x, y):
-        if self.membership is not None:
-            grp, changed, newcomers = self.membership.sync_round()
+        mem = self.membership
+        if mem is not None and not self._skip_round:
+            grp, changed, newcomers = mem.sync_round()
             if changed:
-                self.reshard(grp, old_members=self.membership.prev_members)
+                self._reshard_until_ok(grp, newcomers)
+        self._skip_round = False
         self.flat.zero_grad()
         loss = self.model(x, y)
         loss.backward()
         g = self.flat.grad
-        P = self.world
-        if self.compressor is not None:
-            avg = self.compressor.allreduce_mean(g, self.group)
+        if mem is None:
+            avg = self._average(g)
+            self._adam(avg)
+            self._gather_params(elastic=False)
+            self.buffers.average_(self.group)
         else:
-            allreduce_sum_(g, self.group, self.cfg.algo)
-            if P > 1:
-                g.div_(P)
-            avg = g
-        self._adam(avg)
-        self._gather_params()
+            while True:
+                snap = self.compressor.snapshot() if (self.compressor is not None and self.world > 1) else None
+                try:
+                    with mem.guard("g"):
+                        avg = self._average(g)
+                    break
+                except PeerFailure:
+                    if snap is not None:
+                        self.compressor.restore(snap)
+                    self.failed_phases += 1
+                    grp, _, newcomers = mem.recover()
+                    self._reshard_until_ok(grp, newcomers)
+            self._adam(avg)
+            try:
+                with mem.guard("p"):
+                    self._gather_params(elastic=True)
+                    self.buffers.average_(self.group)
+            except PeerFailure:  # the re-shard rebuilds every parameter from the fp32 masters
+                self.failed_phases += 1
+                grp, _, newcomers = mem.recover()
+                self._reshard_until_ok(grp, newcomers)
         self.t += 1
         return loss.detach()
+
+    def _average(self, g):
+        """Averaged gradient for (at least) every shard this peer holds, in a fresh flat buffer
+        (collectives never write into the live gradient, so an aborted phase can be redone)."""
+        P = self.world
+        self._sumsq = None
+        if self.compressor is not None:
+            return self.compressor.allreduce_mean(g, self.group)
+        if P == 1:
+            return g
+        n = g.numel()
+        algo = self.cfg.algo
+        if algo == "rs" and n % P == 0 and self.prim[1] - self.prim[0] == n // P:
+            avg = torch.empty_like(g)
+            lo, hi = self.prim
+            self.group.reduce_scatter_(avg[lo:hi], g)
+            mine = avg[lo:hi]
+            mine.div_(P)
+            for i in range(1, self.n_replicas + 1):  # ring-shift the averaged shard to its replicas
+                j = (self.rank - i) % P
+                a, b = self.flat.shard_bounds(j, P)
+                self.group.exchange_all(mine, avg[a:b], (self.rank + i) % P, j)
+            if self.cfg.max_grad_norm > 0:  # global norm from the per-shard squared sums
+                sq = torch.linalg.vector_norm(mine, dtype=torch.float32).square().reshape(1)
+                self.group.allreduce_(sq)
+                self._sumsq = sq
+            return avg
+        avg = g.clone()
+        allreduce_sum_(avg, self.group, "rccl" if algo == "rs" else algo)
+        return avg.div_(P)
 
     def _adam_range(self, avg, a, b, master, m, v):
         c = self.cfg
         n_decay = max(0, min(self.flat.n_decay - a, b - a))
         n_decay -= n_decay % 8
-        # the flat kernels read ostate (step/lr/clip) — shared by both ranges, prologue once
+        # the flat kernels read ostate (step/lr/clip) — shared by all ranges, prologue once
         C = ops.native() if self.flat.param.is_cuda else None
         if C is not None:
             C.adamw_flat(self.flat.param[a:b], avg[a:b], master, m, v, n_decay, self.ostate, c.betas[0], c.betas[1],
@@ -155,19 +242,28 @@ class ShardedDPTrainer:
             adamw_step(self.flat.param[a:b], avg[a:b], master, m, v, st, n_decay=n_decay, beta1=c.betas[0],
                        beta2=c.betas[1], eps=c.eps, wd=c.weight_decay, max_norm=0.0)
 
+    def _held_ranges(self):
+        return [self.prim] + [rep["range"] for rep in self.reps]
+
     def _adam(self, avg):
+        """Local AdamW on every held shard (no communication: the global gradient norm of the
+        reduce-scatter path was all-reduced inside the guarded gradient phase)."""
         c = self.cfg
+        sumsq, self._sumsq = self._sumsq, None
         if avg.is_cuda:
             C = ops.native()
             if c.max_grad_norm > 0:
-                self.ostate[OS_SUMSQ].zero_()
-                C.grad_sumsq(avg, self.ostate)
+                if sumsq is not None:
+                    self.ostate[OS_SUMSQ : OS_SUMSQ + 1].copy_(sumsq)
+                else:
+                    self.ostate[OS_SUMSQ].zero_()
+                    C.grad_sumsq(avg, self.ostate)
             C.adam_prologue(self.ostate, float(c.max_grad_norm))
         else:
             self.ostate[0] += 1
             coef = 1.0
             if c.max_grad_norm > 0:
-                nrm = avg.float().norm().item()
+                nrm = float(sumsq.sqrt()) if sumsq is not None else avg.float().norm().item()
                 coef = min(1.0, c.max_grad_norm / (nrm + 1e-6))
             self.ostate[2] = coef
             if coef != 1.0:
@@ -175,65 +271,124 @@ class ShardedDPTrainer:
                 self.ostate[2] = 1.0
         lo, hi = self.prim
         self._adam_range(avg, lo, hi, self.master, self.m, self.v)
-        if self.back is not None:
-            a, b = self.back
-            self._adam_range(avg, a, b, self.b_master, self.b_m, self.b_v)
+        for rep in self.reps:
+            a, b = rep["range"]
+            self._adam_range(avg, a, b, rep["master"], rep["m"], rep["v"])
 
-    def _gather_params(self):
+    def _gather_params(self, elastic: bool):
         if self.world == 1:
             return
         lo, hi = self.prim
         mine = self.flat.param[lo:hi].clone()
-        self.group.all_gather_(self.flat.param, mine)
+        if not elastic:
+            self.group.all_gather_(self.flat.param, mine)
+            return
+        out = torch.empty_like(self.flat.param)  # never let an aborted gather write the params
+        self.group.all_gather_(out, mine)
+        self.flat.param.copy_(out)
 
     # ------------------------------------------------------------------ elastic re-shard
     def join_running_job(self):
         """A newly admitted peer takes part in the re-shard that admitted it (it holds no
-        shard, so it only receives)."""
-        self.reshard(self.membership.group, old_members=self.membership.prev_members)
+        shard, so it only receives); its first step then skips the membership round, which
+        the continuing members already ran."""
+        self._layout_members = []
+        mem = self.membership
+        self._reshard_until_ok(mem.group, mem.newcomers)
+        self._skip_round = True
 
-    def reshard(self, new_group, old_members=None):
-        """Membership changed: rebuild the full optimizer state from the live holders of every
-        old shard (primary, else its buddy), then cut the new primary/buddy slices."""
+    def _reshard_until_ok(self, grp, newcomers):
+        mem = self.membership
+        while True:
+            try:
+                with mem.guard("s"):
+                    new_state = self._reshard_collect(grp, newcomers)
+                self._reshard_apply(grp, *new_state)
+                return
+            except PeerFailure:
+                self.failed_phases += 1
+                grp, _, newcomers = mem.recover()
+
+    def reshard(self, new_group, newcomers=()):
+        """Non-elastic entry point (tests / manual regroup)."""
+        self._reshard_apply(new_group, *self._reshard_collect(new_group, newcomers))
+
+    def _reshard_collect(self, new_group, newcomers):
+        """Rebuild the full fp32 optimizer state from the live holders of every old shard
+        (primary, else the first live replica). Touches no trainer state: the result is
+        applied only after the phase commits."""
         t0 = time.perf_counter()
-        if old_members is None:
-            old_members = list(self.group.members) if self.group is not None else [self.membership.pid]
-        old_P = len(old_members)
-        mine_old = self.prim
-        back_old = self.back
-        my_pid = self.membership.pid if self.membership is not None else self.rank
-        self.group = new_group
-        new_members = list(new_group.members)
+        members = list(new_group.members)
+        my_pid = self.membership.pid if self.membership is not None else members[new_group.rank]
+        cont = [i for i, m in enumerate(members) if m not in newcomers]
+        if not cont:
+            raise StateLost("no member of the new generation holds optimizer state")
+        root0 = cont[0]
+        dev = self.device
+        # the layout that the continuing members' shards follow (newcomers do not know it)
+        hdr = torch.full((257,), -1, dtype=torch.int64, device=dev if new_group.backend == "nccl" else "cpu")
+        if new_group.rank == root0:
+            L = self._layout_members
+            hdr[0] = len(L)
+            hdr[1 : 1 + len(L)] = torch.tensor(L, dtype=torch.int64)
+        new_group.broadcast_(hdr, root=root0)
+        hdr = hdr.cpu()
+        L = [int(x) for x in hdr[1 : 1 + int(hdr[0])]]
+        old_P = len(L)
+        R = min(self.cfg.replicas if self.cfg.replicate else 0, old_P - 1)
         n = self.flat.numel
-        full = [torch.zeros(n, dtype=torch.float32, device=self.device) for _ in range(3)]
+        full = [torch.zeros(n, dtype=torch.float32, device=dev) for _ in range(3)]
         lost = []
-        for j, owner in enumerate(old_members):
+        my_old = L.index(my_pid) if (my_pid in L and my_pid not in newcomers) else None
+        for j in range(old_P):
             a, b = self.flat.shard_bounds(j, old_P)
             if b <= a:
                 continue
-            buddy = old_members[(j + 1) % old_P] if (self.cfg.replicate and old_P > 1) else None
-            if owner in new_members:
-                holder, src = owner, "prim"
-            elif buddy is not None and buddy in new_members:
-                holder, src = buddy, "back"
-            else:
+            holders = [L[(j + i) % old_P] for i in range(R + 1)]
+            live = [h for h in holders if h in members and h not in newcomers]
+            if not live:
                 lost.append((a, b))
                 continue
-            root = new_members.index(holder)
+            holder = live[0]
+            root = members.index(holder)
             if holder == my_pid:
-                bufs = (self.master, self.m, self.v) if src == "prim" else (self.b_master, self.b_m, self.b_v)
-                assert (mine_old if src == "prim" else back_old) == (a, b)
-                for f, s in zip(full, bufs):
+                st = self._shard_state_old(j, my_old, old_P)
+                for f, s in zip(full, st):
                     f[a:b].copy_(s)
             for f in full:
-                new_group.broadcast_(f[a:b], root=root) if new_group.size > 1 else None
-        for a, b in lost:  # no live replica: restart that range from the current bf16 params
+                new_group.broadcast_(f[a:b], root=root)
+        if lost and not self.cfg.allow_state_loss:
+            raise StateLost(f"optimizer-state shards {lost} had no live holder among {members} "
+                            f"(old layout {L}, replicas {R})")
+        ost = self.ostate.clone()
+        new_group.broadcast_(ost, root=root0)  # step counter / lr must agree
+        bufs = None
+        if self.buffers:
+            bufs = self.buffers.as_fp32().to(dev if new_group.backend == "nccl" else "cpu")
+            new_group.broadcast_(bufs, root=root0)
+        ev = {"t": self.t, "old": L, "new": members, "lost": lost, "ms": (time.perf_counter() - t0) * 1e3}
+        return full, ost, bufs, lost, ev
+
+    def _shard_state_old(self, j, my_old, old_P):
+        """(master, m, v) this peer held for shard j of the OLD layout (index my_old of old_P)."""
+        if my_old is None:
+            raise StateLost(f"asked for shard {j} but this peer held no shard")
+        if j == my_old:
+            return self.master, self.m, self.v
+        for rep in self.reps:
+            if rep["shard"] == j:
+                return rep["master"], rep["m"], rep["v"]
+        raise StateLost(f"shard {j} expected on this peer (old index {my_old} of {old_P})")
+
+    def _reshard_apply(self, new_group, full, ost, bufs, lost, ev):
+        for a, b in lost:  # allow_state_loss: no live replica, restart from the bf16 params
             full[0][a:b].copy_(self.flat.param[a:b].float())
-        # joiners (and everybody) now hold the full fp32 master: refresh the bf16 params from it
-        ops.f32_to_bf16(full[0], self.flat.param)
-        if new_group.size > 1:  # ostate (step counter / lr) must agree across peers
-            new_group.broadcast_(self.ostate, root=0)
+        ops.f32_to_bf16(full[0], self.flat.param)  # every peer now holds the full fp32 master
+        self.ostate.copy_(ost)
+        if bufs is not None:
+            self.buffers.load_fp32(bufs)
+        self.group = new_group
+        self._layout_members = list(new_group.members)
         self._layout(*full)
         del full
-        self.reshard_events.append({"t": self.t, "old": old_members, "new": new_members, "lost": lost,
-                                    "ms": (time.perf_counter() - t0) * 1e3})
+        self.reshard_events.append(ev)

@@ -7,9 +7,13 @@ defined here. One directory per step:
         manifest.json            format, step, generation, members, model config, flat layout
                                  (segment name/offset/numel/shape/decay), optimizer config,
                                  and the list of shard files with the flat [lo, hi) range each covers
-        params.safetensors       the bf16 flat parameter buffer (written by one peer)
-        state_<peer>.safetensors fp32 optimizer-state slices ("master", "m", "v", ["anchor", "outer_mom"])
-                                 of the flat range [lo, hi) this peer owned
+        params.safetensors       the bf16 flat parameter buffer, the optimizer scalars ("ostate") and
+                                 global extras: "buffers" (BN running stats, fp32), "psgd_Q"
+                                 (PowerSGD warm start) — written by one peer
+        state_<peer>.safetensors fp32 optimizer-state slices ("master", "m", "v", ["outer_mom"],
+                                 ["ef": mean error feedback]) of the flat range [lo, hi) this peer
+                                 owned; per-peer quantities (local-SGD moments, error feedback)
+                                 are stored as their mean over the peers
 
 Tensors are stored with safetensors (no pickle: loading executes nothing from the file).
 A checkpoint written by P peers can be restored by P' peers: every peer reads just the flat
@@ -52,8 +56,10 @@ def save_checkpoint(trainer, root: str, step: int, *, peer_id: int, is_writer: b
     with open(os.path.join(d, f"state_{peer_id}.json"), "w") as f:
         json.dump({"file": fname, "lo": lo, "hi": hi, "peer": peer_id, "keys": sorted(tensors)}, f)
     if is_writer:
-        save_file({"param": trainer.flat.param.detach().cpu(), "ostate": trainer.ostate.detach().cpu()},
-                  os.path.join(d, "params.safetensors"))
+        glob = {"param": trainer.flat.param.detach().cpu(), "ostate": trainer.ostate.detach().cpu()}
+        if hasattr(trainer, "checkpoint_global"):  # BN buffers, PowerSGD Q, ...
+            glob.update({k: v.detach().contiguous().cpu() for k, v in trainer.checkpoint_global().items()})
+        save_file(glob, os.path.join(d, "params.safetensors"))
     if barrier is not None:
         barrier()
     if is_writer:
@@ -101,6 +107,14 @@ class ShardReader:
     def params(self):
         t = load_file(os.path.join(self.dir, "params.safetensors"))
         return t["param"], t["ostate"]
+
+    def global_tensor(self, key: str):
+        """A tensor of params.safetensors other than param/ostate, or None."""
+        with safe_open(os.path.join(self.dir, "params.safetensors"), framework="pt") as f:
+            return f.get_tensor(key) if key in f.keys() else None
+
+    def has_key(self, key: str) -> bool:
+        return any(key in s["keys"] for s in self.shards)
 
     def read_range(self, key: str, lo: int, hi: int) -> torch.Tensor:
         """Assemble flat[lo:hi] of tensor `key` from the shard files that cover it."""

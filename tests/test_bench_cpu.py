@@ -38,15 +38,31 @@ def test_bench_single_process():
     _check(_json_line(r.stdout), 1)
 
 
-@pytest.mark.slow
-def test_bench_torchrun_two_ranks():
+def _torchrun(n, extra=()):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", *ARGS]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(n), *ARGS, *extra]
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
-    _check(rec, 2)
-    assert "dp2" in rec["config"]["parallelism"]
+    _check(rec, n)
+    assert f"dp{n}" in rec["config"]["parallelism"]
+    return rec
+
+
+@pytest.mark.slow
+def test_bench_torchrun_two_ranks():
+    rec = _torchrun(2)
+    assert "allreduce=direct" in rec["config"]["parallelism"]  # the default averaging schedule
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n,algo", [(4, "direct"), (4, "butterfly"), (4, "ring"), (4, "rs_ag"), (4, "rccl"),
+                                    (8, "direct"), (8, "butterfly")])
+def test_bench_torchrun_more_ranks(n, algo):
+    """The driver's multi-GPU command line at 4 and 8 ranks, each averaging algorithm (gloo)."""
+    rec = _torchrun(n, ["--algo", algo])
+    assert f"allreduce={algo}" in rec["config"]["parallelism"]
+    assert rec["sync_ms"] > 0

@@ -21,3 +21,23 @@ def test_bench_drop_three_peers_one_crash(tmp_path):
     # the regroup waited at least one lease for the silent peer
     assert rec["regroup_sync_ms"] >= 0.5 * 1e3 * 0.9
     assert rec["ms_per_step_after"] > 0 and rec["samples_per_s_after"] > 0
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("fault", ["collective", "stop"])
+def test_bench_drop_two_peers_die_inside_the_collective(tmp_path, fault):
+    """Config 4's failure class: two of four peers die (SIGKILL) or freeze (SIGSTOP) INSIDE the
+    averaging all-reduce; the survivors abort that round, regroup and redo it."""
+    out = tmp_path / "drop.json"
+    env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, os.path.join(ROOT, "bench_drop.py"), "--peers", "4", "--model", "gpt2-tiny", "--batch", "2",
+           "--seq", "32", "--steps", "14", "--warmup", "2", "--lease", "0.5", "--json-out", str(out), "--timeout", "240",
+           "--fault", fault, "--drop-peers", "2,3"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads(out.read_text())
+    assert rec["config"]["fault"] == fault and rec["config"]["drop_peers"] == [2, 3]
+    assert rec["rounds_aborted_and_redone"] >= 1
+    assert rec["regroup_step"] is not None and rec["samples_per_s_after"] > 0
