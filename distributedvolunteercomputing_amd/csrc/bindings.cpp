@@ -89,6 +89,59 @@ void f32_to_bf16(at::Tensor src, at::Tensor dst) {
   vcx_f32_to_bf16(src.data_ptr<float>(), dst.data_ptr(), src.numel(), cur_stream());
 }
 
+// ---------------------------------------------------------------- hand-written MFMA GEMM (gemm.hip)
+// C[M, N] = A[M, K] . B[N, K]^T with epilogue: 0 store, 1 +bias, 2 +bias -> (C = pre, C2 = gelu(pre)),
+// 3 C = acc * gelu'(C2) with fp32 column sums added into `colsum` (must be zeroed by the caller)
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) { return vcx_gemm_nt_supported((int)M, (int)N, (int)K); }
+
+void gemm_nt(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor> c2, c10::optional<at::Tensor> bias,
+             c10::optional<at::Tensor> colsum, int64_t epi) {
+  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_nt: 2-D cuda tensors");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
+              "gemm_nt: bf16 operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm_nt: K-contiguous rows");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_nt: shape mismatch");
+  TORCH_CHECK(vcx_gemm_nt_supported((int)M, (int)N, (int)K), "gemm_nt: needs M % 256 == 0, N % 256 == 0, K % 64 == 0, K >= 128");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm_nt: 16-B aligned rows");
+  void* c2p = nullptr;
+  if (epi >= 2) {
+    TORCH_CHECK(c2 && c2->sizes() == c.sizes() && c2->strides() == c.strides() && c2->scalar_type() == at::kBFloat16,
+                "gemm_nt: epilogue 2/3 needs c2 like c");
+    c2p = c2->data_ptr();
+  }
+  const void* bp = nullptr;
+  if (epi == 1 || epi == 2) {
+    TORCH_CHECK(bias && bias->numel() == N && bias->is_contiguous() && bias->scalar_type() == at::kBFloat16,
+                "gemm_nt: bias [N] bf16");
+    bp = bias->data_ptr();
+  }
+  float* cs = nullptr;
+  if (epi == 3) {
+    TORCH_CHECK(colsum && colsum->numel() == N && colsum->scalar_type() == at::kFloat && colsum->is_contiguous(),
+                "gemm_nt: colsum [N] fp32");
+    cs = colsum->data_ptr<float>();
+  }
+  vcx_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), c2p, bp, cs, (int)M, (int)N, (int)K, (int)a.stride(0),
+              (int)b.stride(0), (int)c.stride(0), (int)epi, cur_stream());
+}
+
+at::Tensor transpose_bf16(at::Tensor src, c10::optional<at::Tensor> dst) {
+  TORCH_CHECK(src.is_cuda() && src.dim() == 2 && src.is_contiguous() && src.scalar_type() == at::kBFloat16,
+              "transpose_bf16: contiguous 2-D bf16");
+  at::Tensor out = dst ? *dst : at::empty({src.size(1), src.size(0)}, src.options());
+  TORCH_CHECK(out.size(0) == src.size(1) && out.size(1) == src.size(0) && out.is_contiguous(), "transpose_bf16: dst");
+  vcx_transpose_bf16(src.data_ptr(), out.data_ptr(), (int)src.size(0), (int)src.size(1), cur_stream());
+  return out;
+}
+
+void add_f32_into_bf16(at::Tensor in, at::Tensor out, bool accumulate) {
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kFloat && out.scalar_type() == at::kBFloat16 &&
+                  in.numel() == out.numel() && in.is_contiguous() && out.is_contiguous(),
+              "add_f32_into_bf16: fp32 in, bf16 out of equal size");
+  vcx_add_f32_into_bf16(in.data_ptr<float>(), out.data_ptr(), (int)in.numel(), accumulate ? 1 : 0, cur_stream());
+}
+
 void reduce_bcast_bf16(at::Tensor in, c10::optional<at::Tensor> out, c10::optional<at::Tensor> mine, int64_t P) {
   TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kBFloat16 && in.is_contiguous(), "reduce_bcast: bf16 cuda in");
   const int64_t n = in.numel() / P;
@@ -524,6 +577,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("axpy_bf16", &axpy_bf16);
   m.def("reduce_bcast_bf16", &reduce_bcast_bf16);
+  m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
+        py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0);
+  m.def("transpose_bf16", &transpose_bf16, py::arg("src"), py::arg("dst") = py::none());
+  m.def("add_f32_into_bf16", &add_f32_into_bf16);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("mean"),

@@ -14,6 +14,11 @@ void vcx_lsgd_apply(const void* avg, float* anchor, float* master, void* param, 
                     float outer_lr, float mu, int nesterov, float avg_scale, hipStream_t s);
 void vcx_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s);
 void vcx_axpy_bf16(const void* src, void* acc, int64_t n, float scale, hipStream_t s);
+bool vcx_gemm_nt_supported(int M, int N, int K);
+void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,
+                 int lda, int ldb, int ldc, int epi, hipStream_t s);
+void vcx_transpose_bf16(const void* src, void* dst, int R, int Cc, hipStream_t s);
+void vcx_add_f32_into_bf16(const float* in, void* out, int n, int accumulate, hipStream_t s);
 void vcx_reduce_bcast_bf16(const void* in, void* out, void* mine, int P, int64_t n, hipStream_t s);
 void vcx_splitk_reduce(const void* part, void* acc, int S, int64_t n, int accumulate, hipStream_t s);
 

@@ -96,8 +96,9 @@ class Block(nn.Module):
         return ops.linear(y.reshape(B, T, C), self.proj_w)
 
     def mlp(self, h):
-        # fc bias fused into the GELU kernel; fc2 bias fused into the next add+LayerNorm
-        return ops.linear(ops.bias_gelu(ops.linear(h, self.fc_w), self.fc_b), self.fc2_w)
+        # fc bias + GELU in the fc GEMM's epilogue (and gelu' + bias grad in the backward GEMM's),
+        # fc2 bias fused into the next add+LayerNorm
+        return ops.mlp_gelu(h, self.fc_w, self.fc_b, self.fc2_w)
 
 
 class GPT2(nn.Module):

@@ -4,7 +4,7 @@ from ._lib import available as native_available, native  # noqa: F401
 from .activations import bias_gelu, gelu, swiglu  # noqa: F401
 from .attention import causal_attention, fused_bias_grad_ok, gqa_attention  # noqa: F401
 from .embedding import embed  # noqa: F401
-from .linear import linear, native_linear_ok, wgrad  # noqa: F401
+from .linear import gemm_nt, linear, mlp_gelu, native_linear_ok, set_gemm_backend, wgrad  # noqa: F401
 from .loss import cross_entropy  # noqa: F401
 from .norm import add_layernorm, add_rmsnorm, layernorm, rmsnorm  # noqa: F401
 from .rope import rope_qkv  # noqa: F401

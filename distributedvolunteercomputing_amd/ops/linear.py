@@ -10,11 +10,16 @@ The S partial products are summed in fp32 by a HIP kernel directly INTO the flat
 buffer (``p.grad`` is a view of it, see parallel/flat_params.py), so no separate autograd
 accumulation pass runs either.
 
-Forward and input-gradient GEMMs go through ``mm``: per GEMM shape, the first call outside graph
-capture times the TunableOp-selected library GEMM (hipBLASLt / rocBLAS, utils/tuning.py) against
-hipBLASLt with this process's own per-shape algorithm search (csrc/bindings_lt.cpp) and keeps the
-faster for the rest of the run (the selections differ by up to ~20% per shape on MI355X). The bias
-gradient is a HIP column-sum kernel added into the flat gradient buffer.
+With ``VCX_GEMM=vcx`` the forward and input-gradient GEMMs run the hand-written MFMA GEMM of
+csrc/kernels/gemm.hip (``gemm_nt``: 256x256 tiles, LDS-DMA ring, bias / bias+GELU / DGELU
+epilogues) whenever the shape tiles (M, N multiples of 256, K of 64, K >= 128); the input
+gradient dX = dY W runs as gemm_nt(dY, W^T) with W^T materialised by a HIP transpose (the
+weights are a few MB; activations are never transposed). Default: library GEMMs, which measure
+faster at the GPT-2 shapes (profiles/r2_gemm_nt.txt). Other shapes go through ``mm``: per GEMM
+shape, the first call outside graph capture can time the TunableOp-selected library GEMM
+(hipBLASLt / rocBLAS, utils/tuning.py) against hipBLASLt with this process's own per-shape
+algorithm search (csrc/bindings_lt.cpp). The bias gradient is a HIP column-sum kernel added into
+the flat gradient buffer.
 """
 from __future__ import annotations
 
@@ -26,6 +31,33 @@ import os
 from ._lib import grad_buffer, native, use_native
 
 MIN_ROWS_PER_SPLIT = 2048
+# The hand-written GEMM is opt-in (VCX_GEMM=vcx): at the GPT-2 bench shapes it runs at 0.74-0.84x
+# the library GEMM, and its fused bias+GELU / DGELU epilogues (not overlapped with MFMA work: one
+# workgroup per CU) cost more than the separate HIP passes they replace (profiles/r2_gemm_nt.txt)
+_VCX_GEMM = [os.environ.get("VCX_GEMM", "lib") == "vcx"]
+
+
+def set_gemm_backend(name: str):
+    """'vcx' (hand-written gemm_nt where the shape tiles) or 'lib' (library GEMMs only)."""
+    _VCX_GEMM[0] = name != "lib"
+
+
+def gemm_nt_ok(M: int, N: int, K: int, t) -> bool:
+    return (_VCX_GEMM[0] and use_native(t) and t.dtype == torch.bfloat16
+            and bool(native().gemm_nt_supported(M, N, K)))
+
+
+def gemm_nt(a, b, bias=None, out=None):
+    """a [M, K] @ b[N, K]^T (+ bias[N]) on the hand-written MFMA kernel (caller checked gemm_nt_ok)."""
+    a = a if a.stride(-1) == 1 else a.contiguous()
+    out = torch.empty(a.shape[0], b.shape[0], device=a.device, dtype=a.dtype) if out is None else out
+    native().gemm_nt(a, b, out, None, bias, None, 1 if bias is not None else 0)
+    return out
+
+
+def transpose_weight(w):
+    """W^T as a contiguous bf16 matrix (HIP transpose; weights only — a few MB)."""
+    return native().transpose_bf16(w.contiguous())
 _GEMM_SELECT = os.environ.get("VCX_GEMM_SELECT", "0") == "1"  # measured: no in-step gain (A/B 956 vs 957 samples/s)
 _CHOICE: dict = {}  # (shapes, layout, bias) -> "torch" | "lt"
 
@@ -187,6 +219,8 @@ class _Linear(torch.autograd.Function):
         ctx.has_bias = b is not None and not bias_grad_elsewhere
         ctx.bias = b
         x2 = x.reshape(-1, x.shape[-1])
+        if gemm_nt_ok(x2.shape[0], w.shape[0], x2.shape[1], x2):
+            return gemm_nt(x2, w, b).view(*x.shape[:-1], w.shape[0])
         return mm(x2, w, trans_b=True, bias=b).view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -196,7 +230,12 @@ class _Linear(torch.autograd.Function):
         dy2 = dy.reshape(-1, N)
         x2 = x.reshape(-1, K)
         dy2 = dy2.contiguous()
-        dx = mm(dy2, w).view(x.shape) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if gemm_nt_ok(dy2.shape[0], K, N, dy2):
+                dx = gemm_nt(dy2, transpose_weight(w)).view(x.shape)
+            else:
+                dx = mm(dy2, w).view(x.shape)
         want_w = bool(ctx.needs_input_grad[1])
         want_b = bool(ctx.has_bias and ctx.needs_input_grad[2])
         bias, ctx.bias = ctx.bias, None
@@ -230,3 +269,63 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
     if native_linear_ok(w):
         return _Linear.apply(x, w, b, bias_grad_elsewhere)
     return F.linear(x, w, b)
+
+
+# ---------------------------------------------------------------- fused GPT-2 MLP
+class _MlpGelu(torch.autograd.Function):
+    """y = gelu_tanh(x W1^T + b1) W2^T on the hand-written GEMM with fused epilogues:
+    forward  fc:  one GEMM writes pre = x W1^T + b1 AND act = gelu(pre) (no bias_gelu pass);
+    backward fc2-dgrad: one GEMM writes dpre = (dy W2) * gelu'(pre) and reduces db1 = sum dpre
+             in its epilogue (no bias_gelu_bwd pass, dact never hits HBM)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2):
+        C = native()
+        x2 = x.reshape(-1, x.shape[-1])
+        M, F_ = x2.shape[0], w1.shape[0]
+        pre = torch.empty(M, F_, device=x.device, dtype=x.dtype)
+        act = torch.empty_like(pre)
+        C.gemm_nt(x2, w1, pre, act, b1, None, 2)
+        y = gemm_nt(act, w2)
+        ctx.save_for_backward(x2, w1, b1, w2, pre, act)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        x2, w1, b1, w2, pre, act = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        M, F_ = pre.shape
+        cs = torch.zeros(F_, device=dy.device, dtype=torch.float32)
+        dpre = torch.empty_like(pre)
+        C.gemm_nt(dy2, transpose_weight(w2), dpre, pre, None, cs, 3)
+        dw2, _ = _param_grads(dy2, act, w2, None, ctx.needs_input_grad[3], False)
+        dw1, _ = _param_grads(dpre, x2, w1, None, ctx.needs_input_grad[1], False)
+        db1 = None
+        if ctx.needs_input_grad[2]:
+            gb = grad_buffer(b1)
+            if gb is not None:
+                C.add_f32_into_bf16(cs, gb, True)
+            else:
+                db1 = cs.to(b1.dtype)
+        dx = gemm_nt(dpre, transpose_weight(w1)).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        return dx, dw1, db1, dw2
+
+
+def mlp_gelu_ok(x, w1, w2) -> bool:
+    M = x.numel() // x.shape[-1]
+    F_, C_ = w1.shape
+    return (native_linear_ok(w1) and x.dtype == torch.bfloat16 and gemm_nt_ok(M, F_, C_, x)
+            and gemm_nt_ok(M, w2.shape[0], F_, x) and gemm_nt_ok(M, C_, w2.shape[0], x)
+            and gemm_nt_ok(M, F_, w2.shape[0], x))
+
+
+def mlp_gelu(x, w1, b1, w2):
+    """gelu_tanh(x W1^T + b1) W2^T (GPT-2 MLP without the fc2 bias, which the following fused
+    add + LayerNorm applies)."""
+    if mlp_gelu_ok(x, w1, w2):
+        return _MlpGelu.apply(x, w1, b1, w2)
+    from .activations import bias_gelu
+
+    return linear(bias_gelu(linear(x, w1), b1), w2)

@@ -26,10 +26,11 @@ def test_topk_exact(gpu, n, ratio):
     thr = torch.topk(acc.abs(), k).values[-1]
     assert (acc[sel].abs() >= thr - 1e-6).all()
     assert torch.allclose(val.float(), acc[sel].to(torch.bfloat16).float())
-    # error feedback: selected zeroed, the rest kept
+    # error feedback: a selected entry keeps its bf16 rounding residual, the rest is kept whole
     mask = torch.ones(n, dtype=torch.bool, device=gpu)
     mask[sel] = False
-    assert (c.e[sel] == 0).all() and torch.equal(c.e[mask], acc[mask])
+    assert torch.equal(c.e[sel], acc[sel] - val.float()) and torch.equal(c.e[mask], acc[mask])
+    assert (c.e[sel].abs() <= acc[sel].abs() * 2.0**-8).all()
 
 
 def test_topk_ties_and_zeros(gpu):

@@ -306,3 +306,72 @@ def test_embedding_grads_accumulate_into_preset_buffers(gpu):
     (((F.embedding(idx, w32) + p32[:T]) * dy).sum()).backward()
     assert torch.allclose(wte.grad.float(), w32.grad + g_te.float(), atol=6e-2, rtol=2e-2)
     assert torch.allclose(wpe.grad.float(), p32.grad + g_pe.float(), atol=2e-1, rtol=2e-2)
+
+
+@pytest.mark.parametrize("P,n", [(2, 64), (5, 4104), (8, 31 * 1024 * 8)])
+def test_reduce_bcast_bf16_vs_fp32(gpu, P, n):
+    """Direct all-reduce middle step: sum of P received shard copies, written to every row of the
+    (aliased) send buffer and to this peer's own shard."""
+    torch.manual_seed(P)
+    inp = _bf(torch.randn(P * n, device=gpu))
+    ref = inp.float().view(P, n).sum(0)
+    mine = torch.empty(n, device=gpu, dtype=torch.bfloat16)
+    ops.reduce_bcast_bf16(inp, inp, mine, P)  # out aliases inp, as in collectives._direct
+    torch.cuda.synchronize()
+    assert ops.native() is not None
+    tol = 2e-2 * ref.abs().max().item()
+    assert (mine.float() - ref).abs().max().item() < tol
+    for r in range(P):
+        assert torch.equal(inp.view(P, n)[r], mine)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 192), (1024, 512, 768), (768, 3072, 256)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+def test_gemm_nt_epilogues_vs_fp32(gpu, M, N, K, epi):
+    """Hand-written MFMA GEMM (gemm.hip) against an fp32 torch reference, every epilogue."""
+    C = ops.native()
+    torch.manual_seed(M + N + K + epi)
+    a = _bf(torch.randn(M, K, device=gpu))
+    b = _bf(torch.randn(N, K, device=gpu) * 0.05)
+    bias = _bf(torch.randn(N, device=gpu) * 0.1)
+    c = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    c2 = _bf(torch.randn(M, N, device=gpu)) if epi == 3 else torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    pre_in = c2.clone()
+    cs = torch.zeros(N, device=gpu, dtype=torch.float32)
+    C.gemm_nt(a, b, c, c2, bias, cs, epi)
+    ref = a.float() @ b.float().t()
+    if epi == 1:
+        ref = ref + bias.float()
+    elif epi == 2:
+        ref = ref + bias.float()
+        g = F.gelu(ref, approximate="tanh")
+        assert (c2.float() - g).abs().max() < 2e-2 * g.abs().max()
+    elif epi == 3:
+        x = pre_in.float().requires_grad_()
+        F.gelu(x, approximate="tanh").backward(ref)
+        ref = x.grad
+        colsum = c.float().sum(0)
+        assert (cs - colsum).abs().max() < 1e-2 * colsum.abs().max() + 1e-3
+    assert (c.float() - ref).abs().max() < 2e-2 * ref.abs().max()
+
+
+def test_mlp_gelu_fused_matches_unfused(gpu):
+    """ops.mlp_gelu on the hand-written GEMM (VCX_GEMM=vcx) vs the library + bias_gelu path."""
+    torch.manual_seed(0)
+    x = _bf(torch.randn(512, 768, device=gpu))
+    w1 = _bf(torch.randn(3072, 768, device=gpu) * 0.02).requires_grad_()
+    b1 = _bf(torch.randn(3072, device=gpu) * 0.02).requires_grad_()
+    w2 = _bf(torch.randn(768, 3072, device=gpu) * 0.02).requires_grad_()
+    dy = _bf(torch.randn(512, 768, device=gpu))
+    outs = {}
+    for backend in ("lib", "vcx"):
+        ops.set_gemm_backend(backend)
+        xi = x.clone().requires_grad_()
+        for p in (w1, b1, w2):
+            p.grad = None
+        y = ops.mlp_gelu(xi, w1, b1, w2)
+        y.backward(dy)
+        outs[backend] = [t.float().clone() for t in (y, xi.grad, w1.grad, b1.grad, w2.grad)]
+    ops.set_gemm_backend("lib")
+    for a, b in zip(outs["lib"], outs["vcx"]):
+        assert (a - b).norm() / b.norm() < 2e-2
