@@ -215,17 +215,34 @@ class client:  # noqa: N801 (reference class name)
 
     # ------------------------------------------------------------------ worker role
     def worker(self):
+        """Worker role, two chunks deep: chunk k+1 is submitted to the engine (its host copy and
+        H2D start at once) before chunk k's result is collected and sent, so the upload of one
+        chunk overlaps the network of the previous one (DetectorEngine.submit)."""
+        pending = None
         while self.continue_procesing:
             try:
-                hdr, arr, requester, nums = self.work_q.get(timeout=0.2)
+                item = self.work_q.get(timeout=0.002 if pending is not None else 0.2)
             except queue.Empty:
-                continue
-            t0 = time.perf_counter()
-            out, counts = self._get_engine().process(arr, requester)
-            self.metrics.observe("chunk_infer_ms", (time.perf_counter() - t0) * 1e3)
-            self.metrics.incr("frames_processed", len(nums))
-            info = f"{requester}||processed||{'-'.join(map(str, nums))}||{out.shape[1]}||{out.shape[2]}"
-            self.sender.send_image(info, out, chunk=hdr.get("chunk", -1))
+                item = None
+            if item is not None:
+                hdr, arr, requester, nums = item
+                job = self._get_engine().submit(arr, requester)
+                nxt = (job, hdr, requester, nums, time.perf_counter())
+            else:
+                nxt = None
+            if pending is not None and (nxt is not None or self.work_q.empty()):
+                self._finish(*pending)
+                pending = None
+            pending = nxt if nxt is not None else pending
+        if pending is not None:
+            self._finish(*pending)
+
+    def _finish(self, job, hdr, requester, nums, t0):
+        out, counts = job.result()
+        self.metrics.observe("chunk_infer_ms", (time.perf_counter() - t0) * 1e3)
+        self.metrics.incr("frames_processed", len(nums))
+        info = f"{requester}||processed||{'-'.join(map(str, nums))}||{out.shape[1]}||{out.shape[2]}"
+        self.sender.send_image(info, out, chunk=hdr.get("chunk", -1))
 
     # ------------------------------------------------------------------ heartbeat / leave
     def _heartbeat(self):

@@ -88,6 +88,48 @@ at::Tensor gemm_bias_act(at::Tensor X, at::Tensor Wt, c10::optional<at::Tensor> 
   return Y;
 }
 
+// SSD head of one source: loc||conf as ONE GEMM whose epilogue writes columns [0, split) into
+// `loc_all` and [split, N) into `conf_all` (both [images, total]) at the source's offsets, rows
+// grouped `rpi` per image — the Permute + Flatten + Concat of the prototxt as address arithmetic.
+void gemm_bias_heads(at::Tensor X, at::Tensor Wt, at::Tensor bias, at::Tensor loc_all, int64_t loc_off,
+                     at::Tensor conf_all, int64_t conf_off, int64_t split, int64_t rpi) {
+  CHK(X, at::kBFloat16);
+  CHK(Wt, at::kBFloat16);
+  CHK(bias, at::kFloat);
+  CHK(loc_all, at::kBFloat16);
+  CHK(conf_all, at::kBFloat16);
+  TORCH_CHECK(X.dim() == 2 && Wt.dim() == 2 && X.size(1) == Wt.size(1), "X [M,K] . Wt[N,K]^T");
+  const int64_t M = X.size(0), K = X.size(1), N = Wt.size(0);
+  TORCH_CHECK(K % 32 == 0 && bias.numel() == N && split > 0 && split < N && rpi > 0 && M % rpi == 0);
+  const int64_t imgs = M / rpi;
+  TORCH_CHECK(loc_all.dim() == 2 && conf_all.dim() == 2 && loc_all.size(0) == imgs && conf_all.size(0) == imgs);
+  TORCH_CHECK(loc_off + rpi * split <= loc_all.size(1) && conf_off + rpi * (N - split) <= conf_all.size(1),
+              "head output out of the concat buffer");
+  vcx_gemm_bias_act_mapped(X.data_ptr(), Wt.data_ptr(), bias.data_ptr<float>(),
+                           (uint16_t*)loc_all.data_ptr() + loc_off, (int)M, (int)N, (int)K, (int)split, 0,
+                           (uint16_t*)conf_all.data_ptr() + conf_off, (int)split, (int)(N - split), (int)rpi,
+                           loc_all.size(1), conf_all.size(1), cur_stream());
+}
+
+// KxK convolution as an implicit GEMM (no im2col matrix): x NHWC bf16 [imgs, H, W, Cs] using
+// its first C channels (C % 8 == 0, or C == 4 == Cs), Wt [N, Kp] columns (ky, kx, c)
+at::Tensor conv_implicit(at::Tensor x, at::Tensor Wt, at::Tensor bias, int64_t C, int64_t KH, int64_t KW,
+                         int64_t stride, int64_t pad, bool relu) {
+  CHK(x, at::kBFloat16);
+  CHK(Wt, at::kBFloat16);
+  CHK(bias, at::kFloat);
+  TORCH_CHECK(x.dim() == 4 && Wt.dim() == 2, "x NHWC, Wt [N, Kp]");
+  const int64_t imgs = x.size(0), H = x.size(1), W = x.size(2), Cs = x.size(3), N = Wt.size(0), Kp = Wt.size(1);
+  TORCH_CHECK(Kp % 32 == 0 && Kp >= KH * KW * C && bias.numel() == N && C <= Cs);
+  TORCH_CHECK((C % 8 == 0 && Cs % 8 == 0) || (C == 4 && Cs == 4), "implicit conv: C % 8 == 0, or C == Cs == 4");
+  const int64_t Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  auto Y = at::empty({imgs, Ho, Wo, N}, x.options());
+  vcx_conv_implicit(x.data_ptr(), Wt.data_ptr(), bias.data_ptr<float>(), Y.data_ptr(), (int)imgs, (int)H, (int)W,
+                    (int)C, (int)Cs, (int)KH, (int)KW, (int)stride, (int)pad, (int)N, (int)Kp, relu ? 1 : 0,
+                    cur_stream());
+  return Y;
+}
+
 std::vector<at::Tensor> ssd_detect(at::Tensor conf, at::Tensor loc, at::Tensor pri, at::Tensor var, int64_t C,
                                    int64_t bg, double thresh, double nms_thresh, int64_t topk, int64_t keep) {
   CHK(conf, at::kBFloat16);
@@ -102,11 +144,13 @@ std::vector<at::Tensor> ssd_detect(at::Tensor conf, at::Tensor loc, at::Tensor p
   TORCH_CHECK((C - 1) * topk <= 4096, "ssd_detect: (C-1)*topk must fit the merge sort");
   auto fo = conf.options().dtype(at::kFloat);
   auto io = conf.options().dtype(at::kInt);
+  TORCH_CHECK(C <= 32, "ssd_detect: at most 32 classes");
+  auto prob = at::empty({N, C, P}, fo);
   auto cls_out = at::empty({N, C, topk, 5}, fo);
   auto cls_cnt = at::zeros({N, C}, io);
   auto out = at::zeros({N, keep, 7}, fo);
   auto cnt = at::empty({N}, io);
-  vcx_ssd_detect(conf.data_ptr(), loc.data_ptr(), pri.data_ptr<float>(), var.data_ptr<float>(),
+  vcx_ssd_detect(conf.data_ptr(), loc.data_ptr(), pri.data_ptr<float>(), var.data_ptr<float>(), prob.data_ptr<float>(),
                  cls_out.data_ptr<float>(), cls_cnt.data_ptr<int>(), out.data_ptr<float>(), cnt.data_ptr<int>(),
                  (int)N, (int)P, (int)C, (int)bg, (float)thresh, (float)nms_thresh, (int)topk, (int)keep,
                  cur_stream());
@@ -143,6 +187,8 @@ void vcx_register_vision(pybind11::module& m) {
   m.def("im2col_nhwc", &im2col_nhwc);
   m.def("dwconv3x3", &dwconv3x3);
   m.def("gemm_bias_act", &gemm_bias_act);
+  m.def("gemm_bias_heads", &gemm_bias_heads);
+  m.def("conv_implicit", &conv_implicit);
   m.def("ssd_detect", &ssd_detect);
   m.def("annotate", &annotate);
 }

@@ -11,10 +11,15 @@ void vcx_im2col_nhwc(const void* x, void* out, int N, int H, int W, int C, int C
                      int stride, int pad, int Kp, hipStream_t s);
 void vcx_dwconv3x3(const void* x, const void* w, const float* b, void* y, int N, int H, int W, int C, int Ho, int Wo,
                    int stride, int relu, hipStream_t s);
+void vcx_gemm_bias_act_mapped(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
+                              int relu, void* Y2, int split, int ldy2, int rpi, int64_t img_stride,
+                              int64_t img_stride2, hipStream_t s);
+void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y, int imgs, int H, int W, int C,
+                       int Cs, int KH, int KW, int stride, int pad, int N, int Kp, int relu, hipStream_t s);
 void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
                        int relu, hipStream_t s);
-void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* cls_out,
-                    int* cls_cnt, float* out, int* out_cnt, int N, int P, int C, int bg, float thresh,
+void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* prob,
+                    float* cls_out, int* cls_cnt, float* out, int* out_cnt, int N, int P, int C, int bg, float thresh,
                     float nms_thresh, int topk, int keep, hipStream_t s);
 void vcx_annotate(uint8_t* frames, int N, int h, int w, const float* dets, const int* det_cnt, int keep, int label,
                   float thresh, uint32_t box_bgr, const uint8_t* name_mask, int nm_h, int nm_w, int nm_x, int nm_y,

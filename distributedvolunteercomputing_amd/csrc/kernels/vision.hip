@@ -166,19 +166,46 @@ __global__ void __launch_bounds__(256) dwconv3x3_kernel(const bf16* __restrict__
 // K6/K7/K8: GEMM  Y[M, N] = act(X[M, K] . W[N, K]^T + bias[N])   (bf16 in, fp32 acc, bf16 out)
 // Block tile 128 x BN (BN = 128 | 64), BK = 32, 256 threads = 4 waves in a 2 x 2 grid; each
 // wave owns a 64 x (BN/2) sub-tile made of 16x16 MFMA tiles (v_mfma_f32_16x16x32_bf16: one
-// MFMA per 16x16 tile per K-step). LDS rows are padded to 40 bf16 (80 B) so the 16 rows a
-// ds_read_b128 lane group touches hit 16 distinct 4-bank slots (conflict-free). Global->LDS
+// MFMA per 16x16 tile per K-step). LDS rows are XOR-swizzled 64-B rows (gidx below). Global->LDS
 // staging is double-buffered through registers (load tile k+1 while tile k feeds the MFMAs).
 // Blocks are remapped so that consecutive tiles of one M panel land on the same XCD (they
 // share the X panel through that XCD's L2). Requires K % 32 == 0; M, N arbitrary.
 // =====================================================================================
 typedef short bf16x8s __attribute__((ext_vector_type(8)));
-constexpr int GBM = 128, GBK = 32, GLDK = 40;
+constexpr int GBM = 128, GBK = 32, GLDK = 32;
 
-template <int BN>
+// LDS image of a [rows][32] bf16 tile: 64-B rows, 16-B chunks XOR-swizzled by
+// F[(row >> 2) & 3] = {0, 2, 3, 1}. Every ds_read_b128 lane group (16 rows, two chunks) then hits
+// 16 distinct 16-B bank slots; the former 80-B padded rows measured 5.3 bank conflicts per LDS
+// instruction (rocprofv3 SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS).
+__device__ __forceinline__ int gswz(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
+__device__ __forceinline__ int gidx(int row, int chunk) { return row * GLDK + ((chunk ^ gswz(row)) << 3); }
+
+// Output mapping (epilogue): row m of image (m / rpi), column n:
+//   n <  split: Y  + (m / rpi) * img_stride  + (m % rpi) * ldy  + n
+//   n >= split: Y2 + (m / rpi) * img_stride2 + (m % rpi) * ldy2 + (n - split)
+// A plain GEMM is rpi = M, split = N. The SSD heads use it to run loc||conf of one source as ONE
+// GEMM that writes both straight into the concatenated mbox_loc / mbox_conf buffers (Permute +
+// Flatten + Concat, prototxt 1172-1858, become address arithmetic).
+struct OutMap {
+  bf16* Y2;
+  int split, ldy2, rpi;
+  int64_t img_stride, img_stride2;
+};
+
+// Implicit-GEMM convolution (IMPLICIT = true): X is the NHWC input [imgs, H, W, Cs] and the A tile
+// row m = (img, oy, ox), column k = (ky, kx, c) is gathered while staging — no im2col matrix
+// is written or read (the stem's was 144 MB per 100-frame chunk). C % 8 == 0: one 16-B load per
+// 8 columns (one tap); C == 4 (the stem's padded BGR0 blob): two 8-B loads (two taps).
+struct ConvGeom {
+  int H, W, C, Cs, Ho, Wo, KW, stride, pad, Kreal;
+};
+
+template <int BN, bool IMPLICIT>
 __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                                                              const float* __restrict__ bias, bf16* __restrict__ Y,
-                                                             int M, int N, int K, int ldy, int relu) {
+                                                             int M, int N, int K, int ldy, int relu, OutMap om,
+                                                             ConvGeom cg) {
   __shared__ __attribute__((aligned(16))) bf16 sA[2][GBM * GLDK];
   __shared__ __attribute__((aligned(16))) bf16 sB[2][BN * GLDK];
   constexpr int WN = BN / 2;          // per-wave N extent
@@ -200,12 +227,50 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
   // staging: A tile 128x32 bf16 = 512 x 16 B -> 2 per thread; B tile BN x 32 -> BN/128 per thread
   constexpr int BL = BN * 4 / 256;  // 16-B loads of B per thread
   bf16x8s ra[2], rb[BL];
+  // implicit conv: the output pixel of each of this thread's two A rows, fixed for the block
+  int pix_img[2], pix_iy[2], pix_ix[2];
+  if constexpr (IMPLICIT) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int gm = m0 + ((tid + i * 256) >> 2);
+      const int hw = cg.Ho * cg.Wo;
+      const int img = gm / hw, r = gm - img * hw, oy = r / cg.Wo, ox = r - oy * cg.Wo;
+      pix_img[i] = gm < M ? img : -1;
+      pix_iy[i] = oy * cg.stride - cg.pad;
+      pix_ix[i] = ox * cg.stride - cg.pad;
+    }
+  }
+  auto tap_ptr = [&](int i, int k) -> const bf16* {  // input address of column k for row i, or null
+    if (k >= cg.Kreal) return nullptr;
+    const int tap = k / cg.C, c = k - tap * cg.C, ky = tap / cg.KW, kx = tap - ky * cg.KW;
+    const int iy = pix_iy[i] + ky, ix = pix_ix[i] + kx;
+    if (iy < 0 || iy >= cg.H || ix < 0 || ix >= cg.W) return nullptr;
+    return X + (((int64_t)pix_img[i] * cg.H + iy) * cg.W + ix) * cg.Cs + c;
+  };
   auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int e = tid + i * 256, row = e >> 2, kc = (e & 3) * 8;
       const int gm = m0 + row;
-      ra[i] = gm < M ? *(const bf16x8s*)(X + (int64_t)gm * K + k0 + kc) : bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr (IMPLICIT) {
+        bf16x8s v = bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+        if (pix_img[i] >= 0) {
+          if (cg.C % 8 == 0) {
+            const bf16* q = tap_ptr(i, k0 + kc);
+            if (q) v = *(const bf16x8s*)q;
+          } else {  // C == 4: two taps of 4 channels
+            typedef short sx4v __attribute__((ext_vector_type(4)));
+            const bf16* q0 = tap_ptr(i, k0 + kc);
+            const bf16* q1 = tap_ptr(i, k0 + kc + 4);
+            const sx4v a = q0 ? *(const sx4v*)q0 : sx4v{0, 0, 0, 0};
+            const sx4v b = q1 ? *(const sx4v*)q1 : sx4v{0, 0, 0, 0};
+            v = bf16x8s{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+          }
+        }
+        ra[i] = v;
+      } else {
+        ra[i] = gm < M ? *(const bf16x8s*)(X + (int64_t)gm * K + k0 + kc) : bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+      }
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
@@ -217,13 +282,13 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int e = tid + i * 256, row = e >> 2, kc = (e & 3) * 8;
-      *(bf16x8s*)(&sA[buf][row * GLDK + kc]) = ra[i];
+      const int e = tid + i * 256, row = e >> 2;
+      *(bf16x8s*)(&sA[buf][gidx(row, e & 3)]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
-      const int e = tid + i * 256, row = e >> 2, kc = (e & 3) * 8;
-      *(bf16x8s*)(&sB[buf][row * GLDK + kc]) = rb[i];
+      const int e = tid + i * 256, row = e >> 2;
+      *(bf16x8s*)(&sB[buf][gidx(row, e & 3)]) = rb[i];
     }
   };
 
@@ -237,38 +302,61 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
   gload(0);
   sstore(0);
   __syncthreads();
-  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  const int fr = lane & 15, fc = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload((kt + 1) * GBK);
     bf16x8s af[4], bfr[TN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8s*)(&sA[cur][(wm * 64 + i * 16 + fr) * GLDK + fk]);
+    for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8s*)(&sA[cur][gidx(wm * 64 + i * 16 + fr, fc)]);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8s*)(&sB[cur][(wn * WN + j * 16 + fr) * GLDK + fk]);
+    for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8s*)(&sB[cur][gidx(wn * WN + j * 16 + fr, fc)]);
+    // operand order W x X: a lane's accumulator holds 4 consecutive output COLUMNS of one row
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
 
-  // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r  (acc[i][j] = A-tile i x B-tile j:
-  // rows from A (M), cols from B (N))
+  // epilogue: acc[i][j][r] = Y[m = .. + (lane & 15)][n = .. + 4 (lane >> 4) + r]: one 8-byte store
+  // per (i, j) where the 4 columns are in range and on the same side of the split
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int gn = n0 + wn * WN + j * 16 + (lane & 15);
-    const float bv = (gn < N && bias) ? bias[gn] : 0.f;
+    const int gn = n0 + wn * WN + j * 16 + 4 * (lane >> 4);
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = (gn + r < N && bias) ? bias[gn + r] : 0.f;
+    const bool lo = gn + 3 < om.split, hi = gn >= om.split && gn + 3 < N;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      const int gm = m0 + wm * 64 + i * 16 + (lane & 15);
+      if (gm >= M) continue;
+      const int64_t img = gm / om.rpi, rr = gm - img * om.rpi;
+      float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int gm = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        if (gm < M && gn < N) {
-          float v = acc[i][j][r] + bv;
-          if (relu) v = fmaxf(v, 0.f);
-          Y[(int64_t)gm * ldy + gn] = (bf16)v;
+        v[r] = acc[i][j][r] + bv[r];
+        if (relu) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (lo && (ldy & 3) == 0 && (om.img_stride & 3) == 0) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)v[r];
+        *(bf16x4*)(Y + img * om.img_stride + rr * ldy + gn) = o;
+      } else if (hi && ((om.ldy2 | (gn - om.split)) & 3) == 0 && (om.img_stride2 & 3) == 0) {
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)v[r];
+        *(bf16x4*)(om.Y2 + img * om.img_stride2 + rr * om.ldy2 + (gn - om.split)) = o;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = gn + r;
+          if (n >= N) break;
+          if (n < om.split) Y[img * om.img_stride + rr * ldy + n] = (bf16)v[r];
+          else om.Y2[img * om.img_stride2 + rr * om.ldy2 + (n - om.split)] = (bf16)v[r];
         }
       }
     }
@@ -285,7 +373,40 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
 // =====================================================================================
 constexpr int DET_MAXP = 2048;
 
-__global__ void __launch_bounds__(256) ssd_class_nms_kernel(const bf16* __restrict__ conf, const bf16* __restrict__ loc,
+// Stage 0: the per-prior class softmax (prototxt mbox_conf_softmax), ONCE per prior: one thread
+// per (image, prior) reads its C logits and writes the C probabilities class-major,
+// prob[n][c][p], so each class block of stage 1 streams one contiguous row (before: every one of
+// the C-1 class blocks recomputed the whole C-way softmax of every prior).
+__global__ void __launch_bounds__(256) ssd_softmax_kernel(const bf16* __restrict__ conf, float* __restrict__ prob,
+                                                           int N, int P, int C) {
+  const int64_t total = (int64_t)N * P;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int n = (int)(i / P), p = (int)(i - (int64_t)n * P);
+    const bf16* row = conf + i * C;
+    float v[32];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (k < C) {
+        v[k] = (float)row[k];
+        mx = fmaxf(mx, v[k]);
+      }
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (k < C) {
+        v[k] = __expf(v[k] - mx);
+        sum += v[k];
+      }
+    const float inv = 1.f / sum;
+    float* o = prob + (int64_t)n * C * P + p;
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (k < C) o[(int64_t)k * P] = v[k] * inv;
+  }
+}
+
+__global__ void __launch_bounds__(256) ssd_class_nms_kernel(const float* __restrict__ prob, const bf16* __restrict__ loc,
                                                              const float* __restrict__ pri, const float* __restrict__ var,
                                                              float* __restrict__ cls_out, int* __restrict__ cls_cnt,
                                                              int P, int C, int bg, float thresh, float nms_thresh,
@@ -301,17 +422,12 @@ __global__ void __launch_bounds__(256) ssd_class_nms_kernel(const bf16* __restri
   const int tid = threadIdx.x;
   if (tid == 0) s_cnt = 0;
   __syncthreads();
-  const bf16* cr = conf + (int64_t)n * P * C;
+  const float* pr = prob + ((int64_t)n * C + c) * P;
   for (int p = tid; p < P; p += 256) {
-    const bf16* row = cr + (int64_t)p * C;
-    float mx = -INFINITY;
-    for (int k = 0; k < C; ++k) mx = fmaxf(mx, (float)row[k]);
-    float s = 0.f;
-    for (int k = 0; k < C; ++k) s += __expf((float)row[k] - mx);
-    const float prob = __expf((float)row[c] - mx) / s;
-    if (prob > thresh) {
+    const float pv = pr[p];
+    if (pv > thresh) {
       const int slot = atomicAdd(&s_cnt, 1);
-      s_score[slot] = prob;
+      s_score[slot] = pv;
       s_idx[slot] = p;
     }
   }
@@ -570,24 +686,53 @@ void vcx_dwconv3x3(const void* x, const void* w, const float* b, void* y, int N,
                      (const bf16*)x, (const bf16*)w, b, (bf16*)y, N, H, W, C, Ho, Wo, stride, relu);
 }
 
-void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
-                       int relu, hipStream_t s) {
+void vcx_gemm_bias_act_mapped(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
+                              int relu, void* Y2, int split, int ldy2, int rpi, int64_t img_stride,
+                              int64_t img_stride2, hipStream_t s) {
+  OutMap om{(bf16*)Y2, split, ldy2, rpi > 0 ? rpi : M, img_stride, img_stride2};
+  ConvGeom cg{};
   if (N <= 64) {
     const int nwg = ((M + GBM - 1) / GBM) * ((N + 63) / 64);
-    hipLaunchKernelGGL(gemm_bias_act_kernel<64>, dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt, bias,
-                       (bf16*)Y, M, N, K, ldy, relu);
+    hipLaunchKernelGGL((gemm_bias_act_kernel<64, false>), dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt,
+                       bias, (bf16*)Y, M, N, K, ldy, relu, om, cg);
   } else {
     const int nwg = ((M + GBM - 1) / GBM) * ((N + 127) / 128);
-    hipLaunchKernelGGL(gemm_bias_act_kernel<128>, dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt, bias,
-                       (bf16*)Y, M, N, K, ldy, relu);
+    hipLaunchKernelGGL((gemm_bias_act_kernel<128, false>), dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt,
+                       bias, (bf16*)Y, M, N, K, ldy, relu, om, cg);
   }
 }
 
-void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* cls_out,
-                    int* cls_cnt, float* out, int* out_cnt, int N, int P, int C, int bg, float thresh,
+// Y [imgs*Ho*Wo, N] = act(conv(x) + bias): x NHWC [imgs, H, W, Cs] (C used channels), weights
+// Wt [N, Kp] with columns (ky, kx, c), Kp % 32 == 0 (zero beyond KH*KW*C)
+void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y, int imgs, int H, int W, int C,
+                       int Cs, int KH, int KW, int stride, int pad, int N, int Kp, int relu, hipStream_t s) {
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  const int M = imgs * Ho * Wo;
+  OutMap om{nullptr, N, 0, M, 0, 0};
+  ConvGeom cg{H, W, C, Cs, Ho, Wo, KW, stride, pad, KH * KW * C};
+  if (N <= 64) {
+    const int nwg = ((M + GBM - 1) / GBM) * ((N + 63) / 64);
+    hipLaunchKernelGGL((gemm_bias_act_kernel<64, true>), dim3(nwg), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt,
+                       bias, (bf16*)Y, M, N, Kp, N, relu, om, cg);
+  } else {
+    const int nwg = ((M + GBM - 1) / GBM) * ((N + 127) / 128);
+    hipLaunchKernelGGL((gemm_bias_act_kernel<128, true>), dim3(nwg), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt,
+                       bias, (bf16*)Y, M, N, Kp, N, relu, om, cg);
+  }
+}
+
+void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
+                       int relu, hipStream_t s) {
+  vcx_gemm_bias_act_mapped(X, Wt, bias, Y, M, N, K, ldy, relu, nullptr, N, 0, M, 0, 0, s);
+}
+
+void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* prob,
+                    float* cls_out, int* cls_cnt, float* out, int* out_cnt, int N, int P, int C, int bg, float thresh,
                     float nms_thresh, int topk, int keep, hipStream_t s) {
-  hipLaunchKernelGGL(ssd_class_nms_kernel, dim3(N * (C - 1)), dim3(256), 0, s, (const bf16*)conf, (const bf16*)loc,
-                     pri, var, cls_out, cls_cnt, P, C, bg, thresh, nms_thresh, topk);
+  hipLaunchKernelGGL(ssd_softmax_kernel, dim3(stream_grid((int64_t)N * P, 256)), dim3(256), 0, s, (const bf16*)conf,
+                     prob, N, P, C);
+  hipLaunchKernelGGL(ssd_class_nms_kernel, dim3(N * (C - 1)), dim3(256), 0, s, prob, (const bf16*)loc, pri, var,
+                     cls_out, cls_cnt, P, C, bg, thresh, nms_thresh, topk);
   hipLaunchKernelGGL(ssd_merge_kernel, dim3(N), dim3(256), 0, s, cls_out, cls_cnt, out, out_cnt, C, bg, topk, keep);
 }
 

@@ -37,8 +37,57 @@ class Engine:
         out, _ = self.process(frames.cpu().numpy(), requester)
         return torch.from_numpy(np.ascontiguousarray(out)).to(frames.device)
 
+    def submit(self, frames, requester):
+        """Start a chunk; the returned job's ``result()`` gives ``process``'s return value.
+        Engines without an asynchronous pipeline compute here."""
+        res = self.process(frames, requester)
+        job = EngineJob(self, None, None, None, None)
+        job.result = lambda: res
+        return job
+
+
+class _Slot:
+    """Pinned host staging for one in-flight chunk (input frames / annotated output)."""
+
+    def __init__(self):
+        self.pin_in = None
+        self.pin_out = None
+        self.h2d_done = None  # event: the pinned input may be refilled
+        self.out_done = None  # event: the annotated chunk is in pin_out
+
+    def buf(self, name, nbytes):
+        b = getattr(self, name)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True)
+            setattr(self, name, b)
+        return b[:nbytes]
+
+
+class EngineJob:
+    """A chunk in flight on the GPU (``DetectorEngine.submit``); ``result()`` waits for it."""
+
+    def __init__(self, engine, slot, out_shape, counts, out_dev):
+        self.engine, self.slot, self.out_shape, self.counts, self.out_dev = engine, slot, out_shape, counts, out_dev
+
+    def result(self):
+        self.slot.out_done.synchronize()
+        n = int(np.prod(self.out_shape))
+        out = self.slot.pin_out[:n].numpy().reshape(self.out_shape)
+        return out, self.counts.cpu().tolist()
+
 
 class DetectorEngine(Engine):
+    """Batched MobileNet-SSD volunteer engine on the GPU (or CPU reference ops).
+
+    Stream-overlapped pipeline (SURVEY.md §2.7 "H2D copy ∥ preprocess ∥ forward ∥ send"):
+    ``submit(chunk)`` copies the frames into one of two pinned staging slots (torch's threaded
+    CPU copy), starts the H2D DMA on a copy stream, and enqueues resize -> blob -> network ->
+    NMS -> annotation -> D2H into pinned output on the compute stream behind an event; it returns
+    at once, so the caller's next chunk is copied and uploaded while this one computes.
+    ``process`` = submit + result (no overlap)."""
+
+    SLOTS = 3  # chunks in flight; a result's pinned output stays valid until SLOTS more submits
+
     def __init__(self, device=None, prototxt=None, caffemodel=None, conf_thresh: float = 0.2, width: int = 400,
                  consider: str = "person"):
         from ..models.mobilenet_ssd import CLASSES, SSDExecutor
@@ -51,49 +100,71 @@ class DetectorEngine(Engine):
         self.width = width
         self.label = CLASSES.index(consider)
         self.consider = consider
-        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        cuda = self.device.type == "cuda"
+        self.stream = torch.cuda.Stream(self.device) if cuda else None
+        self.copy_stream = torch.cuda.Stream(self.device) if cuda else None
+        self._slots = [_Slot() for _ in range(self.SLOTS)] if cuda else []
+        self._next = 0
         self._lock = threading.Lock()
         self.tracer = NULL_TRACER  # set a utils.trace.SpanTracer for per-stage device times
 
     @torch.no_grad()
-    def process(self, frames, requester):
+    def submit(self, frames, requester) -> "EngineJob":
+        """Start a chunk ([n, H, W, 3] uint8 numpy or host tensor); returns an EngineJob."""
+        if self.stream is None:
+            out, counts = self._run(frames, requester)
+            res = (out.cpu().numpy(), counts.cpu().tolist())
+            job = EngineJob(self, None, None, None, None)
+            job.result = lambda: res
+            return job
         with self._lock:
-            if self.stream is not None:
-                with torch.cuda.stream(self.stream):
-                    out, counts = self._run(frames, requester)
-                self.stream.synchronize()
-            else:
-                out, counts = self._run(frames, requester)
-            return out.cpu().numpy(), counts.cpu().tolist()
+            slot = self._slots[self._next]
+            self._next = (self._next + 1) % len(self._slots)
+            a = frames if isinstance(frames, np.ndarray) else frames.numpy()
+            a = np.ascontiguousarray(a)
+            if slot.h2d_done is not None:
+                slot.h2d_done.synchronize()  # this slot's previous upload finished
+            if slot.out_done is not None:
+                slot.out_done.synchronize()  # ... and its previous output was read back
+            pin = slot.buf("pin_in", a.nbytes)
+            pin.copy_(torch.from_numpy(a).view(-1).view(torch.uint8))  # threaded host copy
+            with torch.cuda.stream(self.copy_stream):
+                x = pin.view(a.shape).to(self.device, non_blocking=True)
+                slot.h2d_done = torch.cuda.Event()
+                slot.h2d_done.record(self.copy_stream)
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(slot.h2d_done)
+                x.record_stream(self.stream)
+                out, counts = self._compute(x, requester)
+                po = slot.buf("pin_out", out.numel()).view(out.shape)
+                po.copy_(out, non_blocking=True)
+                slot.out_done = torch.cuda.Event()
+                slot.out_done.record(self.stream)
+            return EngineJob(self, slot, tuple(out.shape), counts, out)
+
+    @torch.no_grad()
+    def process(self, frames, requester):
+        return self.submit(frames, requester).result()
 
     @torch.no_grad()
     def process_tensor(self, frames, requester):
+        """Device-resident chunk in, device-resident annotated chunk out (RCCL / IPC planes)."""
         with self._lock:
-            out, _ = self._run(frames, requester)
+            if self.stream is None:
+                out, _ = self._run(frames, requester)
+                return out
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.stream):
+                out, _ = self._compute(frames.to(self.device), requester)
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
             return out
 
-    def _staging(self, nbytes):
-        """Reusable pinned host buffer: one DMA-able copy per chunk instead of pin_memory()."""
-        buf = getattr(self, "_pinned", None)
-        if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-            self._pinned = buf
-        return buf[:nbytes]
+    def _run(self, frames, requester):  # CPU path / reference
+        x = frames if isinstance(frames, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frames))
+        return self._compute(x.to(self.device), requester)
 
-    def _run(self, frames, requester):
+    def _compute(self, x, requester):
         tr = self.tracer
-        with tr.span("h2d"):
-            if isinstance(frames, torch.Tensor):
-                x = frames.to(self.device)
-            else:
-                a = np.ascontiguousarray(frames)
-                if self.device.type == "cuda":
-                    st = self._staging(a.nbytes)
-                    torch.cuda.current_stream().synchronize()  # previous chunk's H2D done before reuse
-                    st.numpy()[:] = a.reshape(-1)
-                    x = st.view(a.shape).to(self.device, non_blocking=True)
-                else:
-                    x = torch.from_numpy(a)
         with tr.span("resize"):
             small = V.resize_width(x, self.width).contiguous()
         with tr.span("detect"):  # preprocess + MobileNet-SSD forward + decode/NMS

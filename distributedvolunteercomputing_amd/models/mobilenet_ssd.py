@@ -6,9 +6,13 @@ activations for a whole chunk of frames at once:
 
   Convolution group=C (depthwise 3x3)  -> dwconv3x3 kernel (+bias +ReLU fused)
   Convolution 1x1                      -> MFMA GEMM  [N*H*W, Cin] x [Cout, Cin]^T (+bias +ReLU)
-  Convolution kxk (stem, SSD extras)   -> im2col + the same MFMA GEMM
+  Convolution kxk (stem, SSD extras)   -> the same MFMA GEMM as an implicit GEMM (the A tile is
+                                          gathered from the NHWC input while staging: no im2col)
   ReLU after a convolution             -> fused into the producer's epilogue
-  Permute(0,2,3,1) + Flatten           -> free (NHWC is already that order)
+  multibox heads (loc, conf 1x1 convs)
+  + Permute(0,2,3,1) + Flatten + Concat -> ONE GEMM per source (loc||conf weights) whose epilogue
+                                          writes both straight into the mbox_loc / mbox_conf
+                                          concat buffers at the source's offsets
   PriorBox                             -> computed once on the host, cached on the device
   Reshape + Softmax + DetectionOutput  -> one fused softmax/decode/top-k/NMS kernel pair
 
@@ -117,14 +121,75 @@ class SSDExecutor:
         self._plan = self._compile() if self.device.type == "cuda" else None
 
     # ------------------------------------------------------------------ compile
+    def _find_heads(self):
+        """Multibox heads: 1x1 convolutions whose output goes only through Permute(0,2,3,1) ->
+        Flatten into the mbox_loc / mbox_conf Concat (prototxt 1147-1858). Returns
+        {conv index: (concat layer index, position in the concat)} and the layer indices the
+        fused head GEMMs make redundant (the Permute and Flatten layers)."""
+        layers = self.net.layers
+        producer = {}
+        for i, l in enumerate(layers):
+            for t in l.tops:
+                producer[t] = i
+        heads, skip = {}, set()
+        for ci, l in enumerate(layers):
+            if l.type != "Concat" or int(l.p("concat_param", "axis", 1)) != 1:
+                continue
+            chain = []
+            for pos, b in enumerate(l.bottoms):
+                fi = producer.get(b)
+                if fi is None or layers[fi].type != "Flatten":
+                    break
+                pi = producer.get(layers[fi].bottoms[0])
+                if pi is None or layers[pi].type != "Permute":
+                    break
+                cv = producer.get(layers[pi].bottoms[0])
+                if cv is None or layers[cv].type != "Convolution":
+                    break
+                chain.append((cv, pos, fi, pi))
+            else:
+                for cv, pos, fi, pi in chain:
+                    heads[cv] = (ci, pos)
+                    skip.update((fi, pi))
+        return heads, skip
+
     def _compile(self):
         dev = self.device
         plan = []
         layers = self.net.layers
-        consumed = set()
+        heads, consumed = self._find_heads()
+        consumed = set(consumed)
         shapes = {self.net.inputs[0]: 3}  # channels per blob
+        hw = {self.net.inputs[0]: (self.input_size, self.input_size)}  # static spatial sizes
+        head_steps = {}  # source blob -> merged head step
+        concat_cols = {}  # concat index -> [(position, rows per image, cols)]
+        for i, l in enumerate(layers):
+            if l.type == "Convolution" and l.bottoms[0] in hw:
+                k = int(l.p("convolution_param", "kernel_size", 1))
+                st = int(l.p("convolution_param", "stride", 1))
+                pd = int(l.p("convolution_param", "pad", 0))
+                H, W = hw[l.bottoms[0]]
+                hw[l.tops[0]] = ((H + 2 * pd - k) // st + 1, (W + 2 * pd - k) // st + 1)
+            elif l.bottoms and l.bottoms[0] in hw and l.tops and l.tops[0] not in hw:
+                hw[l.tops[0]] = hw[l.bottoms[0]]
         for i, l in enumerate(layers):
             if i in consumed:
+                continue
+            if l.type == "Convolution" and i in heads:
+                # loc || conf of one source: ONE GEMM writing both concat buffers in place
+                w, b = self.ref.conv_weights(l.name)
+                ci, pos = heads[i]
+                src = l.bottoms[0]
+                H, W = hw[src]
+                cout = w.shape[0]
+                concat_cols.setdefault(ci, []).append((pos, H * W, cout))
+                hs = head_steps.get(src)
+                bias = (b.detach().float() if b is not None else torch.zeros(cout))
+                wt = w.detach().float().reshape(cout, -1)
+                if hs is None:
+                    hs = head_steps[src] = dict(parts=[], src=src)
+                    plan.append(("head", l, hs))
+                hs["parts"].append(dict(concat=ci, pos=pos, w=wt, b=bias, cout=cout, rows=H * W))
                 continue
             if l.type == "Convolution":
                 w, b = self.ref.conv_weights(l.name)
@@ -147,12 +212,17 @@ class SSDExecutor:
                     wt = w.detach().float().reshape(cout, cin).to(dev, torch.bfloat16).contiguous()
                     plan.append(("pw", l, dict(w=wt, b=bias, relu=relu)))
                 else:
-                    K = k * k * cin
+                    # implicit GEMM: columns (ky, kx, c); the 3-channel stem reads the 4-channel
+                    # padded blob (c = 3 has zero weights) as two taps per 16-B load
+                    C = 4 if cin == 3 else cin
+                    K = k * k * C
                     Kp = _round_up(K, 32)
+                    wk = torch.zeros(cout, k, k, C)
+                    wk[..., :cin] = w.detach().float().permute(0, 2, 3, 1)
                     wt = torch.zeros(cout, Kp)
-                    wt[:, :K] = w.detach().float().permute(0, 2, 3, 1).reshape(cout, K)
+                    wt[:, :K] = wk.reshape(cout, K)
                     plan.append(("conv", l, dict(w=wt.to(dev, torch.bfloat16).contiguous(), b=bias, k=k,
-                                                 stride=stride, pad=pad, cin=cin, Kp=Kp, relu=relu)))
+                                                 stride=stride, pad=pad, cin=cin, C=C, Kp=Kp, relu=relu)))
                 shapes[l.tops[0]] = cout
             elif l.type == "ReLU":
                 plan.append(("relu", l, {}))
@@ -161,10 +231,34 @@ class SSDExecutor:
                 if order != [0, 2, 3, 1]:
                     raise NotImplementedError(f"{l.name}: permute {order}")
                 plan.append(("nhwc", l, {}))
+            elif l.type == "Concat" and i in concat_cols:
+                plan.append(("concat_buf", l, {"index": i}))
             elif l.type in ("Flatten", "Concat", "PriorBox", "Reshape", "Softmax", "DetectionOutput"):
                 plan.append((l.type.lower(), l, {}))
             else:
                 raise NotImplementedError(f"Caffe layer type {l.type!r} ({l.name})")
+        # concat offsets (per image, in elements) and merged loc||conf weights per source
+        self._concat_total, offs = {}, {}
+        for ci, cols in concat_cols.items():
+            o = 0
+            for pos, rows, cout in sorted(cols):
+                offs[(ci, pos)] = o
+                o += rows * cout
+            self._concat_total[ci] = o
+        for hs in head_steps.values():
+            parts = hs["parts"]
+            if len(parts) != 2:
+                raise NotImplementedError(f"{hs['src']}: expected one loc and one conf head")
+            a, c = parts
+            K = a["w"].shape[1]
+            if K % 32:
+                raise NotImplementedError(f"{hs['src']}: head GEMM needs K % 32 == 0")
+            hs["w"] = torch.cat([a["w"], c["w"]]).to(dev, torch.bfloat16).contiguous()
+            hs["b"] = torch.cat([a["b"], c["b"]]).to(dev)
+            hs["split"] = a["cout"]
+            hs["concats"] = (a["concat"], c["concat"])
+            hs["offs"] = (offs[(a["concat"], a["pos"])], offs[(c["concat"], c["pos"])])
+            hs["rows"] = a["rows"]
         return plan
 
     # ------------------------------------------------------------------ helpers
@@ -198,6 +292,9 @@ class SSDExecutor:
         layout = {self.net.inputs[0]: "nhwc"}
         hw = {self.net.inputs[0]: (blob.shape[1], blob.shape[2])}
         chans = {self.net.inputs[0]: 3}
+        assert blob.shape[1] == self.input_size, "the plan's head offsets are for the prototxt input size"
+        concat_bufs = {ci: torch.empty(N, tot, device=blob.device, dtype=torch.bfloat16)
+                       for ci, tot in self._concat_total.items()}
         for kind, l, p in self._plan:
             src = l.bottoms[0] if l.bottoms else None
             x = t.get(src)
@@ -210,13 +307,18 @@ class SSDExecutor:
                 M = N * H * W
                 y = V.gemm_bias_act(x.reshape(M, x.shape[-1]), p["w"], p["b"], p["relu"])
                 t[top], layout[top], hw[top], chans[top] = y.view(N, H, W, -1), "nhwc", (H, W), y.shape[1]
+            elif kind == "head":
+                x = t[p["src"]]
+                H, W = hw[p["src"]]
+                la, ca = (concat_bufs[c] for c in p["concats"])
+                ops.native().gemm_bias_heads(x.reshape(N * H * W, x.shape[-1]), p["w"], p["b"], la, p["offs"][0],
+                                             ca, p["offs"][1], p["split"], H * W)
+            elif kind == "concat_buf":
+                t[top], layout[top] = concat_bufs[p["index"]], "plain"
             elif kind == "conv":
-                H, W = hw[src]
                 k, s, pd = p["k"], p["stride"], p["pad"]
-                Ho, Wo = (H + 2 * pd - k) // s + 1, (W + 2 * pd - k) // s + 1
-                cols = V.im2col_nhwc(x, p["cin"], k, s, pd, p["Kp"])
-                y = V.gemm_bias_act(cols, p["w"], p["b"], p["relu"]).view(N, Ho, Wo, -1)
-                t[top], layout[top], hw[top], chans[top] = y, "nhwc", (Ho, Wo), y.shape[3]
+                y = ops.native().conv_implicit(x.contiguous(), p["w"], p["b"], p["C"], k, k, s, pd, p["relu"])
+                t[top], layout[top], hw[top], chans[top] = y, "nhwc", (y.shape[1], y.shape[2]), y.shape[3]
             elif kind == "relu":
                 t[top] = torch.relu(x)
                 layout[top], hw[top], chans[top] = layout[src], hw.get(src), chans.get(src)

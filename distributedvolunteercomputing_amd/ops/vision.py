@@ -223,19 +223,26 @@ def _draw_np(frame, dets, nd, label, thresh, name_mask, name_xy, lab_masks, lab_
     return count
 
 
+_MASKS: dict = {}
+
+
 def annotate(frames, dets, counts, requester: str, *, label=15, cls_name="person", thresh=0.2):
     """In-place: boxes for `label` detections with conf > thresh, requester name at (10,25),
     "<cls>: k" at (10, h-20) (cv2.putText origins are text baselines). Returns per-frame counts."""
     h = frames.shape[1]
-    nm = text_mask(requester)
-    lm = label_masks(cls_name)
+    dev = frames.device
+    key = (requester, cls_name, str(dev))
+    masks = _MASKS.get(key)
+    if masks is None:  # rasterised (and uploaded) once per (requester, class, device), not per chunk
+        nm, lm = text_mask(requester), label_masks(cls_name)
+        masks = _MASKS[key] = (nm, lm, torch.from_numpy(nm).to(dev), torch.from_numpy(lm).to(dev))
+    nm, lm, nm_d, lm_d = masks
     name_xy = (10, 25 - nm.shape[0] + 2)
     lab_xy = (10, h - 20 - lm.shape[1] + 2)
     if use_native(frames):
-        dev = frames.device
         return native().annotate(frames, dets.contiguous(), counts.to(torch.int32).contiguous(), label, thresh,
-                                 _pack_bgr(BLUE), torch.from_numpy(nm).to(dev), name_xy[0], name_xy[1],
-                                 _pack_bgr(RED), torch.from_numpy(lm).to(dev), lab_xy[0], lab_xy[1], _pack_bgr(GREEN))
+                                 _pack_bgr(BLUE), nm_d, name_xy[0], name_xy[1],
+                                 _pack_bgr(RED), lm_d, lab_xy[0], lab_xy[1], _pack_bgr(GREEN))
     fr = frames.numpy()
     dn = dets.numpy()
     cn = counts.numpy()
