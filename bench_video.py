@@ -74,12 +74,15 @@ def bench_engine(args, dev):
             "net_tflops": round(gflop / net_ms, 2), "out_shape": list(out.shape)}
 
 
-def bench_job(args, dev):
+def bench_job(args, dev, plane="relay"):
+    """The whole volunteer job on one GPU: a requester and `workers` volunteers in this process.
+    ``relay``: chunk bytes through the coordinator (reference topology); ``p2p``: metadata through
+    the coordinator, chunk bytes over pair groups (gloo here: the volunteers share one GPU)."""
     from distributedvolunteercomputing_amd.control.coordinator import coordinator
     from distributedvolunteercomputing_amd.control.peer import client
     from distributedvolunteercomputing_amd.jobs.video import DetectorEngine
 
-    coord = coordinator("127.0.0.1", 0, ephemeral_ports=True, credits=2)
+    coord = coordinator("127.0.0.1", 0, ephemeral_ports=True, credits=2, data_plane=plane)
     eng = DetectorEngine(device=dev)  # one GPU: volunteers share one engine (serialised by a lock)
     tmp = tempfile.mkdtemp(prefix="vcx_video_")
     req = client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0, engine=eng, out_dir=tmp,
@@ -94,8 +97,9 @@ def bench_job(args, dev):
         for c in [req] + workers:
             c.exit_threads()
         coord.exit_threads()
-    return {"job_time_s": round(t, 3) if t else None, "job_frames": n,
-            "job_frames_per_s": round(n / t, 1) if t else None, "workers": args.workers}
+    pre = "job" if plane == "relay" else f"job_{plane}"
+    return {f"{pre}_time_s": round(t, 3) if t else None, f"{pre}_frames": n,
+            f"{pre}_frames_per_s": round(n / t, 1) if t else None, "workers": args.workers}
 
 
 def main():
@@ -108,14 +112,17 @@ def main():
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--workers", type=int, default=2)
     ap.add_argument("--no-job", action="store_true")
+    ap.add_argument("--data-plane", default="both", choices=["relay", "p2p", "both"])
     a = ap.parse_args()
     dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     rec = {"metric": "MobileNet-SSD video job (reference parity)", "unit": "frames/s", "dtype": "bf16",
            "data": "synthetic 1280x720 frames, random-init weights", "chunk": a.chunk}
     rec.update(bench_engine(a, dev))
     if not a.no_job:
-        rec.update(bench_job(a, dev))
-    rec["value"] = rec.get("job_frames_per_s") or rec["engine_frames_per_s"]
+        for plane in (("relay", "p2p") if a.data_plane == "both" else (a.data_plane,)):
+            rec.update(bench_job(a, dev, plane))
+    rec["value"] = max([rec.get(k) or 0 for k in ("job_frames_per_s", "job_p2p_frames_per_s")]) or \
+        rec["engine_frames_per_s"]
     print(json.dumps(rec), flush=True)
 
 

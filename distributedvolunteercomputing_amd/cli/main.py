@@ -91,41 +91,31 @@ def train_main(argv=None):
 
 
 def video_main(argv=None):
-    """Video job on the RCCL/xGMI data plane: run under torchrun, one rank per GPU; rank 0 is
-    the requester, every other rank a worker volunteer."""
-    import datetime
+    """One-node video job, one process per GPU (torchrun): rank 0 hosts the coordinator on the
+    p2p data plane and requests; every other rank is a worker volunteer (control/node_job.py)."""
     import os
 
     import torch
-    import torch.distributed as dist
 
     ap = argparse.ArgumentParser(prog="video", description=video_main.__doc__)
     ap.add_argument("--source", default="synthetic:1000:1280x720")
-    ap.add_argument("--out", default="video0.y4m")
+    ap.add_argument("--out-dir", default=".")
+    ap.add_argument("--out-ext", default=".y4m", choices=[".y4m", ".npy", ""])
     ap.add_argument("--chunk", type=int, default=100)
+    ap.add_argument("--port", type=int, default=9999, help="coordinator UDP control port")
     ap.add_argument("--store-port", type=int, default=int(os.environ.get("VCX_STORE_PORT", "29612")))
     a = ap.parse_args(argv)
+    from ..control.node_job import run_node_job
     from ..jobs.video import DetectorEngine
-    from ..jobs.video_dist import run_requester, run_worker
-    from ..parallel.peer_group import PeerGroup
 
-    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    cuda = torch.cuda.is_available()
-    dev = torch.device("cuda", local) if cuda else torch.device("cpu")
-    if cuda:
+    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
         torch.cuda.set_device(dev)
-    store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), a.store_port, None, rank == 0,
-                          timeout=datetime.timedelta(seconds=300), wait_for_workers=False)
-    g = PeerGroup(store, rank, world, "nccl" if cuda else "gloo", device=dev) if world > 1 else None
-    eng = DetectorEngine(device=dev)
-    if rank == 0:
-        st = run_requester(g, a.source, a.out, dev, chunk=a.chunk, engine=eng)
-        print(st, flush=True)
-    else:
-        run_worker(g, eng, dev)
-    if g is not None:
-        g.barrier()
+    res = run_node_job(a.source, a.out_dir, engine_factory=lambda: DetectorEngine(device=dev), chunk=a.chunk,
+                       control_port=a.port, store_port=a.store_port, out_ext=a.out_ext)
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(res, flush=True)
     return 0
 
 

@@ -16,6 +16,12 @@ What happens where:
   (the reference shares one REQ socket between two threads).
 * lease monitor                         — expires silent volunteers, re-queues their chunks.
 
+Data planes (``data_plane=``): ``relay`` moves chunk bytes through this process like the
+reference (host TCP, for CPU-only volunteers); ``p2p`` moves only metadata through it — chunks go
+requester -> worker and back over directional pair groups (control/p2p.py: RCCL over xGMI between
+GPU volunteers), the coordinator tells both ends of each transfer when to post it, keeps the
+leases and re-dispatches a dead worker's chunks exactly as on the relay plane.
+
 All mutable state is per instance (the reference keeps it in class attributes shared by every
 instance, server.py:13-24).
 """
@@ -29,14 +35,20 @@ import threading
 import time
 from collections import deque
 
+import numpy as np
+
 from .. import _native_loader
 from ..utils.metrics import Metrics
 from . import protocol
 from .transport import BadFrame, FrameHub, FrameSender
 
 
+_EMPTY = np.zeros(0, dtype=np.uint8)  # payload of a metadata-only frame
+
+
 class _Volunteer:
-    def __init__(self, addr, port, hub, sender):
+    def __init__(self, addr, port, hub, sender, vid=0):
+        self.vid = vid
         self.addr = addr
         self.port = port
         self.hub = hub
@@ -60,9 +72,14 @@ class coordinator:  # noqa: N801  (reference class name)
     def __init__(self, ip: str = "localhost", control_port: int = protocol.DEFAULT_CONTROL_PORT, *,
                  ephemeral_ports: bool = False, max_clients: int | None = None, policy: str = "round_robin",
                  credits: int = 2, lease_s: float | None = None, verbose: bool | None = None,
-                 train_store_port: int | None = None):
+                 train_store_port: int | None = None, data_plane: str = "relay"):
         if verbose is not None:
             self.verbose = verbose
+        if data_plane not in ("relay", "p2p"):
+            raise ValueError(f"data_plane must be 'relay' or 'p2p', not {data_plane!r}")
+        self.data_plane = data_plane
+        if data_plane == "p2p" and train_store_port is None:
+            train_store_port = 0  # the pair groups rendezvous on this process's store
         # Rendezvous store for training peers (heartbeats, generations, RCCL bootstrap). Hosted
         # here so that ANY training peer may die without taking the membership state with it.
         self.train_store = None
@@ -87,6 +104,7 @@ class coordinator:  # noqa: N801  (reference class name)
         self.chunks: dict[int, tuple] = {}
         self.requesters: set[str] = set()
         self._ids = itertools.count(1)
+        self._vids = itertools.count(1)
         self._lock = threading.RLock()
         self._work = threading.Condition()
         self.metrics = Metrics("coordinator")
@@ -137,7 +155,7 @@ class coordinator:  # noqa: N801  (reference class name)
                 self.metrics.incr("spoofed_datagrams")
                 return f"err{protocol.SEP}address {addr} does not match sender {src[0]}".encode()
             return self._join(addr, now)
-        if verb in ("request", "stop", "end", "hb"):
+        if verb in ("request", "stop", "end", "hb", "p2p"):
             with self._lock:
                 known = addr in self.vols
             if not known or (src is not None and not protocol.addr_matches(addr, src[0])):
@@ -163,6 +181,12 @@ class coordinator:  # noqa: N801  (reference class name)
             return protocol.reply_ok(json.dumps(self.status()))
         if verb == "store":  # where training peers rendezvous
             return protocol.reply_ok(str(self.train_store_port) if self.train_store is not None else "")
+        if verb == "p2p":
+            with self._lock:
+                v = self.vols.get(addr)
+            info = {"plane": self.data_plane, "vid": v.vid if v is not None else None,
+                    "store_port": self.train_store_port if self.data_plane == "p2p" else None}
+            return protocol.reply_ok(json.dumps(info))
         return None
 
     def _join(self, addr, now):
@@ -183,7 +207,7 @@ class coordinator:  # noqa: N801  (reference class name)
                 hub.close()
                 self.free_ports.appendleft(0 if self.ephemeral else port)
                 raise
-            v = _Volunteer(addr, port, hub, sender)
+            v = _Volunteer(addr, port, hub, sender, vid=next(self._vids))
             self.vols[addr] = v
             self.port_to_client[port] = addr
             for fn, nm in ((self._ingest, "ingest"), (self._outbox, "outbox")):
@@ -201,6 +225,9 @@ class coordinator:  # noqa: N801  (reference class name)
             v = self.vols.pop(addr, None)
             self.requesters.discard(addr)
         requeued = self.sched.remove_worker(addr)
+        if v is not None:
+            self.metrics.incr("leaves_" + reason)
+        self.metrics.counters["redispatched"] = self.sched.requeued  # by removal and by lease expiry
         dropped = self.sched.cancel_requester(addr)
         if dropped:  # its queued chunks will never be dispatched: free their frames
             with self._lock:
@@ -210,21 +237,24 @@ class coordinator:  # noqa: N801  (reference class name)
         if v is None:
             return
         v.alive = False
+        if self.data_plane == "p2p":  # every other volunteer aborts its pair groups with this one
+            with self._lock:
+                others = list(self.vols.values())
+            for o in others:
+                o.outbox.put(("coordinator||peer_dead", _EMPTY, {"p2p": 1, "cmd": "peer_dead", "vid": v.vid}))
         self.port_to_client.pop(v.port, None)
         self.free_ports.append(0 if self.ephemeral else v.port)
         v.outbox.put(None)
         v.hub.close()
         v.sender.close()
-        self.metrics.incr("leaves_" + reason)
         if requeued:
-            self.metrics.incr("redispatched", len(requeued))
             self.log(f"{addr} left ({reason}); re-queued chunks {requeued}")
         self._kick()
 
     def _lease_monitor(self):
         while self.continue_listening:
             time.sleep(max(0.05, self.lease_s / 4))
-            for addr in self.sched.expire(time.time(), self.lease_s):
+            for addr in self.sched.expire(time.time(), self.lease_s):  # drops them, re-queues their chunks
                 self.log(f"lease expired: {addr}")
                 self._remove(addr, reason="lease")
 
@@ -246,12 +276,15 @@ class coordinator:  # noqa: N801  (reference class name)
             if len(parts) < 2:
                 continue
             requester, command = parts[0], parts[1]
+            p2p = bool(hdr.get("p2p"))
             if command == "request":
                 while self.req_rep and self.sched.queued() > self.max_buffer and v.alive:
                     time.sleep(0.005)  # back-pressure: the hub stops acking, TCP throttles the requester
                 cid = next(self._ids)
                 with self._lock:
-                    self.chunks[cid] = (info, arr)
+                    # p2p: metadata only — the frames stay in the requester's (GPU) memory
+                    self.chunks[cid] = (info, None, {"key": hdr.get("key"), "cshape": hdr.get("cshape"),
+                                                     "src": v.vid}) if p2p else (info, arr, None)
                 self.sched.submit(cid, requester)
                 self.metrics.incr("chunks_in")
                 self._kick()
@@ -259,12 +292,22 @@ class coordinator:  # noqa: N801  (reference class name)
                 cid = int(hdr.get("chunk", -1))
                 if not self.sched.complete(cid):
                     self.metrics.incr("duplicate_results")
+                    if p2p:  # the worker holds the duplicate result: let it free it
+                        v.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "drop", "chunk": cid}))
                     continue  # late duplicate of a re-dispatched chunk
                 with self._lock:
-                    self.chunks.pop(cid, None)
+                    rec = self.chunks.pop(cid, None)
                     dst = self.vols.get(requester)
                 if dst is not None:
-                    dst.outbox.put((info, arr, {"chunk": cid}))
+                    if p2p:  # both ends post the transfer of the result: worker -> requester
+                        key = rec[2]["key"] if rec is not None and rec[2] else None
+                        v.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "send_result", "chunk": cid, "dst": dst.vid}))
+                        dst.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "recv_result", "chunk": cid, "src": v.vid,
+                                                       "cshape": hdr.get("cshape"), "key": key}))
+                    else:
+                        dst.outbox.put((info, arr, {"chunk": cid}))
+                elif p2p:
+                    v.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "drop", "chunk": cid}))
                 self.metrics.incr("chunks_done")
                 self._kick()
 
@@ -295,14 +338,26 @@ class coordinator:  # noqa: N801  (reference class name)
             with self._lock:
                 item = self.chunks.get(a.chunk)
                 v = self.vols.get(a.worker)
+                r = self.vols.get(a.requester)
             if item is None:
                 self.sched.complete(a.chunk)
                 continue
             if v is None:
                 self.sched.requeue_front(a.chunk, a.requester)
                 continue
-            info, arr = item
-            v.outbox.put((info, arr, {"chunk": a.chunk}))
+            info, arr, meta = item
+            if meta is None:
+                v.outbox.put((info, arr, {"chunk": a.chunk}))
+            elif r is None:  # the requester left: nobody holds the frames any more
+                self.sched.complete(a.chunk)
+                with self._lock:
+                    self.chunks.pop(a.chunk, None)
+                continue
+            else:  # p2p: the worker posts the receive, the requester the send, of the same chunk
+                v.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "work", "chunk": a.chunk, "src": meta["src"],
+                                             "cshape": meta["cshape"], "key": meta["key"]}))
+                r.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "send", "chunk": a.chunk, "dst": v.vid,
+                                             "key": meta["key"]}))
             self.metrics.incr("dispatched")
         self.log("send_request terminated.")
 
@@ -315,6 +370,7 @@ class coordinator:  # noqa: N801  (reference class name)
             "inflight": self.sched.inflight(),
             "dispatched": self.sched.dispatched,
             "free_ports": len(self.free_ports),
+            "data_plane": self.data_plane,
             "metrics": self.metrics.snapshot(),
         }
 

@@ -1,0 +1,169 @@
+"""Peer-to-peer chunk data plane of the volunteer video job.
+
+The reference relays every chunk through the coordinator: requester -> coordinator -> worker
+-> coordinator -> requester, four host hops per chunk (/root/reference/server.py:48-62,73,89;
+worker.py:157,164-178). On the p2p plane the coordinator only moves METADATA (which chunk goes
+to which worker, leases, re-dispatch); the chunk bytes travel once from the requester's memory
+to the worker's and the annotated chunk once back, over a **directional pair group** per
+(sender, receiver) volunteer pair:
+
+* RCCL (``ProcessGroupNCCL``, one rank per GPU) between GPU volunteers: the chunk goes
+  requester GPU -> worker GPU over xGMI and never touches the host on either side;
+* gloo between CPU volunteers (and in the CPU tests).
+
+Pairs are created lazily, from the coordinator-hosted rendezvous store, by the two volunteers
+involved only (no global generation: a dead or slow volunteer never blocks the others), and
+each pair carries ONE direction so that a worker's result send and the requester's next chunk
+send can never wait on each other across one ordered communicator. Every pair runs its
+operations in order on its own thread, in the order the coordinator's instructions arrive
+(per-volunteer FIFO outboxes: both ends see the same order), and tags them with the chunk id.
+A pair whose peer the coordinator declares dead is aborted (its watch trips: RCCL
+``ncclCommAbort``; a gloo wait is abandoned), so a transfer to a crashed worker never blocks
+the requester's transfers to the others, and the re-dispatched chunk goes out on another pair.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+import time
+
+import torch
+
+from ..parallel.peer_group import PeerFailure, PeerGroup
+
+
+class _PairWatch:
+    """The ``watch`` protocol of PeerGroup guarded waits, tripped by a peer_dead notice."""
+
+    def __init__(self, pid):
+        self.pid = pid
+        self._ev = threading.Event()
+        self._reason = ""
+
+    def tripped(self) -> bool:
+        return self._ev.is_set()
+
+    def abort_reason(self) -> str:
+        return self._reason
+
+    def declare_abort(self, reason: str):
+        self._reason = reason
+        self._ev.set()
+
+
+class _Pair:
+    def __init__(self, plane, src: int, dst: int):
+        self.plane = plane
+        self.src, self.dst = src, dst
+        self.watch = _PairWatch(plane.vid)
+        self.q: queue.Queue = queue.Queue()
+        self.group = None
+        self.dead = False
+        self.thread = threading.Thread(target=self._loop, name=f"vcx-p2p-{src}>{dst}", daemon=True)
+        self.thread.start()
+
+    def _group(self):
+        if self.group is None:
+            rank = 0 if self.plane.vid == self.src else 1
+            # a store client of its own: a c10d TCPStore client serialises its blocking waits, so
+            # one pair stuck rendezvousing with a dead peer would stall every other pair's connect
+            store = self.plane.store_factory()
+            name = f"p2p/{self.src}>{self.dst}"
+            # non-blocking handshake first: the communicator is built only once both ends are
+            # known to be up, so a peer that never shows (crashed before its first transfer)
+            # leaves no rendezvous blocked inside c10d — the wait below is abortable
+            store.set(f"vcx/{name}/hello{rank}", "1")
+            while not store.check([f"vcx/{name}/hello{1 - rank}"]):
+                if self.watch.tripped():
+                    raise PeerFailure(f"pair {name}: {self.watch.abort_reason()}")
+                time.sleep(0.002)
+            g = PeerGroup(store, rank, 2, self.plane.backend, generation=name, device=self.plane.device,
+                          timeout_s=self.plane.timeout_s, watch=self.watch)
+            g.connect()
+            self.group = g
+        return self.group
+
+    def _loop(self):
+        while True:
+            op = self.q.get()
+            if op is None:
+                return
+            kind, payload, tag, cb = op
+            if self.dead:
+                cb(PeerFailure(f"pair {self.src}>{self.dst} is dead"))
+                continue
+            try:
+                g = self._group()
+                if kind == "send":
+                    g.send(payload, 1, tag)
+                    cb(None)
+                else:
+                    shape, dtype = payload
+                    buf = torch.empty(shape, dtype=dtype, device=self.plane.device)
+                    g.recv(buf, 0, tag)
+                    cb(buf)
+            except PeerFailure as e:
+                self.dead = True
+                self.plane.metrics_incr("p2p_failed")
+                cb(e)
+            except Exception as e:  # noqa: BLE001 — a transport error fails this pair only
+                self.dead = True
+                self.plane.metrics_incr("p2p_failed")
+                cb(e)
+
+    def close(self):
+        self.q.put(None)
+
+
+class PairPlane:
+    """Directional pair groups of one volunteer (id ``vid``) over a shared rendezvous store
+    (``store_factory()`` returns a new client connection to it)."""
+
+    def __init__(self, store_factory, vid: int, backend: str = "gloo", device=None, timeout_s: float = 60.0,
+                 metrics=None):
+        self.store_factory = store_factory  # -> a fresh client of the coordinator-hosted store
+        self.vid = int(vid)
+        self.backend = backend
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.timeout_s = timeout_s
+        self.metrics = metrics
+        self._pairs: dict[tuple[int, int], _Pair] = {}
+        self._lock = threading.Lock()
+
+    def metrics_incr(self, name):
+        if self.metrics is not None:
+            self.metrics.incr(name)
+
+    def _pair(self, src: int, dst: int) -> _Pair:
+        with self._lock:
+            p = self._pairs.get((src, dst))
+            if p is None:
+                p = self._pairs[(src, dst)] = _Pair(self, src, dst)
+            return p
+
+    def send(self, dst: int, tensor: torch.Tensor, tag: int, cb=None):
+        """Queue `tensor` for volunteer `dst` (it must post the matching recv with this tag)."""
+        t = tensor.contiguous()
+        if t.device != self.device:
+            t = t.to(self.device)
+        self._pair(self.vid, dst).q.put(("send", t, int(tag) % (1 << 30), cb or (lambda _r: None)))
+
+    def recv(self, src: int, shape, dtype, tag: int, cb):
+        """Queue a receive from volunteer `src`; ``cb(tensor)`` on arrival, ``cb(exception)`` on failure."""
+        self._pair(src, self.vid).q.put(("recv", (tuple(shape), dtype), int(tag) % (1 << 30), cb))
+
+    def peer_dead(self, vid: int):
+        """The coordinator declared `vid` dead: abort every pair with it (in-flight ops fail fast)."""
+        with self._lock:
+            pairs = [p for (s, d), p in self._pairs.items() if vid in (s, d)]
+        for p in pairs:
+            p.dead = True
+            p.watch.declare_abort(f"volunteer {vid} declared dead by the coordinator")
+
+    def close(self):
+        with self._lock:
+            pairs = list(self._pairs.values())
+            self._pairs.clear()
+        for p in pairs:
+            p.watch.declare_abort("plane closed")
+            p.close()

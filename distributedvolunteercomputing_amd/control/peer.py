@@ -15,9 +15,19 @@ Behavioural fixes, each deliberate:
 * frames are pre-resized to the 400-px annotation width on the requester (the worker would
   resize them anyway, worker.py:243), cutting the uplink ~10x for 720p input;
 * heartbeats keep the lease alive; a dead worker's chunks are re-dispatched by the coordinator.
+
+Data planes: on a ``relay`` coordinator chunk bytes go through the coordinator (host TCP, as in
+the reference). On a ``p2p`` coordinator (``coordinator(data_plane="p2p")``) only metadata does:
+the requester keeps each chunk in its own memory (on its GPU after the batched pre-resize) and,
+when the coordinator says "send chunk c to volunteer w", posts the transfer on the pair group
+requester>w (control/p2p.py; RCCL between GPU volunteers, gloo otherwise) while w posts the
+matching receive; the annotated chunk comes back the same way, straight from the worker's GPU.
+The requester frees a chunk when its result arrives, so a chunk whose worker died is still in
+hand when the coordinator re-dispatches it.
 """
 from __future__ import annotations
 
+import json
 import os
 import queue
 import threading
@@ -32,6 +42,8 @@ from ..ops import vision as V
 from ..utils.metrics import Metrics
 from . import protocol
 from .transport import FrameHub, FrameSender
+
+_EMPTY = np.zeros(0, dtype=np.uint8)
 
 
 class client:  # noqa: N801 (reference class name)
@@ -50,7 +62,7 @@ class client:  # noqa: N801 (reference class name)
     def __init__(self, server_ip: str = "localhost", own_ip: str = "localhost", *,
                  control_port: int = protocol.DEFAULT_CONTROL_PORT, my_port: int | str | None = None,
                  engine: Engine | None = None, out_dir: str = ".", out_ext: str = ".y4m",
-                 verbose: bool | None = None, chunk: int | None = None):
+                 verbose: bool | None = None, chunk: int | None = None, p2p_backend: str | None = None):
         if verbose is not None:
             self.verbose = verbose
         if chunk is not None:
@@ -73,6 +85,12 @@ class client:  # noqa: N801 (reference class name)
         self.connect_to_port = self.ctrl.call("join", self.my_ip)
         self.sender = FrameSender(f"tcp://{server_ip}:{self.connect_to_port}", REQ_REP=self.req_rep)
         self.log(f"joined {server_ip}:{control_port}; uplink port {self.connect_to_port}, data port {self.hub.port}")
+        self.plane = None
+        self._outgoing: dict[int, object] = {}  # p2p: chunk key -> frames held until the result is in
+        self._results: dict[int, object] = {}  # p2p: chunk id -> annotated chunk until told where to send it
+        self._p2p_lock = threading.Lock()
+        self._keys = iter(range(1, 1 << 62))
+        self._setup_plane(server_ip, p2p_backend)
 
         # job state (requester role)
         self.path_out_num = 0
@@ -95,6 +113,32 @@ class client:  # noqa: N801 (reference class name)
             t.start()
             self._threads.append(t)
         self._req_thread = None
+
+    def _setup_plane(self, server_ip, backend):
+        try:
+            info = json.loads(self.ctrl.call("p2p", self.my_ip, retries=3) or "{}")
+        except (TimeoutError, ValueError):
+            info = {}
+        if info.get("plane") != "p2p":
+            return
+        import datetime
+
+        import torch.distributed as dist
+
+        from .p2p import PairPlane
+
+        host = server_ip if server_ip not in ("", "localhost") else "127.0.0.1"
+        port = int(info["store_port"])
+
+        def store():
+            return dist.TCPStore(host, port, None, False, timeout=datetime.timedelta(seconds=60))
+        if backend is None:
+            # RCCL needs one GPU per volunteer; volunteers sharing a device (or none) use gloo
+            backend = os.environ.get("VCX_P2P_BACKEND") or (
+                "nccl" if torch.cuda.is_available() and torch.cuda.device_count() > 1 else "gloo")
+        dev = self.resize_device if backend == "nccl" else torch.device("cpu")
+        self.plane = PairPlane(store, int(info["vid"]), backend=backend, device=dev, metrics=self.metrics)
+        self.log(f"p2p data plane: volunteer id {self.plane.vid}, {backend} pair groups on {dev}")
 
     # ------------------------------------------------------------------ engine
     def _get_engine(self) -> Engine:
@@ -170,9 +214,18 @@ class client:  # noqa: N801 (reference class name)
             if self.preresize and self.resize_device is not None and chunk.shape[2] != 400:
                 # one batched resize kernel per chunk on this volunteer's GPU: ~10x less uplink
                 t = torch.from_numpy(chunk).to(self.resize_device, non_blocking=True)
-                chunk = V.resize_width(t, 400).cpu().numpy()
+                chunk = V.resize_width(t, 400)
+                if self.plane is None or self.plane.device.type != "cuda":
+                    chunk = chunk.cpu().numpy()  # else: it stays on this GPU until sent over RCCL
             info = f"{self.my_ip}||request||{'-'.join(map(str, nums))}||{chunk.shape[1]}||{chunk.shape[2]}"
-            if not self.sender.send_image(info, chunk):
+            if self.plane is not None:  # p2p: the chunk stays here; the coordinator gets its metadata
+                key = next(self._keys)
+                with self._p2p_lock:
+                    self._outgoing[key] = chunk if isinstance(chunk, torch.Tensor) else torch.from_numpy(chunk)
+                ok = self.sender.send_image(info, _EMPTY, p2p=1, key=key, cshape=list(chunk.shape))
+            else:
+                ok = self.sender.send_image(info, chunk)
+            if not ok:
                 self.log("uplink send failed")
             self.metrics.incr("chunks_sent")
             frames.clear()
@@ -201,6 +254,9 @@ class client:  # noqa: N801 (reference class name)
             if r is None:
                 continue
             hdr, arr, _ = r
+            if hdr.get("p2p"):
+                self._p2p_command(hdr)
+                continue
             parts = hdr["msg"].split("||")
             requester, command = parts[0], parts[1]
             nums = [int(x) for x in parts[2].split("-")] if parts[2] else []
@@ -212,6 +268,57 @@ class client:  # noqa: N801 (reference class name)
                     continue
                 for i, n in enumerate(nums):
                     self.sink.push(n, arr[i])
+
+    def _p2p_command(self, hdr):
+        """One coordinator instruction of the p2p plane (see the module docstring)."""
+        cmd, cid = hdr.get("cmd"), int(hdr.get("chunk", -1))
+        plane = self.plane
+        if plane is None:
+            return
+        if cmd == "peer_dead":
+            plane.peer_dead(int(hdr["vid"]))
+        elif cmd == "send":  # requester: chunk `key` -> worker `dst`
+            with self._p2p_lock:
+                t = self._outgoing.get(int(hdr["key"]))
+            if t is not None:
+                plane.send(int(hdr["dst"]), t, cid)
+        elif cmd == "work":  # worker: receive the chunk, then infer it
+            msg = hdr["msg"]
+
+            def got(buf, hdr=hdr, msg=msg):
+                if isinstance(buf, BaseException):
+                    self.metrics.incr("p2p_recv_failed")
+                    return
+                parts = msg.split("||")
+                nums = [int(x) for x in parts[2].split("-")] if parts[2] else []
+                self.work_q.put(({"chunk": cid, "p2p": 1}, buf, parts[0], nums))
+            plane.recv(int(hdr["src"]), hdr["cshape"], torch.uint8, cid, got)
+        elif cmd == "send_result":  # worker: annotated chunk -> requester `dst`
+            with self._p2p_lock:
+                t = self._results.pop(cid, None)
+            if t is not None:
+                plane.send(int(hdr["dst"]), t, cid)
+        elif cmd == "recv_result":  # requester: annotated chunk from worker `src`
+            key, msg = hdr.get("key"), hdr["msg"]
+
+            def done(buf, key=key, msg=msg):
+                if isinstance(buf, BaseException):
+                    self.metrics.incr("p2p_recv_failed")
+                    return
+                with self._p2p_lock:
+                    self._outgoing.pop(int(key), None)
+                parts = msg.split("||")
+                nums = [int(x) for x in parts[2].split("-")] if parts[2] else []
+                if self.sink is None or parts[0] != self.my_ip:
+                    return
+                self.metrics.incr("chunks_returned")
+                out = buf.cpu().numpy()
+                for i, n in enumerate(nums):
+                    self.sink.push(n, out[i])
+            plane.recv(int(hdr["src"]), hdr["cshape"], torch.uint8, cid, done)
+        elif cmd == "drop":  # a duplicate result of a re-dispatched chunk: nobody wants it
+            with self._p2p_lock:
+                self._results.pop(cid, None)
 
     # ------------------------------------------------------------------ worker role
     def worker(self):
@@ -226,6 +333,9 @@ class client:  # noqa: N801 (reference class name)
                 item = None
             if item is not None:
                 hdr, arr, requester, nums = item
+                if hdr.get("p2p") and arr.device.type != "cpu":  # device-resident in and out
+                    self._finish_p2p(hdr, arr, requester, nums)
+                    continue
                 job = self._get_engine().submit(arr, requester)
                 nxt = (job, hdr, requester, nums, time.perf_counter())
             else:
@@ -241,8 +351,28 @@ class client:  # noqa: N801 (reference class name)
         out, counts = job.result()
         self.metrics.observe("chunk_infer_ms", (time.perf_counter() - t0) * 1e3)
         self.metrics.incr("frames_processed", len(nums))
+        if hdr.get("p2p"):  # host chunk from a gloo pair: held (copied out of the pinned slot)
+            self._post_result(hdr, torch.from_numpy(np.array(out)), requester, nums)
+            return
         info = f"{requester}||processed||{'-'.join(map(str, nums))}||{out.shape[1]}||{out.shape[2]}"
         self.sender.send_image(info, out, chunk=hdr.get("chunk", -1))
+
+    def _finish_p2p(self, hdr, t, requester, nums):
+        t0 = time.perf_counter()
+        out = self._get_engine().process_tensor(t, requester)
+        if out.device != self.plane.device:
+            out = out.to(self.plane.device)
+        self.metrics.observe("chunk_infer_ms", (time.perf_counter() - t0) * 1e3)
+        self.metrics.incr("frames_processed", len(nums))
+        self._post_result(hdr, out, requester, nums)
+
+    def _post_result(self, hdr, out, requester, nums):
+        """Hold the annotated chunk until the coordinator names its destination; report it."""
+        cid = int(hdr["chunk"])
+        with self._p2p_lock:
+            self._results[cid] = out.contiguous()
+        info = f"{requester}||processed||{'-'.join(map(str, nums))}||{out.shape[1]}||{out.shape[2]}"
+        self.sender.send_image(info, _EMPTY, p2p=1, chunk=cid, cshape=list(out.shape))
 
     # ------------------------------------------------------------------ heartbeat / leave
     def _heartbeat(self):
@@ -266,6 +396,8 @@ class client:  # noqa: N801 (reference class name)
             t.join(timeout=2)
         self.hub.close()
         self.sender.close()
+        if self.plane is not None:
+            self.plane.close()
         if self.sink is not None:
             self.sink.close()
 

@@ -6,7 +6,9 @@ Requests are UTF-8 datagrams ``"<verb>||<ip>:<port>"`` sent to the coordinator's
 
 Verbs: ``join`` (enter the worker pool, get a data port), ``request`` (become a requester,
 leave the pool), ``stop`` (stop requesting, back to the pool), ``end`` (leave). New verbs:
-``hb`` (heartbeat; renews the lease, reply ``ok``), ``status`` (reply ``ok||<json>``).
+``hb`` (heartbeat; renews the lease, reply ``ok``), ``status`` (reply ``ok||<json>``), ``store``
+(training rendezvous store port), ``p2p`` (reply ``ok||{"plane", "vid", "store_port"}``: the data
+plane of this coordinator and, on the p2p plane, the volunteer's id and the pair-rendezvous store).
 
 Differences from the reference, by design:
 * verbs are matched EXACTLY on the field before ``||`` (the reference matches substrings, so
@@ -21,7 +23,7 @@ import select
 import socket
 import time
 
-VERBS = ("join", "request", "stop", "end", "hb", "status", "store")
+VERBS = ("join", "request", "stop", "end", "hb", "status", "store", "p2p")
 SEP = "||"
 DEFAULT_CONTROL_PORT = 9999
 

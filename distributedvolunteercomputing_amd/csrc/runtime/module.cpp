@@ -102,6 +102,7 @@ PYBIND11_MODULE(_native, m) {
       .def("expire", &ChunkScheduler::expire)
       .def("submit", &ChunkScheduler::submit)
       .def("requeue_front", &ChunkScheduler::requeue_front)
+      .def_property_readonly("requeued", &ChunkScheduler::requeued)
       .def("next", &ChunkScheduler::next)
       .def("complete", &ChunkScheduler::complete)
       .def("cancel_requester", &ChunkScheduler::cancel_requester)

@@ -31,6 +31,7 @@ std::vector<int64_t> ChunkScheduler::drop_worker_locked(const std::string& w) {
     q_.push_front(Pending{*r, req});
   }
   back = ids;
+  requeued_ += ids.size();
   ws_.erase(it);
   order_.erase(std::remove(order_.begin(), order_.end(), w), order_.end());
   return back;

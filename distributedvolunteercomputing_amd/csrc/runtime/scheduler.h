@@ -59,6 +59,7 @@ class ChunkScheduler {
   size_t inflight();
   size_t inflight_of(const std::string& w);
   uint64_t dispatched() const { return dispatched_; }
+  uint64_t requeued() const { return requeued_; }  // chunks re-queued by worker removal / expiry
 
  private:
   struct Pending {
@@ -77,6 +78,7 @@ class ChunkScheduler {
   int credits_;
   uint64_t rr_ = 0;
   uint64_t dispatched_ = 0;
+  uint64_t requeued_ = 0;
   std::vector<std::string> order_;  // join order (round-robin order)
   std::unordered_map<std::string, WorkerState> ws_;
   std::deque<Pending> q_;

@@ -1,5 +1,7 @@
-"""End-to-end volunteer video job on CPU: coordinator + volunteers over the native TCP data
-plane and the UDP control verbs (reference server.py/worker.py flow)."""
+"""End-to-end volunteer video job on CPU: coordinator + volunteers over the UDP control verbs
+(reference server.py/worker.py flow), on both data planes: ``relay`` (chunk
+bytes through the coordinator's native TCP hubs) and ``p2p`` (metadata through the coordinator,
+chunk bytes over directional gloo pair groups between the volunteers)."""
 import time
 
 import numpy as np
@@ -11,9 +13,9 @@ from distributedvolunteercomputing_amd.io.video import decode_frame_index
 from distributedvolunteercomputing_amd.jobs.video import AnnotateOnlyEngine, PassthroughEngine
 
 
-@pytest.fixture
-def coord():
-    c = coordinator("127.0.0.1", 0, ephemeral_ports=True, lease_s=2.0)
+@pytest.fixture(params=["relay", "p2p"])
+def coord(request):
+    c = coordinator("127.0.0.1", 0, ephemeral_ports=True, lease_s=2.0, data_plane=request.param)
     yield c
     c.exit_threads()
 
@@ -43,6 +45,10 @@ def test_join_request_and_inorder_output(coord, tmp_path):
         assert w1.metrics.counters.get("frames_processed", 0) + w2.metrics.counters.get("frames_processed", 0) == 250
         assert req.metrics.counters.get("frames_processed", 0) == 0
         assert coord.clients and req.my_ip in coord.clients  # back in the pool after EOF (stop verb)
+        if coord.data_plane == "p2p":  # no chunk byte went through the coordinator
+            assert all(c.plane is not None for c in (req, w1, w2))
+            assert req.metrics.counters.get("chunks_returned", 0) == 3
+            assert not req._outgoing and not w1._results and not w2._results
     finally:
         for c in (req, w1, w2):
             c.exit_threads()
@@ -101,3 +107,65 @@ def test_status_and_idempotent_join(coord, tmp_path):
         assert w.my_ip in st["workers"]
     finally:
         w.exit_threads()
+
+
+def _worker_proc(port, delay, q):
+    import os
+    import time as _t
+
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from distributedvolunteercomputing_amd.control.peer import client as _client_cls
+    from distributedvolunteercomputing_amd.jobs.video import PassthroughEngine as _PE
+
+    c = _client_cls("127.0.0.1", "127.0.0.1", control_port=port, my_port=0, engine=_PE(delay_s=delay))
+    c.heartbeat_s = 0.2
+    q.put(c.my_ip)
+    while True:
+        _t.sleep(1)
+
+
+def test_p2p_worker_process_killed_mid_transfer(tmp_path):
+    """p2p plane, real crash: a worker PROCESS is SIGKILLed while it holds chunks; its pair
+    groups die with it, the coordinator's lease expiry re-dispatches its chunks, and the
+    requester (which still holds them) sends them to the surviving worker."""
+    import multiprocessing as mp
+    import os
+    import signal
+
+    c = coordinator("127.0.0.1", 0, ephemeral_ports=True, lease_s=1.5, data_plane="p2p")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_proc, args=(c.control_port, d, q), daemon=True) for d in (0.05, 0.3)]
+    for p in procs:
+        p.start()
+    req = None
+    try:
+        addrs = [q.get(timeout=120) for _ in procs]
+        req = _client(c, tmp_path, PassthroughEngine())
+        req.preresize = False
+        req.become_requester("synthetic:600:32x24")
+        slow = None
+        t0 = time.time()
+        while time.time() - t0 < 30 and slow is None:  # kill whichever worker holds chunks first... the slow one
+            for a in addrs:
+                if c.sched.inflight_of(a) > 0 and a == addrs[1]:
+                    slow = a
+            time.sleep(0.01)
+        assert slow is not None
+        os.kill(procs[1].pid, signal.SIGKILL)
+        t = req.wait_job(timeout=90)
+        assert t is not None, "job must complete after a worker process was killed"
+        out = np.load(req.path_out)
+        assert [decode_frame_index(f) for f in out] == list(range(600))
+        cnt = c.metrics.counters
+        assert cnt.get("leaves_lease", 0) + cnt.get("leaves_broken", 0) >= 1, sorted(cnt.items())  # expired or send failed
+        assert cnt.get("redispatched", 0) >= 1, cnt
+        assert req.metrics.counters.get("p2p_failed", 0) >= 1 or cnt.get("duplicate_results", 0) == 0
+    finally:
+        if req is not None:
+            req.exit_threads()
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+            p.join(timeout=5)
+        c.exit_threads()
