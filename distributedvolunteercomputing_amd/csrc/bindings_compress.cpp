@@ -12,7 +12,8 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
   TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor");       \
   TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
 
-// state: int32[8] on device, prepared by the caller: {0, k, 0, 0, ...}; hist: int32[4096] zeros
+// state: int32[8] on device, prepared by the caller: {0, k, 0, ...}; hist: int32[topk_hist_words()]
+// zeros (left zeroed); idx_out / val_out zeroed by the caller (unfilled slots must read 0)
 void topk_ef(at::Tensor g, at::Tensor e, int64_t k, at::Tensor state, at::Tensor hist, at::Tensor idx_out,
              at::Tensor val_out) {
   CHK(g);
@@ -24,7 +25,8 @@ void topk_ef(at::Tensor g, at::Tensor e, int64_t k, at::Tensor state, at::Tensor
   TORCH_CHECK(e.scalar_type() == at::kFloat && g.numel() == e.numel());
   TORCH_CHECK(g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat);
   TORCH_CHECK(state.scalar_type() == at::kInt && state.numel() >= 8 && hist.scalar_type() == at::kInt &&
-              hist.numel() >= 4096);
+              hist.numel() >= vcx_topk_hist_words());
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(state.data_ptr()) & 7) == 0, "state must be 8-byte aligned");
   TORCH_CHECK(idx_out.scalar_type() == at::kInt && idx_out.numel() >= k && val_out.numel() >= k);
   TORCH_CHECK(val_out.scalar_type() == at::kBFloat16 || val_out.scalar_type() == at::kFloat);
   TORCH_CHECK(k > 0 && k <= g.numel() && g.numel() < INT32_MAX);
@@ -33,21 +35,31 @@ void topk_ef(at::Tensor g, at::Tensor e, int64_t k, at::Tensor state, at::Tensor
               val_out.scalar_type() == at::kBFloat16, cur_stream());
 }
 
+// indices come from other peers: out-of-range ones are dropped inside the kernel (no host sync)
 void scatter_add(at::Tensor idx, at::Tensor val, double scale, at::Tensor dense) {
   CHK(idx);
   CHK(val);
   CHK(dense);
   TORCH_CHECK(idx.scalar_type() == at::kInt && dense.scalar_type() == at::kFloat && idx.numel() == val.numel());
   TORCH_CHECK(val.scalar_type() == at::kBFloat16 || val.scalar_type() == at::kFloat);
-  // bounds are enforced on the host: an out-of-range index would be an OOB atomic
-  if (idx.numel()) {
-    auto mx = idx.max().item<int>();
-    auto mn = idx.min().item<int>();
-    TORCH_CHECK(mn >= 0 && mx < dense.numel(), "scatter_add: index out of range");
-  }
+  TORCH_CHECK(dense.numel() < INT32_MAX);
   vcx_scatter_add(idx.data_ptr<int32_t>(), val.data_ptr(), val.scalar_type() == at::kBFloat16, idx.numel(),
-                  (float)scale, dense.data_ptr<float>(), cur_stream());
+                  (float)scale, dense.data_ptr<float>(), dense.numel(), cur_stream());
 }
+
+// wire: int32 [P, L]; per peer k indices then k values of `val_dtype` (bf16 or fp32) packed after them
+void scatter_add_packed(at::Tensor wire, int64_t k, bool val_bf16, double scale, at::Tensor dense) {
+  CHK(wire);
+  CHK(dense);
+  TORCH_CHECK(wire.scalar_type() == at::kInt && wire.dim() == 2 && dense.scalar_type() == at::kFloat);
+  const int64_t L = wire.size(1), vw = val_bf16 ? (k + 1) / 2 : k;
+  TORCH_CHECK(k > 0 && L >= k + vw, "scatter_add_packed: wire rows too short for k pairs");
+  TORCH_CHECK(dense.numel() < INT32_MAX && wire.size(0) * k < INT32_MAX);
+  vcx_scatter_add_packed(wire.data_ptr<int32_t>(), (int)wire.size(0), (int)k, L, val_bf16, (float)scale,
+                         dense.data_ptr<float>(), dense.numel(), cur_stream());
+}
+
+int64_t topk_hist_words() { return vcx_topk_hist_words(); }
 
 void check_desc(const at::Tensor& d, int64_t nmat) {
   CHK(d);
@@ -81,10 +93,14 @@ void psgd_mtp(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::
                Q.data_ptr<float>(), (int)rank, cur_stream());
 }
 
-void psgd_orth(at::Tensor desc, int64_t nmat, at::Tensor P, int64_t rank) {
+void psgd_orth(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor P, at::Tensor G, int64_t rank) {
   check_desc(desc, nmat);
   CHK(P);
-  vcx_psgd_orth(desc.data_ptr(), (int)nmat, P.data_ptr<float>(), (int)rank, cur_stream());
+  CHK(G);
+  TORCH_CHECK(P.scalar_type() == at::kFloat && G.scalar_type() == at::kFloat && G.numel() >= 2 * nmat * rank * rank,
+              "psgd_orth: G must hold 2 * nmat * rank^2 floats");
+  vcx_psgd_orth(desc.data_ptr(), (int)nmat, (int)nblocks, P.data_ptr<float>(), G.data_ptr<float>(), (int)rank,
+                cur_stream());
 }
 
 void psgd_reconstruct(at::Tensor desc, int64_t nmat, int64_t nblocks, at::Tensor M, at::Tensor P, at::Tensor Q,
@@ -112,11 +128,14 @@ void ef_accum(at::Tensor g, at::Tensor e) {
 void vcx_register_compress(pybind11::module& m) {
   m.def("topk_ef", &topk_ef);
   m.def("scatter_add", &scatter_add);
+  m.def("scatter_add_packed", &scatter_add_packed);
+  m.def("topk_hist_words", &topk_hist_words);
   m.def("psgd_mq", &psgd_mq, pybind11::arg("desc"), pybind11::arg("nmat"), pybind11::arg("nblocks"),
         pybind11::arg("M"), pybind11::arg("Q"), pybind11::arg("P"), pybind11::arg("rank"),
         pybind11::arg("G") = pybind11::none(), pybind11::arg("lazy") = false);
   m.def("psgd_mtp", &psgd_mtp);
   m.def("psgd_orth", &psgd_orth);
+  m.def("psgd_orth_rows", &vcx_psgd_orth_rows);
   m.def("psgd_reconstruct", &psgd_reconstruct, pybind11::arg("desc"), pybind11::arg("nmat"), pybind11::arg("nblocks"),
         pybind11::arg("M"), pybind11::arg("P"), pybind11::arg("Q"), pybind11::arg("out"), pybind11::arg("rank"),
         pybind11::arg("update_m") = true);

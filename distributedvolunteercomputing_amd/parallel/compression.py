@@ -25,34 +25,54 @@ from .flat_params import FlatParams
 
 
 class TopKCompressor:
+    """Exact top-k with error feedback. One round on the GPU: ``topk_ef`` (accumulate + 2-pass
+    radix select + compaction, compress.hip) writes the k (index, value) pairs straight into this
+    peer's slot of a packed wire buffer ``[k int32 indices | k values]``; ONE all-gather moves
+    every peer's block; ``scatter_add_packed`` accumulates them into a preallocated fp32 dense
+    buffer, converted into a preallocated bf16 output. No per-round allocation, no host sync."""
+
     def __init__(self, numel: int, ratio: float, device, value_dtype=torch.bfloat16):
         self.n = int(numel)
         self.k = max(1, int(math.ceil(numel * ratio)))
         self.device = torch.device(device)
+        self.value_dtype = value_dtype
         self.e = torch.zeros(self.n, dtype=torch.float32, device=self.device)
-        self.idx = torch.zeros(self.k, dtype=torch.int32, device=self.device)
-        self.val = torch.zeros(self.k, dtype=value_dtype, device=self.device)
+        vwords = (self.k + 1) // 2 if value_dtype == torch.bfloat16 else self.k
+        self.L = self.k + vwords  # int32 words per peer on the wire
+        self.wire = torch.zeros(self.L, dtype=torch.int32, device=self.device)
         self.state = torch.zeros(8, dtype=torch.int32, device=self.device)
         self.state_init = torch.tensor([0, self.k, 0, 0, 0, 0, 0, 0], dtype=torch.int32, device=self.device)
-        self.hist = torch.zeros(4096, dtype=torch.int32, device=self.device)
+        words = native().topk_hist_words() if self.device.type == "cuda" else 1
+        self.hist = torch.zeros(words, dtype=torch.int32, device=self.device)
+        self._gathered = {}  # P -> [P, L] all-gather target
+        self.dense = None  # fp32 [n], allocated on first use
+        self.out = None  # bf16 [n]
         self.bytes_sent = 0
 
     @property
     def ratio(self) -> float:
         return self.k / self.n
 
+    @property
+    def idx(self) -> torch.Tensor:
+        return self.wire[: self.k]
+
+    @property
+    def val(self) -> torch.Tensor:
+        return self.wire[self.k:].view(self.value_dtype)[: self.k]
+
     def compress(self, g: torch.Tensor):
-        """(idx int32 [k], val [k]) of the k largest |g + e|; e keeps the rest."""
+        """(idx int32 [k], val [k]) of the k largest |g + e| (views of the wire buffer); e keeps
+        the rest."""
         if use_native(g):
             self.state.copy_(self.state_init)
-            self.val.zero_()
-            self.idx.zero_()
+            self.wire.zero_()  # unfilled slots (fewer than k nonzero candidates) must read 0
             native().topk_ef(g.contiguous(), self.e, self.k, self.state, self.hist, self.idx, self.val)
             return self.idx, self.val
         self.e.add_(g.float())
         _, i = torch.topk(self.e.abs(), self.k, sorted=False)
         self.idx.copy_(i.to(torch.int32))
-        self.val.copy_(self.e[i].to(self.val.dtype))
+        self.val.copy_(self.e[i].to(self.value_dtype))
         self.e[i] = self.e[i] - self.val.float()  # wire-dtype rounding residual stays in e
         return self.idx, self.val
 
@@ -64,8 +84,8 @@ class TopKCompressor:
     def restore(self, snap: dict):
         # fresh tensors: an abandoned (gloo) op of the aborted round may still hold the old ones
         self.e = snap["e"]
-        self.idx = torch.zeros_like(self.idx)
-        self.val = torch.zeros_like(self.val)
+        self.wire = torch.zeros_like(self.wire)
+        self._gathered = {}
 
     def state_dict(self) -> dict:
         return {"ef": self.e}
@@ -74,22 +94,29 @@ class TopKCompressor:
         self.e.copy_(d["ef"].to(self.e.device))
 
     def allreduce_mean(self, g: torch.Tensor, group) -> torch.Tensor:
-        idx, val = self.compress(g)
+        self.compress(g)
         P = 1 if group is None else group.size
         if P > 1:
-            all_idx = torch.empty(P * self.k, dtype=idx.dtype, device=idx.device)
-            all_val = torch.empty(P * self.k, dtype=val.dtype, device=val.device)
-            group.all_gather_(all_idx, idx)
-            group.all_gather_(all_val, val)
+            allw = self._gathered.get(P)
+            if allw is None:
+                allw = self._gathered[P] = torch.empty(P, self.L, dtype=torch.int32, device=self.device)
+            group.all_gather_(allw.view(-1), self.wire)  # indices and values in ONE collective
         else:
-            all_idx, all_val = idx, val
-        self.bytes_sent += self.k * (idx.element_size() + val.element_size())
-        dense = torch.zeros(self.n, dtype=torch.float32, device=g.device)
-        if use_native(dense):
-            native().scatter_add(all_idx, all_val, 1.0 / P, dense)
+            allw = self.wire.view(1, -1)
+        self.bytes_sent += self.L * 4
+        if self.dense is None:
+            self.dense = torch.empty(self.n, dtype=torch.float32, device=self.device)
+            self.out = torch.empty(self.n, dtype=torch.bfloat16, device=self.device)
+        self.dense.zero_()
+        if use_native(self.dense):
+            native().scatter_add_packed(allw, self.k, self.value_dtype == torch.bfloat16, 1.0 / P, self.dense)
         else:
-            dense.index_add_(0, all_idx.long(), all_val.float() / P)
-        return dense.to(torch.bfloat16)
+            for p in range(P):
+                w = allw[p]
+                vals = w[self.k:].view(self.value_dtype)[: self.k].float()
+                self.dense.index_add_(0, w[: self.k].long(), vals / P)
+        self.out.copy_(self.dense)
+        return self.out
 
 
 class PowerSGDCompressor:
@@ -162,7 +189,10 @@ class PowerSGDCompressor:
         self.d_mtp, self.nb_mtp = table(lambda r, c: ((r + mr - 1) // mr) * ((c + mc - 1) // mc))
         self.d_rec = self.d_mq  # same row-block numbering
         self.nb_rec = self.nb_mq
-        self.d_orth = self.d_mq
+        orows = C.psgd_orth_rows()
+        self.d_orth, self.nb_orth = table(lambda r, c: (r + orows - 1) // orows)
+        self.G = torch.zeros(2 * max(1, len(self.mats)) * self.rank * self.rank, dtype=torch.float32,
+                             device=self.device)
 
     @property
     def compression_ratio(self) -> float:
@@ -191,7 +221,7 @@ class PowerSGDCompressor:
                 group.allreduce_(self.P)
                 self.P.div_(Pn)
             if native_path:
-                C.psgd_orth(self.d_orth, nm, self.P, R)
+                C.psgd_orth(self.d_orth, nm, self.nb_orth, self.P, self.G, R)
             else:
                 self._ref_orth()
             self.Q.zero_()

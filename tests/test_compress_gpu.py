@@ -44,6 +44,62 @@ def test_topk_ties_and_zeros(gpu):
     assert nz == 100 and set(idx[val != 0].tolist()) == set(range(100))
 
 
+@pytest.mark.parametrize("n", [1_000_003, 4_194_304])
+def test_topk_bf16_ties_every_round(gpu, n):
+    """bf16 gradients with e = 0 put thousands of elements exactly on the threshold value: the
+    tie budget must hand out exactly k - (#above) of them, and the scratch state (histogram,
+    claim counter) must be clean for the next round."""
+    torch.manual_seed(7)
+    c = TopKCompressor(n, 0.01, gpu)
+    for rnd in range(3):
+        c.e.zero_()
+        g = torch.randn(n, device=gpu).to(torch.bfloat16)
+        acc = g.float()
+        idx, val = c.compress(g)
+        torch.cuda.synchronize()
+        sel = idx.long()
+        assert sel.unique().numel() == c.k, rnd
+        thr = torch.topk(acc.abs(), c.k).values[-1]
+        above = (acc.abs() > thr).sum().item()
+        ties = (acc.abs() == thr).sum().item()
+        assert ties > 10, "the test needs ties on the threshold"
+        assert (acc[sel].abs() >= thr).all()
+        assert (acc[sel].abs() > thr).sum().item() == above  # every element above is selected
+        assert torch.equal(val.float(), acc[sel])  # bf16 in, bf16 out: no residual
+    assert int(c.hist.abs().sum()) == 0  # left zeroed for the next round
+
+
+def test_allreduce_mean_packed_wire(gpu):
+    """P = 1 path of the packed wire: the bf16 output is the scatter of the selected pairs."""
+    torch.manual_seed(8)
+    n = 300_001
+    c = TopKCompressor(n, 0.02, gpu)
+    g = torch.randn(n, device=gpu).to(torch.bfloat16)
+    out = c.allreduce_mean(g, None)
+    torch.cuda.synchronize()
+    ref = torch.zeros(n, device=gpu)
+    ref[c.idx.long()] = c.val.float()
+    assert torch.equal(out.float(), ref.to(torch.bfloat16).float())
+    assert out.data_ptr() == c.allreduce_mean(g, None).data_ptr()  # preallocated, reused
+
+
+def test_scatter_add_packed_drops_bad_indices(gpu):
+    from distributedvolunteercomputing_amd.ops import native
+
+    k = 3
+    wire = torch.zeros(2, k + 2, dtype=torch.int32, device=gpu)  # bf16 values: 2 words for 3 values
+    wire[0, :k] = torch.tensor([1, 7, 1 << 30], dtype=torch.int32)  # the last index is out of range
+    wire[0, k:].view(torch.bfloat16)[:k] = torch.tensor([1.0, 2.0, 5.0], dtype=torch.bfloat16)
+    wire[1, :k] = torch.tensor([7, -3, 0], dtype=torch.int32)
+    wire[1, k:].view(torch.bfloat16)[:k] = torch.tensor([4.0, 8.0, 0.0], dtype=torch.bfloat16)
+    dense = torch.zeros(10, device=gpu)
+    native().scatter_add_packed(wire, k, True, 0.5, dense)
+    torch.cuda.synchronize()
+    exp = torch.zeros(10, device=gpu)
+    exp[1], exp[7] = 0.5, 3.0
+    assert torch.equal(dense, exp)
+
+
 def test_scatter_add(gpu):
     from distributedvolunteercomputing_amd.ops import native
 
@@ -114,3 +170,43 @@ def test_powersgd_odd_shapes_match_reference(gpu, rank):
         rel = (out - ref).norm() / ref.norm()
         assert rel < 2e-2, (step, float(rel))
         assert (c_gpu.ef() - c_ref.ef()).norm() / (c_ref.ef().norm() + 1e-9) < 2e-2
+
+
+@pytest.mark.parametrize("rank", [1, 2, 4, 8])
+def test_psgd_orth_equals_thin_qr(gpu, rank):
+    """Batched CholeskyQR2 of every matrix's P (rows spanning several 2048-row slabs) equals the
+    thin-QR factor with a positive-diagonal R (the unique orthonormalisation Gram-Schmidt gives)."""
+    from distributedvolunteercomputing_amd.ops import native
+
+    torch.manual_seed(10 + rank)
+    m = torch.nn.Sequential(torch.nn.Linear(300, 5000, bias=False), torch.nn.Linear(5000, 70, bias=False),
+                            torch.nn.Linear(64, 9000, bias=False)).to(gpu, torch.bfloat16)
+    flat = FlatParams(m)
+    c = PowerSGDCompressor(flat, rank=rank, device=gpu)
+    assert len(c.mats) == 3
+    c.P.copy_(torch.randn_like(c.P))
+    before = c.P.clone()
+    native().psgd_orth(c.d_orth, len(c.mats), c.nb_orth, c.P, c.G, rank)
+    torch.cuda.synchronize()
+    for i, (off, r, cc) in enumerate(c.mats):
+        p0 = before[c.p_off[i]: c.p_off[i] + r * rank].view(r, rank).double()
+        q, rr = torch.linalg.qr(p0)
+        q = q * torch.sign(torch.diagonal(rr)).unsqueeze(0)
+        got = c.P[c.p_off[i]: c.p_off[i] + r * rank].view(r, rank).double()
+        assert torch.allclose(got, q, atol=2e-5), (i, float((got - q).abs().max()))
+
+
+def test_psgd_orth_dependent_column_stays_finite(gpu):
+    from distributedvolunteercomputing_amd.ops import native
+
+    m = torch.nn.Sequential(torch.nn.Linear(512, 4096, bias=False)).to(gpu, torch.bfloat16)
+    c = PowerSGDCompressor(FlatParams(m), rank=4, device=gpu)
+    P = c.P[: 4096 * 4].view(4096, 4)
+    P.copy_(torch.randn(4096, 4, device=gpu))
+    P[:, 2] = P[:, 0] * 3.0  # linearly dependent column
+    native().psgd_orth(c.d_orth, len(c.mats), c.nb_orth, c.P, c.G, 4)
+    torch.cuda.synchronize()
+    # the dependent column's fp32 residual is rounding noise: it becomes SOME unit vector
+    # orthogonal to the others (the second CholeskyQR pass cleans it up) — never NaN/inf
+    assert torch.isfinite(P).all()
+    assert torch.allclose(P.t() @ P, torch.eye(4, device=gpu), atol=1e-3)
