@@ -26,10 +26,12 @@ import sys
 import sysconfig
 from pathlib import Path
 
+from . import config
+
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 BUILD = PKG.parent / "build" / "native"
-ARCH = os.environ.get("VCX_OFFLOAD_ARCH", "gfx950")
+ARCH = config.get().offload_arch
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 

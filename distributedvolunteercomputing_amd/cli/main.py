@@ -12,6 +12,8 @@ from __future__ import annotations
 import argparse
 import sys
 
+from .. import config
+
 
 def server_main(argv=None):
     ap = argparse.ArgumentParser(prog="server.py", description="volunteer-computing coordinator")
@@ -103,7 +105,7 @@ def video_main(argv=None):
     ap.add_argument("--out-ext", default=".y4m", choices=[".y4m", ".npy", ""])
     ap.add_argument("--chunk", type=int, default=100)
     ap.add_argument("--port", type=int, default=9999, help="coordinator UDP control port")
-    ap.add_argument("--store-port", type=int, default=int(os.environ.get("VCX_STORE_PORT", "29612")))
+    ap.add_argument("--store-port", type=int, default=config.get().store_port_video)
     a = ap.parse_args(argv)
     from ..control.node_job import run_node_job
     from ..jobs.video import DetectorEngine

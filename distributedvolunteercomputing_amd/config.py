@@ -1,0 +1,130 @@
+"""One place for every runtime tunable of the framework.
+
+Each field has a default, an environment variable that overrides it at import time, and can be
+changed in code with :func:`update` (or temporarily with :func:`override`). Modules read the
+live object (``config.get().field``) at the point of use, never a module-level copy, so an
+update takes effect for the next call.
+
+    from distributedvolunteercomputing_amd import config
+    config.update(gemm="vcx")            # hand-written MFMA GEMM for the Linear layers
+    with config.override(force_reference_ops=True):
+        ...                              # plain torch ops (numerics oracle)
+    print(config.describe())             # every field, its env var and current value
+
+The reference configures itself with module constants and argv only (/root/reference/worker.py:
+16-18, server.py:9-12); those job-level knobs remain command-line flags of the CLIs.
+"""
+from __future__ import annotations
+
+import contextlib
+import dataclasses
+import os
+import threading
+
+
+def _bool(s: str) -> bool:
+    return s.strip().lower() in ("1", "true", "yes", "on")
+
+
+@dataclasses.dataclass
+class RuntimeConfig:
+    # ---- compute path
+    gemm: str = "lib"  # VCX_GEMM: "lib" (hipBLASLt/rocBLAS) or "vcx" (csrc/kernels/gemm.hip, opt-in: 0.74-0.84x lib)
+    gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)
+    wgrad_big_split_min_m: int = 16384  # VCX_WGRAD_BIG_SPLIT_MIN_M: rows above which weight grads split over K
+    async_wgrad: bool = False  # VCX_ASYNC_WGRAD: weight-grad GEMMs on a side stream (measured slower)
+    force_reference_ops: bool = False  # VCX_FORCE_REFERENCE_OPS: torch ops instead of the HIP kernels
+    tunableop: str = "on"  # VCX_TUNABLEOP: "on" loads the shipped hipBLASLt selections, "off" skips them
+    tunableop_file: str = ""  # VCX_TUNABLEOP_FILE: alternative TunableOp results file
+    offload_arch: str = "gfx950"  # VCX_OFFLOAD_ARCH: target of the in-tree HIP build
+    # ---- distributed / control plane
+    gloo_host: str = "127.0.0.1"  # VCX_GLOO_HOST: interface gloo peer groups bind to
+    p2p_backend: str = ""  # VCX_P2P_BACKEND: pair-group backend of the p2p chunk plane ("" = auto)
+    elastic_debug: bool = False  # VCX_ELASTIC_DEBUG: trace membership decisions to stderr
+    store_port_train: int = 29611  # VCX_STORE_PORT (train CLI): rendezvous store port
+    store_port_video: int = 29612  # VCX_STORE_PORT (video CLI): job-control store port
+    # ---- observability
+    trace_dir: str = ""  # VCX_TRACE_DIR: per-span device-time traces (utils/trace.py)
+    metrics_dir: str = ""  # VCX_METRICS_DIR: JSON-lines metrics snapshots (utils/metrics.py)
+
+
+# field -> (environment variable, parser)
+_ENV = {
+    "gemm": ("VCX_GEMM", str),
+    "gemm_select": ("VCX_GEMM_SELECT", _bool),
+    "wgrad_big_split_min_m": ("VCX_WGRAD_BIG_SPLIT_MIN_M", int),
+    "async_wgrad": ("VCX_ASYNC_WGRAD", _bool),
+    "force_reference_ops": ("VCX_FORCE_REFERENCE_OPS", _bool),
+    "tunableop": ("VCX_TUNABLEOP", str),
+    "tunableop_file": ("VCX_TUNABLEOP_FILE", str),
+    "offload_arch": ("VCX_OFFLOAD_ARCH", str),
+    "gloo_host": ("VCX_GLOO_HOST", str),
+    "p2p_backend": ("VCX_P2P_BACKEND", str),
+    "elastic_debug": ("VCX_ELASTIC_DEBUG", _bool),
+    "store_port_train": ("VCX_STORE_PORT", int),
+    "store_port_video": ("VCX_STORE_PORT", int),
+    "trace_dir": ("VCX_TRACE_DIR", str),
+    "metrics_dir": ("VCX_METRICS_DIR", str),
+}
+_CHOICES = {"gemm": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl")}
+
+_lock = threading.Lock()
+
+
+def _validate(cfg: RuntimeConfig):
+    for k, allowed in _CHOICES.items():
+        if getattr(cfg, k) not in allowed:
+            raise ValueError(f"config.{k} must be one of {allowed}, not {getattr(cfg, k)!r}")
+
+
+def from_env(env=None) -> RuntimeConfig:
+    """A config with the defaults overridden by the VCX_* variables present in `env`."""
+    env = os.environ if env is None else env
+    cfg = RuntimeConfig()
+    for field, (var, parse) in _ENV.items():
+        if var in env and env[var] != "":
+            try:
+                setattr(cfg, field, parse(env[var]))
+            except ValueError as e:
+                raise ValueError(f"{var}={env[var]!r}: {e}") from None
+    _validate(cfg)
+    return cfg
+
+
+_CONFIG = from_env()
+
+
+def get() -> RuntimeConfig:
+    return _CONFIG
+
+
+def update(**kw) -> RuntimeConfig:
+    """Change fields of the live config (validated); returns it."""
+    with _lock:
+        unknown = set(kw) - {f.name for f in dataclasses.fields(RuntimeConfig)}
+        if unknown:
+            raise AttributeError(f"unknown config fields: {sorted(unknown)}")
+        new = dataclasses.replace(_CONFIG, **kw)
+        _validate(new)
+        for k, v in kw.items():
+            setattr(_CONFIG, k, v)
+    return _CONFIG
+
+
+@contextlib.contextmanager
+def override(**kw):
+    """Temporarily change fields; restored on exit (not thread-scoped: the config is global)."""
+    old = {k: getattr(_CONFIG, k) for k in kw}
+    update(**kw)
+    try:
+        yield _CONFIG
+    finally:
+        update(**old)
+
+
+def describe() -> str:
+    rows = []
+    for f in dataclasses.fields(RuntimeConfig):
+        var = _ENV.get(f.name, ("", None))[0]
+        rows.append(f"{f.name:24s} {var:28s} {getattr(_CONFIG, f.name)!r}")
+    return "\n".join(rows)

@@ -36,6 +36,7 @@ import time
 import numpy as np
 import torch
 
+from .. import config
 from ..io.video import open_sink, open_source
 from ..jobs.video import DetectorEngine, Engine, OrderedSink
 from ..ops import vision as V
@@ -134,7 +135,7 @@ class client:  # noqa: N801 (reference class name)
             return dist.TCPStore(host, port, None, False, timeout=datetime.timedelta(seconds=60))
         if backend is None:
             # RCCL needs one GPU per volunteer; volunteers sharing a device (or none) use gloo
-            backend = os.environ.get("VCX_P2P_BACKEND") or (
+            backend = config.get().p2p_backend or (
                 "nccl" if torch.cuda.is_available() and torch.cuda.device_count() > 1 else "gloo")
         dev = self.resize_device if backend == "nccl" else torch.device("cpu")
         self.plane = PairPlane(store, int(info["vid"]), backend=backend, device=dev, metrics=self.metrics)

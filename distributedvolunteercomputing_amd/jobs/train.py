@@ -24,6 +24,8 @@ import time
 import torch
 import torch.distributed as dist
 
+from .. import config
+
 
 def build_model(name: str, device, seq: int):
     if name == "mlp":
@@ -100,7 +102,7 @@ def parse(argv=None):
     ap.add_argument("--peer-id", type=int, default=None)
     ap.add_argument("--world", type=int, default=None)
     ap.add_argument("--store-host", default=os.environ.get("MASTER_ADDR", "127.0.0.1"))
-    ap.add_argument("--store-port", type=int, default=int(os.environ.get("VCX_STORE_PORT", "29611")))
+    ap.add_argument("--store-port", type=int, default=config.get().store_port_train)
     ap.add_argument("--coordinator", default=None,
                     help="host:control_port of a coordinator that hosts the rendezvous store (no peer is special)")
     ap.add_argument("--join", action="store_true", help="join a running job instead of bootstrapping")
@@ -110,7 +112,7 @@ def parse(argv=None):
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--log-every", type=int, default=10)
     ap.add_argument("--metrics", default=None, help="JSONL metrics file")
-    ap.add_argument("--trace-dir", default=os.environ.get("VCX_TRACE_DIR"),
+    ap.add_argument("--trace-dir", default=config.get().trace_dir or None,
                     help="write per-stage device-time spans (HIP events) as JSONL here")
     return ap.parse_args(argv)
 

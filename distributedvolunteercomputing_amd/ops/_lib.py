@@ -8,7 +8,8 @@ the numerics oracle in the tests.
 from __future__ import annotations
 
 import importlib
-import os
+
+from .. import config
 
 _C = None
 _ERR: Exception | None = None
@@ -40,12 +41,11 @@ def available() -> bool:
     return _C is not None
 
 
-_FORCE_REF = [os.environ.get("VCX_FORCE_REFERENCE_OPS") == "1"]
 
 
 def use_native(t) -> bool:
     """True when tensor `t` lives on the GPU (then the native kernel is mandatory)."""
-    if _FORCE_REF[0]:
+    if config.get().force_reference_ops:
         return False
     return bool(getattr(t, "is_cuda", False))
 
@@ -65,8 +65,8 @@ class reference_ops:
     Used ONLY by the numerics tests to build an oracle on the same device."""
 
     def __enter__(self):
-        self._old = _FORCE_REF[0]
-        _FORCE_REF[0] = True
+        self._old = config.get().force_reference_ops
+        config.update(force_reference_ops=True)
 
     def __exit__(self, *exc):
-        _FORCE_REF[0] = self._old
+        config.update(force_reference_ops=self._old)

@@ -26,24 +26,24 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-import os
 
+from .. import config
 from ._lib import grad_buffer, native, use_native
 
 MIN_ROWS_PER_SPLIT = 2048
 # The hand-written GEMM is opt-in (VCX_GEMM=vcx): at the GPT-2 bench shapes it runs at 0.74-0.84x
 # the library GEMM, and its fused bias+GELU / DGELU epilogues (not overlapped with MFMA work: one
 # workgroup per CU) cost more than the separate HIP passes they replace (profiles/r2_gemm_nt.txt)
-_VCX_GEMM = [os.environ.get("VCX_GEMM", "lib") == "vcx"]
 
 
 def set_gemm_backend(name: str):
-    """'vcx' (hand-written gemm_nt where the shape tiles) or 'lib' (library GEMMs only)."""
-    _VCX_GEMM[0] = name != "lib"
+    """'vcx' (hand-written gemm_nt where the shape tiles) or 'lib' (library GEMMs only);
+    the ``gemm`` field of the runtime config (config.py)."""
+    config.update(gemm="lib" if name == "lib" else "vcx")
 
 
 def gemm_nt_ok(M: int, N: int, K: int, t) -> bool:
-    return (_VCX_GEMM[0] and use_native(t) and t.dtype == torch.bfloat16
+    return (config.get().gemm == "vcx" and use_native(t) and t.dtype == torch.bfloat16
             and bool(native().gemm_nt_supported(M, N, K)))
 
 
@@ -58,7 +58,6 @@ def gemm_nt(a, b, bias=None, out=None):
 def transpose_weight(w):
     """W^T as a contiguous bf16 matrix (HIP transpose; weights only — a few MB)."""
     return native().transpose_bf16(w.contiguous())
-_GEMM_SELECT = os.environ.get("VCX_GEMM_SELECT", "0") == "1"  # measured: no in-step gain (A/B 956 vs 957 samples/s)
 _CHOICE: dict = {}  # (shapes, layout, bias) -> "torch" | "lt"
 
 
@@ -93,7 +92,8 @@ def _time_ms(fn, reps=3):
 
 def mm(a, b, trans_a: bool = False, trans_b: bool = False, bias=None):
     """op(a) @ op(b) (+ bias) for 2-D bf16 GPU tensors, with per-shape library selection."""
-    if not (_GEMM_SELECT and a.is_cuda and a.dtype == torch.bfloat16 and a.is_contiguous() and b.is_contiguous()):
+    # config.gemm_select; measured: no in-step gain (A/B 956 vs 957 samples/s)
+    if not (config.get().gemm_select and a.is_cuda and a.dtype == torch.bfloat16 and a.is_contiguous() and b.is_contiguous()):
         return _torch_mm(a, b, trans_a, trans_b, bias)
     key = (tuple(a.shape), tuple(b.shape), trans_a, trans_b, bias is not None)
     c = _CHOICE.get(key)
@@ -120,12 +120,11 @@ def gemm_choices() -> dict:
 
 # Big outputs (N*K >= 16M elements) with fewer tokens than this take ONE GEMM that accumulates
 # straight into the bf16 .grad (beta = 1) instead of a split-M batch + fp32 partial reduction
-_BIG_SPLIT_MIN_M = int(os.environ.get("VCX_WGRAD_BIG_SPLIT_MIN_M", "16384"))
 
 
 def _splits(M: int, N: int, K: int) -> int:
     if N * K >= 16 * 1024 * 1024:  # big outputs (LM head) already fill the GPU
-        if M < _BIG_SPLIT_MIN_M:
+        if M < config.get().wgrad_big_split_min_m:
             return 1
         s = 4
     else:
@@ -163,7 +162,6 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor | None = None, 
 # backward pass (autograd engine callback), so the compute-bound split-M wgrad GEMMs run beside
 # the memory-bound kernels of the next layers' input-gradient chain (LayerNorm / GELU / attention
 # backward) instead of after them. Works under hipGraph capture (fork/join become graph edges).
-_ASYNC_WGRAD = os.environ.get("VCX_ASYNC_WGRAD", "0") == "1"  # measured slower: 951 vs 966-971 samples/s
 _SIDE: dict = {}
 _JOIN_PENDING: dict = {}
 
@@ -241,7 +239,8 @@ class _Linear(torch.autograd.Function):
         bias, ctx.bias = ctx.bias, None
         flat_w = w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == w.dtype
         flat_b = (not want_b) or grad_buffer(bias) is not None
-        if _ASYNC_WGRAD and dy2.is_cuda and flat_w and flat_b and (want_w or want_b):
+        # config.async_wgrad: measured slower (951 vs 966-971 samples/s)
+        if config.get().async_wgrad and dy2.is_cuda and flat_w and flat_b and (want_w or want_b):
             # only when every result lands in a flat .grad buffer (nothing is returned to autograd)
             main = torch.cuda.current_stream(dy2.device)
             side = _side_stream(dy2.device)

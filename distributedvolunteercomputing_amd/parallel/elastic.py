@@ -34,14 +34,14 @@ import threading
 import time
 from contextlib import contextmanager
 
+from .. import config
 from .peer_group import PeerFailure, PeerGroup
 
 _P = "vcx/el/"
-_DEBUG = bool(os.environ.get("VCX_ELASTIC_DEBUG"))
 
 
 def _dbg(pid, msg):
-    if _DEBUG:
+    if config.get().elastic_debug:
         print(f"[elastic {pid} {time.time() % 1000:8.3f}] {msg}", flush=True)
 
 

@@ -25,12 +25,13 @@ the blocking send to a dead volunteer that stalls the reference's dispatcher for
 from __future__ import annotations
 
 import datetime as _dt
-import os
 import threading
 import time
 
 import torch
 import torch.distributed as dist
+
+from .. import config
 
 
 class PeerFailure(RuntimeError):
@@ -43,7 +44,7 @@ _GRAVEYARD: list = []  # aborted gloo groups with possibly blocked ops (see modu
 def _gloo_pg(store, rank, size, timeout):
     opts = dist.ProcessGroupGloo._Options()
     opts._timeout = timeout
-    host = os.environ.get("VCX_GLOO_HOST", "127.0.0.1")
+    host = config.get().gloo_host
     opts._devices = [dist.ProcessGroupGloo.create_device(hostname=host)]
     return dist.ProcessGroupGloo(store, rank, size, opts)
 

@@ -12,6 +12,8 @@ import os
 import threading
 import time
 
+from .. import config
+
 
 class Metrics:
     def __init__(self, component: str, path: str | None = None):
@@ -20,7 +22,7 @@ class Metrics:
         self.counters: dict[str, float] = {}
         self.gauges: dict[str, float] = {}
         self.samples: dict[str, list] = {}
-        d = os.environ.get("VCX_METRICS_DIR")
+        d = config.get().metrics_dir
         self.path = path or (os.path.join(d, f"{component}.jsonl") if d else None)
 
     def incr(self, name: str, by: float = 1):

@@ -25,10 +25,12 @@ import time
 
 import torch
 
+from .. import config
+
 
 class SpanTracer:
     def __init__(self, component: str, path: str | None = None, enabled: bool | None = None):
-        d = os.environ.get("VCX_TRACE_DIR")
+        d = config.get().trace_dir
         self.component = component
         self.path = path or (os.path.join(d, f"{component}.jsonl") if d else None)
         self.enabled = bool(self.path) if enabled is None else enabled

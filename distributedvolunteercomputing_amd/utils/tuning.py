@@ -15,14 +15,17 @@ import os
 import shutil
 import tempfile
 
+from .. import config
+
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 RESULTS = os.path.join(ROOT, "tuning", "tunableop_gfx950.csv")
 
 
 def enable_tuned_gemms(local_rank: int = 0) -> bool:
-    if os.environ.get("VCX_TUNABLEOP", "on") == "off" or "PYTORCH_TUNABLEOP_ENABLED" in os.environ:
+    cfg = config.get()
+    if cfg.tunableop == "off" or "PYTORCH_TUNABLEOP_ENABLED" in os.environ:
         return False
-    results = os.environ.get("VCX_TUNABLEOP_FILE", RESULTS)
+    results = cfg.tunableop_file or RESULTS
     if not os.path.exists(results):
         return False
     d = tempfile.mkdtemp(prefix="vcx_tunableop_")

@@ -32,6 +32,40 @@ def test_gpt2_forward_backward_matches_reference(gpu):
         assert (a - b).norm().item() / denom < 0.08, n
 
 
+def test_gpt2_gradients_vs_fp32_oracle(gpu):
+    """The HIP bf16 path against an fp32 copy of the same model run through the plain torch ops
+    (the oracle), per tensor: its error must be within bf16 rounding (2%) and no worse than the
+    torch bf16 path's own error against the same oracle (+25%)."""
+    import copy
+
+    torch.manual_seed(11)
+    m, cfg = _model(gpu)
+    oracle = copy.deepcopy(m).float()
+    x = torch.randint(0, cfg.vocab_size, (4, 128), device=gpu)
+    y = torch.randint(0, cfg.vocab_size, (4, 128), device=gpu)
+    loss = m(x, y)
+    loss.backward()
+    g_native = {n: p.grad.float().clone() for n, p in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    with reference_ops():
+        loss_bf16 = m(x, y)
+        loss_bf16.backward()
+        loss_o = oracle(x, y)
+        loss_o.backward()
+    g_bf16 = {n: p.grad.float() for n, p in m.named_parameters()}
+    g_o = dict(oracle.named_parameters())
+    assert abs(loss.item() - loss_o.item()) < 5e-3 * abs(loss_o.item())
+    worst = {}
+    for n, po in g_o.items():
+        ref = po.grad.float()
+        den = ref.norm().item() + 1e-12
+        e_nat = (g_native[n] - ref).norm().item() / den
+        e_t = (g_bf16[n] - ref).norm().item() / den
+        worst[n] = (round(e_nat, 4), round(e_t, 4))
+        assert e_nat < 0.02, (n, e_nat, e_t)
+        assert e_nat <= 1.25 * e_t + 2e-3, (n, e_nat, e_t)
+
+
 def test_local_sgd_trains(gpu):
     m, cfg = _model(gpu)
     tr = LocalSGDTrainer(m, LocalSGDConfig(H=2, lr=3e-3, weight_decay=0.0), device=gpu)
