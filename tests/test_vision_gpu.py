@@ -73,6 +73,19 @@ def test_preprocess(gpu):
     assert (b.cpu().float() - rb.float()).abs().max() <= 0.0079 + 1e-3
 
 
+@pytest.mark.parametrize("shape,width", [((2, 333, 517), 200), ((1, 1080, 1920), 400), ((3, 97, 601), 600),
+                                         ((2, 40, 64), 13)])
+def test_resize_area_odd_shapes(gpu, shape, width):
+    """Banded INTER_AREA kernel: partial last band, non-integer scales, near-1 and large ratios."""
+    torch.manual_seed(5)
+    f = torch.randint(0, 256, (*shape, 3), dtype=torch.uint8, device=gpu)
+    a = V.resize_width(f, width)
+    with reference_ops():
+        r = V.resize_width(f.cpu(), width)
+    assert a.shape == r.shape
+    assert (a.cpu().int() - r.int()).abs().max() <= 1
+
+
 def _rand_det_inputs(dev, N=4, P=1917, C=21, seed=3):
     g = torch.Generator().manual_seed(seed)
     conf = torch.randn(N, P * C, generator=g) * 2.5
