@@ -33,6 +33,7 @@ class RuntimeConfig:
     gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)
     wgrad_big_split_min_m: int = 16384  # VCX_WGRAD_BIG_SPLIT_MIN_M: rows above which weight grads split over K
     async_wgrad: bool = False  # VCX_ASYNC_WGRAD: weight-grad GEMMs on a side stream (measured slower)
+    lmhead_chunk: int = 0  # VCX_LMHEAD_CHUNK: token rows per LM-head GEMM + xent pass (0 = one pass)
     force_reference_ops: bool = False  # VCX_FORCE_REFERENCE_OPS: torch ops instead of the HIP kernels
     tunableop: str = "on"  # VCX_TUNABLEOP: "on" loads the shipped hipBLASLt selections, "off" skips them
     tunableop_file: str = ""  # VCX_TUNABLEOP_FILE: alternative TunableOp results file
@@ -54,6 +55,7 @@ _ENV = {
     "gemm_select": ("VCX_GEMM_SELECT", _bool),
     "wgrad_big_split_min_m": ("VCX_WGRAD_BIG_SPLIT_MIN_M", int),
     "async_wgrad": ("VCX_ASYNC_WGRAD", _bool),
+    "lmhead_chunk": ("VCX_LMHEAD_CHUNK", int),
     "force_reference_ops": ("VCX_FORCE_REFERENCE_OPS", _bool),
     "tunableop": ("VCX_TUNABLEOP", str),
     "tunableop_file": ("VCX_TUNABLEOP_FILE", str),

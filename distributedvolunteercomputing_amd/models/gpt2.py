@@ -159,7 +159,6 @@ class GPT2(nn.Module):
                 h, resid = ops.add_layernorm(resid, m, nxt.ln1_w, nxt.ln1_b, eps, branch_bias=blk.fc2_b)
             else:
                 h, resid = ops.add_layernorm(resid, m, self.lnf_w, self.lnf_b, eps, branch_bias=blk.fc2_b)
-        logits = ops.linear(h, self.wte)  # tied LM head, [B, T, Vp]
         if targets is None:
-            return logits[..., : cfg.vocab_size]
-        return ops.cross_entropy(logits.view(B * T, -1), targets.reshape(-1), vocab=cfg.vocab_size)
+            return ops.linear(h, self.wte)[..., : cfg.vocab_size]  # tied LM head, [B, T, Vp]
+        return ops.lm_head_cross_entropy(h, self.wte, targets, cfg.vocab_size)

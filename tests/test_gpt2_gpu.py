@@ -106,3 +106,27 @@ def test_hipgraph_step_matches_eager(gpu):
     torch.cuda.synchronize()
     assert abs(float(sa.extra["loss_t"]) - float(sb.extra["loss_t"])) < 1e-2
     assert ((ta.master - tb.master).norm() / ta.master.norm()).item() < 1e-3
+
+
+@pytest.mark.parametrize("chunk", [64, 96])
+def test_lm_head_xent_chunked_matches_whole(gpu, chunk):
+    """Chunked LM head + fused xent (logits chunk in one reused buffer) against the one-pass path:
+    same loss, same input and weight gradients (the same GEMMs, only split by token rows)."""
+    from distributedvolunteercomputing_amd import ops
+
+    torch.manual_seed(12)
+    M, K, Vp, V = 320, 128, 512, 500
+    x = (torch.randn(M, K, device=gpu) * 0.5).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(Vp, K, device=gpu) * 0.05).to(torch.bfloat16).requires_grad_()
+    t = torch.randint(0, V, (M,), device=gpu)
+    t[::7] = -100  # ignored rows
+    res = {}
+    for c in (0, chunk):
+        x.grad = w.grad = None
+        loss = ops.lm_head_cross_entropy(x, w, t, V, chunk=c)
+        (loss * 3.0).backward()
+        res[c] = (loss.item(), x.grad.float().clone(), w.grad.float().clone())
+    (l0, dx0, dw0), (l1, dx1, dw1) = res[0], res[chunk]
+    assert abs(l0 - l1) < 1e-4 * abs(l0)
+    assert (dx0 - dx1).norm() / dx0.norm() < 1e-2
+    assert (dw0 - dw1).norm() / dw0.norm() < 1e-2
