@@ -59,10 +59,15 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=1)
     ap.add_argument("--timeout", type=float, default=900.0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--rejoin", action="store_true",
+                    help="respawn each killed victim; it joins the running job (BASELINE config 4: kill then rejoin)")
+    ap.add_argument("--after-rejoin", type=int, default=8,
+                    help="with --rejoin: survivors keep stepping until the full group ran this many steps")
     # internal (peer processes)
     ap.add_argument("--peer", type=int, default=None)
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--join", action="store_true", help="(internal) a replacement peer joining the running job")
     return ap.parse_args(argv)
 
 
@@ -101,7 +106,10 @@ def peer_main(a):
                 print(f"[peer {a.peer}] fault injection: {signal.Signals(sig).name} inside {op}", flush=True)
                 os.kill(os.getpid(), sig)
         mem.fault_hook = hook
-    mem.bootstrap(list(range(a.peers)))
+    if a.join:
+        mem.join()
+    else:
+        mem.bootstrap(list(range(a.peers)))
     cfg = GPT2Config.preset(a.model)
     cfg.n_ctx = max(cfg.n_ctx, a.seq)
     torch.manual_seed(0)
@@ -109,6 +117,8 @@ def peer_main(a):
     model = GPT2(cfg).to(device=device, dtype=dtype)
     tcfg = LocalSGDConfig(H=a.H, comm_dtype=dtype)
     tr = LocalSGDTrainer(model, tcfg, membership=mem, device=device)
+    if a.join:
+        return joiner_loop(a, tr, mem, store, cfg, device, cuda)
     g = torch.Generator(device=device).manual_seed(1000 + a.peer)
     pool = [torch.randint(0, cfg.vocab_size, (a.batch, a.seq + 1), device=device, generator=g) for _ in range(4)]
 
@@ -129,7 +139,20 @@ def peer_main(a):
     sync()
     mem.group.barrier()
     timeline = []
-    for i in range(a.warmup, a.warmup + a.steps):
+    i = a.warmup
+    t_cap = time.time() + a.timeout * 0.8
+    full_since = None
+    while True:
+        if i >= a.warmup + a.steps:
+            if not a.rejoin or a.peer in victims:
+                break
+            # config 4: keep going until the victims are back and the full group ran a while
+            if timeline and timeline[-1]["members"] == a.peers and timeline[-1]["gen"] > 1:
+                full_since = i if full_since is None else full_since
+                if i - full_since >= a.after_rejoin:
+                    break
+            if time.time() > t_cap:
+                break
         if a.peer in victims and i == a.drop_at:
             if a.fault == "step":
                 print(f"[peer {a.peer}] fault injection: crashing at step {i}", flush=True)
@@ -141,10 +164,35 @@ def peer_main(a):
         sync()
         timeline.append({"step": i, "ms": (time.perf_counter() - t0) * 1e3, "synced": bool(st.synced),
                          "members": st.members, "gen": mem.gen, "sync_ms": st.sync_ms if st.synced else 0.0})
+        i += 1
+    store.set("vcx/drop/done", "1")
     with open(os.path.join(a.out, f"peer{a.peer}.json"), "w") as f:
         json.dump({"peer": a.peer, "backend": backend, "timeline": timeline, "events": mem.events,
                    "failed_rounds": tr.failed_rounds}, f)
-    mem.stop_heartbeat()
+    mem.leave()  # graceful: a joiner still stepping regroups without this peer at its next round
+    return 0
+
+
+def joiner_loop(a, tr, mem, store, cfg, device, cuda):
+    """A replacement peer: admitted into the running job (params, anchor and buffers streamed from
+    a member), then steps with the group until the survivors are done."""
+    import torch
+
+    t0 = time.perf_counter()
+    tr.join_running_job()
+    admit_ms = (time.perf_counter() - t0) * 1e3
+    g = torch.Generator(device=device).manual_seed(2000 + a.peer)
+    pool = [torch.randint(0, cfg.vocab_size, (a.batch, a.seq + 1), device=device, generator=g) for _ in range(2)]
+    n = 0
+    while not store.check(["vcx/drop/done"]):
+        b = pool[n % len(pool)]
+        tr.step(b[:, :-1], b[:, 1:])
+        n += 1
+    if cuda:
+        torch.cuda.synchronize()
+    with open(os.path.join(a.out, f"joiner{a.peer}.json"), "w") as f:
+        json.dump({"peer": a.peer, "admit_ms": admit_ms, "steps": n, "gen": mem.gen, "events": mem.events}, f)
+    mem.leave()
     return 0
 
 
@@ -176,15 +224,32 @@ def launcher(a):
               "--lease", str(a.lease), "--graph", str(a.graph), "--port", str(port), "--out", out]
     if a.backend:
         common += ["--backend", a.backend]
+    if a.rejoin:
+        common += ["--rejoin", "--after-rejoin", str(a.after_rejoin), "--timeout", str(a.timeout)]
     procs = [subprocess.Popen(common + ["--peer", str(r)], env=env) for r in range(a.peers)]
     t_end = time.time() + a.timeout
     rc = {}
     survivors = [r for r in range(a.peers) if r not in victims]
+    joiners = {}
+    t_dead = {}
     while not all(r in rc for r in survivors) and time.time() < t_end:
         for r, p in enumerate(procs):
             if r not in rc and p.poll() is not None:
                 rc[r] = p.returncode
+                t_dead[r] = time.time()
+        if a.rejoin:
+            for v in victims:
+                if v in rc and v not in joiners:  # the victim is gone: start its replacement
+                    joiners[v] = subprocess.Popen(common + ["--peer", str(v), "--join"], env=env)
         time.sleep(0.2)
+    for v, p in joiners.items():
+        try:
+            p.wait(timeout=max(5.0, t_end - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+        if p.returncode != 0:
+            print(f"[bench_drop] joiner {v} exited with {p.returncode}", file=sys.stderr)
     for r, p in enumerate(procs):
         if r not in rc:
             p.kill()  # timeout, or a SIGSTOPped victim still frozen
@@ -240,6 +305,21 @@ def launcher(a):
         "samples_per_s_before": round(a.peers * a.batch / mean(before) * 1e3, 2),
         "samples_per_s_after": round(len(survivors) * a.batch / mean(after) * 1e3, 2) if after else None,
     }
+    if a.rejoin:
+        rj = next((s for s in steps if regroup is not None and s > regroup and tl[s]["members"] == a.peers), None)
+        back = [tl[s]["ms"] for s in steps if rj is not None and s > rj]
+        adm = []
+        for v in victims:
+            fn = os.path.join(out, f"joiner{v}.json")
+            if os.path.exists(fn):
+                with open(fn) as f:
+                    adm.append(json.load(f)["admit_ms"])
+        rec["metric"] = "step-time under peer drop and rejoin, local-SGD"
+        rec["rejoin_step"] = rj
+        rec["rejoin_sync_ms"] = round(tl[rj]["sync_ms"], 3) if rj is not None else None
+        rec["joiner_admission_ms"] = [round(x, 1) for x in adm]
+        rec["ms_per_step_after_rejoin"] = round(mean(back), 3) if back else None
+        rec["samples_per_s_after_rejoin"] = round(a.peers * a.batch / mean(back) * 1e3, 2) if back else None
     line = json.dumps(rec)
     print(line, flush=True)
     if a.json_out:

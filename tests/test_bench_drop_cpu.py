@@ -41,3 +41,21 @@ def test_bench_drop_two_peers_die_inside_the_collective(tmp_path, fault):
     assert rec["config"]["fault"] == fault and rec["config"]["drop_peers"] == [2, 3]
     assert rec["rounds_aborted_and_redone"] >= 1
     assert rec["regroup_step"] is not None and rec["samples_per_s_after"] > 0
+
+
+def test_bench_drop_kill_two_then_rejoin(tmp_path):
+    """BASELINE config 4 end to end: two of four peers are SIGKILLed inside the all-to-all, the
+    survivors regroup and go on, fresh processes for the victims join the running job (admitted
+    with the group's state) and the full group runs on; the launcher reports the rejoin."""
+    out = tmp_path / "drop.json"
+    env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, os.path.join(ROOT, "bench_drop.py"), "--peers", "4", "--model", "gpt2-tiny", "--batch", "2",
+           "--seq", "32", "--steps", "10", "--warmup", "2", "--lease", "0.5", "--json-out", str(out), "--timeout", "240",
+           "--fault", "collective", "--drop-peers", "2,3", "--rejoin", "--after-rejoin", "4"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads(out.read_text())
+    assert rec["rounds_aborted_and_redone"] >= 1
+    assert rec["rejoin_step"] is not None and rec["rejoin_step"] > rec["regroup_step"]
+    assert len(rec["joiner_admission_ms"]) == 2
+    assert rec["samples_per_s_after_rejoin"] > 0
