@@ -184,6 +184,9 @@ def joiner_loop(a, tr, mem, store, cfg, device, cuda):
     g = torch.Generator(device=device).manual_seed(2000 + a.peer)
     pool = [torch.randint(0, cfg.vocab_size, (a.batch, a.seq + 1), device=device, generator=g) for _ in range(2)]
     n = 0
+    if a.graph and cuda:  # replay the local step as one hipGraph like the other peers
+        tr.capture(pool[0][:, :-1], pool[0][:, 1:], warmup=1)
+        n = 1
     while not store.check(["vcx/drop/done"]):
         b = pool[n % len(pool)]
         tr.step(b[:, :-1], b[:, 1:])

@@ -272,10 +272,17 @@ class PeerGroup:
 
     def send(self, t: torch.Tensor, dst: int, tag: int = 0):
         self._check()
+        if self.backend == "gloo" and t.device.type != "cpu":
+            t = t.to("cpu")  # gloo point-to-point moves host memory only (its collectives stage GPU tensors)
         self._wait(self.pg.send([t], dst, tag), "send")
 
     def recv(self, t: torch.Tensor, src: int, tag: int = 0):
         self._check()
+        if self.backend == "gloo" and t.device.type != "cpu":
+            host = torch.empty(t.shape, dtype=t.dtype)  # a fresh buffer: abandoned if the wait aborts
+            self._wait(self.pg.recv([host], src, tag), "recv")
+            t.copy_(host)
+            return
         self._wait(self.pg.recv([t], src, tag), "recv")
 
     def exchange(self, send_t: torch.Tensor, recv_t: torch.Tensor, peer: int, tag: int = 0):
