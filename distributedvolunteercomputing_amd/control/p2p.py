@@ -90,26 +90,25 @@ class _Pair:
                 return
             kind, payload, tag, cb = op
             if self.dead:
-                cb(PeerFailure(f"pair {self.src}>{self.dst} is dead"))
-                continue
+                res = PeerFailure(f"pair {self.src}>{self.dst} is dead")
+            else:
+                try:
+                    g = self._group()
+                    if kind == "send":
+                        g.send(payload, 1, tag)
+                        res = None
+                    else:
+                        shape, dtype = payload
+                        res = torch.empty(shape, dtype=dtype, device=self.plane.device)
+                        g.recv(res, 0, tag)
+                except Exception as e:  # noqa: BLE001 — PeerFailure or a transport error: this pair only
+                    self.dead = True
+                    self.plane.metrics_incr("p2p_failed")
+                    res = e
             try:
-                g = self._group()
-                if kind == "send":
-                    g.send(payload, 1, tag)
-                    cb(None)
-                else:
-                    shape, dtype = payload
-                    buf = torch.empty(shape, dtype=dtype, device=self.plane.device)
-                    g.recv(buf, 0, tag)
-                    cb(buf)
-            except PeerFailure as e:
-                self.dead = True
-                self.plane.metrics_incr("p2p_failed")
-                cb(e)
-            except Exception as e:  # noqa: BLE001 — a transport error fails this pair only
-                self.dead = True
-                self.plane.metrics_incr("p2p_failed")
-                cb(e)
+                cb(res)
+            except Exception:  # noqa: BLE001 — a consumer's bug must not kill the pair thread
+                self.plane.metrics_incr("p2p_callback_errors")
 
     def close(self):
         self.q.put(None)

@@ -155,6 +155,8 @@ class client:  # noqa: N801 (reference class name)
         if self.sink is not None:
             self.sink.close()
         self.final_sent_frame = 0
+        with self._p2p_lock:  # chunks of an earlier job that never came back are not needed any more
+            self._outgoing.clear()
         src = open_source(path)
         time.sleep(0.0 if path != "live" else 0.5)  # camera warm-up in the reference: 2 s
         out_path = self.path_out
@@ -306,8 +308,9 @@ class client:  # noqa: N801 (reference class name)
                 if isinstance(buf, BaseException):
                     self.metrics.incr("p2p_recv_failed")
                     return
-                with self._p2p_lock:
-                    self._outgoing.pop(int(key), None)
+                if key is not None:
+                    with self._p2p_lock:
+                        self._outgoing.pop(int(key), None)
                 parts = msg.split("||")
                 nums = [int(x) for x in parts[2].split("-")] if parts[2] else []
                 if self.sink is None or parts[0] != self.my_ip:
