@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import math
 import re
-import struct
 from dataclasses import dataclass, field
 
 import numpy as np

@@ -21,7 +21,7 @@ On CPU the same object runs the plain-PyTorch ``CaffeNet`` interpreter (the orac
 from __future__ import annotations
 
 import os
-import numpy as np
+
 import torch
 
 from .. import ops
