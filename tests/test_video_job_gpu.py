@@ -1,0 +1,38 @@
+"""The whole volunteer video job on the GPU: coordinator + requester + 2 worker volunteers in
+one process sharing the MI355X, DetectorEngine (HIP MobileNet-SSD) on every worker, on both
+chunk data planes. Checks the in-order 400-px output and that every frame went through a
+worker; on the p2p plane that no chunk byte crossed the coordinator."""
+import numpy as np
+import pytest
+
+from distributedvolunteercomputing_amd.control.coordinator import coordinator
+from distributedvolunteercomputing_amd.control.peer import client
+from distributedvolunteercomputing_amd.jobs.video import DetectorEngine
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("plane", ["relay", "p2p"])
+def test_video_job_detector_engine(gpu, tmp_path, plane):
+    coord = coordinator("127.0.0.1", 0, ephemeral_ports=True, lease_s=5.0, data_plane=plane)
+    eng = DetectorEngine(device=gpu)
+    mk = lambda: client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0,  # noqa: E731
+                        engine=eng, out_dir=str(tmp_path), out_ext=".npy", chunk=50)
+    req, w1, w2 = mk(), mk(), mk()
+    try:
+        req.become_requester("synthetic:230:640x360")
+        t = req.wait_job(timeout=120)
+        assert t is not None and t > 0
+        out = np.load(req.path_out)
+        assert out.shape == (230, 225, 400, 3)
+        served = w1.metrics.counters.get("frames_processed", 0) + w2.metrics.counters.get("frames_processed", 0)
+        assert served == 230 and req.metrics.counters.get("frames_processed", 0) == 0
+        # the green "person: k" label of the annotation kernel is on every frame
+        g = out[:, 180:225, 0:120]
+        assert (((g[..., 1] == 255) & (g[..., 0] == 0) & (g[..., 2] == 0)).sum(axis=(1, 2)) > 10).all()
+        if plane == "p2p":
+            assert req.plane is not None and req.metrics.counters.get("chunks_returned", 0) == 5
+    finally:
+        for c in (req, w1, w2):
+            c.exit_threads()
+        coord.exit_threads()
