@@ -169,3 +169,28 @@ def test_p2p_worker_process_killed_mid_transfer(tmp_path):
                 p.kill()
             p.join(timeout=5)
         c.exit_threads()
+
+
+def test_streaming_transport_mode(tmp_path):
+    """The reference's PUB/SUB alternative (``req_rep = False``): frames stream without per-frame
+    acks; the job still completes in order."""
+    class C(coordinator):
+        req_rep = False
+
+    class V(client):
+        req_rep = False
+
+    c = C("127.0.0.1", 0, ephemeral_ports=True, lease_s=2.0)
+    mk = lambda e: V("127.0.0.1", "127.0.0.1", control_port=c.control_port, my_port=0, engine=e,  # noqa: E731
+                     out_dir=str(tmp_path), out_ext=".npy", chunk=40)
+    req, w = mk(PassthroughEngine()), mk(PassthroughEngine())
+    try:
+        req.preresize = False
+        req.become_requester("synthetic:130:32x24")
+        assert req.wait_job(timeout=60) is not None
+        out = np.load(req.path_out)
+        assert [decode_frame_index(f) for f in out] == list(range(130))
+    finally:
+        req.exit_threads()
+        w.exit_threads()
+        c.exit_threads()
