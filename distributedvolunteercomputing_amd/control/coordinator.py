@@ -103,6 +103,7 @@ class coordinator:  # noqa: N801  (reference class name)
         self.port_to_client: dict[int, str] = {}
         self.chunks: dict[int, tuple] = {}
         self.requesters: set[str] = set()
+        self.peer_metrics: dict[str, dict] = {}  # volunteer -> its last metrics report
         self._ids = itertools.count(1)
         self._vids = itertools.count(1)
         self._lock = threading.RLock()
@@ -224,6 +225,7 @@ class coordinator:  # noqa: N801  (reference class name)
         with self._lock:
             v = self.vols.pop(addr, None)
             self.requesters.discard(addr)
+            self.peer_metrics.pop(addr, None)
         requeued = self.sched.remove_worker(addr)
         if v is not None:
             self.metrics.incr("leaves_" + reason)
@@ -277,6 +279,12 @@ class coordinator:  # noqa: N801  (reference class name)
                 continue
             requester, command = parts[0], parts[1]
             p2p = bool(hdr.get("p2p"))
+            if command == "metrics":  # a volunteer's metrics report: kept per volunteer
+                m = hdr.get("metrics")
+                if isinstance(m, dict):
+                    with self._lock:
+                        self.peer_metrics[v.addr] = m
+                continue
             if command == "request":
                 while self.req_rep and self.sched.queued() > self.max_buffer and v.alive:
                     time.sleep(0.005)  # back-pressure: the hub stops acking, TCP throttles the requester
@@ -372,7 +380,19 @@ class coordinator:  # noqa: N801  (reference class name)
             "free_ports": len(self.free_ports),
             "data_plane": self.data_plane,
             "metrics": self.metrics.snapshot(),
+            "peers": self.peer_report(),
         }
+
+    def peer_report(self) -> dict:
+        """Per-volunteer metrics (last report of each live volunteer) and their counter totals."""
+        with self._lock:
+            per = {a: m for a, m in self.peer_metrics.items() if a in self.vols}
+        totals: dict[str, float] = {}
+        for m in per.values():
+            for k, val in (m.get("counters") or {}).items():
+                if isinstance(val, (int, float)):
+                    totals[k] = totals.get(k, 0) + val
+        return {"volunteers": per, "totals": totals}
 
     @property
     def clients(self):

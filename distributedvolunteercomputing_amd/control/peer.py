@@ -54,6 +54,7 @@ class client:  # noqa: N801 (reference class name)
     max_buffer = 4000
     my_port = "5554"
     heartbeat_s = 1.0
+    report_every = 10  # heartbeats between metrics reports to the coordinator (0: never)
     preresize = True
 
     def log(self, message):
@@ -409,12 +410,26 @@ class client:  # noqa: N801 (reference class name)
 
     # ------------------------------------------------------------------ heartbeat / leave
     def _heartbeat(self):
+        n = 0
         while self.continue_receiving:
             time.sleep(self.heartbeat_s)
             try:
                 self.hb_ctrl.call("hb", self.my_ip, retries=1)
             except Exception:
                 pass
+            n += 1
+            if self.report_every and n % self.report_every == 0:
+                self.report_metrics()
+
+    def report_metrics(self):
+        """Send this volunteer's metrics snapshot to the coordinator over the data uplink (a
+        metadata-only frame); the coordinator aggregates them per volunteer (status verb)."""
+        snap = self.metrics.snapshot()
+        snap.pop("t", None)
+        try:
+            return self.sender.send_image(f"{self.my_ip}||metrics", _EMPTY, metrics=snap, timeout=2.0)
+        except Exception:  # noqa: BLE001 — best effort
+            return False
 
     def exit_threads(self):
         try:

@@ -91,6 +91,29 @@ def test_dead_worker_chunks_are_redispatched(coord, tmp_path):
             c.exit_threads()
 
 
+def test_volunteer_metrics_aggregated_at_coordinator(coord, tmp_path):
+    req = _client(coord, tmp_path, PassthroughEngine())
+    w = _client(coord, tmp_path, PassthroughEngine())
+    try:
+        req.preresize = False
+        req.become_requester("synthetic:120:32x24")
+        assert req.wait_job(timeout=60) is not None
+        assert w.report_metrics() and req.report_metrics()
+        t0 = time.time()
+        while time.time() - t0 < 10:
+            rep = coord.status()["peers"]
+            if len(rep["volunteers"]) == 2 and rep["totals"].get("frames_processed") == 120:
+                break
+            time.sleep(0.05)
+        rep = coord.status()["peers"]
+        assert rep["volunteers"][w.my_ip]["counters"]["frames_processed"] == 120
+        assert rep["totals"]["chunks_sent"] == 2 and rep["totals"]["frames_processed"] == 120
+    finally:
+        for c in (req, w):
+            c.exit_threads()
+    assert coord.status()["peers"]["volunteers"] == {}  # gone with the volunteers
+
+
 def test_status_and_idempotent_join(coord, tmp_path):
     w = _client(coord, tmp_path, PassthroughEngine())
     try:
