@@ -1,0 +1,55 @@
+"""Sharded optimizer (ZeRO-1 + 2 replicas) with PowerSGD on the GPU, three peer processes sharing
+one MI355X (gloo carries the collectives between GPU buffers: RCCL will not run two ranks on one
+device). One peer drops mid-run; the survivors re-shard from the replicas with no state lost and
+keep identical parameters. Exercises the HIP AdamW on device shards, the PowerSGD kernels inside
+the group's gradient average, and the reshard broadcasts of GPU tensors."""
+import pytest
+import torch
+
+from tests import _mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _peer(rank, world, port, drop_rank):
+    from distributedvolunteercomputing_amd.models.llama import Llama, LlamaConfig
+    from distributedvolunteercomputing_amd.parallel.compression import PowerSGDCompressor
+    from distributedvolunteercomputing_amd.parallel.elastic import ElasticMembership
+    from distributedvolunteercomputing_amd.parallel.zero import ShardedConfig, ShardedDPTrainer
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    store = _mp.make_store(rank, world, port)
+    mem = ElasticMembership(store, rank, backend="gloo", device=dev, lease_s=1.0, heartbeat_s=0.1)
+    mem.bootstrap(list(range(world)))
+    cfg = LlamaConfig.preset("llama-tiny")
+    torch.manual_seed(0)
+    m = Llama(cfg).to(dev, torch.bfloat16)
+    tr = ShardedDPTrainer(m, ShardedConfig(lr=3e-3, weight_decay=0.0, replicas=2), membership=mem, device=dev)
+    tr.compressor = PowerSGDCompressor(tr.flat, rank=4, device=dev)
+    g = torch.Generator(device=dev).manual_seed(100 + rank)
+    x = torch.randint(0, cfg.vocab_size, (4, 64), device=dev, generator=g)
+    losses = []
+    for i in range(12):
+        if rank == drop_rank and i == 5:
+            mem.stop_heartbeat()
+            return {"dropped": True}
+        losses.append(float(tr.step(x, x.roll(-1, 1))))
+    torch.cuda.synchronize()
+    p = tr.flat.param.float().clone()
+    ref = p.clone()
+    mem.group.allreduce_(p)
+    same = torch.allclose(p / mem.group.size, ref, atol=1e-6)
+    out = {"same": bool(same), "members": mem.members, "lost": [e["lost"] for e in tr.reshard_events],
+           "first": losses[0], "last": losses[-1]}
+    mem.leave()
+    return out
+
+
+def test_zero_powersgd_gpu_peers_drop_one(gpu):
+    res = _mp.run(_peer, 3, 2, timeout=240, expect_exit=(2,))
+    for r in (0, 1):
+        assert res[r]["same"], res[r]
+        assert res[r]["members"] == [0, 1]
+        assert all(lost == [] for lost in res[r]["lost"]), res[r]["lost"]
+        assert res[r]["last"] < res[r]["first"]
