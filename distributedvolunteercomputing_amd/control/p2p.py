@@ -32,6 +32,19 @@ import torch
 from ..parallel.peer_group import PeerFailure, PeerGroup
 
 
+def _device_key(dev: torch.device) -> str:
+    """Host + physical device identity (PCI bus id), equal for two processes on one GPU."""
+    import socket
+
+    if dev.type != "cuda":
+        return f"{socket.gethostname()}/cpu/{id(dev)}"  # CPU ends never share an RCCL device
+    props = torch.cuda.get_device_properties(dev)
+    bus = getattr(props, "pci_bus_id", None)
+    ident = f"{getattr(props, 'pci_domain_id', 0)}:{bus}:{getattr(props, 'pci_device_id', 0)}" if bus is not None \
+        else str(getattr(props, "uuid", dev.index))
+    return f"{socket.gethostname()}/{ident}"
+
+
 class _PairWatch:
     """The ``watch`` protocol of PeerGroup guarded waits, tripped by a peer_dead notice."""
 
@@ -72,12 +85,19 @@ class _Pair:
             # non-blocking handshake first: the communicator is built only once both ends are
             # known to be up, so a peer that never shows (crashed before its first transfer)
             # leaves no rendezvous blocked inside c10d — the wait below is abortable
-            store.set(f"vcx/{name}/hello{rank}", "1")
-            while not store.check([f"vcx/{name}/hello{1 - rank}"]):
+            # the hello carries the device identity: RCCL refuses two ranks on one GPU, so a pair
+            # whose ends share a device (several volunteers per GPU) uses gloo (host-staged)
+            store.set(f"vcx/{name}/hello{rank}", self.plane.device_key)
+            other = f"vcx/{name}/hello{1 - rank}"
+            while not store.check([other]):
                 if self.watch.tripped():
                     raise PeerFailure(f"pair {name}: {self.watch.abort_reason()}")
                 time.sleep(0.002)
-            g = PeerGroup(store, rank, 2, self.plane.backend, generation=name, device=self.plane.device,
+            backend = self.plane.backend
+            if backend == "nccl" and store.get(other).decode() == self.plane.device_key:
+                backend = "gloo"
+                self.plane.metrics_incr("p2p_same_device_pairs")
+            g = PeerGroup(store, rank, 2, backend, generation=name, device=self.plane.device,
                           timeout_s=self.plane.timeout_s, watch=self.watch)
             g.connect()
             self.group = g
@@ -128,6 +148,7 @@ class PairPlane:
         self.metrics = metrics
         self._pairs: dict[tuple[int, int], _Pair] = {}
         self._lock = threading.Lock()
+        self.device_key = _device_key(self.device)
 
     def metrics_incr(self, name):
         if self.metrics is not None:

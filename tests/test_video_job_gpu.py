@@ -12,12 +12,15 @@ from distributedvolunteercomputing_amd.jobs.video import DetectorEngine
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("plane", ["relay", "p2p"])
+@pytest.mark.parametrize("plane", ["relay", "p2p", "p2p-rccl"])
 def test_video_job_detector_engine(gpu, tmp_path, plane):
-    coord = coordinator("127.0.0.1", 0, ephemeral_ports=True, lease_s=5.0, data_plane=plane)
+    """p2p-rccl: the pair groups are asked for RCCL with device-resident chunks; all volunteers
+    share this one GPU, so every pair detects it in the handshake and runs on gloo (host-staged)."""
+    coord = coordinator("127.0.0.1", 0, ephemeral_ports=True, lease_s=5.0, data_plane=plane.split("-")[0])
     eng = DetectorEngine(device=gpu)
+    backend = "nccl" if plane == "p2p-rccl" else None
     mk = lambda: client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0,  # noqa: E731
-                        engine=eng, out_dir=str(tmp_path), out_ext=".npy", chunk=50)
+                        engine=eng, out_dir=str(tmp_path), out_ext=".npy", chunk=50, p2p_backend=backend)
     req, w1, w2 = mk(), mk(), mk()
     try:
         req.become_requester("synthetic:230:640x360")
@@ -30,8 +33,11 @@ def test_video_job_detector_engine(gpu, tmp_path, plane):
         # the green "person: k" label of the annotation kernel is on every frame
         g = out[:, 180:225, 0:120]
         assert (((g[..., 1] == 255) & (g[..., 0] == 0) & (g[..., 2] == 0)).sum(axis=(1, 2)) > 10).all()
-        if plane == "p2p":
+        if plane.startswith("p2p"):
             assert req.plane is not None and req.metrics.counters.get("chunks_returned", 0) == 5
+        if plane == "p2p-rccl":
+            assert req.plane.device.type == "cuda"
+            assert req.metrics.counters.get("p2p_same_device_pairs", 0) >= 2
     finally:
         for c in (req, w1, w2):
             c.exit_threads()
