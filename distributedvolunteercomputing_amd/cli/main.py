@@ -3,6 +3,9 @@
   python server.py [server_ip] [--port 9999] ...          REPL: `quit`
   python worker.py [server_ip own_ip] [--port 9999] ...   REPL: `request live|<path>`, `end`, anything else quits
   python -m distributedvolunteercomputing_amd.cli.main train ...   local-SGD training peer
+  python -m distributedvolunteercomputing_amd.cli.main video ...   one-node video job (torchrun, one volunteer per GPU)
+  python -m distributedvolunteercomputing_amd.cli.main status [server_ip]   a coordinator's status JSON
+(``vcx <command>`` once installed: pyproject.toml)
 
 Positional arguments keep the reference's form (server.py:166-169, worker.py:341-344);
 everything else is an optional flag with the reference default.
@@ -25,12 +28,16 @@ def server_main(argv=None):
     ap.add_argument("--ephemeral-ports", action="store_true", help="data ports from the OS instead of 5555..5599")
     ap.add_argument("--train-store-port", type=int, default=None,
                     help="also host the rendezvous store for training peers on this TCP port")
+    ap.add_argument("--data-plane", default="relay", choices=["relay", "p2p"],
+                    help="relay: chunk bytes through this process (reference); p2p: metadata only, chunks "
+                         "travel between the volunteers over pair groups (RCCL between GPU volunteers)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
     from ..control.coordinator import coordinator
 
     c = coordinator(a.ip, a.port, ephemeral_ports=a.ephemeral_ports, policy=a.policy, credits=a.credits,
-                    lease_s=a.lease, verbose=a.verbose, train_store_port=a.train_store_port)
+                    lease_s=a.lease, verbose=a.verbose, train_store_port=a.train_store_port,
+                    data_plane=a.data_plane)
     print(f"\nlistening on {a.ip} port {c.control_port}", flush=True)
     while True:
         try:
@@ -59,6 +66,8 @@ def worker_main(argv=None):
     ap.add_argument("--chunk", type=int, default=100)
     ap.add_argument("--out-dir", default=".")
     ap.add_argument("--out-ext", default=".y4m", choices=[".y4m", ".npy", ""])
+    ap.add_argument("--p2p-backend", default=None, choices=[None, "nccl", "gloo"],
+                    help="pair-group backend on a p2p coordinator (default: RCCL with several GPUs)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
     from ..control.peer import client
@@ -66,7 +75,7 @@ def worker_main(argv=None):
 
     eng = DetectorEngine(device=a.device, prototxt=a.prototxt, caffemodel=a.caffemodel, conf_thresh=a.confidence)
     w = client(a.server_ip, a.own_ip, control_port=a.port, my_port=a.data_port, engine=eng, out_dir=a.out_dir,
-               out_ext=a.out_ext, verbose=a.verbose, chunk=a.chunk)
+               out_ext=a.out_ext, verbose=a.verbose, chunk=a.chunk, p2p_backend=a.p2p_backend)
     while True:
         try:
             line = input("\nEnter request to become requester or end to stop requesting or quit to exit\n")
@@ -121,13 +130,39 @@ def video_main(argv=None):
     return 0
 
 
+def status_main(argv=None):
+    """Print a running coordinator's status (pool, queue, data plane, per-volunteer metrics)."""
+    import json
+
+    ap = argparse.ArgumentParser(prog="status", description=status_main.__doc__)
+    ap.add_argument("server_ip", nargs="?", default="localhost")
+    ap.add_argument("--port", type=int, default=9999, help="coordinator UDP control port")
+    ap.add_argument("--config", action="store_true", help="print this process's runtime config instead")
+    a = ap.parse_args(argv)
+    if a.config:
+        print(config.describe())
+        return 0
+    from ..control import protocol
+
+    cc = protocol.ControlClient(a.server_ip, a.port, retries=3)
+    try:
+        print(json.dumps(json.loads(cc.call("status", "status:0")), indent=2))
+    except TimeoutError as e:
+        print(f"no reply: {e}", file=sys.stderr)
+        return 1
+    return 0
+
+
+COMMANDS = {"server": server_main, "worker": worker_main, "train": train_main, "video": video_main,
+            "status": status_main}
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
-    if not argv or argv[0] not in ("server", "worker", "train", "video"):
-        print("usage: python -m distributedvolunteercomputing_amd.cli.main {server|worker|train|video} ...")
+    if not argv or argv[0] not in COMMANDS:
+        print(f"usage: vcx {{{'|'.join(COMMANDS)}}} ...  (or python -m distributedvolunteercomputing_amd.cli.main)")
         return 2
-    cmd, rest = argv[0], argv[1:]
-    return {"server": server_main, "worker": worker_main, "train": train_main, "video": video_main}[cmd](rest)
+    return COMMANDS[argv[0]](argv[1:])
 
 
 if __name__ == "__main__":
