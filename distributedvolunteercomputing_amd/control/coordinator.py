@@ -365,7 +365,7 @@ class coordinator:  # noqa: N801  (reference class name)
                 v.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "work", "chunk": a.chunk, "src": meta["src"],
                                              "cshape": meta["cshape"], "key": meta["key"]}))
                 r.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "send", "chunk": a.chunk, "dst": v.vid,
-                                             "key": meta["key"]}))
+                                             "key": meta["key"], "cshape": meta["cshape"]}))
             self.metrics.incr("dispatched")
         self.log("send_request terminated.")
 

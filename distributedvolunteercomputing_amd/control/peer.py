@@ -313,8 +313,13 @@ class client:  # noqa: N801 (reference class name)
         elif cmd == "send":  # requester: chunk `key` -> worker `dst`
             with self._p2p_lock:
                 t = self._outgoing.get(int(hdr["key"]))
-            if t is not None:
-                plane.send(int(hdr["dst"]), t, cid)
+            if t is None:
+                # a chunk this requester no longer holds (an earlier job's): the worker has posted
+                # the matching receive, so send a placeholder to keep the pair's FIFO in step; its
+                # result lands on frames the sink has already written and is dropped there
+                self.metrics.incr("p2p_placeholder_sends")
+                t = torch.zeros(tuple(hdr.get("cshape") or (0,)), dtype=torch.uint8)
+            plane.send(int(hdr["dst"]), t, cid)
         elif cmd == "work":  # worker: receive the chunk, then infer it
             msg = hdr["msg"]
 
