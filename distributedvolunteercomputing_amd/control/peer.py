@@ -153,6 +153,7 @@ class client:  # noqa: N801 (reference class name)
 
     # ------------------------------------------------------------------ requester role
     def requester(self, path):
+        os.makedirs(self.out_dir, exist_ok=True)
         self.path_out = os.path.join(self.out_dir, f"video{self.path_out_num}{self.out_ext}")
         self.path_out_num += 1
         if self.sink is not None:
@@ -299,8 +300,17 @@ class client:  # noqa: N801 (reference class name)
                 if requester != self.my_ip or self.sink is None:
                     print("frame not mine.", flush=True)
                     continue
-                for i, n in enumerate(nums):
-                    self.sink.push(n, arr[i])
+                self._deliver(nums, arr)
+
+    def _deliver(self, nums, frames):
+        """Hand returned frames to the in-order sink; a sink failure (e.g. an unwritable output)
+        is logged and counted instead of killing the receive thread."""
+        try:
+            for i, n in enumerate(nums):
+                self.sink.push(n, frames[i])
+        except Exception as e:  # noqa: BLE001
+            self.metrics.incr("sink_errors")
+            print(f"output sink failed: {type(e).__name__}: {e}", flush=True)
 
     def _p2p_command(self, hdr):
         """One coordinator instruction of the p2p plane (see the module docstring)."""
@@ -351,9 +361,7 @@ class client:  # noqa: N801 (reference class name)
                 if self.sink is None or parts[0] != self.my_ip:
                     return
                 self.metrics.incr("chunks_returned")
-                out = buf.cpu().numpy()
-                for i, n in enumerate(nums):
-                    self.sink.push(n, out[i])
+                self._deliver(nums, buf.cpu().numpy())
             plane.recv(int(hdr["src"]), hdr["cshape"], torch.uint8, cid, done)
         elif cmd == "drop":  # a duplicate result of a re-dispatched chunk: nobody wants it
             with self._p2p_lock:

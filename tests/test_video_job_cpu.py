@@ -91,6 +91,30 @@ def test_dead_worker_chunks_are_redispatched(coord, tmp_path):
             c.exit_threads()
 
 
+def test_two_requesters_at_once(coord, tmp_path):
+    """Two volunteers submit videos concurrently (reference: several requesters interleave in
+    one FIFO, server.py:24,56,80-82); each gets its own frames back, in order, every frame
+    processed exactly once."""
+    a = _client(coord, tmp_path / "a", PassthroughEngine(), chunk=30)
+    b = _client(coord, tmp_path / "b", PassthroughEngine(), chunk=30)
+    w = _client(coord, tmp_path / "w", PassthroughEngine(delay_s=0.01), chunk=30)
+    try:
+        for c in (a, b):
+            c.preresize = False
+        a.become_requester("synthetic:150:32x24")
+        b.become_requester("synthetic:95:48x32")
+        assert a.wait_job(timeout=60) is not None and b.wait_job(timeout=60) is not None
+        oa, ob = np.load(a.path_out), np.load(b.path_out)
+        assert oa.shape == (150, 24, 32, 3) and ob.shape == (95, 32, 48, 3)
+        assert [decode_frame_index(f) for f in oa] == list(range(150))
+        assert [decode_frame_index(f) for f in ob] == list(range(95))
+        # a requester whose video is done is back in the pool (stop verb) and may serve the other
+        assert sum(c.metrics.counters.get("frames_processed", 0) for c in (a, b, w)) == 245
+    finally:
+        for c in (a, b, w):
+            c.exit_threads()
+
+
 def test_volunteer_metrics_aggregated_at_coordinator(coord, tmp_path):
     req = _client(coord, tmp_path, PassthroughEngine())
     w = _client(coord, tmp_path, PassthroughEngine())
