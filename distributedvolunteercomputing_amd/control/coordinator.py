@@ -179,7 +179,12 @@ class coordinator:  # noqa: N801  (reference class name)
             self.sched.heartbeat(addr, now)
             return protocol.reply_ok()
         if verb == "status":
-            return protocol.reply_ok(json.dumps(self.status()))
+            st = self.status()
+            js = json.dumps(st)
+            if len(js) > 60000:  # one UDP datagram: per-volunteer details give way to the totals
+                st["peers"]["volunteers"] = {a: {"truncated": True} for a in st["peers"]["volunteers"]}
+                js = json.dumps(st)[:60000]
+            return protocol.reply_ok(js)
         if verb == "store":  # where training peers rendezvous
             return protocol.reply_ok(str(self.train_store_port) if self.train_store is not None else "")
         if verb == "p2p":

@@ -50,7 +50,10 @@ def run_node_job(source: str, out_dir: str, *, engine_factory, chunk: int = 100,
             while not store.check([DONE_KEY]):
                 time.sleep(0.05)
             return int(me.metrics.counters.get("frames_processed", 0))
+        t_join = time.time() + 300
         while int(store.add("vcx/node_job/joined", 0)) < world:  # every volunteer is in the pool
+            if time.time() > t_join:
+                raise TimeoutError(f"only {int(store.add('vcx/node_job/joined', 0))} of {world} volunteers joined")
             time.sleep(0.01)
         me.become_requester(source)
         t = me.wait_job(timeout=timeout_s)

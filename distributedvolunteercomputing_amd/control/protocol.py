@@ -111,7 +111,7 @@ class ControlClient:
                 ready, _, _ = select.select([self.sock], [], [], left)
                 if not ready:
                     break
-                data, _ = self.sock.recvfrom(4096)
+                data, _ = self.sock.recvfrom(65535)  # status replies can be large
                 ok, payload = parse_reply(data)
                 if ok:
                     return payload

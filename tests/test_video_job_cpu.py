@@ -132,6 +132,13 @@ def test_volunteer_metrics_aggregated_at_coordinator(coord, tmp_path):
         rep = coord.status()["peers"]
         assert rep["volunteers"][w.my_ip]["counters"]["frames_processed"] == 120
         assert rep["totals"]["chunks_sent"] == 2 and rep["totals"]["frames_processed"] == 120
+        # the status VERB (one UDP datagram) carries the per-volunteer reports too
+        import json
+
+        from distributedvolunteercomputing_amd.control import protocol
+
+        st = json.loads(protocol.ControlClient("127.0.0.1", coord.control_port).call("status", "x:0"))
+        assert st["peers"]["totals"]["frames_processed"] == 120 and len(st["peers"]["volunteers"]) == 2
     finally:
         for c in (req, w):
             c.exit_threads()
