@@ -183,7 +183,7 @@ class coordinator:  # noqa: N801  (reference class name)
             js = json.dumps(st)
             if len(js) > 60000:  # one UDP datagram: per-volunteer details give way to the totals
                 st["peers"]["volunteers"] = {a: {"truncated": True} for a in st["peers"]["volunteers"]}
-                js = json.dumps(st)[:60000]
+                js = json.dumps(st)
             return protocol.reply_ok(js)
         if verb == "store":  # where training peers rendezvous
             return protocol.reply_ok(str(self.train_store_port) if self.train_store is not None else "")
