@@ -290,6 +290,9 @@ class coordinator:  # noqa: N801  (reference class name)
                     with self._lock:
                         self.peer_metrics[v.addr] = m
                 continue
+            if p2p and command in ("request", "processed") and not protocol.valid_chunk_shape(hdr.get("cshape")):
+                self.metrics.incr("bad_frames")  # a shape the other end would have to allocate blindly
+                continue
             if command == "request":
                 while self.req_rep and self.sched.queued() > self.max_buffer and v.alive:
                     time.sleep(0.005)  # back-pressure: the hub stops acking, TCP throttles the requester

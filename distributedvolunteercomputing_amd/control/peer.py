@@ -318,6 +318,9 @@ class client:  # noqa: N801 (reference class name)
         plane = self.plane
         if plane is None:
             return
+        if cmd in ("work", "recv_result", "send") and not protocol.valid_chunk_shape(hdr.get("cshape")):
+            self.metrics.incr("bad_frames")
+            return
         if cmd == "peer_dead":
             plane.peer_dead(int(hdr["vid"]))
         elif cmd == "send":  # requester: chunk `key` -> worker `dst`

@@ -120,3 +120,19 @@ class ControlClient:
 
     def close(self):
         self.sock.close()
+
+
+MAX_CHUNK_BYTES = 2 << 30  # the data plane's frame cap (transport.cpp max_payload default)
+
+
+def valid_chunk_shape(shape, max_bytes: int = MAX_CHUNK_BYTES) -> bool:
+    """A p2p chunk shape announced by a volunteer: 1-4 non-negative ints, at most `max_bytes`
+    uint8 elements (the receiving volunteer allocates exactly this before the transfer)."""
+    if not isinstance(shape, (list, tuple)) or not 1 <= len(shape) <= 4:
+        return False
+    n = 1
+    for d in shape:
+        if not isinstance(d, int) or isinstance(d, bool) or d < 0:
+            return False
+        n *= d
+    return n <= max_bytes

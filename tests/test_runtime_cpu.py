@@ -238,3 +238,11 @@ def test_coordinator_ignores_unjoined_and_bad_frames():
         assert protocol.addr_matches("10.0.0.5:5554", "127.0.0.1")  # local sender: trusted
     finally:
         c.exit_threads()
+
+
+
+def test_valid_chunk_shape():
+    assert protocol.valid_chunk_shape([100, 225, 400, 3])
+    assert protocol.valid_chunk_shape((0,))
+    for bad in (None, [], [1, 2, 3, 4, 5], [-1, 3], [2.5, 3], ["3"], [True], [1 << 20, 1 << 20, 3], "abc"):
+        assert not protocol.valid_chunk_shape(bad), bad
