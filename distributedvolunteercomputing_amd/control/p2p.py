@@ -85,18 +85,21 @@ class _Pair:
             # non-blocking handshake first: the communicator is built only once both ends are
             # known to be up, so a peer that never shows (crashed before its first transfer)
             # leaves no rendezvous blocked inside c10d — the wait below is abortable
-            # the hello carries the device identity: RCCL refuses two ranks on one GPU, so a pair
-            # whose ends share a device (several volunteers per GPU) uses gloo (host-staged)
-            store.set(f"vcx/{name}/hello{rank}", self.plane.device_key)
+            # the hello carries each end's backend and device identity. RCCL only when both ends
+            # run it on DIFFERENT devices (it refuses two ranks on one GPU; a CPU volunteer speaks
+            # gloo only); otherwise the pair uses gloo, GPU tensors staged through host memory
+            me = f"{self.plane.backend}|{self.plane.device_key}"
+            store.set(f"vcx/{name}/hello{rank}", me)
             other = f"vcx/{name}/hello{1 - rank}"
             while not store.check([other]):
                 if self.watch.tripped():
                     raise PeerFailure(f"pair {name}: {self.watch.abort_reason()}")
                 time.sleep(0.002)
-            backend = self.plane.backend
-            if backend == "nccl" and store.get(other).decode() == self.plane.device_key:
-                backend = "gloo"
-                self.plane.metrics_incr("p2p_same_device_pairs")
+            o_backend, _, o_dev = store.get(other).decode().partition("|")
+            backend = "nccl" if self.plane.backend == o_backend == "nccl" and o_dev != self.plane.device_key else "gloo"
+            if self.plane.backend == "nccl" and backend == "gloo":
+                self.plane.metrics_incr("p2p_same_device_pairs" if o_dev == self.plane.device_key
+                                        else "p2p_mixed_backend_pairs")
             g = PeerGroup(store, rank, 2, backend, generation=name, device=self.plane.device,
                           timeout_s=self.plane.timeout_s, watch=self.watch)
             g.connect()

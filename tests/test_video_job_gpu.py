@@ -12,16 +12,18 @@ from distributedvolunteercomputing_amd.jobs.video import DetectorEngine
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("plane", ["relay", "p2p", "p2p-rccl"])
+@pytest.mark.parametrize("plane", ["relay", "p2p", "p2p-rccl", "p2p-mixed"])
 def test_video_job_detector_engine(gpu, tmp_path, plane):
     """p2p-rccl: the pair groups are asked for RCCL with device-resident chunks; all volunteers
     share this one GPU, so every pair detects it in the handshake and runs on gloo (host-staged)."""
     coord = coordinator("127.0.0.1", 0, ephemeral_ports=True, lease_s=5.0, data_plane=plane.split("-")[0])
     eng = DetectorEngine(device=gpu)
-    backend = "nccl" if plane == "p2p-rccl" else None
-    mk = lambda: client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0,  # noqa: E731
-                        engine=eng, out_dir=str(tmp_path), out_ext=".npy", chunk=50, p2p_backend=backend)
-    req, w1, w2 = mk(), mk(), mk()
+    backend = "nccl" if plane in ("p2p-rccl", "p2p-mixed") else None
+    mk = lambda be: client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0,  # noqa: E731
+                           engine=eng, out_dir=str(tmp_path), out_ext=".npy", chunk=50, p2p_backend=be)
+    # p2p-mixed: an RCCL requester with gloo-only (CPU-plane) workers: the pairs negotiate gloo
+    req = mk(backend)
+    w1, w2 = (mk("gloo"), mk("gloo")) if plane == "p2p-mixed" else (mk(backend), mk(backend))
     try:
         req.become_requester("synthetic:230:640x360")
         t = req.wait_job(timeout=120)
@@ -38,6 +40,8 @@ def test_video_job_detector_engine(gpu, tmp_path, plane):
         if plane == "p2p-rccl":
             assert req.plane.device.type == "cuda"
             assert req.metrics.counters.get("p2p_same_device_pairs", 0) >= 2
+        if plane == "p2p-mixed":
+            assert req.metrics.counters.get("p2p_mixed_backend_pairs", 0) >= 2
     finally:
         for c in (req, w1, w2):
             c.exit_threads()
