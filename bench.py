@@ -59,8 +59,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cuda = torch.cuda.is_available()
     if cuda:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        # one rank per GPU; ranks beyond the GPU count share cards (rehearsal launches only)
+        device = torch.device("cuda", local % torch.cuda.device_count())
+        torch.cuda.set_device(device)
     else:
         device = torch.device("cpu")
     if world > 1:

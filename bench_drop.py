@@ -229,7 +229,15 @@ def launcher(a):
         common += ["--backend", a.backend]
     if a.rejoin:
         common += ["--rejoin", "--after-rejoin", str(a.after_rejoin), "--timeout", str(a.timeout)]
-    procs = [subprocess.Popen(common + ["--peer", str(r)], env=env) for r in range(a.peers)]
+    def peer_env(r):
+        if a.backend == "nccl" and a.peers > max(ngpu, 1):
+            # RCCL rehearsal with several peers per GPU: a distinct host identity per peer gets past
+            # RCCL's duplicate-GPU check, and the communicators run over loopback sockets
+            # (scripts/rccl_rehearsal_launch.py); the RCCL code paths are the real ones
+            return dict(env, NCCL_HOSTID=f"vcx-peer-{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+        return env
+
+    procs = [subprocess.Popen(common + ["--peer", str(r)], env=peer_env(r)) for r in range(a.peers)]
     t_end = time.time() + a.timeout
     rc = {}
     survivors = [r for r in range(a.peers) if r not in victims]
@@ -243,7 +251,7 @@ def launcher(a):
         if a.rejoin:
             for v in victims:
                 if v in rc and v not in joiners:  # the victim is gone: start its replacement
-                    joiners[v] = subprocess.Popen(common + ["--peer", str(v), "--join"], env=env)
+                    joiners[v] = subprocess.Popen(common + ["--peer", str(v), "--join"], env=peer_env(v))
         time.sleep(0.2)
     for v, p in joiners.items():
         try:

@@ -123,7 +123,7 @@ def main(argv=None):
     world = a.world if a.world is not None else int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cuda = torch.cuda.is_available()
-    device = torch.device("cuda", local) if cuda else torch.device("cpu")
+    device = torch.device("cuda", local % torch.cuda.device_count()) if cuda else torch.device("cpu")
     if cuda:
         torch.cuda.set_device(device)
     backend = a.backend or ("nccl" if cuda else "gloo")
