@@ -142,12 +142,17 @@ def peer_main(a):
     i = a.warmup
     t_cap = time.time() + a.timeout * 0.8
     full_since = None
+    gen_at_drop = 1 << 30
     while True:
+        if i == a.drop_at:
+            gen_at_drop = mem.gen
         if i >= a.warmup + a.steps:
             if not a.rejoin or a.peer in victims:
                 break
             # config 4: keep going until the victims are back and the full group ran a while
-            if timeline and timeline[-1]["members"] == a.peers and timeline[-1]["gen"] > 1:
+            # (the drop and the rejoin can land in ONE new generation when the replacements
+            # register before the survivors agree on the recovery round)
+            if timeline and timeline[-1]["members"] == a.peers and timeline[-1]["gen"] > gen_at_drop:
                 full_since = i if full_since is None else full_since
                 if i - full_since >= a.after_rejoin:
                     break
@@ -283,9 +288,11 @@ def launcher(a):
             cur["ms"] = max(cur["ms"], e["ms"])  # a step ends when its slowest survivor is done
     steps = sorted(tl)
     before = [tl[s]["ms"] for s in steps if s < a.drop_at]
-    regroup = next((s for s in steps if s >= a.drop_at and tl[s]["members"] == len(survivors) and tl[s]["synced"]),
-                   None)
-    after = [tl[s]["ms"] for s in steps if regroup is not None and s > regroup]
+    gen_before = max((tl[s]["gen"] for s in steps if s < a.drop_at), default=0)
+    regroup = next((s for s in steps if s >= a.drop_at and tl[s]["gen"] > gen_before and tl[s]["synced"]), None)
+    # after the drop: the survivors-only steps (without --rejoin: every step after the regroup)
+    after = [tl[s]["ms"] for s in steps if regroup is not None and s > regroup
+             and (not a.rejoin or tl[s]["members"] < a.peers)]
     window = [tl[s]["ms"] for s in steps]
     mean = lambda xs: sum(xs) / len(xs) if xs else float("nan")  # noqa: E731
     # the stall: the averaging call that detected the silent peer (lease wait + agreement + new
@@ -317,7 +324,7 @@ def launcher(a):
         "samples_per_s_after": round(len(survivors) * a.batch / mean(after) * 1e3, 2) if after else None,
     }
     if a.rejoin:
-        rj = next((s for s in steps if regroup is not None and s > regroup and tl[s]["members"] == a.peers), None)
+        rj = next((s for s in steps if regroup is not None and s >= regroup and tl[s]["members"] == a.peers), None)
         back = [tl[s]["ms"] for s in steps if rj is not None and s > rj]
         adm = []
         for v in victims:

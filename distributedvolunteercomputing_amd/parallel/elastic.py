@@ -97,6 +97,9 @@ class ElasticMembership:
         if backend == "nccl":
             # abortable (non-blocking) RCCL communicator init for every generation's group
             os.environ.setdefault("TORCH_NCCL_USE_COMM_NONBLOCKING", "1")
+            # a collective that outlives the group timeout (e.g. its abort is slow) must not take
+            # the survivor down: c10d's watchdog then only aborts the communicator (CleanUpOnly)
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
 
     # ------------------------------------------------------------------ heartbeat + watchdog
     def start_heartbeat(self):
@@ -299,7 +302,13 @@ class ElasticMembership:
         okey = f"{_P}out/{g}/{k}"
         others = [m for m in self.members if m != self.pid]
         now = time.time()
-        hb_seen = {m: (self._hb(m), now) for m in others}
+        hb_seen = {}
+        for m in others:
+            # recovery: a member the watchdog already saw silent keeps its silence clock (the
+            # aborted round's lease wait is not paid a second time before it is declared dead)
+            hb = self._hb(m)
+            ws = self._watch_seen.get(m) if recovery else None
+            hb_seen[m] = (hb, ws[1]) if ws is not None and ws[0] == hb else (hb, now)
         arrived = {self.pid: self.has_model}
         dead, left = set(), set()
         t0 = now

@@ -39,6 +39,14 @@ class PeerFailure(RuntimeError):
 
 
 _GRAVEYARD: list = []  # aborted gloo groups with possibly blocked ops (see module docstring)
+_ABORTING: list = []  # (RCCL group, thread running its ncclCommAbort): kept alive until it returns
+
+
+def _abort_quietly(pg):
+    try:
+        pg.abort()
+    except Exception:  # noqa: BLE001
+        pass
 
 
 def _gloo_pg(store, rank, size, timeout):
@@ -71,6 +79,7 @@ class PeerGroup:
         self.fault_hook = None  # test hook: called inside every guarded collective (after issue)
         self.poll_s = 2e-4
         self._pending = None  # deferred gloo rendezvous (watched groups connect in connect())
+        self._connected = False
         timeout = _dt.timedelta(seconds=timeout_s)
         prefixed = dist.PrefixStore(f"vcx/pg/{generation}", store)
         self.pg = None
@@ -91,6 +100,7 @@ class PeerGroup:
         """Wrap torch.distributed's default process group (e.g. the torchrun world)."""
         self = cls.__new__(cls)
         self._pending = None
+        self._connected = True  # the default group is connected by init_process_group
         self.generation = 0
         self.size = dist.get_world_size()
         self.rank = dist.get_rank()
@@ -113,12 +123,16 @@ class PeerGroup:
         if self._pending is not None:
             self._connect_gloo()
             return
-        if self.pg is None or self.backend != "nccl" or self.device is None:
+        if self.pg is None or self.backend != "nccl" or self.device is None or self._connected:
             return
         dev = torch.device(self.device)
         if dev.type == "cuda":
             self._check()
+            # once per generation: ProcessGroupNCCL.eager_connect_single_device builds a NEW
+            # communicator on every call (a second bootstrap per round, whose ranks can pick up
+            # different unique ids and hang the next collective)
             self.pg.eager_connect_single_device(dev)
+            self._connected = True
 
     def _connect_gloo(self):
         args, self._pending = self._pending, None
@@ -205,19 +219,27 @@ class PeerGroup:
             raise PeerFailure(f"gen {self.generation}: aborted ({self.watch.abort_reason()})")
 
     def abort(self):
-        """Tear down this generation's communicator; safe to call from the watchdog thread."""
+        """Tear down this generation's communicator; safe to call from the watchdog thread, and
+        it never blocks the caller. For RCCL, ``ncclCommAbort`` (which makes the kernels spinning
+        on a dead peer exit) runs on a helper thread: it waits for RCCL's proxy thread, which
+        can sit in a connect-retry loop towards a dead peer for tens of seconds, and neither the
+        heartbeat thread (a silent survivor looks dead to everyone else) nor the recovering
+        main thread may wait for that. The next generation uses a new communicator and new
+        streams, so nothing queues behind the aborted kernels."""
         if self.aborted:
             return
         self.aborted = True
         pg, self.pg = self.pg, None
         if pg is None:
             return
-        try:
-            pg.abort()  # RCCL: ncclCommAbort unblocks kernels waiting on a dead peer
-        except Exception:  # noqa: BLE001
-            pass
-        if self.backend != "nccl":
-            _GRAVEYARD.append(pg)
+        if self.backend == "nccl":
+            th = threading.Thread(target=_abort_quietly, args=(pg,), name=f"vcx-pg{self.generation}-abort",
+                                  daemon=True)
+            th.start()
+            _ABORTING.append((pg, th))
+            return
+        _abort_quietly(pg)
+        _GRAVEYARD.append(pg)
 
     # ------------------------------------------------------------------ collectives
     def allreduce_(self, t: torch.Tensor):
