@@ -1,6 +1,6 @@
 """Sharded optimizer (ZeRO-1 + 2 replicas) with PowerSGD on the GPU, three peer processes sharing
-one MI355X (gloo carries the collectives between GPU buffers: RCCL will not run two ranks on one
-device). One peer drops mid-run; the survivors re-shard from the replicas with no state lost and
+one MI355X, over gloo and over RCCL (one NCCL_HOSTID per rank: RCCL communicators over loopback
+sockets, since RCCL will not otherwise run two ranks on one device). One peer drops mid-run; the survivors re-shard from the replicas with no state lost and
 keep identical parameters. Exercises the HIP AdamW on device shards, the PowerSGD kernels inside
 the group's gradient average, and the reshard broadcasts of GPU tensors."""
 import pytest
@@ -11,7 +11,11 @@ from tests import _mp
 pytestmark = pytest.mark.gpu
 
 
-def _peer(rank, world, port, drop_rank):
+def _peer(rank, world, port, drop_rank, backend="gloo"):
+    import os
+
+    if backend == "nccl":  # RCCL between ranks sharing the card (tests/test_rccl_rehearsal_gpu.py)
+        os.environ.update(NCCL_HOSTID=f"vcx-zero-{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
     from distributedvolunteercomputing_amd.models.llama import Llama, LlamaConfig
     from distributedvolunteercomputing_amd.parallel.compression import PowerSGDCompressor
     from distributedvolunteercomputing_amd.parallel.elastic import ElasticMembership
@@ -20,7 +24,7 @@ def _peer(rank, world, port, drop_rank):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     store = _mp.make_store(rank, world, port)
-    mem = ElasticMembership(store, rank, backend="gloo", device=dev, lease_s=1.0, heartbeat_s=0.1)
+    mem = ElasticMembership(store, rank, backend=backend, device=dev, lease_s=1.0, heartbeat_s=0.1)
     mem.bootstrap(list(range(world)))
     cfg = LlamaConfig.preset("llama-tiny")
     torch.manual_seed(0)
@@ -46,8 +50,9 @@ def _peer(rank, world, port, drop_rank):
     return out
 
 
-def test_zero_powersgd_gpu_peers_drop_one(gpu):
-    res = _mp.run(_peer, 3, 2, timeout=240, expect_exit=(2,))
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_zero_powersgd_gpu_peers_drop_one(gpu, backend):
+    res = _mp.run(_peer, 3, 2, backend, timeout=240, expect_exit=(2,))
     for r in (0, 1):
         assert res[r]["same"], res[r]
         assert res[r]["members"] == [0, 1]
