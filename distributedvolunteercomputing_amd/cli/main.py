@@ -120,7 +120,7 @@ def video_main(argv=None):
     from ..jobs.video import DetectorEngine
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    dev = torch.device("cuda", local % torch.cuda.device_count()) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     res = run_node_job(a.source, a.out_dir, engine_factory=lambda: DetectorEngine(device=dev), chunk=a.chunk,

@@ -58,7 +58,8 @@ def run_node_job(source: str, out_dir: str, *, engine_factory, chunk: int = 100,
         me.become_requester(source)
         t = me.wait_job(timeout=timeout_s)
         st = {"frames": me.final_sent_frame, "job_s": t, "chunks": int(me.metrics.counters.get("chunks_sent", 0)),
-              "out": me.path_out, "coordinator": dict(coord.metrics.counters)}
+              "out": me.path_out, "coordinator": dict(coord.metrics.counters),
+              "requester": dict(me.metrics.counters)}
         store.set(DONE_KEY, "1")
         return st
     finally:

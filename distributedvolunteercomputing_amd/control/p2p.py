@@ -33,16 +33,21 @@ from ..parallel.peer_group import PeerFailure, PeerGroup
 
 
 def _device_key(dev: torch.device) -> str:
-    """Host + physical device identity (PCI bus id), equal for two processes on one GPU."""
+    """Host + physical device identity (PCI bus id), equal for two processes on one GPU. The
+    host part is RCCL's own: ``NCCL_HOSTID`` when set (RCCL's duplicate-GPU check compares that
+    host hash and the bus id, so processes with distinct host ids may share a card — the one-GPU
+    rehearsal of scripts/rccl_rehearsal_launch.py), else the hostname."""
+    import os
     import socket
 
+    host = os.environ.get("NCCL_HOSTID") or socket.gethostname()
     if dev.type != "cuda":
-        return f"{socket.gethostname()}/cpu/{id(dev)}"  # CPU ends never share an RCCL device
+        return f"{host}/cpu/{id(dev)}"  # CPU ends never share an RCCL device
     props = torch.cuda.get_device_properties(dev)
     bus = getattr(props, "pci_bus_id", None)
     ident = f"{getattr(props, 'pci_domain_id', 0)}:{bus}:{getattr(props, 'pci_device_id', 0)}" if bus is not None \
         else str(getattr(props, "uuid", dev.index))
-    return f"{socket.gethostname()}/{ident}"
+    return f"{host}/{ident}"
 
 
 class _PairWatch:
@@ -100,6 +105,7 @@ class _Pair:
             if self.plane.backend == "nccl" and backend == "gloo":
                 self.plane.metrics_incr("p2p_same_device_pairs" if o_dev == self.plane.device_key
                                         else "p2p_mixed_backend_pairs")
+            self.plane.metrics_incr(f"p2p_pairs_{backend}")
             g = PeerGroup(store, rank, 2, backend, generation=name, device=self.plane.device,
                           timeout_s=self.plane.timeout_s, watch=self.watch)
             g.connect()
@@ -190,3 +196,13 @@ class PairPlane:
         for p in pairs:
             p.watch.declare_abort("plane closed")
             p.close()
+        # release the pair communicators now, from this thread, once their pair threads are done:
+        # a gloo process group left to interpreter finalisation aborts the process in its
+        # destructor ("terminate called without an active exception")
+        for p in pairs:
+            p.thread.join(timeout=5.0)
+            if not p.thread.is_alive() and p.group is not None:
+                g, p.group = p.group, None
+                if g.backend == "nccl":
+                    g.shutdown()
+                g.pg = None

@@ -26,3 +26,24 @@ def test_node_job_over_p2p_plane(tmp_path):
     assert st["coordinator"].get("chunks_done") == 5
     frames = np.load(st["out"])
     assert [decode_frame_index(f) for f in frames] == list(range(230))
+
+
+def test_video_cli_three_processes_exit_cleanly(tmp_path):
+    """The `video` command as three separate processes (torchrun-style env, gloo pairs): every
+    volunteer exits 0 (a gloo pair group left to interpreter finalisation used to abort the
+    process with "terminate called without an active exception")."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "scripts", "rccl_rehearsal_launch.py"), "--nproc", "3", "--timeout",
+           "150", "--log-dir", str(tmp_path), "--", sys.executable, "-u", "-m",
+           "distributedvolunteercomputing_amd.cli.main", "video", "--source", "synthetic:80:96x64", "--out-dir",
+           str(tmp_path), "--out-ext", ".npy", "--chunk", "40", "--port", str(_mp.free_port()), "--store-port",
+           str(_mp.free_port())]
+    env = dict(os.environ, VCX_P2P_BACKEND="gloo")
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=200, env=env)
+    errs = "".join((tmp_path / f"rank{i}.err").read_text()[-1500:] for i in range(3))
+    assert r.returncode == 0, r.stderr + errs
+    assert "terminate called" not in errs
