@@ -30,6 +30,7 @@ def _bool(s: str) -> bool:
 class RuntimeConfig:
     # ---- compute path
     gemm: str = "lib"  # VCX_GEMM: "lib" (hipBLASLt/rocBLAS) or "vcx" (csrc/kernels/gemm.hip, opt-in: 0.74-0.84x lib)
+    gemm_wgrad: str = "lib"  # VCX_GEMM_WGRAD: weight gradients on "lib" (split-M batched GEMM) or "vcx" (gemm_tn)
     gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)
     wgrad_big_split_min_m: int = 16384  # VCX_WGRAD_BIG_SPLIT_MIN_M: rows above which weight grads split over K
     async_wgrad: bool = False  # VCX_ASYNC_WGRAD: weight-grad GEMMs on a side stream (measured slower)
@@ -52,6 +53,7 @@ class RuntimeConfig:
 # field -> (environment variable, parser)
 _ENV = {
     "gemm": ("VCX_GEMM", str),
+    "gemm_wgrad": ("VCX_GEMM_WGRAD", str),
     "gemm_select": ("VCX_GEMM_SELECT", _bool),
     "wgrad_big_split_min_m": ("VCX_WGRAD_BIG_SPLIT_MIN_M", int),
     "async_wgrad": ("VCX_ASYNC_WGRAD", _bool),
@@ -68,7 +70,7 @@ _ENV = {
     "trace_dir": ("VCX_TRACE_DIR", str),
     "metrics_dir": ("VCX_METRICS_DIR", str),
 }
-_CHOICES = {"gemm": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl")}
+_CHOICES = {"gemm": ("lib", "vcx"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl")}
 
 _lock = threading.Lock()
 

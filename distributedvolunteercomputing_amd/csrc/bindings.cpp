@@ -126,6 +126,27 @@ void gemm_nt(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
               (int)b.stride(0), (int)c.stride(0), (int)epi, cur_stream());
 }
 
+// Weight gradient out[M, N] (+)= a[K, M]^T . b[K, N] (token-major operands) on the hand-written
+// transposed-read MFMA kernel, split-K over the token axis with fp32 partials
+bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t splits) {
+  return vcx_gemm_tn_supported((int)M, (int)N, (int)K, (int)splits);
+}
+
+void gemm_tn(at::Tensor a, at::Tensor b, at::Tensor out, int64_t splits, bool accumulate) {
+  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_tn: 2-D cuda tensors");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
+              "gemm_tn: bf16 operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.is_contiguous(), "gemm_tn: row-major operands, contiguous out");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "gemm_tn: shape mismatch");
+  TORCH_CHECK(vcx_gemm_tn_supported((int)M, (int)N, (int)K, (int)splits),
+              "gemm_tn: needs M % 256 == 0, N % 256 == 0, K % 64 == 0, K / 128 >= splits");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_tn: 16-B aligned rows");
+  at::Tensor ws = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
+  vcx_gemm_tn(a.data_ptr(), b.data_ptr(), ws.data_ptr<float>(), out.data_ptr(), (int)M, (int)N, (int)K,
+              (int)a.stride(0), (int)b.stride(0), (int)splits, accumulate ? 1 : 0, cur_stream());
+}
+
 at::Tensor transpose_bf16(at::Tensor src, c10::optional<at::Tensor> dst) {
   TORCH_CHECK(src.is_cuda() && src.dim() == 2 && src.is_contiguous() && src.scalar_type() == at::kBFloat16,
               "transpose_bf16: contiguous 2-D bf16");
@@ -578,6 +599,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("axpy_bf16", &axpy_bf16);
   m.def("reduce_bcast_bf16", &reduce_bcast_bf16);
   m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_tn_supported", &gemm_tn_supported);
+  m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("splits"), py::arg("accumulate"));
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0);
   m.def("transpose_bf16", &transpose_bf16, py::arg("src"), py::arg("dst") = py::none());

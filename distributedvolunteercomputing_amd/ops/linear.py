@@ -134,10 +134,29 @@ def _splits(M: int, N: int, K: int) -> int:
     return s
 
 
+def tn_splits(M: int, N: int, K: int) -> int:
+    """Token-axis splits of the hand-written weight-gradient GEMM: about one round of
+    workgroups over the 256 CUs ((N/256)(K/256) output tiles x S), at least 192 tokens each."""
+    tiles = (N // 256) * (K // 256)
+    return max(1, min(256 // max(tiles, 1), M // 192))
+
+
+def gemm_tn_ok(M: int, N: int, K: int, t) -> bool:
+    return (config.get().gemm_wgrad == "vcx" and use_native(t) and t.dtype == torch.bfloat16
+            and bool(native().gemm_tn_supported(N, K, M, tn_splits(M, N, K))))
+
+
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False):
     """dW = dy2^T @ x2 ([M, N], [M, K] -> [N, K]); written into / added onto `out` if given."""
     M, N = dy2.shape
     K = x2.shape[1]
+    if gemm_tn_ok(M, N, K, dy2) and dy2.stride(1) == 1 and x2.stride(1) == 1:
+        # hand-written transposed-read MFMA GEMM (csrc/kernels/gemm.hip gemm_tn), fp32 split partials
+        if out is None:
+            out = torch.empty(N, K, device=dy2.device, dtype=dy2.dtype)
+            accumulate = False
+        native().gemm_tn(dy2, x2, out, tn_splits(M, N, K), accumulate)
+        return out
     S = _splits(M, N, K)
     if S == 1 or not use_native(dy2) or (N * K) % 8:
         if out is None:
