@@ -7,18 +7,20 @@ fused AdamW — runs in full):
   3: ResNet-50, synthetic ImageNet, local-SGD H=4 + top-k (1%) error-feedback compression
   4: GPT-2-medium local-SGD H=4
   5: Llama-3-8B sharded-optimizer trainer + PowerSGD rank 4 (HBM sizing check on 288 GB)
-Prints one JSON line per config.
+Prints one JSON line per config. Under a torchrun-style env (WORLD_SIZE > 1) config 5 runs one
+sharded peer per rank (ZeRO-1 over the group, PowerSGD-averaged gradients, parameter all-gather).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 import time
 
 from distributedvolunteercomputing_amd.utils.tuning import enable_tuned_gemms
 
-enable_tuned_gemms(0)
+enable_tuned_gemms(int(os.environ.get("LOCAL_RANK", "0")))
 
 import torch  # noqa: E402
 
@@ -89,12 +91,25 @@ def cfg5(a, dev):
         for p in m.parameters():
             p.normal_(0.0, 0.02) if p.dim() >= 2 else p.fill_(1.0)
     torch.cuda.reset_peak_memory_stats()
-    tr = ShardedDPTrainer(m, ShardedConfig(lr=1e-4), device=dev)
+    group = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:  # one sharded peer per rank (torchrun-style env)
+        import torch.distributed as dist
+
+        from distributedvolunteercomputing_amd.parallel.peer_group import PeerGroup
+
+        if not dist.is_initialized():
+            dist.init_process_group("nccl", device_id=dev)
+        group = PeerGroup.from_default(dev)
+    reps = min(a.llama_replicas, group.size - 1) if group is not None else 0
+    tr = ShardedDPTrainer(m, ShardedConfig(lr=1e-4, replicas=max(reps, 1), replicate=reps > 0), group=group,
+                          device=dev)
     tr.compressor = PowerSGDCompressor(tr.flat, rank=4, device=dev)
     B, T = a.llama_batch, a.llama_seq
     x = torch.randint(0, cfg.vocab_size, (B, T + 1), device=dev)
     dt, loss = _time(lambda: tr.step(x[:, :-1], x[:, 1:]), 2, max(2, a.steps // 2))
-    return {"config": 5, "model": name, "params": m.num_params(), "tokens_per_s": round(B * T / dt, 1),
+    peers = group.size if group is not None else 1
+    return {"config": 5, "model": name, "params": m.num_params(), "peers": peers, "replicas": reps,
+            "tokens_per_s": round(B * T / dt, 1),
             "ms_per_step": round(dt * 1e3, 1), "batch": B, "seq": T, "loss": round(float(loss), 3),
             "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1),
             "powersgd_compression_ratio": round(tr.compressor.compression_ratio, 1),
@@ -110,8 +125,11 @@ def main():
     ap.add_argument("--llama", default="llama3-8b")
     ap.add_argument("--llama-batch", type=int, default=2)
     ap.add_argument("--llama-seq", type=int, default=2048)
+    ap.add_argument("--llama-replicas", type=int, default=2, help="config 5 with several peers: shard replicas")
     a = ap.parse_args()
-    dev = torch.device("cuda", 0)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     fns = {"3": cfg3, "4": cfg4, "5": cfg5}
     rc = 0
     for c in a.configs.split(","):
@@ -119,8 +137,11 @@ def main():
             rec = fns[c](a, dev)
         except Exception as e:  # report and continue with the next config
             rec = {"config": int(c), "error": repr(e)[:500]}
+            print(f"[bench_configs rank {os.environ.get('RANK', '0')}] config {c} failed: {e!r}", file=sys.stderr,
+                  flush=True)
             rc = 1
-        print(json.dumps(rec), flush=True)
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps(rec), flush=True)
         torch.cuda.empty_cache()
     return rc
 

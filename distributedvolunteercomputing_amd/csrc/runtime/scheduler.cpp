@@ -7,9 +7,8 @@ namespace vcxrt {
 void ChunkScheduler::add_worker(const std::string& w, double now) {
   std::lock_guard<std::mutex> g(mu_);
   auto it = ws_.find(w);
-  if (it != ws_.end()) {  // idempotent re-join (a lost `ok||port` reply must not double-insert)
-    it->second.available = true;
-    it->second.last_seen = now;
+  if (it != ws_.end()) {  // idempotent re-join (a lost `ok||port` reply must not double-insert);
+    it->second.last_seen = now;  // it changes nothing else: a requester stays out of the worker pool
     return;
   }
   WorkerState s;
