@@ -90,7 +90,26 @@ def bench_engine(args, dev):
             "net_tflops": round(gflop / net_ms, 2), "out_shape": list(out.shape)}
 
 
-def bench_job(args, dev, plane="relay"):
+def bench_y4m_job(args, dev):
+    """The whole job on a Y4M file (a real-video container: 4:4:4 planes decoded to BGR by the
+    requester) with a Y4M sink (annotated frames encoded back to YUV), relay plane."""
+    from distributedvolunteercomputing_amd.io.video import Y4MWriter, synthetic_frame
+
+    path = os.path.join(tempfile.gettempdir(), f"vcx_bench_{os.getpid()}.y4m")
+    w = Y4MWriter(path, args.width, args.height)
+    for i in range(args.y4m_frames):
+        w.write(synthetic_frame(i, args.width, args.height))
+    w.release()
+    try:
+        a = argparse.Namespace(**vars(args))
+        a.frames = args.y4m_frames
+        rec = bench_job(a, dev, "relay", source=path, out_ext=".y4m")
+    finally:
+        os.unlink(path)
+    return {k.replace("job_", "job_y4m_"): v for k, v in rec.items() if k != "workers"}
+
+
+def bench_job(args, dev, plane="relay", source=None, out_ext=".npy"):
     """The whole volunteer job on one GPU: a requester and `workers` volunteers in this process.
     ``relay``: chunk bytes through the coordinator (reference topology); ``p2p``: metadata through
     the coordinator, chunk bytes over pair groups (gloo here: the volunteers share one GPU)."""
@@ -102,13 +121,13 @@ def bench_job(args, dev, plane="relay"):
     eng = DetectorEngine(device=dev)  # one GPU: volunteers share one engine (serialised by a lock)
     tmp = tempfile.mkdtemp(prefix="vcx_video_")
     req = client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0, engine=eng, out_dir=tmp,
-                 out_ext=".npy")
+                 out_ext=out_ext)
     workers = [client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0, engine=eng,
-                      out_dir=tmp, out_ext=".npy") for _ in range(args.workers)]
+                      out_dir=tmp, out_ext=out_ext) for _ in range(args.workers)]
     try:
-        req.become_requester(f"synthetic:{args.frames}:{args.width}x{args.height}")
+        req.become_requester(source or f"synthetic:{args.frames}:{args.width}x{args.height}")
         t = req.wait_job(timeout=600)
-        n = int(np.load(req.path_out, mmap_mode="r").shape[0]) if t else 0
+        n = req.sink.written if (t and req.sink is not None) else 0
     finally:
         for c in [req] + workers:
             c.exit_threads()
@@ -129,6 +148,7 @@ def main():
     ap.add_argument("--workers", type=int, default=2)
     ap.add_argument("--no-job", action="store_true")
     ap.add_argument("--data-plane", default="both", choices=["relay", "p2p", "both"])
+    ap.add_argument("--y4m-frames", type=int, default=0, help="also run the job on a Y4M file of this many frames")
     a = ap.parse_args()
     dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     rec = {"metric": "MobileNet-SSD video job (reference parity)", "unit": "frames/s", "dtype": "bf16",
@@ -137,6 +157,8 @@ def main():
     if not a.no_job:
         for plane in (("relay", "p2p") if a.data_plane == "both" else (a.data_plane,)):
             rec.update(bench_job(a, dev, plane))
+        if a.y4m_frames:
+            rec.update(bench_y4m_job(a, dev))
     rec["value"] = max([rec.get(k) or 0 for k in ("job_frames_per_s", "job_p2p_frames_per_s")]) or \
         rec["engine_frames_per_s"]
     print(json.dumps(rec), flush=True)

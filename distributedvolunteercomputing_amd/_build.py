@@ -134,7 +134,7 @@ def build_native(nproc: int = 8, force: bool = False) -> Path:
     BUILD.mkdir(parents=True, exist_ok=True)
     rt = CSRC / "runtime"
     headers = list(rt.glob("*.h"))
-    flags = ["-O2", "-fPIC", "-std=c++17", "-pthread", f"-I{rt}", *_py_includes()]
+    flags = ["-O3", "-fPIC", "-std=c++17", "-pthread", f"-I{rt}", *_py_includes()]
     jobs, objs = [], []
     for src in sorted(rt.glob("*.cpp")):
         obj = BUILD / ("rt_" + src.stem + ".o")

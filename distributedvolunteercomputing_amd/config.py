@@ -39,6 +39,7 @@ class RuntimeConfig:
     tunableop: str = "on"  # VCX_TUNABLEOP: "on" loads the shipped hipBLASLt selections, "off" skips them
     tunableop_file: str = ""  # VCX_TUNABLEOP_FILE: alternative TunableOp results file
     offload_arch: str = "gfx950"  # VCX_OFFLOAD_ARCH: target of the in-tree HIP build
+    colour_native: bool = True  # VCX_COLOUR_NATIVE: video BGR<->YUV in the C++ runtime (False: numpy)
     # ---- distributed / control plane
     gloo_host: str = "127.0.0.1"  # VCX_GLOO_HOST: interface gloo peer groups bind to
     p2p_backend: str = ""  # VCX_P2P_BACKEND: pair-group backend of the p2p chunk plane ("" = auto)
@@ -62,6 +63,7 @@ _ENV = {
     "tunableop": ("VCX_TUNABLEOP", str),
     "tunableop_file": ("VCX_TUNABLEOP_FILE", str),
     "offload_arch": ("VCX_OFFLOAD_ARCH", str),
+    "colour_native": ("VCX_COLOUR_NATIVE", _bool),
     "gloo_host": ("VCX_GLOO_HOST", str),
     "p2p_backend": ("VCX_P2P_BACKEND", str),
     "elastic_debug": ("VCX_ELASTIC_DEBUG", _bool),

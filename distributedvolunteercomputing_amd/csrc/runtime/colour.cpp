@@ -1,0 +1,72 @@
+#include "colour.h"
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+namespace vcxrt {
+
+// rows [0, h) in up to 8 contiguous bands on their own threads (a 720p frame is ~1 M pixels;
+// below 64k pixels it stays on the calling thread)
+template <class F>
+static void parallel_rows(int64_t h, int64_t w, F&& fn) {
+  const int64_t hw = (int64_t)std::max(1u, std::thread::hardware_concurrency());
+  const int64_t nt = std::min<int64_t>({8, hw, std::max<int64_t>(1, h * w / 65536), h});
+  if (nt <= 1) {
+    fn(0, h);
+    return;
+  }
+  std::vector<std::thread> th;
+  const int64_t band = (h + nt - 1) / nt;
+  for (int64_t t = 1; t < nt; ++t) {
+    const int64_t r0 = t * band, r1 = std::min(h, r0 + band);
+    if (r0 < r1) th.emplace_back([&fn, r0, r1] { fn(r0, r1); });
+  }
+  fn(0, std::min(h, band));
+  for (auto& x : th) x.join();
+}
+
+static inline uint8_t sat(float x) {
+  x += 0.5f;
+  x = x < 0.f ? 0.f : (x > 255.f ? 255.f : x);
+  return (uint8_t)x;  // truncation, as numpy's astype(uint8) after clip
+}
+
+void bgr_to_yuv444(const uint8_t* bgr, uint8_t* yuv, int64_t w, int64_t h) {
+  const int64_t n = w * h;
+  uint8_t* Y = yuv;
+  uint8_t* U = yuv + n;
+  uint8_t* V = yuv + 2 * n;
+  parallel_rows(h, w, [&](int64_t r0, int64_t r1) {
+    for (int64_t i = r0 * w; i < r1 * w; ++i) {
+      const float b = bgr[3 * i], g = bgr[3 * i + 1], r = bgr[3 * i + 2];
+      const float y = 0.299f * r + 0.587f * g + 0.114f * b;
+      Y[i] = sat(y);
+      U[i] = sat((b - y) * 0.564f + 128.0f);
+      V[i] = sat((r - y) * 0.713f + 128.0f);
+    }
+  });
+}
+
+void yuv_to_bgr(const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* bgr, int64_t w, int64_t h,
+                int64_t cw) {
+  const bool sub = cw != w;  // 4:2:0
+  parallel_rows(h, w, [&](int64_t r0, int64_t r1) {
+  for (int64_t r = r0; r < r1; ++r) {
+    const uint8_t* yr = y + r * w;
+    const int64_t cr = sub ? r / 2 : r;
+    const uint8_t* ur = u + cr * cw;
+    const uint8_t* vr = v + cr * cw;
+    uint8_t* o = bgr + r * w * 3;
+    for (int64_t c = 0; c < w; ++c) {
+      const int64_t cc = sub ? c / 2 : c;
+      const float Y = yr[c], Uc = (float)ur[cc] - 128.0f, Vc = (float)vr[cc] - 128.0f;
+      o[3 * c] = sat(Y + 1.773f * Uc);
+      o[3 * c + 1] = sat(Y - 0.344f * Uc - 0.714f * Vc);
+      o[3 * c + 2] = sat(Y + 1.403f * Vc);
+    }
+  }
+  });
+}
+
+}  // namespace vcxrt

@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "colour.h"
 #include "scheduler.h"
 #include "transport.h"
 
@@ -110,6 +111,30 @@ PYBIND11_MODULE(_native, m) {
       .def("inflight", &ChunkScheduler::inflight)
       .def("inflight_of", &ChunkScheduler::inflight_of)
       .def_property_readonly("dispatched", &ChunkScheduler::dispatched);
+
+  // colour conversion for the video I/O path (GIL released); buffers are C-contiguous uint8
+  m.def(
+      "bgr_to_yuv444",
+      [](py::buffer src, py::buffer dst, int64_t w, int64_t h) {
+        py::buffer_info a = src.request(), b = dst.request(true);
+        if (a.size * a.itemsize < 3 * w * h || b.size * b.itemsize < 3 * w * h)
+          throw std::invalid_argument("bgr_to_yuv444: buffers smaller than 3 * w * h bytes");
+        py::gil_scoped_release rel;
+        bgr_to_yuv444((const uint8_t*)a.ptr, (uint8_t*)b.ptr, w, h);
+      },
+      py::arg("src"), py::arg("dst"), py::arg("w"), py::arg("h"));
+  m.def(
+      "yuv_to_bgr",
+      [](py::buffer y, py::buffer u, py::buffer v, py::buffer dst, int64_t w, int64_t h, int64_t cw) {
+        py::buffer_info Y = y.request(), U = u.request(), V = v.request(), D = dst.request(true);
+        const int64_t ch = cw == w ? h : (h + 1) / 2;
+        if ((cw != w && cw != (w + 1) / 2) || Y.size < w * h || U.size < cw * ch || V.size < cw * ch ||
+            D.size < 3 * w * h)
+          throw std::invalid_argument("yuv_to_bgr: plane sizes do not match w, h, cw");
+        py::gil_scoped_release rel;
+        yuv_to_bgr((const uint8_t*)Y.ptr, (const uint8_t*)U.ptr, (const uint8_t*)V.ptr, (uint8_t*)D.ptr, w, h, cw);
+      },
+      py::arg("y"), py::arg("u"), py::arg("v"), py::arg("dst"), py::arg("w"), py::arg("h"), py::arg("cw"));
 
   py::class_<ReorderIndex>(m, "ReorderIndex")
       .def(py::init<int64_t>(), py::arg("first") = 1)

@@ -26,7 +26,32 @@ import numpy as np
 
 
 # ----------------------------------------------------------------------------- colour
+def _rt():
+    """The C++ runtime's colour loops (csrc/runtime/colour.cpp), or None when it is not built
+    (or config.colour_native is off)."""
+    from .. import config
+
+    if not config.get().colour_native:
+        return None
+    try:
+        from .._native_loader import native
+
+        return native()
+    except RuntimeError:
+        return None
+
+
 def bgr_to_yuv444(frame: np.ndarray) -> np.ndarray:
+    rt = _rt()
+    if rt is not None and frame.dtype == np.uint8 and frame.ndim == 3 and frame.shape[2] == 3:
+        h, w = frame.shape[:2]
+        out = np.empty((3, h, w), np.uint8)
+        rt.bgr_to_yuv444(np.ascontiguousarray(frame), out, w, h)
+        return out
+    return _bgr_to_yuv444_np(frame)
+
+
+def _bgr_to_yuv444_np(frame: np.ndarray) -> np.ndarray:
     f = frame.astype(np.float32)
     b, g, r = f[..., 0], f[..., 1], f[..., 2]
     y = 0.299 * r + 0.587 * g + 0.114 * b
@@ -36,6 +61,17 @@ def bgr_to_yuv444(frame: np.ndarray) -> np.ndarray:
 
 
 def yuv444_to_bgr(yuv: np.ndarray) -> np.ndarray:
+    rt = _rt()
+    if rt is not None and yuv.dtype == np.uint8 and yuv.ndim == 3 and yuv.shape[0] == 3:
+        h, w = yuv.shape[1:]
+        yuv = np.ascontiguousarray(yuv)
+        out = np.empty((h, w, 3), np.uint8)
+        rt.yuv_to_bgr(yuv[0], yuv[1], yuv[2], out, w, h, w)
+        return out
+    return _yuv444_to_bgr_np(yuv)
+
+
+def _yuv444_to_bgr_np(yuv: np.ndarray) -> np.ndarray:
     y, u, v = (yuv[i].astype(np.float32) for i in range(3))
     r = y + 1.403 * (v - 128.0)
     g = y - 0.344 * (u - 128.0) - 0.714 * (v - 128.0)
@@ -173,6 +209,11 @@ class Y4MSource(FrameSource):
             cw, ch = (w + 1) // 2, (h + 1) // 2
             u = np.frombuffer(self.f.read(cw * ch), np.uint8).reshape(ch, cw)
             v = np.frombuffer(self.f.read(cw * ch), np.uint8).reshape(ch, cw)
+            rt = _rt()
+            if rt is not None:  # upsampling folded into the C++ conversion loop
+                out = np.empty((h, w, 3), np.uint8)
+                rt.yuv_to_bgr(y, u, v, out, w, h, cw)
+                return True, out
             u = u.repeat(2, 0).repeat(2, 1)[:h, :w]
             v = v.repeat(2, 0).repeat(2, 1)[:h, :w]
             yuv = np.stack([y, u, v])

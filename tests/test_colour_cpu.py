@@ -1,0 +1,40 @@
+"""C++ colour conversion of the video I/O path (csrc/runtime/colour.cpp) against the numpy
+formulas it replaces: bit-identical for BGR -> YUV 4:4:4, YUV 4:4:4 -> BGR and YUV 4:2:0 -> BGR
+(2x2 chroma replication, odd sizes included), and a 4:2:0 Y4M file read through Y4MSource."""
+import numpy as np
+import pytest
+
+from distributedvolunteercomputing_amd.io import video as V
+
+
+@pytest.mark.parametrize("h,w", [(720, 1280), (225, 400), (7, 9), (721, 1281), (1, 1)])
+def test_bgr_yuv444_roundtrip_bit_exact(h, w):
+    f = np.random.default_rng(h * w).integers(0, 256, (h, w, 3), dtype=np.uint8)
+    y = V.bgr_to_yuv444(f)
+    assert np.array_equal(y, V._bgr_to_yuv444_np(f))
+    assert np.array_equal(V.yuv444_to_bgr(y), V._yuv444_to_bgr_np(y))
+
+
+def _write_y4m_420(path, planes, w, h):
+    with open(path, "wb") as fh:
+        fh.write(f"YUV4MPEG2 W{w} H{h} F30:1 Ip A1:1 C420jpeg\n".encode())
+        for y, u, v in planes:
+            fh.write(b"FRAME\n" + y.tobytes() + u.tobytes() + v.tobytes())
+
+
+@pytest.mark.parametrize("h,w", [(72, 128), (9, 13)])
+def test_y4m_420_source_matches_numpy(tmp_path, h, w):
+    rng = np.random.default_rng(w)
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    planes = [(rng.integers(0, 256, (h, w), dtype=np.uint8), rng.integers(0, 256, (ch, cw), dtype=np.uint8),
+               rng.integers(0, 256, (ch, cw), dtype=np.uint8)) for _ in range(3)]
+    p = tmp_path / "a.y4m"
+    _write_y4m_420(p, planes, w, h)
+    src = V.Y4MSource(str(p))
+    for y, u, v in planes:
+        ok, f = src.read()
+        assert ok
+        ref = V._yuv444_to_bgr_np(np.stack([y, u.repeat(2, 0).repeat(2, 1)[:h, :w], v.repeat(2, 0).repeat(2, 1)[:h, :w]]))
+        assert np.array_equal(f, ref)
+    assert src.read()[0] is False
+    src.release()
