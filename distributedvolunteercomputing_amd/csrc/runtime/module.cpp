@@ -18,6 +18,15 @@ struct PyFrame {
   Frame f;
 };
 
+// C-contiguous check for raw uint8 buffers handed to the colour loops (which index them linearly)
+void require_c_contiguous(const py::buffer_info& b, const char* what) {
+  py::ssize_t expect = b.itemsize;
+  for (int d = (int)b.ndim - 1; d >= 0; --d) {
+    if (b.shape[d] > 1 && b.strides[d] != expect) throw std::invalid_argument(std::string(what) + ": not C-contiguous");
+    expect *= b.shape[d];
+  }
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -117,6 +126,8 @@ PYBIND11_MODULE(_native, m) {
       "bgr_to_yuv444",
       [](py::buffer src, py::buffer dst, int64_t w, int64_t h) {
         py::buffer_info a = src.request(), b = dst.request(true);
+        require_c_contiguous(a, "bgr_to_yuv444 src");
+        require_c_contiguous(b, "bgr_to_yuv444 dst");
         if (a.size * a.itemsize < 3 * w * h || b.size * b.itemsize < 3 * w * h)
           throw std::invalid_argument("bgr_to_yuv444: buffers smaller than 3 * w * h bytes");
         py::gil_scoped_release rel;
@@ -127,6 +138,7 @@ PYBIND11_MODULE(_native, m) {
       "yuv_to_bgr",
       [](py::buffer y, py::buffer u, py::buffer v, py::buffer dst, int64_t w, int64_t h, int64_t cw) {
         py::buffer_info Y = y.request(), U = u.request(), V = v.request(), D = dst.request(true);
+        for (auto* b : {&Y, &U, &V, &D}) require_c_contiguous(*b, "yuv_to_bgr");
         const int64_t ch = cw == w ? h : (h + 1) / 2;
         if ((cw != w && cw != (w + 1) / 2) || Y.size < w * h || U.size < cw * ch || V.size < cw * ch ||
             D.size < 3 * w * h)

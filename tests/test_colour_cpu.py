@@ -38,3 +38,12 @@ def test_y4m_420_source_matches_numpy(tmp_path, h, w):
         assert np.array_equal(f, ref)
     assert src.read()[0] is False
     src.release()
+
+
+def test_native_colour_rejects_strided_buffers():
+    from distributedvolunteercomputing_amd._native_loader import native
+
+    f = np.zeros((8, 16, 3), np.uint8)
+    out = np.zeros((3, 8, 32), np.uint8)[:, :, ::2]  # a strided view: must not be written linearly
+    with pytest.raises(ValueError):
+        native().bgr_to_yuv444(f, out, 16, 8)
