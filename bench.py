@@ -146,6 +146,8 @@ def main():
             "sync_ms": round(trainer.last_sync_ms, 3),
             "tuned_gemms": TUNED_GEMMS,
             "hipgraph": graphed,
+            # ranks sharing a card (scripts/rccl_rehearsal_launch.py): a functional run, not a per-GPU number
+            "ranks_share_gpu": bool(cuda and world > torch.cuda.device_count()),
             "gemm_lt_shapes": sum(1 for v in gemm_choices().values() if v == "lt"),
             "gemm_shapes": len(gemm_choices()),
         }

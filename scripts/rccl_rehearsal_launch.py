@@ -10,8 +10,9 @@ per-generation communicators, ncclCommAbort on a dead peer.
 
 Usage: python scripts/rccl_rehearsal_launch.py --nproc 2 [--timeout 300] -- python bench.py --gpus 2 ...
 This launcher never touches the GPU itself (it only spawns children), and every child gets the
-torchrun-style env (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT). Exit status: the first
-non-zero child status, 124 on timeout (all children are killed).
+torchrun-style env (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT). Exit status: that of the
+rank whose failure ended the job (128 + signal if it was killed), 124 on timeout (all children
+are killed).
 """
 from __future__ import annotations
 
@@ -65,6 +66,7 @@ def main() -> int:
             break
         time.sleep(0.1)
     timed_out = any(c is None for c in codes) and time.monotonic() > deadline
+    first_bad = next((c for c in codes if c not in (None, 0)), None)  # the failure that ended the job
     for i, p in enumerate(procs):  # a failed or hung rank ends the whole job
         if p.poll() is None:
             try:
@@ -76,8 +78,9 @@ def main() -> int:
     print(f"[rehearsal] rank exit codes: {codes}", file=sys.stderr, flush=True)
     if timed_out:
         return 124
-    bad = [c for c in codes if c != 0]
-    return bad[0] if bad else 0
+    if first_bad is not None:
+        return first_bad if first_bad > 0 else 128 - first_bad  # killed by a signal: 128 + signal number
+    return 0
 
 
 if __name__ == "__main__":

@@ -66,3 +66,20 @@ def test_bench_torchrun_more_ranks(n, algo):
     rec = _torchrun(n, ["--algo", algo])
     assert f"allreduce={algo}" in rec["config"]["parallelism"]
     assert rec["sync_ms"] > 0
+
+
+def test_rehearsal_launcher_propagates_a_failed_rank(tmp_path):
+    """scripts/rccl_rehearsal_launch.py: every rank gets the torchrun env and its own NCCL_HOSTID;
+    one rank failing ends the job with that rank's exit status (the others are killed)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prog = ("import os, sys, time\n"
+            "r = int(os.environ['RANK'])\n"
+            "assert os.environ['WORLD_SIZE'] == '3' and os.environ['NCCL_HOSTID'] == f'vcx-rehearsal-{r}'\n"
+            "sys.exit(7) if r == 1 else time.sleep(60)\n")
+    cmd = [sys.executable, os.path.join(root, "scripts", "rccl_rehearsal_launch.py"), "--nproc", "3", "--timeout", "50",
+           "--", sys.executable, "-c", prog]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=90)
+    assert r.returncode == 7, r.stderr
