@@ -91,11 +91,19 @@ __global__ void __launch_bounds__(NT, 1)
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 2, wn = wid & 3;
 
-  // ---- XCD-aware bijective tile order
+  // ---- XCD-aware bijective tile order: consecutive logical tiles share an XCD (and its L2), and
+  // the logical order walks GROUP_M row panels x all column panels in column-major blocks, so the
+  // ~32 tiles an XCD runs at once are a 4 x 8 block (4 A + 8 B panels in flight) instead of one A
+  // panel x 32 B panels (the whole B operand re-streamed by every XCD every round at large N)
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int m0 = (wg / tilesN) * BM, n0 = (wg % tilesN) * BN;
+  constexpr int GROUP_M = 4;
+  const int tilesM = nwg / tilesN;
+  const int per_group = GROUP_M * tilesN;
+  const int gfirst = (wg / per_group) * GROUP_M;
+  const int gsize = min(tilesM - gfirst, GROUP_M);
+  const int m0 = (gfirst + (wg % per_group) % gsize) * BM, n0 = ((wg % per_group) / gsize) * BN;
 
   // ---- LDS-DMA staging: a slice is 32 pieces of 16 rows x 64 B (A: 16, B: 16); wave w moves
   // A pieces w, w+8 and B pieces w, w+8. Lane l of a piece writes LDS bytes [16 l, 16 l + 16):
