@@ -102,6 +102,12 @@ def main():
             trainer.graph = None
     for i in range(w0, a.warmup):
         trainer.step(*batch(i))
+    if group is not None:
+        # connect every peer pair of the averaging collective before the timed window (RCCL sets up
+        # its point-to-point channels on first use), even when --warmup is shorter than H
+        from distributedvolunteercomputing_amd.parallel.collectives import allreduce_sum_
+
+        allreduce_sum_(torch.zeros_like(trainer.delta), group, a.algo)  # same size as the real round
     sync_all()
     t0 = time.perf_counter()
     last = None
