@@ -17,9 +17,11 @@ any peer may die) and starts P peer processes, one per visible GPU (round-robin 
 the GPUs; RCCL does not run two ranks on one device, so peers sharing a GPU use gloo). Every
 peer runs the elastic local-SGD trainer (parallel/elastic.py + parallel/local_sgd.py). At step
 ``--drop-at`` (default: mid-window, between two averaging rounds) peer ``--drop-peer`` crashes
-without a goodbye (heartbeat stops, process exits). The survivors notice at their next
-averaging round (lease expiry), agree on the next generation, build a fresh process group and
-go on. Every peer times each step (device-synchronised); the launcher prints ONE JSON line
+without a goodbye (the process exits). The survivors notice at once through their liveness links
+to it (a closed TCP connection; a SIGSTOPped victim closes nothing and is found by the lease),
+agree on the next generation, build a fresh process group and go on. The JSON line breaks the
+stall into ``detect_ms`` (fault -> first sign), ``comm_build_ms`` (the new communicator) and
+``redo_ms`` (new communicator -> end of the redone round). Every peer times each step (device-synchronised); the launcher prints ONE JSON line
 with the step time before the drop, across the window that contains it, after it, and the
 stall of the round that absorbed the detection and regroup.
 
@@ -104,6 +106,7 @@ def peer_main(a):
         def hook(grp, op):  # fires after the op was issued: the other peers are inside it
             if armed["on"] and op in ("allreduce", "alltoall", "all_gather"):
                 print(f"[peer {a.peer}] fault injection: {signal.Signals(sig).name} inside {op}", flush=True)
+                store.set(f"vcx/drop/t_fault/{a.peer}", repr(time.time()))
                 os.kill(os.getpid(), sig)
         mem.fault_hook = hook
     if a.join:
@@ -161,19 +164,22 @@ def peer_main(a):
         if a.peer in victims and i == a.drop_at:
             if a.fault == "step":
                 print(f"[peer {a.peer}] fault injection: crashing at step {i}", flush=True)
-                mem.stop_heartbeat()
-                os._exit(0)  # no leave(): the survivors must detect the silence
+                store.set(f"vcx/drop/t_fault/{a.peer}", repr(time.time()))
+                os._exit(0)  # no leave(), no goodbye: the survivors must notice on their own
             armed["on"] = True  # die inside the next averaging collective
         t0 = time.perf_counter()
         st = tr.step(*batch(i))
         sync()
         timeline.append({"step": i, "ms": (time.perf_counter() - t0) * 1e3, "synced": bool(st.synced),
-                         "members": st.members, "gen": mem.gen, "sync_ms": st.sync_ms if st.synced else 0.0})
+                         "members": st.members, "gen": mem.gen, "sync_ms": st.sync_ms if st.synced else 0.0,
+                         "t_end": time.time()})
         i += 1
     store.set("vcx/drop/done", "1")
     with open(os.path.join(a.out, f"peer{a.peer}.json"), "w") as f:
+        t_fault = {v: float(store.get(f"vcx/drop/t_fault/{v}")) for v in victims
+                   if store.check([f"vcx/drop/t_fault/{v}"])}
         json.dump({"peer": a.peer, "backend": backend, "timeline": timeline, "events": mem.events,
-                   "failed_rounds": tr.failed_rounds}, f)
+                   "failed_rounds": tr.failed_rounds, "eof": mem.eof_events, "t_fault": t_fault}, f)
     mem.leave()  # graceful: a joiner still stepping regroups without this peer at its next round
     return 0
 
@@ -278,11 +284,32 @@ def launcher(a):
     tl = {}
     backend = None
     failed_rounds = 0
+    detect, build, redo = [], [], []
     for r in survivors:
         with open(os.path.join(out, f"peer{r}.json")) as f:
             d = json.load(f)
         backend = d["backend"]
         failed_rounds = max(failed_rounds, d.get("failed_rounds", 0))
+        tf = min(d.get("t_fault", {}).values(), default=None)
+        if tf is not None:
+            # detection: the first sign of the failure on this survivor (a liveness EOF from a
+            # victim, an aborted collective, or — without either — the regroup itself)
+            sig = [t for m, t in d.get("eof", []) if m in victims and t >= tf]
+            sig += [e["t"] for e in d["events"] if e["event"] == "abort" and e["t"] >= tf]
+            rg = [e for e in d["events"] if e["event"] == "regroup" and e.get("t", 0) >= tf]
+            if rg and not sig:
+                sig = [rg[0]["t"]]
+            if sig:
+                detect.append((min(sig) - tf) * 1e3)
+            if rg:
+                cn = [e for e in d["events"] if e["event"] == "connect" and e["gen"] == rg[0]["gen"]]
+                if cn:
+                    build.append(cn[0]["ms"])
+                    # redo: from the new generation's communicator to the end of the step that
+                    # carried the redone (or delayed) averaging round
+                    ends = [e["t_end"] for e in d["timeline"] if e["gen"] >= rg[0]["gen"] and e["synced"]]
+                    if ends:
+                        redo.append((min(ends) - cn[0]["t"]) * 1e3)
         for e in d["timeline"]:
             cur = tl.setdefault(e["step"], dict(e))
             cur["ms"] = max(cur["ms"], e["ms"])  # a step ends when its slowest survivor is done
@@ -320,6 +347,12 @@ def launcher(a):
         "steady_sync_ms": round(steady_sync, 3),
         "regroup_sync_ms": round(regroup_sync, 3),
         "drop_stall_ms": round(regroup_sync - steady_sync, 3),
+        # stall anatomy (max over survivors): fault -> first sign of it, the new generation's
+        # communicator build, and communicator -> end of the redone round
+        "detect_ms": round(max(detect), 3) if detect else None,
+        "comm_build_ms": round(max(build), 3) if build else None,
+        "redo_ms": round(max(redo), 3) if redo else None,
+        "liveness": os.environ.get("VCX_ELASTIC_LIVENESS", "1") not in ("0", "false", "no", "off"),
         "samples_per_s_before": round(a.peers * a.batch / mean(before) * 1e3, 2),
         "samples_per_s_after": round(len(survivors) * a.batch / mean(after) * 1e3, 2) if after else None,
     }

@@ -28,6 +28,8 @@ def server_main(argv=None):
     ap.add_argument("--ephemeral-ports", action="store_true", help="data ports from the OS instead of 5555..5599")
     ap.add_argument("--train-store-port", type=int, default=None,
                     help="also host the rendezvous store for training peers on this TCP port")
+    ap.add_argument("--train-token", default=None,
+                    help="admission token training peers must present (tjoin) to get the rendezvous store")
     ap.add_argument("--data-plane", default="relay", choices=["relay", "p2p"],
                     help="relay: chunk bytes through this process (reference); p2p: metadata only, chunks "
                          "travel between the volunteers over pair groups (RCCL between GPU volunteers)")
@@ -37,7 +39,7 @@ def server_main(argv=None):
 
     c = coordinator(a.ip, a.port, ephemeral_ports=a.ephemeral_ports, policy=a.policy, credits=a.credits,
                     lease_s=a.lease, verbose=a.verbose, train_store_port=a.train_store_port,
-                    data_plane=a.data_plane)
+                    data_plane=a.data_plane, train_token=a.train_token)
     print(f"\nlistening on {a.ip} port {c.control_port}", flush=True)
     while True:
         try:
@@ -61,7 +63,9 @@ def worker_main(argv=None):
     ap.add_argument("--prototxt", default=None, help="Caffe prototxt (default: built-in MobileNet-SSD)")
     ap.add_argument("--caffemodel", default="MobileNetSSD_deploy.caffemodel",
                     help="weights (random init when absent, as in this environment)")
-    ap.add_argument("--device", default=None, help="cuda:N or cpu (default: cuda if available)")
+    ap.add_argument("--device", default=None,
+                    help="cuda:N or cpu (default: LOCAL_RANK's GPU under a launcher, else the first GPU no other "
+                         "volunteer on this host holds, so hand-launched volunteers spread over a node's GPUs)")
     ap.add_argument("--confidence", type=float, default=0.2)
     ap.add_argument("--chunk", type=int, default=100)
     ap.add_argument("--out-dir", default=".")
@@ -73,7 +77,10 @@ def worker_main(argv=None):
     from ..control.peer import client
     from ..jobs.video import DetectorEngine
 
-    eng = DetectorEngine(device=a.device, prototxt=a.prototxt, caffemodel=a.caffemodel, conf_thresh=a.confidence)
+    from ..utils.devices import claim_device
+
+    dev = a.device or claim_device()
+    eng = DetectorEngine(device=dev, prototxt=a.prototxt, caffemodel=a.caffemodel, conf_thresh=a.confidence)
     w = client(a.server_ip, a.own_ip, control_port=a.port, my_port=a.data_port, engine=eng, out_dir=a.out_dir,
                out_ext=a.out_ext, verbose=a.verbose, chunk=a.chunk, p2p_backend=a.p2p_backend)
     while True:

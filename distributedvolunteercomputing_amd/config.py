@@ -44,6 +44,7 @@ class RuntimeConfig:
     gloo_host: str = "127.0.0.1"  # VCX_GLOO_HOST: interface gloo peer groups bind to
     p2p_backend: str = ""  # VCX_P2P_BACKEND: pair-group backend of the p2p chunk plane ("" = auto)
     elastic_debug: bool = False  # VCX_ELASTIC_DEBUG: trace membership decisions to stderr
+    elastic_liveness: bool = True  # VCX_ELASTIC_LIVENESS: TCP liveness links (process death seen at once)
     store_port_train: int = 29611  # VCX_STORE_PORT (train CLI): rendezvous store port
     store_port_video: int = 29612  # VCX_STORE_PORT (video CLI): job-control store port
     # ---- observability
@@ -67,6 +68,7 @@ _ENV = {
     "gloo_host": ("VCX_GLOO_HOST", str),
     "p2p_backend": ("VCX_P2P_BACKEND", str),
     "elastic_debug": ("VCX_ELASTIC_DEBUG", _bool),
+    "elastic_liveness": ("VCX_ELASTIC_LIVENESS", _bool),
     "store_port_train": ("VCX_STORE_PORT", int),
     "store_port_video": ("VCX_STORE_PORT", int),
     "trace_dir": ("VCX_TRACE_DIR", str),

@@ -30,6 +30,7 @@ from __future__ import annotations
 import itertools
 import json
 import queue
+import secrets
 import socket
 import threading
 import time
@@ -72,7 +73,7 @@ class coordinator:  # noqa: N801  (reference class name)
     def __init__(self, ip: str = "localhost", control_port: int = protocol.DEFAULT_CONTROL_PORT, *,
                  ephemeral_ports: bool = False, max_clients: int | None = None, policy: str = "round_robin",
                  credits: int = 2, lease_s: float | None = None, verbose: bool | None = None,
-                 train_store_port: int | None = None, data_plane: str = "relay"):
+                 train_store_port: int | None = None, data_plane: str = "relay", train_token: str | None = None):
         if verbose is not None:
             self.verbose = verbose
         if data_plane not in ("relay", "p2p"):
@@ -82,6 +83,16 @@ class coordinator:  # noqa: N801  (reference class name)
             train_store_port = 0  # the pair groups rendezvous on this process's store
         # Rendezvous store for training peers (heartbeats, generations, RCCL bootstrap). Hosted
         # here so that ANY training peer may die without taking the membership state with it.
+        # Access control: torch's TCPStore listens on every interface and has no authentication,
+        # so every key the peers use lives under a per-coordinator random prefix (`store_secret`)
+        # that is handed out only to joined volunteers (the `join` reply) and to admitted training
+        # peers (`tjoin`, optionally gated by `train_token`); the `store` verb is refused to anyone
+        # else. A host that can reach the port but never joined cannot name, so cannot forge, the
+        # abort / join / pair-hello records the peers act on (the reference binds every interface
+        # with no auth at all: /root/reference/server.py:96).
+        self.store_secret = secrets.token_hex(16)
+        self.train_token = train_token
+        self.train_peers: set[str] = set()
         self.train_store = None
         if train_store_port is not None:
             import datetime
@@ -156,9 +167,11 @@ class coordinator:  # noqa: N801  (reference class name)
                 self.metrics.incr("spoofed_datagrams")
                 return f"err{protocol.SEP}address {addr} does not match sender {src[0]}".encode()
             return self._join(addr, now)
-        if verb in ("request", "stop", "end", "hb", "p2p"):
+        if verb == "tjoin":  # a training peer asks for the rendezvous store
+            return self._tjoin(addr, src)
+        if verb in ("request", "stop", "end", "hb", "p2p", "store"):
             with self._lock:
-                known = addr in self.vols
+                known = addr in self.vols or (verb == "store" and addr in self.train_peers)
             if not known or (src is not None and not protocol.addr_matches(addr, src[0])):
                 self.metrics.incr("unknown_datagrams")
                 return f"err{protocol.SEP}{addr} has not joined".encode()
@@ -185,22 +198,49 @@ class coordinator:  # noqa: N801  (reference class name)
                 st["peers"]["volunteers"] = {a: {"truncated": True} for a in st["peers"]["volunteers"]}
                 js = json.dumps(st)
             return protocol.reply_ok(js)
-        if verb == "store":  # where training peers rendezvous
-            return protocol.reply_ok(str(self.train_store_port) if self.train_store is not None else "")
+        if verb == "store":  # where training peers rendezvous (joined volunteers / admitted peers only)
+            return protocol.reply_ok(self._store_ref())
         if verb == "p2p":
             with self._lock:
                 v = self.vols.get(addr)
             info = {"plane": self.data_plane, "vid": v.vid if v is not None else None,
-                    "store_port": self.train_store_port if self.data_plane == "p2p" else None}
+                    "store_port": self.train_store_port if self.data_plane == "p2p" else None,
+                    "store_prefix": self.store_secret if self.data_plane == "p2p" else None}
             return protocol.reply_ok(json.dumps(info))
         return None
+
+    def _store_ref(self) -> str:
+        """`<port>||<key prefix>` of the rendezvous store ('' when this coordinator hosts none)."""
+        if self.train_store is None:
+            return ""
+        return f"{self.train_store_port}{protocol.SEP}{self.store_secret}"
+
+    def _join_reply(self, port) -> bytes:
+        # `ok||<port>` as in the reference; with a rendezvous store a third field carries the key
+        # prefix (the reference client reads only field 1: worker.py:61)
+        if self.train_store is None:
+            return protocol.reply_ok(str(port))
+        return protocol.reply_ok(f"{port}{protocol.SEP}{self.store_secret}")
+
+    def _tjoin(self, addr, src):
+        """Admit a training peer `<id>[||<token>]`: reply `ok||<store port>||<key prefix>`."""
+        ident, _, token = addr.partition(protocol.SEP)
+        if self.train_store is None:
+            return f"err{protocol.SEP}this coordinator hosts no rendezvous store".encode()
+        if self.train_token is not None and not secrets.compare_digest(token, self.train_token):
+            self.metrics.incr("refused_tjoin")
+            return f"err{protocol.SEP}bad admission token".encode()
+        with self._lock:
+            self.train_peers.add(ident)
+        self.metrics.incr("train_peers")
+        return protocol.reply_ok(self._store_ref())
 
     def _join(self, addr, now):
         with self._lock:
             v = self.vols.get(addr)
             if v is not None:  # idempotent re-join (lost ack): same port, no duplicate
                 self.sched.add_worker(addr, now)
-                return protocol.reply_ok(str(v.port))
+                return self._join_reply(v.port)
             if not self.free_ports:
                 return f"err{protocol.SEP}no free data port".encode()
             port = self.free_ports.popleft()
@@ -224,7 +264,7 @@ class coordinator:  # noqa: N801  (reference class name)
             self.metrics.incr("joins")
             self.log(f"join {addr} -> data port {port}")
         self._kick()
-        return protocol.reply_ok(str(port))
+        return self._join_reply(port)
 
     def _remove(self, addr, reason):
         with self._lock:

@@ -84,7 +84,8 @@ class client:  # noqa: N801 (reference class name)
         self.my_ip = f"{own_ip}:{self.hub.port}"
         self.ctrl = protocol.ControlClient(server_ip, control_port, verbose=self.verbose)
         self.hb_ctrl = protocol.ControlClient(server_ip, control_port, timeout_s=0.5)  # own socket: no reply theft
-        self.connect_to_port = self.ctrl.call("join", self.my_ip)
+        # `<port>` or `<port>||<store key prefix>` (coordinators that host a rendezvous store)
+        self.connect_to_port, _, self.store_prefix = (self.ctrl.call("join", self.my_ip) or "").partition("||")
         self.sender = FrameSender(f"tcp://{server_ip}:{self.connect_to_port}", REQ_REP=self.req_rep)
         self.log(f"joined {server_ip}:{control_port}; uplink port {self.connect_to_port}, data port {self.hub.port}")
         self.plane = None
@@ -134,8 +135,11 @@ class client:  # noqa: N801 (reference class name)
         host = server_ip if server_ip not in ("", "localhost") else "127.0.0.1"
         port = int(info["store_port"])
 
-        def store():
-            return dist.TCPStore(host, port, None, False, timeout=datetime.timedelta(seconds=60))
+        prefix = info.get("store_prefix") or self.store_prefix
+
+        def store():  # every pair-rendezvous key lives under the coordinator's secret prefix
+            st = dist.TCPStore(host, port, None, False, timeout=datetime.timedelta(seconds=60))
+            return dist.PrefixStore(prefix, st) if prefix else st
         if backend is None:
             # RCCL needs one GPU per volunteer; volunteers sharing a device (or none) use gloo
             backend = config.get().p2p_backend or (

@@ -6,9 +6,13 @@ Requests are UTF-8 datagrams ``"<verb>||<ip>:<port>"`` sent to the coordinator's
 
 Verbs: ``join`` (enter the worker pool, get a data port), ``request`` (become a requester,
 leave the pool), ``stop`` (stop requesting, back to the pool), ``end`` (leave). New verbs:
-``hb`` (heartbeat; renews the lease, reply ``ok``), ``status`` (reply ``ok||<json>``), ``store``
-(training rendezvous store port), ``p2p`` (reply ``ok||{"plane", "vid", "store_port"}``: the data
-plane of this coordinator and, on the p2p plane, the volunteer's id and the pair-rendezvous store).
+``hb`` (heartbeat; renews the lease, reply ``ok``), ``status`` (reply ``ok||<json>``), ``tjoin``
+(admit a training peer ``<id>[||<token>]``; reply ``ok||<store port>||<key prefix>``), ``store``
+(the same reply, for joined volunteers and admitted training peers only), ``p2p`` (reply
+``ok||{"plane", "vid", "store_port", "store_prefix"}``: the data plane of this coordinator and, on the
+p2p plane, the volunteer's id and the pair-rendezvous store). When the coordinator hosts a
+rendezvous store, the ``join`` reply is ``ok||<port>||<key prefix>`` (the reference client reads
+only the port field).
 
 Differences from the reference, by design:
 * verbs are matched EXACTLY on the field before ``||`` (the reference matches substrings, so
@@ -23,7 +27,7 @@ import select
 import socket
 import time
 
-VERBS = ("join", "request", "stop", "end", "hb", "status", "store", "p2p")
+VERBS = ("join", "request", "stop", "end", "hb", "status", "store", "p2p", "tjoin")
 SEP = "||"
 DEFAULT_CONTROL_PORT = 9999
 
@@ -58,6 +62,12 @@ def parse_reply(data: bytes):
     if s.startswith("ok" + SEP):
         return True, s[len("ok" + SEP):]
     return False, s
+
+
+def split_store_ref(payload: str):
+    """`<port>||<prefix>` (a `join` / `tjoin` / `store` reply payload) -> (port, prefix)."""
+    port, _, prefix = (payload or "").partition(SEP)
+    return int(port), prefix
 
 
 def split_addr(addr: str):

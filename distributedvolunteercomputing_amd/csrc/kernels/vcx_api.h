@@ -20,6 +20,10 @@ void vcx_gemm_tn(const void* A, const void* B, float* Cpart, void* out, int M, i
 bool vcx_gemm_nt_supported(int M, int N, int K);
 void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,
                  int lda, int ldb, int ldc, int epi, hipStream_t s);
+// gemm_persistent.hip: persistent role-split GEMM, layout 0: C = A B^T (B [N, K]), 1: C = A B (B [K, N])
+bool vcx_gemm_p_supported(int M, int N, int K, int layout);
+void vcx_gemm_p(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,
+                int lda, int ldb, int ldc, int epi, int layout, hipStream_t s);
 void vcx_transpose_bf16(const void* src, void* dst, int R, int Cc, hipStream_t s);
 void vcx_add_f32_into_bf16(const float* in, void* out, int n, int accumulate, hipStream_t s);
 void vcx_reduce_bcast_bf16(const void* in, void* out, void* mine, int P, int64_t n, hipStream_t s);

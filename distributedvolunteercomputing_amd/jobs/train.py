@@ -105,6 +105,8 @@ def parse(argv=None):
     ap.add_argument("--store-port", type=int, default=config.get().store_port_train)
     ap.add_argument("--coordinator", default=None,
                     help="host:control_port of a coordinator that hosts the rendezvous store (no peer is special)")
+    ap.add_argument("--train-token", default=os.environ.get("VCX_TRAIN_TOKEN"),
+                    help="admission token for a coordinator started with one (tjoin)")
     ap.add_argument("--join", action="store_true", help="join a running job instead of bootstrapping")
     ap.add_argument("--drop-at", type=int, default=-1, help="fault injection: crash this peer at that step")
     ap.add_argument("--ckpt-dir", default=None)
@@ -129,14 +131,18 @@ def main(argv=None):
     backend = a.backend or ("nccl" if cuda else "gloo")
     from ..parallel.peer_group import PeerGroup
 
-    if a.coordinator:  # the coordinator hosts the rendezvous store: ask it where
-        from ..control.protocol import ControlClient
+    prefix = ""
+    if a.coordinator:  # the coordinator hosts the rendezvous store: get admitted, learn where
+        from ..control.protocol import ControlClient, split_store_ref
 
         host, _, cport = a.coordinator.rpartition(":")
         a.store_host = host
-        a.store_port = int(ControlClient(host, int(cport)).call("store", f"train-peer-{rank}"))
+        ident = f"train-peer-{rank}" + (f"||{a.train_token}" if a.train_token else "")
+        a.store_port, prefix = split_store_ref(ControlClient(host, int(cport)).call("tjoin", ident))
     store = dist.TCPStore(a.store_host, a.store_port, None, rank == 0 and not a.join and not a.coordinator,
                           timeout=datetime.timedelta(seconds=300), wait_for_workers=False)
+    if prefix:  # every rendezvous key under the coordinator's secret prefix
+        store = dist.PrefixStore(prefix, store)
     membership = group = None
     if a.elastic:
         from ..parallel.elastic import ElasticMembership

@@ -25,11 +25,19 @@ Here every peer
   outside the next generation and rejoins transparently as a newcomer;
 * a new or returning peer registers under ``join/<seq>`` and is admitted at the next round's
   outcome; newcomers (and any member that has not yet completed a committed round since it
-  joined) receive the model inside the admission round.
+  joined) receive the model inside the admission round;
+* process death is seen at once, not after a lease: every peer listens on a TCP "liveness" port
+  (published as ``live/<pid>``) and holds one connection to each other member's. Nothing is ever
+  sent on them; when a peer process dies (SIGKILL, crash, OOM) its kernel closes its sockets and
+  every survivor's blocking read returns EOF within milliseconds. Inside a guarded collective that
+  aborts the generation right away; between rounds it marks the member dead for the next
+  arrival. The lease remains the detector for what closes no socket (a hang, SIGSTOP, a
+  partition).
 """
 from __future__ import annotations
 
 import os
+import socket
 import threading
 import time
 from contextlib import contextmanager
@@ -62,10 +70,110 @@ def _parse_gen(rec: str):
     return _ints(members), _ints(newcomers), int(njoin)
 
 
+def _route_ip(target: str) -> str:
+    """This host's address on the route to `target` (what the other peers can connect to)."""
+    try:
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        try:
+            s.connect((target, 9))
+            return s.getsockname()[0]
+        finally:
+            s.close()
+    except OSError:
+        return "127.0.0.1"
+
+
+class _Liveness:
+    """Process-death detector (see the module docstring): a listening socket whose accepted
+    connections are held open (our death = their EOF) and one outgoing connection per other
+    member, each read by a thread that reports EOF / error once as on_eof(member, address)."""
+
+    def __init__(self, store, pid: int, host: str, on_eof):
+        self.store, self.pid, self.on_eof = store, pid, on_eof
+        self.srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        self.srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self.srv.bind(("0.0.0.0", 0))
+        self.srv.listen(128)
+        self.addr = f"{host}:{self.srv.getsockname()[1]}"
+        self._held: list[socket.socket] = []
+        self._conn: dict[int, tuple[str, socket.socket]] = {}
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        threading.Thread(target=self._accept, name=f"vcx-live-acc-{pid}", daemon=True).start()
+        store.set(f"{_P}live/{pid}", self.addr)
+
+    def _accept(self):
+        while not self._stop.is_set():
+            try:
+                c, _ = self.srv.accept()
+            except OSError:
+                return
+            with self._lock:
+                self._held.append(c)
+
+    def address_of(self, m: int) -> str | None:
+        key = f"{_P}live/{m}"
+        try:
+            return _s(self.store.get(key)) if self.store.check([key]) else None
+        except Exception:  # noqa: BLE001
+            return None
+
+    def watch(self, members):
+        """Hold a connection to every member (new ones, or a restarted one's new address)."""
+        for m in members:
+            if m == self.pid or self._stop.is_set():
+                continue
+            addr = self.address_of(m)
+            with self._lock:
+                cur = self._conn.get(m)
+            if addr is None or (cur is not None and cur[0] == addr):
+                continue
+            host, _, port = addr.rpartition(":")
+            try:
+                c = socket.create_connection((host, int(port)), timeout=2.0)
+                c.settimeout(None)
+            except OSError:
+                self.on_eof(m, addr)  # published, but nobody listens: that process is gone
+                continue
+            with self._lock:
+                old = self._conn.get(m)
+                self._conn[m] = (addr, c)
+            if old is not None:
+                try:
+                    old[1].close()
+                except OSError:
+                    pass
+            threading.Thread(target=self._read, args=(m, addr, c), name=f"vcx-live-{self.pid}-{m}",
+                             daemon=True).start()
+
+    def _read(self, m, addr, c):
+        try:
+            while c.recv(64):
+                pass
+        except OSError:
+            pass
+        with self._lock:
+            mine = self._conn.get(m, (None, None))[1] is c
+        if mine and not self._stop.is_set():
+            self.on_eof(m, addr)
+
+    def close(self):
+        self._stop.set()
+        with self._lock:
+            socks = [c for _, c in self._conn.values()] + self._held
+            self._conn.clear()
+            self._held.clear()
+        for c in socks + [self.srv]:
+            try:
+                c.close()
+            except OSError:
+                pass
+
+
 class ElasticMembership:
     def __init__(self, store, peer_id: int, *, backend: str = "gloo", device=None, lease_s: float = 3.0,
                  heartbeat_s: float = 0.2, arrive_timeout_s: float = 600.0, pg_timeout_s: float | None = None,
-                 poll_s: float = 0.002):
+                 poll_s: float = 0.002, liveness: bool | None = None, live_host: str | None = None):
         self.store = store
         self.pid = int(peer_id)
         self.backend = backend
@@ -94,6 +202,12 @@ class ElasticMembership:
         self._abort = threading.Event()
         self._abort_reason = ""
         self._watch_seen: dict[int, tuple[int, float]] = {}
+        # liveness links: member -> the address of the incarnation whose connection hit EOF
+        self.liveness = config.get().elastic_liveness if liveness is None else liveness
+        self.live_host = live_host or _route_ip(os.environ.get("MASTER_ADDR", "127.0.0.1"))
+        self._live: _Liveness | None = None
+        self._eof: dict[int, str] = {}
+        self.eof_events: list[tuple[int, float]] = []  # (member, time) of every EOF seen
         if backend == "nccl":
             # abortable (non-blocking) RCCL communicator init for every generation's group
             os.environ.setdefault("TORCH_NCCL_USE_COMM_NONBLOCKING", "1")
@@ -114,6 +228,12 @@ class ElasticMembership:
                     self.store.add(key, 1)
                 except Exception:  # noqa: BLE001 — the store is gone: nothing left to do
                     return
+                live = self._live
+                if live is not None:
+                    try:
+                        live.watch(list(self.members))
+                    except Exception:  # noqa: BLE001 — best effort; the lease still applies
+                        pass
                 if self._armed:
                     try:
                         self._watch()
@@ -121,6 +241,8 @@ class ElasticMembership:
                         self._trip(f"watchdog error: {e!r}")
 
         self.store.add(f"{_P}hb/{self.pid}", 1)
+        if self.liveness and self._live is None:
+            self._live = _Liveness(self.store, self.pid, self.live_host, self._on_eof)
         self._hb_thread = threading.Thread(target=loop, name=f"vcx-hb-{self.pid}", daemon=True)
         self._hb_thread.start()
 
@@ -129,6 +251,29 @@ class ElasticMembership:
         if self._hb_thread is not None:
             self._hb_thread.join(timeout=2)
         self._hb_thread = None
+        if self._live is not None:
+            self._live.close()
+            self._live = None
+
+    def _on_eof(self, m: int, addr: str):
+        """A member's liveness connection closed: that process is gone."""
+        now = time.time()
+        with self._lock:
+            self._eof[m] = addr
+            self.eof_events.append((m, now))
+            armed = self._armed and m in self.members and not self._abort.is_set()
+        _dbg(self.pid, f"liveness EOF from peer {m} ({addr})")
+        if armed:
+            self.declare_abort(f"peer {m} process gone (liveness EOF) inside a collective of gen {self.gen}")
+
+    def _gone(self, m: int) -> bool:
+        """Did the connection to member m's CURRENT incarnation close (a restarted peer publishes
+        a new address and is not 'gone')?"""
+        with self._lock:
+            addr = self._eof.get(m)
+        if addr is None or self._live is None:
+            return False
+        return self._live.address_of(m) == addr
 
     def _watch(self):
         """One watchdog tick while a guarded collective is in flight."""
@@ -143,6 +288,9 @@ class ElasticMembership:
         for m in list(self.members):
             if m == self.pid:
                 continue
+            if m in self._eof and self._gone(m):  # died between the round's outcome and this guard
+                self.declare_abort(f"peer {m} process gone (liveness EOF) before a collective of gen {g}")
+                return
             hb = self._hb(m)
             last = self._watch_seen.get(m)
             if last is None or hb != last[0]:
@@ -258,7 +406,12 @@ class ElasticMembership:
             self._armed = True
         try:
             _dbg(self.pid, f"guard {self.gen}/{tag}: connect")
+            fresh = not getattr(grp, "_connected", True) or getattr(grp, "_pending", None) is not None
+            t0 = time.time()
             grp.connect()
+            if fresh:  # communicator build of a new generation (RCCL init / gloo full mesh)
+                self.events.append({"event": "connect", "gen": self.gen, "ms": (time.time() - t0) * 1e3,
+                                    "t": time.time()})
             _dbg(self.pid, f"guard {self.gen}/{tag}: body")
             yield
             _dbg(self.pid, f"guard {self.gen}/{tag}: commit")
@@ -331,6 +484,9 @@ class ElasticMembership:
                     continue
                 if m in joiners or self.store.check([f"{_P}leave/{m}"]):
                     left.add(m)  # announced leave, or restarted and re-registered as a joiner
+                    continue
+                if m in self._eof and self._gone(m):
+                    dead.add(m)  # its liveness link closed: no lease wait
                     continue
                 hb = self._hb(m)
                 last, seen_at = hb_seen[m]
@@ -407,6 +563,8 @@ class ElasticMembership:
         grp.fault_hook = self.fault_hook
         with self._lock:
             self.group = grp
+        if self._live is not None:
+            self._live.watch(members)
 
     def _hb(self, m) -> int:
         return int(self.store.add(f"{_P}hb/{m}", 0))

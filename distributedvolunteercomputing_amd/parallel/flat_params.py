@@ -128,14 +128,20 @@ class FlatBuffers:
     def names(self):
         return [qn for _, _, qn, *_ in self.entries]
 
-    def average_(self, group):
-        """Mean over the group's peers (collective on a scratch copy: an aborted op of an
-        elastic round can never write into the live buffers)."""
+    def averaged(self, group):
+        """The mean over the group's peers as a new fp32 vector (None when there is nothing to
+        average). The live buffers are not touched: an elastic round loads the result only after
+        its verdict is `commit`, so an aborted round leaves every peer's buffers as they were."""
         if not self.entries or group is None or group.size == 1:
-            return
+            return None
         v = self.as_fp32()
         dev = group.device if group.backend == "nccl" else "cpu"
         v = v.to(dev)
         group.allreduce_(v)
-        v.div_(group.size)
-        self.load_fp32(v)
+        return v.div_(group.size)
+
+    def average_(self, group):
+        """Mean over the group's peers, loaded into the live buffers (non-elastic callers)."""
+        v = self.averaged(group)
+        if v is not None:
+            self.load_fp32(v)

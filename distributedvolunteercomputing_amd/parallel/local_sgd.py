@@ -170,11 +170,11 @@ class LocalSGDTrainer:
             snap = self.compressor.snapshot() if (self.compressor is not None and grp.size > 1) else None
             try:
                 with mem.guard():
-                    if newcomers:
-                        self._admit_newcomers(newcomers)
+                    adopted = self._admit_newcomers(newcomers) if newcomers else None
                     res = self._reduce(newcomers)
-                    self.buffers.average_(grp)
-                self._apply(res)
+                    bufs = self.buffers.averaged(grp)
+                self._adopt(adopted)  # nothing is applied before the verdict is `commit`
+                self._apply(res, bufs)
                 return
             except PeerFailure:
                 if snap is not None:
@@ -197,7 +197,9 @@ class LocalSGDTrainer:
         allreduce_sum_(self.delta, g, self.cfg.algo)
         return self.delta, 1.0 / contributors
 
-    def _apply(self, res):
+    def _apply(self, res, bufs=None):
+        if bufs is not None:
+            self.buffers.load_fp32(bufs)
         if res is None:
             self.anchor.copy_(self.master)
             return
@@ -211,43 +213,47 @@ class LocalSGDTrainer:
 
     def _admit_newcomers(self, newcomers):
         """The generation contains peers without the model (joiners, or members whose earlier
-        admission was aborted): the first continuing member sends them the anchor (identical on
-        all continuing members), the outer momentum and the BN buffers, point-to-point, so a
-        failed transfer can never corrupt a continuing member. Newcomers receive into scratch
-        buffers and adopt the model only when the transfer completed."""
+        admission was aborted): the first continuing member broadcasts ONE packed fp32 vector
+        [anchor | outer momentum | BN buffers] (identical on every continuing member) to the whole
+        group, so every newcomer gets it in one pipelined collective instead of one point-to-point
+        transfer per newcomer from the same root (RCCL: ring/tree broadcast over the xGMI links).
+        Everyone receives into scratch; a newcomer adopts the model only after the round's verdict
+        is `commit` (``_adopt``), so an aborted transfer can never corrupt any peer.
+        Returns what the newcomer adopts (None on continuing members)."""
         g = self.group
         members = g.members
         cont = [i for i, m in enumerate(members) if m not in newcomers]
         if not cont:
-            return  # nobody holds a model yet: everyone starts from its own (identical) init
+            return None  # nobody holds a model yet: everyone starts from its own (identical) init
         root = cont[0]
-        new_ranks = [i for i, m in enumerate(members) if m in newcomers]
         dev = self.anchor.device
+        parts = [self.anchor] + ([self.outer_mom] if self.outer_mom is not None else [])
+        nb = self.buffers.numel if self.buffers else 0
+        n = sum(p.numel() for p in parts) + nb
+        bdev = dev if g.backend == "nccl" else torch.device("cpu")
         if g.rank == root:
-            bufs = [self.anchor] + ([self.outer_mom] if self.outer_mom is not None else [])
-            if self.buffers:
-                bufs.append(self.buffers.as_fp32().to(dev))
-            for r in new_ranks:
-                for b in bufs:
-                    g.send(b, r, tag=7)
-        elif g.rank in new_ranks:
-            anchor = torch.empty_like(self.anchor)
-            g.recv(anchor, root, tag=7)
-            mom = None
-            if self.outer_mom is not None:
-                mom = torch.empty_like(self.outer_mom)
-                g.recv(mom, root, tag=7)
-            bv = None
-            if self.buffers:
-                bv = torch.empty(self.buffers.numel, dtype=torch.float32, device=dev)
-                g.recv(bv, root, tag=7)
-            self.anchor.copy_(anchor)
-            if mom is not None:
-                self.outer_mom.copy_(mom)
-            if bv is not None:
-                self.buffers.load_fp32(bv)
-            self.master.copy_(self.anchor)
-            ops.f32_to_bf16(self.anchor, self.flat.param)
+            pack = torch.cat([p.reshape(-1).to(bdev) for p in parts]
+                             + ([self.buffers.as_fp32().to(bdev)] if nb else []))
+        else:
+            pack = torch.empty(n, dtype=torch.float32, device=bdev)
+        g.broadcast_(pack, root)
+        return pack if members[g.rank] in newcomers else None
+
+    def _adopt(self, pack):
+        """A newcomer takes the admitted model (after `commit`)."""
+        if pack is None:
+            return
+        pack = pack.to(self.anchor.device)
+        n0 = self.anchor.numel()
+        self.anchor.copy_(pack[:n0])
+        pos = n0
+        if self.outer_mom is not None:
+            self.outer_mom.copy_(pack[pos:pos + n0])
+            pos += n0
+        if self.buffers:
+            self.buffers.load_fp32(pack[pos:pos + self.buffers.numel])
+        self.master.copy_(self.anchor)
+        ops.f32_to_bf16(self.anchor, self.flat.param)
 
     def join_running_job(self):
         """Called by a peer that was just admitted (``membership.join()``): receive the model
@@ -259,10 +265,11 @@ class LocalSGDTrainer:
             self.group = grp
             try:
                 with mem.guard():
-                    self._admit_newcomers(newcomers)
+                    adopted = self._admit_newcomers(newcomers)
                     res = self._reduce(newcomers)
-                    self.buffers.average_(grp)
-                self._apply(res)
+                    bufs = self.buffers.averaged(grp)
+                self._adopt(adopted)
+                self._apply(res, bufs)
                 return
             except PeerFailure:
                 self.delta = torch.zeros_like(self.delta)

@@ -14,9 +14,9 @@ R = 2, so BASELINE.json config 4's "kill 2 mid-training" — any two peers, adja
 never loses fp32 optimizer state). Replicas apply the very same AdamW update from the same
 averaged gradient: no extra traffic per step beyond the ring-shifts; only (1+R)x the
 HBM-bound optimizer work on (1+R)/P of the model. When the membership changes the survivors
-re-shard: every live holder of an old shard broadcasts it, every peer rebuilds the full fp32
-state (12 B/param: 96 GB at 8B parameters, inside 288 GB of HBM) and cuts its new primary and
-replica slices. If a shard has no live holder left the re-shard fails loudly (StateLost)
+re-shard point to point: each slice of the new layout a peer must hold comes from one live old
+holder (or its own old shards), in one variable-split all-to-all; only the slices that change
+holder travel and nothing is materialised at full-model size. If a shard has no live holder left the re-shard fails loudly (StateLost)
 unless ``allow_state_loss`` is set. Under elastic membership every collective phase runs
 guarded (parallel/elastic.py): a peer dying inside the gradient reduction or the parameter
 gather aborts the phase on all survivors, which recover to a new generation, re-shard, and
@@ -75,7 +75,7 @@ class ShardedDPTrainer:
         self._skip_round = False
         self._sumsq = None  # global squared gradient norm from the reduce-scatter path
         self._layout_members = list(self.group.members) if self.group is not None else [0]
-        self._layout(full_master=self.flat.param.float(), full_m=None, full_v=None)
+        self._layout(full_master=self.flat.param, full_m=None, full_v=None)  # slices converted one by one
 
     # ------------------------------------------------------------------ layout
     @property
@@ -100,7 +100,7 @@ class ShardedDPTrainer:
         def cut(full, a, b):
             if full is None:
                 return torch.zeros(b - a, dtype=torch.float32, device=self.device)
-            return full[a:b].clone()
+            return full[a:b].to(torch.float32, copy=True)
 
         self.master = cut(full_master, lo, hi)
         self.m = cut(full_m, lo, hi)
@@ -186,12 +186,21 @@ class ShardedDPTrainer:
             self._adam(avg)
             try:
                 with mem.guard("p"):
-                    self._gather_params(elastic=True)
-                    self.buffers.average_(self.group)
-            except PeerFailure:  # the re-shard rebuilds every parameter from the fp32 masters
+                    params = self._gather_params(elastic=True)
+                    bufs = self.buffers.averaged(self.group)
+                if params is not None:  # applied only after the phase committed
+                    self.flat.param.copy_(params)
+                if bufs is not None:
+                    self.buffers.load_fp32(bufs)
+            except PeerFailure:
                 self.failed_phases += 1
                 grp, _, newcomers = mem.recover()
-                self._reshard_until_ok(grp, newcomers)
+                self._reshard_until_ok(grp, newcomers)  # also re-gathers exact bf16 parameters
+                # the re-shard ran this step's membership round: the next step must not run
+                # another one (a peer admitted in the recovery goes straight into the gradient
+                # phase, as join_running_job() arranges), or the two sides wait on different
+                # rounds until a process-group timeout
+                self._skip_round = True
         self.t += 1
         return loss.detach()
 
@@ -276,16 +285,27 @@ class ShardedDPTrainer:
             self._adam_range(avg, a, b, rep["master"], rep["m"], rep["v"])
 
     def _gather_params(self, elastic: bool):
+        """All-gather of the updated bf16 primaries. Elastic: into a fresh buffer that the caller
+        copies into the parameters only after the phase's verdict is `commit`."""
         if self.world == 1:
-            return
+            return None
         lo, hi = self.prim
         mine = self.flat.param[lo:hi].clone()
         if not elastic:
             self.group.all_gather_(self.flat.param, mine)
-            return
+            return None
         out = torch.empty_like(self.flat.param)  # never let an aborted gather write the params
         self.group.all_gather_(out, mine)
-        self.flat.param.copy_(out)
+        return out
+
+    def _refresh_params(self):
+        """bf16 parameters of every slice this peer holds, from its fp32 masters."""
+        for (a, b), master in [(self.prim, self.master)] + [(r["range"], r["master"]) for r in self.reps]:
+            if b > a:
+                if master.is_cuda:
+                    ops.f32_to_bf16(master, self.flat.param[a:b])
+                else:
+                    self.flat.param[a:b].copy_(master)
 
     # ------------------------------------------------------------------ elastic re-shard
     def join_running_job(self):
@@ -313,10 +333,46 @@ class ShardedDPTrainer:
         """Non-elastic entry point (tests / manual regroup)."""
         self._reshard_apply(new_group, *self._reshard_collect(new_group, newcomers))
 
+    def _reshard_plan(self, L, R_old, members, R_new, newcomers):
+        """Where every piece of the NEW layout comes from. For each member d of the new group and
+        each shard it must hold (its primary and R_new replicas), the intersections with the OLD
+        layout's shards: (d, k (index among d's held shards), src pid, old shard j, [x, y)).
+        src is d itself when d held old shard j (a local copy), else one live old holder of j,
+        chosen round-robin over the holders so the senders share the load. Pieces whose old
+        shard has no live holder are returned as lost. Identical on every member."""
+        old_P, new_P = len(L), len(members)
+        live = {}
+        for j in range(old_P):
+            hs = [L[(j + i) % old_P] for i in range(R_old + 1)]
+            live[j] = [h for h in hs if h in members and h not in newcomers]
+        old_bounds = [self.flat.shard_bounds(j, old_P) for j in range(old_P)]
+        plan, lost = [], []
+        for d, pid in enumerate(members):
+            held = [d] + [(d - i) % new_P for i in range(1, R_new + 1)]
+            for k, sh in enumerate(held):
+                a, b = self.flat.shard_bounds(sh, new_P)
+                for j, (aj, bj) in enumerate(old_bounds):
+                    x, y = max(a, aj), min(b, bj)
+                    if y <= x:
+                        continue
+                    H = live[j]
+                    if not H:
+                        lost.append((d, k, x, y))
+                        continue
+                    src = pid if pid in H else H[(d + j) % len(H)]
+                    plan.append((d, k, src, j, x, y))
+        return plan, lost
+
     def _reshard_collect(self, new_group, newcomers):
-        """Rebuild the full fp32 optimizer state from the live holders of every old shard
-        (primary, else the first live replica). Touches no trainer state: the result is
-        applied only after the phase commits."""
+        """Targeted re-shard: every slice of optimizer state (fp32 master, m, v)
+        that a member must hold in the NEW layout is assembled from pieces of the OLD layout; a
+        piece it already holds is copied locally, every other piece comes from ONE live old
+        holder, point to point, all of it in ONE variable-split all-to-all (RCCL: grouped
+        send/recv over the xGMI links). Nothing is materialised at full-model size (the previous
+        scheme rebuilt the full 12 B/param state on every peer: 96 GB per peer and per regroup at
+        8B parameters); the wire carries exactly the state of the slices that change holder.
+        Newcomers additionally get the bf16 parameters from an all-gather of the new primaries'
+        masters. Touches no trainer state: the result is applied only after the phase commits."""
         t0 = time.perf_counter()
         members = list(new_group.members)
         my_pid = self.membership.pid if self.membership is not None else members[new_group.rank]
@@ -325,8 +381,9 @@ class ShardedDPTrainer:
             raise StateLost("no member of the new generation holds optimizer state")
         root0 = cont[0]
         dev = self.device
+        cdev = dev if new_group.backend == "nccl" else torch.device("cpu")
         # the layout that the continuing members' shards follow (newcomers do not know it)
-        hdr = torch.full((257,), -1, dtype=torch.int64, device=dev if new_group.backend == "nccl" else "cpu")
+        hdr = torch.full((257,), -1, dtype=torch.int64, device=cdev)
         if new_group.rank == root0:
             L = self._layout_members
             hdr[0] = len(L)
@@ -334,40 +391,78 @@ class ShardedDPTrainer:
         new_group.broadcast_(hdr, root=root0)
         hdr = hdr.cpu()
         L = [int(x) for x in hdr[1 : 1 + int(hdr[0])]]
-        old_P = len(L)
-        R = min(self.cfg.replicas if self.cfg.replicate else 0, old_P - 1)
-        n = self.flat.numel
-        full = [torch.zeros(n, dtype=torch.float32, device=dev) for _ in range(3)]
-        lost = []
-        my_old = L.index(my_pid) if (my_pid in L and my_pid not in newcomers) else None
-        for j in range(old_P):
-            a, b = self.flat.shard_bounds(j, old_P)
-            if b <= a:
-                continue
-            holders = [L[(j + i) % old_P] for i in range(R + 1)]
-            live = [h for h in holders if h in members and h not in newcomers]
-            if not live:
-                lost.append((a, b))
-                continue
-            holder = live[0]
-            root = members.index(holder)
-            if holder == my_pid:
-                st = self._shard_state_old(j, my_old, old_P)
-                for f, s in zip(full, st):
-                    f[a:b].copy_(s)
-            for f in full:
-                new_group.broadcast_(f[a:b], root=root)
+        old_P, new_P = len(L), len(members)
+        R_old = min(self.cfg.replicas if self.cfg.replicate else 0, old_P - 1)
+        R_new = max(0, min(self.cfg.replicas, new_P - 1)) if self.cfg.replicate else 0
+        plan, lost = self._reshard_plan(L, R_old, members, R_new, newcomers)
         if lost and not self.cfg.allow_state_loss:
-            raise StateLost(f"optimizer-state shards {lost} had no live holder among {members} "
-                            f"(old layout {L}, replicas {R})")
+            raise StateLost(f"optimizer-state ranges {[(x, y) for *_, x, y in lost]} had no live holder among "
+                            f"{members} (old layout {L}, replicas {R_old})")
+        me = new_group.rank
+        my_old = L.index(my_pid) if (my_pid in L and my_pid not in newcomers) else None
+        held = [me] + [(me - i) % new_P for i in range(1, R_new + 1)]
+        dst = []  # this peer's new (primary, replicas): fresh tensors, live state untouched
+        for sh in held:
+            a, b = self.flat.shard_bounds(sh, new_P)
+            dst.append({"shard": sh, "range": (a, b),
+                        **{f: torch.zeros(b - a, dtype=torch.float32, device=dev) for f in ("master", "m", "v")}})
+
+        def old_piece(j, x, y):
+            st = self._shard_state_old(j, my_old, old_P)
+            aj = self.flat.shard_bounds(j, old_P)[0]
+            return [t[x - aj : y - aj] for t in st]
+
+        send = [[] for _ in range(new_P)]
+        recv = [[] for _ in range(new_P)]
+        for d, k, src, j, x, y in plan:
+            if members[d] == my_pid and src == my_pid:
+                a = dst[k]["range"][0]
+                for f, t in zip(("master", "m", "v"), old_piece(j, x, y)):
+                    dst[k][f][x - a : y - a].copy_(t)
+            elif src == my_pid:
+                send[d].extend(old_piece(j, x, y))
+            elif members[d] == my_pid:
+                recv[members.index(src)].append((k, x, y))
+        send_splits = [sum(t.numel() for t in parts) for parts in send]
+        recv_splits = [3 * sum(y - x for _, x, y in pieces) for pieces in recv]
+        moved = 0
+        if sum(send_splits) or sum(recv_splits) or new_P > 1:
+            sbuf = (torch.cat([t.to(cdev) for parts in send for t in parts]) if sum(send_splits)
+                    else torch.zeros(0, dtype=torch.float32, device=cdev))
+            rbuf = torch.empty(sum(recv_splits), dtype=torch.float32, device=cdev)
+            if new_P > 1:
+                new_group.alltoall_(rbuf, sbuf, recv_splits, send_splits)
+            pos = 0
+            for src_rank in range(new_P):
+                for k, x, y in recv[src_rank]:
+                    a = dst[k]["range"][0]
+                    for f in ("master", "m", "v"):
+                        dst[k][f][x - a : y - a].copy_(rbuf[pos : pos + y - x].to(dev))
+                        pos += y - x
+            moved = 4 * sum(send_splits)
+        changed = 12 * sum(y - x for pieces in recv for _, x, y in pieces)
         ost = self.ostate.clone()
         new_group.broadcast_(ost, root=root0)  # step counter / lr must agree
         bufs = None
         if self.buffers:
-            bufs = self.buffers.as_fp32().to(dev if new_group.backend == "nccl" else "cpu")
+            bufs = self.buffers.as_fp32().to(cdev)
             new_group.broadcast_(bufs, root=root0)
-        ev = {"t": self.t, "old": L, "new": members, "lost": lost, "ms": (time.perf_counter() - t0) * 1e3}
-        return full, ost, bufs, lost, ev
+        params = None
+        if new_P > 1:
+            # exact bf16 parameters for everyone from the new primaries' masters (newcomers hold
+            # none; after an aborted parameter gather the survivors' copies are one step stale)
+            for d, k, x, y in lost:
+                if members[d] == my_pid:  # allow_state_loss: restart from the bf16 params we have
+                    a = dst[k]["range"][0]
+                    dst[k]["master"][x - a : y - a].copy_(self.flat.param[x:y].float())
+            lo, hi = dst[0]["range"]
+            mine = torch.empty(hi - lo, dtype=self.flat.param.dtype, device=dev)
+            ops.f32_to_bf16(dst[0]["master"], mine) if mine.is_cuda else mine.copy_(dst[0]["master"])
+            params = torch.empty_like(self.flat.param)
+            new_group.all_gather_(params, mine)
+        ev = {"t": self.t, "old": L, "new": members, "lost": [(x, y) for *_, x, y in lost],
+              "bytes_sent": moved, "bytes_changed": changed, "ms": (time.perf_counter() - t0) * 1e3}
+        return dst, ost, bufs, params, lost, ev
 
     def _shard_state_old(self, j, my_old, old_P):
         """(master, m, v) this peer held for shard j of the OLD layout (index my_old of old_P)."""
@@ -380,15 +475,24 @@ class ShardedDPTrainer:
                 return rep["master"], rep["m"], rep["v"]
         raise StateLost(f"shard {j} expected on this peer (old index {my_old} of {old_P})")
 
-    def _reshard_apply(self, new_group, full, ost, bufs, lost, ev):
-        for a, b in lost:  # allow_state_loss: no live replica, restart from the bf16 params
-            full[0][a:b].copy_(self.flat.param[a:b].float())
-        ops.f32_to_bf16(full[0], self.flat.param)  # every peer now holds the full fp32 master
+    def _reshard_apply(self, new_group, dst, ost, bufs, params, lost, ev):
+        members = list(new_group.members)
+        my_pid = self.membership.pid if self.membership is not None else members[new_group.rank]
+        for d, k, x, y in lost:  # allow_state_loss: no live holder, restart from the bf16 params
+            if members[d] == my_pid and params is None:
+                a = dst[k]["range"][0]
+                dst[k]["master"][x - a : y - a].copy_(self.flat.param[x:y].float())
         self.ostate.copy_(ost)
         if bufs is not None:
             self.buffers.load_fp32(bufs)
         self.group = new_group
-        self._layout_members = list(new_group.members)
-        self._layout(*full)
-        del full
+        self._layout_members = members
+        self.prim = dst[0]["range"]
+        self.master, self.m, self.v = dst[0]["master"], dst[0]["m"], dst[0]["v"]
+        self.reps = [{"shard": r["shard"], "range": r["range"], "master": r["master"], "m": r["m"], "v": r["v"]}
+                     for r in dst[1:]]
+        if params is not None:
+            self.flat.param.copy_(params)
+        else:  # a single survivor holds everything: its parameters from its masters
+            self._refresh_params()
         self.reshard_events.append(ev)

@@ -44,17 +44,17 @@ def _hash(t):
     return hashlib.sha1(t.detach().float().cpu().numpy().tobytes()).hexdigest()[:16]
 
 
-def _peer(pid, port, q, mode, kind, join, victims, n_rejoin):
+def _peer(pid, port, q, mode, kind, join, victims, n_rejoin, fault_op=None):
     os.environ.setdefault("OMP_NUM_THREADS", "1")
     try:
         torch.set_num_threads(1)
-        res = _peer_body(pid, port, mode, kind, join, victims, n_rejoin)
+        res = _peer_body(pid, port, mode, kind, join, victims, n_rejoin, fault_op)
         q.put((pid, join, "ok", res))
     except BaseException as e:  # noqa: BLE001
         q.put((pid, join, "err", f"{e!r}\n{traceback.format_exc()}"))
 
 
-def _peer_body(pid, port, mode, kind, join, victims, n_rejoin):
+def _peer_body(pid, port, mode, kind, join, victims, n_rejoin, fault_op_override=None):
     """A peer that, unless it is a victim, runs until both victims are back and it has
     committed 3 more rounds in the latest generation, recording a state hash per round."""
     from distributedvolunteercomputing_amd.models.mlp import MLP, synthetic_mnist
@@ -76,6 +76,7 @@ def _peer_body(pid, port, mode, kind, join, victims, n_rejoin):
         mk = lambda: ShardedDPTrainer(model, ShardedConfig(lr=1e-2, weight_decay=0.0, replicas=2),  # noqa: E731
                                       membership=mem, device="cpu")
         fault_op, state = "reduce_scatter", (lambda tr: tr.flat.param)
+    fault_op = fault_op_override or fault_op
 
     if pid in victims and not join:
         def hook(grp, op):
@@ -123,13 +124,14 @@ def _peer_body(pid, port, mode, kind, join, victims, n_rejoin):
             "failed": getattr(tr, "failed_rounds", getattr(tr, "failed_phases", 0))}
 
 
-def _run(mode, kind, victims=(3, 4), timeout=150):
+def _run(mode, kind, victims=(3, 4), timeout=150, fault_op=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _mp.free_port()
     store = _store(port, master=True)  # noqa: F841 — this process hosts the rendezvous
     n_rejoin = len(victims)
-    procs = {pid: ctx.Process(target=_peer, args=(pid, port, q, mode, kind, False, victims, n_rejoin), daemon=True)
+    procs = {pid: ctx.Process(target=_peer, args=(pid, port, q, mode, kind, False, victims, n_rejoin, fault_op),
+                              daemon=True)
              for pid in range(W)}
     for p in procs.values():
         p.start()
@@ -226,9 +228,13 @@ def test_localsgd_two_peers_die_inside_allreduce_then_rejoin(kind):
         assert any(len(shared.get(k, {})) >= 3 for k in late), (who, out[who]["hist"])
 
 
-def test_sharded_two_adjacent_peers_killed_inside_reduce_scatter_no_state_lost():
+@pytest.mark.parametrize("fault_op", ["reduce_scatter", "all_gather"])
+def test_sharded_two_adjacent_peers_killed_inside_a_phase_no_state_lost(fault_op):
+    """reduce_scatter: the gradient phase; all_gather: the parameter phase, while the victims'
+    replacements register as joiners (after a parameter-phase recovery the survivors
+    and a peer admitted in it must enter the same next phase)."""
     victims = (2, 3)  # adjacent: shard 2's primary and first replica die together
-    out = _run("zero", "kill", victims)
+    out = _run("zero", "kill", victims, fault_op=fault_op)
     _assert_recovered(out, victims)
     _check_consistent(out)
     for who, r in out.items():

@@ -153,7 +153,7 @@ def test_status_and_idempotent_join(coord, tmp_path):
         cc = protocol.ControlClient("127.0.0.1", coord.control_port)
         p1 = cc.call("join", w.my_ip)
         p2 = cc.call("join", w.my_ip)
-        assert p1 == p2 == w.connect_to_port
+        assert p1 == p2 and p1.split("||")[0] == w.connect_to_port  # port [|| store key prefix]
         assert coord.sched.workers().count(w.my_ip) == 1
         import json
 
