@@ -333,6 +333,12 @@ class coordinator:  # noqa: N801  (reference class name)
             if p2p and command in ("request", "processed") and not protocol.valid_chunk_shape(hdr.get("cshape")):
                 self.metrics.incr("bad_frames")  # a shape the other end would have to allocate blindly
                 continue
+            if command == "failed" and p2p:  # a pair transfer of this chunk to v failed
+                cid = int(hdr.get("chunk", -1))
+                if self.sched.fail(cid, v.addr):
+                    self.metrics.incr("p2p_failed_requeued")
+                    self._kick()
+                continue
             if command == "request":
                 while self.req_rep and self.sched.queued() > self.max_buffer and v.alive:
                     time.sleep(0.005)  # back-pressure: the hub stops acking, TCP throttles the requester
@@ -357,7 +363,8 @@ class coordinator:  # noqa: N801  (reference class name)
                 if dst is not None:
                     if p2p:  # both ends post the transfer of the result: worker -> requester
                         key = rec[2]["key"] if rec is not None and rec[2] else None
-                        v.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "send_result", "chunk": cid, "dst": dst.vid}))
+                        v.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "send_result", "chunk": cid, "dst": dst.vid,
+                                                     "cshape": hdr.get("cshape")}))
                         dst.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "recv_result", "chunk": cid, "src": v.vid,
                                                        "cshape": hdr.get("cshape"), "key": key}))
                     else:

@@ -20,6 +20,15 @@ operations in order on its own thread, in the order the coordinator's instructio
 A pair whose peer the coordinator declares dead is aborted (its watch trips: RCCL
 ``ncclCommAbort``; a gloo wait is abandoned), so a transfer to a crashed worker never blocks
 the requester's transfers to the others, and the re-dispatched chunk goes out on another pair.
+
+A transfer that fails between two LIVE volunteers (a transport error, a timeout) kills only that
+pair's communicator: the failing end bumps the pair's generation in the store
+(``vcx/p2p/<src>><dst>/gen``, one compare-and-set, so both ends' failures bump it once), drops
+the pair, and reports the failure to its caller (the volunteer then tells the coordinator, which
+re-dispatches the chunk). Before every operation a pair compares its generation with the store's
+and is rebuilt under the new name if it is behind, so the other end — whose own operation may
+have completed before the failure — moves to the fresh communicator too instead of waiting on
+the broken one.
 """
 from __future__ import annotations
 
@@ -51,14 +60,25 @@ def _device_key(dev: torch.device) -> str:
 
 
 class _PairWatch:
-    """The ``watch`` protocol of PeerGroup guarded waits, tripped by a peer_dead notice."""
+    """The ``watch`` protocol of PeerGroup guarded waits, tripped by a peer_dead notice or — polled
+    at most every 50 ms from the waiting pair thread — by the other end moving the pair to a new
+    generation (its side of the transfer failed: this side's pending operation never completes)."""
 
-    def __init__(self, pid):
+    def __init__(self, pid, moved=None):
         self.pid = pid
         self._ev = threading.Event()
         self._reason = ""
+        self._moved = moved  # () -> bool: has the pair's generation advanced in the store?
+        self._next_check = 0.0
 
     def tripped(self) -> bool:
+        if not self._ev.is_set() and self._moved is not None and time.monotonic() >= self._next_check:
+            self._next_check = time.monotonic() + 0.05
+            try:
+                if self._moved():
+                    self.declare_abort("the other end moved the pair to a new generation")
+            except Exception:  # noqa: BLE001 — store unreachable: leave it to the timeouts
+                pass
         return self._ev.is_set()
 
     def abort_reason(self) -> str:
@@ -77,16 +97,50 @@ class _Pair:
         self.q: queue.Queue = queue.Queue()
         self.group = None
         self.dead = False
+        self.gen = None  # generation of the current communicator (from the store)
+        self._store = None
         self.thread = threading.Thread(target=self._loop, name=f"vcx-p2p-{src}>{dst}", daemon=True)
         self.thread.start()
 
+    def _gen_key(self):
+        return f"vcx/p2p/{self.src}>{self.dst}/gen"
+
+    def _store_gen(self) -> int:
+        return int(self._store.add(self._gen_key(), 0))
+
+    def _drop_group(self):
+        g, self.group = self.group, None
+        if g is not None:
+            try:
+                g.abort()
+            except Exception:  # noqa: BLE001
+                pass
+
+    def _failed(self):
+        """This end saw the communicator fail: move the pair to the next generation (once)."""
+        if self._store is not None and self.gen is not None:
+            try:
+                self._store.compare_set(self._gen_key(), str(self.gen), str(self.gen + 1))
+            except Exception:  # noqa: BLE001
+                pass
+        self._drop_group()
+
     def _group(self):
-        if self.group is None:
-            rank = 0 if self.plane.vid == self.src else 1
+        if self._store is None:
             # a store client of its own: a c10d TCPStore client serialises its blocking waits, so
             # one pair stuck rendezvousing with a dead peer would stall every other pair's connect
-            store = self.plane.store_factory()
-            name = f"p2p/{self.src}>{self.dst}"
+            self._store = self.plane.store_factory()
+            self._store.add(self._gen_key(), 0)
+        cur = self._store_gen()
+        if self.group is not None and cur != self.gen:  # the other end failed and moved on
+            self.plane.metrics_incr("p2p_pair_rebuilt")
+            self._drop_group()
+        if self.group is None:
+            rank = 0 if self.plane.vid == self.src else 1
+            store = self._store
+            self.gen = cur
+            self.watch = _PairWatch(self.plane.vid, moved=lambda g=cur: self._store_gen() != g)
+            name = f"p2p/{self.src}>{self.dst}/g{cur}"
             # non-blocking handshake first: the communicator is built only once both ends are
             # known to be up, so a peer that never shows (crashed before its first transfer)
             # leaves no rendezvous blocked inside c10d — the wait below is abortable
@@ -123,6 +177,9 @@ class _Pair:
             else:
                 try:
                     g = self._group()
+                    if self.plane.inject_failures > 0 and kind == "recv":  # fault-injection tests
+                        self.plane.inject_failures -= 1
+                        raise PeerFailure(f"pair {self.src}>{self.dst}: injected transfer failure")
                     if kind == "send":
                         g.send(payload, 1, tag)
                         res = None
@@ -131,8 +188,11 @@ class _Pair:
                         res = torch.empty(shape, dtype=dtype, device=self.plane.device)
                         g.recv(res, 0, tag)
                 except Exception as e:  # noqa: BLE001 — PeerFailure or a transport error: this pair only
-                    self.dead = True
                     self.plane.metrics_incr("p2p_failed")
+                    if self.plane.is_dead_peer(self.src, self.dst):
+                        self.dead = True  # the other end is gone for good
+                    else:
+                        self._failed()  # a live peer: a new generation at the next operation
                     res = e
             try:
                 cb(res)
@@ -158,6 +218,11 @@ class PairPlane:
         self._pairs: dict[tuple[int, int], _Pair] = {}
         self._lock = threading.Lock()
         self.device_key = _device_key(self.device)
+        self._dead: set[int] = set()  # volunteers the coordinator declared dead
+        self.inject_failures = 0  # tests: make this many receives fail like a broken transport
+
+    def is_dead_peer(self, src: int, dst: int) -> bool:
+        return src in self._dead or dst in self._dead
 
     def metrics_incr(self, name):
         if self.metrics is not None:
@@ -184,6 +249,7 @@ class PairPlane:
     def peer_dead(self, vid: int):
         """The coordinator declared `vid` dead: abort every pair with it (in-flight ops fail fast)."""
         with self._lock:
+            self._dead.add(int(vid))
             pairs = [p for (s, d), p in self._pairs.items() if vid in (s, d)]
         for p in pairs:
             p.dead = True

@@ -342,7 +342,10 @@ class client:  # noqa: N801 (reference class name)
 
             def got(buf, hdr=hdr, msg=msg):
                 if isinstance(buf, BaseException):
+                    # the chunk never arrived: hand it back to the coordinator, which re-queues it
+                    # at the front (the requester still holds its frames)
                     self.metrics.incr("p2p_recv_failed")
+                    self.sender.send_image(f"{msg.split('||')[0]}||failed", _EMPTY, p2p=1, chunk=cid)
                     return
                 parts = msg.split("||")
                 nums = [int(x) for x in parts[2].split("-")] if parts[2] else []
@@ -351,14 +354,21 @@ class client:  # noqa: N801 (reference class name)
         elif cmd == "send_result":  # worker: annotated chunk -> requester `dst`
             with self._p2p_lock:
                 t = self._results.pop(cid, None)
-            if t is not None:
-                plane.send(int(hdr["dst"]), t, cid)
+            if t is None:
+                # the requester has posted its receive: keep the pair's FIFO in step with a
+                # placeholder of the announced shape (that requester re-submits the chunk)
+                self.metrics.incr("p2p_placeholder_results")
+                t = torch.zeros(tuple(hdr.get("cshape") or (0,)), dtype=torch.uint8)
+            plane.send(int(hdr["dst"]), t, cid)
         elif cmd == "recv_result":  # requester: annotated chunk from worker `src`
             key, msg = hdr.get("key"), hdr["msg"]
 
             def done(buf, key=key, msg=msg):
                 if isinstance(buf, BaseException):
+                    # the annotated chunk was lost on the way back (the worker is done with it):
+                    # submit the frames again as a new chunk; they are still held under `key`
                     self.metrics.incr("p2p_recv_failed")
+                    self._resubmit(key, msg)
                     return
                 if key is not None:
                     with self._p2p_lock:
@@ -373,6 +383,18 @@ class client:  # noqa: N801 (reference class name)
         elif cmd == "drop":  # a duplicate result of a re-dispatched chunk: nobody wants it
             with self._p2p_lock:
                 self._results.pop(cid, None)
+
+    def _resubmit(self, key, msg):
+        if key is None:
+            return
+        with self._p2p_lock:
+            t = self._outgoing.get(int(key))
+        if t is None:
+            return
+        parts = msg.split("||")
+        info = f"{self.my_ip}||request||{parts[2]}||{t.shape[1]}||{t.shape[2]}"
+        self.metrics.incr("p2p_resubmitted")
+        self.sender.send_image(info, _EMPTY, p2p=1, key=int(key), cshape=list(t.shape))
 
     # ------------------------------------------------------------------ worker role
     def worker(self):

@@ -104,10 +104,14 @@ void gemm_nt(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
   TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_nt: shape mismatch");
   TORCH_CHECK(vcx_gemm_nt_supported((int)M, (int)N, (int)K), "gemm_nt: needs M % 256 == 0, N % 256 == 0, K % 64 == 0, K >= 128");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm_nt: 16-B aligned rows");
+  // the kernel moves 16 B per lane: a column-offset view (e.g. c[:, 4:260]) would be misaligned
+  for (const at::Tensor* t : {&a, &b, &c})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_nt: 16-B aligned base pointers");
   void* c2p = nullptr;
   if (epi >= 2) {
     TORCH_CHECK(c2 && c2->sizes() == c.sizes() && c2->strides() == c.strides() && c2->scalar_type() == at::kBFloat16,
                 "gemm_nt: epilogue 2/3 needs c2 like c");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(c2->data_ptr()) % 16 == 0, "gemm_nt: 16-B aligned c2");
     c2p = c2->data_ptr();
   }
   const void* bp = nullptr;
@@ -171,6 +175,22 @@ void gemm_p(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor> 
              (int)b.stride(0), (int)c.stride(0), (int)epi, (int)layout, cur_stream());
 }
 
+// 4-wave one-wave-per-SIMD GEMM (gemm4.hip): c[M, N] = a[M, K] . b[N, K]^T
+void gemm4(at::Tensor a, at::Tensor b, at::Tensor c) {
+  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm4: 2-D cuda tensors");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
+              "gemm4: bf16 operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm4: K-contiguous rows");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm4: shape mismatch");
+  TORCH_CHECK(vcx_gemm4_supported((int)M, (int)N, (int)K), "gemm4: needs M, N % 256 == 0, K % 64 == 0, K >= 128");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm4: 16-B aligned rows");
+  for (const at::Tensor* t : {&a, &b, &c})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm4: 16-B aligned base pointers");
+  vcx_gemm4(a.data_ptr(), b.data_ptr(), c.data_ptr(), (int)M, (int)N, (int)K, (int)a.stride(0), (int)b.stride(0),
+            (int)c.stride(0), cur_stream());
+}
+
 // Weight gradient out[M, N] (+)= a[K, M]^T . b[K, N] (token-major operands) on the hand-written
 // transposed-read MFMA kernel, split-K over the token axis with fp32 partials
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t splits) {
@@ -187,6 +207,8 @@ void gemm_tn(at::Tensor a, at::Tensor b, at::Tensor out, int64_t splits, bool ac
   TORCH_CHECK(vcx_gemm_tn_supported((int)M, (int)N, (int)K, (int)splits),
               "gemm_tn: needs M % 256 == 0, N % 256 == 0, K % 64 == 0, K / 128 >= splits");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_tn: 16-B aligned rows");
+  for (const at::Tensor* t : {&a, &b, &out})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_tn: 16-B aligned base pointers");
   at::Tensor ws = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
   vcx_gemm_tn(a.data_ptr(), b.data_ptr(), ws.data_ptr<float>(), out.data_ptr(), (int)M, (int)N, (int)K,
               (int)a.stride(0), (int)b.stride(0), (int)splits, accumulate ? 1 : 0, cur_stream());
@@ -645,6 +667,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("reduce_bcast_bf16", &reduce_bcast_bf16);
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_p_supported", &gemm_p_supported);
+  m.def("gemm4", &gemm4);
   m.def("gemm_p", &gemm_p, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("layout") = 0);
   m.def("gemm_tn_supported", &gemm_tn_supported);

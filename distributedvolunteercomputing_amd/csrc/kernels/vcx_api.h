@@ -24,6 +24,9 @@ void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bi
 bool vcx_gemm_p_supported(int M, int N, int K, int layout);
 void vcx_gemm_p(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,
                 int lda, int ldb, int ldc, int epi, int layout, hipStream_t s);
+// gemm4.hip: 4-wave one-wave-per-SIMD GEMM (main-loop study), C = A B^T
+bool vcx_gemm4_supported(int M, int N, int K);
+void vcx_gemm4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, hipStream_t s);
 void vcx_transpose_bf16(const void* src, void* dst, int R, int Cc, hipStream_t s);
 void vcx_add_f32_into_bf16(const float* in, void* out, int n, int accumulate, hipStream_t s);
 void vcx_reduce_bcast_bf16(const void* in, void* out, void* mine, int P, int64_t n, hipStream_t s);

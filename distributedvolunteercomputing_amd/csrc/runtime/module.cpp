@@ -115,6 +115,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("requeued", &ChunkScheduler::requeued)
       .def("next", &ChunkScheduler::next)
       .def("complete", &ChunkScheduler::complete)
+      .def("fail", &ChunkScheduler::fail)
       .def("cancel_requester", &ChunkScheduler::cancel_requester)
       .def("queued", &ChunkScheduler::queued)
       .def("inflight", &ChunkScheduler::inflight)

@@ -146,6 +146,18 @@ bool ChunkScheduler::complete(int64_t chunk) {
   return true;
 }
 
+bool ChunkScheduler::fail(int64_t chunk, const std::string& worker) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto o = owner_.find(chunk);
+  if (o == owner_.end() || o->second.first != worker) return false;
+  auto w = ws_.find(worker);
+  if (w != ws_.end()) w->second.inflight.erase(chunk);
+  q_.push_front(Pending{chunk, o->second.second});
+  owner_.erase(o);
+  ++requeued_;
+  return true;
+}
+
 std::vector<int64_t> ChunkScheduler::cancel_requester(const std::string& requester) {
   std::lock_guard<std::mutex> g(mu_);
   std::vector<int64_t> dropped;

@@ -53,6 +53,9 @@ class ChunkScheduler {
   void requeue_front(int64_t chunk, const std::string& requester);
   Assignment next();  // invalid Assignment when nothing is dispatchable
   bool complete(int64_t chunk);  // returns false for an unknown / duplicate completion
+  // The transfer of `chunk` to `worker` failed (p2p plane): if it is still in flight there, take
+  // it back and re-queue it at the front. Returns false when the chunk is not w's any more.
+  bool fail(int64_t chunk, const std::string& worker);
   std::vector<int64_t> cancel_requester(const std::string& requester);  // drop (and return) its queued chunks
 
   size_t queued();

@@ -217,12 +217,18 @@ def main(argv=None):
             from ..parallel.peer_group import PeerFailure
             from ..utils.checkpoint import save_checkpoint
 
+            import contextlib
+
             g = tr.group
             try:
-                save_checkpoint(tr, a.ckpt_dir, step, peer_id=rank, is_writer=(g is None or g.rank == 0),
-                                members=(g.members if g is not None else [rank]),
-                                generation=(membership.gen if membership else 0), model_config=mcfg,
-                                barrier=(g.barrier if g is not None else None))
+                # guarded like every other collective phase: a peer dying inside the checkpoint's
+                # reduce-scatters / barrier aborts it within one lease (or at once through its
+                # liveness link) instead of after the process-group timeout
+                with (membership.guard("c") if membership is not None else contextlib.nullcontext()):
+                    save_checkpoint(tr, a.ckpt_dir, step, peer_id=rank, is_writer=(g is None or g.rank == 0),
+                                    members=(g.members if g is not None else [rank]),
+                                    generation=(membership.gen if membership else 0), model_config=mcfg,
+                                    barrier=(g.barrier if g is not None else None))
             except PeerFailure as e:  # a peer died mid-checkpoint: skip it, the next round regroups
                 print(f"[peer {rank}] checkpoint at step {step} skipped: {e}", flush=True)
         if step % a.log_every == 0 or step == a.steps:

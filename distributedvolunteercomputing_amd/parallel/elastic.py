@@ -196,6 +196,7 @@ class ElasticMembership:
         self.failures = 0
         self.events: list[dict] = []  # membership change log (for metrics / tests)
         self._hb_stop = threading.Event()
+        self._wake = threading.Event()
         self._hb_thread = None
         self._lock = threading.RLock()
         self._armed = False
@@ -223,7 +224,13 @@ class ElasticMembership:
 
         def loop():
             key = f"{_P}hb/{self.pid}"
-            while not self._hb_stop.wait(self.heartbeat_s):
+            while True:
+                # a liveness EOF wakes this thread at once (the watchdog acts on it here, on the
+                # one thread that has always owned aborts), otherwise one tick per heartbeat_s
+                self._wake.wait(self.heartbeat_s)
+                self._wake.clear()
+                if self._hb_stop.is_set():
+                    break
                 try:
                     self.store.add(key, 1)
                 except Exception:  # noqa: BLE001 — the store is gone: nothing left to do
@@ -248,6 +255,7 @@ class ElasticMembership:
 
     def stop_heartbeat(self):
         self._hb_stop.set()
+        self._wake.set()
         if self._hb_thread is not None:
             self._hb_thread.join(timeout=2)
         self._hb_thread = None
@@ -261,10 +269,8 @@ class ElasticMembership:
         with self._lock:
             self._eof[m] = addr
             self.eof_events.append((m, now))
-            armed = self._armed and m in self.members and not self._abort.is_set()
         _dbg(self.pid, f"liveness EOF from peer {m} ({addr})")
-        if armed:
-            self.declare_abort(f"peer {m} process gone (liveness EOF) inside a collective of gen {self.gen}")
+        self._wake.set()  # the watchdog (heartbeat thread) aborts a collective in flight right away
 
     def _gone(self, m: int) -> bool:
         """Did the connection to member m's CURRENT incarnation close (a restarted peer publishes
@@ -288,8 +294,8 @@ class ElasticMembership:
         for m in list(self.members):
             if m == self.pid:
                 continue
-            if m in self._eof and self._gone(m):  # died between the round's outcome and this guard
-                self.declare_abort(f"peer {m} process gone (liveness EOF) before a collective of gen {g}")
+            if m in self._eof and self._gone(m):  # its liveness link closed: the process is gone
+                self.declare_abort(f"peer {m} process gone (liveness EOF) during a collective of gen {g}")
                 return
             hb = self._hb(m)
             last = self._watch_seen.get(m)

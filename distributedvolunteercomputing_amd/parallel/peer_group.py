@@ -76,6 +76,7 @@ class PeerGroup:
         self.device = device
         self.watch = watch  # ElasticMembership (or None: plain blocking collectives)
         self.aborted = False
+        self._abort_lock = threading.Lock()  # abort() may race between the watchdog and the waiter
         self.fault_hook = None  # test hook: called inside every guarded collective (after issue)
         self.poll_s = 2e-4
         self._pending = None  # deferred gloo rendezvous (watched groups connect in connect())
@@ -109,6 +110,7 @@ class PeerGroup:
         self.device = device
         self.watch = None
         self.aborted = False
+        self._abort_lock = threading.Lock()
         self.fault_hook = None
         self.poll_s = 2e-4
         self.pg = dist.distributed_c10d._get_default_group() if self.size > 1 else None
@@ -226,10 +228,11 @@ class PeerGroup:
         heartbeat thread (a silent survivor looks dead to everyone else) nor the recovering
         main thread may wait for that. The next generation uses a new communicator and new
         streams, so nothing queues behind the aborted kernels."""
-        if self.aborted:
-            return
-        self.aborted = True
-        pg, self.pg = self.pg, None
+        with self._abort_lock:  # exactly one caller tears the communicator down
+            if self.aborted:
+                return
+            self.aborted = True
+            pg, self.pg = self.pg, None
         if pg is None:
             return
         if self.backend == "nccl":

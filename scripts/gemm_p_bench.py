@@ -91,7 +91,39 @@ def timeit(fns, rounds=5, it=10):
     return [sorted(r)[len(r) // 2] for r in res]
 
 
+def check4():
+    for (m, n, k) in [(256, 256, 128), (512, 768, 256), (2048, 3072, 768), (4096, 2304, 768)]:
+        a = torch.randn(m, k, device=dev, dtype=bf)
+        b = torch.randn(n, k, device=dev, dtype=bf) * 0.05
+        c = torch.empty(m, n, device=dev, dtype=bf)
+        C.gemm4(a, b, c)
+        torch.cuda.synchronize()
+        ref = a.float() @ b.float().t()
+        err = (c.float() - ref).abs().max().item()
+        assert err < 2e-2 * ref.abs().max().item(), (m, n, k, "gemm4", err)
+        print(f"ok  gemm4 M={m} N={n} K={k}", flush=True)
+
+
 def main():
+    check4()
+    if "--gemm4" in sys.argv:
+        for name, n, k in [("qkv", 2304, 768), ("proj", 768, 768), ("fc", 3072, 768), ("fc2", 768, 3072)]:
+            a = torch.randn(M, k, device=dev, dtype=bf)
+            b = torch.randn(n, k, device=dev, dtype=bf) * 0.02
+            c = torch.empty(M, n, device=dev, dtype=bf)
+            fl = 2.0 * M * n * k
+            t_lib, t_nt, t_4 = timeit([lambda: F.linear(a, b), lambda: C.gemm_nt(a, b, c), lambda: C.gemm4(a, b, c)])
+            print(f"{name:7s} N={n:5d} K={k:5d}  library {t_lib:7.1f} us ({fl / t_lib / 1e6:5.0f} TF)  gemm_nt {t_nt:7.1f} "
+                  f"({fl / t_nt / 1e6:5.0f})  gemm4 {t_4:7.1f} ({fl / t_4 / 1e6:5.0f} TF)", flush=True)
+        for n in (4096, 8192):
+            a = torch.rand(n, n, device=dev, dtype=bf) * 2 - 1
+            b = torch.rand(n, n, device=dev, dtype=bf) * 2 - 1
+            c = torch.empty(n, n, device=dev, dtype=bf)
+            fl = 2.0 * n ** 3
+            t_lib, t_nt, t_4 = timeit([lambda: F.linear(a, b), lambda: C.gemm_nt(a, b, c), lambda: C.gemm4(a, b, c)])
+            print(f"{n}^3  library {fl / t_lib / 1e6:5.0f} TF  gemm_nt {fl / t_nt / 1e6:5.0f} TF  gemm4 {fl / t_4 / 1e6:5.0f} TF",
+                  flush=True)
+        return
     check()
     quick = "--quick" in sys.argv
     shapes = [("qkv", 2304, 768), ("proj", 768, 768), ("fc", 3072, 768), ("fc2", 768, 3072)]

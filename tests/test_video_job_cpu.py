@@ -248,3 +248,28 @@ def test_streaming_transport_mode(tmp_path):
         req.exit_threads()
         w.exit_threads()
         c.exit_threads()
+
+
+def test_p2p_transfer_failure_between_live_volunteers_is_redispatched(tmp_path):
+    """on the p2p plane a transfer that fails between two LIVE volunteers must not lose
+    its chunk. The worker's first receive fails like a broken transport; it reports the chunk back
+    (`failed`), the coordinator re-queues it at the front, both ends rebuild the pair under a new
+    generation, and the job completes with every frame in order."""
+    c = coordinator("127.0.0.1", 0, ephemeral_ports=True, lease_s=5.0, data_plane="p2p")
+    req = _client(c, tmp_path, PassthroughEngine(), chunk=30)
+    w = _client(c, tmp_path, PassthroughEngine(), chunk=30)
+    try:
+        assert w.plane is not None
+        w.plane.inject_failures = 1
+        req.preresize = False
+        req.become_requester("synthetic:90:32x24")
+        assert req.wait_job(timeout=90) is not None, "job must complete despite the failed transfer"
+        out = np.load(req.path_out)
+        assert [decode_frame_index(f) for f in out] == list(range(90))
+        assert w.metrics.counters.get("p2p_recv_failed", 0) == 1
+        assert c.metrics.counters.get("p2p_failed_requeued", 0) == 1
+        assert w.plane.inject_failures == 0
+    finally:
+        req.exit_threads()
+        w.exit_threads()
+        c.exit_threads()
