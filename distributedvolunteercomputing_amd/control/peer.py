@@ -47,6 +47,16 @@ from .transport import FrameHub, FrameSender
 _EMPTY = np.zeros(0, dtype=np.uint8)
 
 
+def _host_tensor(a: np.ndarray) -> torch.Tensor:
+    """A tensor view of a host chunk; read-only arrays (memory-mapped sources) are only ever read
+    by the transfers, so torch's non-writable warning does not apply."""
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", UserWarning)
+        return torch.from_numpy(a)
+
+
 class client:  # noqa: N801 (reference class name)
     verbose = False
     req_rep = True
@@ -178,7 +188,15 @@ class client:  # noqa: N801 (reference class name)
         self.sink = OrderedSink(lambda w, h: open_sink(out_path, w, h, 30), on_done=done)
         self.start_time = time.time()
         n = 0
+        C = self.number_of_frames_in_chunk
         while self.continue_requesting:
+            if src.chunked:  # whole chunks straight from the source (memory-mapped file: no copy here)
+                arr = src.read_chunk(C)
+                if len(arr) == 0:
+                    break
+                self.send_q.put(("chunk", (n + 1, arr)))
+                n += len(arr)
+                continue
             ok, frame = src.read()
             if not ok:
                 break
@@ -218,18 +236,19 @@ class client:  # noqa: N801 (reference class name)
         frames, nums = [], []
         C = self.number_of_frames_in_chunk
 
-        def flush():
-            if not frames:
+        def flush(block=None):
+            if block is None and not frames:
                 return
-            if self.preresize and self.resize_device is not None and frames[0].shape[1] != 400:
-                chunk = self._resize_chunk(frames)
+            first = frames[0] if block is None else block[0]
+            if self.preresize and self.resize_device is not None and first.shape[1] != 400:
+                chunk = self._resize_chunk(frames if block is None else block)
             else:
-                chunk = np.stack(frames)
+                chunk = np.stack(frames) if block is None else np.ascontiguousarray(block)
             info = f"{self.my_ip}||request||{'-'.join(map(str, nums))}||{chunk.shape[1]}||{chunk.shape[2]}"
             if self.plane is not None:  # p2p: the chunk stays here; the coordinator gets its metadata
                 key = next(self._keys)
                 with self._p2p_lock:
-                    self._outgoing[key] = chunk if isinstance(chunk, torch.Tensor) else torch.from_numpy(chunk)
+                    self._outgoing[key] = chunk if isinstance(chunk, torch.Tensor) else _host_tensor(chunk)
                 ok = self.sender.send_image(info, _EMPTY, p2p=1, key=key, cshape=list(chunk.shape))
             else:
                 ok = self.sender.send_image(info, chunk)
@@ -247,6 +266,12 @@ class client:  # noqa: N801 (reference class name)
             n, f = item
             if n == "flush":
                 flush()
+                continue
+            if n == "chunk":  # a whole chunk from a chunked source: frames first..first+k-1
+                flush()
+                first, block = f
+                nums.extend(range(first, first + len(block)))
+                flush(block)
                 continue
             if frames and f.shape != frames[0].shape:
                 flush()  # a chunk holds frames of one size only
@@ -270,9 +295,12 @@ class client:  # noqa: N801 (reference class name)
         dev = self.resize_device
         if self._h2d_done is not None:
             self._h2d_done.synchronize()  # the previous chunk's upload has left the pinned buffer
-        pin = self._pinned("in", (len(frames),) + frames[0].shape)
-        for i, f in enumerate(frames):
-            pin[i].copy_(torch.from_numpy(f))
+        pin = self._pinned("in", (len(frames),) + tuple(frames[0].shape))
+        if isinstance(frames, np.ndarray):  # one block (e.g. a memory-mapped chunk): one threaded copy
+            pin.copy_(_host_tensor(frames))
+        else:
+            for i, f in enumerate(frames):
+                pin[i].copy_(torch.from_numpy(f))
         x = pin.to(dev, non_blocking=True)
         self._h2d_done = torch.cuda.Event()
         self._h2d_done.record(torch.cuda.current_stream(dev))
@@ -398,9 +426,11 @@ class client:  # noqa: N801 (reference class name)
 
     # ------------------------------------------------------------------ worker role
     def worker(self):
-        """Worker role, two chunks deep: chunk k+1 is submitted to the engine (its host copy and
-        H2D start at once) before chunk k's result is collected and sent, so the upload of one
-        chunk overlaps the network of the previous one (DetectorEngine.submit)."""
+        """Worker role, two chunks deep on both planes: chunk k+1 is submitted to the engine
+        before chunk k's result is collected and sent. Host chunks: k+1's host copy and H2D
+        overlap k's network (DetectorEngine.submit). Device-resident chunks of the RCCL pair
+        plane: k+1's compute is enqueued behind its receive while k's result is posted and sent,
+        so receive k+1 ∥ infer k ∥ send k-1 (DetectorEngine.submit_tensor)."""
         pending = None
         while self.continue_procesing:
             try:
@@ -409,11 +439,10 @@ class client:  # noqa: N801 (reference class name)
                 item = None
             if item is not None:
                 hdr, arr, requester, nums = item
-                if hdr.get("p2p") and arr.device.type != "cpu":  # device-resident in and out
-                    self._finish_p2p(hdr, arr, requester, nums)
-                    continue
-                job = self._get_engine().submit(arr, requester)
-                nxt = (job, hdr, requester, nums, time.perf_counter())
+                dev_res = bool(hdr.get("p2p")) and arr.device.type != "cpu"
+                eng = self._get_engine()
+                job = eng.submit_tensor(arr, requester) if dev_res else eng.submit(arr, requester)
+                nxt = (job, hdr, requester, nums, time.perf_counter(), dev_res)
             else:
                 nxt = None
             if pending is not None and (nxt is not None or self.work_q.empty()):
@@ -423,7 +452,15 @@ class client:  # noqa: N801 (reference class name)
         if pending is not None:
             self._finish(*pending)
 
-    def _finish(self, job, hdr, requester, nums, t0):
+    def _finish(self, job, hdr, requester, nums, t0, dev_res=False):
+        if dev_res:  # annotated chunk on the device: held for the pair send to the requester
+            out = job.result()
+            if out.device != self.plane.device:
+                out = out.to(self.plane.device)
+            self.metrics.observe("chunk_infer_ms", (time.perf_counter() - t0) * 1e3)
+            self.metrics.incr("frames_processed", len(nums))
+            self._post_result(hdr, out, requester, nums)
+            return
         out, counts = job.result()
         self.metrics.observe("chunk_infer_ms", (time.perf_counter() - t0) * 1e3)
         self.metrics.incr("frames_processed", len(nums))
@@ -432,15 +469,6 @@ class client:  # noqa: N801 (reference class name)
             return
         info = f"{requester}||processed||{'-'.join(map(str, nums))}||{out.shape[1]}||{out.shape[2]}"
         self.sender.send_image(info, out, chunk=hdr.get("chunk", -1))
-
-    def _finish_p2p(self, hdr, t, requester, nums):
-        t0 = time.perf_counter()
-        out = self._get_engine().process_tensor(t, requester)
-        if out.device != self.plane.device:
-            out = out.to(self.plane.device)
-        self.metrics.observe("chunk_infer_ms", (time.perf_counter() - t0) * 1e3)
-        self.metrics.incr("frames_processed", len(nums))
-        self._post_result(hdr, out, requester, nums)
 
     def _post_result(self, hdr, out, requester, nums):
         """Hold the annotated chunk until the coordinator names its destination; report it."""

@@ -81,9 +81,21 @@ def _yuv444_to_bgr_np(yuv: np.ndarray) -> np.ndarray:
 
 # ----------------------------------------------------------------------------- sources
 class FrameSource:
+    chunked = False  # True: read_chunk() hands out many frames at once without a per-frame copy
+
     def read(self):
         """Returns (ok, frame) like cv2.VideoCapture.read()."""
         raise NotImplementedError
+
+    def read_chunk(self, n: int):
+        """Up to n frames as one [k, H, W, 3] array (k = 0 at the end)."""
+        frames = []
+        for _ in range(n):
+            ok, f = self.read()
+            if not ok:
+                break
+            frames.append(f)
+        return np.stack(frames) if frames else np.zeros((0, 0, 0, 3), np.uint8)
 
     def release(self):
         pass
@@ -150,6 +162,11 @@ class SyntheticSource(FrameSource):
 
 
 class NpySource(FrameSource):
+    """Frames of a uint8 [N, H, W, 3] .npy file, memory-mapped: read_chunk() returns views into
+    the mapping (no copy here; the consumer's one copy goes straight into pinned memory)."""
+
+    chunked = True
+
     def __init__(self, path):
         self.a = np.load(path, mmap_mode="r", allow_pickle=False)
         if self.a.ndim != 4 or self.a.shape[-1] != 3 or self.a.dtype != np.uint8:
@@ -162,6 +179,11 @@ class NpySource(FrameSource):
         f = np.ascontiguousarray(self.a[self.i])
         self.i += 1
         return True, f
+
+    def read_chunk(self, n: int):
+        v = self.a[self.i : self.i + n]
+        self.i += len(v)
+        return v
 
 
 class ImageDirSource(FrameSource):

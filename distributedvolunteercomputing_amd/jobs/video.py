@@ -45,6 +45,31 @@ class Engine:
         job.result = lambda: res
         return job
 
+    def submit_tensor(self, frames: torch.Tensor, requester: str):
+        """Device-resident variant of ``submit``: ``result()`` gives the annotated chunk as a
+        tensor on the same device. Engines without an asynchronous pipeline compute here."""
+        out = self.process_tensor(frames, requester)
+        return _DoneJob(out)
+
+
+class _DoneJob:
+    def __init__(self, out):
+        self.out = out
+
+    def result(self):
+        return self.out
+
+
+class _TensorJob:
+    """A device-resident chunk in flight on the engine's compute stream."""
+
+    def __init__(self, out, event):
+        self.out, self.event = out, event
+
+    def result(self):
+        self.event.synchronize()
+        return self.out
+
 
 class _Slot:
     """Pinned host staging for one in-flight chunk (input frames / annotated output)."""
@@ -158,6 +183,24 @@ class DetectorEngine(Engine):
                 out, _ = self._compute(frames.to(self.device), requester)
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
             return out
+
+    @torch.no_grad()
+    def submit_tensor(self, frames, requester):
+        """Device-resident chunk in, annotated chunk out, asynchronously: the compute is enqueued on
+        the engine's stream behind the producer of `frames` and the job's result() waits on an
+        event, so a worker can receive chunk k+1 while chunk k computes and chunk k-1 is sent."""
+        with self._lock:
+            if self.stream is None:
+                out, _ = self._run(frames, requester)
+                return _DoneJob(out)
+            x = frames.to(self.device)
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.stream):
+                out, _ = self._compute(x, requester)
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+            x.record_stream(self.stream)
+            return _TensorJob(out, ev)
 
     def _run(self, frames, requester):  # CPU path / reference
         x = frames if isinstance(frames, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frames))

@@ -118,6 +118,7 @@ class SSDExecutor:
         self.device = torch.device(device)
         self.input_size = int(net.input_shapes[0][2]) if net.input_shapes else 300
         self._prior_cache = {}
+        self.step_events = None
         self._plan = self._compile() if self.device.type == "cuda" else None
 
     # ------------------------------------------------------------------ compile
@@ -295,7 +296,12 @@ class SSDExecutor:
         assert blob.shape[1] == self.input_size, "the plan's head offsets are for the prototxt input size"
         concat_bufs = {ci: torch.empty(N, tot, device=blob.device, dtype=torch.bfloat16)
                        for ci, tot in self._concat_total.items()}
+        marks = self.step_events  # optional per-step timing: list of (layer name, kind, event)
         for kind, l, p in self._plan:
+            if marks is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                marks.append((l.name, kind, ev))
             src = l.bottoms[0] if l.bottoms else None
             x = t.get(src)
             top = l.tops[0] if l.tops else None
@@ -353,7 +359,26 @@ class SSDExecutor:
                                          top_k=int(l.sub("detection_output_param", "nms_param", "top_k", 100)),
                                          keep_top_k=int(dp("keep_top_k", 100)))
                 t[top] = (dets, cnt)
+        if marks is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            marks.append(("<end>", "", ev))
         return t
+
+    def step_times(self, blob: torch.Tensor, iters: int = 10) -> list:
+        """Per plan step GPU time (ms, mean over `iters` passes): [(layer, kind, ms)]. Steps that
+        launch nothing (relu folded, concat views, priors cached) show ~0."""
+        self.forward_blob(blob)
+        acc = None
+        for _ in range(iters):
+            self.step_events = []
+            self.forward_blob(blob)
+            torch.cuda.synchronize()
+            ev = self.step_events
+            ms = [(a[0], a[1], a[2].elapsed_time(b[2])) for a, b in zip(ev, ev[1:])]
+            acc = ms if acc is None else [(n, k, s + m[2]) for (n, k, s), m in zip(acc, ms)]
+        self.step_events = None
+        return [(n, k, s / iters) for n, k, s in acc]
 
     def detect(self, frames_u8: torch.Tensor):
         """frames [N, H, W, 3] uint8 BGR (already at the annotation size) -> (dets, counts)."""

@@ -273,3 +273,25 @@ def test_p2p_transfer_failure_between_live_volunteers_is_redispatched(tmp_path):
         req.exit_threads()
         w.exit_threads()
         c.exit_threads()
+
+
+def test_memory_mapped_npy_source_sends_whole_chunks(coord, tmp_path):
+    """A .npy video is read as memory-mapped chunks (one copy per chunk, no per-frame copy); the
+    tail chunk, the frame numbering and the in-order output are unchanged."""
+    from distributedvolunteercomputing_amd.io.video import synthetic_frame
+
+    src = tmp_path / "in.npy"
+    np.save(src, np.stack([synthetic_frame(i, 64, 48) for i in range(230)]))
+    req = _client(coord, tmp_path, PassthroughEngine())
+    w = _client(coord, tmp_path, PassthroughEngine())
+    try:
+        req.preresize = False
+        req.become_requester(str(src))
+        assert req.wait_job(timeout=60) is not None
+        out = np.load(req.path_out)
+        assert out.shape == (230, 48, 64, 3)
+        assert [decode_frame_index(f) for f in out] == list(range(230))
+        assert req.metrics.counters.get("chunks_sent", 0) == 3
+    finally:
+        req.exit_threads()
+        w.exit_threads()

@@ -154,3 +154,26 @@ def test_executor_matches_caffe_reference(gpu):
         assert rel < 0.05, (name, float(rel))
     dets, cnt = out["detection_out"]
     assert dets.shape == (2, 100, 7) and cnt.shape == (2,)
+    # detection_out values: the executor's DetectionOutput (fused softmax + decode + NMS kernel)
+    # against the fp32 Caffe DetectionOutput on the executor's own mbox tensors, then the same with
+    # the logits sharpened x6 so that the random-weight net yields many boxes above the threshold.
+    loc, conf, pri = out["mbox_loc"], out["mbox_conf"], out["mbox_priorbox"]
+    P = pri.shape[-1] // 4
+    for scale in (1.0, 6.0):
+        c = (conf.float() * scale).to(conf.dtype)
+        if scale == 1.0:
+            d, k = dets, cnt
+        else:
+            d, k = V.ssd_detect(c.reshape(2, P * 21), loc.reshape(2, P * 4), pri[0, 0], pri[0, 1])
+            assert int(k.sum()) >= 20, k  # the sharpened case must exercise decode + NMS
+        prob = torch.softmax(c.float().cpu().view(2, P, 21), -1).view(2, -1)
+        ref_d = detection_output(loc.float().cpu().reshape(2, -1), prob, pri[0, 0].float().cpu(),
+                                 pri[0, 1].float().cpu(), conf_thresh=0.25)
+        for n in range(2):
+            kk = int(k[n])
+            assert kk == min(len(ref_d[n]), 100), (scale, n, kk, len(ref_d[n]))
+            gs = sorted(d[n, :kk].cpu().tolist(), key=lambda z: (-z[2], z[1]))
+            rs = sorted(ref_d[n][:kk].tolist(), key=lambda z: (-z[2], z[1]))
+            for a, b in zip(gs, rs):
+                assert a[1] == b[1] and abs(a[2] - b[2]) < 2e-3, (a, b)
+                assert max(abs(x - y) for x, y in zip(a[3:], b[3:])) < 2e-3, (a, b)
