@@ -61,7 +61,10 @@ at::Tensor dwconv3x3(at::Tensor x, at::Tensor w, at::Tensor b, int64_t stride, b
   CHK(b, at::kFloat);
   TORCH_CHECK(x.dim() == 4);
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  TORCH_CHECK(C % 8 == 0 && w.numel() == 9 * C && b.numel() == C && (stride == 1 || stride == 2));
+  TORCH_CHECK(C % 8 == 0 && w.numel() == 10 * C && b.numel() == C && (stride == 1 || stride == 2),
+              "dwconv3x3: paired weights [5, C, 2] (ops/vision.py dw_pair_weights)");
+  TORCH_CHECK(((uintptr_t)x.data_ptr() & 15) == 0 && ((uintptr_t)w.data_ptr() & 15) == 0 &&
+              ((uintptr_t)b.data_ptr() & 15) == 0, "dwconv3x3: 16-B aligned operands");
   const int64_t Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   auto y = at::empty({N, Ho, Wo, C}, x.options());
   vcx_dwconv3x3(x.data_ptr(), w.data_ptr(), b.data_ptr<float>(), y.data_ptr(), (int)N, (int)H, (int)W, (int)C,
@@ -85,6 +88,33 @@ at::Tensor gemm_bias_act(at::Tensor X, at::Tensor Wt, c10::optional<at::Tensor> 
   auto Y = at::empty({M, N}, X.options());
   vcx_gemm_bias_act(X.data_ptr(), Wt.data_ptr(), bp, Y.data_ptr(), (int)M, (int)N, (int)K, (int)N, relu ? 1 : 0,
                     cur_stream());
+  return Y;
+}
+
+// MobileNet block in one kernel: depthwise 3x3 (pad 1, stride 1|2) + bias (+ReLU), then the
+// pointwise GEMM + bias (+ReLU); the depthwise activation stays on chip.
+at::Tensor dw_pw(at::Tensor x, at::Tensor dw_w, at::Tensor dw_b, bool dw_relu, int64_t stride, at::Tensor Wt,
+                 at::Tensor bias, bool relu) {
+  CHK(x, at::kBFloat16);
+  CHK(dw_w, at::kBFloat16);
+  CHK(dw_b, at::kFloat);
+  CHK(Wt, at::kBFloat16);
+  CHK(bias, at::kFloat);
+  TORCH_CHECK(x.dim() == 4 && Wt.dim() == 2, "x NHWC, Wt [N, K]");
+  const int64_t imgs = x.size(0), H = x.size(1), W = x.size(2), K = x.size(3), N = Wt.size(0);
+  TORCH_CHECK(K % 32 == 0 && K <= 1024 && Wt.size(1) == K && dw_w.numel() == 10 * K && dw_b.numel() == K &&
+                  bias.numel() == N,
+              "dw_pw: K % 32 == 0, K <= 1024, paired dw_w [5, K, 2], dw_b [K], Wt [N, K], bias [N]");
+  TORCH_CHECK(stride == 1 || stride == 2);
+  TORCH_CHECK(((uintptr_t)x.data_ptr() & 15) == 0 && ((uintptr_t)dw_w.data_ptr() & 15) == 0 &&
+              ((uintptr_t)dw_b.data_ptr() & 15) == 0 && ((uintptr_t)Wt.data_ptr() & 15) == 0,
+              "dw_pw: 16-B aligned operands");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  TORCH_CHECK(imgs * Ho * Wo < INT32_MAX && imgs * H * W * K < ((int64_t)1 << 40));
+  auto Y = at::empty({imgs, Ho, Wo, N}, x.options());
+  vcx_dw_pw(x.data_ptr(), dw_w.data_ptr(), dw_b.data_ptr<float>(), dw_relu ? 1 : 0, Wt.data_ptr(),
+            bias.data_ptr<float>(), Y.data_ptr(), (int)imgs, (int)H, (int)W, (int)K, (int)stride, (int)N,
+            relu ? 1 : 0, cur_stream());
   return Y;
 }
 
@@ -188,6 +218,7 @@ void vcx_register_vision(pybind11::module& m) {
   m.def("dwconv3x3", &dwconv3x3);
   m.def("gemm_bias_act", &gemm_bias_act);
   m.def("gemm_bias_heads", &gemm_bias_heads);
+  m.def("dw_pw", &dw_pw);
   m.def("conv_implicit", &conv_implicit);
   m.def("ssd_detect", &ssd_detect);
   m.def("annotate", &annotate);

@@ -16,6 +16,8 @@ void vcx_gemm_bias_act_mapped(const void* X, const void* Wt, const float* bias, 
                               int64_t img_stride2, hipStream_t s);
 void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y, int imgs, int H, int W, int C,
                        int Cs, int KH, int KW, int stride, int pad, int N, int Kp, int relu, hipStream_t s);
+void vcx_dw_pw(const void* x, const void* dw_w, const float* dw_b, int dw_relu, const void* Wt, const float* bias,
+               void* Y, int imgs, int H, int W, int K, int stride, int N, int relu, hipStream_t s);
 void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
                        int relu, hipStream_t s);
 void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* prob,

@@ -56,6 +56,69 @@ __global__ void __launch_bounds__(256) resize_area_u8_kernel(const uint8_t* __re
   }
 }
 
+// (a') the same INTER_AREA as a row-band kernel: one workgroup per (image, output row) stages
+//      the input rows of its footprint in LDS with coalesced 16-B loads (every input byte is read
+//      from HBM once, plus the fractional rows two bands share) and each thread reduces the
+//      footprints of its output pixels from LDS, rows weighted by their vertical overlap.
+//      Requires (W*3) % 16 == 0 (1280/1920/640-wide video), w <= RA_XMAX*256 and one input row
+//      <= RA_LDS bytes; the launcher falls back to (a) otherwise.
+constexpr int RA_LDS = 24 * 1024, RA_XMAX = 4;
+__global__ void __launch_bounds__(256) resize_area_rows_kernel(const uint8_t* __restrict__ src,
+                                                                uint8_t* __restrict__ dst, int N, int H, int W, int h,
+                                                                int w) {
+  __shared__ __attribute__((aligned(16))) uint8_t rows[RA_LDS];
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x;
+  const int y = blockIdx.x % h, n = blockIdx.x / h;
+  const float sx = (float)W / w, sy = (float)H / h;
+  const float fy0 = y * sy, fy1 = fminf((y + 1) * sy, (float)H);
+  const int iy0 = (int)fy0, iy1 = min((int)ceilf(fy1), H);
+  const int rb = W * 3, rpp = RA_LDS / rb;
+  float acc[RA_XMAX][3];
+#pragma unroll
+  for (int j = 0; j < RA_XMAX; ++j) acc[j][0] = acc[j][1] = acc[j][2] = 0.f;
+  for (int r0 = iy0; r0 < iy1; r0 += rpp) {
+    const int nr = min(rpp, iy1 - r0);
+    __syncthreads();  // the previous pass has finished reading the band
+    const u32x4_t* g = (const u32x4_t*)(src + ((int64_t)n * H + r0) * rb);
+    for (int e = tid; e < nr * rb / 16; e += 256) ((u32x4_t*)rows)[e] = g[e];
+    __syncthreads();
+    for (int r = 0; r < nr; ++r) {
+      const float wy = fminf(fy1, (float)(r0 + r + 1)) - fmaxf(fy0, (float)(r0 + r));
+      if (wy <= 0.f) continue;
+      const uint8_t* row = rows + r * rb;
+#pragma unroll
+      for (int j = 0; j < RA_XMAX; ++j) {
+        const int x = tid + 256 * j;
+        if (x >= w) break;
+        const float fx0 = x * sx, fx1 = fminf((x + 1) * sx, (float)W);
+        float h0 = 0.f, h1 = 0.f, h2 = 0.f;
+        for (int xx = (int)fx0; xx < (int)ceilf(fx1) && xx < W; ++xx) {
+          const float wx = fminf(fx1, (float)(xx + 1)) - fmaxf(fx0, (float)xx);
+          if (wx <= 0.f) continue;
+          const uint8_t* p = row + xx * 3;
+          h0 = fmaf(wx, (float)p[0], h0);
+          h1 = fmaf(wx, (float)p[1], h1);
+          h2 = fmaf(wx, (float)p[2], h2);
+        }
+        acc[j][0] = fmaf(wy, h0, acc[j][0]);
+        acc[j][1] = fmaf(wy, h1, acc[j][1]);
+        acc[j][2] = fmaf(wy, h2, acc[j][2]);
+      }
+    }
+  }
+  uint8_t* q = dst + ((int64_t)n * h + y) * w * 3;
+#pragma unroll
+  for (int j = 0; j < RA_XMAX; ++j) {
+    const int x = tid + 256 * j;
+    if (x >= w) break;
+    const float fx0 = x * sx, fx1 = fminf((x + 1) * sx, (float)W);
+    const float inv = 1.f / ((fx1 - fx0) * (fy1 - fy0));
+#pragma unroll
+    for (int c = 0; c < 3; ++c) q[x * 3 + c] = (uint8_t)fminf(255.f, fmaxf(0.f, rintf(acc[j][c] * inv)));
+  }
+}
+
 // (b) bilinear (half-pixel centres, cv2.INTER_LINEAR) uint8 [N,H,W,3] -> uint8 [N,h,w,3]
 __global__ void __launch_bounds__(256) resize_bilinear_u8_kernel(const uint8_t* __restrict__ src,
                                                                   uint8_t* __restrict__ dst, int N, int H, int W,
@@ -129,12 +192,54 @@ __global__ void __launch_bounds__(256) im2col_nhwc_kernel(const bf16* __restrict
 
 // =====================================================================================
 // K5: depthwise 3x3 conv + bias + ReLU, NHWC bf16, stride 1|2, pad 1. 8 channels per lane.
-// w: [9][C] bf16 (tap-major so the 8 channels of one tap are one 16-B load), b: [C] fp32.
+// The 9-tap reduction runs on v_dot2_f32_bf16: taps (2p, 2p+1) of one channel are paired with
+// one v_perm_b32 and reduced with their paired weights in one dot2 (4 pairs + the 9th tap against
+// (w8, 0) / (0, w8)): 9 VALU ops per output instead of 9 FMAs plus 18 bf16->fp32 unpacks — the
+// fp32 version was VALU-bound (r2: 40.7 us per layer at 2.85 TB/s).
+// Paired weights wp: [5][C] dwords, wp[p][c] = (w[2p][c], w[2p+1][c]) for p < 4,
+// wp[4][c] = (w[8][c], 0) for even c and (0, w[8][c]) for odd c (ops/vision.py dw_pair_weights).
 // =====================================================================================
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float dot2bf(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2v, a), __builtin_bit_cast(bf16x2v, b), c, false);
+}
+
+// a[j] += sum_t x[t][j] * w[t][j] for the 8 channels of one lane; wp -> paired weights of the
+// first of those channels, ldw = dwords between pair rows (C)
+__device__ __forceinline__ void dw9_accum(const u32x4 (&x)[9], const uint32_t* wp, int ldw, float (&a)[8]) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const u32x4 w0 = *(const u32x4*)(wp + p * ldw), w1 = *(const u32x4*)(wp + p * ldw + 4);
+    const uint32_t w[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t lo = x[2 * p][q], hi = x[2 * p + 1][q];
+      a[2 * q] = dot2bf(__builtin_amdgcn_perm(hi, lo, 0x05040100u), w[2 * q], a[2 * q]);
+      a[2 * q + 1] = dot2bf(__builtin_amdgcn_perm(hi, lo, 0x07060302u), w[2 * q + 1], a[2 * q + 1]);
+    }
+  }
+  const u32x4 w0 = *(const u32x4*)(wp + 4 * ldw), w1 = *(const u32x4*)(wp + 4 * ldw + 4);
+  const uint32_t w[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    a[2 * q] = dot2bf(x[8][q], w[2 * q], a[2 * q]);
+    a[2 * q + 1] = dot2bf(x[8][q], w[2 * q + 1], a[2 * q + 1]);
+  }
+}
+
+__device__ __forceinline__ u32x4 dw_out8(const float (&a)[8], int relu) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16)(relu ? fmaxf(a[j], 0.f) : a[j]);
+  return __builtin_bit_cast(u32x4, o);
+}
+
 // (A 4-outputs-per-thread sliding-window variant halves the tap loads but strides the lanes
 // 4 pixels apart, and a 2-D grid without the grid-stride loop launches ~35k short blocks: both
 // measured 1.4x slower per network pass than this grid-stride kernel.)
-__global__ void __launch_bounds__(256) dwconv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+__global__ void __launch_bounds__(256) dwconv3x3_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ wp,
                                                          const float* __restrict__ b, bf16* __restrict__ y, int N,
                                                          int H, int W, int C, int Ho, int Wo, int stride, int relu) {
   const int C8 = C >> 3;
@@ -145,28 +250,20 @@ __global__ void __launch_bounds__(256) dwconv3x3_kernel(const bf16* __restrict__
     const int ox = (int)(p % Wo), oy = (int)((p / Wo) % Ho), n = (int)(p / ((int64_t)Wo * Ho));
     float acc[8];
     {
-      f32x4 b0 = *(const f32x4*)(b + c8 * 8), b1 = *(const f32x4*)(b + c8 * 8 + 4);
+      const f32x4 b0 = *(const f32x4*)(b + c8 * 8), b1 = *(const f32x4*)(b + c8 * 8 + 4);
       acc[0] = b0[0]; acc[1] = b0[1]; acc[2] = b0[2]; acc[3] = b0[3];
       acc[4] = b1[0]; acc[5] = b1[1]; acc[6] = b1[2]; acc[7] = b1[3];
     }
+    u32x4 xv[9];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const int iy = oy * stride - 1 + ky;
-      if (iy < 0 || iy >= H) continue;
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int ix = ox * stride - 1 + kx;
-        if (ix < 0 || ix >= W) continue;
-        bf16x8 xv = *(const bf16x8*)(x + (((int64_t)n * H + iy) * W + ix) * C + c8 * 8);
-        bf16x8 wv = *(const bf16x8*)(w + (ky * 3 + kx) * C + c8 * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] = fmaf((float)xv[j], (float)wv[j], acc[j]);
-      }
+    for (int t = 0; t < 9; ++t) {
+      const int iy = oy * stride - 1 + t / 3, ix = ox * stride - 1 + t % 3;
+      xv[t] = (iy >= 0 && iy < H && ix >= 0 && ix < W)
+                  ? *(const u32x4*)(x + (((int64_t)n * H + iy) * W + ix) * C + c8 * 8)
+                  : u32x4{0u, 0u, 0u, 0u};
     }
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (bf16)(relu ? fmaxf(acc[j], 0.f) : acc[j]);
-    *(bf16x8*)(y + p * C + c8 * 8) = o;
+    dw9_accum(xv, wp + c8 * 8, C, acc);
+    *(u32x4*)(y + p * C + c8 * 8) = dw_out8(acc, relu);
   }
 }
 
@@ -201,25 +298,48 @@ struct OutMap {
   int64_t img_stride, img_stride2;
 };
 
-// Implicit-GEMM convolution (IMPLICIT = true): X is the NHWC input [imgs, H, W, Cs] and the A tile
-// row m = (img, oy, ox), column k = (ky, kx, c) is gathered while staging — no im2col matrix
-// is written or read (the stem's was 144 MB per 100-frame chunk). C % 8 == 0: one 16-B load per
-// 8 columns (one tap); C == 4 (the stem's padded BGR0 blob): two 8-B loads (two taps).
+// A-operand modes of the GEMM below:
+//  AM_PLAIN    X is the [M, K] activation matrix.
+//  AM_IMPLICIT implicit-GEMM convolution: X is the NHWC input [imgs, H, W, Cs] and the A tile
+//              row m = (img, oy, ox), column k = (ky, kx, c) is gathered while staging — no
+//              im2col matrix is written or read (the stem's was 144 MB per 100-frame chunk).
+//              C % 8 == 0: one 16-B load per 8 columns (one tap); C == 4 (the stem's padded BGR0
+//              blob): two 8-B loads (two taps).
+//  AM_DW       depthwise 3x3 (pad 1, stride 1|2) + bias (+ReLU) fused in front of the pointwise
+//              GEMM (SURVEY K5 "optionally fused with the following pointwise GEMM"; prototxt
+//              conv1/dw -> conv1 and the 12 pairs after it, MobileNetSSD_deploy.prototxt:42-106):
+//              X is the depthwise INPUT [imgs, H, W, K] and each K-slice of the A tile is computed
+//              from its 9 taps while staging, so the depthwise output never goes through HBM.
+enum { AM_PLAIN = 0, AM_IMPLICIT = 1, AM_DW = 2 };
+constexpr int DW_KMAX = 1024;
 struct ConvGeom {
   int H, W, C, Cs, Ho, Wo, KW, stride, pad, Kreal;
+  const uint32_t* dw_w;  // AM_DW: [5][K] paired depthwise weights (see dw9_accum)
+  const float* dw_b;  // AM_DW: [K] depthwise bias
+  int dw_relu;
 };
 
-template <int BN, bool IMPLICIT>
+template <int BN, int AM>
 __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wt,
                                                              const float* __restrict__ bias, bf16* __restrict__ Y,
                                                              int M, int N, int K, int ldy, int relu, OutMap om,
                                                              ConvGeom cg) {
-  __shared__ __attribute__((aligned(16))) bf16 sA[2][GBM * GLDK];
-  __shared__ __attribute__((aligned(16))) bf16 sB[2][BN * GLDK];
+  // operand ring (2 x A 128x32 + 2 x B BNx32) and, after the main loop, the bf16 output tile
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * GBM * GLDK + 2 * BN * GLDK];
+  bf16* const sA0 = smem;
+  bf16* const sB0 = smem + 2 * GBM * GLDK;
   constexpr int WN = BN / 2;          // per-wave N extent
   constexpr int TN = WN / 16;         // 16x16 tiles per wave along N
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
+  // AM_DW: paired depthwise weights [5][K] dwords + bias [K] fp32 for the whole K (K <= DW_KMAX)
+  __shared__ __attribute__((aligned(16))) uint32_t dw_lds_w[AM == AM_DW ? 5 * DW_KMAX : 4];
+  __shared__ __attribute__((aligned(16))) float dw_lds_b[AM == AM_DW ? DW_KMAX : 4];
+  if constexpr (AM == AM_DW) {
+    for (int e = tid; e < 5 * K / 4; e += 256) ((u32x4*)dw_lds_w)[e] = ((const u32x4*)cg.dw_w)[e];
+    for (int e = tid; e < K / 4; e += 256) ((f32x4*)dw_lds_b)[e] = ((const f32x4*)cg.dw_b)[e];
+    __syncthreads();
+  }
 
   // XCD-aware, bijective block remap (cdna guide §5 T1): group label = bid % 8
   const int ntm = (M + GBM - 1) / GBM, ntn = (N + BN - 1) / BN;
@@ -235,9 +355,9 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
   // staging: A tile 128x32 bf16 = 512 x 16 B -> 2 per thread; B tile BN x 32 -> BN/128 per thread
   constexpr int BL = BN * 4 / 256;  // 16-B loads of B per thread
   bf16x8s ra[2], rb[BL];
-  // implicit conv: the output pixel of each of this thread's two A rows, fixed for the block
+  // implicit conv / depthwise: the output pixel of each of this thread's two A rows (fixed)
   int pix_img[2], pix_iy[2], pix_ix[2];
-  if constexpr (IMPLICIT) {
+  if constexpr (AM != AM_PLAIN) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int gm = m0 + ((tid + i * 256) >> 2);
@@ -255,29 +375,60 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
     if (iy < 0 || iy >= cg.H || ix < 0 || ix >= cg.W) return nullptr;
     return X + (((int64_t)pix_img[i] * cg.H + iy) * cg.W + ix) * cg.Cs + c;
   };
-  auto gload = [&](int k0) {
+  // AM_DW: the 9 taps of both rows of this thread's 8 channels, loaded in gload (in flight during
+  // the MFMAs) and reduced in sstore against the depthwise weights, which sit in LDS for the
+  // whole K (dw_lds: [9][K] bf16 then [K] fp32 bias; at most 9*1024*2 + 4096 B)
+  u32x4 dtap[2][9];
+  uint32_t tapok[2] = {0, 0};    // bit t: tap t inside the image
+  const bf16* pixbase[2] = {X, X};  // input address of tap 0 (row above, column left)
+  if constexpr (AM == AM_DW) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int e = tid + i * 256, row = e >> 2, kc = (e & 3) * 8;
-      const int gm = m0 + row;
-      if constexpr (IMPLICIT) {
-        bf16x8s v = bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
-        if (pix_img[i] >= 0) {
-          if (cg.C % 8 == 0) {
-            const bf16* q = tap_ptr(i, k0 + kc);
-            if (q) v = *(const bf16x8s*)q;
-          } else {  // C == 4: two taps of 4 channels
-            typedef short sx4v __attribute__((ext_vector_type(4)));
-            const bf16* q0 = tap_ptr(i, k0 + kc);
-            const bf16* q1 = tap_ptr(i, k0 + kc + 4);
-            const sx4v a = q0 ? *(const sx4v*)q0 : sx4v{0, 0, 0, 0};
-            const sx4v b = q1 ? *(const sx4v*)q1 : sx4v{0, 0, 0, 0};
-            v = bf16x8s{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-          }
+      if (pix_img[i] < 0) continue;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int iy = pix_iy[i] + t / 3, ix = pix_ix[i] + t % 3;
+        if (iy >= 0 && iy < cg.H && ix >= 0 && ix < cg.W) tapok[i] |= 1u << t;
+      }
+      pixbase[i] = X + (((int64_t)pix_img[i] * cg.H + pix_iy[i]) * cg.W + pix_ix[i]) * K;
+    }
+  }
+  auto gload = [&](int k0) {
+    if constexpr (AM == AM_DW) {
+      const int c = k0 + (tid & 3) * 8;  // the same 8 channels for both rows (256 % 4 == 0)
+      const int rowst = cg.W * K;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int off = (t / 3) * rowst + (t % 3) * K + c;
+          dtap[i][t] = (tapok[i] >> t) & 1 ? *(const u32x4*)(pixbase[i] + off) : u32x4{0u, 0u, 0u, 0u};
         }
-        ra[i] = v;
-      } else {
-        ra[i] = gm < M ? *(const bf16x8s*)(X + (int64_t)gm * K + k0 + kc) : bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int e = tid + i * 256, row = e >> 2, kc = (e & 3) * 8;
+        const int gm = m0 + row;
+        if constexpr (AM == AM_IMPLICIT) {
+          bf16x8s v = bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+          if (pix_img[i] >= 0) {
+            if (cg.C % 8 == 0) {
+              const bf16* q = tap_ptr(i, k0 + kc);
+              if (q) v = *(const bf16x8s*)q;
+            } else {  // C == 4: two taps of 4 channels
+              typedef short sx4v __attribute__((ext_vector_type(4)));
+              const bf16* q0 = tap_ptr(i, k0 + kc);
+              const bf16* q1 = tap_ptr(i, k0 + kc + 4);
+              const sx4v a = q0 ? *(const sx4v*)q0 : sx4v{0, 0, 0, 0};
+              const sx4v b = q1 ? *(const sx4v*)q1 : sx4v{0, 0, 0, 0};
+              v = bf16x8s{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+            }
+          }
+          ra[i] = v;
+        } else {
+          ra[i] = gm < M ? *(const bf16x8s*)(X + (int64_t)gm * K + k0 + kc) : bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
+        }
       }
     }
 #pragma unroll
@@ -287,16 +438,27 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
       rb[i] = gn < N ? *(const bf16x8s*)(Wt + (int64_t)gn * K + k0 + kc) : bf16x8s{0, 0, 0, 0, 0, 0, 0, 0};
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, int k0) {
+    if constexpr (AM == AM_DW) {
+      const int c = k0 + (tid & 3) * 8;
+      const f32x4 b0 = *(const f32x4*)(dw_lds_b + c), b1 = *(const f32x4*)(dw_lds_b + c + 4);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float a[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        dw9_accum(dtap[i], dw_lds_w + c, K, a);
+        // rounded to bf16 exactly where the unfused depthwise kernel writes its output
+        ra[i] = __builtin_bit_cast(bf16x8s, dw_out8(a, cg.dw_relu));
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int e = tid + i * 256, row = e >> 2;
-      *(bf16x8s*)(&sA[buf][gidx(row, e & 3)]) = ra[i];
+      *(bf16x8s*)(&sA0[buf * GBM * GLDK + gidx(row, e & 3)]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       const int e = tid + i * 256, row = e >> 2;
-      *(bf16x8s*)(&sB[buf][gidx(row, e & 3)]) = rb[i];
+      *(bf16x8s*)(&sB0[buf * BN * GLDK + gidx(row, e & 3)]) = rb[i];
     }
   };
 
@@ -308,65 +470,75 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
 
   const int nk = K / GBK;
   gload(0);
-  sstore(0);
+  sstore(0, 0);
   __syncthreads();
   const int fr = lane & 15, fc = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload((kt + 1) * GBK);
+    const bf16* sA = sA0 + cur * GBM * GLDK;
+    const bf16* sB = sB0 + cur * BN * GLDK;
     bf16x8s af[4], bfr[TN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8s*)(&sA[cur][gidx(wm * 64 + i * 16 + fr, fc)]);
+    for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8s*)(&sA[gidx(wm * 64 + i * 16 + fr, fc)]);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8s*)(&sB[cur][gidx(wn * WN + j * 16 + fr, fc)]);
+    for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8s*)(&sB[gidx(wn * WN + j * 16 + fr, fc)]);
     // operand order W x X: a lane's accumulator holds 4 consecutive output COLUMNS of one row
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    if (kt + 1 < nk) sstore(cur ^ 1);
+    if (kt + 1 < nk) sstore(cur ^ 1, (kt + 1) * GBK);
     __syncthreads();
   }
 
-  // epilogue: acc[i][j][r] = Y[m = .. + (lane & 15)][n = .. + 4 (lane >> 4) + r]: one 8-byte store
-  // per (i, j) where the 4 columns are in range and on the same side of the split
+  // epilogue: bias + act, the bf16 tile staged in LDS (16-B chunks XOR-swizzled by row), then
+  // written back as whole row segments, 16 B per lane (the direct 8-B-per-lane stores of 16-row
+  // x 32-B fragments measured 1.4-1.9 TB/s on these write-heavy layers)
+  constexpr int CH = BN / 8;  // 16-B chunks per tile row
+  bf16* const sC = smem;      // [GBM][BN]; the loop's last barrier freed the operand ring
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int gn = n0 + wn * WN + j * 16 + 4 * (lane >> 4);
+    const int cl = wn * WN + j * 16 + 4 * (lane >> 4);  // local column of this lane's 4 values
+    const int gn = n0 + cl;
     float bv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[r] = (gn + r < N && bias) ? bias[gn + r] : 0.f;
-    const bool lo = gn + 3 < om.split, hi = gn >= om.split && gn + 3 < N;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int gm = m0 + wm * 64 + i * 16 + (lane & 15);
-      if (gm >= M) continue;
-      const int64_t img = gm / om.rpi, rr = gm - img * om.rpi;
-      float v[4];
+      const int row = wm * 64 + i * 16 + (lane & 15);
+      bf16x4 o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        v[r] = acc[i][j][r] + bv[r];
-        if (relu) v[r] = fmaxf(v[r], 0.f);
+        float v = acc[i][j][r] + bv[r];
+        o[r] = (bf16)(relu ? fmaxf(v, 0.f) : v);
       }
-      if (lo && (ldy & 3) == 0 && (om.img_stride & 3) == 0) {
-        bf16x4 o;
+      *(bf16x4*)(sC + row * BN + (((cl >> 3) ^ (row & (CH - 1))) << 3) + (cl & 4)) = o;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < GBM * CH; e += 256) {
+    const int row = e / CH, ch = e - row * CH;
+    const int gm = m0 + row, gn = n0 + ch * 8;
+    if (gm >= M || gn >= N) continue;
+    const bf16x8 v = *(const bf16x8*)(sC + row * BN + ((ch ^ (row & (CH - 1))) << 3));
+    const int64_t img = gm / om.rpi, rr = gm - img * om.rpi;
+    bf16* const lo = Y + img * om.img_stride + rr * ldy + gn;
+    if (gn + 8 <= om.split && ((uintptr_t)lo & 15) == 0) {
+      *(bf16x8*)lo = v;
+      continue;
+    }
+    bf16* const hi = om.Y2 + img * om.img_stride2 + rr * om.ldy2 + (gn - om.split);
+    if (gn >= om.split && gn + 8 <= N && ((uintptr_t)hi & 15) == 0) {
+      *(bf16x8*)hi = v;
+      continue;
+    }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)v[r];
-        *(bf16x4*)(Y + img * om.img_stride + rr * ldy + gn) = o;
-      } else if (hi && ((om.ldy2 | (gn - om.split)) & 3) == 0 && (om.img_stride2 & 3) == 0) {
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)v[r];
-        *(bf16x4*)(om.Y2 + img * om.img_stride2 + rr * om.ldy2 + (gn - om.split)) = o;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = gn + r;
-          if (n >= N) break;
-          if (n < om.split) Y[img * om.img_stride + rr * ldy + n] = (bf16)v[r];
-          else om.Y2[img * om.img_stride2 + rr * om.ldy2 + (n - om.split)] = (bf16)v[r];
-        }
-      }
+    for (int r = 0; r < 8; ++r) {
+      const int n = gn + r;
+      if (n >= N) break;
+      if (n < om.split) Y[img * om.img_stride + rr * ldy + n] = v[r];
+      else om.Y2[img * om.img_stride2 + rr * om.ldy2 + (n - om.split)] = v[r];
     }
   }
 }
@@ -667,6 +839,11 @@ __global__ void __launch_bounds__(256) annotate_kernel(uint8_t* __restrict__ fra
 using namespace vcx;
 
 void vcx_resize_area_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int h, int w, hipStream_t s) {
+  if ((W * 3) % 16 == 0 && ((uintptr_t)src & 15) == 0 && w <= RA_XMAX * 256 && W * 3 <= RA_LDS && h <= H &&
+      w <= W && (int64_t)N * h < INT32_MAX) {
+    hipLaunchKernelGGL(resize_area_rows_kernel, dim3(N * h), dim3(256), 0, s, src, dst, N, H, W, h, w);
+    return;
+  }
   hipLaunchKernelGGL(resize_area_u8_kernel, dim3(stream_grid((int64_t)N * h * w, 256)), dim3(256), 0, s, src, dst, N,
                      H, W, h, w);
 }
@@ -691,7 +868,7 @@ void vcx_im2col_nhwc(const void* x, void* out, int N, int H, int W, int C, int C
 void vcx_dwconv3x3(const void* x, const void* w, const float* b, void* y, int N, int H, int W, int C, int Ho, int Wo,
                    int stride, int relu, hipStream_t s) {
   hipLaunchKernelGGL(dwconv3x3_kernel, dim3(stream_grid((int64_t)N * Ho * Wo * (C / 8), 256)), dim3(256), 0, s,
-                     (const bf16*)x, (const bf16*)w, b, (bf16*)y, N, H, W, C, Ho, Wo, stride, relu);
+                     (const bf16*)x, (const uint32_t*)w, b, (bf16*)y, N, H, W, C, Ho, Wo, stride, relu);
 }
 
 void vcx_gemm_bias_act_mapped(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
@@ -701,11 +878,11 @@ void vcx_gemm_bias_act_mapped(const void* X, const void* Wt, const float* bias, 
   ConvGeom cg{};
   if (N <= 64) {
     const int nwg = ((M + GBM - 1) / GBM) * ((N + 63) / 64);
-    hipLaunchKernelGGL((gemm_bias_act_kernel<64, false>), dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt,
+    hipLaunchKernelGGL((gemm_bias_act_kernel<64, AM_PLAIN>), dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt,
                        bias, (bf16*)Y, M, N, K, ldy, relu, om, cg);
   } else {
     const int nwg = ((M + GBM - 1) / GBM) * ((N + 127) / 128);
-    hipLaunchKernelGGL((gemm_bias_act_kernel<128, false>), dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt,
+    hipLaunchKernelGGL((gemm_bias_act_kernel<128, AM_PLAIN>), dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt,
                        bias, (bf16*)Y, M, N, K, ldy, relu, om, cg);
   }
 }
@@ -717,15 +894,34 @@ void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   const int M = imgs * Ho * Wo;
   OutMap om{nullptr, N, 0, M, 0, 0};
-  ConvGeom cg{H, W, C, Cs, Ho, Wo, KW, stride, pad, KH * KW * C};
+  ConvGeom cg{H, W, C, Cs, Ho, Wo, KW, stride, pad, KH * KW * C, nullptr, nullptr, 0};
   if (N <= 64) {
     const int nwg = ((M + GBM - 1) / GBM) * ((N + 63) / 64);
-    hipLaunchKernelGGL((gemm_bias_act_kernel<64, true>), dim3(nwg), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt,
+    hipLaunchKernelGGL((gemm_bias_act_kernel<64, AM_IMPLICIT>), dim3(nwg), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt,
                        bias, (bf16*)Y, M, N, Kp, N, relu, om, cg);
   } else {
     const int nwg = ((M + GBM - 1) / GBM) * ((N + 127) / 128);
-    hipLaunchKernelGGL((gemm_bias_act_kernel<128, true>), dim3(nwg), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt,
+    hipLaunchKernelGGL((gemm_bias_act_kernel<128, AM_IMPLICIT>), dim3(nwg), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt,
                        bias, (bf16*)Y, M, N, Kp, N, relu, om, cg);
+  }
+}
+
+// depthwise 3x3 (pad 1) + bias (+ReLU) -> pointwise GEMM + bias (+ReLU), one kernel:
+// x NHWC [imgs, H, W, K], dw_w [9][K], dw_b [K], Wt [N, K] -> Y [imgs*Ho*Wo, N]
+void vcx_dw_pw(const void* x, const void* dw_w, const float* dw_b, int dw_relu, const void* Wt, const float* bias,
+               void* Y, int imgs, int H, int W, int K, int stride, int N, int relu, hipStream_t s) {
+  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  const int M = imgs * Ho * Wo;
+  OutMap om{nullptr, N, 0, M, 0, 0};
+  ConvGeom cg{H, W, K, K, Ho, Wo, 3, stride, 1, 9 * K, (const uint32_t*)dw_w, dw_b, dw_relu};
+  if (N <= 64) {
+    const int nwg = ((M + GBM - 1) / GBM) * ((N + 63) / 64);
+    hipLaunchKernelGGL((gemm_bias_act_kernel<64, AM_DW>), dim3(nwg), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt,
+                       bias, (bf16*)Y, M, N, K, N, relu, om, cg);
+  } else {
+    const int nwg = ((M + GBM - 1) / GBM) * ((N + 127) / 128);
+    hipLaunchKernelGGL((gemm_bias_act_kernel<128, AM_DW>), dim3(nwg), dim3(256), 0, s, (const bf16*)x,
+                       (const bf16*)Wt, bias, (bf16*)Y, M, N, K, N, relu, om, cg);
   }
 }
 

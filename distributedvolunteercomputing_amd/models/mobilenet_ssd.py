@@ -4,7 +4,9 @@ run by OpenCV DNN on CPU at /root/reference/worker.py:194,245-249).
 ``SSDExecutor`` compiles the Caffe ``NetDef`` into a plan of MI355X kernels over NHWC bf16
 activations for a whole chunk of frames at once:
 
-  Convolution group=C (depthwise 3x3)  -> dwconv3x3 kernel (+bias +ReLU fused)
+  Convolution group=C (depthwise 3x3)  -> fused into the following pointwise GEMM (dw_pw: the
+                                          depthwise tile is computed while staging the A operand),
+                                          or the dwconv3x3 kernel (+bias +ReLU) for wide blocks
   Convolution 1x1                      -> MFMA GEMM  [N*H*W, Cin] x [Cout, Cin]^T (+bias +ReLU)
   Convolution kxk (stem, SSD extras)   -> the same MFMA GEMM as an implicit GEMM (the A tile is
                                           gathered from the NHWC input while staging: no im2col)
@@ -208,7 +210,8 @@ class SSDExecutor:
                     if not (group == cin == cout and k == 3 and pad == 1):
                         raise NotImplementedError(f"{l.name}: only depthwise 3x3 pad 1 grouped conv is supported")
                     w9 = w.detach().float().permute(2, 3, 0, 1).reshape(9, cout).contiguous()
-                    plan.append(("dw", l, dict(w=w9.to(dev, torch.bfloat16), b=bias, stride=stride, relu=relu)))
+                    plan.append(("dw", l, dict(w=V.dw_pair_weights(w9.to(dev, torch.bfloat16)), b=bias,
+                                               stride=stride, relu=relu)))
                 elif k == 1 and stride == 1 and pad == 0 and cin % 32 == 0:
                     wt = w.detach().float().reshape(cout, cin).to(dev, torch.bfloat16).contiguous()
                     plan.append(("pw", l, dict(w=wt, b=bias, relu=relu)))
@@ -260,7 +263,34 @@ class SSDExecutor:
             hs["concats"] = (a["concat"], c["concat"])
             hs["offs"] = (offs[(a["concat"], a["pos"])], offs[(c["concat"], c["pos"])])
             hs["rows"] = a["rows"]
-        return plan
+        return self._fuse_dw_pw(plan)
+
+    def _fuse_dw_pw(self, plan):
+        """Depthwise -> pointwise pairs (every MobileNet block, prototxt 42-106 and after) become one
+        `dwpw` step when the depthwise output feeds only that pointwise conv. Blocks whose
+        pointwise output is wider than `max_cout` stay two kernels: the fused kernel recomputes
+        the depthwise tile once per 128 output channels (VCX_DWPW_MAX_COUT, 0 disables)."""
+        max_cout = int(os.environ.get("VCX_DWPW_MAX_COUT", "256"))
+        uses = {}
+        for l in self.net.layers:
+            if l.tops == l.bottoms:
+                continue  # in-place (the ReLUs folded into their producer)
+            for b in l.bottoms:
+                uses[b] = uses.get(b, 0) + 1
+        out, i = [], 0
+        while i < len(plan):
+            kind, l, p = plan[i]
+            if kind == "dw" and i + 1 < len(plan) and max_cout > 0:
+                k2, l2, p2 = plan[i + 1]
+                K = p["w"].shape[1]
+                if (k2 == "pw" and l2.bottoms[0] == l.tops[0] and uses.get(l.tops[0], 0) == 1
+                        and p2["w"].shape[0] <= max_cout and K <= 1024 and K % 32 == 0):
+                    out.append(("dwpw", l2, dict(dw=p, pw=p2, src=l.bottoms[0])))
+                    i += 2
+                    continue
+            out.append(plan[i])
+            i += 1
+        return out
 
     # ------------------------------------------------------------------ helpers
     def _priors(self, layer, fh, fw):
@@ -307,6 +337,10 @@ class SSDExecutor:
             top = l.tops[0] if l.tops else None
             if kind == "dw":
                 y = V.dwconv3x3(x, p["w"], p["b"], p["stride"], p["relu"])
+                t[top], layout[top], hw[top], chans[top] = y, "nhwc", (y.shape[1], y.shape[2]), y.shape[3]
+            elif kind == "dwpw":
+                d, q = p["dw"], p["pw"]
+                y = V.dw_pw(t[p["src"]], d["w"], d["b"], d["relu"], d["stride"], q["w"], q["b"], q["relu"])
                 t[top], layout[top], hw[top], chans[top] = y, "nhwc", (y.shape[1], y.shape[2]), y.shape[3]
             elif kind == "pw":
                 H, W = hw[src]

@@ -95,16 +95,51 @@ def blob_from_frames(frames: torch.Tensor, size: int = 300, scale: float = 0.007
 
 
 # ----------------------------------------------------------------------------- conv / gemm
-def dwconv3x3(x, w9c, b, stride, relu=True):
-    """NHWC depthwise 3x3, pad 1. w9c: [9, C] bf16 (tap-major), b: [C] fp32."""
+def dw_pair_weights(w9c):
+    """[9, C] tap-major depthwise weights -> the paired layout of the dot2 kernels, [5, C, 2] bf16:
+    row p < 4 holds (w[2p], w[2p+1]) per channel, row 4 holds (w[8], 0) for even channels and
+    (0, w[8]) for odd ones (csrc/kernels/vision.hip dw9_accum)."""
+    C = w9c.shape[1]
+    w = w9c.to(torch.bfloat16)
+    wp = torch.zeros(5, C, 2, dtype=torch.bfloat16, device=w9c.device)
+    wp[:4, :, 0] = w[0:8:2]
+    wp[:4, :, 1] = w[1:8:2]
+    wp[4, 0::2, 0] = w[8, 0::2]
+    wp[4, 1::2, 1] = w[8, 1::2]
+    return wp
+
+
+def _dw_unpair(wp):
+    w = torch.empty(9, wp.shape[1], dtype=wp.dtype, device=wp.device)
+    w[0:8:2], w[1:8:2] = wp[:4, :, 0], wp[:4, :, 1]
+    w[8] = wp[4, :, 0] + wp[4, :, 1]
+    return w
+
+
+def dwconv3x3(x, w, b, stride, relu=True):
+    """NHWC depthwise 3x3, pad 1. w: [9, C] bf16 tap-major or the paired [5, C, 2] layout of
+    dw_pair_weights; b: [C] fp32."""
     if use_native(x):
-        return native().dwconv3x3(x, w9c, b, stride, relu)
+        return native().dwconv3x3(x, w if w.dim() == 3 else dw_pair_weights(w), b, stride, relu)
+    w9c = _dw_unpair(w) if w.dim() == 3 else w
     C = x.shape[3]
     wt = w9c.float().t().reshape(C, 1, 3, 3)
     y = F.conv2d(x.permute(0, 3, 1, 2).float(), wt, b.float(), stride=stride, padding=1, groups=C)
     if relu:
         y = F.relu(y)
     return y.permute(0, 2, 3, 1).contiguous().to(x.dtype)
+
+
+def dw_pw(x, wp, db, dw_relu, stride, Wt, bias, relu=True):
+    """A MobileNet block as one kernel: depthwise 3x3 (pad 1) + bias (+ReLU) on NHWC x [N, H, W, K],
+    then the pointwise GEMM with Wt [Cout, K] + bias (+ReLU) -> [N, Ho, Wo, Cout]. wp: paired
+    depthwise weights (dw_pair_weights). The depthwise activation is rounded to bf16 as the
+    two-kernel path rounds it, and never goes through memory."""
+    if use_native(x):
+        return native().dw_pw(x, wp, db, dw_relu, stride, Wt, bias, relu)
+    d = dwconv3x3(x, wp, db, stride, dw_relu)
+    N, Ho, Wo, K = d.shape
+    return gemm_bias_act(d.reshape(-1, K), Wt, bias, relu).view(N, Ho, Wo, -1)
 
 
 def gemm_bias_act(X, Wt, bias=None, relu=False):

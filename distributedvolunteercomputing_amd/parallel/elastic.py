@@ -38,6 +38,7 @@ from __future__ import annotations
 
 import os
 import socket
+import datetime
 import threading
 import time
 from contextlib import contextmanager
@@ -209,6 +210,12 @@ class ElasticMembership:
         self._live: _Liveness | None = None
         self._eof: dict[int, str] = {}
         self.eof_events: list[tuple[int, float]] = []  # (member, time) of every EOF seen
+        self._ring_pending = False  # an EOF arrived: the heartbeat thread rings the round's bell
+        self._tag = ""  # the armed guard's round tag (its verdict key is posted on a trip)
+        self._gc: dict[tuple[int, int], list[str]] = {}  # (gen, round) -> keys to delete later
+        # blocking store waits (server-side wake-up) instead of sleep-polling on the fast paths; a
+        # wait that runs out falls back to the polling scan, which owns lease/EOF detection
+        self.bell_s = min(2.0, max(0.25, lease_s / 4))
         if backend == "nccl":
             # abortable (non-blocking) RCCL communicator init for every generation's group
             os.environ.setdefault("TORCH_NCCL_USE_COMM_NONBLOCKING", "1")
@@ -241,6 +248,13 @@ class ElasticMembership:
                         live.watch(list(self.members))
                     except Exception:  # noqa: BLE001 — best effort; the lease still applies
                         pass
+                if self._ring_pending:
+                    # wake the peers blocked on this round's bell: their scan sees the EOF now
+                    self._ring_pending = False
+                    try:
+                        self.store.set(f"{_P}bell/{self.gen}/{self.round}", "eof")
+                    except Exception:  # noqa: BLE001
+                        pass
                 if self._armed:
                     try:
                         self._watch()
@@ -269,6 +283,7 @@ class ElasticMembership:
         with self._lock:
             self._eof[m] = addr
             self.eof_events.append((m, now))
+            self._ring_pending = True
         _dbg(self.pid, f"liveness EOF from peer {m} ({addr})")
         self._wake.set()  # the watchdog (heartbeat thread) aborts a collective in flight right away
 
@@ -320,6 +335,9 @@ class ElasticMembership:
             self._abort_reason = reason
             self._abort.set()
             grp = self.group
+            tag = self._tag if self._armed else ""
+        if tag:  # peers blocked on this round's verdict wake up to the abort
+            self._vote(tag, "abort")
         self.events.append({"event": "abort", "gen": self.gen, "reason": reason, "t": time.time()})
         _dbg(self.pid, f"trip gen {self.gen}: {reason}")
         if grp is not None:
@@ -379,7 +397,23 @@ class ElasticMembership:
         if self._abort.is_set() or self.store.check([f"{_P}abort/{self.gen}"]):
             return self.recover()
         self.round += 1
+        self._collect(self.round - 2)
         return self._round(str(self.round), recovery=False)
+
+    def _collect(self, r: int):
+        """Delete round r's keys of the current generation: every member has passed round r+1
+        (its guard could not commit otherwise), so nothing reads them again."""
+        keys = self._gc.pop((self.gen, r), None)
+        for key in keys or ():
+            try:
+                self.store.delete_key(key)
+            except Exception:  # noqa: BLE001
+                pass
+        for stale in [gk for gk in self._gc if gk[0] != self.gen]:
+            self._gc.pop(stale)  # an old generation's keys stay (an evicted peer may still read them)
+
+    def _mark(self, r, *keys):
+        self._gc.setdefault((self.gen, r), []).extend(keys)
 
     def recover(self):
         """After a PeerFailure: leave the aborted generation and form the next one from the
@@ -409,6 +443,9 @@ class ElasticMembership:
             if self._abort.is_set():
                 raise PeerFailure(f"gen {self.gen}: aborted ({self._abort_reason})")
             self._watch_seen = {}
+            self._tag = tag
+            if self.pid == self.members[0]:
+                self._mark(self.round, f"{_P}ok/{self.gen}/{tag}", f"{_P}verdict/{self.gen}/{tag}")
             self._armed = True
         try:
             _dbg(self.pid, f"guard {self.gen}/{tag}: connect")
@@ -434,21 +471,32 @@ class ElasticMembership:
         except Exception:  # noqa: BLE001
             return "abort"
 
+    def _wait_keys(self, keys, timeout_s: float) -> bool:
+        """Block until every key exists (the store wakes us), or the timeout passes."""
+        try:
+            self.store.wait(keys, datetime.timedelta(seconds=timeout_s))
+            return True
+        except Exception:  # noqa: BLE001 — DistStoreError on timeout
+            return False
+
     def _commit(self, tag):
         g, P = self.gen, len(self.members)
         okk, vk = f"{_P}ok/{g}/{tag}", f"{_P}verdict/{g}/{tag}"
-        self.store.add(okk, 1)
-        while True:
-            if self.store.check([vk]):
-                v = _s(self.store.get(vk))
-                break
-            if int(self.store.add(okk, 0)) >= P:
-                v = self._vote(tag, "commit")
-                break
-            if self._abort.is_set():
-                v = self._vote(tag, "abort")
-                break
-            time.sleep(self.poll_s)
+        if int(self.store.add(okk, 1)) >= P:
+            v = self._vote(tag, "commit")  # the last member in: everyone's body completed
+        else:
+            # everyone else blocks on the verdict key: written by the last member in, by a member
+            # whose body failed, or by a watchdog trip (EOF / lease) of any member
+            while True:
+                if self._wait_keys([vk], self.bell_s):
+                    v = _s(self.store.get(vk))
+                    break
+                if self._abort.is_set():
+                    v = self._vote(tag, "abort")
+                    break
+                if int(self.store.add(okk, 0)) >= P:
+                    v = self._vote(tag, "commit")
+                    break
         _dbg(self.pid, f"verdict {g}/{tag}: {v}")
         if v != "commit":
             self._trip(f"round {g}/{tag} voted abort")
@@ -459,6 +507,23 @@ class ElasticMembership:
         g = self.gen
         self.store.set(f"{_P}arr/{g}/{k}/{self.pid}", "1" if self.has_model else "0")
         okey = f"{_P}out/{g}/{k}"
+        bell = f"{_P}bell/{g}/{k}"
+        if not recovery:
+            self._mark(self.round, f"{_P}arr/{g}/{k}/{self.pid}")
+            if self.members and self.pid == self.members[0]:
+                self._mark(self.round, f"{_P}narr/{g}/{k}", okey, bell)
+            # fast path (every member arrives, nobody joins): the last one in proposes "same" and
+            # rings the bell; the others sleep in a store wait instead of scanning the members
+            n = int(self.store.add(f"{_P}narr/{g}/{k}", 1))
+            if n >= len(self.members):
+                if self._njoin() <= self.joins_seen:
+                    self.store.compare_set(okey, "", "same")
+                    self.store.set(bell, "1")
+                    return self._follow(okey)
+            elif not any(m != self.pid and m in self._eof and self._gone(m) for m in self.members) and \
+                    self._wait_keys([bell], self.bell_s) and self.store.check([okey]):
+                # (a member whose link already closed will not arrive: straight to the scan)
+                return self._follow(okey)
         others = [m for m in self.members if m != self.pid]
         now = time.time()
         hb_seen = {}
@@ -517,6 +582,7 @@ class ElasticMembership:
             newcomers = sorted(set([m for m in survivors if not arrived[m]] + new_ids))
             decision = f"next:{_csv(members)}|{_csv(newcomers)}|{njoin}"
         won = _s(self.store.compare_set(okey, "", decision))
+        self.store.set(bell, "1")
         _dbg(self.pid, f"round {g}/{k}: proposed {decision!r} (dead={sorted(dead)} left={sorted(left)}), agreed {won!r}")
         return self._follow(okey)
 

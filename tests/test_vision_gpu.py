@@ -46,6 +46,38 @@ def test_dwconv(gpu, C, stride, H):
     assert torch.allclose(y.float(), r.float(), atol=3e-2, rtol=2e-2)
 
 
+def test_dw_pair_weights_roundtrip():
+    w = torch.randn(9, 24).to(torch.bfloat16)
+    wp = V.dw_pair_weights(w)
+    assert wp.shape == (5, 24, 2) and torch.equal(V._dw_unpair(wp), w)
+
+
+@pytest.mark.parametrize("N,H,K,stride,cout", [(3, 150, 32, 1, 64), (2, 150, 64, 2, 128), (3, 75, 128, 1, 128),
+                                                (2, 75, 128, 2, 256), (2, 38, 256, 1, 256), (3, 19, 512, 1, 512),
+                                                (2, 10, 1024, 1, 1024), (1, 7, 96, 2, 72)])
+def test_dw_pw_fused_vs_fp32(gpu, N, H, K, stride, cout):
+    """One kernel for depthwise 3x3 + bias + ReLU -> pointwise GEMM + bias + ReLU, against the
+    fp32 PyTorch convolutions of the same bf16 operands (the fused path rounds the depthwise
+    activation to bf16, as the two-kernel path does)."""
+    torch.manual_seed(2)
+    x = torch.randn(N, H, H, K, device=gpu).to(torch.bfloat16)
+    w9 = (torch.randn(9, K, device=gpu) * 0.3).to(torch.bfloat16)
+    db = torch.randn(K, device=gpu) * 0.1
+    Wt = (torch.randn(cout, K, device=gpu) / K**0.5).to(torch.bfloat16)
+    b = torch.randn(cout, device=gpu) * 0.1
+    y = V.dw_pw(x, V.dw_pair_weights(w9), db, True, stride, Wt, b, True)
+    xc = x.permute(0, 3, 1, 2).float()
+    d = F.relu(F.conv2d(xc, w9.float().t().reshape(K, 1, 3, 3), db, stride=stride, padding=1, groups=K))
+    r = F.relu(F.conv2d(d.to(torch.bfloat16).float(), Wt.float().reshape(cout, K, 1, 1), b)).permute(0, 2, 3, 1)
+    assert y.shape == r.shape
+    rel = float((y.float() - r).norm() / r.norm())
+    assert rel < 1e-2, rel
+    # and the two-kernel path of the same block
+    d2 = V.dwconv3x3(x, w9, db, stride, True)
+    y2 = V.gemm_bias_act(d2.reshape(-1, K), Wt, b, True).view_as(y)
+    assert float((y.float() - y2.float()).norm() / y2.float().norm()) < 1e-2
+
+
 def test_im2col(gpu):
     x = torch.randn(2, 10, 10, 256, device=gpu).to(torch.bfloat16)
     a = V.im2col_nhwc(x, 256, 3, 2, 1, 2304)
