@@ -66,6 +66,8 @@ at::Tensor dwconv3x3(at::Tensor x, at::Tensor w, at::Tensor b, int64_t stride, b
   TORCH_CHECK(((uintptr_t)x.data_ptr() & 15) == 0 && ((uintptr_t)w.data_ptr() & 15) == 0 &&
               ((uintptr_t)b.data_ptr() & 15) == 0, "dwconv3x3: 16-B aligned operands");
   const int64_t Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  TORCH_CHECK(Wo * (C / 8) < INT32_MAX && N * ((Ho + 1) / 2) <= 65535 && N * H * W * C < ((int64_t)1 << 40),
+              "dwconv3x3: grid limits");
   auto y = at::empty({N, Ho, Wo, C}, x.options());
   vcx_dwconv3x3(x.data_ptr(), w.data_ptr(), b.data_ptr<float>(), y.data_ptr(), (int)N, (int)H, (int)W, (int)C,
                 (int)Ho, (int)Wo, (int)stride, relu ? 1 : 0, cur_stream());
@@ -86,8 +88,10 @@ at::Tensor gemm_bias_act(at::Tensor X, at::Tensor Wt, c10::optional<at::Tensor> 
     bp = bias->data_ptr<float>();
   }
   auto Y = at::empty({M, N}, X.options());
+  const int S = vcx_vision_ksplit((int)M, (int)N, (int)K);
+  at::Tensor ws = S > 1 ? at::empty({S, M, N}, X.options().dtype(at::kFloat)) : at::Tensor();
   vcx_gemm_bias_act(X.data_ptr(), Wt.data_ptr(), bp, Y.data_ptr(), (int)M, (int)N, (int)K, (int)N, relu ? 1 : 0,
-                    cur_stream());
+                    S > 1 ? ws.data_ptr<float>() : nullptr, S, cur_stream());
   return Y;
 }
 
@@ -135,10 +139,13 @@ void gemm_bias_heads(at::Tensor X, at::Tensor Wt, at::Tensor bias, at::Tensor lo
   TORCH_CHECK(loc_all.dim() == 2 && conf_all.dim() == 2 && loc_all.size(0) == imgs && conf_all.size(0) == imgs);
   TORCH_CHECK(loc_off + rpi * split <= loc_all.size(1) && conf_off + rpi * (N - split) <= conf_all.size(1),
               "head output out of the concat buffer");
+  const int S = vcx_vision_ksplit((int)M, (int)N, (int)K);
+  at::Tensor ws = S > 1 ? at::empty({S, M, N}, X.options().dtype(at::kFloat)) : at::Tensor();
   vcx_gemm_bias_act_mapped(X.data_ptr(), Wt.data_ptr(), bias.data_ptr<float>(),
                            (uint16_t*)loc_all.data_ptr() + loc_off, (int)M, (int)N, (int)K, (int)split, 0,
                            (uint16_t*)conf_all.data_ptr() + conf_off, (int)split, (int)(N - split), (int)rpi,
-                           loc_all.size(1), conf_all.size(1), cur_stream());
+                           loc_all.size(1), conf_all.size(1), S > 1 ? ws.data_ptr<float>() : nullptr, S,
+                           cur_stream());
 }
 
 // KxK convolution as an implicit GEMM (no im2col matrix): x NHWC bf16 [imgs, H, W, Cs] using
@@ -154,9 +161,11 @@ at::Tensor conv_implicit(at::Tensor x, at::Tensor Wt, at::Tensor bias, int64_t C
   TORCH_CHECK((C % 8 == 0 && Cs % 8 == 0) || (C == 4 && Cs == 4), "implicit conv: C % 8 == 0, or C == Cs == 4");
   const int64_t Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   auto Y = at::empty({imgs, Ho, Wo, N}, x.options());
+  const int S = vcx_vision_ksplit((int)(imgs * Ho * Wo), (int)N, (int)Kp);
+  at::Tensor ws = S > 1 ? at::empty({S, imgs * Ho * Wo, N}, x.options().dtype(at::kFloat)) : at::Tensor();
   vcx_conv_implicit(x.data_ptr(), Wt.data_ptr(), bias.data_ptr<float>(), Y.data_ptr(), (int)imgs, (int)H, (int)W,
                     (int)C, (int)Cs, (int)KH, (int)KW, (int)stride, (int)pad, (int)N, (int)Kp, relu ? 1 : 0,
-                    cur_stream());
+                    S > 1 ? ws.data_ptr<float>() : nullptr, S, cur_stream());
   return Y;
 }
 

@@ -8,6 +8,8 @@
 //   * the SSD heads' Permute(0,2,3,1)+Flatten is the identity on NHWC data.
 // A whole 100-frame chunk is one batch, which turns the per-frame GEMVs of the reference into
 // real GEMMs (M = 100*19*19 = 36100 rows for conv11).
+#include <algorithm>
+
 #include "vcx_common.h"
 
 namespace vcx {
@@ -66,7 +68,7 @@ constexpr int RA_LDS = 24 * 1024, RA_XMAX = 4;
 __global__ void __launch_bounds__(256) resize_area_rows_kernel(const uint8_t* __restrict__ src,
                                                                 uint8_t* __restrict__ dst, int N, int H, int W, int h,
                                                                 int w) {
-  __shared__ __attribute__((aligned(16))) uint8_t rows[RA_LDS];
+  __shared__ __attribute__((aligned(16))) uint8_t rows[RA_LDS + 1024];  // + a wave's tail lanes
   typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x;
   const int y = blockIdx.x % h, n = blockIdx.x / h;
@@ -80,8 +82,15 @@ __global__ void __launch_bounds__(256) resize_area_rows_kernel(const uint8_t* __
   for (int r0 = iy0; r0 < iy1; r0 += rpp) {
     const int nr = min(rpp, iy1 - r0);
     __syncthreads();  // the previous pass has finished reading the band
-    const u32x4_t* g = (const u32x4_t*)(src + ((int64_t)n * H + r0) * rb);
-    for (int e = tid; e < nr * rb / 16; e += 256) ((u32x4_t*)rows)[e] = g[e];
+    // the band's rows straight into LDS (global_load_lds, 16 B per lane): all in flight at once
+    const uint8_t* g = src + ((int64_t)n * H + r0) * rb;
+    const int chunks = nr * rb / 16;
+    for (int e0 = (tid & ~63); e0 < chunks; e0 += 256) {
+      const int e = min(e0 + (tid & 63), chunks - 1);  // tail lanes re-copy the last chunk
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + (int64_t)e * 16),
+                                       (__attribute__((address_space(3))) void*)(rows + e0 * 16), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
     __syncthreads();
     for (int r = 0; r < nr; ++r) {
       const float wy = fminf(fy1, (float)(r0 + r + 1)) - fmaxf(fy0, (float)(r0 + r));
@@ -236,34 +245,48 @@ __device__ __forceinline__ u32x4 dw_out8(const float (&a)[8], int relu) {
   return __builtin_bit_cast(u32x4, o);
 }
 
-// (A 4-outputs-per-thread sliding-window variant halves the tap loads but strides the lanes
-// 4 pixels apart, and a 2-D grid without the grid-stride loop launches ~35k short blocks: both
-// measured 1.4x slower per network pass than this grid-stride kernel.)
+// One thread = one (column ox, 8-channel group) and R consecutive output rows: the (R-1)*stride+3
+// input rows x 3 columns it needs are ALL loaded before any reduction (R = 4 at stride 1: 18
+// loads for 4 outputs instead of 36, and every wave keeps 18 KB of loads in flight, most of it
+// L1/L2 hits around ~3 KB of new HBM data). 2-D grid: blockIdx.y = (image, row group) so the
+// image/row split is scalar; lanes run along (ox, c8) with C8 a power of two (a shift). The
+// previous grid-stride version (one output per iteration, 64-bit index division) measured
+// 135 us for conv1/dw (288 MB, 2.1 TB/s).
+template <int STRIDE, int R>
 __global__ void __launch_bounds__(256) dwconv3x3_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ wp,
-                                                         const float* __restrict__ b, bf16* __restrict__ y, int N,
-                                                         int H, int W, int C, int Ho, int Wo, int stride, int relu) {
-  const int C8 = C >> 3;
-  const int64_t total = (int64_t)N * Ho * Wo * C8;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int c8 = (int)(i % C8);
-    const int64_t p = i / C8;
-    const int ox = (int)(p % Wo), oy = (int)((p / Wo) % Ho), n = (int)(p / ((int64_t)Wo * Ho));
-    float acc[8];
-    {
-      const f32x4 b0 = *(const f32x4*)(b + c8 * 8), b1 = *(const f32x4*)(b + c8 * 8 + 4);
-      acc[0] = b0[0]; acc[1] = b0[1]; acc[2] = b0[2]; acc[3] = b0[3];
-      acc[4] = b1[0]; acc[5] = b1[1]; acc[6] = b1[2]; acc[7] = b1[3];
-    }
-    u32x4 xv[9];
+                                                         const float* __restrict__ b, bf16* __restrict__ y, int H,
+                                                         int W, int C, int Ho, int Wo, int c8_shift, int relu) {
+  constexpr int NR = (R - 1) * STRIDE + 3;  // input rows per thread
+  const int C8 = 1 << c8_shift;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int ox = idx >> c8_shift, c8 = idx & (C8 - 1);
+  if (ox >= Wo) return;
+  const int groups = (Ho + R - 1) / R;
+  const int n = blockIdx.y / groups, oy0 = (blockIdx.y - n * groups) * R;
+  const int iy0 = oy0 * STRIDE - 1, ix0 = ox * STRIDE - 1;
+  const bf16* xn = x + (int64_t)n * H * W * C + c8 * 8;
+  u32x4 xv[NR][3];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int iy = oy * stride - 1 + t / 3, ix = ox * stride - 1 + t % 3;
-      xv[t] = (iy >= 0 && iy < H && ix >= 0 && ix < W)
-                  ? *(const u32x4*)(x + (((int64_t)n * H + iy) * W + ix) * C + c8 * 8)
-                  : u32x4{0u, 0u, 0u, 0u};
+  for (int r = 0; r < NR; ++r) {
+    const int iy = iy0 + r;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int ix = ix0 + kx;
+      xv[r][kx] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? *(const u32x4*)(xn + ((int64_t)iy * W + ix) * C)
+                                                           : u32x4{0u, 0u, 0u, 0u};
     }
-    dw9_accum(xv, wp + c8 * 8, C, acc);
-    *(u32x4*)(y + p * C + c8 * 8) = dw_out8(acc, relu);
+  }
+  f32x4 b0 = *(const f32x4*)(b + c8 * 8), b1 = *(const f32x4*)(b + c8 * 8 + 4);
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int oy = oy0 + j;
+    if (oy >= Ho) break;
+    float acc[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+    const u32x4 t9[9] = {xv[j * STRIDE][0],     xv[j * STRIDE][1],     xv[j * STRIDE][2],
+                         xv[j * STRIDE + 1][0], xv[j * STRIDE + 1][1], xv[j * STRIDE + 1][2],
+                         xv[j * STRIDE + 2][0], xv[j * STRIDE + 2][1], xv[j * STRIDE + 2][2]};
+    dw9_accum(t9, wp + c8 * 8, C, acc);
+    *(u32x4*)(y + (((int64_t)n * Ho + oy) * Wo + ox) * C + c8 * 8) = dw_out8(acc, relu);
   }
 }
 
@@ -296,7 +319,25 @@ struct OutMap {
   bf16* Y2;
   int split, ldy2, rpi;
   int64_t img_stride, img_stride2;
+  float* part;  // split-K: fp32 partial sums [gridDim.z][M][N] instead of the epilogue (else null)
+  int kchunk;   // split-K: K columns per z (multiple of 32)
 };
+
+// split-K reduction + the epilogue (bias, ReLU, bf16, output mapping) for the partials above
+__global__ void __launch_bounds__(256) splitk_bias_act_kernel(const float* __restrict__ part, int S,
+                                                               const float* __restrict__ bias, bf16* __restrict__ Y,
+                                                               int M, int N, int ldy, int relu, OutMap om) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    float v = bias ? bias[e % N] : 0.f;
+    for (int z = 0; z < S; ++z) v += part[z * total + e];
+    if (relu) v = fmaxf(v, 0.f);
+    const int gm = (int)(e / N), n = (int)(e - (int64_t)gm * N);
+    const int64_t img = gm / om.rpi, rr = gm - img * om.rpi;
+    if (n < om.split) Y[img * om.img_stride + rr * ldy + n] = (bf16)v;
+    else om.Y2[img * om.img_stride2 + rr * om.ldy2 + (n - om.split)] = (bf16)v;
+  }
+}
 
 // A-operand modes of the GEMM below:
 //  AM_PLAIN    X is the [M, K] activation matrix.
@@ -468,14 +509,17 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / GBK;
-  gload(0);
-  sstore(0, 0);
+  // split-K (small-M layers, part != nullptr): blockIdx.z takes K columns [kz0, kz0 + kc)
+  const int kc = om.part ? om.kchunk : K;
+  const int kz0 = om.part ? blockIdx.z * kc : 0;
+  const int nk = kc / GBK;
+  gload(kz0);
+  sstore(0, kz0);
   __syncthreads();
   const int fr = lane & 15, fc = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * GBK);
+    if (kt + 1 < nk) gload(kz0 + (kt + 1) * GBK);
     const bf16* sA = sA0 + cur * GBM * GLDK;
     const bf16* sB = sB0 + cur * BN * GLDK;
     bf16x8s af[4], bfr[TN];
@@ -488,10 +532,31 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    if (kt + 1 < nk) sstore(cur ^ 1, (kt + 1) * GBK);
+    if (kt + 1 < nk) sstore(cur ^ 1, kz0 + (kt + 1) * GBK);
     __syncthreads();
   }
 
+  if (om.part) {  // split-K partial: fp32 accumulators straight out, [z][M][N] (reduced by splitk_bias_act)
+    float* const pz = om.part + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int gn = n0 + wn * WN + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int gm = m0 + wm * 64 + i * 16 + (lane & 15);
+        if (gm >= M) continue;
+        float* q = pz + (int64_t)gm * N + gn;
+        if (gn + 3 < N && (N & 3) == 0) {
+          *(f32x4*)q = acc[i][j];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (gn + r < N) q[r] = acc[i][j][r];
+        }
+      }
+    }
+    return;
+  }
   // epilogue: bias + act, the bf16 tile staged in LDS (16-B chunks XOR-swizzled by row), then
   // written back as whole row segments, 16 B per lane (the direct 8-B-per-lane stores of 16-row
   // x 32-B fragments measured 1.4-1.9 TB/s on these write-heavy layers)
@@ -867,67 +932,87 @@ void vcx_im2col_nhwc(const void* x, void* out, int N, int H, int W, int C, int C
 
 void vcx_dwconv3x3(const void* x, const void* w, const float* b, void* y, int N, int H, int W, int C, int Ho, int Wo,
                    int stride, int relu, hipStream_t s) {
-  hipLaunchKernelGGL(dwconv3x3_kernel, dim3(stream_grid((int64_t)N * Ho * Wo * (C / 8), 256)), dim3(256), 0, s,
-                     (const bf16*)x, (const uint32_t*)w, b, (bf16*)y, N, H, W, C, Ho, Wo, stride, relu);
+  int sh = 0;
+  while ((8 << sh) < C) ++sh;
+  if ((8 << sh) != C) sh = -1;  // C8 = C / 8 = 1 << sh, or -1: not a power of two
+  const int bx = (Wo * (C / 8) + 255) / 256;
+  if (stride == 1) {
+    constexpr int R = 4;
+    hipLaunchKernelGGL((dwconv3x3_kernel<1, R>), dim3(bx, N * ((Ho + R - 1) / R)), dim3(256), 0, s, (const bf16*)x,
+                       (const uint32_t*)w, b, (bf16*)y, H, W, C, Ho, Wo, sh, relu);
+  } else {
+    constexpr int R = 2;
+    hipLaunchKernelGGL((dwconv3x3_kernel<2, R>), dim3(bx, N * ((Ho + R - 1) / R)), dim3(256), 0, s, (const bf16*)x,
+                       (const uint32_t*)w, b, (bf16*)y, H, W, C, Ho, Wo, sh, relu);
+  }
+}
+
+// K-split factor for a launch that would leave most CUs idle (the SSD extras and heads: M = 100..
+// 10,000 rows, K up to 2,304): each z-slice of the grid takes K / S columns, fp32 partials go to a
+// workspace and splitk_bias_act applies bias/ReLU/mapping. 1 = no split.
+int vcx_vision_ksplit(int M, int N, int K) {
+  const int nwg = ((M + GBM - 1) / GBM) * ((N + (N <= 64 ? 63 : 127)) / (N <= 64 ? 64 : 128));
+  if (nwg >= 192 || K < 256) return 1;
+  int S = std::min(8, std::min(K / 128, (384 + nwg - 1) / nwg));
+  while (S > 1 && (K / GBK) % S) --S;
+  return std::max(S, 1);
+}
+
+template <int AM>
+static void launch_gba(const bf16* X, const bf16* Wt, const float* bias, bf16* Y, int M, int N, int K, int ldy,
+                       int relu, OutMap om, const ConvGeom& cg, float* ws, int S, hipStream_t s) {
+  if (S > 1) {
+    om.part = ws;
+    om.kchunk = K / S;
+  }
+  const int tm = (M + GBM - 1) / GBM;
+  if (N <= 64)
+    hipLaunchKernelGGL((gemm_bias_act_kernel<64, AM>), dim3(tm * ((N + 63) / 64), 1, S), dim3(256), 0, s, X, Wt, bias,
+                       Y, M, N, K, ldy, relu, om, cg);
+  else
+    hipLaunchKernelGGL((gemm_bias_act_kernel<128, AM>), dim3(tm * ((N + 127) / 128), 1, S), dim3(256), 0, s, X, Wt,
+                       bias, Y, M, N, K, ldy, relu, om, cg);
+  if (S > 1) {
+    om.part = nullptr;
+    hipLaunchKernelGGL(splitk_bias_act_kernel, dim3(stream_grid((int64_t)M * N, 256)), dim3(256), 0, s, ws, S, bias,
+                       Y, M, N, ldy, relu, om);
+  }
 }
 
 void vcx_gemm_bias_act_mapped(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
                               int relu, void* Y2, int split, int ldy2, int rpi, int64_t img_stride,
-                              int64_t img_stride2, hipStream_t s) {
-  OutMap om{(bf16*)Y2, split, ldy2, rpi > 0 ? rpi : M, img_stride, img_stride2};
+                              int64_t img_stride2, float* ws, int S, hipStream_t s) {
+  OutMap om{(bf16*)Y2, split, ldy2, rpi > 0 ? rpi : M, img_stride, img_stride2, nullptr, 0};
   ConvGeom cg{};
-  if (N <= 64) {
-    const int nwg = ((M + GBM - 1) / GBM) * ((N + 63) / 64);
-    hipLaunchKernelGGL((gemm_bias_act_kernel<64, AM_PLAIN>), dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt,
-                       bias, (bf16*)Y, M, N, K, ldy, relu, om, cg);
-  } else {
-    const int nwg = ((M + GBM - 1) / GBM) * ((N + 127) / 128);
-    hipLaunchKernelGGL((gemm_bias_act_kernel<128, AM_PLAIN>), dim3(nwg), dim3(256), 0, s, (const bf16*)X, (const bf16*)Wt,
-                       bias, (bf16*)Y, M, N, K, ldy, relu, om, cg);
-  }
+  launch_gba<AM_PLAIN>((const bf16*)X, (const bf16*)Wt, bias, (bf16*)Y, M, N, K, ldy, relu, om, cg, ws, S, s);
 }
 
 // Y [imgs*Ho*Wo, N] = act(conv(x) + bias): x NHWC [imgs, H, W, Cs] (C used channels), weights
 // Wt [N, Kp] with columns (ky, kx, c), Kp % 32 == 0 (zero beyond KH*KW*C)
 void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y, int imgs, int H, int W, int C,
-                       int Cs, int KH, int KW, int stride, int pad, int N, int Kp, int relu, hipStream_t s) {
+                       int Cs, int KH, int KW, int stride, int pad, int N, int Kp, int relu, float* ws, int S,
+                       hipStream_t s) {
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   const int M = imgs * Ho * Wo;
-  OutMap om{nullptr, N, 0, M, 0, 0};
+  OutMap om{nullptr, N, 0, M, 0, 0, nullptr, 0};
   ConvGeom cg{H, W, C, Cs, Ho, Wo, KW, stride, pad, KH * KW * C, nullptr, nullptr, 0};
-  if (N <= 64) {
-    const int nwg = ((M + GBM - 1) / GBM) * ((N + 63) / 64);
-    hipLaunchKernelGGL((gemm_bias_act_kernel<64, AM_IMPLICIT>), dim3(nwg), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt,
-                       bias, (bf16*)Y, M, N, Kp, N, relu, om, cg);
-  } else {
-    const int nwg = ((M + GBM - 1) / GBM) * ((N + 127) / 128);
-    hipLaunchKernelGGL((gemm_bias_act_kernel<128, AM_IMPLICIT>), dim3(nwg), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt,
-                       bias, (bf16*)Y, M, N, Kp, N, relu, om, cg);
-  }
+  launch_gba<AM_IMPLICIT>((const bf16*)x, (const bf16*)Wt, bias, (bf16*)Y, M, N, Kp, N, relu, om, cg, ws, S, s);
 }
 
 // depthwise 3x3 (pad 1) + bias (+ReLU) -> pointwise GEMM + bias (+ReLU), one kernel:
-// x NHWC [imgs, H, W, K], dw_w [9][K], dw_b [K], Wt [N, K] -> Y [imgs*Ho*Wo, N]
+// x NHWC [imgs, H, W, K], dw_w [5][K] paired, dw_b [K], Wt [N, K] -> Y [imgs*Ho*Wo, N]
 void vcx_dw_pw(const void* x, const void* dw_w, const float* dw_b, int dw_relu, const void* Wt, const float* bias,
                void* Y, int imgs, int H, int W, int K, int stride, int N, int relu, hipStream_t s) {
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   const int M = imgs * Ho * Wo;
-  OutMap om{nullptr, N, 0, M, 0, 0};
+  OutMap om{nullptr, N, 0, M, 0, 0, nullptr, 0};
   ConvGeom cg{H, W, K, K, Ho, Wo, 3, stride, 1, 9 * K, (const uint32_t*)dw_w, dw_b, dw_relu};
-  if (N <= 64) {
-    const int nwg = ((M + GBM - 1) / GBM) * ((N + 63) / 64);
-    hipLaunchKernelGGL((gemm_bias_act_kernel<64, AM_DW>), dim3(nwg), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt,
-                       bias, (bf16*)Y, M, N, K, N, relu, om, cg);
-  } else {
-    const int nwg = ((M + GBM - 1) / GBM) * ((N + 127) / 128);
-    hipLaunchKernelGGL((gemm_bias_act_kernel<128, AM_DW>), dim3(nwg), dim3(256), 0, s, (const bf16*)x,
-                       (const bf16*)Wt, bias, (bf16*)Y, M, N, K, N, relu, om, cg);
-  }
+  launch_gba<AM_DW>((const bf16*)x, (const bf16*)Wt, bias, (bf16*)Y, M, N, K, N, relu, om, cg, nullptr, 1, s);
 }
 
 void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
-                       int relu, hipStream_t s) {
-  vcx_gemm_bias_act_mapped(X, Wt, bias, Y, M, N, K, ldy, relu, nullptr, N, 0, M, 0, 0, s);
+                       int relu, float* ws, int S, hipStream_t s) {
+  vcx_gemm_bias_act_mapped(X, Wt, bias, Y, M, N, K, ldy, relu, nullptr, N, 0, M, 0, 0, ws, S, s);
 }
 
 void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* prob,

@@ -10,5 +10,7 @@ timeout -k 10 120 python -u scripts/video_layers.py 10 > $O/layers_fused.log 2>&
 VCX_DWPW_MAX_COUT=0 timeout -k 10 120 python -u scripts/video_layers.py 10 > $O/layers_unfused.log 2>&1 || exit $?
 VCX_DWPW_MAX_COUT=1024 timeout -k 10 120 python -u scripts/video_layers.py 10 > $O/layers_fuseall.log 2>&1 || exit $?
 tail -n 1 $O/layers_*.log
-timeout -k 10 200 python -u scripts/gemm_p_bench.py --gemm4 > $O/gemm4.log 2>&1; echo "gemm4 rc=$?"
-tail -n 20 $O/gemm4.log
+if [ -n "$GEMM4" ]; then
+  timeout -k 10 200 python -u scripts/gemm_p_bench.py --gemm4 > $O/gemm4.log 2>&1; echo "gemm4 rc=$?"
+  tail -n 20 $O/gemm4.log
+fi

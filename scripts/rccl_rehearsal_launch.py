@@ -38,12 +38,15 @@ def main() -> int:
     ap.add_argument("--nproc", type=int, default=2)
     ap.add_argument("--timeout", type=float, default=300.0)
     ap.add_argument("--log-dir", default=None, help="per-rank stdout/stderr files (default: inherit)")
+    ap.add_argument("--expect-killed", default="", help="comma-separated ranks that SIGKILL themselves on purpose "
+                    "(fault-injection runs): their -9 exit does not end the job")
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
     if not cmd:
         ap.error("no command")
     port = free_port()
+    victims = {int(r) for r in a.expect_killed.split(",") if r.strip()}
     procs = []
     for r in range(a.nproc):
         env = dict(os.environ)
@@ -62,11 +65,13 @@ def main() -> int:
         for i, p in enumerate(procs):
             if codes[i] is None:
                 codes[i] = p.poll()
-        if any(c not in (None, 0) for c in codes) or time.monotonic() > deadline:
+        bad = [c for i, c in enumerate(codes) if c not in (None, 0) and not (i in victims and c == -signal.SIGKILL)]
+        if bad or time.monotonic() > deadline:
             break
         time.sleep(0.1)
     timed_out = any(c is None for c in codes) and time.monotonic() > deadline
-    first_bad = next((c for c in codes if c not in (None, 0)), None)  # the failure that ended the job
+    first_bad = next((c for i, c in enumerate(codes) if c not in (None, 0)
+                      and not (i in victims and c == -signal.SIGKILL)), None)  # the failure that ended the job
     for i, p in enumerate(procs):  # a failed or hung rank ends the whole job
         if p.poll() is None:
             try:
