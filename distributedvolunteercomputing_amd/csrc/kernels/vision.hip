@@ -257,9 +257,10 @@ __global__ void __launch_bounds__(256) dwconv3x3_kernel(const bf16* __restrict__
                                                          const float* __restrict__ b, bf16* __restrict__ y, int H,
                                                          int W, int C, int Ho, int Wo, int c8_shift, int relu) {
   constexpr int NR = (R - 1) * STRIDE + 3;  // input rows per thread
-  const int C8 = 1 << c8_shift;
+  const int C8 = C >> 3;
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  const int ox = idx >> c8_shift, c8 = idx & (C8 - 1);
+  const int ox = c8_shift >= 0 ? idx >> c8_shift : idx / C8;  // (C8 not a power of two: a divide)
+  const int c8 = idx - ox * C8;
   if (ox >= Wo) return;
   const int groups = (Ho + R - 1) / R;
   const int n = blockIdx.y / groups, oy0 = (blockIdx.y - n * groups) * R;

@@ -121,6 +121,8 @@ class SSDExecutor:
         self.input_size = int(net.input_shapes[0][2]) if net.input_shapes else 300
         self._prior_cache = {}
         self.step_events = None
+        self.use_graph = os.environ.get("VCX_VISION_GRAPH", "1") != "0"
+        self._graphs = {}
         self._plan = self._compile() if self.device.type == "cuda" else None
 
     # ------------------------------------------------------------------ compile
@@ -415,9 +417,38 @@ class SSDExecutor:
         return [(n, k, s / iters) for n, k, s in acc]
 
     def detect(self, frames_u8: torch.Tensor):
-        """frames [N, H, W, 3] uint8 BGR (already at the annotation size) -> (dets, counts)."""
+        """frames [N, H, W, 3] uint8 BGR (already at the annotation size) -> (dets, counts).
+        On the GPU the whole chunk (blob + ~60 kernels of the plan + detection) replays as one HIP
+        graph per input shape: eager launching costs ~25 us of host time per plan step, as much
+        as the network's GPU time (VCX_VISION_GRAPH=0 runs it eagerly)."""
+        if self._plan is not None and self.use_graph and frames_u8.is_cuda:
+            return self._detect_graphed(frames_u8)
         blob = V.blob_from_frames(frames_u8, self.input_size)
         return self.forward_blob(blob)["detection_out"]
+
+    def _detect_eager(self, frames_u8):
+        return self.forward_blob(V.blob_from_frames(frames_u8, self.input_size))["detection_out"]
+
+    def _detect_graphed(self, frames_u8):
+        key = (tuple(frames_u8.shape), frames_u8.device.index)
+        g = self._graphs.get(key)
+        if g is None:
+            static_in = frames_u8.clone()
+            side = torch.cuda.Stream(frames_u8.device)
+            side.wait_stream(torch.cuda.current_stream(frames_u8.device))
+            with torch.cuda.stream(side):  # warm-up: priors cached, allocator primed
+                for _ in range(2):
+                    self._detect_eager(static_in)
+            torch.cuda.current_stream(frames_u8.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static_out = self._detect_eager(static_in)
+            g = self._graphs[key] = (graph, static_in, static_out)
+        graph, static_in, (dets, cnt) = g
+        static_in.copy_(frames_u8)
+        graph.replay()
+        # the next replay overwrites the graph's buffers: hand out copies (280 KB per 100 frames)
+        return dets.clone(), cnt.clone()
 
 
 def smoke_detect(dev):

@@ -40,6 +40,21 @@ for r in rows:
     by_kind[r["kind"]] = round(by_kind.get(r["kind"], 0.0) + r["us"], 1)
 print(json.dumps({"total_ms": round(total, 3), "by_kind_us": by_kind}), flush=True)
 
+# the same network as the engine runs it: one HIP graph replay per chunk (blob + plan + detection)
+for mode in ("graph", "eager"):
+    ex.use_graph = mode == "graph"
+    ex.detect(frames)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(it):
+        ex.detect(frames)
+    e1.record()
+    torch.cuda.synchronize()
+    print(json.dumps({"detect_chunk_ms": round(e0.elapsed_time(e1) / it, 3), "mode": mode, "frames": 100}),
+          flush=True)
+ex.use_graph = True
+
 # preprocessing of the same chunk from 720p: INTER_AREA to 400 px, then the 300x300 blob
 big = torch.randint(0, 256, (100, 720, 1280, 3), dtype=torch.uint8, device=dev)
 for name, fn in (("resize_area 720p->400", lambda: V.resize_width(big, 400)),

@@ -213,3 +213,19 @@ def test_executor_matches_caffe_reference(gpu):
                             and max(abs(x - y) for x, y in zip(a[3:], b[3:])) < 2e-3), None)
                 assert hit is not None, (scale, n, a)
                 used[hit] = True
+
+
+def test_detect_graph_replay_matches_eager(gpu):
+    """The chunk's HIP-graph replay (the engine's path) returns what eager launching returns,
+    for two different inputs through the same captured graph."""
+    ex = SSDExecutor(device=gpu)
+    torch.manual_seed(7)
+    for _ in range(2):
+        frames = torch.randint(0, 256, (4, 225, 400, 3), dtype=torch.uint8, device=gpu)
+        ex.use_graph = True
+        dg, cg = ex.detect(frames)
+        ex.use_graph = False
+        de, ce = ex.detect(frames)
+        assert torch.equal(cg, ce)
+        assert torch.equal(dg, de)
+    assert len(ex._graphs) == 1
