@@ -93,6 +93,9 @@ void f32_to_bf16(at::Tensor src, at::Tensor dst) {
 // C[M, N] = A[M, K] . B[N, K]^T with epilogue: 0 store, 1 +bias, 2 +bias -> (C = pre, C2 = gelu(pre)),
 // 3 C = acc * gelu'(C2) with fp32 column sums added into `colsum` (must be zeroed by the caller)
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) { return vcx_gemm_nt_supported((int)M, (int)N, (int)K); }
+bool gemm_nt_supported_epi(int64_t M, int64_t N, int64_t K, int64_t epi) {
+  return vcx_gemm_nt_supported_epi((int)M, (int)N, (int)K, (int)epi);
+}
 
 void gemm_nt(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor> c2, c10::optional<at::Tensor> bias,
              c10::optional<at::Tensor> colsum, int64_t epi) {
@@ -102,20 +105,22 @@ void gemm_nt(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm_nt: K-contiguous rows");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_nt: shape mismatch");
-  TORCH_CHECK(vcx_gemm_nt_supported((int)M, (int)N, (int)K), "gemm_nt: needs M % 256 == 0, N % 256 == 0, K % 64 == 0, K >= 128");
+  TORCH_CHECK(vcx_gemm_nt_supported_epi((int)M, (int)N, (int)K, (int)epi),
+              "gemm_nt: needs N % 256 == 0, K % 64 == 0, K >= 128, and M % 256 == 0 for epilogues 2/3");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm_nt: 16-B aligned rows");
   // the kernel moves 16 B per lane: a column-offset view (e.g. c[:, 4:260]) would be misaligned
   for (const at::Tensor* t : {&a, &b, &c})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_nt: 16-B aligned base pointers");
+  TORCH_CHECK(epi >= 0 && epi <= 4, "gemm_nt: epilogue 0..4");
   void* c2p = nullptr;
-  if (epi >= 2) {
+  if (epi == 2 || epi == 3) {
     TORCH_CHECK(c2 && c2->sizes() == c.sizes() && c2->strides() == c.strides() && c2->scalar_type() == at::kBFloat16,
                 "gemm_nt: epilogue 2/3 needs c2 like c");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(c2->data_ptr()) % 16 == 0, "gemm_nt: 16-B aligned c2");
     c2p = c2->data_ptr();
   }
   const void* bp = nullptr;
-  if (epi == 1 || epi == 2) {
+  if (epi == 1 || epi == 2 || epi == 4) {
     TORCH_CHECK(bias && bias->numel() == N && bias->is_contiguous() && bias->scalar_type() == at::kBFloat16,
                 "gemm_nt: bias [N] bf16");
     bp = bias->data_ptr();
@@ -666,6 +671,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("axpy_bf16", &axpy_bf16);
   m.def("reduce_bcast_bf16", &reduce_bcast_bf16);
   m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt_supported_epi", &gemm_nt_supported_epi);
   m.def("gemm_p_supported", &gemm_p_supported);
   m.def("gemm4", &gemm4);
   m.def("gemm_p", &gemm_p, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),

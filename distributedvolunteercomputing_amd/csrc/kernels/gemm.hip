@@ -43,7 +43,7 @@ constexpr int SLOT_A = BM * ROWB;              // 16 KB
 constexpr int SLOT_BYTES = (BM + BN) * ROWB;   // 32 KB
 constexpr int LDS_BYTES = NSLOT * SLOT_BYTES;  // 128 KB
 
-enum Epi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 3 };
+enum Epi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 3, EPI_BIAS_RELU = 4 };
 
 // chunk swizzle F[(row >> 2) & 3] = {0, 2, 3, 1}, packed 2 bits per entry
 __device__ __forceinline__ int swz(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
@@ -110,9 +110,11 @@ __global__ void __launch_bounds__(NT, 1)
   // row l >> 2, physical chunk l & 3, which holds logical chunk (l & 3) ^ swz(row) of that row
   const int prow = lane >> 2;
   const int pchunk = (lane & 3) ^ swz(prow);
-  const bf16* a_src = A + (int64_t)(m0 + wid * 16 + prow) * lda + pchunk * 8;
+  // ragged M (the detector's N*H*W rows): rows past M re-read row M - 1 (their outputs are never
+  // stored), so no load leaves the operand
+  const bf16* a_src = A + (int64_t)min(m0 + wid * 16 + prow, M - 1) * lda + pchunk * 8;
+  const bf16* a_src8 = A + (int64_t)min(m0 + wid * 16 + prow + 128, M - 1) * lda + pchunk * 8;  // piece w + 8
   const bf16* b_src = B + (int64_t)(n0 + wid * 16 + prow) * ldb + pchunk * 8;
-  const int64_t a_step8 = (int64_t)128 * lda;  // piece w + 8 is 128 rows further
   const int64_t b_step8 = (int64_t)128 * ldb;
   char* const lds_piece = smem + wid * 1024;
 
@@ -120,7 +122,7 @@ __global__ void __launch_bounds__(NT, 1)
     char* slot = lds_piece + (s & 3) * SLOT_BYTES;
     const int k0 = s * BKS;
     if (p == 0) glds16(a_src + k0, slot);
-    if (p == 1) glds16(a_src + a_step8 + k0, slot + 8 * 1024);
+    if (p == 1) glds16(a_src8 + k0, slot + 8 * 1024);
     if (p == 2) glds16(b_src + k0, slot + SLOT_A);
     if (p == 3) glds16(b_src + b_step8 + k0, slot + SLOT_A + 8 * 1024);
   };
@@ -233,7 +235,7 @@ __global__ void __launch_bounds__(NT, 1)
   const int mrow = m0 + wm * 128 + (lane & 15);
   const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
   float bsv[4][4];
-  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const bf16x4 bv = *(const bf16x4*)(bias + ncol + 16 * j);
@@ -263,11 +265,12 @@ __global__ void __launch_bounds__(NT, 1)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int k = lane & 7;
     bf16* base = dst + (int64_t)(m0 + wm * 128) * ldc + n0 + wn * 64 + k * 8;
+    const int mrem = M - (m0 + wm * 128);  // rows of this wave's block inside M
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int r = it * 8 + (lane >> 3);
       const bf16x8 v = *(const bf16x8*)(stg + r * 128 + ((k ^ (r & 7)) << 4));
-      *(bf16x8*)(base + (int64_t)r * ldc) = v;
+      if (r < mrem) *(bf16x8*)(base + (int64_t)r * ldc) = v;
     }
   };
 #pragma unroll
@@ -282,6 +285,9 @@ __global__ void __launch_bounds__(NT, 1)
       } else if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) out[t] = (bf16)(acc[i][j][t] + bsv[j][t]);
+      } else if constexpr (EPI == EPI_BIAS_RELU) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) out[t] = (bf16)fmaxf(acc[i][j][t] + bsv[j][t], 0.f);
       } else {  // EPI_DGELU: C2 holds the pre-activation, acc the gradient w.r.t. gelu(pre)
         const bf16x4 pre = *(const bf16x4*)(C2 + rowoff + ncol + 16 * j);
 #pragma unroll
@@ -588,14 +594,22 @@ bool vcx_gemm_nt_supported(int M, int N, int K) {
   return M > 0 && N > 0 && K >= 128 && M % gemm::BM == 0 && N % gemm::BN == 0 && K % 64 == 0;
 }
 
+// epilogues without a second operand read (STORE, BIAS, BIAS_RELU) also take a ragged M
+bool vcx_gemm_nt_supported_epi(int M, int N, int K, int epi) {
+  if (epi == gemm::EPI_STORE || epi == gemm::EPI_BIAS || epi == gemm::EPI_BIAS_RELU)
+    return M > 0 && N > 0 && K >= 128 && N % gemm::BN == 0 && K % 64 == 0;
+  return epi >= 0 && epi <= 3 && vcx_gemm_nt_supported(M, N, K);
+}
+
 // C = A . B^T with epilogue `epi` (gemm::Epi); colsum (EPI_DGELU) must be zeroed by the caller.
 void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,
                  int lda, int ldb, int ldc, int epi, hipStream_t s) {
   using namespace gemm;
-  const int tilesN = N / BN, tiles = (M / BM) * tilesN;
+  const int tilesN = N / BN, tiles = ((M + BM - 1) / BM) * tilesN;
   static const bool attrs = [] {  // 128 KB of dynamic LDS per workgroup (above the 64 KB default)
     for (const void* k : {(const void*)gemm_nt_kernel<EPI_STORE>, (const void*)gemm_nt_kernel<EPI_BIAS>,
-                          (const void*)gemm_nt_kernel<EPI_BIAS_GELU>, (const void*)gemm_nt_kernel<EPI_DGELU>})
+                          (const void*)gemm_nt_kernel<EPI_BIAS_GELU>, (const void*)gemm_nt_kernel<EPI_DGELU>,
+                          (const void*)gemm_nt_kernel<EPI_BIAS_RELU>})
       hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     return true;
   }();
@@ -608,6 +622,7 @@ void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bi
     case EPI_STORE: args(gemm_nt_kernel<EPI_STORE>); break;
     case EPI_BIAS: args(gemm_nt_kernel<EPI_BIAS>); break;
     case EPI_BIAS_GELU: args(gemm_nt_kernel<EPI_BIAS_GELU>); break;
+    case EPI_BIAS_RELU: args(gemm_nt_kernel<EPI_BIAS_RELU>); break;
     default: args(gemm_nt_kernel<EPI_DGELU>); break;
   }
 }

@@ -18,6 +18,7 @@ bool vcx_gemm_tn_supported(int M, int N, int K, int splits);
 void vcx_gemm_tn(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
                  int splits, int accumulate, hipStream_t s);
 bool vcx_gemm_nt_supported(int M, int N, int K);
+bool vcx_gemm_nt_supported_epi(int M, int N, int K, int epi);
 void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,
                  int lda, int ldb, int ldc, int epi, hipStream_t s);
 // gemm_persistent.hip: persistent role-split GEMM, layout 0: C = A B^T (B [N, K]), 1: C = A B (B [K, N])

@@ -1,7 +1,10 @@
 // pybind11 module `_native`: host runtime of the volunteer-computing framework.
-// All blocking calls release the GIL.
+// All blocking calls release the GIL (without_gil: never re-entering a finalizing interpreter).
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#include <unistd.h>
+
+#include <algorithm>
 
 #include "colour.h"
 #include "scheduler.h"
@@ -24,6 +27,38 @@ void require_c_contiguous(const py::buffer_info& b, const char* what) {
   for (int d = (int)b.ndim - 1; d >= 0; --d) {
     if (b.shape[d] > 1 && b.strides[d] != expect) throw std::invalid_argument(std::string(what) + ": not C-contiguous");
     expect *= b.shape[d];
+  }
+}
+
+// Blocking calls run without the GIL. A daemon Python thread still inside one when the
+// interpreter finalizes is pthread_exit()ed the moment it re-takes the GIL; from inside
+// gil_scoped_release's (noexcept) destructor that forced unwind is a std::terminate — "terminate
+// called without an active exception", exit status 134 after an otherwise clean run. Such a
+// thread parks instead of re-entering the interpreter; process exit reclaims it.
+[[noreturn]] void park_forever() {
+  for (;;) ::pause();
+}
+
+template <class F>
+auto without_gil(F&& f) {
+  PyThreadState* ts = PyEval_SaveThread();
+  auto r = f();
+  if (_Py_IsFinalizing()) park_forever();
+  PyEval_RestoreThread(ts);
+  return r;
+}
+
+// Hub::recv in slices of <= 100 ms, so a finalizing interpreter is noticed promptly
+bool recv_sliced(Hub& h, Frame* f, double timeout) {
+  for (;;) {
+    const double slice = timeout < 0 ? 0.1 : std::min(timeout, 0.1);
+    if (h.recv(f, slice)) return true;
+    if (_Py_IsFinalizing()) park_forever();
+    if (timeout >= 0) {
+      timeout -= slice;
+      if (timeout <= 0) return false;
+    }
+    if (h.closed()) return false;
   }
 }
 
@@ -50,24 +85,22 @@ PYBIND11_MODULE(_native, m) {
           "recv",
           [](Hub& h, double timeout) -> py::object {
             auto pf = std::make_unique<PyFrame>();
-            bool ok;
-            {
-              py::gil_scoped_release rel;
-              ok = h.recv(&pf->f, timeout);
-            }
+            const bool ok = without_gil([&] { return recv_sliced(h, &pf->f, timeout); });
             if (!ok) return py::none();
             return py::cast(pf.release(), py::return_value_policy::take_ownership);
           },
           py::arg("timeout") = -1.0)
       .def("pending", &Hub::pending)
-      .def("close", &Hub::close, py::call_guard<py::gil_scoped_release>())
+      .def("close", [](Hub& h) { without_gil([&] { h.close(); return 0; }); })
       .def_property_readonly("frames_received", &Hub::frames_received)
       .def_property_readonly("bytes_received", &Hub::bytes_received)
       .def_property_readonly("frames_rejected", &Hub::frames_rejected);
 
   py::class_<Sender>(m, "Sender")
-      .def(py::init<const std::string&, int, bool, double>(), py::arg("host"), py::arg("port"),
-           py::arg("ack") = true, py::arg("connect_timeout") = 10.0, py::call_guard<py::gil_scoped_release>())
+      .def(py::init([](const std::string& host, int port, bool ack, double connect_timeout) {
+             return without_gil([&] { return new Sender(host, port, ack, connect_timeout); });
+           }),
+           py::arg("host"), py::arg("port"), py::arg("ack") = true, py::arg("connect_timeout") = 10.0)
       .def(
           "send",
           [](Sender& s, const std::string& header, py::buffer payload, double timeout) {
@@ -83,8 +116,7 @@ PYBIND11_MODULE(_native, m) {
               }
             }
             const uint8_t* ptr = (const uint8_t*)bi.ptr;
-            py::gil_scoped_release rel;
-            return s.send(header, ptr, n, timeout);
+            return without_gil([&] { return s.send(header, ptr, n, timeout); });
           },
           py::arg("header"), py::arg("payload"), py::arg("timeout") = 60.0)
       .def("close", &Sender::close)
@@ -131,8 +163,10 @@ PYBIND11_MODULE(_native, m) {
         require_c_contiguous(b, "bgr_to_yuv444 dst");
         if (a.size * a.itemsize < 3 * w * h || b.size * b.itemsize < 3 * w * h)
           throw std::invalid_argument("bgr_to_yuv444: buffers smaller than 3 * w * h bytes");
-        py::gil_scoped_release rel;
-        bgr_to_yuv444((const uint8_t*)a.ptr, (uint8_t*)b.ptr, w, h);
+        without_gil([&] {
+          bgr_to_yuv444((const uint8_t*)a.ptr, (uint8_t*)b.ptr, w, h);
+          return 0;
+        });
       },
       py::arg("src"), py::arg("dst"), py::arg("w"), py::arg("h"));
   m.def(
@@ -144,8 +178,10 @@ PYBIND11_MODULE(_native, m) {
         if ((cw != w && cw != (w + 1) / 2) || Y.size < w * h || U.size < cw * ch || V.size < cw * ch ||
             D.size < 3 * w * h)
           throw std::invalid_argument("yuv_to_bgr: plane sizes do not match w, h, cw");
-        py::gil_scoped_release rel;
-        yuv_to_bgr((const uint8_t*)Y.ptr, (const uint8_t*)U.ptr, (const uint8_t*)V.ptr, (uint8_t*)D.ptr, w, h, cw);
+        without_gil([&] {
+          yuv_to_bgr((const uint8_t*)Y.ptr, (const uint8_t*)U.ptr, (const uint8_t*)V.ptr, (uint8_t*)D.ptr, w, h, cw);
+          return 0;
+        });
       },
       py::arg("y"), py::arg("u"), py::arg("v"), py::arg("dst"), py::arg("w"), py::arg("h"), py::arg("cw"));
 

@@ -46,6 +46,7 @@ class Hub {
   bool recv(Frame* out, double timeout_s);
   size_t pending();
   void close();
+  bool closed() const { return closed_.load(); }
   uint64_t frames_received() const { return frames_; }
   uint64_t bytes_received() const { return bytes_; }
   uint64_t frames_rejected() const { return rejected_; }

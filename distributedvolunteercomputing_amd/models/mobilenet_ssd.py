@@ -122,6 +122,7 @@ class SSDExecutor:
         self._prior_cache = {}
         self.step_events = None
         self.use_graph = os.environ.get("VCX_VISION_GRAPH", "1") != "0"
+        self.pw_gemm = os.environ.get("VCX_VISION_PW", "nt")  # nt: gemm_nt where it applies | vision
         self._graphs = {}
         self._plan = self._compile() if self.device.type == "cuda" else None
 
@@ -216,7 +217,7 @@ class SSDExecutor:
                                                stride=stride, relu=relu)))
                 elif k == 1 and stride == 1 and pad == 0 and cin % 32 == 0:
                     wt = w.detach().float().reshape(cout, cin).to(dev, torch.bfloat16).contiguous()
-                    plan.append(("pw", l, dict(w=wt, b=bias, relu=relu)))
+                    plan.append(("pw", l, dict(w=wt, b=bias, b16=bias.to(torch.bfloat16), relu=relu)))
                 else:
                     # implicit GEMM: columns (ky, kx, c); the 3-channel stem reads the 4-channel
                     # padded blob (c = 3 has zero weights) as two taps per 16-B load
@@ -347,7 +348,15 @@ class SSDExecutor:
             elif kind == "pw":
                 H, W = hw[src]
                 M = N * H * W
-                y = V.gemm_bias_act(x.reshape(M, x.shape[-1]), p["w"], p["b"], p["relu"])
+                K, Co = x.shape[-1], p["w"].shape[0]
+                epi = 4 if p["relu"] else 1
+                if self.pw_gemm == "nt" and ops.native().gemm_nt_supported_epi(M, Co, K, epi):
+                    # the wide pointwise layers (K, Cout >= 256) on the training GEMM: 256 x 256
+                    # tiles, LDS-DMA ring, bias(+ReLU) epilogue, ragged M
+                    y = torch.empty(M, Co, device=x.device, dtype=torch.bfloat16)
+                    ops.native().gemm_nt(x.reshape(M, K), p["w"], y, None, p["b16"], None, epi)
+                else:
+                    y = V.gemm_bias_act(x.reshape(M, K), p["w"], p["b"], p["relu"])
                 t[top], layout[top], hw[top], chans[top] = y.view(N, H, W, -1), "nhwc", (H, W), y.shape[1]
             elif kind == "head":
                 x = t[p["src"]]
