@@ -37,6 +37,7 @@ at::Tensor resize_bilinear_u8(at::Tensor src, int64_t h, int64_t w) {
 at::Tensor blob_bilinear(at::Tensor src, int64_t S, double scale, double mean) {
   CHK(src, at::kByte);
   TORCH_CHECK(src.dim() == 4 && src.size(3) == 3 && S > 0);
+  TORCH_CHECK(src.size(0) <= 65535 && S <= 65535, "blob_bilinear: grid limits");
   auto dst = at::empty({src.size(0), S, S, 4}, src.options().dtype(at::kBFloat16));
   vcx_blob_bilinear(src.data_ptr<uint8_t>(), dst.data_ptr(), (int)src.size(0), (int)src.size(1), (int)src.size(2),
                     (int)S, (float)scale, (float)mean, cur_stream());

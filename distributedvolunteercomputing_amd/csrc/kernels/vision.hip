@@ -152,28 +152,33 @@ __global__ void __launch_bounds__(256) resize_bilinear_u8_kernel(const uint8_t* 
 
 // (c) cv2.resize(frame, (S,S)) bilinear -> blobFromImage(scale, mean) -> NHWC bf16, channel
 //     padded to CP (=4) lanes with zeros: [N, S, S, CP]. BGR order kept (no swapRB).
-__global__ void __launch_bounds__(256) blob_bilinear_kernel(const uint8_t* __restrict__ src, bf16* __restrict__ dst,
+//     3-D grid: blockIdx.z = image, blockIdx.y = output row, so the source rows and vertical weights are
+//     scalar; one thread per output column (the grid-stride version with 64-bit index division
+//     per pixel ran at 1.7 TB/s).
+__global__ void __launch_bounds__(320) blob_bilinear_kernel(const uint8_t* __restrict__ src, bf16* __restrict__ dst,
                                                              int N, int H, int W, int S, float scale, float mean) {
-  const int64_t total = (int64_t)N * S * S;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= S) return;
+  const int n = blockIdx.z, y = blockIdx.y;
   const float sx = (float)W / S, sy = (float)H / S;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int x = (int)(i % S), y = (int)((i / S) % S), n = (int)(i / ((int64_t)S * S));
-    float fx = fmaxf((x + 0.5f) * sx - 0.5f, 0.f), fy = fmaxf((y + 0.5f) * sy - 0.5f, 0.f);
-    int x0 = min((int)fx, W - 1), y0 = min((int)fy, H - 1);
-    int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
-    float ax = fx - x0, ay = fy - y0;
-    const uint8_t* b = src + (int64_t)n * H * W * 3;
-    bf16x4 o;
-    for (int c = 0; c < 3; ++c) {
-      float v00 = b[((int64_t)y0 * W + x0) * 3 + c], v01 = b[((int64_t)y0 * W + x1) * 3 + c];
-      float v10 = b[((int64_t)y1 * W + x0) * 3 + c], v11 = b[((int64_t)y1 * W + x1) * 3 + c];
-      float v = (v00 * (1 - ax) + v01 * ax) * (1 - ay) + (v10 * (1 - ax) + v11 * ax) * ay;
-      v = rintf(fminf(255.f, fmaxf(0.f, v)));  // cv2.resize output is uint8
-      o[c] = (bf16)((v - mean) * scale);
-    }
-    o[3] = (bf16)0.f;
-    *(bf16x4*)(dst + i * 4) = o;
+  const float fy = fmaxf((y + 0.5f) * sy - 0.5f, 0.f);
+  const int y0 = min((int)fy, H - 1), y1 = min(y0 + 1, H - 1);
+  const float ay = fy - y0;
+  const float fx = fmaxf((x + 0.5f) * sx - 0.5f, 0.f);
+  const int x0 = min((int)fx, W - 1), x1 = min(x0 + 1, W - 1);
+  const float ax = fx - x0;
+  const uint8_t* r0 = src + ((int64_t)n * H + y0) * W * 3;
+  const uint8_t* r1 = src + ((int64_t)n * H + y1) * W * 3;
+  bf16x4 o;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float v00 = r0[x0 * 3 + c], v01 = r0[x1 * 3 + c], v10 = r1[x0 * 3 + c], v11 = r1[x1 * 3 + c];
+    float v = (v00 * (1 - ax) + v01 * ax) * (1 - ay) + (v10 * (1 - ax) + v11 * ax) * ay;
+    v = rintf(fminf(255.f, fmaxf(0.f, v)));  // cv2.resize output is uint8
+    o[c] = (bf16)((v - mean) * scale);
   }
+  o[3] = (bf16)0.f;
+  *(bf16x4*)(dst + (((int64_t)n * S + y) * S + x) * 4) = o;
 }
 
 // =====================================================================================
@@ -265,18 +270,21 @@ __global__ void __launch_bounds__(256) dwconv3x3_kernel(const bf16* __restrict__
   const int groups = (Ho + R - 1) / R;
   const int n = blockIdx.y / groups, oy0 = (blockIdx.y - n * groups) * R;
   const int iy0 = oy0 * STRIDE - 1, ix0 = ox * STRIDE - 1;
-  const bf16* xn = x + (int64_t)n * H * W * C + c8 * 8;
+  // taps through a buffer resource over this image: rows above/below the image fall outside the
+  // resource and read as zero (the pad), so only the left/right pad columns need a mask
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + (int64_t)n * H * W * C), (short)0,
+                                                    H * W * C * 2, 0x00020000);
+  const int rowb = W * C * 2, pixb = C * 2;
+  const int base = (iy0 * W + ix0) * pixb + c8 * 16;
+  int coff[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) coff[kx] = (ix0 + kx >= 0 && ix0 + kx < W) ? base + kx * pixb : (int)0x80000000;
   u32x4 xv[NR][3];
 #pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int iy = iy0 + r;
+  for (int r = 0; r < NR; ++r)
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int ix = ix0 + kx;
-      xv[r][kx] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? *(const u32x4*)(xn + ((int64_t)iy * W + ix) * C)
-                                                           : u32x4{0u, 0u, 0u, 0u};
-    }
-  }
+    for (int kx = 0; kx < 3; ++kx)
+      xv[r][kx] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, coff[kx] + r * rowb, 0, 0));
   f32x4 b0 = *(const f32x4*)(b + c8 * 8), b1 = *(const f32x4*)(b + c8 * 8 + 4);
 #pragma unroll
   for (int j = 0; j < R; ++j) {
@@ -610,6 +618,72 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
 }
 
 // =====================================================================================
+// K4: the stem, conv0 3x3 (stride 2, pad 1) over the 4-channel padded blob, as MFMA fed straight
+// from global memory: with K = 9 taps x 4 channels the v_mfma_f32_16x16x32_bf16 operand a lane
+// holds (8 consecutive k = two whole taps of one pixel) is exactly two 8-B loads, so neither an
+// LDS tile nor an im2col exists; the weight fragments (Cout x 64 k) stay in registers for the
+// wave's life. One wave = 64 output pixels (4 MFMA row groups) x COUT channels.
+// (The generic implicit GEMM spent 119 us on this layer: 2 K-steps per 128-row tile, half of
+// every 64-wide N tile idle.)
+// =====================================================================================
+template <int COUT>
+__global__ void __launch_bounds__(256) stem_conv_c4_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wt,
+                                                            const float* __restrict__ bias, bf16* __restrict__ y,
+                                                            int M, int H, int W, int Ho, int Wo, int stride, int pad,
+                                                            int relu) {
+  constexpr int NT = COUT / 16;
+  typedef short sx4v __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  // weight fragments: out channel 16 t + r, k = 32 s + 8 q .. + 7 (columns (ky, kx, c), Kp = 64)
+  bf16x8s wf[NT][2];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) wf[t][st] = *(const bf16x8s*)(wt + (16 * t + r) * 64 + 32 * st + 8 * q);
+  float bv[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[t][i] = bias[16 * t + 4 * q + i];
+  const int hw = Ho * Wo;
+  auto tap = [&](int img, int iy0, int ix0, int tp) -> sx4v {  // 4 channels of tap tp, or zeros
+    if (tp >= 9) return sx4v{0, 0, 0, 0};
+    const int iy = iy0 + tp / 3, ix = ix0 + tp % 3;
+    if (iy < 0 || iy >= H || ix < 0 || ix >= W) return sx4v{0, 0, 0, 0};
+    return *(const sx4v*)(x + (((int64_t)img * H + iy) * W + ix) * 4);
+  };
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int m = wave * 64 + g * 16 + r;  // this lane's pixel in MFMA row group g
+    const bool ok = m < M;
+    const int mm = ok ? m : M - 1;
+    const int img = mm / hw, rem = mm - img * hw, oy = rem / Wo, ox = rem - oy * Wo;
+    const int iy0 = oy * stride - pad, ix0 = ox * stride - pad;
+    // k chunk q of step 0: taps 2q, 2q+1; of step 1: taps 8 + 2q, 9 + 2q (only tap 8 is real)
+    const sx4v a0 = tap(img, iy0, ix0, 2 * q), a1 = tap(img, iy0, ix0, 2 * q + 1);
+    const sx4v b0 = tap(img, iy0, ix0, 8 + 2 * q);
+    const bf16x8s x0 = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    const bf16x8s x1 = {b0[0], b0[1], b0[2], b0[3], 0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][0], x0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][1], x1, acc, 0, 0, 0);
+      // acc[i] = out channel 16 t + 4 q + i of pixel m
+      bf16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = acc[i] + bv[t][i];
+        o[i] = (bf16)(relu ? fmaxf(v, 0.f) : v);
+      }
+      if (ok) *(bf16x4*)(y + (int64_t)m * COUT + 16 * t + 4 * q) = o;
+    }
+  }
+}
+
+// =====================================================================================
 // K12+K13: DetectionOutput. Stage 1: one block per (image, foreground class).
 //   softmax(conf row)[class] > thresh -> candidates -> bitonic sort (desc score, asc prior)
 //   -> top_k -> CENTER_SIZE decode -> greedy NMS -> per-class kept list.
@@ -921,8 +995,9 @@ void vcx_resize_bilinear_u8(const uint8_t* src, uint8_t* dst, int N, int H, int 
 
 void vcx_blob_bilinear(const uint8_t* src, void* dst, int N, int H, int W, int S, float scale, float mean,
                        hipStream_t s) {
-  hipLaunchKernelGGL(blob_bilinear_kernel, dim3(stream_grid((int64_t)N * S * S, 256)), dim3(256), 0, s, src,
-                     (bf16*)dst, N, H, W, S, scale, mean);
+  const int bt = std::min(320, (S + 63) / 64 * 64);
+  hipLaunchKernelGGL(blob_bilinear_kernel, dim3((S + bt - 1) / bt, S, N), dim3(bt), 0, s, src, (bf16*)dst, N, H, W, S,
+                     scale, mean);
 }
 
 void vcx_im2col_nhwc(const void* x, void* out, int N, int H, int W, int C, int Cs, int Ho, int Wo, int KH, int KW,
@@ -995,6 +1070,17 @@ void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y
                        hipStream_t s) {
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   const int M = imgs * Ho * Wo;
+  if (C == 4 && Cs == 4 && KH == 3 && KW == 3 && Kp == 64 && (N == 16 || N == 32 || N == 64)) {
+    const int blocks = (M + 255) / 256;  // 4 waves x 64 pixels
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, (const bf16*)x, (const bf16*)Wt, bias, (bf16*)Y, M, H,
+                         W, Ho, Wo, stride, pad, relu);
+    };
+    if (N == 16) go(stem_conv_c4_kernel<16>);
+    else if (N == 32) go(stem_conv_c4_kernel<32>);
+    else go(stem_conv_c4_kernel<64>);
+    return;
+  }
   OutMap om{nullptr, N, 0, M, 0, 0, nullptr, 0};
   ConvGeom cg{H, W, C, Cs, Ho, Wo, KW, stride, pad, KH * KW * C, nullptr, nullptr, 0};
   launch_gba<AM_IMPLICIT>((const bf16*)x, (const bf16*)Wt, bias, (bf16*)Y, M, N, Kp, N, relu, om, cg, ws, S, s);

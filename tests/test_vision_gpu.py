@@ -229,3 +229,32 @@ def test_detect_graph_replay_matches_eager(gpu):
         assert torch.equal(cg, ce)
         assert torch.equal(dg, de)
     assert len(ex._graphs) == 1
+
+
+@pytest.mark.parametrize("N,H,C,cout,k,stride,pad", [(3, 300, 4, 32, 3, 2, 1), (2, 37, 4, 16, 3, 1, 1),
+                                                     (2, 10, 256, 512, 3, 2, 1), (4, 5, 128, 256, 3, 2, 1),
+                                                     (2, 3, 128, 256, 3, 2, 1), (1, 19, 64, 64, 3, 1, 1)])
+def test_conv_implicit_vs_fp32(gpu, N, H, C, cout, k, stride, pad):
+    """Implicit-GEMM convolution (the SSD extras, split-K when the grid is small) and the MFMA
+    stem kernel (C == 4: the padded BGR0 blob, channel 3 zero) against fp32 F.conv2d."""
+    from distributedvolunteercomputing_amd.ops import native
+    torch.manual_seed(3)
+    x = torch.randn(N, H, H, C, device=gpu)
+    if C == 4:
+        x[..., 3] = 0
+    x = x.to(torch.bfloat16)
+    cin = 3 if C == 4 else C
+    w = (torch.randn(cout, cin, k, k, device=gpu) / (cin * k * k) ** 0.5)
+    b = torch.randn(cout, device=gpu) * 0.1
+    K = k * k * C
+    Kp = (K + 31) // 32 * 32
+    wk = torch.zeros(cout, k, k, C, device=gpu)
+    wk[..., :cin] = w.permute(0, 2, 3, 1)
+    wt = torch.zeros(cout, Kp, device=gpu)
+    wt[:, :K] = wk.reshape(cout, K)
+    y = native().conv_implicit(x, wt.to(torch.bfloat16).contiguous(), b, C, k, k, stride, pad, True)
+    r = F.relu(F.conv2d(x[..., :cin].permute(0, 3, 1, 2).float(), w.to(torch.bfloat16).float(), b, stride=stride,
+                        padding=pad)).permute(0, 2, 3, 1)
+    assert y.shape == r.shape
+    rel = float((y.float() - r).norm() / r.norm())
+    assert rel < 1e-2, rel
