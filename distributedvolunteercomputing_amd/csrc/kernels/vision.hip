@@ -65,17 +65,35 @@ __global__ void __launch_bounds__(256) resize_area_u8_kernel(const uint8_t* __re
 //      Requires (W*3) % 16 == 0 (1280/1920/640-wide video), w <= RA_XMAX*256 and one input row
 //      <= RA_LDS bytes; the launcher falls back to (a) otherwise.
 constexpr int RA_LDS = 24 * 1024, RA_XMAX = 4;
+// Each thread's output columns are fixed for the whole image, so their horizontal footprints
+// (first input column + up to RA_TAPS weights, zero past the footprint) are computed once into
+// registers; every row is then a branch-free weighted sum over LDS bytes. (The per-row
+// footprint walk with data-dependent trip counts ran 605 instructions per thread, 1.2 TB/s.)
+template <int RA_TAPS>
 __global__ void __launch_bounds__(256) resize_area_rows_kernel(const uint8_t* __restrict__ src,
                                                                 uint8_t* __restrict__ dst, int N, int H, int W, int h,
-                                                                int w) {
+                                                                int w, float sx, float sy) {
   __shared__ __attribute__((aligned(16))) uint8_t rows[RA_LDS + 1024];  // + a wave's tail lanes
-  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x;
   const int y = blockIdx.x % h, n = blockIdx.x / h;
-  const float sx = (float)W / w, sy = (float)H / h;
   const float fy0 = y * sy, fy1 = fminf((y + 1) * sy, (float)H);
   const int iy0 = (int)fy0, iy1 = min((int)ceilf(fy1), H);
   const int rb = W * 3, rpp = RA_LDS / rb;
+  int cx0[RA_XMAX];
+  float wx[RA_XMAX][RA_TAPS], inv[RA_XMAX];
+#pragma unroll
+  for (int j = 0; j < RA_XMAX; ++j) {
+    const int x = min(tid + 256 * j, w - 1);
+    const float fx0 = x * sx, fx1 = fminf((x + 1) * sx, (float)W);
+    const int x0 = (int)fx0;
+    cx0[j] = min(x0, W - RA_TAPS > 0 ? W - RA_TAPS : 0);  // window start kept inside the row
+#pragma unroll
+    for (int t = 0; t < RA_TAPS; ++t) {
+      const int xx = cx0[j] + t;
+      wx[j][t] = fmaxf(0.f, fminf(fx1, (float)(xx + 1)) - fmaxf(fx0, (float)xx));
+    }
+    inv[j] = 1.f / ((fx1 - fx0) * (fy1 - fy0));
+  }
   float acc[RA_XMAX][3];
 #pragma unroll
   for (int j = 0; j < RA_XMAX; ++j) acc[j][0] = acc[j][1] = acc[j][2] = 0.f;
@@ -93,22 +111,18 @@ __global__ void __launch_bounds__(256) resize_area_rows_kernel(const uint8_t* __
     __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
     __syncthreads();
     for (int r = 0; r < nr; ++r) {
-      const float wy = fminf(fy1, (float)(r0 + r + 1)) - fmaxf(fy0, (float)(r0 + r));
-      if (wy <= 0.f) continue;
+      const float wy = fmaxf(0.f, fminf(fy1, (float)(r0 + r + 1)) - fmaxf(fy0, (float)(r0 + r)));
       const uint8_t* row = rows + r * rb;
 #pragma unroll
       for (int j = 0; j < RA_XMAX; ++j) {
-        const int x = tid + 256 * j;
-        if (x >= w) break;
-        const float fx0 = x * sx, fx1 = fminf((x + 1) * sx, (float)W);
+        if (256 * j >= w) break;  // uniform
         float h0 = 0.f, h1 = 0.f, h2 = 0.f;
-        for (int xx = (int)fx0; xx < (int)ceilf(fx1) && xx < W; ++xx) {
-          const float wx = fminf(fx1, (float)(xx + 1)) - fmaxf(fx0, (float)xx);
-          if (wx <= 0.f) continue;
-          const uint8_t* p = row + xx * 3;
-          h0 = fmaf(wx, (float)p[0], h0);
-          h1 = fmaf(wx, (float)p[1], h1);
-          h2 = fmaf(wx, (float)p[2], h2);
+        const uint8_t* p = row + cx0[j] * 3;
+#pragma unroll
+        for (int t = 0; t < RA_TAPS; ++t) {
+          h0 = fmaf(wx[j][t], (float)p[3 * t], h0);
+          h1 = fmaf(wx[j][t], (float)p[3 * t + 1], h1);
+          h2 = fmaf(wx[j][t], (float)p[3 * t + 2], h2);
         }
         acc[j][0] = fmaf(wy, h0, acc[j][0]);
         acc[j][1] = fmaf(wy, h1, acc[j][1]);
@@ -121,10 +135,8 @@ __global__ void __launch_bounds__(256) resize_area_rows_kernel(const uint8_t* __
   for (int j = 0; j < RA_XMAX; ++j) {
     const int x = tid + 256 * j;
     if (x >= w) break;
-    const float fx0 = x * sx, fx1 = fminf((x + 1) * sx, (float)W);
-    const float inv = 1.f / ((fx1 - fx0) * (fy1 - fy0));
 #pragma unroll
-    for (int c = 0; c < 3; ++c) q[x * 3 + c] = (uint8_t)fminf(255.f, fmaxf(0.f, rintf(acc[j][c] * inv)));
+    for (int c = 0; c < 3; ++c) q[x * 3 + c] = (uint8_t)fminf(255.f, fmaxf(0.f, rintf(acc[j][c] * inv[j])));
   }
 }
 
@@ -155,12 +167,57 @@ __global__ void __launch_bounds__(256) resize_bilinear_u8_kernel(const uint8_t* 
 //     3-D grid: blockIdx.z = image, blockIdx.y = output row, so the source rows and vertical weights are
 //     scalar; one thread per output column (the grid-stride version with 64-bit index division
 //     per pixel ran at 1.7 TB/s).
+constexpr int BLOB_LDS = 12 * 1024;  // two source rows of up to 2048 px
 __global__ void __launch_bounds__(320) blob_bilinear_kernel(const uint8_t* __restrict__ src, bf16* __restrict__ dst,
-                                                             int N, int H, int W, int S, float scale, float mean) {
+                                                             int N, int H, int W, int S, float sx, float sy,
+                                                             float scale, float mean) {
+  __shared__ __attribute__((aligned(16))) uint8_t rows[2 * BLOB_LDS + 1024];
+  const int tid = threadIdx.x;
+  const int n = blockIdx.z, y = blockIdx.y;
+  const float fy = fmaxf((y + 0.5f) * sy - 0.5f, 0.f);
+  const int y0 = min((int)fy, H - 1), y1 = min(y0 + 1, H - 1);
+  const float ay = fy - y0;
+  const int rb = W * 3;
+  // the two source rows into LDS (16-B LDS-DMA; row bytes are a multiple of 16, host-checked),
+  // so each output pixel's 12 byte taps are LDS reads instead of 12 global byte loads
+  const int chunks = rb / 16;
+  for (int rr = 0; rr < 2; ++rr) {
+    const uint8_t* g = src + ((int64_t)n * H + (rr ? y1 : y0)) * rb;
+    for (int e0 = (tid & ~63); e0 < chunks; e0 += blockDim.x) {
+      const int e = min(e0 + (tid & 63), chunks - 1);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + (int64_t)e * 16),
+                                       (__attribute__((address_space(3))) void*)(rows + rr * BLOB_LDS + e0 * 16), 16,
+                                       0, 0);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+  __syncthreads();
+  for (int x = blockIdx.x * blockDim.x + tid; x < S; x += gridDim.x * blockDim.x) {
+    const float fx = fmaxf((x + 0.5f) * sx - 0.5f, 0.f);
+    const int x0 = min((int)fx, W - 1), x1 = min(x0 + 1, W - 1);
+    const float ax = fx - x0;
+    const uint8_t* r0 = rows;
+    const uint8_t* r1 = rows + BLOB_LDS;
+    bf16x4 o;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v00 = r0[x0 * 3 + c], v01 = r0[x1 * 3 + c], v10 = r1[x0 * 3 + c], v11 = r1[x1 * 3 + c];
+      float v = (v00 * (1 - ax) + v01 * ax) * (1 - ay) + (v10 * (1 - ax) + v11 * ax) * ay;
+      v = rintf(fminf(255.f, fmaxf(0.f, v)));  // cv2.resize output is uint8
+      o[c] = (bf16)((v - mean) * scale);
+    }
+    o[3] = (bf16)0.f;
+    *(bf16x4*)(dst + (((int64_t)n * S + y) * S + x) * 4) = o;
+  }
+}
+
+// the same for widths whose rows are not 16-B multiples (global byte taps)
+__global__ void __launch_bounds__(256) blob_bilinear_any_kernel(const uint8_t* __restrict__ src,
+                                                                 bf16* __restrict__ dst, int N, int H, int W, int S,
+                                                                 float sx, float sy, float scale, float mean) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x;
   if (x >= S) return;
   const int n = blockIdx.z, y = blockIdx.y;
-  const float sx = (float)W / S, sy = (float)H / S;
   const float fy = fmaxf((y + 0.5f) * sy - 0.5f, 0.f);
   const int y0 = min((int)fy, H - 1), y1 = min(y0 + 1, H - 1);
   const float ay = fy - y0;
@@ -174,7 +231,7 @@ __global__ void __launch_bounds__(320) blob_bilinear_kernel(const uint8_t* __res
   for (int c = 0; c < 3; ++c) {
     const float v00 = r0[x0 * 3 + c], v01 = r0[x1 * 3 + c], v10 = r1[x0 * 3 + c], v11 = r1[x1 * 3 + c];
     float v = (v00 * (1 - ax) + v01 * ax) * (1 - ay) + (v10 * (1 - ax) + v11 * ax) * ay;
-    v = rintf(fminf(255.f, fmaxf(0.f, v)));  // cv2.resize output is uint8
+    v = rintf(fminf(255.f, fmaxf(0.f, v)));
     o[c] = (bf16)((v - mean) * scale);
   }
   o[3] = (bf16)0.f;
@@ -243,6 +300,31 @@ __device__ __forceinline__ void dw9_accum(const u32x4 (&x)[9], const uint32_t* w
   }
 }
 
+// the same with the paired weights of the lane's 8 channels already in registers (w[p][j])
+__device__ __forceinline__ void load_dw_weights(const uint32_t* wp, int ldw, uint32_t (&w)[5][8]) {
+#pragma unroll
+  for (int p = 0; p < 5; ++p) {
+    const u32x4 w0 = *(const u32x4*)(wp + p * ldw), w1 = *(const u32x4*)(wp + p * ldw + 4);
+    w[p][0] = w0[0], w[p][1] = w0[1], w[p][2] = w0[2], w[p][3] = w0[3];
+    w[p][4] = w1[0], w[p][5] = w1[1], w[p][6] = w1[2], w[p][7] = w1[3];
+  }
+}
+__device__ __forceinline__ void dw9_accum_w(const u32x4 (&x)[9], const uint32_t (&w)[5][8], float (&a)[8]) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t lo = x[2 * p][q], hi = x[2 * p + 1][q];
+      a[2 * q] = dot2bf(__builtin_amdgcn_perm(hi, lo, 0x05040100u), w[p][2 * q], a[2 * q]);
+      a[2 * q + 1] = dot2bf(__builtin_amdgcn_perm(hi, lo, 0x07060302u), w[p][2 * q + 1], a[2 * q + 1]);
+    }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    a[2 * q] = dot2bf(x[8][q], w[4][2 * q], a[2 * q]);
+    a[2 * q + 1] = dot2bf(x[8][q], w[4][2 * q + 1], a[2 * q + 1]);
+  }
+}
+
 __device__ __forceinline__ u32x4 dw_out8(const float (&a)[8], int relu) {
   bf16x8 o;
 #pragma unroll
@@ -286,6 +368,11 @@ __global__ void __launch_bounds__(256) dwconv3x3_kernel(const bf16* __restrict__
     for (int kx = 0; kx < 3; ++kx)
       xv[r][kx] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, coff[kx] + r * rowb, 0, 0));
   f32x4 b0 = *(const f32x4*)(b + c8 * 8), b1 = *(const f32x4*)(b + c8 * 8 + 4);
+  // the weights once per thread, in registers: reloading them per output row (the loop's early
+  // exit keeps the compiler from hoisting) tripled the L1 traffic — 40 weight loads against 18
+  // tap loads per thread, and the kernel ran L1/TA-bound at 2.7 TB/s
+  uint32_t wr[5][8];
+  load_dw_weights(wp + c8 * 8, C, wr);
 #pragma unroll
   for (int j = 0; j < R; ++j) {
     const int oy = oy0 + j;
@@ -294,7 +381,7 @@ __global__ void __launch_bounds__(256) dwconv3x3_kernel(const bf16* __restrict__
     const u32x4 t9[9] = {xv[j * STRIDE][0],     xv[j * STRIDE][1],     xv[j * STRIDE][2],
                          xv[j * STRIDE + 1][0], xv[j * STRIDE + 1][1], xv[j * STRIDE + 1][2],
                          xv[j * STRIDE + 2][0], xv[j * STRIDE + 2][1], xv[j * STRIDE + 2][2]};
-    dw9_accum(t9, wp + c8 * 8, C, acc);
+    dw9_accum_w(t9, wr, acc);
     *(u32x4*)(y + (((int64_t)n * Ho + oy) * Wo + ox) * C + c8 * 8) = dw_out8(acc, relu);
   }
 }
@@ -979,9 +1066,14 @@ __global__ void __launch_bounds__(256) annotate_kernel(uint8_t* __restrict__ fra
 using namespace vcx;
 
 void vcx_resize_area_u8(const uint8_t* src, uint8_t* dst, int N, int H, int W, int h, int w, hipStream_t s) {
+  const float sx = (float)W / w, sy = (float)H / h;
+  const int taps = (int)ceilf(sx) + 1;  // input columns an output column can touch
   if ((W * 3) % 16 == 0 && ((uintptr_t)src & 15) == 0 && w <= RA_XMAX * 256 && W * 3 <= RA_LDS && h <= H &&
-      w <= W && (int64_t)N * h < INT32_MAX) {
-    hipLaunchKernelGGL(resize_area_rows_kernel, dim3(N * h), dim3(256), 0, s, src, dst, N, H, W, h, w);
+      w <= W && W >= 8 && taps <= 8 && (int64_t)N * h < INT32_MAX) {
+    if (taps <= 5)
+      hipLaunchKernelGGL(resize_area_rows_kernel<5>, dim3(N * h), dim3(256), 0, s, src, dst, N, H, W, h, w, sx, sy);
+    else
+      hipLaunchKernelGGL(resize_area_rows_kernel<8>, dim3(N * h), dim3(256), 0, s, src, dst, N, H, W, h, w, sx, sy);
     return;
   }
   hipLaunchKernelGGL(resize_area_u8_kernel, dim3(stream_grid((int64_t)N * h * w, 256)), dim3(256), 0, s, src, dst, N,
@@ -995,9 +1087,15 @@ void vcx_resize_bilinear_u8(const uint8_t* src, uint8_t* dst, int N, int H, int 
 
 void vcx_blob_bilinear(const uint8_t* src, void* dst, int N, int H, int W, int S, float scale, float mean,
                        hipStream_t s) {
-  const int bt = std::min(320, (S + 63) / 64 * 64);
-  hipLaunchKernelGGL(blob_bilinear_kernel, dim3((S + bt - 1) / bt, S, N), dim3(bt), 0, s, src, (bf16*)dst, N, H, W, S,
-                     scale, mean);
+  const float sx = (float)W / S, sy = (float)H / S;
+  if ((W * 3) % 16 == 0 && W * 3 <= BLOB_LDS && ((uintptr_t)src & 15) == 0) {
+    const int bt = std::min(320, (S + 63) / 64 * 64);
+    hipLaunchKernelGGL(blob_bilinear_kernel, dim3(1, S, N), dim3(bt), 0, s, src, (bf16*)dst, N, H, W, S, sx, sy, scale,
+                       mean);
+  } else {
+    hipLaunchKernelGGL(blob_bilinear_any_kernel, dim3((S + 255) / 256, S, N), dim3(256), 0, s, src, (bf16*)dst, N, H,
+                       W, S, sx, sy, scale, mean);
+  }
 }
 
 void vcx_im2col_nhwc(const void* x, void* out, int N, int H, int W, int C, int Cs, int Ho, int Wo, int KH, int KW,
