@@ -22,6 +22,7 @@ On CPU the same object runs the plain-PyTorch ``CaffeNet`` interpreter (the orac
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -104,6 +105,10 @@ def mobilenet_ssd_netdef(num_classes: int = 21, size: int = 300) -> NetDef:
     return NetDef("MobileNet-SSD", ["data"], [[1, 3, size, size]], L)
 
 
+def _nullctx():
+    return contextlib.nullcontext()
+
+
 def _round_up(n, a):
     return (n + a - 1) // a * a
 
@@ -124,6 +129,7 @@ class SSDExecutor:
         self.use_graph = os.environ.get("VCX_VISION_GRAPH", "1") != "0"
         self.pw_gemm = os.environ.get("VCX_VISION_PW", "nt")  # nt: gemm_nt where it applies | vision
         self._graphs = {}
+        self._sides = {}
         self._plan = self._compile() if self.device.type == "cuda" else None
 
     # ------------------------------------------------------------------ compile
@@ -330,6 +336,12 @@ class SSDExecutor:
         concat_bufs = {ci: torch.empty(N, tot, device=blob.device, dtype=torch.bfloat16)
                        for ci, tot in self._concat_total.items()}
         marks = self.step_events  # optional per-step timing: list of (layer name, kind, event)
+        # the multibox heads (small GEMMs, split-K) run on a side stream, concurrently with the
+        # backbone / extras layers after their source; joined before DetectionOutput. Inside the
+        # chunk's HIP graph this becomes parallel branches. (Per-step timing keeps one stream.)
+        main = torch.cuda.current_stream(blob.device)
+        side = self._side_stream(blob.device) if marks is None else None
+        side_refs, forked = [], False
         for kind, l, p in self._plan:
             if marks is not None:
                 ev = torch.cuda.Event(enable_timing=True)
@@ -362,8 +374,13 @@ class SSDExecutor:
                 x = t[p["src"]]
                 H, W = hw[p["src"]]
                 la, ca = (concat_bufs[c] for c in p["concats"])
-                ops.native().gemm_bias_heads(x.reshape(N * H * W, x.shape[-1]), p["w"], p["b"], la, p["offs"][0],
-                                             ca, p["offs"][1], p["split"], H * W)
+                if side is not None:
+                    side.wait_stream(main)  # the source activation is ready
+                    side_refs.append(x)  # kept alive (not reused by the allocator) until the join
+                    forked = True
+                with torch.cuda.stream(side) if side is not None else _nullctx():
+                    ops.native().gemm_bias_heads(x.reshape(N * H * W, x.shape[-1]), p["w"], p["b"], la,
+                                                 p["offs"][0], ca, p["offs"][1], p["split"], H * W)
             elif kind == "concat_buf":
                 t[top], layout[top] = concat_bufs[p["index"]], "plain"
             elif kind == "conv":
@@ -392,6 +409,9 @@ class SSDExecutor:
                 # folded into DetectionOutput: the detect kernel takes raw logits
                 t[top], layout[top] = x, "logits"
             elif kind == "detectionoutput":
+                if forked:
+                    main.wait_stream(side)  # every head has written the concat buffers
+                    forked = False
                 loc, conf, pri = (t[b] for b in l.bottoms)
                 dp = lambda k, d: l.p("detection_output_param", k, d)  # noqa: E731
                 P = pri.shape[-1] // 4
@@ -404,11 +424,22 @@ class SSDExecutor:
                                          top_k=int(l.sub("detection_output_param", "nms_param", "top_k", 100)),
                                          keep_top_k=int(dp("keep_top_k", 100)))
                 t[top] = (dets, cnt)
+        if forked:
+            main.wait_stream(side)
+        side_refs.clear()
         if marks is not None:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             marks.append(("<end>", "", ev))
         return t
+
+    def _side_stream(self, dev):
+        if os.environ.get("VCX_VISION_STREAMS", "2") == "1":
+            return None
+        s = self._sides.get(dev)
+        if s is None:
+            s = self._sides[dev] = torch.cuda.Stream(dev)
+        return s
 
     def step_times(self, blob: torch.Tensor, iters: int = 10) -> list:
         """Per plan step GPU time (ms, mean over `iters` passes): [(layer, kind, ms)]. Steps that
