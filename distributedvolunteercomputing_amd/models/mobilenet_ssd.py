@@ -401,8 +401,12 @@ class SSDExecutor:
             elif kind == "concat":
                 ax = int(l.p("concat_param", "axis", 1))
                 parts = [t[b] for b in l.bottoms]
-                if layout[l.bottoms[0]] == "priors":
-                    t[top], layout[top] = torch.cat(parts, ax), "priors"
+                if layout[l.bottoms[0]] == "priors":  # constant for a given input size: concatenated once
+                    key = ("cat", l.name, blob.device.index)
+                    if key not in self._prior_cache:
+                        cat = torch.cat(parts, ax)
+                        self._prior_cache[key] = (cat, cat[0, 0].float().contiguous(), cat[0, 1].float().contiguous())
+                    t[top], layout[top] = self._prior_cache[key][0], "priors"
                 else:
                     t[top], layout[top] = torch.cat([q.reshape(N, -1) for q in parts], ax), "plain"
             elif kind in ("reshape", "softmax"):
@@ -416,7 +420,9 @@ class SSDExecutor:
                 dp = lambda k, d: l.p("detection_output_param", k, d)  # noqa: E731
                 P = pri.shape[-1] // 4
                 nc = int(dp("num_classes", 21))
-                dets, cnt = V.ssd_detect(conf.reshape(N, P * nc), loc.reshape(N, P * 4), pri[0, 0], pri[0, 1],
+                cached = next((v for k, v in self._prior_cache.items() if k[0] == "cat" and v[0] is pri), None)
+                boxes, var = (cached[1], cached[2]) if cached is not None else (pri[0, 0], pri[0, 1])
+                dets, cnt = V.ssd_detect(conf.reshape(N, P * nc), loc.reshape(N, P * 4), boxes, var,
                                          num_classes=nc, background=int(dp("background_label_id", 0)),
                                          conf_thresh=float(dp("confidence_threshold", 0.01)),
                                          nms_thresh=float(l.sub("detection_output_param", "nms_param",

@@ -23,3 +23,38 @@ def gpu():
 
     native()  # loud failure if the extension is missing on a GPU box
     return torch.device("cuda", 0)
+
+
+_EXIT = {}
+
+
+def pytest_sessionfinish(session, exitstatus):
+    _EXIT["status"] = int(exitstatus)
+    if os.environ.get("VCX_TEST_THREADS"):
+        import threading
+
+        print("\n[threads at session end]", sorted(t.name for t in threading.enumerate()), flush=True)
+
+
+@pytest.hookimpl(trylast=True)
+def pytest_unconfigure(config):
+    """End the test process without interpreter finalization once the result is known.
+
+    Tests leave daemon threads of in-process coordinators / elastic peers behind, some of them
+    inside GIL-released torch calls (TCPStore waits). Finalization pthread_exit()s such a thread
+    when it re-takes the GIL, from a noexcept frame of libtorch_python: std::terminate, and the
+    process exits 134 after a green run (the backtrace: PyEval_RestoreThread -> pthread_exit ->
+    _Unwind_ForcedUnwind -> terminate). Our own native runtime parks such threads instead
+    (csrc/runtime/module.cpp without_gil); torch's bindings do not. VCX_TEST_HARD_EXIT=0 keeps the
+    normal teardown."""
+    if "status" not in _EXIT or os.environ.get("VCX_TEST_HARD_EXIT", "1") != "1":
+        return
+    # CPU runs only (device_count() does not initialise the GPU): a GPU process keeps its normal
+    # teardown, and no GPU test leaves an abandoned gloo point-to-point waiter behind (the thread
+    # seen alive at session end here: 'vcx-p2p-send' of the p2p transfer-failure test)
+    import torch
+
+    if torch.cuda.device_count() == 0:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(_EXIT["status"])

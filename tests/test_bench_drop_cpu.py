@@ -20,7 +20,9 @@ def test_bench_drop_three_peers_one_crash(tmp_path):
     assert rec["regroup_step"] is not None and rec["regroup_step"] >= rec["config"]["drop_at"]
     # the crashed peer's liveness link closed: the survivors regrouped without waiting a lease
     assert rec["liveness"] and rec["detect_ms"] is not None and rec["detect_ms"] < 0.5 * 1e3
-    assert rec["regroup_sync_ms"] < 0.5 * 1e3 * 0.9
+    # the regroup round costs less than a lease beyond a steady round (absolute times vary with the
+    # load of this 8-CPU container; a lease wait would add >= 500 ms)
+    assert rec["regroup_sync_ms"] - rec["steady_sync_ms"] < 0.5 * 1e3 * 0.9, rec
     assert rec["comm_build_ms"] is not None and rec["redo_ms"] is not None
     assert rec["ms_per_step_after"] > 0 and rec["samples_per_s_after"] > 0
 
