@@ -1,6 +1,8 @@
 // Torch bindings for the MobileNet-SSD inference kernels (kernels/vision.hip).
 // Host-side shape checks guard every launch (no hand-written kernel sees a shape it was not
 // written for).
+#include <map>
+#include <mutex>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
@@ -56,6 +58,20 @@ at::Tensor im2col_nhwc(at::Tensor x, int64_t C, int64_t k, int64_t stride, int64
   return out;
 }
 
+// Split-K ticket counters for the in-kernel reduction: one zeroed int array per stream (kernels
+// on one stream never overlap; the last block of every tile re-arms its counter to zero). Created
+// on first use outside graph capture (the executor's warm-up passes run before its capture).
+static int* splitk_counters(const at::Tensor& like) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, at::Tensor> bufs;
+  const hipStream_t st = cur_stream();
+  std::lock_guard<std::mutex> g(mu);
+  auto key = std::make_pair((int)like.get_device(), st);
+  auto it = bufs.find(key);
+  if (it == bufs.end()) it = bufs.emplace(key, at::zeros({4096}, like.options().dtype(at::kInt))).first;
+  return it->second.data_ptr<int>();
+}
+
 at::Tensor dwconv3x3(at::Tensor x, at::Tensor w, at::Tensor b, int64_t stride, bool relu) {
   CHK(x, at::kBFloat16);
   CHK(w, at::kBFloat16);
@@ -92,7 +108,7 @@ at::Tensor gemm_bias_act(at::Tensor X, at::Tensor Wt, c10::optional<at::Tensor> 
   const int S = vcx_vision_ksplit((int)M, (int)N, (int)K);
   at::Tensor ws = S > 1 ? at::empty({S, M, N}, X.options().dtype(at::kFloat)) : at::Tensor();
   vcx_gemm_bias_act(X.data_ptr(), Wt.data_ptr(), bp, Y.data_ptr(), (int)M, (int)N, (int)K, (int)N, relu ? 1 : 0,
-                    S > 1 ? ws.data_ptr<float>() : nullptr, S, cur_stream());
+                    S > 1 ? ws.data_ptr<float>() : nullptr, S, S > 1 ? splitk_counters(X) : nullptr, cur_stream());
   return Y;
 }
 
@@ -146,7 +162,7 @@ void gemm_bias_heads(at::Tensor X, at::Tensor Wt, at::Tensor bias, at::Tensor lo
                            (uint16_t*)loc_all.data_ptr() + loc_off, (int)M, (int)N, (int)K, (int)split, 0,
                            (uint16_t*)conf_all.data_ptr() + conf_off, (int)split, (int)(N - split), (int)rpi,
                            loc_all.size(1), conf_all.size(1), S > 1 ? ws.data_ptr<float>() : nullptr, S,
-                           cur_stream());
+                           S > 1 ? splitk_counters(X) : nullptr, cur_stream());
 }
 
 // KxK convolution as an implicit GEMM (no im2col matrix): x NHWC bf16 [imgs, H, W, Cs] using
@@ -166,7 +182,7 @@ at::Tensor conv_implicit(at::Tensor x, at::Tensor Wt, at::Tensor bias, int64_t C
   at::Tensor ws = S > 1 ? at::empty({S, imgs * Ho * Wo, N}, x.options().dtype(at::kFloat)) : at::Tensor();
   vcx_conv_implicit(x.data_ptr(), Wt.data_ptr(), bias.data_ptr<float>(), Y.data_ptr(), (int)imgs, (int)H, (int)W,
                     (int)C, (int)Cs, (int)KH, (int)KW, (int)stride, (int)pad, (int)N, (int)Kp, relu ? 1 : 0,
-                    S > 1 ? ws.data_ptr<float>() : nullptr, S, cur_stream());
+                    S > 1 ? ws.data_ptr<float>() : nullptr, S, S > 1 ? splitk_counters(x) : nullptr, cur_stream());
   return Y;
 }
 

@@ -14,14 +14,14 @@ void vcx_dwconv3x3(const void* x, const void* w, const float* b, void* y, int N,
 int vcx_vision_ksplit(int M, int N, int K);
 void vcx_gemm_bias_act_mapped(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
                               int relu, void* Y2, int split, int ldy2, int rpi, int64_t img_stride,
-                              int64_t img_stride2, float* ws, int S, hipStream_t s);
+                              int64_t img_stride2, float* ws, int S, int* cnt, hipStream_t s);
 void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y, int imgs, int H, int W, int C,
                        int Cs, int KH, int KW, int stride, int pad, int N, int Kp, int relu, float* ws, int S,
-                       hipStream_t s);
+                       int* cnt, hipStream_t s);
 void vcx_dw_pw(const void* x, const void* dw_w, const float* dw_b, int dw_relu, const void* Wt, const float* bias,
                void* Y, int imgs, int H, int W, int K, int stride, int N, int relu, hipStream_t s);
 void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
-                       int relu, float* ws, int S, hipStream_t s);
+                       int relu, float* ws, int S, int* cnt, hipStream_t s);
 void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* prob,
                     float* cls_out, int* cls_cnt, float* out, int* out_cnt, int N, int P, int C, int bg, float thresh,
                     float nms_thresh, int topk, int keep, hipStream_t s);

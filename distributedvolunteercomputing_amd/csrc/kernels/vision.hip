@@ -417,6 +417,7 @@ struct OutMap {
   int64_t img_stride, img_stride2;
   float* part;  // split-K: fp32 partial sums [gridDim.z][M][N] instead of the epilogue (else null)
   int kchunk;   // split-K: K columns per z (multiple of 32)
+  int* cnt;     // split-K: per-tile tickets (zero between launches) -> the last block reduces, or null
 };
 
 // split-K reduction + the epilogue (bias, ReLU, bf16, output mapping) for the partials above
@@ -651,6 +652,40 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
         }
       }
     }
+    if (!om.cnt) return;  // reduced by splitk_bias_act
+    // the LAST of the tile's S blocks reduces it (no separate reduction launch): publish the
+    // partial (stores retired, agent-scope release), take a ticket; the block holding the final
+    // ticket acquires, sums the S partials of the tile and runs the epilogue; it also re-arms
+    // the tile's counter for the next launch (self-resetting, one counter array per stream)
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = atomicAdd(om.cnt + blockIdx.x, 1);
+      s_last = t == (int)gridDim.z - 1;
+      if (s_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        atomicExch(om.cnt + blockIdx.x, 0);
+      }
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const int S = gridDim.z;
+    const int64_t MN = (int64_t)M * N;
+    for (int e = tid; e < GBM * BN; e += 256) {
+      const int gm = m0 + e / BN, n = n0 + e % BN;
+      if (gm >= M || n >= N) continue;
+      const float* src = om.part + (int64_t)gm * N + n;
+      float v = bias ? bias[n] : 0.f;
+      for (int z = 0; z < S; ++z) v += __builtin_nontemporal_load(src + z * MN);
+      if (relu) v = fmaxf(v, 0.f);
+      const int64_t img = gm / om.rpi, rr = gm - img * om.rpi;
+      if (n < om.split) Y[img * om.img_stride + rr * ldy + n] = (bf16)v;
+      else om.Y2[img * om.img_stride2 + rr * om.ldy2 + (n - om.split)] = (bf16)v;
+    }
     return;
   }
   // epilogue: bias + act, the bf16 tile staged in LDS (16-B chunks XOR-swizzled by row), then
@@ -701,6 +736,123 @@ __global__ void __launch_bounds__(256) gemm_bias_act_kernel(const bf16* __restri
       if (n < om.split) Y[img * om.img_stride + rr * ldy + n] = v[r];
       else om.Y2[img * om.img_stride2 + rr * om.ldy2 + (n - om.split)] = v[r];
     }
+  }
+}
+
+// =====================================================================================
+// K5+K6 fused, 2-D pixel tiles: one workgroup = a TH x TW tile of output pixels of one image.
+//   1. the input halo ((TH-1)S+3 x (TW-1)S+3 pixels x K channels) -> LDS, 16-B buffer loads
+//      (rows above/below the image read as zero through the buffer range, side pad columns masked)
+//   2. depthwise 3x3 + bias (+ReLU) from LDS (dot2 reduction, weights in registers) -> the
+//      bf16 A tile [TH*TW px][K] in LDS (rounded where the two-kernel path rounds it)
+//   3. pointwise GEMM on MFMA against W [N][K] (in LDS), + bias (+ReLU) -> staged in LDS ->
+//      coalesced NHWC row segments.
+// The depthwise activation never goes through HBM, and every input pixel is read from HBM once
+// (plus the halo rows/columns neighbouring tiles share through L2). For the early, wide MobileNet
+// blocks (conv1..conv3: 150^2 / 75^2 pixels, K = 32..128, N = 64..128). The 1-D-tile fusion
+// inside the GEMM's A staging (AM_DW) re-read every tap from L1 (9x) and lost to two kernels.
+// =====================================================================================
+template <int K, int N, int S, int TH, int TW>
+__global__ void __launch_bounds__(256) dwpw_tile_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dwp,
+                                                         const float* __restrict__ dwb, int dw_relu,
+                                                         const bf16* __restrict__ Wt, const float* __restrict__ pb,
+                                                         int relu, bf16* __restrict__ y, int H, int W, int Ho, int Wo) {
+  constexpr int HH = (TH - 1) * S + 3, HW = (TW - 1) * S + 3;  // halo rows / columns
+  constexpr int K8 = K / 8, MT = TH * TW, KS = K / 32;            // 8-ch groups, tile pixels, K slices
+  constexpr int HALO_B = HH * HW * K * 2, A_B = MT * K * 2, W_B = N * K * 2, OUT_B = MT * N * 2;
+  constexpr int R0 = HALO_B > OUT_B ? HALO_B : OUT_B;             // halo, later the output staging
+  static_assert(256 % K8 == 0 && K % 32 == 0 && N % 64 == 0 && MT % 16 == 0, "tile shape");
+  __shared__ __attribute__((aligned(16))) char smem[R0 + A_B + W_B];
+  char* const halo = smem;
+  bf16* const sA = (bf16*)(smem + R0);      // KS slices of [MT][32], gidx-swizzled
+  bf16* const sW = (bf16*)(smem + R0 + A_B);  // KS slices of [N][32], gidx-swizzled
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n = blockIdx.z, oy0 = blockIdx.y * TH, ox0 = blockIdx.x * TW;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+
+  // ---- 1. halo + pointwise weights -> LDS
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + (int64_t)n * H * W * K), (short)0, H * W * K * 2,
+                                                    0x00020000);
+  for (int e = tid; e < HH * HW * K8; e += 256) {
+    const int c = e % K8, px = e / K8, hx = px % HW, hy = px / HW;
+    const int iy = iy0 + hy, ix = ix0 + hx;
+    const int off = (ix >= 0 && ix < W) ? ((iy * W + ix) * K + c * 8) * 2 : (int)0x80000000;
+    *(u32x4*)(halo + e * 16) = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+  }
+  for (int e = tid; e < N * K8; e += 256) {
+    const int row = e / K8, c = e % K8;
+    *(u32x4*)(sW + (c >> 2) * N * 32 + gidx(row, c & 3)) = *(const u32x4*)(Wt + (int64_t)row * K + c * 8);
+  }
+  // depthwise weights of this thread's channel group (fixed: 256 % K8 == 0), in registers
+  const int c8 = tid % K8;
+  uint32_t wr[5][8];
+  load_dw_weights(dwp + c8 * 8, K, wr);
+  const f32x4 db0 = *(const f32x4*)(dwb + c8 * 8), db1 = *(const f32x4*)(dwb + c8 * 8 + 4);
+  __syncthreads();
+
+  // ---- 2. depthwise from LDS -> A tile
+  for (int p = tid / K8; p < MT; p += 256 / K8) {
+    const int ty = p / TW, tx = p % TW;
+    u32x4 t9[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int hy = ty * S + t / 3, hx = tx * S + t % 3;
+      t9[t] = *(const u32x4*)(halo + ((hy * HW + hx) * K + c8 * 8) * 2);
+    }
+    float a[8] = {db0[0], db0[1], db0[2], db0[3], db1[0], db1[1], db1[2], db1[3]};
+    dw9_accum_w(t9, wr, a);
+    *(u32x4*)(sA + (c8 >> 2) * MT * 32 + gidx(p, c8 & 3)) = dw_out8(a, dw_relu);
+  }
+  __syncthreads();
+
+  // ---- 3. pointwise GEMM: wave w takes columns [w N/4, (w+1) N/4) for all MT rows
+  constexpr int NB = N / 64, MB = MT / 16;
+  f32x4 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fc = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    bf16x8s bw[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) bw[j] = *(const bf16x8s*)(sW + ks * N * 32 + gidx(wid * (N / 4) + j * 16 + fr, fc));
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const bf16x8s af = *(const bf16x8s*)(sA + ks * MT * 32 + gidx(i * 16 + fr, fc));
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af, acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue: acc[i][j][r] = out[px = 16 i + fr][col = w N/4 + 16 j + 4 fc + r], staged as [MT][N]
+  // bf16 rows (16-B chunks XOR-swizzled by px) in the halo region (free since the barrier)
+  bf16* const sO = (bf16*)halo;
+  constexpr int CH = N / 8;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int col = wid * (N / 4) + j * 16 + 4 * fc;
+    float bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[r] = pb[col + r];
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int px = i * 16 + fr;
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[i][j][r] + bv[r];
+        o[r] = (bf16)(relu ? fmaxf(v, 0.f) : v);
+      }
+      *(bf16x4*)(sO + px * N + (((col >> 3) ^ (px & (CH - 1))) << 3) + (col & 4)) = o;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < MT * CH; e += 256) {
+    const int px = e / CH, ch = e % CH, oy = oy0 + px / TW, ox = ox0 + px % TW;
+    if (oy >= Ho || ox >= Wo) continue;
+    *(u32x4*)(y + (((int64_t)n * Ho + oy) * Wo + ox) * N + ch * 8) =
+        *(const u32x4*)(sO + px * N + ((ch ^ (px & (CH - 1))) << 3));
   }
 }
 
@@ -1134,10 +1286,11 @@ int vcx_vision_ksplit(int M, int N, int K) {
 
 template <int AM>
 static void launch_gba(const bf16* X, const bf16* Wt, const float* bias, bf16* Y, int M, int N, int K, int ldy,
-                       int relu, OutMap om, const ConvGeom& cg, float* ws, int S, hipStream_t s) {
+                       int relu, OutMap om, const ConvGeom& cg, float* ws, int S, int* cnt, hipStream_t s) {
   if (S > 1) {
     om.part = ws;
     om.kchunk = K / S;
+    om.cnt = cnt;
   }
   const int tm = (M + GBM - 1) / GBM;
   if (N <= 64)
@@ -1146,7 +1299,7 @@ static void launch_gba(const bf16* X, const bf16* Wt, const float* bias, bf16* Y
   else
     hipLaunchKernelGGL((gemm_bias_act_kernel<128, AM>), dim3(tm * ((N + 127) / 128), 1, S), dim3(256), 0, s, X, Wt,
                        bias, Y, M, N, K, ldy, relu, om, cg);
-  if (S > 1) {
+  if (S > 1 && !cnt) {
     om.part = nullptr;
     hipLaunchKernelGGL(splitk_bias_act_kernel, dim3(stream_grid((int64_t)M * N, 256)), dim3(256), 0, s, ws, S, bias,
                        Y, M, N, ldy, relu, om);
@@ -1155,17 +1308,17 @@ static void launch_gba(const bf16* X, const bf16* Wt, const float* bias, bf16* Y
 
 void vcx_gemm_bias_act_mapped(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
                               int relu, void* Y2, int split, int ldy2, int rpi, int64_t img_stride,
-                              int64_t img_stride2, float* ws, int S, hipStream_t s) {
-  OutMap om{(bf16*)Y2, split, ldy2, rpi > 0 ? rpi : M, img_stride, img_stride2, nullptr, 0};
+                              int64_t img_stride2, float* ws, int S, int* cnt, hipStream_t s) {
+  OutMap om{(bf16*)Y2, split, ldy2, rpi > 0 ? rpi : M, img_stride, img_stride2, nullptr, 0, nullptr};
   ConvGeom cg{};
-  launch_gba<AM_PLAIN>((const bf16*)X, (const bf16*)Wt, bias, (bf16*)Y, M, N, K, ldy, relu, om, cg, ws, S, s);
+  launch_gba<AM_PLAIN>((const bf16*)X, (const bf16*)Wt, bias, (bf16*)Y, M, N, K, ldy, relu, om, cg, ws, S, cnt, s);
 }
 
 // Y [imgs*Ho*Wo, N] = act(conv(x) + bias): x NHWC [imgs, H, W, Cs] (C used channels), weights
 // Wt [N, Kp] with columns (ky, kx, c), Kp % 32 == 0 (zero beyond KH*KW*C)
 void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y, int imgs, int H, int W, int C,
                        int Cs, int KH, int KW, int stride, int pad, int N, int Kp, int relu, float* ws, int S,
-                       hipStream_t s) {
+                       int* cnt, hipStream_t s) {
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   const int M = imgs * Ho * Wo;
   if (C == 4 && Cs == 4 && KH == 3 && KW == 3 && Kp == 64 && (N == 16 || N == 32 || N == 64)) {
@@ -1179,9 +1332,9 @@ void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y
     else go(stem_conv_c4_kernel<64>);
     return;
   }
-  OutMap om{nullptr, N, 0, M, 0, 0, nullptr, 0};
+  OutMap om{nullptr, N, 0, M, 0, 0, nullptr, 0, nullptr};
   ConvGeom cg{H, W, C, Cs, Ho, Wo, KW, stride, pad, KH * KW * C, nullptr, nullptr, 0};
-  launch_gba<AM_IMPLICIT>((const bf16*)x, (const bf16*)Wt, bias, (bf16*)Y, M, N, Kp, N, relu, om, cg, ws, S, s);
+  launch_gba<AM_IMPLICIT>((const bf16*)x, (const bf16*)Wt, bias, (bf16*)Y, M, N, Kp, N, relu, om, cg, ws, S, cnt, s);
 }
 
 // depthwise 3x3 (pad 1) + bias (+ReLU) -> pointwise GEMM + bias (+ReLU), one kernel:
@@ -1189,15 +1342,25 @@ void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y
 void vcx_dw_pw(const void* x, const void* dw_w, const float* dw_b, int dw_relu, const void* Wt, const float* bias,
                void* Y, int imgs, int H, int W, int K, int stride, int N, int relu, hipStream_t s) {
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  // 2-D-tile kernels for the MobileNet blocks they are instantiated for (K, N, stride)
+  auto tile = [&](auto kern, int th, int tw) {
+    hipLaunchKernelGGL(kern, dim3((Wo + tw - 1) / tw, (Ho + th - 1) / th, imgs), dim3(256), 0, s, (const bf16*)x,
+                       (const uint32_t*)dw_w, dw_b, dw_relu, (const bf16*)Wt, bias, relu, (bf16*)Y, H, W, Ho, Wo);
+  };
+  if ((int64_t)H * W * K * 2 < INT32_MAX && imgs <= 65535 && (Ho + 3) / 4 <= 65535) {
+    if (K == 32 && N == 64 && stride == 1) return tile(dwpw_tile_kernel<32, 64, 1, 8, 16>, 8, 16);
+    if (K == 64 && N == 128 && stride == 2) return tile(dwpw_tile_kernel<64, 128, 2, 4, 16>, 4, 16);
+    if (K == 128 && N == 128 && stride == 1) return tile(dwpw_tile_kernel<128, 128, 1, 4, 16>, 4, 16);
+  }
   const int M = imgs * Ho * Wo;
-  OutMap om{nullptr, N, 0, M, 0, 0, nullptr, 0};
+  OutMap om{nullptr, N, 0, M, 0, 0, nullptr, 0, nullptr};
   ConvGeom cg{H, W, K, K, Ho, Wo, 3, stride, 1, 9 * K, (const uint32_t*)dw_w, dw_b, dw_relu};
-  launch_gba<AM_DW>((const bf16*)x, (const bf16*)Wt, bias, (bf16*)Y, M, N, K, N, relu, om, cg, nullptr, 1, s);
+  launch_gba<AM_DW>((const bf16*)x, (const bf16*)Wt, bias, (bf16*)Y, M, N, K, N, relu, om, cg, nullptr, 1, nullptr, s);
 }
 
 void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
-                       int relu, float* ws, int S, hipStream_t s) {
-  vcx_gemm_bias_act_mapped(X, Wt, bias, Y, M, N, K, ldy, relu, nullptr, N, 0, M, 0, 0, ws, S, s);
+                       int relu, float* ws, int S, int* cnt, hipStream_t s) {
+  vcx_gemm_bias_act_mapped(X, Wt, bias, Y, M, N, K, ldy, relu, nullptr, N, 0, M, 0, 0, ws, S, cnt, s);
 }
 
 void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* prob,

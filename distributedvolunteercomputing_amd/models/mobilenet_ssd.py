@@ -276,10 +276,13 @@ class SSDExecutor:
 
     def _fuse_dw_pw(self, plan):
         """Depthwise -> pointwise pairs (every MobileNet block, prototxt 42-106 and after) become one
-        `dwpw` step when the depthwise output feeds only that pointwise conv. Blocks whose
-        pointwise output is wider than `max_cout` stay two kernels: the fused kernel recomputes
-        the depthwise tile once per 128 output channels (VCX_DWPW_MAX_COUT, 0 disables)."""
-        max_cout = int(os.environ.get("VCX_DWPW_MAX_COUT", "256"))
+        `dwpw` step when the depthwise output feeds only that pointwise conv and the block shape
+        has a 2-D-tile fused kernel (ops.vision.DWPW_TILE: conv1..conv3, the 150^2 / 75^2 blocks
+        where the depthwise round trip through HBM costs most). VCX_DWPW=off keeps every block two
+        kernels; VCX_DWPW=all also fuses the others through the GEMM's A-staging path (slower)."""
+        mode = os.environ.get("VCX_DWPW", "tile")
+        if mode == "off":
+            return plan
         uses = {}
         for l in self.net.layers:
             if l.tops == l.bottoms:
@@ -289,11 +292,11 @@ class SSDExecutor:
         out, i = [], 0
         while i < len(plan):
             kind, l, p = plan[i]
-            if kind == "dw" and i + 1 < len(plan) and max_cout > 0:
+            if kind == "dw" and i + 1 < len(plan):
                 k2, l2, p2 = plan[i + 1]
-                K = p["w"].shape[1]
-                if (k2 == "pw" and l2.bottoms[0] == l.tops[0] and uses.get(l.tops[0], 0) == 1
-                        and p2["w"].shape[0] <= max_cout and K <= 1024 and K % 32 == 0):
+                K, Co = p["w"].shape[1], (p2["w"].shape[0] if k2 == "pw" else 0)
+                shape_ok = (K, Co, p["stride"]) in V.DWPW_TILE or (mode == "all" and K <= 1024 and K % 32 == 0)
+                if k2 == "pw" and l2.bottoms[0] == l.tops[0] and uses.get(l.tops[0], 0) == 1 and shape_ok:
                     out.append(("dwpw", l2, dict(dw=p, pw=p2, src=l.bottoms[0])))
                     i += 2
                     continue

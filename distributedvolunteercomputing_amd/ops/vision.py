@@ -130,6 +130,11 @@ def dwconv3x3(x, w, b, stride, relu=True):
     return y.permute(0, 2, 3, 1).contiguous().to(x.dtype)
 
 
+# (K, N, stride) of the MobileNet blocks with a 2-D-tile fused depthwise->pointwise kernel
+# (csrc/kernels/vision.hip dwpw_tile_kernel); other shapes fuse through the GEMM A staging
+DWPW_TILE = {(32, 64, 1), (64, 128, 2), (128, 128, 1)}
+
+
 def dw_pw(x, wp, db, dw_relu, stride, Wt, bias, relu=True):
     """A MobileNet block as one kernel: depthwise 3x3 (pad 1) + bias (+ReLU) on NHWC x [N, H, W, K],
     then the pointwise GEMM with Wt [Cout, K] + bias (+ReLU) -> [N, Ho, Wo, Cout]. wp: paired
