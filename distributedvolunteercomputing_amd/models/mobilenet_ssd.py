@@ -295,7 +295,8 @@ class SSDExecutor:
             if kind == "dw" and i + 1 < len(plan):
                 k2, l2, p2 = plan[i + 1]
                 K, Co = p["w"].shape[1], (p2["w"].shape[0] if k2 == "pw" else 0)
-                shape_ok = (K, Co, p["stride"]) in V.DWPW_TILE or (mode == "all" and K <= 1024 and K % 32 == 0)
+                tiles = V.DWPW_TILE_ALL if mode in ("tile3", "all") else V.DWPW_TILE
+                shape_ok = (K, Co, p["stride"]) in tiles or (mode == "all" and K <= 1024 and K % 32 == 0)
                 if k2 == "pw" and l2.bottoms[0] == l.tops[0] and uses.get(l.tops[0], 0) == 1 and shape_ok:
                     out.append(("dwpw", l2, dict(dw=p, pw=p2, src=l.bottoms[0])))
                     i += 2

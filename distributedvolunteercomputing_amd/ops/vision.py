@@ -130,9 +130,13 @@ def dwconv3x3(x, w, b, stride, relu=True):
     return y.permute(0, 2, 3, 1).contiguous().to(x.dtype)
 
 
-# (K, N, stride) of the MobileNet blocks with a 2-D-tile fused depthwise->pointwise kernel
-# (csrc/kernels/vision.hip dwpw_tile_kernel); other shapes fuse through the GEMM A staging
-DWPW_TILE = {(32, 64, 1), (64, 128, 2), (128, 128, 1)}
+# (K, N, stride) of the MobileNet blocks whose 2-D-tile fused depthwise->pointwise kernel
+# (csrc/kernels/vision.hip dwpw_tile_kernel) beats the two kernels: conv1 145 us vs 79 + 94. The
+# kernel also has conv2 (64, 128, 2) and conv3 (128, 128, 1) instances, which lose at 2 blocks
+# per CU (199 / 179 us vs 136 / 145: the halo-load -> depthwise -> GEMM -> store phases of one
+# tile do not overlap); VCX_DWPW=tile3 fuses all three
+DWPW_TILE = {(32, 64, 1)}
+DWPW_TILE_ALL = {(32, 64, 1), (64, 128, 2), (128, 128, 1)}
 
 
 def dw_pw(x, wp, db, dw_relu, stride, Wt, bias, relu=True):
