@@ -272,7 +272,27 @@ class SSDExecutor:
             hs["concats"] = (a["concat"], c["concat"])
             hs["offs"] = (offs[(a["concat"], a["pos"])], offs[(c["concat"], c["pos"])])
             hs["rows"] = a["rows"]
-        return self._fuse_dw_pw(plan)
+        return self._heads_after_sources(self._fuse_dw_pw(plan))
+
+    @staticmethod
+    def _heads_after_sources(plan):
+        """Move each multibox head step right behind the step that produces its source (the
+        prototxt lists every head after the last extra layer): the head then forks onto the side
+        stream as soon as its input exists and overlaps the rest of the backbone / extras,
+        instead of waiting behind all of them."""
+        heads = [st for st in plan if st[0] == "head"]
+        rest = [st for st in plan if st[0] != "head"]
+        out = []
+        for st in rest:
+            out.append(st)
+            top = st[1].tops[0] if st[1].tops else None
+            for h in heads:
+                if h[2]["src"] == top:
+                    out.append(h)
+        placed = sum(1 for st in out if st[0] == "head")
+        if placed != len(heads):  # a source produced outside the plan's steps: keep the original order
+            return plan
+        return out
 
     def _fuse_dw_pw(self, plan):
         """Depthwise -> pointwise pairs (every MobileNet block, prototxt 42-106 and after) become one
