@@ -105,6 +105,9 @@ def mobilenet_ssd_netdef(num_classes: int = 21, size: int = 300) -> NetDef:
     return NetDef("MobileNet-SSD", ["data"], [[1, 3, size, size]], L)
 
 
+_GRAPH_GRAVEYARD = []
+
+
 def _nullctx():
     return contextlib.nullcontext()
 
@@ -126,10 +129,14 @@ class SSDExecutor:
         self.input_size = int(net.input_shapes[0][2]) if net.input_shapes else 300
         self._prior_cache = {}
         self.step_events = None
-        self.use_graph = os.environ.get("VCX_VISION_GRAPH", "1") != "0"
+        # one HIP graph per chunk shape is opt-in: measured no faster than eager launching (1.39 vs
+        # 1.31-1.33 ms per 100-frame chunk: the GPU, not the host, is the bound), and a capture
+        # inside the multi-threaded volunteer job was invalidated by the other threads' GPU calls
+        self.use_graph = os.environ.get("VCX_VISION_GRAPH", "0") == "1"
         self.pw_gemm = os.environ.get("VCX_VISION_PW", "nt")  # nt: gemm_nt where it applies | vision
         self._graphs = {}
         self._sides = {}
+        self.graph_error = None
         self._plan = self._compile() if self.device.type == "cuda" else None
 
     # ------------------------------------------------------------------ compile
@@ -488,9 +495,9 @@ class SSDExecutor:
 
     def detect(self, frames_u8: torch.Tensor):
         """frames [N, H, W, 3] uint8 BGR (already at the annotation size) -> (dets, counts).
-        On the GPU the whole chunk (blob + ~60 kernels of the plan + detection) replays as one HIP
-        graph per input shape: eager launching costs ~25 us of host time per plan step, as much
-        as the network's GPU time (VCX_VISION_GRAPH=0 runs it eagerly)."""
+        With VCX_VISION_GRAPH=1 the whole chunk (blob + the plan's kernels + detection) replays
+        as one HIP graph per input shape (measured no faster than eager: the GPU is the bound).
+        """
         if self._plan is not None and self.use_graph and frames_u8.is_cuda:
             return self._detect_graphed(frames_u8)
         blob = V.blob_from_frames(frames_u8, self.input_size)
@@ -511,8 +518,16 @@ class SSDExecutor:
                     self._detect_eager(static_in)
             torch.cuda.current_stream(frames_u8.device).wait_stream(side)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                static_out = self._detect_eager(static_in)
+            try:
+                # thread_local: volunteers' other threads (pre-resize, transfers) keep using the
+                # GPU while a worker captures; only this thread's calls belong to the capture
+                with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                    static_out = self._detect_eager(static_in)
+            except RuntimeError as e:  # capture invalidated: run this executor eagerly from now on
+                _GRAPH_GRAVEYARD.append(graph)  # a failed capture's destructor throws: never run it
+                self.use_graph = False
+                self.graph_error = f"{type(e).__name__}: {str(e)[:200]}"
+                return self._detect_eager(frames_u8)
             g = self._graphs[key] = (graph, static_in, static_out)
         graph, static_in, (dets, cnt) = g
         static_in.copy_(frames_u8)
