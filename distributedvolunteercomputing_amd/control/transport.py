@@ -29,8 +29,12 @@ class BadFrame(ValueError):
 
 
 # plain numeric dtypes only: no object / void / string dtypes from the wire
-_DTYPES = {np.dtype(t).str for t in (np.uint8, np.int8, np.uint16, np.int16, np.uint32, np.int32, np.uint64,
-                                     np.int64, np.float16, np.float32, np.float64, np.bool_)}
+# (looked up by name or by the dtype's .str form; the wire string never reaches numpy's dtype
+# parser, which accepts comma/repeat mini-languages and raises more than TypeError)
+_DTYPE_TYPES = (np.uint8, np.int8, np.uint16, np.int16, np.uint32, np.int32, np.uint64, np.int64, np.float16,
+                np.float32, np.float64, np.bool_)
+_DTYPES = {np.dtype(t).str for t in _DTYPE_TYPES}
+_DTYPE_BY_NAME = {k: np.dtype(t) for t in _DTYPE_TYPES for k in (np.dtype(t).name, np.dtype(t).str)}
 _MAX_DIMS = 8
 
 
@@ -44,12 +48,10 @@ def decode_frame(header: str, nbytes: int):
         raise BadFrame("header is not a JSON object")
     if not isinstance(hdr.get("msg", ""), str):
         raise BadFrame("msg must be a string")
-    try:
-        dt = np.dtype(hdr.get("dtype", "uint8"))
-    except TypeError:
-        raise BadFrame(f"unknown dtype {hdr.get('dtype')!r}") from None
-    if dt.str not in _DTYPES:
-        raise BadFrame(f"dtype {dt.str!r} not allowed")
+    name = hdr.get("dtype", "uint8")
+    dt = _DTYPE_BY_NAME.get(name) if isinstance(name, str) else None
+    if dt is None:
+        raise BadFrame(f"dtype {name!r} not allowed")
     shape = hdr.get("shape")
     if shape is not None:
         if (not isinstance(shape, list) or len(shape) > _MAX_DIMS
