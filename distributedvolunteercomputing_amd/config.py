@@ -30,6 +30,8 @@ def _bool(s: str) -> bool:
 class RuntimeConfig:
     # ---- compute path
     gemm: str = "lib"  # VCX_GEMM: "lib" (hipBLASLt/rocBLAS) or "vcx" (csrc/kernels/gemm.hip, opt-in: 0.74-0.84x lib)
+    mlp: str = "fused"  # VCX_MLP: GPT-2 MLP fc (+bias+GELU) and fc2-dgrad (*gelu' + bias grad) on the persistent
+    # hand-written GEMM's fused epilogues (csrc/kernels/gemm_ps.hip), other GEMMs on `gemm`; "lib": library + passes
     gemm_wgrad: str = "lib"  # VCX_GEMM_WGRAD: weight gradients on "lib" (split-M batched GEMM) or "vcx" (gemm_tn)
     gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)
     wgrad_big_split_min_m: int = 16384  # VCX_WGRAD_BIG_SPLIT_MIN_M: rows above which weight grads split over K
@@ -55,6 +57,7 @@ class RuntimeConfig:
 # field -> (environment variable, parser)
 _ENV = {
     "gemm": ("VCX_GEMM", str),
+    "mlp": ("VCX_MLP", str),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),
     "gemm_select": ("VCX_GEMM_SELECT", _bool),
     "wgrad_big_split_min_m": ("VCX_WGRAD_BIG_SPLIT_MIN_M", int),
@@ -74,7 +77,7 @@ _ENV = {
     "trace_dir": ("VCX_TRACE_DIR", str),
     "metrics_dir": ("VCX_METRICS_DIR", str),
 }
-_CHOICES = {"gemm": ("lib", "vcx"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl")}
+_CHOICES = {"gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl")}
 
 _lock = threading.Lock()
 

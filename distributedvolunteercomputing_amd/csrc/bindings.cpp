@@ -3,6 +3,7 @@
 // reset the whole node) and launches on the caller's current HIP stream, so the ops compose
 // with torch streams and hipGraph capture.
 #include <torch/extension.h>
+#include <map>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
@@ -178,6 +179,51 @@ void gemm_p(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor> 
   }
   vcx_gemm_p(a.data_ptr(), b.data_ptr(), c.data_ptr(), c2p, bp, cs, (int)M, (int)N, (int)K, (int)a.stride(0),
              (int)b.stride(0), (int)c.stride(0), (int)epi, (int)layout, cur_stream());
+}
+
+// Persistent store-overlapped GEMM (gemm_ps.hip): c[M, N] = a[M, K] . b[N, K]^T with epilogue
+// 0 store, 1 +bias, 2 +bias -> (c = pre, c2 = gelu(pre)); grid_cap <= 0: one workgroup per CU
+bool gemm_ps_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
+  return vcx_gemm_ps_supported((int)M, (int)N, (int)K, (int)epi);
+}
+
+void gemm_ps(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor> c2, c10::optional<at::Tensor> bias,
+             c10::optional<at::Tensor> colsum, int64_t epi, int64_t grid_cap) {
+  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_ps: 2-D cuda tensors");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
+              "gemm_ps: bf16 operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm_ps: K-contiguous rows");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_ps: shape mismatch");
+  TORCH_CHECK(vcx_gemm_ps_supported((int)M, (int)N, (int)K, (int)epi),
+              "gemm_ps: needs M, N % 256 == 0, K % 128 == 0, K >= 256, epilogue 0..4, N <= 16384 with a bias");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm_ps: 16-B aligned rows");
+  for (const at::Tensor* t : {&a, &b, &c})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_ps: 16-B aligned base pointers");
+  // buffer resources cover one 256-row panel each: 32-bit byte offsets
+  TORCH_CHECK(256 * std::max({a.stride(0), b.stride(0), c.stride(0)}) * 2 < (int64_t(1) << 31), "gemm_ps: rows too long");
+  void* c2p = nullptr;
+  if (epi == 2 || epi == 4) {
+    TORCH_CHECK(c2 && c2->sizes() == c.sizes() && c2->strides() == c.strides() && c2->scalar_type() == at::kBFloat16,
+                "gemm_ps: epilogue 2/4 needs c2 like c");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(c2->data_ptr()) % 16 == 0, "gemm_ps: 16-B aligned c2");
+    c2p = c2->data_ptr();
+  }
+  const void* bp = nullptr;
+  if (epi == 1 || epi == 2) {
+    TORCH_CHECK(bias && bias->numel() == N && bias->is_contiguous() && bias->scalar_type() == at::kBFloat16,
+                "gemm_ps: bias [N] bf16");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0, "gemm_ps: 16-B aligned bias");
+    bp = bias->data_ptr();
+  }
+  float* cs = nullptr;
+  if (epi == 4) {
+    TORCH_CHECK(colsum && colsum->numel() == N && colsum->scalar_type() == at::kFloat && colsum->is_contiguous(),
+                "gemm_ps: colsum [N] fp32");
+    cs = colsum->data_ptr<float>();
+  }
+  vcx_gemm_ps(a.data_ptr(), b.data_ptr(), c.data_ptr(), c2p, bp, cs, (int)M, (int)N, (int)K, (int)a.stride(0),
+              (int)b.stride(0), (int)c.stride(0), (int)epi, (int)grid_cap, cur_stream());
 }
 
 // 4-wave one-wave-per-SIMD GEMM (gemm4.hip): c[M, N] = a[M, K] . b[N, K]^T
@@ -674,6 +720,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nt_supported_epi", &gemm_nt_supported_epi);
   m.def("gemm_p_supported", &gemm_p_supported);
   m.def("gemm4", &gemm4);
+  m.def("gemm_ps_supported", &gemm_ps_supported);
+  m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
+        py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0);
   m.def("gemm_p", &gemm_p, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("layout") = 0);
   m.def("gemm_tn_supported", &gemm_tn_supported);

@@ -25,6 +25,13 @@ void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bi
 bool vcx_gemm_p_supported(int M, int N, int K, int layout);
 void vcx_gemm_p(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,
                 int lda, int ldb, int ldc, int epi, int layout, hipStream_t s);
+// gemm_ps.hip: persistent store-overlapped GEMM, C = A B^T (B [N, K]); epi 0 store, 1 +bias,
+// 2 +bias -> (C = pre, C2 = gelu(pre)); grid_cap <= 0: one workgroup per CU
+bool vcx_gemm_ps_supported(int M, int N, int K, int epi);
+int vcx_gemm_ps_grid(int M, int N, int grid_cap);
+// epi 4: C = (A B^T) * gelu'(C2) with fp32 column sums added into colsum
+void vcx_gemm_ps(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N,
+                 int K, int lda, int ldb, int ldc, int epi, int grid_cap, hipStream_t s);
 // gemm4.hip: 4-wave one-wave-per-SIMD GEMM (main-loop study), C = A B^T
 bool vcx_gemm4_supported(int M, int N, int K);
 void vcx_gemm4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, hipStream_t s);

@@ -290,23 +290,37 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
 
 
 # ---------------------------------------------------------------- fused GPT-2 MLP
+def gemm_ps_ok(M: int, N: int, K: int, epi: int, t) -> bool:
+    """The persistent store-overlapped GEMM (csrc/kernels/gemm_ps.hip) takes this shape/epilogue."""
+    return (config.get().mlp == "fused" and use_native(t) and t.dtype == torch.bfloat16
+            and bool(native().gemm_ps_supported(M, N, K, epi)))
+
+
 class _MlpGelu(torch.autograd.Function):
-    """y = gelu_tanh(x W1^T + b1) W2^T on the hand-written GEMM with fused epilogues:
+    """y = gelu_tanh(x W1^T + b1) W2^T with the two memory-bound MLP passes folded into GEMM epilogues:
     forward  fc:  one GEMM writes pre = x W1^T + b1 AND act = gelu(pre) (no bias_gelu pass);
     backward fc2-dgrad: one GEMM writes dpre = (dy W2) * gelu'(pre) and reduces db1 = sum dpre
-             in its epilogue (no bias_gelu_bwd pass, dact never hits HBM)."""
+             in its epilogue (no bias_gelu_bwd pass, dact never hits HBM).
+    `ps`: those two GEMMs run gemm_ps (persistent, 4 of 8 shapes at or above the library with the
+    fused epilogue; profiles/r3_gemm_ps.txt) and the other MLP GEMMs the library; otherwise all four
+    run the tiled gemm_nt (VCX_GEMM=vcx)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2):
+    def forward(ctx, x, w1, b1, w2, ps):
         C = native()
         x2 = x.reshape(-1, x.shape[-1])
         M, F_ = x2.shape[0], w1.shape[0]
         pre = torch.empty(M, F_, device=x.device, dtype=x.dtype)
         act = torch.empty_like(pre)
-        C.gemm_nt(x2, w1, pre, act, b1, None, 2)
-        y = gemm_nt(act, w2)
+        if ps:
+            C.gemm_ps(x2, w1, pre, act, b1, None, 2)
+            y = mm(act, w2, trans_b=True)
+        else:
+            C.gemm_nt(x2, w1, pre, act, b1, None, 2)
+            y = gemm_nt(act, w2)
         ctx.save_for_backward(x2, w1, b1, w2, pre, act)
         ctx.xshape = x.shape
+        ctx.ps = ps
         return y.view(*x.shape[:-1], w2.shape[0])
 
     @staticmethod
@@ -317,7 +331,10 @@ class _MlpGelu(torch.autograd.Function):
         M, F_ = pre.shape
         cs = torch.zeros(F_, device=dy.device, dtype=torch.float32)
         dpre = torch.empty_like(pre)
-        C.gemm_nt(dy2, transpose_weight(w2), dpre, pre, None, cs, 3)
+        if ctx.ps:
+            C.gemm_ps(dy2, transpose_weight(w2), dpre, pre, None, cs, 4)
+        else:
+            C.gemm_nt(dy2, transpose_weight(w2), dpre, pre, None, cs, 3)
         dw2, _ = _param_grads(dy2, act, w2, None, ctx.needs_input_grad[3], False)
         dw1, _ = _param_grads(dpre, x2, w1, None, ctx.needs_input_grad[1], False)
         db1 = None
@@ -327,23 +344,36 @@ class _MlpGelu(torch.autograd.Function):
                 C.add_f32_into_bf16(cs, gb, True)
             else:
                 db1 = cs.to(b1.dtype)
-        dx = gemm_nt(dpre, transpose_weight(w1)).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        return dx, dw1, db1, dw2
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (mm(dpre, w1) if ctx.ps else gemm_nt(dpre, transpose_weight(w1))).view(ctx.xshape)
+        return dx, dw1, db1, dw2, None
 
 
 def mlp_gelu_ok(x, w1, w2) -> bool:
+    return _mlp_mode(x, w1, w2) is not None
+
+
+def _mlp_mode(x, w1, w2):
+    """'ps' (fused epilogues on gemm_ps), 'nt' (everything on gemm_nt) or None (library + passes)."""
+    if not (native_linear_ok(w1) and x.dtype == torch.bfloat16):
+        return None
     M = x.numel() // x.shape[-1]
     F_, C_ = w1.shape
-    return (native_linear_ok(w1) and x.dtype == torch.bfloat16 and gemm_nt_ok(M, F_, C_, x)
-            and gemm_nt_ok(M, w2.shape[0], F_, x) and gemm_nt_ok(M, C_, w2.shape[0], x)
-            and gemm_nt_ok(M, F_, w2.shape[0], x))
+    if gemm_ps_ok(M, F_, C_, 2, x) and gemm_ps_ok(M, F_, w2.shape[0], 4, x):
+        return "ps"
+    if (gemm_nt_ok(M, F_, C_, x) and gemm_nt_ok(M, w2.shape[0], F_, x) and gemm_nt_ok(M, C_, w2.shape[0], x)
+            and gemm_nt_ok(M, F_, w2.shape[0], x)):
+        return "nt"
+    return None
 
 
 def mlp_gelu(x, w1, b1, w2):
     """gelu_tanh(x W1^T + b1) W2^T (GPT-2 MLP without the fc2 bias, which the following fused
     add + LayerNorm applies)."""
-    if mlp_gelu_ok(x, w1, w2):
-        return _MlpGelu.apply(x, w1, b1, w2)
+    mode = _mlp_mode(x, w1, w2)
+    if mode is not None:
+        return _MlpGelu.apply(x, w1, b1, w2, mode == "ps")
     from .activations import bias_gelu
 
     return linear(bias_gelu(linear(x, w1), b1), w2)

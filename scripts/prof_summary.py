@@ -9,7 +9,8 @@ idx = [i for i, r in enumerate(rows) if "adamw_flat" in r["Kernel_Name"]]
 a, b = idx[-2] + 1, idx[-1] + 1
 KEYS = ["attn_fwd", "attn_bwd_dq", "attn_bwd_dkdv", "attn_bwd_delta", "ln_fwd", "ln_bwd", "bias_gelu_fwd",
         "bias_gelu_bwd", "xent_fwd", "xent_bwd", "embed_fwd", "embed_bwd", "colsum", "adamw", "grad_sumsq",
-        "reduce_kernel", "elementwise", "copyBuffer", "fillBuffer", "adam_prologue", "splitk_reduce", "xent_fused"]
+        "reduce_kernel", "elementwise", "copyBuffer", "fillBuffer", "adam_prologue", "splitk_reduce", "xent_fused",
+        "gemm_ps_kernel", "gemm_nt_kernel", "transpose_bf16"]
 
 
 def short(n):

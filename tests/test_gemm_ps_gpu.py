@@ -1,0 +1,64 @@
+"""Persistent store-overlapped GEMM (csrc/kernels/gemm_ps.hip) against an fp32 PyTorch reference:
+every epilogue, one tile per workgroup, several tiles per workgroup (the continuous LDS ring across
+tile boundaries and the stores left in flight into the next tile), a reduced grid, strided rows."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,N,K,cap", [(256, 256, 256, 0), (2048, 3072, 768, 0), (4096, 2304, 768, 16),
+                                       (8192, 768, 3072, 8), (256 * 40, 512, 1024, 0)])
+def test_gemm_ps_matches_fp32(gpu, M, N, K, cap):
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    torch.manual_seed(M + N + K)
+    dev = "cuda"
+    a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    b = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.05
+    bias = torch.randn(N, device=dev, dtype=torch.bfloat16) * 0.1
+    ref = a.float() @ b.float().t()
+    for epi in range(3):
+        c = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+        c2 = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+        C.gemm_ps(a, b, c, c2, bias, None, epi, cap)
+        torch.cuda.synchronize()
+        want = ref if epi == 0 else ref + bias.float()
+        err = (c.float() - want).abs().max().item()
+        assert err < 2e-2 * want.abs().max().item(), (epi, err)
+        if epi == 2:
+            g = F.gelu(want, approximate="tanh")
+            assert (c2.float() - g).abs().max().item() < 3e-2 * g.abs().max().item()
+    # DGELU: c = (a b^T) * gelu'(pre) and fp32 column sums (the bias gradient) into cs
+    pre = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
+    c = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+    cs = torch.zeros(N, device=dev, dtype=torch.float32)
+    C.gemm_ps(a, b, c, pre, None, cs, 4, cap)
+    torch.cuda.synchronize()
+    x = pre.float().requires_grad_()
+    F.gelu(x, approximate="tanh").backward(ref.to(torch.bfloat16).float())
+    assert (c.float() - x.grad).abs().max().item() < 2e-2 * x.grad.abs().max().item()
+    s = x.grad.sum(0)
+    assert (cs - s).abs().max().item() < 1e-2 * s.abs().max().item() + 1e-2
+
+
+def test_gemm_ps_strided_rows_and_refusals(gpu):
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    dev = "cuda"
+    a = torch.randn(512, 1024, device=dev, dtype=torch.bfloat16)[:, :768]  # lda = 1024
+    b = torch.randn(768, 768, device=dev, dtype=torch.bfloat16) * 0.05
+    wide = torch.zeros(512, 1024, device=dev, dtype=torch.bfloat16)
+    c = wide[:, :768]  # ldc = 1024; columns past 768 must stay untouched
+    C.gemm_ps(a, b, c)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().t()
+    assert (c.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    assert wide[:, 768:].abs().max().item() == 0
+    assert not C.gemm_ps_supported(512, 768, 192, 0)  # K % 128
+    assert not C.gemm_ps_supported(500, 768, 768, 0)  # M % 256
+    with pytest.raises(RuntimeError):
+        C.gemm_ps(a[:, 4:260], b[:256, :256].contiguous(), torch.empty(512, 256, device=dev, dtype=torch.bfloat16))
