@@ -628,8 +628,8 @@ __global__ void __launch_bounds__(256) xent_bwd_kernel(const bf16* logits, const
 // (softmax - onehot) / nvalid over the same buffer, versus a read for the loss plus a read and a
 // write for the gradient. The loss backward's incoming scalar is applied afterwards only if it is
 // not 1 (xent_rescale_kernel). Rows with a negative target contribute neither loss nor gradient.
-template <int TPB, int NV>
-__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(6))) xent_fused_kernel(
+template <int TPB, int NV, int WPE = 6>
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) xent_fused_kernel(
     bf16* __restrict__ logits, const int64_t* __restrict__ tgt, const float* __restrict__ nvalid,
     float* __restrict__ loss_out, int V, int Vp) {
   constexpr int NW = TPB / 64;
@@ -898,6 +898,20 @@ int vcx_xent_fused(void* logits, const int64_t* tgt, const float* nvalid, float*
   // other's reductions and stores
   const int Vp8 = Vp / 8;
   dim3 grid(R);
+  // VCX_XENT_TPB=256 / 512: more, smaller row blocks per CU (4-5 rows in flight per CU instead of
+  // 2, each thread holding more of its row); A/B in profiles/r3_xent_variants.txt
+  static const int tpb = [] {
+    const char* e = getenv("VCX_XENT_TPB");
+    return e ? atoi(e) : 768;
+  }();
+  if (tpb == 256 && Vp8 <= 256 * 25) {
+    hipLaunchKernelGGL((xent_fused_kernel<256, 25, 4>), grid, dim3(256), 0, s, (bf16*)logits, tgt, nvalid, loss, V, Vp);
+    return 1;
+  }
+  if (tpb == 512 && Vp8 <= 512 * 13) {
+    hipLaunchKernelGGL((xent_fused_kernel<512, 13, 5>), grid, dim3(512), 0, s, (bf16*)logits, tgt, nvalid, loss, V, Vp);
+    return 1;
+  }
   if (Vp8 <= 768 * 4)
     hipLaunchKernelGGL((xent_fused_kernel<768, 4>), grid, dim3(768), 0, s, (bf16*)logits, tgt, nvalid, loss, V, Vp);
   else if (Vp8 <= 768 * 9)
