@@ -221,30 +221,30 @@ __global__ void __launch_bounds__(NT, 1)
   // for the stores. (Counting stores as younger ops in flight is not safe: stores retired ahead
   // of older operand DMA on vmcnt, measured as rare wrong tiles.)
   auto step = [&](int s, Frags& fc, Frags& fn, const Rs& sa, const Rs& sb, int ks, bool nowait, auto LD,
-                  auto VM) {
-    constexpr bool ld = decltype(LD)::value;
+                  auto VM, auto ST) {
+    constexpr bool ld = decltype(LD)::value, st = decltype(ST)::value;
     if (nowait)
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     else
       wait_vm<decltype(VM)::value>();
     barrier();
     const int slot = s & 3, nslot = (s + 1) & 3;
-    stage_piece(sa, sb, ks, slot, P0{});
+    if constexpr (st) stage_piece(sa, sb, ks, slot, P0{});
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I0c{}, I2c{});
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (ld) load_x(nslot, 0), load_w(fn, nslot, 0);
-    stage_piece(sa, sb, ks, slot, P1{});
+    if constexpr (st) stage_piece(sa, sb, ks, slot, P1{});
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I2c{}, I4c{});
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (ld) load_x(nslot, 2), load_w(fn, nslot, 2);
-    stage_piece(sa, sb, ks, slot, P2{});
+    if constexpr (st) stage_piece(sa, sb, ks, slot, P2{});
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I4c{}, I6c{});
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (ld) load_x(nslot, 4), load_y(fn, nslot);
-    stage_piece(sa, sb, ks, slot, P3{});
+    if constexpr (st) stage_piece(sa, sb, ks, slot, P3{});
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I6c{}, I8c{});
   };
@@ -270,14 +270,17 @@ __global__ void __launch_bounds__(NT, 1)
         pre[i][q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, c_offA + q * 8 * ldc * 2,
                                                                                       i * 16 * ldc * 2, 0));
   };
-  auto epilogue = [&](int m0, int n0) {
+  auto epilogue = [&](int m0, int n0, auto DRAIN) {
     float cs[8];  // EPI_DGELU: fp32 column sums of this lane's 8 columns over its 16 rows
 #pragma unroll
     for (int e = 0; e < 8; ++e) cs[e] = 0.f;
     // the next tile's slices 0..3 land before any store is issued (see step); the last MFMAs'
     // results -> VALU readers (v_permlane16_swap): 12 wait states for an 8-pass XDL op; the MFMAs are
     // inline asm, so hipcc's hazard recognizer does not pad this
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 4" ::: "memory");
+    if constexpr (decltype(DRAIN)::value)
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 4" ::: "memory");
+    else
+      asm volatile("s_nop 7\n\ts_nop 4" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     const u32x4 rc = desc_of(C + (int64_t)m0 * ldc + n0, BM * ldc * 2);
     u32x4 rc2;
@@ -400,32 +403,36 @@ __global__ void __launch_bounds__(NT, 1)
     Rs na, nb;  // the next tile's resources (the last tile re-stages its own first slices: never read)
     tile_rs(more ? vn : vb, na, nb);
     using V8 = std::integral_constant<int, 8>;
+    using Tt = std::true_type;
+    using Ff = std::false_type;
     int s = 0;
-    for (; s + 2 < nk; s += 2) {
-      const int k4 = s + 4, k5 = s + 5;
-      const bool n4 = k4 >= nk, n5 = k5 >= nk;
-      step(s, f0, f1, n4 ? na : ra, n4 ? nb : rb, n4 ? k4 - nk : k4, s < 3, std::true_type{}, V8{});
-      step(s + 1, f1, f0, n5 ? na : ra, n5 ? nb : rb, n5 ? k5 - nk : k5, s + 1 < 3, std::true_type{}, V8{});
+    for (; s + 4 < nk; s += 2) {  // staging this tile's slices s + 4, s + 5
+      step(s, f0, f1, ra, rb, s + 4, s < 3, Tt{}, V8{}, Tt{});
+      step(s + 1, f1, f0, ra, rb, s + 5, s + 1 < 3, Tt{}, V8{}, Tt{});
     }
-    // last pair: slices s, s + 1 = nk - 2, nk - 1; staging the next tile's slices 2, 3
-    step(s, f0, f1, na, nb, 2, false, std::true_type{}, V8{});
+    // last 4 steps: the next tile's slices 0..3 go into the same ring
+    step(s, f0, f1, na, nb, 0, false, Tt{}, V8{}, Tt{});
+    step(s + 1, f1, f0, na, nb, 1, false, Tt{}, V8{}, Tt{});
+    step(s + 2, f0, f1, na, nb, 2, false, Tt{}, V8{}, Tt{});
     if constexpr (EPI == EPI_DGELU) {
       load_pre(m0, n0);  // lands behind the last step's MFMAs; its fragments are not read there
       // the 16 pre loads are younger loads than the awaited slice (loads retire in order)
-      step(s + 1, f1, f0, na, nb, 3, false, std::false_type{}, std::integral_constant<int, 24>{});
-      epilogue(m0, n0);
+      step(s + 3, f1, f0, na, nb, 3, false, Ff{}, std::integral_constant<int, 24>{}, Tt{});
+      epilogue(m0, n0, Tt{});
       // the next tile's slice 0 (slot 0) landed before the epilogue's vmcnt(0)
       load_x(0, 0), load_x(0, 2), load_x(0, 4), load_y(f0, 0), load_w(f0, 0, 0), load_w(f0, 0, 2);
     } else {
-      step(s + 1, f1, f0, na, nb, 3, false, std::true_type{}, V8{});
-      epilogue(m0, n0);  // the fragments of the next tile's slice 0 are in (x, f0) already
+      step(s + 3, f1, f0, na, nb, 3, false, Tt{}, V8{}, Tt{});
+      epilogue(m0, n0, Tt{});  // the fragments of the next tile's slice 0 are in (x, f0) already
     }
     if (!more) break;
     vb = vn;
     ra = na;
     rb = nb;
   }
-  wait_vm<0>();  // drain the stores and the dummy staging before the workgroup's LDS is released
+  // no final drain: the last epilogue's vmcnt(0) retired every LDS-DMA (the last tile re-stages
+  // its own first slices as dummies), so only its stores are in flight, and those may outlive the
+  // waves -- the next workgroup on this CU starts while they drain
 }
 
 }  // namespace gemm_ps
@@ -446,7 +453,7 @@ int vcx_gemm_ps_grid(int M, int N, int grid_cap) {
     return n;
   }();
   const int tiles = (M / gemm_ps::BM) * (N / gemm_ps::BN);
-  int grid = grid_cap > 0 ? std::min(grid_cap, ncu) : ncu;  // co-resident workgroups only (flag waits)
+  int grid = grid_cap > 0 ? grid_cap : ncu;
   grid = grid < tiles ? grid & ~7 : tiles;                   // a multiple of 8 (XCD remap) or one tile each
   return grid <= 0 ? tiles : grid;
 }
