@@ -188,15 +188,18 @@ bool gemm_ps_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
 }
 
 void gemm_ps(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor> c2, c10::optional<at::Tensor> bias,
-             c10::optional<at::Tensor> colsum, int64_t epi, int64_t grid_cap) {
+             c10::optional<at::Tensor> colsum, int64_t epi, int64_t grid_cap, int64_t waves, int64_t stagger) {
   TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_ps: 2-D cuda tensors");
+  TORCH_CHECK(waves == 8 || waves == 4, "gemm_ps: waves 8 (one workgroup per CU) or 4 (two per CU)");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
               "gemm_ps: bf16 operands");
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm_ps: K-contiguous rows");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_ps: shape mismatch");
-  TORCH_CHECK(vcx_gemm_ps_supported((int)M, (int)N, (int)K, (int)epi),
-              "gemm_ps: needs M, N % 256 == 0, K % 128 == 0, K >= 256, epilogue 0..4, N <= 16384 with a bias");
+  TORCH_CHECK(waves == 8 ? vcx_gemm_ps_supported((int)M, (int)N, (int)K, (int)epi)
+                         : vcx_gemm_ps2_supported((int)M, (int)N, (int)K, (int)epi),
+              "gemm_ps: needs M, N % 256 == 0, K % 128 == 0, K >= 256, epilogue 0..4, N <= 16384 with a bias "
+              "(4 waves: N % 128 == 0, K % 96 == 0, K >= 192, epilogue 0..3)");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm_ps: 16-B aligned rows");
   for (const at::Tensor* t : {&a, &b, &c})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_ps: 16-B aligned base pointers");
@@ -223,7 +226,7 @@ void gemm_ps(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
     cs = colsum->data_ptr<float>();
   }
   vcx_gemm_ps(a.data_ptr(), b.data_ptr(), c.data_ptr(), c2p, bp, cs, (int)M, (int)N, (int)K, (int)a.stride(0),
-              (int)b.stride(0), (int)c.stride(0), (int)epi, (int)grid_cap, cur_stream());
+              (int)b.stride(0), (int)c.stride(0), (int)epi, (int)grid_cap, (int)waves, (int)stagger, cur_stream());
 }
 
 // 4-wave one-wave-per-SIMD GEMM (gemm4.hip): c[M, N] = a[M, K] . b[N, K]^T
@@ -722,7 +725,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm4", &gemm4);
   m.def("gemm_ps_supported", &gemm_ps_supported);
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
-        py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0);
+        py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0,
+        py::arg("waves") = 8, py::arg("stagger") = 0);
   m.def("gemm_p", &gemm_p, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("layout") = 0);
   m.def("gemm_tn_supported", &gemm_tn_supported);

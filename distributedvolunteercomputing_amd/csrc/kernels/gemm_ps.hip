@@ -84,26 +84,42 @@ __device__ __forceinline__ u32x4 desc_of(const void* base, int bytes) {
   return u32x4{(unsigned)a, (unsigned)(a >> 32) & 0xffffu, (unsigned)bytes, 0x00020000u};
 }
 
+// Workgroup geometry. NW = 8: one 512-thread workgroup per CU, 256 x 256 tiles, 4-slot ring.
+// NW = 4: two co-resident 256-thread workgroups per CU, 256 x 128 tiles, 3-slot rings (72 KB each):
+// the same 128 x 64 wave tile and main loop, but one workgroup's epilogue stall is the other's
+// compute time (their vmcnt queues are separate).
+template <int NW>
+struct Geo {
+  static constexpr int NTH = NW * 64, BNt = NW == 8 ? 256 : 128, WNC = NW / 2, NSLOT = NW == 8 ? 4 : 3;
+  static constexpr int SLOTA = BM * ROWB, SLOTB = SLOTA + BNt * ROWB, RINGB = NSLOT * SLOTB;
+  static constexpr int APW = 16 / NW, BPW = BNt / 16 / NW, PPW = APW + BPW;  // LDS-DMA pieces per wave
+  static constexpr int VMW = PPW * (NSLOT - 2);  // vmcnt of a step: the slices younger than the awaited one
+};
+
 struct Frags {
   sx8 y[2];  // A fragments of the wave's row blocks 6, 7
   sx8 w[4];  // B fragments: the wave's 4 column blocks of 16
 };
 
-template <int EPI>
-__global__ void __launch_bounds__(NT, 1)
-    gemm_ps_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
-                   bf16* __restrict__ C2, const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
-                   int K, int lda, int ldb, int ldc, int tilesN, int tiles) {
+// (the body is a device function shared by two kernel templates with literal launch bounds: a
+// kernel template on NW lost its host-side stubs)
+template <int EPI, int NW>
+__device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                             bf16* __restrict__ C, bf16* __restrict__ C2,
+                                             const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
+                                             int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger) {
+  using Gm = Geo<NW>;
+  constexpr int BNt = Gm::BNt, SLOTA = Gm::SLOTA, SLOTB = Gm::SLOTB, RINGB = Gm::RINGB, NSLOT = Gm::NSLOT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
+  const int wm = wid / Gm::WNC, wn = wid % Gm::WNC;
   const int G = gridDim.x, bid = blockIdx.x;
   const int nk = K / BKS;  // multiple of 4, >= 8 (host check)
 
   if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {  // the bias row, once per workgroup
-    bf16* bl = (bf16*)(smem + RING);
-    for (int c = tid * 8; c < N; c += NT * 8) *(bf16x8*)(bl + c) = *(const bf16x8*)(bias + c);
+    bf16* bl = (bf16*)(smem + RINGB);
+    for (int c = tid * 8; c < N; c += Gm::NTH * 8) *(bf16x8*)(bl + c) = *(const bf16x8*)(bias + c);
     __syncthreads();
   }
 
@@ -119,7 +135,7 @@ __global__ void __launch_bounds__(NT, 1)
     const int gsize = min(tilesM - gfirst, GROUP_M);
     const int rr = wg - (wg / per_group) * per_group;
     m0 = (gfirst + rr % gsize) * BM;
-    n0 = (rr / gsize) * BN;
+    n0 = (rr / gsize) * BNt;
   };
 
   // ---- LDS-DMA staging through per-tile buffer resources; per-lane offsets are tile-invariant.
@@ -128,8 +144,9 @@ __global__ void __launch_bounds__(NT, 1)
   // chunk l & 3 holding logical chunk (l & 3) ^ swz(row) (swizzle applied to the source address)
   const int prow = lane >> 2;
   const int pch = (lane & 3) ^ swz(prow);
-  const int a_off0 = ((wid * 16 + prow) * lda + pch * 8) * 2, a_off1 = a_off0 + 128 * lda * 2;
-  const int b_off0 = ((wid * 16 + prow) * ldb + pch * 8) * 2, b_off1 = b_off0 + 128 * ldb * 2;
+  // piece p < APW: A rows (wid + NW p) * 16 + prow; else B rows (wid + NW (p - APW)) * 16 + prow
+  const int a_off0 = ((wid * 16 + prow) * lda + pch * 8) * 2, a_pstep = NW * 16 * lda * 2;
+  const int b_off0 = ((wid * 16 + prow) * ldb + pch * 8) * 2, b_pstep = NW * 16 * ldb * 2;
   char* const lds_piece = smem + wid * 1024;
   auto rsrc = [](const bf16* base, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
@@ -139,23 +156,31 @@ __global__ void __launch_bounds__(NT, 1)
     int m0, n0;
     coords(vb, m0, n0);
     ra = rsrc(A + (int64_t)m0 * lda, BM * lda * 2);
-    rb = rsrc(B + (int64_t)n0 * ldb, BN * ldb * 2);
+    rb = rsrc(B + (int64_t)n0 * ldb, BNt * ldb * 2);
   };
   auto stage_piece = [&](const Rs& ra, const Rs& rb, int kslice, int slot, auto P) {
     constexpr int p = decltype(P)::value;
-    char* sl = lds_piece + slot * SLOT;
+    char* sl = lds_piece + slot * SLOTB;
     const int soff = kslice * (BKS * 2);
-    if constexpr (p == 0)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)sl, 16, a_off0, soff, 0, 0);
-    if constexpr (p == 1)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(sl + 8 * 1024), 16,
-                                               a_off1, soff, 0, 0);
-    if constexpr (p == 2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)(sl + SLOT_A), 16, b_off0,
-                                               soff, 0, 0);
-    if constexpr (p == 3)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)(sl + SLOT_A + 8 * 1024),
-                                               16, b_off1, soff, 0, 0);
+    if constexpr (p < Gm::APW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(sl + NW * p * 1024), 16,
+                                               a_off0 + p * a_pstep, soff, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, (__attribute__((address_space(3))) void*)(sl + SLOTA + NW * (p - Gm::APW) * 1024), 16,
+          b_off0 + (p - Gm::APW) * b_pstep, soff, 0, 0);
+  };
+  // the pieces of one slice spread over the step's 4 MFMA groups (NW = 8: one each; NW = 4: 2,1,2,1)
+  auto stage_group = [&](const Rs& ra, const Rs& rb, int kslice, int slot, auto GR) {
+    constexpr int g = decltype(GR)::value;
+    if constexpr (Gm::PPW == 4) {
+      stage_piece(ra, rb, kslice, slot, std::integral_constant<int, g>{});
+    } else {
+      static_assert(Gm::PPW == 6, "pieces per wave");
+      constexpr int first = g == 0 ? 0 : g == 1 ? 2 : g == 2 ? 3 : 5;
+      stage_piece(ra, rb, kslice, slot, std::integral_constant<int, first>{});
+      if constexpr (g == 0 || g == 2) stage_piece(ra, rb, kslice, slot, std::integral_constant<int, first + 1>{});
+    }
   };
   using P0 = std::integral_constant<int, 0>;
   using P1 = std::integral_constant<int, 1>;
@@ -166,23 +191,23 @@ __global__ void __launch_bounds__(NT, 1)
   const int frow = lane & 15;
   const int foff = frow * ROWB + (((lane >> 4) ^ swz(frow)) << 4);
   const char* xa = smem + (wm * 128) * ROWB + foff;
-  const char* wb = smem + SLOT_A + (wn * 64) * ROWB + foff;
+  const char* wb = smem + SLOTA + (wn * 64) * ROWB + foff;
   // A rows 0..5 are single-buffered (x, refilled right behind the MFMA group that used them);
   // rows 6, 7 and the B fragments alternate between two named sets (Frags), so every read of the
   // next slice is issued before the step's last MFMA group (96 -> 72 fragment VGPRs)
   sx8 x[6];
   auto load_x = [&](int slot, int i0) {
-    const int so = slot * SLOT;
+    const int so = slot * SLOTB;
     x[i0] = *(const sx8*)(xa + so + i0 * 16 * ROWB);
     x[i0 + 1] = *(const sx8*)(xa + so + (i0 + 1) * 16 * ROWB);
   };
   auto load_w = [&](Frags& f, int slot, int j0) {
-    const int so = slot * SLOT;
+    const int so = slot * SLOTB;
     f.w[j0] = *(const sx8*)(wb + so + j0 * 16 * ROWB);
     f.w[j0 + 1] = *(const sx8*)(wb + so + (j0 + 1) * 16 * ROWB);
   };
   auto load_y = [&](Frags& f, int slot) {
-    const int so = slot * SLOT;
+    const int so = slot * SLOTB;
     f.y[0] = *(const sx8*)(xa + so + 6 * 16 * ROWB);
     f.y[1] = *(const sx8*)(xa + so + 7 * 16 * ROWB);
   };
@@ -228,23 +253,23 @@ __global__ void __launch_bounds__(NT, 1)
     else
       wait_vm<decltype(VM)::value>();
     barrier();
-    const int slot = s & 3, nslot = (s + 1) & 3;
-    if constexpr (st) stage_piece(sa, sb, ks, slot, P0{});
+    const int slot = s % NSLOT, nslot = (s + 1) % NSLOT;
+    if constexpr (st) stage_group(sa, sb, ks, slot, P0{});
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I0c{}, I2c{});
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (ld) load_x(nslot, 0), load_w(fn, nslot, 0);
-    if constexpr (st) stage_piece(sa, sb, ks, slot, P1{});
+    if constexpr (st) stage_group(sa, sb, ks, slot, P1{});
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I2c{}, I4c{});
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (ld) load_x(nslot, 2), load_w(fn, nslot, 2);
-    if constexpr (st) stage_piece(sa, sb, ks, slot, P2{});
+    if constexpr (st) stage_group(sa, sb, ks, slot, P2{});
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I4c{}, I6c{});
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (ld) load_x(nslot, 4), load_y(fn, nslot);
-    if constexpr (st) stage_piece(sa, sb, ks, slot, P3{});
+    if constexpr (st) stage_group(sa, sb, ks, slot, P3{});
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I6c{}, I8c{});
   };
@@ -257,7 +282,7 @@ __global__ void __launch_bounds__(NT, 1)
   // store A of row block i: lanes of rows 0..7 write (row r, jp 0), rows 8..15 write (row r - 8,
   // jp 1); store B is 8 rows further down
   const int c_offA = ((wm * 128 + (frow & 7)) * ldc + ccol + ((frow & 8) ? 32 : 0)) * 2;
-  const bf16* bl = (const bf16*)(smem + RING);
+  const bf16* bl = (const bf16*)(smem + RINGB);
   // EPI_DGELU: the pre-activation tile, read into registers (16 KB per wave) while the tile's last
   // step computes, at the positions the exchanged stores write
   u32x4 pre[8][2];
@@ -378,23 +403,31 @@ __global__ void __launch_bounds__(NT, 1)
   };
 
 
-  // ---- prologue: slices 0..3 of the first tile
+  // NW = 4: the second workgroup of each CU pair starts `stagger` x ~8k cycles late, so that the
+  // two co-resident workgroups reach their tile boundaries at different times
+  if (NW == 4 && stagger > 0 && bid >= G / 2)
+    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
+
+  // ---- prologue: slices 0..NSLOT-1 of the first tile
   int vb = bid;
   Rs ra, rb;
   tile_rs(vb, ra, rb);
 #define VCX_PS_STAGE_U(U_)                                                                                   \
-  stage_piece(ra, rb, (U_), (U_), P0{}), stage_piece(ra, rb, (U_), (U_), P1{}),                              \
-      stage_piece(ra, rb, (U_), (U_), P2{}), stage_piece(ra, rb, (U_), (U_), P3{});
+  stage_group(ra, rb, (U_), (U_), P0{}), stage_group(ra, rb, (U_), (U_), P1{}),                              \
+      stage_group(ra, rb, (U_), (U_), P2{}), stage_group(ra, rb, (U_), (U_), P3{});
   VCX_PS_STAGE_U(0)
   VCX_PS_STAGE_U(1)
   VCX_PS_STAGE_U(2)
-  VCX_PS_STAGE_U(3)
+  if constexpr (NSLOT == 4) VCX_PS_STAGE_U(3)
 #undef VCX_PS_STAGE_U
-  wait_vm<0>();  // slices 0..3 landed
+  wait_vm<0>();  // the first NSLOT slices landed
   barrier();
   Frags f0, f1;
   load_x(0, 0), load_x(0, 2), load_x(0, 4), load_y(f0, 0), load_w(f0, 0, 0), load_w(f0, 0, 2);
 
+  using VM = std::integral_constant<int, Gm::VMW>;
+  using Tt = std::true_type;
+  using Ff = std::false_type;
   while (true) {
     int m0, n0;
     coords(vb, m0, n0);
@@ -402,27 +435,36 @@ __global__ void __launch_bounds__(NT, 1)
     const bool more = vn < tiles;
     Rs na, nb;  // the next tile's resources (the last tile re-stages its own first slices: never read)
     tile_rs(more ? vn : vb, na, nb);
-    using V8 = std::integral_constant<int, 8>;
-    using Tt = std::true_type;
-    using Ff = std::false_type;
-    int s = 0;
-    for (; s + 4 < nk; s += 2) {  // staging this tile's slices s + 4, s + 5
-      step(s, f0, f1, ra, rb, s + 4, s < 3, Tt{}, V8{}, Tt{});
-      step(s + 1, f1, f0, ra, rb, s + 5, s + 1 < 3, Tt{}, V8{}, Tt{});
-    }
-    // last 4 steps: the next tile's slices 0..3 go into the same ring
-    step(s, f0, f1, na, nb, 0, false, Tt{}, V8{}, Tt{});
-    step(s + 1, f1, f0, na, nb, 1, false, Tt{}, V8{}, Tt{});
-    step(s + 2, f0, f1, na, nb, 2, false, Tt{}, V8{}, Tt{});
-    if constexpr (EPI == EPI_DGELU) {
-      load_pre(m0, n0);  // lands behind the last step's MFMAs; its fragments are not read there
-      // the 16 pre loads are younger loads than the awaited slice (loads retire in order)
-      step(s + 3, f1, f0, na, nb, 3, false, Ff{}, std::integral_constant<int, 24>{}, Tt{});
-      epilogue(m0, n0, Tt{});
-      // the next tile's slice 0 (slot 0) landed before the epilogue's vmcnt(0)
-      load_x(0, 0), load_x(0, 2), load_x(0, 4), load_y(f0, 0), load_w(f0, 0, 0), load_w(f0, 0, 2);
+    if constexpr (NW == 8) {
+      int s = 0;
+      for (; s + 4 < nk; s += 2) {  // staging this tile's slices s + 4, s + 5
+        step(s, f0, f1, ra, rb, s + 4, s < 3, Tt{}, VM{}, Tt{});
+        step(s + 1, f1, f0, ra, rb, s + 5, s + 1 < 3, Tt{}, VM{}, Tt{});
+      }
+      // last 4 steps: the next tile's slices 0..3 go into the same ring
+      step(s, f0, f1, na, nb, 0, false, Tt{}, VM{}, Tt{});
+      step(s + 1, f1, f0, na, nb, 1, false, Tt{}, VM{}, Tt{});
+      step(s + 2, f0, f1, na, nb, 2, false, Tt{}, VM{}, Tt{});
+      if constexpr (EPI == EPI_DGELU) {
+        load_pre(m0, n0);  // lands behind the last step's MFMAs; its fragments are not read there
+        // the 16 pre loads are younger loads than the awaited slice (loads retire in order)
+        step(s + 3, f1, f0, na, nb, 3, false, Ff{}, std::integral_constant<int, 24>{}, Tt{});
+        epilogue(m0, n0, Tt{});
+        // the next tile's slice 0 (slot 0) landed before the epilogue's vmcnt(0)
+        load_x(0, 0), load_x(0, 2), load_x(0, 4), load_y(f0, 0), load_w(f0, 0, 0), load_w(f0, 0, 2);
+      } else {
+        step(s + 3, f1, f0, na, nb, 3, false, Tt{}, VM{}, Tt{});
+        epilogue(m0, n0, Tt{});  // the fragments of the next tile's slice 0 are in (x, f0) already
+      }
     } else {
-      step(s + 3, f1, f0, na, nb, 3, false, Tt{}, V8{}, Tt{});
+      // 3-slot ring: step s stages slice s + 3 (the next tile's slices 0..2 in the last 3 steps);
+      // steps 0, 1 wait for slices that landed before the previous epilogue's stores
+      for (int s = 0; s < nk; s += 2) {
+        const int k3 = s + 3, k4 = s + 4;
+        const bool n3 = k3 >= nk, n4 = k4 >= nk;
+        step(s, f0, f1, n3 ? na : ra, n3 ? nb : rb, n3 ? k3 - nk : k3, s < 2, Tt{}, VM{}, Tt{});
+        step(s + 1, f1, f0, n4 ? na : ra, n4 ? nb : rb, n4 ? k4 - nk : k4, s + 1 < 2, Tt{}, VM{}, Tt{});
+      }
       epilogue(m0, n0, Tt{});  // the fragments of the next tile's slice 0 are in (x, f0) already
     }
     if (!more) break;
@@ -432,7 +474,23 @@ __global__ void __launch_bounds__(NT, 1)
   }
   // no final drain: the last epilogue's vmcnt(0) retired every LDS-DMA (the last tile re-stages
   // its own first slices as dummies), so only its stores are in flight, and those may outlive the
-  // waves -- the next workgroup on this CU starts while they drain
+  // waves
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1)
+    gemm_ps_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
+                   bf16* __restrict__ C2, const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
+                   int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger) {
+  gemm_ps_body<EPI, 8>(A, B, C, C2, bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger);
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(256, 2)
+    gemm_ps4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
+                    bf16* __restrict__ C2, const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
+                    int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger) {
+  gemm_ps_body<EPI, 4>(A, B, C, C2, bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger);
 }
 
 }  // namespace gemm_ps
@@ -445,37 +503,56 @@ bool vcx_gemm_ps_supported(int M, int N, int K, int epi) {
          epi <= 4 && (epi == 0 || epi >= 3 || N <= gemm_ps::BIAS_MAX);
 }
 
-int vcx_gemm_ps_grid(int M, int N, int grid_cap) {
+// the two-workgroups-per-CU geometry (NW = 4): N % 128, K % 96 (3-slot ring), no DGELU epilogue
+bool vcx_gemm_ps2_supported(int M, int N, int K, int epi) {
+  return M > 0 && N > 0 && M % gemm_ps::BM == 0 && N % 128 == 0 && K % 96 == 0 && K >= 192 && epi >= 0 && epi <= 3 &&
+         (epi == 0 || epi == 3 || N <= gemm_ps::BIAS_MAX);
+}
+
+int vcx_gemm_ps_grid(int M, int N, int grid_cap, int nw) {
   static const int ncu = [] {
     int dev = 0, n = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     return n;
   }();
-  const int tiles = (M / gemm_ps::BM) * (N / gemm_ps::BN);
-  int grid = grid_cap > 0 ? grid_cap : ncu;
-  grid = grid < tiles ? grid & ~7 : tiles;                   // a multiple of 8 (XCD remap) or one tile each
+  const int tiles = (M / gemm_ps::BM) * (N / (nw == 8 ? 256 : 128));
+  int grid = grid_cap > 0 ? grid_cap : (nw == 8 ? ncu : 2 * ncu);
+  grid = grid < tiles ? grid & ~7 : tiles;  // a multiple of 8 (XCD remap) or one tile each
   return grid <= 0 ? tiles : grid;
 }
 
 void vcx_gemm_ps(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N,
-                 int K, int lda, int ldb, int ldc, int epi, int grid_cap, hipStream_t s) {
+                 int K, int lda, int ldb, int ldc, int epi, int grid_cap, int nw, int stagger, hipStream_t s) {
   using namespace gemm_ps;
   static const bool attrs = [] {
     for (const void* k : {(const void*)gemm_ps_kernel<EPI_STORE>, (const void*)gemm_ps_kernel<EPI_BIAS>,
                           (const void*)gemm_ps_kernel<EPI_BIAS_GELU>, (const void*)gemm_ps_kernel<EPI_NONE>,
-                          (const void*)gemm_ps_kernel<EPI_DGELU>})
+                          (const void*)gemm_ps_kernel<EPI_DGELU>, (const void*)gemm_ps4_kernel<EPI_STORE>,
+                          (const void*)gemm_ps4_kernel<EPI_BIAS>, (const void*)gemm_ps4_kernel<EPI_BIAS_GELU>,
+                          (const void*)gemm_ps4_kernel<EPI_NONE>})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, RING + 2 * BIAS_MAX);
     return true;
   }();
   (void)attrs;
-  const int tilesN = N / BN, tiles = (M / BM) * tilesN;
-  const int grid = vcx_gemm_ps_grid(M, N, grid_cap);
-  const int lds = RING + (epi == EPI_BIAS || epi == EPI_BIAS_GELU ? (N * 2 + 15) & ~15 : 0);
+  const int bn = nw == 8 ? 256 : 128;
+  const int tilesN = N / bn, tiles = (M / BM) * tilesN;
+  const int grid = vcx_gemm_ps_grid(M, N, grid_cap, nw);
+  const int ring = nw == 8 ? Geo<8>::RINGB : Geo<4>::RINGB;
+  const int lds = ring + (epi == EPI_BIAS || epi == EPI_BIAS_GELU ? (N * 2 + 15) & ~15 : 0);
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, s, (const bf16*)A, (const bf16*)B, (bf16*)C, (bf16*)C2,
-                       (const bf16*)bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(nw * 64), lds, s, (const bf16*)A, (const bf16*)B, (bf16*)C,
+                       (bf16*)C2, (const bf16*)bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger);
   };
+  if (nw == 4) {
+    switch (epi) {
+      case EPI_STORE: go(gemm_ps4_kernel<EPI_STORE>); break;
+      case EPI_BIAS: go(gemm_ps4_kernel<EPI_BIAS>); break;
+      case EPI_BIAS_GELU: go(gemm_ps4_kernel<EPI_BIAS_GELU>); break;
+      default: go(gemm_ps4_kernel<EPI_NONE>); break;
+    }
+    return;
+  }
   switch (epi) {
     case EPI_STORE: go(gemm_ps_kernel<EPI_STORE>); break;
     case EPI_BIAS: go(gemm_ps_kernel<EPI_BIAS>); break;

@@ -28,10 +28,13 @@ void vcx_gemm_p(const void* A, const void* B, void* C, void* C2, const void* bia
 // gemm_ps.hip: persistent store-overlapped GEMM, C = A B^T (B [N, K]); epi 0 store, 1 +bias,
 // 2 +bias -> (C = pre, C2 = gelu(pre)); grid_cap <= 0: one workgroup per CU
 bool vcx_gemm_ps_supported(int M, int N, int K, int epi);
-int vcx_gemm_ps_grid(int M, int N, int grid_cap);
+bool vcx_gemm_ps2_supported(int M, int N, int K, int epi);
+int vcx_gemm_ps_grid(int M, int N, int grid_cap, int nw);
 // epi 4: C = (A B^T) * gelu'(C2) with fp32 column sums added into colsum
+// nw = 8: one 512-thread workgroup per CU (256 x 256 tiles); nw = 4: two 256-thread workgroups
+// per CU (256 x 128 tiles), the second half of the grid starting `stagger` x ~8k cycles late
 void vcx_gemm_ps(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N,
-                 int K, int lda, int ldb, int ldc, int epi, int grid_cap, hipStream_t s);
+                 int K, int lda, int ldb, int ldc, int epi, int grid_cap, int nw, int stagger, hipStream_t s);
 // gemm4.hip: 4-wave one-wave-per-SIMD GEMM (main-loop study), C = A B^T
 bool vcx_gemm4_supported(int M, int N, int K);
 void vcx_gemm4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, hipStream_t s);
