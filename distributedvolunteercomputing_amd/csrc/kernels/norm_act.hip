@@ -5,6 +5,8 @@
 // One wave64 owns one row; a 256-thread block covers 4 rows. The row is held in registers
 // (CH = ceil(C/512) chunks of 8 elements per lane), so the variance is an exact two-pass
 // computation over registers with a single HBM read of the row.
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "vcx_api.h"
@@ -93,6 +95,97 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16* __restrict__ a,
   if (lane == 0) {
     mean_out[row] = mean;
     rstd_out[row] = rstd;
+  }
+}
+
+// Row lengths that are a multiple of 256 (GPT-2: C = 768): every lane holds Q chunks of 4
+// elements (8-B accesses, all 64 lanes busy; the 8-element form leaves half the lanes idle in
+// the last chunk at C = 768), and each wave walks rows gw, gw + nw, ... with the next row's a/b
+// loads issued before this row's two cross-lane reductions (a one-row software pipeline, as in
+// the backward), so every lane keeps 2 x Q loads in flight through the shuffles.
+template <int Q>
+__global__ void __launch_bounds__(256) ln_fwd4_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
+                                                       bf16* __restrict__ xout, bf16* __restrict__ y,
+                                                       const bf16* __restrict__ w, const bf16* __restrict__ bias,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                       int R, int C, float eps, int rms, const bf16* __restrict__ bb) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * 4, gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  float wv[Q][4], bv_[Q][4], bbv[Q][4];
+#pragma unroll
+  for (int k = 0; k < Q; ++k) {
+    const int c = k * 256 + lane * 4;
+    const bf16x4 t = *(const bf16x4*)(w + c);
+    const bf16x4 u = bias ? *(const bf16x4*)(bias + c) : bf16x4{};
+    const bf16x4 v = bb ? *(const bf16x4*)(bb + c) : bf16x4{};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      wv[k][j] = (float)t[j];
+      bv_[k][j] = bias ? (float)u[j] : 0.f;
+      bbv[k][j] = bb ? (float)v[j] : 0.f;
+    }
+  }
+  const float invC = 1.f / (float)C;
+  bf16x4 av[Q], bvv[Q];
+  auto load_row = [&](int row, bf16x4(&aa)[Q], bf16x4(&bbx)[Q]) {
+    const int64_t off = (int64_t)row * C + lane * 4;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+      aa[k] = *(const bf16x4*)(a + off + k * 256);
+      if (b) bbx[k] = *(const bf16x4*)(b + off + k * 256);
+    }
+  };
+  if (gw < R) load_row(gw, av, bvv);
+  for (int row = gw; row < R; row += nw) {
+    bf16x4 nav[Q], nbv[Q];
+    const int nxt = row + nw;
+    if (nxt < R) load_row(nxt, nav, nbv);
+    const int64_t off = (int64_t)row * C + lane * 4;
+    float v[Q][4];
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+      if (b) {
+        bf16x4 sres;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sres[j] = (bf16)((float)av[k][j] + ((float)bvv[k][j] + bbv[k][j]));
+          v[k][j] = (float)sres[j];  // normalise the rounded residual actually stored
+        }
+        *(bf16x4*)(xout + off + k * 256) = sres;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[k][j] = (float)av[k][j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sum += v[k][j];
+    }
+    const float mean = rms ? 0.f : wave_sum(sum) * invC;
+    float var = 0.f;
+#pragma unroll
+    for (int k = 0; k < Q; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[k][j] - mean;
+        var = fmaf(d, d, var);
+      }
+    const float rstd = rsqrtf(wave_sum(var) * invC + eps);
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (bf16)fmaf((v[k][j] - mean) * rstd, wv[k][j], bv_[k][j]);
+      *(bf16x4*)(y + off + k * 256) = o;
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+      av[k] = nav[k];
+      if (b) bvv[k] = nbv[k];
+    }
   }
 }
 
@@ -731,6 +824,30 @@ using namespace vcx;
 
 void vcx_ln_fwd(const void* a, const void* b, void* xout, void* y, const void* w, const void* bias, float* mean,
                 float* rstd, int R, int C, float eps, int rms, const void* bb, hipStream_t s) {
+  // VCX_LN_FWD4=0 keeps the one-row-per-wave kernel below (A/B: profiles/r3_ln_fwd_ab.txt)
+  static const bool fwd4 = [] {
+    const char* e = getenv("VCX_LN_FWD4");
+    return !(e && atoi(e) == 0);
+  }();
+  if (fwd4 && C % 256 == 0 && C <= 1024) {
+    static const int resident = [] {  // 5 waves per SIMD (94 VGPRs at C = 768): 5 blocks of 4 waves per CU
+      int dev = 0, n = 256;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      return 5 * n;
+    }();
+    const int blocks = std::min((R + 3) / 4, resident);
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, (const bf16*)a, (const bf16*)b, (bf16*)xout, (bf16*)y,
+                         (const bf16*)w, (const bf16*)bias, mean, rstd, R, C, eps, rms, (const bf16*)bb);
+    };
+    switch (C / 256) {
+      case 1: go(ln_fwd4_kernel<1>); return;
+      case 2: go(ln_fwd4_kernel<2>); return;
+      case 3: go(ln_fwd4_kernel<3>); return;
+      default: go(ln_fwd4_kernel<4>); return;
+    }
+  }
   const int ch = (C / 8 + 63) / 64;
   dim3 grid((R + 3) / 4);
   VCX_LN_DISPATCH(ch, hipLaunchKernelGGL(ln_fwd_kernel<CH>, grid, dim3(256), 0, s, (const bf16*)a,

@@ -62,3 +62,27 @@ def test_gemm_ps_strided_rows_and_refusals(gpu):
     assert not C.gemm_ps_supported(500, 768, 768, 0)  # M % 256
     with pytest.raises(RuntimeError):
         C.gemm_ps(a[:, 4:260], b[:256, :256].contiguous(), torch.empty(512, 256, device=dev, dtype=torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 384, 768), (4096, 2304, 768), (8192, 768, 3072)])
+def test_gemm_ps_two_workgroups_per_cu(gpu, M, N, K):
+    """The opt-in 4-wave geometry (256 x 128 tiles, two co-resident workgroups per CU, staggered)."""
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    torch.manual_seed(K)
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16) * 0.1
+    ref = a.float() @ b.float().t() + bias.float()
+    for stagger in (0, 2):
+        c = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        act = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        C.gemm_ps(a, b, c, act, bias, None, 2, 0, 4, stagger)
+        torch.cuda.synchronize()
+        assert (c.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+        g = F.gelu(ref, approximate="tanh")
+        assert (act.float() - g).abs().max().item() < 3e-2 * g.abs().max().item()
+    assert not C.gemm_ps_supported(512, 256, 200, 0)
+    with pytest.raises(RuntimeError):  # no DGELU epilogue in the 4-wave geometry
+        C.gemm_ps(a, b, c, act, None, torch.zeros(N, device="cuda"), 4, 0, 4, 0)
