@@ -86,3 +86,27 @@ def test_gemm_ps_two_workgroups_per_cu(gpu, M, N, K):
     assert not C.gemm_ps_supported(512, 256, 200, 0)
     with pytest.raises(RuntimeError):  # no DGELU epilogue in the 4-wave geometry
         C.gemm_ps(a, b, c, act, None, torch.zeros(N, device="cuda"), 4, 0, 4, 0)
+
+
+def test_gemm_ps_repeat_runs_bit_identical(gpu):
+    """The fused-MLP launches are deterministic (no atomics in the outputs): repeats must reproduce
+    the first run bit for bit — a slot read before its DMA landed would show as differing tiles
+    (scripts/gemm_ps_stress.py runs the full-size version)."""
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    torch.manual_seed(3)
+    M, N, K = 16384, 3072, 768
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.03
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16) * 0.1
+    pre, act = torch.empty(M, N, device="cuda", dtype=torch.bfloat16), torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    C.gemm_ps(x, w, pre, act, b, None, 2)
+    g_pre, g_act = pre.clone(), act.clone()
+    d, cs = torch.empty_like(pre), torch.zeros(N, device="cuda")
+    C.gemm_ps(x, w, d, g_pre, None, cs, 4)
+    g_d = d.clone()
+    for _ in range(20):
+        C.gemm_ps(x, w, pre, act, b, None, 2)
+        C.gemm_ps(x, w, d, g_pre, None, cs, 4)
+        assert torch.equal(pre, g_pre) and torch.equal(act, g_act) and torch.equal(d, g_d)
