@@ -170,6 +170,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--workers", type=int, default=2)
+    ap.add_argument("--job-repeats", type=int, default=3, help="job runs per plane (median reported)")
     ap.add_argument("--no-job", action="store_true")
     ap.add_argument("--data-plane", default="both", choices=["relay", "p2p", "both"])
     ap.add_argument("--y4m-frames", type=int, default=0, help="also run the job on a Y4M file of this many frames")
@@ -185,8 +186,22 @@ def main():
         src = make_npy_source(a) if a.source == "npy" else None
         rec["job_source"] = "npy memory-mapped (/dev/shm), pre-generated" if src else "synthetic, generated per frame"
         try:
-            for plane in (("relay", "p2p") if a.data_plane == "both" else (a.data_plane,)):
-                rec.update(bench_job(a, dev, plane, source=src))
+            # each plane's job runs --job-repeats times, interleaved (run-to-run spread of a
+            # sub-second job on a shared host is +-15 %): the median is reported, every run listed
+            planes = ("relay", "p2p") if a.data_plane == "both" else (a.data_plane,)
+            runs = {pl: [] for pl in planes}
+            for _ in range(max(1, a.job_repeats)):
+                for plane in planes:
+                    runs[plane].append(bench_job(a, dev, plane, source=src))
+            for plane, rs in runs.items():
+                pre = "job" if plane == "relay" else f"job_{plane}"
+                ok = [r for r in rs if r.get(f"{pre}_frames_per_s")]
+                if not ok:
+                    rec.update(rs[-1])
+                    continue
+                ok.sort(key=lambda r: r[f"{pre}_frames_per_s"])
+                rec.update(ok[len(ok) // 2])
+                rec[f"{pre}_frames_per_s_runs"] = [r.get(f"{pre}_frames_per_s") for r in rs]
         finally:
             if src:
                 os.unlink(src)
