@@ -9,6 +9,7 @@
 // A whole 100-frame chunk is one batch, which turns the per-frame GEMVs of the reference into
 // real GEMMs (M = 100*19*19 = 36100 rows for conv11).
 #include <algorithm>
+#include <cstdlib>
 
 #include "vcx_common.h"
 
@@ -856,6 +857,132 @@ __global__ void __launch_bounds__(256) dwpw_tile_kernel(const bf16* __restrict__
   }
 }
 
+// Persistent form of dwpw_tile_kernel: a workgroup walks tiles blockIdx.x, + gridDim.x, ... with
+// the pointwise weights loaded into LDS ONCE (32 KB per tile launch at conv3: 300 MB of L2 reads
+// over a chunk in the one-tile form) and the NEXT tile's halo loaded into registers while this
+// tile's depthwise output goes through the MFMA GEMM and the stores, so the halo latency overlaps
+// compute inside a workgroup, not only across the 2 co-resident workgroups of the conv2/conv3 forms.
+template <int K, int N, int S, int TH, int TW>
+__global__ void __launch_bounds__(256) dwpw_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dwp,
+                                                            const float* __restrict__ dwb, int dw_relu,
+                                                            const bf16* __restrict__ Wt, const float* __restrict__ pb,
+                                                            int relu, bf16* __restrict__ y, int H, int W, int Ho, int Wo,
+                                                            int imgs) {
+  constexpr int HH = (TH - 1) * S + 3, HW = (TW - 1) * S + 3;
+  constexpr int K8 = K / 8, MT = TH * TW, KS = K / 32;
+  constexpr int HALO_B = HH * HW * K * 2, A_B = MT * K * 2, W_B = N * K * 2, OUT_B = MT * N * 2;
+  constexpr int R0 = HALO_B > OUT_B ? HALO_B : OUT_B;
+  constexpr int NE = HH * HW * K8, NH = (NE + 255) / 256;  // halo 16-B pieces, per thread
+  static_assert(256 % K8 == 0 && K % 32 == 0 && N % 64 == 0 && MT % 16 == 0, "tile shape");
+  __shared__ __attribute__((aligned(16))) char smem[R0 + A_B + W_B];
+  char* const halo = smem;
+  bf16* const sA = (bf16*)(smem + R0);
+  bf16* const sW = (bf16*)(smem + R0 + A_B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntx = (Wo + TW - 1) / TW, nty = (Ho + TH - 1) / TH, per = ntx * nty, ntiles = per * imgs;
+  for (int e = tid; e < N * K8; e += 256) {
+    const int row = e / K8, c = e % K8;
+    *(u32x4*)(sW + (c >> 2) * N * 32 + gidx(row, c & 3)) = *(const u32x4*)(Wt + (int64_t)row * K + c * 8);
+  }
+  const int c8 = tid % K8;
+  uint32_t wr[5][8];
+  load_dw_weights(dwp + c8 * 8, K, wr);
+  const f32x4 db0 = *(const f32x4*)(dwb + c8 * 8), db1 = *(const f32x4*)(dwb + c8 * 8 + 4);
+  u32x4 hr[NH];
+  auto gload = [&](int t) {
+    const int n = t / per, r = t - n * per;
+    const int iy0 = (r / ntx) * TH * S - 1, ix0 = (r % ntx) * TW * S - 1;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + (int64_t)n * H * W * K), (short)0, H * W * K * 2,
+                                                      0x00020000);
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+      const int e = tid + i * 256;
+      if (e < NE) {
+        const int c = e % K8, px = e / K8, hx = px % HW, hy = px / HW;
+        const int iy = iy0 + hy, ix = ix0 + hx;
+        const int off = (ix >= 0 && ix < W) ? ((iy * W + ix) * K + c * 8) * 2 : (int)0x80000000;
+        hr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      }
+    }
+  };
+  if ((int)blockIdx.x < ntiles) gload(blockIdx.x);
+  constexpr int NB = N / 64, MB = MT / 16, CH = N / 8;
+  const int fr = lane & 15, fc = lane >> 4;
+  bf16* const sO = (bf16*)halo;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int n = t / per, r = t - n * per, oy0 = (r / ntx) * TH, ox0 = (r % ntx) * TW;
+    // 1. this tile's halo (registers) -> LDS (the previous tile's output staging there was drained
+    //    before the barrier that ended the previous iteration)
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+      const int e = tid + i * 256;
+      if (e < NE) *(u32x4*)(halo + e * 16) = hr[i];
+    }
+    __syncthreads();
+    // 2. depthwise from LDS -> A tile
+    for (int p = tid / K8; p < MT; p += 256 / K8) {
+      const int ty = p / TW, tx = p % TW;
+      u32x4 t9[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        const int hy = ty * S + q / 3, hx = tx * S + q % 3;
+        t9[q] = *(const u32x4*)(halo + ((hy * HW + hx) * K + c8 * 8) * 2);
+      }
+      float a[8] = {db0[0], db0[1], db0[2], db0[3], db1[0], db1[1], db1[2], db1[3]};
+      dw9_accum_w(t9, wr, a);
+      *(u32x4*)(sA + (c8 >> 2) * MT * 32 + gidx(p, c8 & 3)) = dw_out8(a, dw_relu);
+    }
+    __syncthreads();
+    // 3. the next tile's halo loads go out now and land during the GEMM and the stores
+    if (t + (int)gridDim.x < ntiles) gload(t + gridDim.x);
+    // 4. pointwise GEMM (wave w: columns [w N/4, (w+1) N/4)), output staged in the halo region
+    f32x4 acc[MB][NB];
+#pragma unroll
+    for (int i = 0; i < MB; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8s bw[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) bw[j] = *(const bf16x8s*)(sW + ks * N * 32 + gidx(wid * (N / 4) + j * 16 + fr, fc));
+#pragma unroll
+      for (int i = 0; i < MB; ++i) {
+        const bf16x8s af = *(const bf16x8s*)(sA + ks * MT * 32 + gidx(i * 16 + fr, fc));
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af, acc[i][j], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int col = wid * (N / 4) + j * 16 + 4 * fc;
+      float bv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[q] = pb[col + q];
+#pragma unroll
+      for (int i = 0; i < MB; ++i) {
+        const int px = i * 16 + fr;
+        bf16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = acc[i][j][q] + bv[q];
+          o[q] = (bf16)(relu ? fmaxf(v, 0.f) : v);
+        }
+        *(bf16x4*)(sO + px * N + (((col >> 3) ^ (px & (CH - 1))) << 3) + (col & 4)) = o;
+      }
+    }
+    __syncthreads();
+    // 5. coalesced NHWC row segments
+    for (int e = tid; e < MT * CH; e += 256) {
+      const int px = e / CH, ch = e % CH, oy = oy0 + px / TW, ox = ox0 + px % TW;
+      if (oy >= Ho || ox >= Wo) continue;
+      *(u32x4*)(y + (((int64_t)n * Ho + oy) * Wo + ox) * N + ch * 8) =
+          *(const u32x4*)(sO + px * N + ((ch ^ (px & (CH - 1))) << 3));
+    }
+    __syncthreads();
+  }
+}
+
 // =====================================================================================
 // K4: the stem, conv0 3x3 (stride 2, pad 1) over the 4-channel padded blob, as MFMA fed straight
 // from global memory: with K = 9 taps x 4 channels the v_mfma_f32_16x16x32_bf16 operand a lane
@@ -1337,6 +1464,16 @@ void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y
   launch_gba<AM_IMPLICIT>((const bf16*)x, (const bf16*)Wt, bias, (bf16*)Y, M, N, Kp, N, relu, om, cg, ws, S, cnt, s);
 }
 
+static int vision_cus() {
+  static int n = [] {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    return c;
+  }();
+  return n;
+}
+
 // depthwise 3x3 (pad 1) + bias (+ReLU) -> pointwise GEMM + bias (+ReLU), one kernel:
 // x NHWC [imgs, H, W, K], dw_w [5][K] paired, dw_b [K], Wt [N, K] -> Y [imgs*Ho*Wo, N]
 void vcx_dw_pw(const void* x, const void* dw_w, const float* dw_b, int dw_relu, const void* Wt, const float* bias,
@@ -1347,6 +1484,23 @@ void vcx_dw_pw(const void* x, const void* dw_w, const float* dw_b, int dw_relu, 
     hipLaunchKernelGGL(kern, dim3((Wo + tw - 1) / tw, (Ho + th - 1) / th, imgs), dim3(256), 0, s, (const bf16*)x,
                        (const uint32_t*)dw_w, dw_b, dw_relu, (const bf16*)Wt, bias, relu, (bf16*)Y, H, W, Ho, Wo);
   };
+  // persistent form (dwpw_persist_kernel): grid = min(tiles, blocks-per-CU x CUs); VCX_DWPW_PERSIST=0
+  // selects the one-tile-per-workgroup form
+  static const bool persist = [] {
+    const char* e = std::getenv("VCX_DWPW_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  auto ptile = [&](auto kern, int th, int tw, int per_cu) {
+    const int64_t tiles = (int64_t)((Wo + tw - 1) / tw) * ((Ho + th - 1) / th) * imgs;
+    const int grid = (int)std::min<int64_t>(tiles, (int64_t)per_cu * vision_cus());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const bf16*)x, (const uint32_t*)dw_w, dw_b, dw_relu,
+                       (const bf16*)Wt, bias, relu, (bf16*)Y, H, W, Ho, Wo, imgs);
+  };
+  if (persist && (int64_t)H * W * K * 2 < INT32_MAX && (int64_t)imgs * H * W < INT32_MAX) {
+    if (K == 32 && N == 64 && stride == 1) return ptile(dwpw_persist_kernel<32, 64, 1, 8, 16>, 8, 16, 3);
+    if (K == 64 && N == 128 && stride == 2) return ptile(dwpw_persist_kernel<64, 128, 2, 4, 16>, 4, 16, 2);
+    if (K == 128 && N == 128 && stride == 1) return ptile(dwpw_persist_kernel<128, 128, 1, 4, 16>, 4, 16, 2);
+  }
   if ((int64_t)H * W * K * 2 < INT32_MAX && imgs <= 65535 && (Ho + 3) / 4 <= 65535) {
     if (K == 32 && N == 64 && stride == 1) return tile(dwpw_tile_kernel<32, 64, 1, 8, 16>, 8, 16);
     if (K == 64 && N == 128 && stride == 2) return tile(dwpw_tile_kernel<64, 128, 2, 4, 16>, 4, 16);

@@ -305,7 +305,7 @@ class SSDExecutor:
         """Depthwise -> pointwise pairs (every MobileNet block, prototxt 42-106 and after) become one
         `dwpw` step when the depthwise output feeds only that pointwise conv and the block shape
         has a 2-D-tile fused kernel (ops.vision.DWPW_TILE: conv1..conv3, the 150^2 / 75^2 blocks
-        where the depthwise round trip through HBM costs most). VCX_DWPW=off keeps every block two
+        where the depthwise round trip through HBM costs most; tile1 = conv1 only). VCX_DWPW=off keeps every block two
         kernels; VCX_DWPW=all also fuses the others through the GEMM's A-staging path (slower)."""
         mode = os.environ.get("VCX_DWPW", "tile")
         if mode == "off":
@@ -322,7 +322,8 @@ class SSDExecutor:
             if kind == "dw" and i + 1 < len(plan):
                 k2, l2, p2 = plan[i + 1]
                 K, Co = p["w"].shape[1], (p2["w"].shape[0] if k2 == "pw" else 0)
-                tiles = V.DWPW_TILE_ALL if mode in ("tile3", "all") else V.DWPW_TILE
+                tiles = (V.DWPW_TILE_ALL if mode in ("tile3", "all") else {(32, 64, 1)} if mode == "tile1"
+                         else V.DWPW_TILE)
                 shape_ok = (K, Co, p["stride"]) in tiles or (mode == "all" and K <= 1024 and K % 32 == 0)
                 if k2 == "pw" and l2.bottoms[0] == l.tops[0] and uses.get(l.tops[0], 0) == 1 and shape_ok:
                     out.append(("dwpw", l2, dict(dw=p, pw=p2, src=l.bottoms[0])))

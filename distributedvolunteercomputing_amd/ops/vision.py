@@ -7,8 +7,10 @@ implementations with the same arithmetic (used by CPU volunteers and as test ora
 from __future__ import annotations
 
 import functools
+import os
 
 import numpy as np
+
 import torch
 import torch.nn.functional as F
 
@@ -131,12 +133,15 @@ def dwconv3x3(x, w, b, stride, relu=True):
 
 
 # (K, N, stride) of the MobileNet blocks whose 2-D-tile fused depthwise->pointwise kernel
-# (csrc/kernels/vision.hip dwpw_tile_kernel) beats the two kernels: conv1 145 us vs 79 + 94. The
-# kernel also has conv2 (64, 128, 2) and conv3 (128, 128, 1) instances, which lose at 2 blocks
-# per CU (199 / 179 us vs 136 / 145: the halo-load -> depthwise -> GEMM -> store phases of one
-# tile do not overlap); VCX_DWPW=tile3 fuses all three
-DWPW_TILE = {(32, 64, 1)}
+# (csrc/kernels/vision.hip) beats the two kernels. The persistent form (dwpw_persist_kernel: weights
+# in LDS once per workgroup, next tile's halo loaded during this tile's GEMM and stores; default)
+# wins for conv1..conv3: 325 us for the three vs 405 as conv1 fused + two kernels each for conv2 and
+# conv3, detector chunk 1.22 vs 1.33 ms (profiles/r3_dwpw_persist_ab.txt). The one-tile form
+# (VCX_DWPW_PERSIST=0) only wins for conv1 (its conv2/conv3 instances run 199 / 179 us vs 136 / 145
+# unfused: one tile's load -> depthwise -> GEMM -> store phases do not overlap), so that setting
+# fuses conv1 alone; VCX_DWPW=tile1 / tile3 choose explicitly.
 DWPW_TILE_ALL = {(32, 64, 1), (64, 128, 2), (128, 128, 1)}
+DWPW_TILE = DWPW_TILE_ALL if os.environ.get("VCX_DWPW_PERSIST", "1") != "0" else {(32, 64, 1)}
 
 
 def dw_pw(x, wp, db, dw_relu, stride, Wt, bias, relu=True):

@@ -54,7 +54,9 @@ def test_dw_pair_weights_roundtrip():
 
 @pytest.mark.parametrize("N,H,K,stride,cout", [(3, 150, 32, 1, 64), (2, 150, 64, 2, 128), (3, 75, 128, 1, 128),
                                                 (2, 75, 128, 2, 256), (2, 38, 256, 1, 256), (3, 19, 512, 1, 512),
-                                                (2, 10, 1024, 1, 1024), (1, 7, 96, 2, 72)])
+                                                (2, 10, 1024, 1, 1024), (1, 7, 96, 2, 72),
+                                                # enough tiles that every persistent workgroup walks several
+                                                (12, 150, 32, 1, 64), (12, 150, 64, 2, 128), (12, 75, 128, 1, 128)])
 def test_dw_pw_fused_vs_fp32(gpu, N, H, K, stride, cout):
     """One kernel for depthwise 3x3 + bias + ReLU -> pointwise GEMM + bias + ReLU, against the
     fp32 PyTorch convolutions of the same bf16 operands (the fused path rounds the depthwise
