@@ -212,6 +212,53 @@ __global__ void __launch_bounds__(320) blob_bilinear_kernel(const uint8_t* __res
   }
 }
 
+// RB output rows per workgroup: the source rows they need (consecutive in memory: one linear
+// LDS-DMA copy of at most (RB - 1) * sy + 3 rows) are loaded once and shared, instead of two source
+// rows per one-row workgroup (each source row was fetched ~2.7 times at 225 -> 300, and a 2.4 KB
+// row of output per workgroup left too few bytes in flight: 2.2 TB/s).
+template <int RB>
+__global__ void __launch_bounds__(320) blob_bilinear_rows_kernel(const uint8_t* __restrict__ src,
+                                                                  bf16* __restrict__ dst, int N, int H, int W, int S,
+                                                                  float sx, float sy, float scale, float mean) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t brows[];
+  const int tid = threadIdx.x;
+  const int n = blockIdx.z, yb = blockIdx.y * RB, ye = min(yb + RB, S);
+  const int rb = W * 3;
+  auto row0 = [&](int y) { return min((int)fmaxf((y + 0.5f) * sy - 0.5f, 0.f), H - 1); };
+  const int ry0 = row0(yb), ry1 = min(row0(ye - 1) + 1, H - 1);
+  const int chunks = (ry1 - ry0 + 1) * rb / 16;
+  const uint8_t* g = src + ((int64_t)n * H + ry0) * rb;
+  for (int e0 = (tid & ~63); e0 < chunks; e0 += blockDim.x) {
+    const int e = min(e0 + (tid & 63), chunks - 1);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + (int64_t)e * 16),
+                                     (__attribute__((address_space(3))) void*)(brows + e0 * 16), 16, 0, 0);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+  __syncthreads();
+  for (int y = yb; y < ye; ++y) {
+    const float fy = fmaxf((y + 0.5f) * sy - 0.5f, 0.f);
+    const int y0 = min((int)fy, H - 1), y1 = min(y0 + 1, H - 1);
+    const float ay = fy - y0;
+    const uint8_t* r0 = brows + (y0 - ry0) * rb;
+    const uint8_t* r1 = brows + (y1 - ry0) * rb;
+    for (int x = tid; x < S; x += blockDim.x) {
+      const float fx = fmaxf((x + 0.5f) * sx - 0.5f, 0.f);
+      const int x0 = min((int)fx, W - 1), x1 = min(x0 + 1, W - 1);
+      const float ax = fx - x0;
+      bf16x4 o;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float v00 = r0[x0 * 3 + c], v01 = r0[x1 * 3 + c], v10 = r1[x0 * 3 + c], v11 = r1[x1 * 3 + c];
+        float v = (v00 * (1 - ax) + v01 * ax) * (1 - ay) + (v10 * (1 - ax) + v11 * ax) * ay;
+        v = rintf(fminf(255.f, fmaxf(0.f, v)));
+        o[c] = (bf16)((v - mean) * scale);
+      }
+      o[3] = (bf16)0.f;
+      *(bf16x4*)(dst + (((int64_t)n * S + y) * S + x) * 4) = o;
+    }
+  }
+}
+
 // the same for widths whose rows are not 16-B multiples (global byte taps)
 __global__ void __launch_bounds__(256) blob_bilinear_any_kernel(const uint8_t* __restrict__ src,
                                                                  bf16* __restrict__ dst, int N, int H, int W, int S,
@@ -1367,6 +1414,18 @@ void vcx_resize_bilinear_u8(const uint8_t* src, uint8_t* dst, int N, int H, int 
 void vcx_blob_bilinear(const uint8_t* src, void* dst, int N, int H, int W, int S, float scale, float mean,
                        hipStream_t s) {
   const float sx = (float)W / S, sy = (float)H / S;
+  constexpr int RB = 8;
+  const int64_t rows_lds = ((int64_t)((RB - 1) * sy) + 3) * W * 3 + 1024;  // + the DMA tail's overrun
+  static const bool rows_form = [] {
+    const char* e = std::getenv("VCX_BLOB_ROWS");
+    return !(e && e[0] == '0');
+  }();
+  if (rows_form && (W * 3) % 16 == 0 && rows_lds <= 48 * 1024 && ((uintptr_t)src & 15) == 0) {
+    const int bt = std::min(320, (S + 63) / 64 * 64);
+    hipLaunchKernelGGL(blob_bilinear_rows_kernel<RB>, dim3(1, (S + RB - 1) / RB, N), dim3(bt), (size_t)rows_lds, s, src,
+                       (bf16*)dst, N, H, W, S, sx, sy, scale, mean);
+    return;
+  }
   if ((W * 3) % 16 == 0 && W * 3 <= BLOB_LDS && ((uintptr_t)src & 15) == 0) {
     const int bt = std::min(320, (S + 63) / 64 * 64);
     hipLaunchKernelGGL(blob_bilinear_kernel, dim3(1, S, N), dim3(bt), 0, s, src, (bf16*)dst, N, H, W, S, sx, sy, scale,

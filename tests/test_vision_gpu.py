@@ -107,6 +107,22 @@ def test_preprocess(gpu):
     assert (b.cpu().float() - rb.float()).abs().max() <= 0.0079 + 1e-3
 
 
+@pytest.mark.parametrize("shape", [(2, 480, 640), (1, 225, 400), (2, 1200, 1600)])
+def test_blob_rows_kernel_vs_reference(gpu, shape):
+    """The multi-row blob kernel (8 output rows per workgroup sharing their source rows) for up- and
+    down-scaling to 300 x 300, against the reference bilinear + blobFromImage."""
+    torch.manual_seed(4)
+    f = torch.randint(0, 256, (*shape, 3), dtype=torch.uint8, device=gpu)
+    b = V.blob_from_frames(f, 300)
+    with reference_ops():
+        rb = V.blob_from_frames(f.cpu(), 300)
+    assert b.shape == rb.shape
+    d = (b.cpu().float() - rb.float()).abs()
+    # at most one uint8 level (1/127.5) apart from the reference's rounding of the interpolated
+    # value, plus bf16 rounding of the scaled result
+    assert d.max() <= 2 * 0.0079 + 1e-3 and float((d > 0.0079 + 1e-3).float().mean()) < 1e-3
+
+
 @pytest.mark.parametrize("shape,width", [((2, 333, 517), 200), ((1, 1080, 1920), 400), ((3, 97, 601), 600),
                                          ((2, 40, 64), 13)])
 def test_resize_area_odd_shapes(gpu, shape, width):
