@@ -172,7 +172,7 @@ def peer_main(a):
         sync()
         timeline.append({"step": i, "ms": (time.perf_counter() - t0) * 1e3, "synced": bool(st.synced),
                          "members": st.members, "gen": mem.gen, "sync_ms": st.sync_ms if st.synced else 0.0,
-                         "t_end": time.time()})
+                         "t_end": time.time(), "t_sync_end": tr.t_sync_end if st.synced else None})
         i += 1
     store.set("vcx/drop/done", "1")
     with open(os.path.join(a.out, f"peer{a.peer}.json"), "w") as f:
@@ -285,6 +285,7 @@ def launcher(a):
     backend = None
     failed_rounds = 0
     detect, build, redo = [], [], []
+    stages = {}  # regroup-round anatomy, max over survivors (where a slow one goes)
     for r in survivors:
         with open(os.path.join(out, f"peer{r}.json")) as f:
             d = json.load(f)
@@ -310,6 +311,31 @@ def launcher(a):
                     ends = [e["t_end"] for e in d["timeline"] if e["gen"] >= rg[0]["gen"] and e["synced"]]
                     if ends:
                         redo.append((min(ends) - cn[0]["t"]) * 1e3)
+                # the averaging call that absorbed the failure, stage by stage
+                st_ = next((e for e in d["timeline"] if e["gen"] >= rg[0]["gen"] and e["synced"]), None) if rg else None
+                if st_ is not None and st_.get("t_sync_end") and rg[0].get("t_in"):
+                    t1 = st_["t_sync_end"]
+                    t0 = t1 - st_["sync_ms"] / 1e3
+                    ab = [e["t"] for e in d["events"] if e["event"] == "abort" and t0 <= e["t"] <= t1]
+                    cn = [e for e in d["events"] if e["event"] == "connect" and e["gen"] == rg[0]["gen"]]
+                    parts = {
+                        # sync start -> first sign of trouble inside it (aborted collective), if any
+                        "before_abort_ms": (min(ab) - t0) * 1e3 if ab else 0.0,
+                        # (abort ->) entry into the round that formed the new generation
+                        "to_round_ms": (rg[0]["t_in"] - (min(ab) if ab else t0)) * 1e3,
+                        "bell_wait_ms": rg[0].get("bell_wait_ms") or 0.0,
+                        "scan_ms": rg[0].get("scan_ms") or 0.0,
+                        "decide_ms": rg[0].get("decide_ms") or 0.0,
+                        "group_object_ms": rg[0].get("adopt_ms") or 0.0,
+                        "comm_build_ms": cn[0]["ms"] if cn else 0.0,
+                        "collective_after_build_ms": (t1 - cn[0]["t"]) * 1e3 if cn else 0.0,
+                    }
+                    acc = parts["before_abort_ms"] + parts["to_round_ms"] + parts["decide_ms"] + \
+                        parts["group_object_ms"] + parts["comm_build_ms"] + parts["collective_after_build_ms"]
+                    parts["unaccounted_ms"] = st_["sync_ms"] - acc
+                    parts["sync_ms"] = st_["sync_ms"]
+                    for k_, v_ in parts.items():
+                        stages[k_] = max(stages.get(k_, v_), v_)
         for e in d["timeline"]:
             cur = tl.setdefault(e["step"], dict(e))
             cur["ms"] = max(cur["ms"], e["ms"])  # a step ends when its slowest survivor is done
@@ -352,6 +378,7 @@ def launcher(a):
         "detect_ms": round(max(detect), 3) if detect else None,
         "comm_build_ms": round(max(build), 3) if build else None,
         "redo_ms": round(max(redo), 3) if redo else None,
+        "regroup_stages_ms": {k: round(v, 3) for k, v in stages.items()} or None,
         "liveness": os.environ.get("VCX_ELASTIC_LIVENESS", "1") not in ("0", "false", "no", "off"),
         "samples_per_s_before": round(a.peers * a.batch / mean(before) * 1e3, 2),
         "samples_per_s_after": round(len(survivors) * a.batch / mean(after) * 1e3, 2) if after else None,

@@ -90,7 +90,12 @@ class coordinator:  # noqa: N801  (reference class name)
         # else. A host that can reach the port but never joined cannot name, so cannot forge, the
         # abort / join / pair-hello records the peers act on (the reference binds every interface
         # with no auth at all: /root/reference/server.py:96).
+        # Two prefixes: `store_secret` (the training membership keys) and `p2p_secret` (the chunk
+        # plane's pair-group rendezvous). A joined volunteer only ever learns the p2p one; with a
+        # `train_token` the training prefix goes out only through an admitted `tjoin`, so joining
+        # as a volunteer (unauthenticated, any host) gives no way to read or forge training keys.
         self.store_secret = secrets.token_hex(16)
+        self.p2p_secret = secrets.token_hex(16)
         self.train_token = train_token
         self.train_peers: set[str] = set()
         self.train_store = None
@@ -171,7 +176,10 @@ class coordinator:  # noqa: N801  (reference class name)
             return self._tjoin(addr, src)
         if verb in ("request", "stop", "end", "hb", "p2p", "store"):
             with self._lock:
-                known = addr in self.vols or (verb == "store" and addr in self.train_peers)
+                if verb == "store" and self.train_token is not None:
+                    known = addr in self.train_peers  # token-gated job: admitted training peers only
+                else:
+                    known = addr in self.vols or (verb == "store" and addr in self.train_peers)
             if not known or (src is not None and not protocol.addr_matches(addr, src[0])):
                 self.metrics.incr("unknown_datagrams")
                 return f"err{protocol.SEP}{addr} has not joined".encode()
@@ -205,7 +213,7 @@ class coordinator:  # noqa: N801  (reference class name)
                 v = self.vols.get(addr)
             info = {"plane": self.data_plane, "vid": v.vid if v is not None else None,
                     "store_port": self.train_store_port if self.data_plane == "p2p" else None,
-                    "store_prefix": self.store_secret if self.data_plane == "p2p" else None}
+                    "store_prefix": self.p2p_secret if self.data_plane == "p2p" else None}
             return protocol.reply_ok(json.dumps(info))
         return None
 
@@ -216,11 +224,12 @@ class coordinator:  # noqa: N801  (reference class name)
         return f"{self.train_store_port}{protocol.SEP}{self.store_secret}"
 
     def _join_reply(self, port) -> bytes:
-        # `ok||<port>` as in the reference; with a rendezvous store a third field carries the key
-        # prefix (the reference client reads only field 1: worker.py:61)
+        # `ok||<port>` as in the reference; with a rendezvous store a third field carries the p2p
+        # plane's key prefix (the reference client reads only field 1: worker.py:61). Never the
+        # training prefix: `join` is unauthenticated.
         if self.train_store is None:
             return protocol.reply_ok(str(port))
-        return protocol.reply_ok(f"{port}{protocol.SEP}{self.store_secret}")
+        return protocol.reply_ok(f"{port}{protocol.SEP}{self.p2p_secret}")
 
     def _tjoin(self, addr, src):
         """Admit a training peer `<id>[||<token>]`: reply `ok||<store port>||<key prefix>`."""

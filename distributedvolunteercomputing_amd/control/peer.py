@@ -45,6 +45,23 @@ from . import protocol
 from .transport import FrameHub, FrameSender
 
 _EMPTY = np.zeros(0, dtype=np.uint8)
+# first bytes of a placeholder result (a worker asked to send a result it no longer holds): the
+# pair FIFO needs a buffer of the announced shape, and the requester must tell it from a real one
+_PLACEHOLDER_TAG = torch.frombuffer(bytearray(b"VCX/p2p/placeholder-result/v1\0\0"), dtype=torch.uint8)
+
+
+def _placeholder(shape) -> torch.Tensor:
+    t = torch.zeros(tuple(shape or (0,)), dtype=torch.uint8)
+    flat = t.view(-1)
+    n = min(flat.numel(), _PLACEHOLDER_TAG.numel())
+    flat[:n] = _PLACEHOLDER_TAG[:n]
+    return t
+
+
+def _is_placeholder(buf) -> bool:
+    flat = buf.reshape(-1)
+    n = _PLACEHOLDER_TAG.numel()
+    return flat.numel() >= n and torch.equal(flat[:n].cpu(), _PLACEHOLDER_TAG)
 
 
 def _host_tensor(a: np.ndarray) -> torch.Tensor:
@@ -384,9 +401,10 @@ class client:  # noqa: N801 (reference class name)
                 t = self._results.pop(cid, None)
             if t is None:
                 # the requester has posted its receive: keep the pair's FIFO in step with a
-                # placeholder of the announced shape (that requester re-submits the chunk)
+                # tagged placeholder of the announced shape; the requester recognises the tag and
+                # re-submits the chunk (its frames are still held under the chunk's key)
                 self.metrics.incr("p2p_placeholder_results")
-                t = torch.zeros(tuple(hdr.get("cshape") or (0,)), dtype=torch.uint8)
+                t = _placeholder(hdr.get("cshape"))
             plane.send(int(hdr["dst"]), t, cid)
         elif cmd == "recv_result":  # requester: annotated chunk from worker `src`
             key, msg = hdr.get("key"), hdr["msg"]
@@ -396,6 +414,10 @@ class client:  # noqa: N801 (reference class name)
                     # the annotated chunk was lost on the way back (the worker is done with it):
                     # submit the frames again as a new chunk; they are still held under `key`
                     self.metrics.incr("p2p_recv_failed")
+                    self._resubmit(key, msg)
+                    return
+                if _is_placeholder(buf):  # the worker no longer held the result: not frames
+                    self.metrics.incr("p2p_placeholder_received")
                     self._resubmit(key, msg)
                     return
                 if key is not None:

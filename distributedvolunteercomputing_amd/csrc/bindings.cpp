@@ -198,8 +198,9 @@ void gemm_ps(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
   TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_ps: shape mismatch");
   TORCH_CHECK(waves == 8 ? vcx_gemm_ps_supported((int)M, (int)N, (int)K, (int)epi)
                          : vcx_gemm_ps2_supported((int)M, (int)N, (int)K, (int)epi),
-              "gemm_ps: needs M, N % 256 == 0, K % 128 == 0, K >= 256, epilogue 0..4, N <= 16384 with a bias "
-              "(4 waves: N % 128 == 0, K % 96 == 0, K >= 192, epilogue 0..3)");
+              "gemm_ps: needs M, N % 256 == 0, K % 128 == 0, K >= 256, epilogue 0 (store), 1 (bias), 2 (bias+GELU), "
+              "4 (DGELU + bias grad) or 7 (diagnostic, no stores), N <= 16384 with a bias "
+              "(4 waves: N % 128 == 0, K % 192 == 0, epilogue 0, 1, 2 or 7)");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm_ps: 16-B aligned rows");
   for (const at::Tensor* t : {&a, &b, &c})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_ps: 16-B aligned base pointers");
@@ -227,6 +228,26 @@ void gemm_ps(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
   }
   vcx_gemm_ps(a.data_ptr(), b.data_ptr(), c.data_ptr(), c2p, bp, cs, (int)M, (int)N, (int)K, (int)a.stride(0),
               (int)b.stride(0), (int)c.stride(0), (int)epi, (int)grid_cap, (int)waves, (int)stagger, cur_stream());
+}
+
+// gemm_ps diagnostics (scripts/gemm_ps_diag.py): store cache policy 0 plain / 1 nt / 2 sc1 / 3 sc0 sc1,
+// epi 0 (store) or 7 (no stores), optional per-tile s_memtime stamps int64 [grid, 64, 5]
+void gemm_ps_diag(at::Tensor a, at::Tensor b, at::Tensor c, int64_t epi, int64_t policy,
+                  c10::optional<at::Tensor> stamps, int64_t grid_cap, int64_t stagger) {
+  TORCH_CHECK(a.is_cuda() && a.is_contiguous() && b.is_contiguous() && c.is_contiguous(), "gemm_ps_diag: contiguous");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N && (epi == 0 || epi == 7) && policy >= 0 &&
+                  policy <= 3 && vcx_gemm_ps_supported((int)M, (int)N, (int)K, (int)epi),
+              "gemm_ps_diag: shape / epi / policy");
+  unsigned long long* sp = nullptr;
+  if (stamps) {
+    const int grid = vcx_gemm_ps_grid((int)M, (int)N, (int)grid_cap, 8);
+    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->is_contiguous() && stamps->numel() >= grid * 64 * 5,
+                "gemm_ps_diag: stamps int64 [grid, 64, 5]");
+    sp = reinterpret_cast<unsigned long long*>(stamps->data_ptr());
+  }
+  vcx_gemm_ps_diag(a.data_ptr(), b.data_ptr(), c.data_ptr(), (int)M, (int)N, (int)K, (int)K, (int)K, (int)N, (int)epi,
+                   (int)policy, sp, (int)grid_cap, (int)stagger, cur_stream());
 }
 
 // 4-wave one-wave-per-SIMD GEMM (gemm4.hip): c[M, N] = a[M, K] . b[N, K]^T
@@ -724,6 +745,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_p_supported", &gemm_p_supported);
   m.def("gemm4", &gemm4);
   m.def("gemm_ps_supported", &gemm_ps_supported);
+  m.def("gemm_ps_diag", &gemm_ps_diag, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("epi") = 0,
+        py::arg("policy") = 0, py::arg("stamps") = py::none(), py::arg("grid_cap") = 0, py::arg("stagger") = 0);
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0,
         py::arg("waves") = 8, py::arg("stagger") = 0);

@@ -42,7 +42,9 @@ constexpr int SLOT = 2 * SLOT_A;        // 32 KB
 constexpr int RING = 4 * SLOT;          // 128 KB
 constexpr int BIAS_MAX = 16384;         // bias row resident in LDS behind the ring (32 KB)
 
-enum Epi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_NONE = 3 /* diagnostic: no stores */, EPI_DGELU = 4 };
+// (3 is not used: gemm_nt's code 3 is DGELU, so a caller reusing its numbering is refused, not
+// silently given the diagnostic no-store epilogue)
+enum Epi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 4, EPI_NONE = 7 /* diagnostic: no stores */ };
 
 __device__ __forceinline__ int swz(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
 
@@ -73,10 +75,29 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // VGPRs of a builtin buffer_store_dwordx4 4 instructions after it (lanes 12-15 of each row stored
 // stale dword 1, measured), so the store's read of its data registers is padded by hand
 // (cdna_hip_programming.md §5.7 item 1, stores)
+// SPOL (diagnostic builds only): the store's cache policy -- 0 plain, 1 nt, 2 sc1 (write-through,
+// line dropped from L2), 3 sc0 sc1
+template <int SPOL = 0>
 __device__ __forceinline__ void store16(u32x4 v, u32x4 desc, int voff, int soff) {
-  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(desc), "s"(soff)
-               : "memory");
+  if constexpr (SPOL == 0)
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(desc), "s"(soff)
+                 : "memory");
+  else if constexpr (SPOL == 1)
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(desc), "s"(soff)
+                 : "memory");
+  else if constexpr (SPOL == 2)
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(desc), "s"(soff)
+                 : "memory");
+  else
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen sc0 sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(desc),
+                 "s"(soff)
+                 : "memory");
 }
+
+// Diagnostic stamps (STAMP builds): thread 0 of each workgroup records s_memtime per tile into LDS
+// behind the ring, copied out at the end: [0] tile start, [1] before step 3's wait, [2] after
+// step 3's wait + barrier, [3] epilogue start, [4] epilogue end (every store issued)
+constexpr int NSTAMP = 5, STAMP_TILES = 64;
 // raw buffer descriptor words: 48-bit base, stride 0, num_records bytes, the flags word used by
 // __builtin_amdgcn_make_buffer_rsrc elsewhere in the tree
 __device__ __forceinline__ u32x4 desc_of(const void* base, int bytes) {
@@ -103,11 +124,12 @@ struct Frags {
 
 // (the body is a device function shared by two kernel templates with literal launch bounds: a
 // kernel template on NW lost its host-side stubs)
-template <int EPI, int NW>
+template <int EPI, int NW, int SPOL = 0, bool STAMP = false>
 __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                              bf16* __restrict__ C, bf16* __restrict__ C2,
                                              const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
-                                             int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger) {
+                                             int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger,
+                                             unsigned long long* __restrict__ stamps = nullptr) {
   using Gm = Geo<NW>;
   constexpr int BNt = Gm::BNt, SLOTA = Gm::SLOTA, SLOTB = Gm::SLOTB, RINGB = Gm::RINGB, NSLOT = Gm::NSLOT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -116,6 +138,13 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
   const int wm = wid / Gm::WNC, wn = wid % Gm::WNC;
   const int G = gridDim.x, bid = blockIdx.x;
   const int nk = K / BKS;  // multiple of 4, >= 8 (host check)
+  int ti = 0;  // STAMP: this workgroup's tile index
+  auto stamp = [&](int k) {
+    if constexpr (STAMP) {
+      if (tid == 0 && ti < STAMP_TILES)
+        ((unsigned long long*)(smem + RINGB))[ti * NSTAMP + k] = __builtin_amdgcn_s_memtime();
+    }
+  };
 
   if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {  // the bias row, once per workgroup
     bf16* bl = (bf16*)(smem + RINGB);
@@ -248,11 +277,13 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
   auto step = [&](int s, Frags& fc, Frags& fn, const Rs& sa, const Rs& sb, int ks, bool nowait, auto LD,
                   auto VM, auto ST) {
     constexpr bool ld = decltype(LD)::value, st = decltype(ST)::value;
+    if (STAMP && s == 3) stamp(1);
     if (nowait)
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     else
       wait_vm<decltype(VM)::value>();
     barrier();
+    if (STAMP && s == 3) stamp(2);
     const int slot = s % NSLOT, nslot = (s + 1) % NSLOT;
     if constexpr (st) stage_group(sa, sb, ks, slot, P0{});
     __builtin_amdgcn_sched_barrier(0);
@@ -296,6 +327,7 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
                                                                                       i * 16 * ldc * 2, 0));
   };
   auto epilogue = [&](int m0, int n0, auto DRAIN) {
+    stamp(3);
     float cs[8];  // EPI_DGELU: fp32 column sums of this lane's 8 columns over its 16 rows
 #pragma unroll
     for (int e = 0; e < 8; ++e) cs[e] = 0.f;
@@ -371,8 +403,8 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
           v[q] = __builtin_bit_cast(u32x4, o8);
         }
       }
-      store16(v[0], rc, c_offA, soff);
-      store16(v[1], rc, c_offA + 8 * ldc * 2, soff);
+      store16<SPOL>(v[0], rc, c_offA, soff);
+      store16<SPOL>(v[1], rc, c_offA + 8 * ldc * 2, soff);
       if constexpr (EPI == EPI_BIAS_GELU) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -380,7 +412,7 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
           bf16x8 act;
 #pragma unroll
           for (int e = 0; e < 8; ++e) act[e] = (bf16)gelu_tanh((float)pre[e]);
-          store16(__builtin_bit_cast(u32x4, act), rc2, c_offA + q * 8 * ldc * 2, soff);
+          store16<SPOL>(__builtin_bit_cast(u32x4, act), rc2, c_offA + q * 8 * ldc * 2, soff);
         }
       }
     }
@@ -400,6 +432,7 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
         for (int e = 0; e < 8; ++e) atomicAdd(dst + e, cs[e]);
       }
     }
+    stamp(4);
   };
 
 
@@ -407,6 +440,10 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
   // two co-resident workgroups reach their tile boundaries at different times
   if (NW == 4 && stagger > 0 && bid >= G / 2)
     for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  // diagnostic (STAMP/SPOL builds): NW = 8 workgroups in 4 start phases inside every XCD, phase p
+  // sleeping p x stagger x ~8k cycles, so that tile boundaries -- and the output bursts -- spread
+  if (NW == 8 && stagger > 0)
+    for (int i = 0; i < ((bid >> 3) & 3) * stagger; ++i) __builtin_amdgcn_s_sleep(127);
 
   // ---- prologue: slices 0..NSLOT-1 of the first tile
   int vb = bid;
@@ -431,6 +468,7 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
   while (true) {
     int m0, n0;
     coords(vb, m0, n0);
+    stamp(0);
     const int vn = vb + G;
     const bool more = vn < tiles;
     Rs na, nb;  // the next tile's resources (the last tile re-stages its own first slices: never read)
@@ -467,10 +505,17 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
       }
       epilogue(m0, n0, Tt{});  // the fragments of the next tile's slice 0 are in (x, f0) already
     }
+    ++ti;
     if (!more) break;
     vb = vn;
     ra = na;
     rb = nb;
+  }
+  if constexpr (STAMP) {
+    if (tid == 0) {
+      const unsigned long long* src = (const unsigned long long*)(smem + RINGB);
+      for (int i = 0; i < min(ti, STAMP_TILES) * NSTAMP; ++i) stamps[(size_t)bid * STAMP_TILES * NSTAMP + i] = src[i];
+    }
   }
   // no final drain: the last epilogue's vmcnt(0) retired every LDS-DMA (the last tile re-stages
   // its own first slices as dummies), so only its stores are in flight, and those may outlive the
@@ -483,6 +528,16 @@ __global__ void __launch_bounds__(512, 1)
                    bf16* __restrict__ C2, const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
                    int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger) {
   gemm_ps_body<EPI, 8>(A, B, C, C2, bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger);
+}
+
+// diagnostic instances: store cache policy x stamps (scripts/gemm_ps_diag.py)
+template <int EPI, int SPOL, bool STAMP>
+__global__ void __launch_bounds__(512, 1)
+    gemm_ps_diag_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C, int M, int N,
+                        int K, int lda, int ldb, int ldc, int tilesN, int tiles, unsigned long long* stamps,
+                        int stagger) {
+  gemm_ps_body<EPI, 8, SPOL, STAMP>(A, B, C, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, tilesN, tiles,
+                                    stagger, stamps);
 }
 
 template <int EPI>
@@ -499,14 +554,20 @@ __global__ void __launch_bounds__(256, 2)
 using namespace vcx;
 
 bool vcx_gemm_ps_supported(int M, int N, int K, int epi) {
-  return M > 0 && N > 0 && M % gemm_ps::BM == 0 && N % gemm_ps::BN == 0 && K % 128 == 0 && K >= 256 && epi >= 0 &&
-         epi <= 4 && (epi == 0 || epi >= 3 || N <= gemm_ps::BIAS_MAX);
+  using namespace gemm_ps;
+  const bool known = epi == EPI_STORE || epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_DGELU || epi == EPI_NONE;
+  return M > 0 && N > 0 && M % BM == 0 && N % BN == 0 && K % 128 == 0 && K >= 256 && known &&
+         ((epi != EPI_BIAS && epi != EPI_BIAS_GELU) || N <= BIAS_MAX);
 }
 
-// the two-workgroups-per-CU geometry (NW = 4): N % 128, K % 96 (3-slot ring), no DGELU epilogue
+// the two-workgroups-per-CU geometry (NW = 4): N % 128, no DGELU epilogue. K % 192: the 3-slot ring
+// stages 3 slices ahead and the loop takes 2 steps per iteration, so nk = K / 32 must be a multiple
+// of both (an odd nk ran one step too many into the next tile's slot 0: wrong tiles)
 bool vcx_gemm_ps2_supported(int M, int N, int K, int epi) {
-  return M > 0 && N > 0 && M % gemm_ps::BM == 0 && N % 128 == 0 && K % 96 == 0 && K >= 192 && epi >= 0 && epi <= 3 &&
-         (epi == 0 || epi == 3 || N <= gemm_ps::BIAS_MAX);
+  using namespace gemm_ps;
+  const bool known = epi == EPI_STORE || epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_NONE;
+  return M > 0 && N > 0 && M % BM == 0 && N % 128 == 0 && K % 192 == 0 && K >= 192 && known &&
+         ((epi != EPI_BIAS && epi != EPI_BIAS_GELU) || N <= BIAS_MAX);
 }
 
 int vcx_gemm_ps_grid(int M, int N, int grid_cap, int nw) {
@@ -559,5 +620,34 @@ void vcx_gemm_ps(const void* A, const void* B, void* C, void* C2, const void* bi
     case EPI_BIAS_GELU: go(gemm_ps_kernel<EPI_BIAS_GELU>); break;
     case EPI_DGELU: go(gemm_ps_kernel<EPI_DGELU>); break;
     default: go(gemm_ps_kernel<EPI_NONE>); break;
+  }
+}
+
+// diagnostic launcher: epi 0 (store) or 7 (no stores), policy 0..3, stamps [grid, 64, 5] or null
+void vcx_gemm_ps_diag(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, int epi,
+                      int policy, unsigned long long* stamps, int grid_cap, int stagger, hipStream_t s) {
+  using namespace gemm_ps;
+  const int tilesN = N / 256, tiles = (M / BM) * tilesN;
+  const int grid = vcx_gemm_ps_grid(M, N, grid_cap, 8);
+  const int lds = Geo<8>::RINGB + NSTAMP * STAMP_TILES * 8;
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, (const bf16*)A, (const bf16*)B, (bf16*)C, M, N, K, lda,
+                       ldb, ldc, tilesN, tiles, stamps, stagger);
+  };
+  const bool st = stamps != nullptr;
+  if (epi == EPI_NONE) {
+    st ? go(gemm_ps_diag_kernel<EPI_NONE, 0, true>) : go(gemm_ps_diag_kernel<EPI_NONE, 0, false>);
+    return;
+  }
+  switch (policy * 2 + (st ? 1 : 0)) {
+    case 0: go(gemm_ps_diag_kernel<EPI_STORE, 0, false>); break;
+    case 1: go(gemm_ps_diag_kernel<EPI_STORE, 0, true>); break;
+    case 2: go(gemm_ps_diag_kernel<EPI_STORE, 1, false>); break;
+    case 3: go(gemm_ps_diag_kernel<EPI_STORE, 1, true>); break;
+    case 4: go(gemm_ps_diag_kernel<EPI_STORE, 2, false>); break;
+    case 5: go(gemm_ps_diag_kernel<EPI_STORE, 2, true>); break;
+    case 6: go(gemm_ps_diag_kernel<EPI_STORE, 3, false>); break;
+    default: go(gemm_ps_diag_kernel<EPI_STORE, 3, true>); break;
   }
 }

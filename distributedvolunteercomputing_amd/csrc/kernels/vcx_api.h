@@ -29,6 +29,8 @@ void vcx_gemm_p(const void* A, const void* B, void* C, void* C2, const void* bia
 // 2 +bias -> (C = pre, C2 = gelu(pre)); grid_cap <= 0: one workgroup per CU
 bool vcx_gemm_ps_supported(int M, int N, int K, int epi);
 bool vcx_gemm_ps2_supported(int M, int N, int K, int epi);
+void vcx_gemm_ps_diag(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, int epi,
+                      int policy, unsigned long long* stamps, int grid_cap, int stagger, hipStream_t s);
 int vcx_gemm_ps_grid(int M, int N, int grid_cap, int nw);
 // epi 4: C = (A B^T) * gelu'(C2) with fp32 column sums added into colsum
 // nw = 8: one 512-thread workgroup per CU (256 x 256 tiles); nw = 4: two 256-thread workgroups

@@ -145,9 +145,10 @@ def main(argv=None):
         store = dist.PrefixStore(prefix, store)
     membership = group = None
     if a.elastic:
-        from ..parallel.elastic import ElasticMembership
+        from ..parallel.elastic import ElasticMembership, _route_ip
 
-        membership = ElasticMembership(store, rank, backend=backend, device=device, lease_s=a.lease)
+        membership = ElasticMembership(store, rank, backend=backend, device=device, lease_s=a.lease,
+                                       live_host=_route_ip(a.store_host))
         if a.join:
             membership.join()
         else:

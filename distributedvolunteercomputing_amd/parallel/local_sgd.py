@@ -78,6 +78,7 @@ class LocalSGDTrainer:
         self.t = 0
         self.sync_count = 0
         self.last_sync_ms = 0.0
+        self.t_sync_end = None
         self.failed_rounds = 0  # elastic rounds aborted mid-collective and redone
 
     # ------------------------------------------------------------------ per step
@@ -156,6 +157,7 @@ class LocalSGDTrainer:
             self._sync_elastic()
         self.sync_count += 1
         self.last_sync_ms = (time.perf_counter() - t0) * 1e3
+        self.t_sync_end = time.time()
 
     def _sync_elastic(self):
         """One elastic averaging round: agreed outcome -> guarded admission + reduction ->

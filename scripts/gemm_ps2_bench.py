@@ -40,7 +40,7 @@ for name, n, k in [("qkv", 2304, 768), ("proj", 768, 768), ("fc", 3072, 768), ("
     c = torch.empty(M, n, device=dev, dtype=bf)
     fns = [lambda: F.linear(a, b), lambda: C.gemm_ps(a, b, c), lambda: C.gemm_ps(a, b, c, waves=4),
            lambda: C.gemm_ps(a, b, c, waves=4, stagger=1), lambda: C.gemm_ps(a, b, c, waves=4, stagger=3),
-           lambda: C.gemm_ps(a, b, c, epi=3, waves=4)]
+           lambda: C.gemm_ps(a, b, c, epi=7, waves=4)]
     t = timeit(fns)
     print(f"{name:7s} N={n:5d} K={k:5d}  library {t[0]:6.1f}  ps8 {t[1]:6.1f}  ps4 {t[2]:6.1f}  ps4 st1 {t[3]:6.1f}  "
           f"ps4 st3 {t[4]:6.1f}  ps4 no-store {t[5]:6.1f} us", flush=True)

@@ -96,7 +96,7 @@ def main():
         else:
             lib = lambda: F.linear(a, b)  # noqa: E731
         t_lib, t_ps, t_ps2, t_no = timeit([lib, lambda: C.gemm_ps(a, b, c), lambda: C.gemm_ps(a, b, c, grid_cap=512),
-                                           lambda: C.gemm_ps(a, b, c, epi=3)])
+                                           lambda: C.gemm_ps(a, b, c, epi=7)])
         tl, tn, tp = tl + t_lib, tn + min(t_ps, t_ps2), tp + t_no
         print(f"{name:7s} N={n:5d} K={k:5d}  library {t_lib:7.1f} us ({fl / t_lib / 1e6:5.0f} TF)  gemm_ps {t_ps:7.1f} "
               f"({fl / t_ps / 1e6:5.0f})  grid512 {t_ps2:7.1f} ({fl / t_ps2 / 1e6:5.0f})  no-store {t_no:7.1f} "
@@ -130,7 +130,7 @@ def main():
         c = torch.empty(n, n, device=dev, dtype=bf)
         fl = 2.0 * n ** 3
         t_lib, t_ps, t_no = timeit([lambda: F.linear(a, b), lambda: C.gemm_ps(a, b, c),
-                                    lambda: C.gemm_ps(a, b, c, epi=3)])
+                                    lambda: C.gemm_ps(a, b, c, epi=7)])
         print(f"{n}^3  library {fl / t_lib / 1e6:5.0f} TF  gemm_ps {fl / t_ps / 1e6:5.0f} TF  no-store {fl / t_no / 1e6:5.0f} TF",
               flush=True)
     # grid sweep at the qkv shape (persistence: tiles per workgroup)

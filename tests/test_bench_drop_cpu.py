@@ -25,6 +25,12 @@ def test_bench_drop_three_peers_one_crash(tmp_path):
     assert rec["regroup_sync_ms"] - rec["steady_sync_ms"] < 0.5 * 1e3 * 0.9, rec
     assert rec["comm_build_ms"] is not None and rec["redo_ms"] is not None
     assert rec["ms_per_step_after"] > 0 and rec["samples_per_s_after"] > 0
+    # stage anatomy of the regroup round: the stages add up to the round, and
+    # the bell wait -- which used to hold the heartbeat thread's store ops behind it on a shared
+    # client (a 0.65 s round with 41 ms detection) -- stays within one bell period
+    st = rec["regroup_stages_ms"]
+    assert st is not None and abs(st["unaccounted_ms"]) < 0.25 * st["sync_ms"] + 5, st
+    assert st["bell_wait_ms"] < 300, st
 
 
 import pytest  # noqa: E402

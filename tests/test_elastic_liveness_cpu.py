@@ -66,7 +66,7 @@ def _body(pid, port):
             break
     ev = [e for e in mem.events if e["event"] in ("abort", "regroup")]
     out = {"gen": mem.gen, "members": list(mem.members), "events": ev,
-           "eof": [m for m, _ in mem.eof_events], "failed": tr.failed_rounds}
+           "eof": [m for m, _ in mem.eof_events] + list(mem._refused), "failed": tr.failed_rounds}
     mem.leave()
     return out
 
@@ -98,10 +98,60 @@ def test_sigkilled_peer_dropped_by_liveness_eof_not_lease():
     for pid in range(W - 1):
         r = out[pid]
         assert r["gen"] >= 1 and r["members"] == [0, 1], r
-        assert W - 1 in r["eof"], r  # the liveness link of the dead peer closed
+        # the liveness link of the dead peer closed (or, when it died before this survivor's first
+        # connect, its port refused the connect while its heartbeat stood still)
+        assert W - 1 in r["eof"], r
         abort = next(e for e in r["events"] if e["event"] == "abort")
         regroup = next(e for e in r["events"] if e["event"] == "regroup")
         assert regroup["dropped"] == [W - 1], regroup
         # abort -> agreed new generation without the dead peer: far below the 30 s lease
         assert regroup["t"] - abort["t"] < 5.0, (abort, regroup)
         assert r["failed"] >= 1
+
+
+def test_unreachable_liveness_address_is_not_a_death():
+    """a member whose published liveness address cannot be reached (wrong route,
+    firewall, nobody listening) must not be declared dead -- only an EOF on an established
+    connection is; the caller (the heartbeat thread) must not block on the connect either."""
+    from distributedvolunteercomputing_amd.parallel.elastic import _P, ElasticMembership, _Liveness
+
+    port = _mp.free_port()
+    store = _mp.make_store(0, 1, port)
+    eofs = []
+    live = _Liveness(store, 0, "127.0.0.1", lambda m, a: eofs.append((m, a)))
+    try:
+        closed = _mp.free_port()  # nobody listens here: ECONNREFUSED
+        store.set(f"{_P}live/1", f"127.0.0.1:{closed}")
+        store.set(f"{_P}live/2", "10.255.255.1:9")  # unroutable: the connect times out
+        t0 = time.time()
+        live.watch([0, 1, 2])
+        assert time.time() - t0 < 0.5  # connects run off the caller's thread
+        deadline = time.time() + 5
+        while live.connect_failures < 1 and time.time() < deadline:
+            time.sleep(0.02)
+        live.watch([0, 1, 2])  # a retry inside retry_s is skipped, never an EOF
+        time.sleep(0.3)
+        assert live.connect_failures >= 1
+        assert eofs == []
+        # a reachable member is connected, and its death is still an EOF
+        other = _Liveness(store, 3, "127.0.0.1", lambda m, a: None)
+        live.watch([3])
+        deadline = time.time() + 5
+        while 3 not in live._conn and time.time() < deadline:
+            time.sleep(0.02)
+        assert 3 in live._conn
+        other.close()
+        deadline = time.time() + 5
+        while not eofs and time.time() < deadline:
+            time.sleep(0.02)
+        assert [m for m, _ in eofs] == [3]
+    finally:
+        live.close()
+    # the published host follows the route to the store's host, not MASTER_ADDR
+    old = os.environ.pop("MASTER_ADDR", None)
+    try:
+        mem = ElasticMembership(store, 5, backend="gloo", liveness=False)
+        assert mem.live_host == "127.0.0.1"
+    finally:
+        if old is not None:
+            os.environ["MASTER_ADDR"] = old

@@ -60,10 +60,13 @@ def test_join_reply_carries_the_prefix_after_the_port(coord):
         addr = f"127.0.0.1:{hub.port}"
         r = _udp(coord.control_port, protocol.encode("join", addr))
         fields = r.split("||")
-        assert fields[0] == "ok" and int(fields[1]) > 0 and fields[2] == coord.store_secret
-        assert protocol.split_store_ref(
-            protocol.ControlClient("127.0.0.1", coord.control_port).call("store", addr)) == (
-            coord.train_store_port, coord.store_secret)
+        # the p2p plane's prefix, never the training one (join is unauthenticated)
+        assert fields[0] == "ok" and int(fields[1]) > 0 and fields[2] == coord.p2p_secret
+        assert coord.p2p_secret != coord.store_secret
+        # with an admission token, a joined volunteer cannot get the training store reference
+        with pytest.raises(Exception):
+            protocol.ControlClient("127.0.0.1", coord.control_port, retries=1).call("store", addr)
+        assert coord.store_secret not in r
     finally:
         _udp(coord.control_port, protocol.encode("end", f"127.0.0.1:{hub.port}"))
         hub.close()
@@ -91,3 +94,28 @@ def test_abort_posted_without_the_prefix_is_not_followed(coord):
         assert peer.tripped() and peer.abort_reason() == "real abort"
     finally:
         peer.stop_heartbeat()
+
+
+def test_joined_volunteer_cannot_touch_training_keys(coord):
+    """a host that joins as a volunteer (no token) learns only the p2p prefix; the keys it
+    can write under it are not the ones the training peers act on, and it cannot read theirs."""
+    from distributedvolunteercomputing_amd.control.transport import FrameHub
+
+    raw = dist.TCPStore("127.0.0.1", coord.train_store_port, None, False, timeout=datetime.timedelta(seconds=10))
+    peer = ElasticMembership(dist.PrefixStore(coord.store_secret, raw), 0, lease_s=5.0)
+    peer.bootstrap([0])
+    hub = FrameHub(0)
+    try:
+        addr = f"127.0.0.1:{hub.port}"
+        leaked = _udp(coord.control_port, protocol.encode("join", addr)).split("||")[2]
+        vol = dist.PrefixStore(leaked, dist.TCPStore("127.0.0.1", coord.train_store_port, None, False,
+                                                     timeout=datetime.timedelta(seconds=10)))
+        assert not vol.check(["vcx/el/gen/0"])  # the training generation record is invisible
+        vol.set("vcx/el/abort/0", "forged by a joined volunteer")
+        vol.add("vcx/el/njoin", 1)
+        peer._watch()
+        assert not peer.tripped() and peer._njoin() == 0
+    finally:
+        peer.stop_heartbeat()
+        _udp(coord.control_port, protocol.encode("end", f"127.0.0.1:{hub.port}"))
+        hub.close()
