@@ -42,6 +42,8 @@ class RuntimeConfig:
     tunableop_file: str = ""  # VCX_TUNABLEOP_FILE: alternative TunableOp results file
     offload_arch: str = "gfx950"  # VCX_OFFLOAD_ARCH: target of the in-tree HIP build
     colour_native: bool = True  # VCX_COLOUR_NATIVE: video BGR<->YUV in the C++ runtime (False: numpy)
+    resnet_conv1x1: str = "gemm"  # VCX_RESNET_CONV1X1: ResNet 1x1 convolutions as GEMMs on the NHWC view ("gemm")
+    # or through the convolution library ("conv")
     # ---- distributed / control plane
     gloo_host: str = "127.0.0.1"  # VCX_GLOO_HOST: interface gloo peer groups bind to
     p2p_backend: str = ""  # VCX_P2P_BACKEND: pair-group backend of the p2p chunk plane ("" = auto)
@@ -58,6 +60,7 @@ class RuntimeConfig:
 _ENV = {
     "gemm": ("VCX_GEMM", str),
     "mlp": ("VCX_MLP", str),
+    "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),
     "gemm_select": ("VCX_GEMM_SELECT", _bool),
     "wgrad_big_split_min_m": ("VCX_WGRAD_BIG_SPLIT_MIN_M", int),

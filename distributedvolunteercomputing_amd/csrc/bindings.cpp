@@ -136,50 +136,6 @@ void gemm_nt(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
               (int)b.stride(0), (int)c.stride(0), (int)epi, cur_stream());
 }
 
-// Persistent role-split GEMM (gemm_persistent.hip): c[M, N] = a[M, K] . op(b), op(b) = b^T for b [N, K]
-// (layout 0) or b for b [K, N] (layout 1); epilogues as gemm_nt
-bool gemm_p_supported(int64_t M, int64_t N, int64_t K, int64_t layout) {
-  return vcx_gemm_p_supported((int)M, (int)N, (int)K, (int)layout);
-}
-
-void gemm_p(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor> c2, c10::optional<at::Tensor> bias,
-            c10::optional<at::Tensor> colsum, int64_t epi, int64_t layout) {
-  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_p: 2-D cuda tensors");
-  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
-              "gemm_p: bf16 operands");
-  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm_p: unit inner strides");
-  TORCH_CHECK(layout == 0 || layout == 1, "gemm_p: layout 0 (b [N, K]) or 1 (b [K, N])");
-  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_p: epilogue 0..3");
-  const int64_t M = a.size(0), K = a.size(1), N = layout == 0 ? b.size(0) : b.size(1);
-  TORCH_CHECK((layout == 0 ? b.size(1) : b.size(0)) == K && c.size(0) == M && c.size(1) == N, "gemm_p: shape mismatch");
-  TORCH_CHECK(vcx_gemm_p_supported((int)M, (int)N, (int)K, (int)layout),
-              "gemm_p: needs M % 256 == 0, K % 64 == 0, K >= 192, N % 128 (NT) / 256 (NN) == 0");
-  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm_p: 16-B aligned rows");
-  for (const at::Tensor* t : {&a, &b, &c})
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_p: 16-B aligned base pointers");
-  TORCH_CHECK(M * std::max<int64_t>(c.stride(0), 1) * 2 < (int64_t(1) << 40), "gemm_p: output too large");
-  void* c2p = nullptr;
-  if (epi >= 2) {
-    TORCH_CHECK(c2 && c2->sizes() == c.sizes() && c2->strides() == c.strides() && c2->scalar_type() == at::kBFloat16,
-                "gemm_p: epilogue 2/3 needs c2 like c");
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(c2->data_ptr()) % 16 == 0, "gemm_p: 16-B aligned c2");
-    c2p = c2->data_ptr();
-  }
-  const void* bp = nullptr;
-  if (epi == 1 || epi == 2) {
-    TORCH_CHECK(bias && bias->numel() == N && bias->is_contiguous() && bias->scalar_type() == at::kBFloat16,
-                "gemm_p: bias [N] bf16");
-    bp = bias->data_ptr();
-  }
-  float* cs = nullptr;
-  if (epi == 3) {
-    TORCH_CHECK(colsum && colsum->numel() == N && colsum->scalar_type() == at::kFloat && colsum->is_contiguous(),
-                "gemm_p: colsum [N] fp32");
-    cs = colsum->data_ptr<float>();
-  }
-  vcx_gemm_p(a.data_ptr(), b.data_ptr(), c.data_ptr(), c2p, bp, cs, (int)M, (int)N, (int)K, (int)a.stride(0),
-             (int)b.stride(0), (int)c.stride(0), (int)epi, (int)layout, cur_stream());
-}
 
 // Persistent store-overlapped GEMM (gemm_ps.hip): c[M, N] = a[M, K] . b[N, K]^T with epilogue
 // 0 store, 1 +bias, 2 +bias -> (c = pre, c2 = gelu(pre)); grid_cap <= 0: one workgroup per CU
@@ -742,7 +698,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("reduce_bcast_bf16", &reduce_bcast_bf16);
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_supported_epi", &gemm_nt_supported_epi);
-  m.def("gemm_p_supported", &gemm_p_supported);
   m.def("gemm4", &gemm4);
   m.def("gemm_ps_supported", &gemm_ps_supported);
   m.def("gemm_ps_diag", &gemm_ps_diag, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("epi") = 0,
@@ -750,8 +705,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0,
         py::arg("waves") = 8, py::arg("stagger") = 0);
-  m.def("gemm_p", &gemm_p, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
-        py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("layout") = 0);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("splits"), py::arg("accumulate"));
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),

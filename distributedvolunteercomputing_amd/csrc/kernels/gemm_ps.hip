@@ -124,12 +124,15 @@ struct Frags {
 
 // (the body is a device function shared by two kernel templates with literal launch bounds: a
 // kernel template on NW lost its host-side stubs)
-template <int EPI, int NW, int SPOL = 0, bool STAMP = false>
+// (TAG: the diagnostic kernels instantiate their own specialisations -- a second call site of one
+// already used by gemm_ps_kernel made hipcc's host pass reject both, ROCm 7.2)
+template <int EPI, int NW, int SPOL = 0, bool STAMP = false, int TAG = 0>
 __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                              bf16* __restrict__ C, bf16* __restrict__ C2,
                                              const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
                                              int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger,
-                                             unsigned long long* __restrict__ stamps = nullptr) {
+                                             void* stamps_v) {
+  unsigned long long* stamps = (unsigned long long*)stamps_v;
   using Gm = Geo<NW>;
   constexpr int BNt = Gm::BNt, SLOTA = Gm::SLOTA, SLOTB = Gm::SLOTB, RINGB = Gm::RINGB, NSLOT = Gm::NSLOT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -142,7 +145,7 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
   auto stamp = [&](int k) {
     if constexpr (STAMP) {
       if (tid == 0 && ti < STAMP_TILES)
-        ((unsigned long long*)(smem + RINGB))[ti * NSTAMP + k] = __builtin_amdgcn_s_memtime();
+        ((unsigned long long*)(smem + RINGB))[ti * NSTAMP + k] = (unsigned long long)clock64();  // s_memtime: shader clock cycles
     }
   };
 
@@ -527,25 +530,35 @@ __global__ void __launch_bounds__(512, 1)
     gemm_ps_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
                    bf16* __restrict__ C2, const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
                    int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger) {
-  gemm_ps_body<EPI, 8>(A, B, C, C2, bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger);
+  gemm_ps_body<EPI, 8, 0, false>(A, B, C, C2, bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger, nullptr);
 }
 
 // diagnostic instances: store cache policy x stamps (scripts/gemm_ps_diag.py)
-template <int EPI, int SPOL, bool STAMP>
-__global__ void __launch_bounds__(512, 1)
-    gemm_ps_diag_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C, int M, int N,
-                        int K, int lda, int ldb, int ldc, int tilesN, int tiles, unsigned long long* stamps,
-                        int stagger) {
-  gemm_ps_body<EPI, 8, SPOL, STAMP>(A, B, C, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, tilesN, tiles,
-                                    stagger, stamps);
-}
+#define VCX_PS_DIAG(NAME, E, P, S)                                                                              \
+  __global__ void __launch_bounds__(512, 1)                                                                    \
+      NAME(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C, int M, int N, int K,   \
+           int lda, int ldb, int ldc, int tilesN, int tiles, unsigned long long* stamps, int stagger) {         \
+    gemm_ps_body<E, 8, P, S, 1>(A, B, C, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger, \
+                             (void*)stamps);                                                                   \
+  }
+VCX_PS_DIAG(gemm_ps_diag_none, EPI_NONE, 0, false)
+VCX_PS_DIAG(gemm_ps_diag_none_st, EPI_NONE, 0, true)
+VCX_PS_DIAG(gemm_ps_diag_p0, EPI_STORE, 0, false)
+VCX_PS_DIAG(gemm_ps_diag_p0_st, EPI_STORE, 0, true)
+VCX_PS_DIAG(gemm_ps_diag_p1, EPI_STORE, 1, false)
+VCX_PS_DIAG(gemm_ps_diag_p1_st, EPI_STORE, 1, true)
+VCX_PS_DIAG(gemm_ps_diag_p2, EPI_STORE, 2, false)
+VCX_PS_DIAG(gemm_ps_diag_p2_st, EPI_STORE, 2, true)
+VCX_PS_DIAG(gemm_ps_diag_p3, EPI_STORE, 3, false)
+VCX_PS_DIAG(gemm_ps_diag_p3_st, EPI_STORE, 3, true)
+#undef VCX_PS_DIAG
 
 template <int EPI>
 __global__ void __launch_bounds__(256, 2)
     gemm_ps4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
                     bf16* __restrict__ C2, const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
                     int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger) {
-  gemm_ps_body<EPI, 4>(A, B, C, C2, bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger);
+  gemm_ps_body<EPI, 4, 0, false>(A, B, C, C2, bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger, nullptr);
 }
 
 }  // namespace gemm_ps
@@ -637,17 +650,17 @@ void vcx_gemm_ps_diag(const void* A, const void* B, void* C, int M, int N, int K
   };
   const bool st = stamps != nullptr;
   if (epi == EPI_NONE) {
-    st ? go(gemm_ps_diag_kernel<EPI_NONE, 0, true>) : go(gemm_ps_diag_kernel<EPI_NONE, 0, false>);
+    st ? go(gemm_ps_diag_none_st) : go(gemm_ps_diag_none);
     return;
   }
   switch (policy * 2 + (st ? 1 : 0)) {
-    case 0: go(gemm_ps_diag_kernel<EPI_STORE, 0, false>); break;
-    case 1: go(gemm_ps_diag_kernel<EPI_STORE, 0, true>); break;
-    case 2: go(gemm_ps_diag_kernel<EPI_STORE, 1, false>); break;
-    case 3: go(gemm_ps_diag_kernel<EPI_STORE, 1, true>); break;
-    case 4: go(gemm_ps_diag_kernel<EPI_STORE, 2, false>); break;
-    case 5: go(gemm_ps_diag_kernel<EPI_STORE, 2, true>); break;
-    case 6: go(gemm_ps_diag_kernel<EPI_STORE, 3, false>); break;
-    default: go(gemm_ps_diag_kernel<EPI_STORE, 3, true>); break;
+    case 0: go(gemm_ps_diag_p0); break;
+    case 1: go(gemm_ps_diag_p0_st); break;
+    case 2: go(gemm_ps_diag_p1); break;
+    case 3: go(gemm_ps_diag_p1_st); break;
+    case 4: go(gemm_ps_diag_p2); break;
+    case 5: go(gemm_ps_diag_p2_st); break;
+    case 6: go(gemm_ps_diag_p3); break;
+    default: go(gemm_ps_diag_p3_st); break;
   }
 }

@@ -21,10 +21,6 @@ bool vcx_gemm_nt_supported(int M, int N, int K);
 bool vcx_gemm_nt_supported_epi(int M, int N, int K, int epi);
 void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,
                  int lda, int ldb, int ldc, int epi, hipStream_t s);
-// gemm_persistent.hip: persistent role-split GEMM, layout 0: C = A B^T (B [N, K]), 1: C = A B (B [K, N])
-bool vcx_gemm_p_supported(int M, int N, int K, int layout);
-void vcx_gemm_p(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,
-                int lda, int ldb, int ldc, int epi, int layout, hipStream_t s);
 // gemm_ps.hip: persistent store-overlapped GEMM, C = A B^T (B [N, K]); epi 0 store, 1 +bias,
 // 2 +bias -> (C = pre, C2 = gelu(pre)); grid_cap <= 0: one workgroup per CU
 bool vcx_gemm_ps_supported(int M, int N, int K, int epi);

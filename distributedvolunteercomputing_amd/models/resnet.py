@@ -1,14 +1,40 @@
 """ResNet-50 for synthetic ImageNet-shaped data (BASELINE.json config 3: "ResNet-50 on
 synthetic ImageNet shapes, top-k sparsified gradients + error feedback, 8 peers").
 
-Channels-last bf16 so MIOpen picks its NHWC implicit-GEMM (MFMA) convolution kernels;
-BatchNorm statistics are buffers that the trainers average at every synchronisation.
+Channels-last bf16. The 1x1 convolutions (about 70 % of the FLOPs) are plain GEMMs on the NHWC
+view -- [N*H*W, Cin] x [Cout, Cin]^T -- and run through the framework's linear layer (library
+GEMMs picked per shape, split-M weight gradients summed straight into the flat gradient buffer);
+stride-2 ones subsample the NHWC view first. The 3x3 / 7x7 convolutions go through MIOpen's NHWC
+kernels. BatchNorm statistics are buffers that the trainers average at every synchronisation.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from .. import config
+
+
+class Conv1x1(nn.Conv2d):
+    """1x1 convolution (no bias) computed as a GEMM on the channels-last layout (same parameter as
+    nn.Conv2d, so checkpoints and the flat parameter buffer are unchanged)."""
+
+    def __init__(self, cin, cout, stride=1):
+        super().__init__(cin, cout, 1, stride=stride, bias=False)
+
+    def forward(self, x):
+        if not (x.is_cuda and config.get().resnet_conv1x1 == "gemm"
+                and x.is_contiguous(memory_format=torch.channels_last)):
+            return super().forward(x)
+        from ..ops.linear import linear
+
+        xh = x.permute(0, 2, 3, 1)  # [N, H, W, C] view of the channels-last storage
+        if self.stride[0] != 1:
+            xh = xh[:, ::self.stride[0], ::self.stride[1], :].contiguous()
+        N, H, W, C = xh.shape
+        y = linear(xh.reshape(N * H * W, C), self.weight.view(self.out_channels, C))
+        return y.view(N, H, W, self.out_channels).permute(0, 3, 1, 2)
 
 
 class Bottleneck(nn.Module):
@@ -17,16 +43,16 @@ class Bottleneck(nn.Module):
     def __init__(self, cin, width, stride=1):
         super().__init__()
         cout = width * self.expansion
-        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.conv1 = Conv1x1(cin, width)
         self.bn1 = nn.BatchNorm2d(width)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
         self.bn2 = nn.BatchNorm2d(width)
-        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.conv3 = Conv1x1(width, cout)
         self.bn3 = nn.BatchNorm2d(cout)
         nn.init.zeros_(self.bn3.weight)  # zero-init residual branch (Goyal et al.)
         self.down = None
         if stride != 1 or cin != cout:
-            self.down = nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride, bias=False), nn.BatchNorm2d(cout))
+            self.down = nn.Sequential(Conv1x1(cin, cout, stride=stride), nn.BatchNorm2d(cout))
 
     def forward(self, x):
         idt = x if self.down is None else self.down(x)

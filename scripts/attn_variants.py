@@ -33,18 +33,34 @@ def tm(fn, it=10):
     return sorted(ts)[len(ts) // 2]
 
 
+# fp32 reference of the forward (first 4 batch elements suffice for the error check: the kernels do not
+# mix batch elements; computed for the whole batch to compare whole tensors)
+qf32 = qkv.float()
+q_, k_, v_ = qf32[:, :, 0].transpose(1, 2), qf32[:, :, 1].transpose(1, 2), qf32[:, :, 2].transpose(1, 2)
+o32, l32 = [], []
+for i in range(B):
+    sc = (q_[i] @ k_[i].transpose(-1, -2)) * scale
+    sc = sc.masked_fill(torch.ones(T, T, device=dev, dtype=torch.bool).triu(1), float("-inf"))
+    l32.append(torch.logsumexp(sc, -1) * 1.4426950408889634)  # log2 domain, as the kernel stores it
+    o32.append((torch.softmax(sc, -1) @ v_[i]).transpose(0, 1))
+o32, l32 = torch.stack(o32), torch.stack(l32)
+del qf32, q_, k_, v_
 C.attn_set_variant(2, 0, 0, 0)  # reference outputs: the simplest variant
 o_ref, lse_ref = C.attn_fwd(qkv, scale)
 g_ref = C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)
 torch.cuda.synchronize()
 res = {}
 for rnd in range(3):
-    for fv in ((2, 0, 1), (3, 0, 1), (2, 1, 1), (3, 1, 0), (3, 1, 1)):  # (waves/SIMD, DMA, LDS-staged output stores)
+    # (waves/SIMD, DMA (2 = the v2 kernel: prescaled Q, -m as the initial S accumulator), LDS-staged stores)
+    for fv in ((3, 1, 1), (2, 2, 1), (3, 2, 1)):
         C.attn_set_variant(fv[0], fv[1], 1, fv[2])
         o, l = C.attn_fwd(qkv, scale)
         if rnd == 0:
             err = (o.float() - o_ref.float()).abs().max().item()
-            print(f"fwd variant {fv}: max|o - o_ref| = {err:.3e}", flush=True)
+            e32 = (o.float() - o32).abs().max().item()
+            el = (l.float() - l32).abs().max().item()
+            print(f"fwd variant {fv}: max|o - o_ref| = {err:.3e}  vs fp32: max|o - o32| = {e32:.3e}  max|lse - lse32| "
+                  f"= {el:.3e}", flush=True)
         res.setdefault(("fwd", fv), []).append(tm(lambda: C.attn_fwd(qkv, scale)))
     for bd in ((0, 1), (1, 0), (1, 1)):  # (backward LDS-DMA mask, LDS-staged output stores)
         C.attn_set_variant(3, 1, *bd)

@@ -9,9 +9,10 @@ O=gpurun_out/rccl8
 mkdir -p $O
 L="python -u scripts/rccl_rehearsal_launch.py"
 B="python -u bench.py --steps 8 --warmup 4 --batch 8"
-step() {  # name, seconds, command...
+step() {  # name, seconds, command... (ONLY="name1 name2": run just those)
   local name=$1 secs=$2
   shift 2
+  if [ -n "$ONLY" ] && [[ " $ONLY " != *" $name "* ]]; then return 0; fi
   echo "== $name $(date +%T)" | tee -a $O/summary.txt
   timeout -k 10 "$secs" "$@" > $O/$name.log 2>&1
   local rc=$?

@@ -146,3 +146,25 @@ def test_rope_qkv_matches_reference(gpu):
     sum((r * g).sum() for r, g in zip((qr, kr, vr), gs)).backward()
     rel = float((qkv.grad.float() - x32.grad).norm() / x32.grad.norm())
     assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_resnet_conv1x1_gemm_matches_conv(gpu, stride):
+    """The ResNet 1x1 convolution as a GEMM on the NHWC view (models/resnet.py Conv1x1) against an
+    fp32 F.conv2d: output, input gradient and weight gradient, stride 1 and 2."""
+    from distributedvolunteercomputing_amd.models.resnet import Conv1x1
+
+    torch.manual_seed(stride)
+    conv = Conv1x1(64, 256, stride=stride).to(gpu, torch.bfloat16)
+    x = torch.randn(8, 64, 28, 28, device=gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x.requires_grad_()
+    y = conv(x)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    g = torch.randn_like(y.float())
+    y.backward(g.to(y.dtype))
+    x32 = x.detach().float().requires_grad_()
+    w32 = conv.weight.detach().float().requires_grad_()
+    y32 = torch.nn.functional.conv2d(x32, w32, stride=stride)
+    y32.backward(g)
+    for a, r in ((y.float(), y32), (x.grad.float(), x32.grad), (conv.weight.grad.float(), w32.grad)):
+        assert (a - r).norm() / r.norm() < 1e-2, float((a - r).norm() / r.norm())
