@@ -127,16 +127,23 @@ def bench_job(args, dev, plane="relay", source=None, out_ext=".npy"):
     workers = [client("127.0.0.1", "127.0.0.1", control_port=coord.control_port, my_port=0, engine=eng,
                       out_dir=tmp, out_ext=out_ext) for _ in range(args.workers)]
     try:
+        if source and source.endswith(".npy") and args.source_frames and args.source_frames < args.frames:
+            source = f"{source}@{args.frames}"  # the pre-generated file played in a loop
         req.become_requester(source or f"synthetic:{args.frames}:{args.width}x{args.height}")
-        t = req.wait_job(timeout=600)
+        t = req.wait_job(timeout=1800)
         n = req.sink.written if (t and req.sink is not None) else 0
+        # host busy time per stage of each volunteer thread (where the job's wall time goes)
+        spans = {"requester": req.hspans.snapshot()}
+        for i, w in enumerate(workers):
+            spans[f"worker{i}"] = w.hspans.snapshot()
     finally:
         for c in [req] + workers:
             c.exit_threads()
         coord.exit_threads()
     pre = "job" if plane == "relay" else f"job_{plane}"
     return {f"{pre}_time_s": round(t, 3) if t else None, f"{pre}_frames": n,
-            f"{pre}_frames_per_s": round(n / t, 1) if t else None, "workers": args.workers}
+            f"{pre}_frames_per_s": round(n / t, 1) if t else None, "workers": args.workers,
+            f"{pre}_host_spans": spans}
 
 
 def make_npy_source(args) -> str:
@@ -148,9 +155,10 @@ def make_npy_source(args) -> str:
 
     d = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
     path = os.path.join(d, f"vcx_bench_src_{os.getpid()}.npy")
-    arr = np.lib.format.open_memmap(path, mode="w+", dtype=np.uint8, shape=(args.frames, args.height, args.width, 3))
-    base = [synthetic_frame(i, args.width, args.height) for i in range(min(args.frames, 64))]
-    for i in range(args.frames):  # 64 distinct frames, each frame's own index bar code
+    nf = min(args.frames, args.source_frames) if args.source_frames else args.frames
+    arr = np.lib.format.open_memmap(path, mode="w+", dtype=np.uint8, shape=(nf, args.height, args.width, 3))
+    base = [synthetic_frame(i, args.width, args.height) for i in range(min(nf, 64))]
+    for i in range(nf):  # 64 distinct frames, each frame's own index bar code
         f = base[i % len(base)]
         arr[i] = f
         seg = max(1, args.width // 16)
@@ -170,6 +178,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--workers", type=int, default=2)
+    ap.add_argument("--source-frames", type=int, default=0,
+                    help="npy source: pre-generate this many frames and play them in a loop up to --frames "
+                         "(a steady-state job without an --frames-sized file in RAM)")
     ap.add_argument("--job-repeats", type=int, default=3, help="job runs per plane (median reported)")
     ap.add_argument("--no-job", action="store_true")
     ap.add_argument("--data-plane", default="both", choices=["relay", "p2p", "both"])

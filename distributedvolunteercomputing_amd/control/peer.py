@@ -41,6 +41,7 @@ from ..io.video import open_sink, open_source
 from ..jobs.video import DetectorEngine, Engine, OrderedSink
 from ..ops import vision as V
 from ..utils.metrics import Metrics
+from ..utils.trace import HostSpans
 from . import protocol
 from .transport import FrameHub, FrameSender
 
@@ -103,6 +104,7 @@ class client:  # noqa: N801 (reference class name)
         self.resize_device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
         self.out_ext = out_ext
         self.metrics = Metrics("client")
+        self.hspans = HostSpans()  # host busy time per stage (bench_video.py reports it)
         self.engine = engine
         self._engine_lock = threading.Lock()
         # data port first: the coordinator connects to it while handling our join
@@ -208,13 +210,15 @@ class client:  # noqa: N801 (reference class name)
         C = self.number_of_frames_in_chunk
         while self.continue_requesting:
             if src.chunked:  # whole chunks straight from the source (memory-mapped file: no copy here)
-                arr = src.read_chunk(C)
+                with self.hspans.span("req_read"):
+                    arr = src.read_chunk(C)
                 if len(arr) == 0:
                     break
                 self.send_q.put(("chunk", (n + 1, arr)))
                 n += len(arr)
                 continue
-            ok, frame = src.read()
+            with self.hspans.span("req_read"):
+                ok, frame = src.read()
             if not ok:
                 break
             n += 1
@@ -257,10 +261,11 @@ class client:  # noqa: N801 (reference class name)
             if block is None and not frames:
                 return
             first = frames[0] if block is None else block[0]
-            if self.preresize and self.resize_device is not None and first.shape[1] != 400:
-                chunk = self._resize_chunk(frames if block is None else block)
-            else:
-                chunk = np.stack(frames) if block is None else np.ascontiguousarray(block)
+            with self.hspans.span("req_pack_resize"):
+                if self.preresize and self.resize_device is not None and first.shape[1] != 400:
+                    chunk = self._resize_chunk(frames if block is None else block)
+                else:
+                    chunk = np.stack(frames) if block is None else np.ascontiguousarray(block)
             info = f"{self.my_ip}||request||{'-'.join(map(str, nums))}||{chunk.shape[1]}||{chunk.shape[2]}"
             if self.plane is not None:  # p2p: the chunk stays here; the coordinator gets its metadata
                 key = next(self._keys)
@@ -268,7 +273,8 @@ class client:  # noqa: N801 (reference class name)
                     self._outgoing[key] = chunk if isinstance(chunk, torch.Tensor) else _host_tensor(chunk)
                 ok = self.sender.send_image(info, _EMPTY, p2p=1, key=key, cshape=list(chunk.shape))
             else:
-                ok = self.sender.send_image(info, chunk)
+                with self.hspans.span("req_send"):
+                    ok = self.sender.send_image(info, chunk)
             if not ok:
                 self.log("uplink send failed")
             self.metrics.incr("chunks_sent")
@@ -355,8 +361,9 @@ class client:  # noqa: N801 (reference class name)
         """Hand returned frames to the in-order sink; a sink failure (e.g. an unwritable output)
         is logged and counted instead of killing the receive thread."""
         try:
-            for i, n in enumerate(nums):
-                self.sink.push(n, frames[i])
+            with self.hspans.span("req_sink"):
+                for i, n in enumerate(nums):
+                    self.sink.push(n, frames[i])
         except Exception as e:  # noqa: BLE001
             self.metrics.incr("sink_errors")
             print(f"output sink failed: {type(e).__name__}: {e}", flush=True)
@@ -463,7 +470,8 @@ class client:  # noqa: N801 (reference class name)
                 hdr, arr, requester, nums = item
                 dev_res = bool(hdr.get("p2p")) and arr.device.type != "cpu"
                 eng = self._get_engine()
-                job = eng.submit_tensor(arr, requester) if dev_res else eng.submit(arr, requester)
+                with self.hspans.span("wk_submit"):
+                    job = eng.submit_tensor(arr, requester) if dev_res else eng.submit(arr, requester)
                 nxt = (job, hdr, requester, nums, time.perf_counter(), dev_res)
             else:
                 nxt = None
@@ -476,21 +484,24 @@ class client:  # noqa: N801 (reference class name)
 
     def _finish(self, job, hdr, requester, nums, t0, dev_res=False):
         if dev_res:  # annotated chunk on the device: held for the pair send to the requester
-            out = job.result()
+            with self.hspans.span("wk_result"):
+                out = job.result()
             if out.device != self.plane.device:
                 out = out.to(self.plane.device)
             self.metrics.observe("chunk_infer_ms", (time.perf_counter() - t0) * 1e3)
             self.metrics.incr("frames_processed", len(nums))
             self._post_result(hdr, out, requester, nums)
             return
-        out, counts = job.result()
+        with self.hspans.span("wk_result"):
+            out, counts = job.result()
         self.metrics.observe("chunk_infer_ms", (time.perf_counter() - t0) * 1e3)
         self.metrics.incr("frames_processed", len(nums))
         if hdr.get("p2p"):  # host chunk from a gloo pair: held (copied out of the pinned slot)
             self._post_result(hdr, torch.from_numpy(np.array(out)), requester, nums)
             return
         info = f"{requester}||processed||{'-'.join(map(str, nums))}||{out.shape[1]}||{out.shape[2]}"
-        self.sender.send_image(info, out, chunk=hdr.get("chunk", -1))
+        with self.hspans.span("wk_send"):
+            self.sender.send_image(info, out, chunk=hdr.get("chunk", -1))
 
     def _post_result(self, hdr, out, requester, nums):
         """Hold the annotated chunk until the coordinator names its destination; report it."""

@@ -206,6 +206,69 @@ void gemm_ps_diag(at::Tensor a, at::Tensor b, at::Tensor c, int64_t epi, int64_t
                    (int)policy, sp, (int)grid_cap, (int)stagger, cur_stream());
 }
 
+// Train-mode BatchNorm (+ residual) (+ ReLU) on NHWC bf16 activations (batchnorm.hip). x / res / y:
+// contiguous [..., C] (the NHWC view of a channels-last tensor); gamma / beta bf16 [C]; running stats
+// bf16 or fp32 [C], updated in place (skipped when undefined). Returns y, mean, rstd, scale (fp32 [C]).
+std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma, at::Tensor beta,
+                                     c10::optional<at::Tensor> run_mean, c10::optional<at::Tensor> run_var, double eps,
+                                     double momentum, bool relu) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == at::kBFloat16, "bn: x bf16 contiguous NHWC");
+  const int64_t C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(vcx_bn_supported((int)C) && R > 0, "bn: C must be a power of two in 8..2048");
+  TORCH_CHECK(gamma.numel() == C && beta.numel() == C && gamma.scalar_type() == at::kBFloat16 &&
+                  beta.scalar_type() == at::kBFloat16 && gamma.is_contiguous() && beta.is_contiguous(), "bn: gamma/beta bf16 [C]");
+  if (res) TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous() && res->scalar_type() == at::kBFloat16, "bn: residual like x");
+  void *rm = nullptr, *rv = nullptr;
+  int fp32 = 0;
+  if (run_mean && run_mean->defined()) {
+    TORCH_CHECK(run_var && run_mean->numel() == C && run_var->numel() == C && run_mean->is_contiguous() &&
+                    run_var->is_contiguous() && run_mean->scalar_type() == run_var->scalar_type() &&
+                    (run_mean->scalar_type() == at::kBFloat16 || run_mean->scalar_type() == at::kFloat), "bn: running stats [C]");
+    rm = run_mean->data_ptr();
+    rv = run_var->data_ptr();
+    fp32 = run_mean->scalar_type() == at::kFloat;
+  }
+  auto f = x.options().dtype(at::kFloat);
+  at::Tensor ws = at::zeros({2 * C}, f), st = at::empty({4, C}, f);
+  at::Tensor y = at::empty_like(x);
+  vcx_bn_fwd_train(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), R, (int)C, gamma.data_ptr(),
+                   beta.data_ptr(), rm, rv, fp32, (float)eps, (float)momentum, ws.data_ptr<float>(), st[0].data_ptr<float>(),
+                   st[1].data_ptr<float>(), st[2].data_ptr<float>(), st[3].data_ptr<float>(), relu ? 1 : 0, cur_stream());
+  return {y, st[0], st[1], st[2]};
+}
+
+at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor scale, at::Tensor shift, bool relu) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == at::kBFloat16, "bn: x bf16 contiguous NHWC");
+  const int64_t C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(vcx_bn_supported((int)C), "bn: C must be a power of two in 8..2048");
+  TORCH_CHECK(scale.numel() == C && shift.numel() == C && scale.scalar_type() == at::kFloat &&
+                  shift.scalar_type() == at::kFloat && scale.is_contiguous() && shift.is_contiguous(), "bn: scale/shift fp32 [C]");
+  if (res) TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous() && res->scalar_type() == at::kBFloat16, "bn: residual like x");
+  at::Tensor y = at::empty_like(x);
+  vcx_bn_apply(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), R, (int)C, scale.data_ptr<float>(),
+               shift.data_ptr<float>(), relu ? 1 : 0, cur_stream());
+  return y;
+}
+
+// returns dx, d residual (undefined unless want_dres), dgamma, dbeta (fp32 [C])
+std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Tensor mean, at::Tensor rstd,
+                               at::Tensor scale, bool relu, bool want_dres) {
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && x.is_contiguous() && y.is_contiguous() &&
+                  dy.sizes() == x.sizes() && y.sizes() == x.sizes() && dy.scalar_type() == at::kBFloat16 &&
+                  x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16, "bn_bwd: dy, y, x bf16 NHWC alike");
+  const int64_t C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(vcx_bn_supported((int)C), "bn: C must be a power of two in 8..2048");
+  for (const at::Tensor* t : {&mean, &rstd, &scale})
+    TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(), "bn_bwd: stats fp32 [C]");
+  at::Tensor ws = at::zeros({2 * C}, x.options().dtype(at::kFloat));
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dres = want_dres ? at::empty_like(x) : at::Tensor();
+  vcx_bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+             scale.data_ptr<float>(), R, (int)C, ws.data_ptr<float>(), dx.data_ptr(),
+             want_dres ? dres.data_ptr() : nullptr, relu ? 1 : 0, cur_stream());
+  return {dx, dres, ws.narrow(0, C, C), ws.narrow(0, 0, C)};
+}
+
 // 4-wave one-wave-per-SIMD GEMM (gemm4.hip): c[M, N] = a[M, K] . b[N, K]^T
 void gemm4(at::Tensor a, at::Tensor b, at::Tensor c) {
   TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm4: 2-D cuda tensors");
@@ -700,6 +763,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nt_supported_epi", &gemm_nt_supported_epi);
   m.def("gemm4", &gemm4);
   m.def("gemm_ps_supported", &gemm_ps_supported);
+  m.def("bn_supported", [](int64_t C) { return vcx_bn_supported((int)C); });
+  m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
+        py::arg("run_mean"), py::arg("run_var"), py::arg("eps"), py::arg("momentum"), py::arg("relu"));
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd", &bn_bwd);
   m.def("gemm_ps_diag", &gemm_ps_diag, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("epi") = 0,
         py::arg("policy") = 0, py::arg("stamps") = py::none(), py::arg("grid_cap") = 0, py::arg("stagger") = 0);
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),

@@ -1,0 +1,284 @@
+// Train-mode BatchNorm fused with its ReLU and the residual add, channels-last (NHWC) bf16, for the
+// ResNet-50 of BASELINE config 3 (models/resnet.py). Torch runs each of these as separate passes
+// (batch statistics, normalise, add, ReLU; and in the backward ReLU', statistics of the gradient,
+// input gradient), each reading or writing the whole activation; here:
+//   forward : stats  (read x once: per-channel sum / sum of squares in fp32, block partials + atomics)
+//             finalize (mean, 1/std, the per-channel affine scale/shift, running-stat update)
+//             apply  (read x [+ residual], write y = relu(x * scale + shift [+ residual]))
+//   backward: reduce (read dy, y, x: per-channel sum dz and sum dz * xhat, dz = dy * [y > 0])
+//             dx     (read dy, y, x, write dx [and d residual = dz])
+// Rows R = N * H * W, C channels (a power of two, 8 .. 2048); every lane moves 16 B (8 channels) per
+// access. No reference analog (north-star config 3).
+#include "vcx_common.h"
+
+namespace vcx {
+namespace bn {
+
+constexpr int NT = 256;
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void load8(const bf16* p, float (&v)[8]) {
+  const bf16x8 x = *(const bf16x8*)p;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)x[i];
+}
+
+// per-channel partial sums of this block over rows [r0, r1), reduced in LDS over the threads that
+// share a channel chunk, then added to out0 / out1 (fp32 [C]) with one atomic per channel
+template <typename F>
+__device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&& body, float* out0, float* out1) {
+  __shared__ float red[2][NT][9];  // [quantity][thread][8 channels + pad]
+  const int tid = threadIdx.x;
+  const int cpr = C / 8;                // chunks per row
+  const int rpp = NT / cpr;             // rows per pass (>= 1)
+  const int ch = tid % cpr, rr = tid / cpr;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s0[i] = s1[i] = 0.f;
+  if (rr < rpp)
+    for (int64_t r = r0 + rr; r < r1; r += rpp) body(r * C + ch * 8, s0, s1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red[0][tid][i] = s0[i];
+    red[1][tid][i] = s1[i];
+  }
+  __syncthreads();
+  // thread t < C: channel t = chunk t / 8, element t % 8, summed over the rpp row slots
+  for (int c = tid; c < C; c += NT) {
+    const int k = c / 8, e = c % 8;
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < rpp; ++q) {
+      a += red[0][k + q * cpr][e];
+      b += red[1][k + q * cpr][e];
+    }
+    atomicAdd(out0 + c, a);
+    atomicAdd(out1 + c, b);
+  }
+}
+
+__global__ void __launch_bounds__(NT) stats_kernel(const bf16* __restrict__ x, int64_t R, int C, int64_t rows_per_block,
+                                                   float* __restrict__ sum, float* __restrict__ sumsq) {
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(R, r0 + rows_per_block);
+  channel_reduce(
+      C, r0, r1,
+      [&](int64_t off, float(&s0)[8], float(&s1)[8]) {
+        float v[8];
+        load8(x + off, v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s0[i] += v[i];
+          s1[i] = fmaf(v[i], v[i], s1[i]);
+        }
+      },
+      sum, sumsq);
+}
+
+// mean, 1/std, scale = gamma/std, shift = beta - mean * scale; running stats (unbiased variance)
+// updated in place in their own dtype (bf16 or fp32)
+template <typename RT>
+__global__ void finalize_kernel(const float* __restrict__ sum, const float* __restrict__ sumsq, int64_t R, int C,
+                                const bf16* __restrict__ gamma, const bf16* __restrict__ beta, float eps, float momentum,
+                                RT* __restrict__ run_mean, RT* __restrict__ run_var, float* __restrict__ mean_out,
+                                float* __restrict__ rstd_out, float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = 1.f / (float)R;
+  const float m = sum[c] * inv;
+  const float var = fmaxf(sumsq[c] * inv - m * m, 0.f);
+  const float rs = rsqrtf(var + eps);
+  const float g = (float)gamma[c], b = (float)beta[c];
+  mean_out[c] = m;
+  rstd_out[c] = rs;
+  scale[c] = g * rs;
+  shift[c] = b - m * g * rs;
+  if (run_mean) {
+    const float unb = R > 1 ? var * (float)R / (float)(R - 1) : var;
+    run_mean[c] = (RT)((1.f - momentum) * (float)run_mean[c] + momentum * m);
+    run_var[c] = (RT)((1.f - momentum) * (float)run_var[c] + momentum * unb);
+  }
+}
+
+// grid-stride loops whose stride (grid x 256 chunks) is a multiple of C / 8 (host check: C divides
+// 2048): every thread keeps the same 8 channels, so their constants load once
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(NT) apply_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                   const float* __restrict__ scale, const float* __restrict__ shift,
+                                                   bf16* __restrict__ y, int64_t n8, int cpr) {
+  int64_t e = blockIdx.x * (int64_t)NT + threadIdx.x;
+  const int c0 = (int)(e % cpr) * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = scale[c0 + i];
+    sh[i] = shift[c0 + i];
+  }
+  for (; e < n8; e += (int64_t)gridDim.x * NT) {
+    float v[8], r[8];
+    load8(x + e * 8, v);
+    if (RES) load8(res + e * 8, r);
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float z = fmaf(v[i], sc[i], sh[i]);
+      if (RES) z += r[i];
+      if (RELU) z = fmaxf(z, 0.f);
+      o[i] = (bf16)z;
+    }
+    *(bf16x8*)(y + e * 8) = o;
+  }
+}
+
+// backward reductions: sum dz and sum dz * xhat per channel, dz = dy [* (y > 0)]
+template <bool RELU>
+__global__ void __launch_bounds__(NT) bwd_reduce_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+                                                        const bf16* __restrict__ x, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, int64_t R, int C,
+                                                        int64_t rows_per_block, float* __restrict__ sdz,
+                                                        float* __restrict__ sdzx) {
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(R, r0 + rows_per_block);
+  const int ch = (threadIdx.x % (C / 8)) * 8;
+  float m[8], rs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    m[i] = mean[ch + i];
+    rs[i] = rstd[ch + i];
+  }
+  channel_reduce(
+      C, r0, r1,
+      [&](int64_t off, float(&s0)[8], float(&s1)[8]) {
+        float g[8], yy[8], xx[8];
+        load8(dy + off, g);
+        load8(x + off, xx);
+        if (RELU) load8(y + off, yy);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float dz = RELU ? (yy[i] > 0.f ? g[i] : 0.f) : g[i];
+          s0[i] += dz;
+          s1[i] = fmaf(dz, (xx[i] - m[i]) * rs[i], s1[i]);
+        }
+      },
+      sdz, sdzx);
+}
+
+// dx = gamma rstd (dz - (sum dz + xhat sum dz xhat) / R); d residual = dz
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(NT) bwd_dx_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+                                                    const bf16* __restrict__ x, const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd, const float* __restrict__ scale,
+                                                    const float* __restrict__ sdz, const float* __restrict__ sdzx,
+                                                    bf16* __restrict__ dx, bf16* __restrict__ dres, int64_t n8, int cpr,
+                                                    float invR) {
+  int64_t e = blockIdx.x * (int64_t)NT + threadIdx.x;
+  const int c0 = (int)(e % cpr) * 8;
+  float sc[8], m[8], rs[8], u[8], w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = scale[c0 + i];
+    m[i] = mean[c0 + i];
+    rs[i] = rstd[c0 + i];
+    u[i] = sdz[c0 + i] * invR;
+    w[i] = sdzx[c0 + i] * invR;
+  }
+  for (; e < n8; e += (int64_t)gridDim.x * NT) {
+    float g[8], yy[8], xx[8];
+    load8(dy + e * 8, g);
+    load8(x + e * 8, xx);
+    if (RELU) load8(y + e * 8, yy);
+    bf16x8 o, od;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float dz = RELU ? (yy[i] > 0.f ? g[i] : 0.f) : g[i];
+      const float xh = (xx[i] - m[i]) * rs[i];
+      o[i] = (bf16)(sc[i] * (dz - fmaf(xh, w[i], u[i])));
+      od[i] = (bf16)dz;
+    }
+    *(bf16x8*)(dx + e * 8) = o;
+    if (RES) *(bf16x8*)(dres + e * 8) = od;
+  }
+}
+
+inline int64_t rows_per_block(int64_t R, int C) {
+  // at most ~1024 blocks, each at least 32 passes of its row slots (bounds the 2C atomics per block)
+  const int64_t rpp = NT / (C / 8);
+  int64_t rpb = (R + 1023) / 1024;
+  rpb = ((rpb + rpp - 1) / rpp) * rpp;
+  return rpb < 32 * rpp ? 32 * rpp : rpb;
+}
+inline int grid_for(int64_t n8) {
+  int64_t g = (n8 + NT - 1) / NT;
+  return (int)(g < 8192 ? g : 8192);
+}
+
+}  // namespace bn
+}  // namespace vcx
+
+using namespace vcx;
+
+// C a power of two in 8 .. 2048 (the grid-stride loops keep a thread on one channel chunk)
+bool vcx_bn_supported(int C) { return C >= 8 && C <= 2048 && (2048 % C) == 0; }
+
+// forward (train): ws = [sum | sumsq] fp32 [2C] zeroed by the caller; mean/rstd/scale/shift fp32 [C]
+void vcx_bn_fwd_train(const void* x, const void* res, void* y, int64_t R, int C, const void* gamma, const void* beta,
+                      void* run_mean, void* run_var, int run_fp32, float eps, float momentum, float* ws, float* mean,
+                      float* rstd, float* scale, float* shift, int relu, hipStream_t s) {
+  using namespace bn;
+  const int64_t rpb = rows_per_block(R, C);
+  const int nb = (int)((R + rpb - 1) / rpb);
+  hipLaunchKernelGGL(stats_kernel, dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
+  if (run_fp32)
+    hipLaunchKernelGGL(finalize_kernel<float>, dim3((C + 255) / 256), dim3(256), 0, s, ws, ws + C, R, C,
+                       (const bf16*)gamma, (const bf16*)beta, eps, momentum, (float*)run_mean, (float*)run_var, mean,
+                       rstd, scale, shift);
+  else
+    hipLaunchKernelGGL(finalize_kernel<bf16>, dim3((C + 255) / 256), dim3(256), 0, s, ws, ws + C, R, C,
+                       (const bf16*)gamma, (const bf16*)beta, eps, momentum, (bf16*)run_mean, (bf16*)run_var, mean,
+                       rstd, scale, shift);
+  const int64_t n8 = R * C / 8;
+  const int g = grid_for(n8);
+  auto go = [&](auto k) {
+    hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)x, (const bf16*)res, scale, shift, (bf16*)y, n8, C / 8);
+  };
+  if (res)
+    relu ? go(apply_kernel<true, true>) : go(apply_kernel<true, false>);
+  else
+    relu ? go(apply_kernel<false, true>) : go(apply_kernel<false, false>);
+}
+
+// y = act(x * scale + shift [+ res]) with given per-channel scale/shift (eval mode)
+void vcx_bn_apply(const void* x, const void* res, void* y, int64_t R, int C, const float* scale, const float* shift,
+                  int relu, hipStream_t s) {
+  using namespace bn;
+  const int64_t n8 = R * C / 8;
+  const int g = grid_for(n8);
+  auto go = [&](auto k) {
+    hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)x, (const bf16*)res, scale, shift, (bf16*)y, n8, C / 8);
+  };
+  if (res)
+    relu ? go(apply_kernel<true, true>) : go(apply_kernel<true, false>);
+  else
+    relu ? go(apply_kernel<false, true>) : go(apply_kernel<false, false>);
+}
+
+// backward: ws = [sum dz | sum dz xhat] fp32 [2C] zeroed by the caller (they are also dbeta / dgamma)
+void vcx_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* scale,
+                int64_t R, int C, float* ws, void* dx, void* dres, int relu, hipStream_t s) {
+  using namespace bn;
+  const int64_t rpb = rows_per_block(R, C);
+  const int nb = (int)((R + rpb - 1) / rpb);
+  if (relu)
+    hipLaunchKernelGGL(bwd_reduce_kernel<true>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const bf16*)y,
+                       (const bf16*)x, mean, rstd, R, C, rpb, ws, ws + C);
+  else
+    hipLaunchKernelGGL(bwd_reduce_kernel<false>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const bf16*)y,
+                       (const bf16*)x, mean, rstd, R, C, rpb, ws, ws + C);
+  const int64_t n8 = R * C / 8;
+  const int g = grid_for(n8);
+  auto go = [&](auto k) {
+    hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)dy, (const bf16*)y, (const bf16*)x, mean, rstd, scale,
+                       (const float*)ws, (const float*)(ws + C), (bf16*)dx, (bf16*)dres, n8, C / 8, 1.f / (float)R);
+  };
+  if (dres)
+    relu ? go(bwd_dx_kernel<true, true>) : go(bwd_dx_kernel<true, false>);
+  else
+    relu ? go(bwd_dx_kernel<false, true>) : go(bwd_dx_kernel<false, false>);
+}

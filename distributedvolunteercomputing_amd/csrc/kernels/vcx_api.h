@@ -101,3 +101,12 @@ void vcx_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* o
 // bf16 dwte); dwpe (+)= per-position sums of dx over the batch (nullptr: no position table)
 void vcx_embed_bwd(const int64_t* idx, const void* dx, float* dwte_scratch, void* dwte, int accum_wte, void* dwpe,
                    int accum_wpe, int64_t R, int T, int C, int V, hipStream_t s);
+// batchnorm.hip: train-mode BatchNorm (+ residual) (+ ReLU), NHWC bf16 [R, C]
+bool vcx_bn_supported(int C);
+void vcx_bn_fwd_train(const void* x, const void* res, void* y, int64_t R, int C, const void* gamma, const void* beta,
+                      void* run_mean, void* run_var, int run_fp32, float eps, float momentum, float* ws, float* mean,
+                      float* rstd, float* scale, float* shift, int relu, hipStream_t s);
+void vcx_bn_apply(const void* x, const void* res, void* y, int64_t R, int C, const float* scale, const float* shift,
+                  int relu, hipStream_t s);
+void vcx_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* scale,
+                int64_t R, int C, float* ws, void* dx, void* dres, int relu, hipStream_t s);

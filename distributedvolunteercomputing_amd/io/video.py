@@ -163,25 +163,30 @@ class SyntheticSource(FrameSource):
 
 class NpySource(FrameSource):
     """Frames of a uint8 [N, H, W, 3] .npy file, memory-mapped: read_chunk() returns views into
-    the mapping (no copy here; the consumer's one copy goes straight into pinned memory)."""
+    the mapping (no copy here; the consumer's one copy goes straight into pinned memory). With
+    `total` the file is played in a loop until `total` frames (a long steady-state job from a
+    file that fits in RAM: spec ``<file>.npy@<total>``)."""
 
     chunked = True
 
-    def __init__(self, path):
+    def __init__(self, path, total: int | None = None):
         self.a = np.load(path, mmap_mode="r", allow_pickle=False)
         if self.a.ndim != 4 or self.a.shape[-1] != 3 or self.a.dtype != np.uint8:
             raise ValueError(f"{path}: expected uint8 [N,H,W,3], got {self.a.dtype} {self.a.shape}")
+        self.total = len(self.a) if total is None else int(total)
         self.i = 0
 
     def read(self):
-        if self.i >= len(self.a):
+        if self.i >= self.total:
             return False, None
-        f = np.ascontiguousarray(self.a[self.i])
+        f = np.ascontiguousarray(self.a[self.i % len(self.a)])
         self.i += 1
         return True, f
 
     def read_chunk(self, n: int):
-        v = self.a[self.i : self.i + n]
+        j = self.i % len(self.a)
+        k = min(n, len(self.a) - j, self.total - self.i)  # a view never wraps around the file's end
+        v = self.a[j : j + max(k, 0)]
         self.i += len(v)
         return v
 
@@ -255,6 +260,9 @@ def open_source(spec: str) -> FrameSource:
         if len(parts) > 2:
             w, h = (int(v) for v in parts[2].lower().split("x"))
         return SyntheticSource(n, w, h)
+    if "@" in spec and spec.rsplit("@", 1)[0].endswith(".npy"):  # <file>.npy@<total>: looped
+        f, total = spec.rsplit("@", 1)
+        return NpySource(Path(f), int(total))
     p = Path(spec)
     if p.is_dir():
         return ImageDirSource(p)

@@ -5,7 +5,9 @@ Channels-last bf16. The 1x1 convolutions (about 70 % of the FLOPs) are plain GEM
 view -- [N*H*W, Cin] x [Cout, Cin]^T -- and run through the framework's linear layer (library
 GEMMs picked per shape, split-M weight gradients summed straight into the flat gradient buffer);
 stride-2 ones subsample the NHWC view first. The 3x3 / 7x7 convolutions go through MIOpen's NHWC
-kernels. BatchNorm statistics are buffers that the trainers average at every synchronisation.
+kernels. Train-mode BatchNorm runs fused with its ReLU and the residual add (ops/batchnorm.py,
+csrc/kernels/batchnorm.hip). BatchNorm statistics are buffers that the trainers average at every
+synchronisation.
 """
 from __future__ import annotations
 
@@ -14,6 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import config
+from ..ops.batchnorm import bn_act
 
 
 class Conv1x1(nn.Conv2d):
@@ -55,11 +58,11 @@ class Bottleneck(nn.Module):
             self.down = nn.Sequential(Conv1x1(cin, cout, stride=stride), nn.BatchNorm2d(cout))
 
     def forward(self, x):
-        idt = x if self.down is None else self.down(x)
-        y = F.relu(self.bn1(self.conv1(x)))
-        y = F.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        return F.relu(y + idt)
+        # BatchNorm + ReLU (+ the residual add) as fused HIP passes in train mode (ops/batchnorm.py)
+        idt = x if self.down is None else bn_act(self.down[0](x), self.down[1], relu=False)
+        y = bn_act(self.conv1(x), self.bn1)
+        y = bn_act(self.conv2(y), self.bn2)
+        return bn_act(self.conv3(y), self.bn3, residual=idt)
 
 
 class ResNet(nn.Module):
@@ -81,7 +84,7 @@ class ResNet(nn.Module):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
 
     def forward(self, x, y=None):
-        x = F.relu(self.bn(self.stem(x)))
+        x = bn_act(self.stem(x), self.bn)
         x = F.max_pool2d(x, 3, 2, 1)
         x = self.blocks(x)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -1,0 +1,62 @@
+"""Train-mode BatchNorm fused with the ReLU after it and the residual add before that ReLU, on
+channels-last bf16 activations (csrc/kernels/batchnorm.hip): y = relu(bn(x) [+ residual]).
+
+Forward: one statistics pass (read x), a per-channel finalize (running stats updated in place),
+one apply pass (read x [+ residual], write y). Backward: one reduction pass (read dy, y, x) and
+one input-gradient pass (read dy, y, x; write dx [and d residual]): the ReLU mask comes from y, so
+the pre-activation is never stored. On CPU, in fp32 or for unsupported channel counts the
+torch composition runs instead (the numerics oracle of tests/test_models_gpu.py).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ._lib import native, use_native
+
+
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    return t.permute(0, 2, 3, 1)  # a contiguous [N, H, W, C] view of channels-last storage
+
+
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, run_mean, run_var, eps, momentum, relu):
+        C = native()
+        xh = _nhwc(x)
+        rh = _nhwc(residual) if residual is not None else None
+        y, mean, rstd, scale = C.bn_fwd_train(xh, rh, weight, bias, run_mean, run_var, eps, momentum, relu)
+        ctx.save_for_backward(xh, y, mean, rstd, scale)
+        ctx.relu, ctx.has_res, ctx.pdtype = relu, residual is not None, weight.dtype
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xh, y, mean, rstd, scale = ctx.saved_tensors
+        dyh = _nhwc(dy)
+        if not dyh.is_contiguous():
+            dyh = dyh.contiguous()
+        dx, dres, dgamma, dbeta = native().bn_bwd(dyh, y, xh, mean, rstd, scale, ctx.relu, ctx.has_res)
+        dx = dx.permute(0, 3, 1, 2)
+        dres = dres.permute(0, 3, 1, 2) if ctx.has_res else None
+        return dx, dgamma.to(ctx.pdtype), dbeta.to(ctx.pdtype), dres, None, None, None, None, None
+
+
+def bn_act_ok(x: torch.Tensor, bn: torch.nn.BatchNorm2d) -> bool:
+    return (use_native(x) and bn.training and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and bn.affine and bn.weight.dtype == torch.bfloat16
+            and bn.track_running_stats and bn.momentum is not None and bool(native().bn_supported(x.shape[1])))
+
+
+def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, residual: torch.Tensor | None = None,
+           relu: bool = True) -> torch.Tensor:
+    """relu(bn(x) + residual) with `bn`'s parameters and running statistics (train mode)."""
+    if bn_act_ok(x, bn) and (residual is None or (residual.dtype == x.dtype and residual.shape == x.shape
+                                                  and residual.is_contiguous(memory_format=torch.channels_last))):
+        bn.num_batches_tracked.add_(1)
+        return _BNAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, bn.momentum,
+                            relu)
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y

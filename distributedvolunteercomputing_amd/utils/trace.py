@@ -89,3 +89,41 @@ class SpanTracer:
 
 
 NULL_TRACER = SpanTracer("null", enabled=False)
+
+
+class HostSpans:
+    """Host wall-clock busy time per named stage, summed per thread-safe stage name: where a
+    pipeline thread spends its time (the device spans above time GPU work; these time what the
+    host threads of a volunteer do: packing, sending, waiting for the engine, writing the sink).
+    Cost: two perf_counter calls and one locked dict update per span."""
+
+    def __init__(self):
+        import threading
+
+        self._lock = threading.Lock()
+        self.totals: dict[str, list] = {}  # name -> [count, total_s, max_s]
+
+    @contextlib.contextmanager
+    def span(self, name: str):
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            dt = time.perf_counter() - t0
+            with self._lock:
+                c = self.totals.get(name)
+                if c is None:
+                    self.totals[name] = [1, dt, dt]
+                else:
+                    c[0] += 1
+                    c[1] += dt
+                    c[2] = max(c[2], dt)
+
+    def snapshot(self) -> dict:
+        with self._lock:
+            return {k: {"n": v[0], "total_ms": round(v[1] * 1e3, 2), "mean_ms": round(v[1] / v[0] * 1e3, 3),
+                        "max_ms": round(v[2] * 1e3, 2)} for k, v in sorted(self.totals.items())}
+
+    def reset(self):
+        with self._lock:
+            self.totals.clear()

@@ -5,7 +5,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 timeout -k 10 120 python -u scripts/ssd_tail_ab.py > gpurun_out/b_ssd_tail_ab.log 2>&1 && \
 timeout -k 10 200 bash scripts/gpu_det_prof.sh > gpurun_out/b_detprof.log 2>&1 && \
 timeout -k 10 120 python -u scripts/detector_rel_err.py > gpurun_out/det_rel_err.log 2>&1 && \
-timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_models_gpu.py -k "resnet" > gpurun_out/rn50/tests.log 2>&1 && \
+timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_models_gpu.py -k "resnet or batchnorm" > gpurun_out/rn50/tests.log 2>&1 && \
 for m in conv gemm conv gemm; do VCX_RESNET_CONV1X1=$m timeout -k 10 200 python -u bench_configs.py --configs 3 --steps 10 >> gpurun_out/rn50/ab_conv1x1.log 2>&1 && echo "^ $m" >> gpurun_out/rn50/ab_conv1x1.log || exit 1; done && \
 ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/rn50/trace -o run -- \
     python3 $GRAFT_REPO_ROOT/bench_configs.py --configs 3 --steps 3 > $GRAFT_REPO_ROOT/gpurun_out/rn50/run.log 2>&1 ) && \

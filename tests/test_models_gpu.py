@@ -168,3 +168,43 @@ def test_resnet_conv1x1_gemm_matches_conv(gpu, stride):
     y32.backward(g)
     for a, r in ((y.float(), y32), (x.grad.float(), x32.grad), (conv.weight.grad.float(), w32.grad)):
         assert (a - r).norm() / r.norm() < 1e-2, float((a - r).norm() / r.norm())
+
+
+@pytest.mark.parametrize("C,res,relu", [(64, False, True), (256, True, True), (2048, True, True), (512, False, False)])
+def test_fused_batchnorm_act_vs_fp32(gpu, C, res, relu):
+    """Train-mode BatchNorm (+ residual) (+ ReLU) on channels-last bf16 (csrc/kernels/batchnorm.hip)
+    against torch in fp32: output, input / residual / gamma / beta gradients, running statistics."""
+    from distributedvolunteercomputing_amd.ops.batchnorm import bn_act
+
+    torch.manual_seed(C)
+    bn = torch.nn.BatchNorm2d(C).to(gpu)
+    torch.nn.init.uniform_(bn.weight, 0.5, 1.5)
+    torch.nn.init.uniform_(bn.bias, -0.5, 0.5)
+    bn32 = torch.nn.BatchNorm2d(C).to(gpu)
+    bn32.load_state_dict(bn.state_dict())
+    bn = bn.to(torch.bfloat16)
+    H = 7 if C >= 1024 else 14
+    x = (torch.randn(16, C, H, H, device=gpu) * 2 + 0.5).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    r = torch.randn_like(x) if res else None
+    x.requires_grad_()
+    if r is not None:
+        r.requires_grad_()
+    y = bn_act(x, bn, r, relu)
+    g = torch.randn_like(y)
+    y.backward(g)
+    x32 = x.detach().float().requires_grad_()
+    r32 = r.detach().float().requires_grad_() if res else None
+    y32 = bn32(x32)
+    if res:
+        y32 = y32 + r32
+    if relu:
+        y32 = torch.relu(y32)
+    y32.backward(g.float())
+    rel = lambda a, b: float((a.float() - b).norm() / (b.norm() + 1e-6))  # noqa: E731
+    assert rel(y, y32) < 1e-2
+    assert rel(x.grad, x32.grad) < 2e-2
+    if res:
+        assert rel(r.grad, r32.grad) < 1e-2
+    assert rel(bn.weight.grad, bn32.weight.grad) < 2e-2
+    assert rel(bn.bias.grad, bn32.bias.grad) < 2e-2
+    assert rel(bn.running_mean, bn32.running_mean) < 2e-2 and rel(bn.running_var, bn32.running_var) < 2e-2
