@@ -44,6 +44,8 @@ class RuntimeConfig:
     colour_native: bool = True  # VCX_COLOUR_NATIVE: video BGR<->YUV in the C++ runtime (False: numpy)
     resnet_conv1x1: str = "gemm"  # VCX_RESNET_CONV1X1: ResNet 1x1 convolutions as GEMMs on the NHWC view ("gemm")
     # or through the convolution library ("conv")
+    resnet_bn: str = "fused"  # VCX_RESNET_BN: ResNet train-mode BatchNorm (+ add) + ReLU as fused HIP passes ("fused")
+    # or the torch composition ("torch")
     # ---- distributed / control plane
     gloo_host: str = "127.0.0.1"  # VCX_GLOO_HOST: interface gloo peer groups bind to
     p2p_backend: str = ""  # VCX_P2P_BACKEND: pair-group backend of the p2p chunk plane ("" = auto)
@@ -61,6 +63,7 @@ _ENV = {
     "gemm": ("VCX_GEMM", str),
     "mlp": ("VCX_MLP", str),
     "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
+    "resnet_bn": ("VCX_RESNET_BN", str),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),
     "gemm_select": ("VCX_GEMM_SELECT", _bool),
     "wgrad_big_split_min_m": ("VCX_WGRAD_BIG_SPLIT_MIN_M", int),

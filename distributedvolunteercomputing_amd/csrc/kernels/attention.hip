@@ -192,181 +192,6 @@ attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
 #undef sV_
 }
 
-// Forward v2 (fwd_dma = 2): the v1 tile loop with its per-score VALU work trimmed (the forward is
-// bound by VALU issue, ~190 VALU instructions per 16 MFMAs per 64-key tile: profiles/r2_attention_isa_mix.txt):
-//   * Q is prescaled by the score scale (log2 domain) once per kernel, and the running row max
-//     enters the S^T chain as its INITIAL ACCUMULATOR (C operand = 16 registers holding -m), so
-//     P = exp2(S') needs no per-score fma;
-//   * m starts at the row's own diagonal score S[q, q] (computed in the prologue from Q and K row
-//     q): never above the true row max, so p(max) >= 1 and the sum never underflows, and the
-//     deferred-rescale test (T13, threshold 2^8) fires only when a later key scores > 8 above it;
-//     the rare rescale subtracts the shift from the tile's S' and rewrites the -m registers;
-//   * the K/V LDS-DMA source offsets go through buffer resources with tile-invariant per-lane parts.
-template <int WPE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
-attn_fwd2_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int B, int T, int H,
-                     float scale_log2, int staged_epi) {
-  __shared__ __attribute__((aligned(16))) bf16 sKV0[2][A_BK * AD];  // [K | V], swizzled (swz)
-  __shared__ __attribute__((aligned(16))) bf16 sKV1[2][A_BK * AD];
-#define sK_(b) ((b) ? &sKV1[0][0] : &sKV0[0][0])
-#define sV_(b) ((b) ? &sKV1[1][0] : &sKV0[1][0])
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
-  const int nqt = (T + A_BQ - 1) / A_BQ;
-  const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int qt = nqt - 1 - (lb % nqt);  // heaviest (last) query tiles first
-  const int bh = lb / nqt;
-  const int b = bh / H, hh = bh % H;
-  const int64_t tok = 3ll * H * AD;
-  const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
-  const int q0 = qt * A_BQ;
-  const int qw = q0 + w * 32;
-  const int q = qw + col;
-  const int qc = min(q, T - 1);
-  sx8 qf[4], kd[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = *(const sx8*)(base + (int64_t)qc * tok + 16 * s + 8 * h2);
-    kd[s] = *(const sx8*)(base + H * AD + (int64_t)qc * tok + 16 * s + 8 * h2);
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = prescale(qf[s], scale_log2);
-  // m = S'[q, q] (log2 domain, from the prescaled bf16 Q as the MFMAs see it)
-  float m;
-  {
-    float acc = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const short a = qf[s][j], k = kd[s][j];
-        acc = fmaf((float)*(const bf16*)&a, (float)*(const bf16*)&k, acc);
-      }
-    m = xhalf_sum(acc);
-  }
-  f32x16 nm16 = splat16(-m);
-  f32x16 o0 = {}, o1 = {};
-  float l = 0.f;
-  const int kend = min(T, q0 + A_BQ);
-  const int nkt = (kend + A_BK - 1) / A_BK;
-  // LDS-DMA through buffer resources: [K | V] columns of this (batch, head), byte offsets
-  // row * tok * 2 + chunk * 16 with the per-lane (row in tile, swizzled chunk) fixed per kernel
-  const __amdgpu_buffer_rsrc_t rK =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(base + H * AD), (short)0, (int)(T * tok * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rV =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(base + 2 * H * AD), (short)0, (int)(T * tok * 2), 0x00020000);
-  int prow[2], pchk[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int pp = (w * 2 + i) * 64 + lane;
-    const int r = pp >> 3, k = (r >> 1) & 7;
-    prow[i] = r;
-    pchk[i] = ((pp & 7) ^ (((k & 1) << 2) | (k >> 1))) * 16;
-  }
-  auto gload = [&](int kt, int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = min(kt * A_BK + prow[i], T - 1);
-      const int off = row * (int)(tok * 2) + pchk[i];
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rK, (__attribute__((address_space(3))) void*)(sK_(buf) + (w * 2 + i) * 512),
-                                               16, off, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rV, (__attribute__((address_space(3))) void*)(sV_(buf) + (w * 2 + i) * 512),
-                                               16, off, 0, 0, 0);
-    }
-  };
-  auto tile = [&](int kt, auto cur_c, auto mask_c) {
-    constexpr int cur = decltype(cur_c)::value;
-    constexpr bool MASK = decltype(mask_c)::value;
-    const int kb = kt * A_BK;
-    if (MASK && kb > qw + 31) return;
-    f32x16 s0 = mfma32(row_frag_swz(sK_(cur), col, 0, h2), qf[0], nm16);
-    f32x16 s1 = mfma32(row_frag_swz(sK_(cur), 32 + col, 0, h2), qf[0], nm16);
-#pragma unroll
-    for (int s = 1; s < 4; ++s) {
-      s0 = mfma32(row_frag_swz(sK_(cur), col, s, h2), qf[s], s0);
-      s1 = mfma32(row_frag_swz(sK_(cur), 32 + col, s, h2), qf[s], s1);
-    }
-    mfma_read_fence(s0, s1);
-    if (MASK) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
-        s0[r] = key > q ? -INFINITY : s0[r];
-        s1[r] = key + 32 > q ? -INFINITY : s1[r];
-      }
-    }
-    float mx0 = max3(s0[0], s0[1], s1[0]), mx1 = max3(s1[1], s0[2], s1[2]);
-#pragma unroll
-    for (int r = 3; r < 15; r += 2) {
-      mx0 = max3(mx0, s0[r], s1[r]);
-      mx1 = max3(mx1, s0[r + 1], s1[r + 1]);
-    }
-    const float mx = xhalf_max(max3(mx0, mx1, fmaxf(s0[15], s1[15])));  // S' = S - m: relative
-    if (!__all(mx <= 8.f)) {  // deferred rescale (T13): only a key > 2^8 above the running max
-      const float d = fmaxf(mx, 0.f);
-      const float alpha = __builtin_amdgcn_exp2f(-d);
-      l *= alpha;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        o0[r] *= alpha;
-        o1[r] *= alpha;
-        s0[r] -= d;
-        s1[r] -= d;
-      }
-      m += d;
-      nm16 = splat16(-m);
-    }
-    float ps0 = 0.f, ps1 = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p0 = __builtin_amdgcn_exp2f(s0[r]);
-      const float p1 = __builtin_amdgcn_exp2f(s1[r]);
-      s0[r] = p0;
-      s1[r] = p1;
-      ps0 += p0;
-      ps1 += p1;
-    }
-    l += xhalf_sum(ps0 + ps1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const f32x16& sp = (s < 2) ? s0 : s1;
-      sx8 pb;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pb[j] = bf16_bits(sp[8 * (s & 1) + j]);
-      o0 = mfma32(vt_frag_swz(sV_(cur), (s >> 1) * 32, 0, s & 1, lane), pb, o0);
-      o1 = mfma32(vt_frag_swz(sV_(cur), (s >> 1) * 32, 1, s & 1, lane), pb, o1);
-    }
-  };
-  gload(0, 0);
-  __syncthreads();
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // every prologue load retired (see the v1 kernel)
-  __syncthreads();
-  const int kdiag = q0 / A_BK;
-  auto step = [&](int kt, auto cur_c, auto mask_c) {
-    constexpr int cur = decltype(cur_c)::value;
-    if (kt + 1 < nkt) gload(kt + 1, cur ^ 1);
-    tile(kt, cur_c, mask_c);
-    __syncthreads();
-  };
-  int kt = 0;
-  for (; kt + 1 < kdiag; kt += 2) {
-    step(kt, I0{}, std::false_type{});
-    step(kt + 1, I1{}, std::false_type{});
-  }
-  if (kt < kdiag) step(kt++, I0{}, std::false_type{});
-  for (; kt < nkt; ++kt) {
-    if (kt & 1)
-      step(kt, I1{}, std::true_type{});
-    else
-      step(kt, I0{}, std::true_type{});
-  }
-  const float inv = 1.f / l;
-  store_acc_tile(o0, o1, inv, out + ((int64_t)b * T + qw) * H * AD + hh * AD, (int64_t)H * AD, T - qw,
-                 &sKV0[0][0] + w * 32 * AD, staged_epi, lane);
-  if (q < T && h2 == 0) lse[((int64_t)b * H + hh) * T + q] = m + __log2f(l);
-#undef sK_
-#undef sV_
-}
-
 // ============================================================================ backward
 // dQ (query-parallel; same tiling as the forward): per 32-key sub-tile
 //   S^T = K Q^T, P^T = exp2(S^T c - lse), dP^T = V dO^T, dS^T = P^T (dP^T - delta),
@@ -747,7 +572,7 @@ static int g_stage_epi = 1;
 
 void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma, int stage_epi) {
   if (fwd_wpe == 2 || fwd_wpe == 3) g_fwd_wpe = fwd_wpe;
-  if (fwd_dma >= 0 && fwd_dma <= 2) g_fwd_dma = fwd_dma;  // 2: the v2 kernel (attn_fwd2_d64_kernel)
+  if (fwd_dma == 0 || fwd_dma == 1) g_fwd_dma = fwd_dma;
   if (bwd_dma >= 0 && bwd_dma <= 3) g_bwd_dma = bwd_dma;
   if (stage_epi == 0 || stage_epi == 1) g_stage_epi = stage_epi;
 }
@@ -783,14 +608,7 @@ void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int 
 #define VCX_FWD(W, D)                                                                                      \
   hipLaunchKernelGGL((attn_fwd_d64_kernel<W, D>), g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H, \
                      scale * LOG2E, g_stage_epi)
-  if (g_fwd_dma == 2) {
-    if (g_fwd_wpe == 2)
-      hipLaunchKernelGGL((attn_fwd2_d64_kernel<2>), g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H,
-                         scale * LOG2E, g_stage_epi);
-    else
-      hipLaunchKernelGGL((attn_fwd2_d64_kernel<3>), g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H,
-                         scale * LOG2E, g_stage_epi);
-  } else if (g_fwd_dma) {
+  if (g_fwd_dma) {
     if (g_fwd_wpe == 2) VCX_FWD(2, true); else VCX_FWD(3, true);
   } else {
     if (g_fwd_wpe == 2) VCX_FWD(2, false); else VCX_FWD(3, false);

@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from .. import config
 from ._lib import native, use_native
 
 
@@ -43,7 +44,7 @@ class _BNAct(torch.autograd.Function):
 
 
 def bn_act_ok(x: torch.Tensor, bn: torch.nn.BatchNorm2d) -> bool:
-    return (use_native(x) and bn.training and x.dtype == torch.bfloat16 and x.dim() == 4
+    return (config.get().resnet_bn == "fused" and use_native(x) and bn.training and x.dtype == torch.bfloat16 and x.dim() == 4
             and x.is_contiguous(memory_format=torch.channels_last) and bn.affine and bn.weight.dtype == torch.bfloat16
             and bn.track_running_stats and bn.momentum is not None and bool(native().bn_supported(x.shape[1])))
 
