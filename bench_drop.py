@@ -205,7 +205,8 @@ def joiner_loop(a, tr, mem, store, cfg, device, cuda):
     if cuda:
         torch.cuda.synchronize()
     with open(os.path.join(a.out, f"joiner{a.peer}.json"), "w") as f:
-        json.dump({"peer": a.peer, "admit_ms": admit_ms, "steps": n, "gen": mem.gen, "events": mem.events}, f)
+        json.dump({"peer": a.peer, "admit_ms": admit_ms, "admit_stages": getattr(tr, "admit_stages", None), "steps": n,
+                   "gen": mem.gen, "events": mem.events}, f)
     mem.leave()
     return 0
 
@@ -386,16 +387,19 @@ def launcher(a):
     if a.rejoin:
         rj = next((s for s in steps if regroup is not None and s >= regroup and tl[s]["members"] == a.peers), None)
         back = [tl[s]["ms"] for s in steps if rj is not None and s > rj]
-        adm = []
+        adm, adm_st = [], []
         for v in victims:
             fn = os.path.join(out, f"joiner{v}.json")
             if os.path.exists(fn):
                 with open(fn) as f:
-                    adm.append(json.load(f)["admit_ms"])
+                    jd = json.load(f)
+                adm.append(jd["admit_ms"])
+                adm_st.append(jd.get("admit_stages"))
         rec["metric"] = "step-time under peer drop and rejoin, local-SGD"
         rec["rejoin_step"] = rj
         rec["rejoin_sync_ms"] = round(tl[rj]["sync_ms"], 3) if rj is not None else None
         rec["joiner_admission_ms"] = [round(x, 1) for x in adm]
+        rec["joiner_admission_stages"] = adm_st  # connect / model broadcast / reduction / verdict + apply
         rec["ms_per_step_after_rejoin"] = round(mean(back), 3) if back else None
         rec["samples_per_s_after_rejoin"] = round(a.peers * a.batch / mean(back) * 1e3, 2) if back else None
     line = json.dumps(rec)

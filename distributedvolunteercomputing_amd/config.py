@@ -32,6 +32,7 @@ class RuntimeConfig:
     gemm: str = "lib"  # VCX_GEMM: "lib" (hipBLASLt/rocBLAS) or "vcx" (csrc/kernels/gemm.hip, opt-in: 0.74-0.84x lib)
     mlp: str = "fused"  # VCX_MLP: GPT-2 MLP fc (+bias+GELU) and fc2-dgrad (*gelu' + bias grad) on the persistent
     # hand-written GEMM's fused epilogues (csrc/kernels/gemm_ps.hip), other GEMMs on `gemm`; "lib": library + passes
+    dgrad_ps: bool = True  # VCX_DGRAD_PS: input gradients dX = dY W with K <= 2304 on gemm_ps (measured faster)
     gemm_wgrad: str = "lib"  # VCX_GEMM_WGRAD: weight gradients on "lib" (split-M batched GEMM) or "vcx" (gemm_tn)
     gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)
     wgrad_big_split_min_m: int = 16384  # VCX_WGRAD_BIG_SPLIT_MIN_M: rows above which weight grads split over K
@@ -62,6 +63,7 @@ class RuntimeConfig:
 _ENV = {
     "gemm": ("VCX_GEMM", str),
     "mlp": ("VCX_MLP", str),
+    "dgrad_ps": ("VCX_DGRAD_PS", _bool),
     "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
     "resnet_bn": ("VCX_RESNET_BN", str),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),

@@ -198,7 +198,8 @@ void ssd_tail(int64_t nchain, std::vector<int64_t> meta, std::vector<at::Tensor>
     TORCH_CHECK(kind >= 0 && kind <= 2 && x.dim() == 4 && w.dim() == 2 && b.numel() == w.size(0), "ssd_tail: layer ", l);
     const int64_t H = x.size(1), W = x.size(2), C = x.size(3), N = w.size(0), K = w.size(1);
     const int64_t Ho = kind == 1 ? (H - 1) / 2 + 1 : H, Wo = kind == 1 ? (W - 1) / 2 + 1 : W;
-    TORCH_CHECK(K % 64 == 0 && C % 8 == 0 && K == (kind == 1 ? 9 * C : C), "ssd_tail: layer ", l, " K/C");
+    TORCH_CHECK(K % 32 == 0 && C % 8 == 0 && (C & (C - 1)) == 0 && K == (kind == 1 ? 9 * C : C), "ssd_tail: layer ", l,
+                " K/C (C a power of two)");
     if (frames < 0) frames = x.size(0);
     TORCH_CHECK(x.size(0) == frames, "ssd_tail: every layer sees the same frames");
     const at::Tensor& y = outs[l];

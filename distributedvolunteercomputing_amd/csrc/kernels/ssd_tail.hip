@@ -13,10 +13,11 @@
 //   * role B, the two wide heads (sources conv11 19x19 and conv13 10x10, all frames as one GEMM
 //     each), split into 64 x 128 output tiles over the remaining workgroups.
 // One tile routine serves all: out[64 x 128] of act(A W^T + b), A either the rows of an NHWC tensor
-// (1x1 convolution) or gathered on the fly (3x3 stride 2 pad 1 implicit GEMM, 16-B taps); 4 waves
-// as 2 x 2, 32 x 64 per wave on v_mfma_f32_16x16x32_bf16; K in steps of 64 (two 32-deep LDS
-// slices, XOR-swizzled 64-B rows), register-staged TWO steps ahead (these k-loops are short and
-// L2-latency-bound: one step of MFMAs cannot cover a load round trip). Head outputs are written
+// (1x1 convolution) or gathered on the fly (3x3 stride 2 pad 1 implicit GEMM, 16-B taps); 8 waves
+// as 2 x 4, 32 x 32 per wave on v_mfma_f32_16x16x32_bf16 (two waves per SIMD hide each other's waits); K in steps of 128 (four 32-deep LDS
+// slices, XOR-swizzled 64-B rows), register-staged two steps ahead through three register sets
+// (these k-loops are short and L2/MALL-latency-bound: with 64-deep steps and one step of lookahead
+// the tail took 433 us per 100-frame chunk, profiles/r4_detector_chunk.txt). Head outputs are written
 // straight into the concatenated mbox_loc / mbox_conf buffers (Permute + Flatten + Concat as
 // address arithmetic, as the per-layer head GEMM does).
 #include "vcx_common.h"
@@ -26,7 +27,7 @@ namespace ssd_tail {
 
 typedef short sx8 __attribute__((ext_vector_type(8)));
 
-constexpr int TBM = 64, TBN = 128, SLK = 32, STEPK = 64, NTH = 256;
+constexpr int TBM = 64, TBN = 128, SLK = 32, STEPK = 128, NTH = 512;
 constexpr int MAXL = 16;
 
 // kind: 0 = 1x1 convolution (+bias, act) -> NHWC Y;  1 = 3x3 stride-2 pad-1 convolution -> NHWC Y;
@@ -52,45 +53,46 @@ struct Plan {
 __device__ __forceinline__ int gswz(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
 __device__ __forceinline__ int sidx(int row, int chunk) { return row * SLK + ((chunk ^ gswz(row)) << 3); }
 
-// LDS: 2 buffers x (A 64 x 64 + B 128 x 64) bf16 = 48 KB
+// LDS: 2 buffers x (A 64 x 128 + B 128 x 128) bf16 = 96 KB
 constexpr int A_ELEMS = TBM * STEPK, B_ELEMS = TBN * STEPK, BUF_ELEMS = A_ELEMS + B_ELEMS;
 
 // one 64 x 128 output tile of layer Lr for the image range starting at img0: rows m0 .. m0+63 of the
 // M rows (M = Ho * Wo for one frame in role A; imgs * Ho * Wo in role B), columns n0 .. n0+127
 __device__ void run_tile(bf16* smem, const Layer& Lr, int img0, int M, int m0, int n0) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid >> 2, wn = wid & 3;  // 8 waves as 2 (M) x 4 (N): 32 x 32 per wave
   const int K = Lr.K, N = Lr.N, C = Lr.C;
-  const int nk = K / STEPK;
   const bool conv3 = Lr.kind == 1;
   const int pix = Lr.Ho * Lr.Wo;
-  // this thread's 2 A rows and 4 B rows per step (fixed per tile): chunk e = tid + 256 i,
-  // row = e >> 3, k offset (e & 7) * 8
-  const int kc = (tid & 7) * 8;
-  int arow_img[2], arow_iy[2], arow_ix[2];
+  // staging: each step moves A 64 x 128 (1024 16-B chunks: 2 per thread) and B 128 x 128 (4 per
+  // thread); chunk e = tid + 512 i: row e >> 4, k offset (e & 15) * 8 (slice (e & 15) >> 2). Columns
+  // past K (a K that is not a multiple of 128, e.g. conv17_2's 576) load as zero.
+  const int kc = (tid & 15) * 8;
+  int arow_ok[2], arow_iy[2], arow_ix[2];
   const bf16* arow_ptr[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int gm = m0 + (tid >> 3) + 32 * i;
-    arow_img[i] = gm < M ? 1 : 0;
-    const int im = gm / pix, p = gm - im * pix, oy = p / Lr.Wo, ox = p - oy * Lr.Wo;
+    const int gm = m0 + (tid >> 4) + 32 * i;
+    arow_ok[i] = gm < M ? 1 : 0;
+    const int g2 = gm < M ? gm : 0;
+    const int im = g2 / pix, p = g2 - im * pix, oy = p / Lr.Wo, ox = p - oy * Lr.Wo;
     arow_iy[i] = oy * 2 - 1;
     arow_ix[i] = ox * 2 - 1;
     // 1x1: the input row (same pixel grid); 3x3: the image base
-    arow_ptr[i] = conv3 ? Lr.X + (size_t)(img0 + im) * Lr.H * Lr.W * C
-                        : Lr.X + ((size_t)img0 * pix + (gm < M ? gm : 0)) * C;
+    arow_ptr[i] = conv3 ? Lr.X + (size_t)(img0 + im) * Lr.H * Lr.W * C : Lr.X + ((size_t)img0 * pix + g2) * C;
   }
+  const int cshift = 31 - __builtin_clz(C);  // C is a power of two (host check)
   auto loadA = [&](int i, int k) -> sx8 {
-    if (!arow_img[i]) return sx8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (!arow_ok[i] || k >= K) return sx8{0, 0, 0, 0, 0, 0, 0, 0};
     if (!conv3) return *(const sx8*)(arow_ptr[i] + k);
-    const int tap = k / C, c = k - tap * C, ky = tap / 3, kx = tap - ky * 3;
+    const int tap = k >> cshift, c = k & (C - 1), ky = tap / 3, kx = tap - ky * 3;
     const int iy = arow_iy[i] + ky, ix = arow_ix[i] + kx;
     if (iy < 0 || iy >= Lr.H || ix < 0 || ix >= Lr.W) return sx8{0, 0, 0, 0, 0, 0, 0, 0};
     return *(const sx8*)(arow_ptr[i] + (iy * Lr.W + ix) * C + c);
   };
   auto loadB = [&](int i, int k) -> sx8 {
-    const int gn = n0 + (tid >> 3) + 32 * i;
-    return gn < N ? *(const sx8*)(Lr.Wt + (size_t)gn * K + k) : sx8{0, 0, 0, 0, 0, 0, 0, 0};
+    const int gn = n0 + (tid >> 4) + 32 * i;
+    return gn < N && k < K ? *(const sx8*)(Lr.Wt + (size_t)gn * K + k) : sx8{0, 0, 0, 0, 0, 0, 0, 0};
   };
   struct Regs {
     sx8 a[2], b[4];
@@ -102,60 +104,69 @@ __device__ void run_tile(bf16* smem, const Layer& Lr, int img0, int M, int m0, i
 #pragma unroll
     for (int i = 0; i < 4; ++i) r.b[i] = loadB(i, k);
   };
-  // the thread's 16-B chunk: slice kc / 32, chunk (kc % 32) / 8 of row (tid >> 3) + 32 i
   const int sl = kc >> 5, ch = (kc & 31) >> 3;
   auto sstore = [&](const Regs& r, int buf) {
     bf16* sA = smem + buf * BUF_ELEMS + sl * TBM * SLK;
     bf16* sB = smem + buf * BUF_ELEMS + A_ELEMS + sl * TBN * SLK;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *(sx8*)(sA + sidx((tid >> 3) + 32 * i, ch)) = r.a[i];
+    for (int i = 0; i < 2; ++i) *(sx8*)(sA + sidx((tid >> 4) + 32 * i, ch)) = r.a[i];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *(sx8*)(sB + sidx((tid >> 3) + 32 * i, ch)) = r.b[i];
+    for (int i = 0; i < 4; ++i) *(sx8*)(sB + sidx((tid >> 4) + 32 * i, ch)) = r.b[i];
   };
-  f32x4 acc[2][4];
+  f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fc = lane >> 4;
   auto compute = [&](int buf) {
 #pragma unroll
     for (int s = 0; s < STEPK / SLK; ++s) {
       const bf16* sA = smem + buf * BUF_ELEMS + s * TBM * SLK;
       const bf16* sB = smem + buf * BUF_ELEMS + A_ELEMS + s * TBN * SLK;
-      sx8 af[2], bfr[4];
+      sx8 af[2], bfr[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) af[i] = *(const sx8*)(sA + sidx(wm * 32 + i * 16 + fr, fc));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = *(const sx8*)(sB + sidx(wn * 64 + j * 16 + fr, fc));
+      for (int j = 0; j < 2; ++j) bfr[j] = *(const sx8*)(sB + sidx(wn * 32 + j * 16 + fr, fc));
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   };
-  // two register sets, two steps ahead: set (k & 1) is reloaded with step k + 2 as soon as its
-  // step-k data sits in LDS (stored during step k - 1)
-  Regs r0, r1;
+  // three register sets, loads issued two steps ahead of their LDS store (these k-loops are short
+  // and L2/MALL-latency-bound); two LDS buffers. Step k: load step k + 2 into set (k + 2) % 3 (its
+  // step k - 1 data went to LDS during step k - 2), compute buffer k % 2, store set (k + 1) % 3 into
+  // buffer (k + 1) % 2 (last read by step k - 1, before the previous barrier), barrier.
+  const int nk = (K + STEPK - 1) / STEPK;
+  Regs r0, r1, r2;
   gload(r0, 0);
   if (nk > 1) gload(r1, 1);
   sstore(r0, 0);
   __syncthreads();
-  for (int k = 0; k < nk; k += 2) {
-    if (k + 2 < nk) gload(r0, k + 2);
-    compute(0);
-    if (k + 1 < nk) sstore(r1, 1);
-    __syncthreads();
-    if (k + 1 >= nk) break;
-    if (k + 3 < nk) gload(r1, k + 3);
-    compute(1);
-    if (k + 2 < nk) sstore(r0, 0);
-    __syncthreads();
+#define VCX_TAIL_STEP(KK, RL, RS, BC, BS)            \
+  {                                                  \
+    const int k_ = (KK);                             \
+    if (k_ >= nk) break;                             \
+    if (k_ + 2 < nk) gload(RL, k_ + 2);              \
+    compute(BC);                                     \
+    if (k_ + 1 < nk) sstore(RS, BS);                 \
+    __syncthreads();                                 \
   }
+  for (int k = 0; k < nk; k += 6) {
+    VCX_TAIL_STEP(k + 0, r2, r1, 0, 1)
+    VCX_TAIL_STEP(k + 1, r0, r2, 1, 0)
+    VCX_TAIL_STEP(k + 2, r1, r0, 0, 1)
+    VCX_TAIL_STEP(k + 3, r2, r1, 1, 0)
+    VCX_TAIL_STEP(k + 4, r0, r2, 0, 1)
+    VCX_TAIL_STEP(k + 5, r1, r0, 1, 0)
+  }
+#undef VCX_TAIL_STEP
   // epilogue: lane holds 4 consecutive columns of one row per (i, j)
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int gn = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+  for (int j = 0; j < 2; ++j) {
+    const int gn = n0 + wn * 32 + j * 16 + 4 * (lane >> 4);
     float bv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) bv[r] = gn + r < N ? Lr.b[gn + r] : 0.f;
@@ -262,7 +273,7 @@ bool vcx_ssd_tail(int nchain, int nlayers, int frames, const long long* ints, co
     L.b = (const float*)ptrs[5 * l + 2];
     L.Y = (bf16*)ptrs[5 * l + 3];
     L.Y2 = (bf16*)ptrs[5 * l + 4];
-    if (L.K % STEPK || L.C % 8 || (L.kind == 1 ? L.K != 9 * L.C : L.K != L.C)) return false;
+    if (L.K % 32 || L.C % 8 || (L.C & (L.C - 1)) || (L.kind == 1 ? L.K != 9 * L.C : L.K != L.C)) return false;
     if (L.kind == 2 && (L.split <= 0 || L.split >= L.N)) return false;
     if (l >= nchain) {
       tiles += ((frames * L.Ho * L.Wo + TBM - 1) / TBM) * ((L.N + TBN - 1) / TBN);

@@ -10,16 +10,18 @@ The S partial products are summed in fp32 by a HIP kernel directly INTO the flat
 buffer (``p.grad`` is a view of it, see parallel/flat_params.py), so no separate autograd
 accumulation pass runs either.
 
-With ``VCX_GEMM=vcx`` the forward and input-gradient GEMMs run the hand-written MFMA GEMM of
-csrc/kernels/gemm.hip (``gemm_nt``: 256x256 tiles, LDS-DMA ring, bias / bias+GELU / DGELU
-epilogues) whenever the shape tiles (M, N multiples of 256, K of 64, K >= 128); the input
-gradient dX = dY W runs as gemm_nt(dY, W^T) with W^T materialised by a HIP transpose (the
-weights are a few MB; activations are never transposed). Default: library GEMMs, which measure
-faster at the GPT-2 shapes (profiles/r2_gemm_nt.txt). Other shapes go through ``mm``: per GEMM
-shape, the first call outside graph capture can time the TunableOp-selected library GEMM
-(hipBLASLt / rocBLAS, utils/tuning.py) against hipBLASLt with this process's own per-shape
-algorithm search (csrc/bindings_lt.cpp). The bias gradient is a HIP column-sum kernel added into
-the flat gradient buffer.
+Hand-written GEMMs on the default path (round 4, profiles/r4_gemm_ps_bench.txt): the persistent
+``gemm_ps`` (csrc/kernels/gemm_ps.hip, nt output stores) runs the GPT-2 MLP's fc + bias + GELU and
+fc2 input gradient x gelu' + bias grad (``_MlpGelu``; 342 vs 422 us and 458 vs 541 us against the
+library GEMM + pass), and the input gradients of the qkv and attention-output projections (dX = dY
+W on W^T, 200 vs 207 us and 72 vs 77 us; ``dgrad_ps_ok``). The other forward GEMMs stay on the
+library, where gemm_ps measures 0.86-0.97x (its stores slow the next tile's main loop:
+profiles/r4_gemm_ps_diag.txt). ``VCX_GEMM=vcx`` switches the forward and input-gradient GEMMs to
+the older tiled ``gemm_nt`` (csrc/kernels/gemm.hip), slower at these shapes (profiles/r2_gemm_nt.txt).
+Other shapes go through ``mm``: per GEMM shape, the first call outside graph capture can time the
+TunableOp-selected library GEMM (hipBLASLt / rocBLAS, utils/tuning.py) against hipBLASLt with this
+process's own per-shape algorithm search (csrc/bindings_lt.cpp). The bias gradient is a HIP
+column-sum kernel added into the flat gradient buffer.
 """
 from __future__ import annotations
 
@@ -31,9 +33,6 @@ from .. import config
 from ._lib import grad_buffer, native, use_native
 
 MIN_ROWS_PER_SPLIT = 2048
-# The hand-written GEMM is opt-in (VCX_GEMM=vcx): at the GPT-2 bench shapes it runs at 0.74-0.84x
-# the library GEMM, and its fused bias+GELU / DGELU epilogues (not overlapped with MFMA work: one
-# workgroup per CU) cost more than the separate HIP passes they replace (profiles/r2_gemm_nt.txt)
 
 
 def set_gemm_backend(name: str):
@@ -251,6 +250,12 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if gemm_nt_ok(dy2.shape[0], K, N, dy2):
                 dx = gemm_nt(dy2, transpose_weight(w)).view(x.shape)
+            elif dgrad_ps_ok(dy2.shape[0], K, N, dy2):
+                # dX = dY W on the persistent hand-written GEMM (B = W^T, a few MB): faster than the
+                # library at the GPT-2 attention shapes (profiles/r4_gemm_ps_bench.txt: dg_qkv, dg_proj)
+                dx = torch.empty(dy2.shape[0], K, device=dy2.device, dtype=dy2.dtype)
+                native().gemm_ps(dy2, transpose_weight(w), dx)
+                dx = dx.view(x.shape)
             else:
                 dx = mm(dy2, w).view(x.shape)
         want_w = bool(ctx.needs_input_grad[1])
@@ -290,6 +295,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
 
 
 # ---------------------------------------------------------------- fused GPT-2 MLP
+def dgrad_ps_ok(M: int, N: int, K: int, t) -> bool:
+    """Input gradient dX[M, N] = dY[M, K] W[K, N] on gemm_ps: where it measured faster than the
+    library (K <= 2304: the qkv and attention-output projections; at K = 3072 it is 3 % slower)."""
+    return (config.get().dgrad_ps and K <= 2304 and use_native(t) and t.dtype == torch.bfloat16
+            and t.is_contiguous() and bool(native().gemm_ps_supported(M, N, K, 0)))
+
+
 def gemm_ps_ok(M: int, N: int, K: int, epi: int, t) -> bool:
     """The persistent store-overlapped GEMM (csrc/kernels/gemm_ps.hip) takes this shape/epilogue."""
     return (config.get().mlp == "fused" and use_native(t) and t.dtype == torch.bfloat16
@@ -301,9 +313,9 @@ class _MlpGelu(torch.autograd.Function):
     forward  fc:  one GEMM writes pre = x W1^T + b1 AND act = gelu(pre) (no bias_gelu pass);
     backward fc2-dgrad: one GEMM writes dpre = (dy W2) * gelu'(pre) and reduces db1 = sum dpre
              in its epilogue (no bias_gelu_bwd pass, dact never hits HBM).
-    `ps`: those two GEMMs run gemm_ps (persistent, 4 of 8 shapes at or above the library with the
-    fused epilogue; profiles/r3_gemm_ps.txt) and the other MLP GEMMs the library; otherwise all four
-    run the tiled gemm_nt (VCX_GEMM=vcx)."""
+    `ps`: those two GEMMs run gemm_ps (persistent, nt stores; 0.81x and 0.85x the time of the library
+    GEMM + pass, profiles/r4_gemm_ps_bench.txt) and the other MLP GEMMs the library; otherwise all
+    four run the tiled gemm_nt (VCX_GEMM=vcx)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, ps):
