@@ -398,8 +398,16 @@ def launcher(a):
         rec["metric"] = "step-time under peer drop and rejoin, local-SGD"
         rec["rejoin_step"] = rj
         rec["rejoin_sync_ms"] = round(tl[rj]["sync_ms"], 3) if rj is not None else None
+        # joiner_admission_ms: the joiner's whole join_running_job (communicator connect, the wait for
+        # the members to finish their local steps, the admission round); joiner_admission_round_ms:
+        # the admission round alone (model broadcast + reduction + verdict/apply); rejoin_stall_ms:
+        # what the admission round cost the running members over a steady averaging round
         rec["joiner_admission_ms"] = [round(x, 1) for x in adm]
-        rec["joiner_admission_stages"] = adm_st  # connect / model broadcast / reduction / verdict + apply
+        rec["joiner_admission_round_ms"] = [round(s_["admission_round_ms"], 1) for s_ in adm_st
+                                            if s_ and "admission_round_ms" in s_]
+        rec["joiner_admission_stages"] = adm_st
+        rec["staged_admission"] = os.environ.get("VCX_ELASTIC_STAGE_JOINS", "1") not in ("0", "false", "no", "off")
+        rec["rejoin_stall_ms"] = round(tl[rj]["sync_ms"] - steady_sync, 3) if rj is not None else None
         rec["ms_per_step_after_rejoin"] = round(mean(back), 3) if back else None
         rec["samples_per_s_after_rejoin"] = round(a.peers * a.batch / mean(back) * 1e3, 2) if back else None
     line = json.dumps(rec)

@@ -52,6 +52,9 @@ class RuntimeConfig:
     p2p_backend: str = ""  # VCX_P2P_BACKEND: pair-group backend of the p2p chunk plane ("" = auto)
     elastic_debug: bool = False  # VCX_ELASTIC_DEBUG: trace membership decisions to stderr
     elastic_liveness: bool = True  # VCX_ELASTIC_LIVENESS: TCP liveness links (process death seen at once)
+    # VCX_ELASTIC_STAGE_JOINS: a joiner's generation is agreed one round early and its communicator
+    # built during the local steps (the admission round pays no communicator init)
+    elastic_stage_joins: bool = True
     store_port_train: int = 29611  # VCX_STORE_PORT (train CLI): rendezvous store port
     store_port_video: int = 29612  # VCX_STORE_PORT (video CLI): job-control store port
     # ---- observability
@@ -80,6 +83,7 @@ _ENV = {
     "p2p_backend": ("VCX_P2P_BACKEND", str),
     "elastic_debug": ("VCX_ELASTIC_DEBUG", _bool),
     "elastic_liveness": ("VCX_ELASTIC_LIVENESS", _bool),
+    "elastic_stage_joins": ("VCX_ELASTIC_STAGE_JOINS", _bool),
     "store_port_train": ("VCX_STORE_PORT", int),
     "store_port_video": ("VCX_STORE_PORT", int),
     "trace_dir": ("VCX_TRACE_DIR", str),

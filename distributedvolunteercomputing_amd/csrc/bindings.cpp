@@ -269,22 +269,6 @@ std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Te
   return {dx, dres, ws.narrow(0, C, C), ws.narrow(0, 0, C)};
 }
 
-// 4-wave one-wave-per-SIMD GEMM (gemm4.hip): c[M, N] = a[M, K] . b[N, K]^T
-void gemm4(at::Tensor a, at::Tensor b, at::Tensor c) {
-  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm4: 2-D cuda tensors");
-  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
-              "gemm4: bf16 operands");
-  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm4: K-contiguous rows");
-  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm4: shape mismatch");
-  TORCH_CHECK(vcx_gemm4_supported((int)M, (int)N, (int)K), "gemm4: needs M, N % 256 == 0, K % 64 == 0, K >= 128");
-  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm4: 16-B aligned rows");
-  for (const at::Tensor* t : {&a, &b, &c})
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm4: 16-B aligned base pointers");
-  vcx_gemm4(a.data_ptr(), b.data_ptr(), c.data_ptr(), (int)M, (int)N, (int)K, (int)a.stride(0), (int)b.stride(0),
-            (int)c.stride(0), cur_stream());
-}
-
 // Weight gradient out[M, N] (+)= a[K, M]^T . b[K, N] (token-major operands) on the hand-written
 // transposed-read MFMA kernel, split-K over the token axis with fp32 partials
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t splits) {
@@ -761,7 +745,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("reduce_bcast_bf16", &reduce_bcast_bf16);
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_supported_epi", &gemm_nt_supported_epi);
-  m.def("gemm4", &gemm4);
   m.def("gemm_ps_supported", &gemm_ps_supported);
   m.def("bn_supported", [](int64_t C) { return vcx_bn_supported((int)C); });
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"),

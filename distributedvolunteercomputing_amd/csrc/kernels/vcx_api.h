@@ -33,9 +33,6 @@ int vcx_gemm_ps_grid(int M, int N, int grid_cap, int nw);
 // per CU (256 x 128 tiles), the second half of the grid starting `stagger` x ~8k cycles late
 void vcx_gemm_ps(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N,
                  int K, int lda, int ldb, int ldc, int epi, int grid_cap, int nw, int stagger, hipStream_t s);
-// gemm4.hip: 4-wave one-wave-per-SIMD GEMM (main-loop study), C = A B^T
-bool vcx_gemm4_supported(int M, int N, int K);
-void vcx_gemm4(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, hipStream_t s);
 void vcx_transpose_bf16(const void* src, void* dst, int R, int Cc, hipStream_t s);
 void vcx_add_f32_into_bf16(const float* in, void* out, int n, int accumulate, hipStream_t s);
 void vcx_reduce_bcast_bf16(const void* in, void* out, void* mine, int P, int64_t n, hipStream_t s);

@@ -308,7 +308,8 @@ class SSDExecutor:
         of one launch. Applies when the run of pw / conv / head steps at the end of the plan has the
         MobileNet-SSD shape (1x1, or 3x3 stride 2 pad 1, ReLU, K % 64 == 0); VCX_SSD_TAIL=0 keeps the
         per-layer steps."""
-        if os.environ.get("VCX_SSD_TAIL", "1") == "0":
+        mode = os.environ.get("VCX_SSD_TAIL", "1")
+        if mode == "0":
             return plan
         kinds = [st[0] for st in plan]
         j = max((i for i, k in enumerate(kinds) if k in ("pw", "conv", "head")), default=-1)
@@ -342,18 +343,22 @@ class SSDExecutor:
             chain_tops.add(l.tops[0])
         if not chain:
             return plan
-        # every head: its source inside the chain (per-frame) or before it (wide, all frames at once)
-        wide = [st for st in plan[:i + 1] if st[0] == "head"]
+        # every head: its source inside the chain (per-frame) or before it (wide, all frames at once);
+        # mode "chain": the wide heads stay per-layer steps (side stream, split-K head kernel)
+        wide = [st for st in plan[:i + 1] if st[0] == "head" and mode != "chain"]
         for st in heads + wide:
             if st[2]["w"].shape[1] % 64:
                 return plan
         chain_heads = [st for st in heads if st[2]["src"] in chain_tops]
-        wide += [st for st in heads if st[2]["src"] not in chain_tops]
+        run_wide = [st for st in heads if st[2]["src"] not in chain_tops]  # e.g. the head on the tail's input
+        if mode != "chain":
+            wide += run_wide
+            run_wide = []
         order = []  # the chain in dependency order, each layer's heads right after it
         for st in chain:
             order.append(st)
             order += [h for h in chain_heads if h[2]["src"] == st[1].tops[0]]
-        keep = [st for st in plan[:i + 1] if st[0] != "head"]
+        keep = [st for st in plan[:i + 1] if st[0] != "head" or mode == "chain"] + run_wide
         return keep + [("tail", chain[0][1], dict(order=order, wide=wide))] + plan[j + 1:]
 
     def _fuse_dw_pw(self, plan):

@@ -25,7 +25,11 @@ Here every peer
   outside the next generation and rejoins transparently as a newcomer;
 * a new or returning peer registers under ``join/<seq>`` and is admitted at the next round's
   outcome; newcomers (and any member that has not yet completed a committed round since it
-  joined) receive the model inside the admission round;
+  joined) receive the model inside the admission round. Staged admission (default): when the
+  only change is joiners, the outcome is ``pre:<members>|<newcomers>|<joins>`` -- generation g+1
+  is agreed now, the current round still runs on g, every member starts building g+1's
+  communicator on a helper thread, and the group switches to g+1 at the NEXT round, whose
+  admission then pays only the model broadcast (the RCCL init ran during the local steps);
 * process death is seen at once, not after a lease: every peer listens on a TCP "liveness" port
   (published as ``live/<pid>``) and holds one connection to each other member's. Nothing is ever
   sent on them; when a peer process dies (SIGKILL, crash, OOM) its kernel closes its sockets and
@@ -293,6 +297,8 @@ class ElasticMembership:
         # blocking store waits (server-side wake-up) instead of sleep-polling on the fast paths; a
         # wait that runs out falls back to the polling scan, which owns lease/EOF detection
         self.bell_s = min(2.0, max(0.25, lease_s / 4))
+        self.stage_joins = config.get().elastic_stage_joins
+        self._staged = None  # (gen, members, newcomers, njoin, group) agreed, built in the background
         if backend == "nccl":
             # abortable (non-blocking) RCCL communicator init for every generation's group
             os.environ.setdefault("TORCH_NCCL_USE_COMM_NONBLOCKING", "1")
@@ -496,6 +502,7 @@ class ElasticMembership:
         self.store.set(f"{_P}leave/{self.pid}", str(self.gen))
         self.stop_heartbeat()
         self._drop_group()
+        self._drop_staged()
 
     # ------------------------------------------------------------------ rounds
     def sync_round(self):
@@ -503,6 +510,8 @@ class ElasticMembership:
         (group, changed, newcomers); if this peer was voted out it rejoins transparently."""
         if self._abort.is_set() or self.store.check([f"{_P}abort/{self.gen}"]):
             return self.recover()
+        if self._staged is not None:
+            return self._switch()
         self.round += 1
         self._collect(self.round - 2)
         return self._round(str(self.round), recovery=False)
@@ -693,7 +702,10 @@ class ElasticMembership:
             new_ids = [j for j in joiners if j not in arrived]
             members = sorted(set(survivors) | set(new_ids))
             newcomers = sorted(set([m for m in survivors if not arrived[m]] + new_ids))
-            decision = f"next:{_csv(members)}|{_csv(newcomers)}|{njoin}"
+            # only joiners, every member holds the model: stage the generation (see module docstring)
+            kind = "pre" if (self.stage_joins and not recovery and not dead and not left and new_ids
+                             and all(arrived.values())) else "next"
+            decision = f"{kind}:{_csv(members)}|{_csv(newcomers)}|{njoin}"
         self._rt["scan_ms"] = (time.time() - t_scan) * 1e3
         won = _s(self.store.compare_set(okey, "", decision))
         self.store.set(bell, "1")
@@ -706,9 +718,13 @@ class ElasticMembership:
         if v == "same":
             return self.group, False, []
         g = self.gen + 1
+        kind, body = v.split(":", 1)
         # every follower proposes the same record; the first write fixes generation g
-        rec = _s(self.store.compare_set(f"{_P}gen/{g}", "", v.split(":", 1)[1]))
+        rec = _s(self.store.compare_set(f"{_P}gen/{g}", "", body))
         members, newcomers, njoin = _parse_gen(rec)
+        if kind == "pre" and rec == body and self.pid in members:
+            self._stage(g, members, newcomers, njoin)
+            return self.group, False, []  # this round still runs on the current generation
         old = list(self.members)
         k = okey.rsplit("/", 1)[1]
         if self.pid not in members:
@@ -730,6 +746,57 @@ class ElasticMembership:
                             "adopt_ms": (t - t_dec) * 1e3})
         return self.group, True, newcomers
 
+    def _stage(self, g, members, newcomers, njoin):
+        """Generation g (the current members + joiners) is agreed: start building its communicator
+        on a helper thread, on a store client of its own; ``sync_round`` switches to it next round."""
+        try:
+            st = self._stores.base.clone()
+        except Exception:  # noqa: BLE001
+            st = self.store
+        grp = PeerGroup(st, members.index(self.pid), len(members), self.backend, generation=g, members=members,
+                        timeout_s=self.pg_timeout_s, device=self.device, watch=self)
+        grp.fault_hook = self.fault_hook
+        grp.start_connect()
+        self._staged = (g, list(members), list(newcomers), int(njoin), grp)
+        self.joins_seen = max(self.joins_seen, int(njoin))
+        self.events.append({"event": "staged", "gen": g, "members": list(members), "joined": list(newcomers),
+                            "t": time.time()})
+        if self._live is not None:
+            self._live.watch(members)  # liveness links to the joiners before their admission round
+        _dbg(self.pid, f"staged gen {g}: {members} (+{newcomers})")
+
+    def _switch(self):
+        """Move to the staged generation (its communicator has been building since the last round)."""
+        g, members, newcomers, njoin, _ = self._staged
+        old = list(self.members)
+        t_in = time.time()
+        self._adopt(g, members, newcomers, njoin)
+        t = time.time()
+        self.events.append({"event": "regroup", "gen": g, "members": members, "round": "staged",
+                            "dropped": sorted(set(old) - set(members)), "joined": newcomers, "t": t, "t_in": t_in,
+                            "bell_wait_ms": 0.0, "scan_ms": 0.0, "decide_ms": 0.0, "adopt_ms": (t - t_in) * 1e3})
+        return self.group, True, list(newcomers)
+
+    def _drop_staged(self):
+        st, self._staged = self._staged, None
+        if st is not None:
+            st[4].abort()
+
+    def wait_round_start(self, timeout_s: float | None = None):
+        """A newcomer, inside its admission guard: block until the continuing members have entered
+        this generation (they post ``go/<gen>`` when they adopt it). Lets the joiner time its
+        admission from the round's start; aborts like a collective if a member dies meanwhile."""
+        if not any(m not in self.newcomers for m in self.members):
+            return  # nobody holds a model: no admission transfer to wait for
+        key = f"{_P}go/{self.gen}"
+        t0 = time.time()
+        while not self.store.check([key]):
+            if self._abort.is_set():
+                raise PeerFailure(f"gen {self.gen}: aborted before the admission round ({self._abort_reason})")
+            if timeout_s is not None and time.time() - t0 > timeout_s:
+                raise PeerFailure(f"gen {self.gen}: no member entered the admission round in {timeout_s}s")
+            time.sleep(self.poll_s)
+
     def _drop_group(self):
         with self._lock:
             grp, self.group = self.group, None
@@ -750,13 +817,24 @@ class ElasticMembership:
         self.joins_seen = max(self.joins_seen, int(njoin))
         if self.pid in newcomers:
             self.has_model = False
-        grp = PeerGroup(self.store, members.index(self.pid), len(members), self.backend, generation=g,
-                        members=members, timeout_s=self.pg_timeout_s, device=self.device, watch=self)
-        grp.fault_hook = self.fault_hook
+        staged, self._staged = self._staged, None
+        if staged is not None and staged[0] == g and staged[1] == list(members):
+            grp = staged[4]  # its communicator is already building (or built)
+        else:
+            if staged is not None:
+                staged[4].abort()  # superseded (a recovery formed another generation)
+            grp = PeerGroup(self.store, members.index(self.pid), len(members), self.backend, generation=g,
+                            members=members, timeout_s=self.pg_timeout_s, device=self.device, watch=self)
+            grp.fault_hook = self.fault_hook
         with self._lock:
             self.group = grp
         if self._live is not None:
             self._live.watch(members)
+        if self.has_model:
+            try:  # a newcomer times its admission from here (wait_round_start)
+                self.store.set(f"{_P}go/{g}", "1")
+            except Exception:  # noqa: BLE001
+                pass
 
     def _hb(self, m) -> int:
         return int(self.store.add(f"{_P}hb/{m}", 0))

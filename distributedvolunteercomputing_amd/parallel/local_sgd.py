@@ -268,25 +268,29 @@ class LocalSGDTrainer:
             self.group = grp
             try:
                 # stage times of the admission (bench_drop.py reports them): communicator connect,
-                # the model broadcast, the round's reduction, verdict + apply
+                # the wait for the members to enter the admission round (staged admission: they
+                # finish their local steps first), then the round itself -- model broadcast,
+                # reduction, verdict + apply
                 t0 = time.perf_counter()
-                st = {}
                 with mem.guard():
                     dev_sync()
                     t1 = time.perf_counter()
+                    mem.wait_round_start()
+                    t2 = time.perf_counter()
                     adopted = self._admit_newcomers(newcomers)
                     dev_sync()
-                    t2 = time.perf_counter()
+                    t3 = time.perf_counter()
                     res = self._reduce(newcomers)
                     bufs = self.buffers.averaged(grp)
                     dev_sync()
-                    t3 = time.perf_counter()
+                    t4 = time.perf_counter()
                 self._adopt(adopted)
                 self._apply(res, bufs)
                 dev_sync()
-                t4 = time.perf_counter()
-                st = {"connect_ms": (t1 - t0) * 1e3, "broadcast_ms": (t2 - t1) * 1e3, "reduce_ms": (t3 - t2) * 1e3,
-                      "verdict_apply_ms": (t4 - t3) * 1e3,
+                t5 = time.perf_counter()
+                st = {"connect_ms": (t1 - t0) * 1e3, "wait_round_ms": (t2 - t1) * 1e3,
+                      "broadcast_ms": (t3 - t2) * 1e3, "reduce_ms": (t4 - t3) * 1e3,
+                      "verdict_apply_ms": (t5 - t4) * 1e3, "admission_round_ms": (t5 - t2) * 1e3,
                       "broadcast_bytes": int(self.anchor.numel() * 4 * (2 if self.outer_mom is not None else 1))}
                 self.admit_stages = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in st.items()}
                 return

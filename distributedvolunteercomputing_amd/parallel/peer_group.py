@@ -81,6 +81,8 @@ class PeerGroup:
         self.poll_s = 2e-4
         self._pending = None  # deferred gloo rendezvous (watched groups connect in connect())
         self._connected = False
+        self._bg = None  # (thread, result box) of a communicator build started by start_connect()
+        self.bg_build_ms = None  # how long that build ran (staged admission)
         timeout = _dt.timedelta(seconds=timeout_s)
         prefixed = dist.PrefixStore(f"vcx/pg/{generation}", store)
         self.pg = None
@@ -101,6 +103,8 @@ class PeerGroup:
         """Wrap torch.distributed's default process group (e.g. the torchrun world)."""
         self = cls.__new__(cls)
         self._pending = None
+        self._bg = None
+        self.bg_build_ms = None
         self._connected = True  # the default group is connected by init_process_group
         self.generation = 0
         self.size = dist.get_world_size()
@@ -121,7 +125,11 @@ class PeerGroup:
         right after adopting the generation, with the watchdog armed), instead of lazily inside
         the first collective. With ``TORCH_NCCL_USE_COMM_NONBLOCKING=1`` (set by the elastic
         membership) the init is non-blocking, so a member dying during it is aborted like any
-        collective. No-op for gloo (connected in the constructor)."""
+        collective. No-op for gloo (connected in the constructor). A build started earlier by
+        ``start_connect`` is joined here (abortable like the gloo rendezvous)."""
+        if self._bg is not None:
+            self._join_bg()
+            return
         if self._pending is not None:
             self._connect_gloo()
             return
@@ -135,6 +143,68 @@ class PeerGroup:
             # different unique ids and hang the next collective)
             self.pg.eager_connect_single_device(dev)
             self._connected = True
+
+    def start_connect(self):
+        """Start building this generation's communicator on a helper thread and return at once
+        (staged admission: the members of the current generation build the next one -- which adds
+        the joiners -- during their local steps, so the admission round itself pays no RCCL init).
+        Construct such a group on a store client of its own: a TCPStore client serialises the
+        requests of all its threads, and the bootstrap must not queue behind the training thread's
+        waits."""
+        if self._bg is not None or self._connected or self.size == 1:
+            return
+        if self._pending is not None:
+            args, self._pending = self._pending, None
+
+            def build(box):
+                box["pg"] = _gloo_pg(*args)
+        elif self.pg is not None and self.backend == "nccl" and self.device is not None \
+                and torch.device(self.device).type == "cuda":
+            pg, dev = self.pg, torch.device(self.device)
+
+            def build(box):
+                pg.eager_connect_single_device(dev)
+        else:
+            return
+        box = {}
+
+        def run():
+            t0 = time.perf_counter()
+            try:
+                build(box)
+            except Exception as e:  # noqa: BLE001
+                box["err"] = e
+            box["ms"] = (time.perf_counter() - t0) * 1e3
+
+        th = threading.Thread(target=run, name=f"vcx-pg{self.generation}-build", daemon=True)
+        th.start()
+        self._bg = (th, box)
+
+    def _join_bg(self):
+        th, box = self._bg
+        while th.is_alive():
+            if self.watch is not None and self.watch.tripped():
+                self._bg = None
+                if self.backend == "nccl":
+                    self.abort()
+                self.aborted = True
+                raise PeerFailure(f"gen {self.generation}: connect aborted ({self.watch.abort_reason()})")
+            th.join(0.005)
+        self._bg = None
+        self.bg_build_ms = box.get("ms")
+        if "err" in box:
+            if self.watch is not None:
+                self.watch.declare_abort(f"gen {self.generation} connect failed on peer {self.watch.pid}: {box['err']}")
+            self.aborted = True
+            raise PeerFailure(f"gen {self.generation}: connect failed: {box['err']}")
+        if "pg" in box:
+            self.pg = box["pg"]
+        self._connected = True
+        if self.aborted:  # the watchdog aborted us while the build was finishing
+            pg, self.pg = self.pg, None
+            if pg is not None and self.backend == "gloo":
+                _GRAVEYARD.append(pg)
+            raise PeerFailure(f"gen {self.generation}: aborted during connect")
 
     def _connect_gloo(self):
         args, self._pending = self._pending, None
@@ -212,7 +282,7 @@ class PeerGroup:
             raise PeerFailure(f"gen {self.generation}: {op} failed: {e}") from e
 
     def _check(self):
-        if self._pending is not None:
+        if self._pending is not None or self._bg is not None:
             self.connect()
         if self.aborted or self.pg is None and self.size > 1:
             raise PeerFailure(f"gen {self.generation}: group aborted or never connected")

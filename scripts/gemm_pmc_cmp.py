@@ -1,4 +1,4 @@
-"""The library GEMM, gemm_nt (8 waves) and gemm4 (4 waves, one per SIMD) at 4096^3 and the GPT-2
+"""The library GEMM and gemm_nt (8 waves) at 4096^3 and the GPT-2
 fc shape, a few calls each: the program profiled by scripts/pmc_gemm_cmp.sh."""
 import os
 import sys
@@ -17,5 +17,4 @@ for m, n, k in ((4096, 4096, 4096), (65536, 3072, 768)):
     for _ in range(3):
         F.linear(a, b)
         C.gemm_nt(a, b, c)
-        C.gemm4(a, b, c)
 torch.cuda.synchronize()

@@ -13,7 +13,7 @@ from distributedvolunteercomputing_amd.ops import vision as V  # noqa: E402
 
 dev = torch.device("cuda", 0)
 exs = {}
-for v in ("0", "1"):
+for v in ("0", "1", "chain"):
     os.environ["VCX_SSD_TAIL"] = v
     exs[v] = SSDExecutor(device=dev)
 torch.manual_seed(0)
@@ -36,6 +36,7 @@ for v, ts in res.items():
     print(f"VCX_SSD_TAIL={v}: network {sorted(ts)[len(ts) // 2]:.3f} ms per 100-frame chunk (rounds "
           f"{', '.join('%.3f' % t for t in ts)})", flush=True)
 # per-step split with events (the tail as one step)
-steps = exs["1"].step_times(blob, 10)
-tail = [s for s in steps if s[1] == "tail"]
-print("tail step:", tail, " sum of steps %.3f ms" % sum(s[2] for s in steps), flush=True)
+for v in ("1", "chain"):
+    steps = exs[v].step_times(blob, 10)
+    tail = [s for s in steps if s[1] == "tail"]
+    print(f"VCX_SSD_TAIL={v} tail step:", tail, " sum of steps %.3f ms" % sum(s[2] for s in steps), flush=True)

@@ -196,12 +196,13 @@ def test_executor_matches_caffe_reference(gpu):
         a = out[name].float().cpu().permute(0, 3, 1, 2)
         r = ref[name]
         rel = (a - r).norm() / (r.norm() + 1e-6)
-        assert rel < 0.05, (name, float(rel))
+        # bf16 activations, fp32 accumulation: measured <= 0.018 on every layer (scripts/detector_rel_err.py)
+        assert rel < 0.02, (name, float(rel))
     for name in ["mbox_loc", "mbox_conf"]:
         a = out[name].float().cpu()
         r = ref[name]
         rel = (a - r).norm() / (r.norm() + 1e-6)
-        assert rel < 0.05, (name, float(rel))
+        assert rel < 0.02, (name, float(rel))
     dets, cnt = out["detection_out"]
     assert dets.shape == (2, 100, 7) and cnt.shape == (2,)
     # detection_out values: the executor's DetectionOutput (fused softmax + decode + NMS kernel)
