@@ -287,10 +287,17 @@ def launcher(a):
     failed_rounds = 0
     detect, build, redo = [], [], []
     stages = {}  # regroup-round anatomy, max over survivors (where a slow one goes)
+    staged = []  # staged admission on the survivors: (bg build ms, connect wait ms, go wait ms)
     for r in survivors:
         with open(os.path.join(out, f"peer{r}.json")) as f:
             d = json.load(f)
         backend = d["backend"]
+        for e in d["events"]:
+            if e["event"] == "staged":
+                cn = [c for c in d["events"] if c["event"] == "connect" and c["gen"] == e["gen"]]
+                go = [c for c in d["events"] if c["event"] == "go" and c["gen"] == e["gen"]]
+                staged.append({"gen": e["gen"], "bg_build_ms": cn[0].get("bg_build_ms") if cn else None,
+                               "connect_wait_ms": cn[0]["ms"] if cn else 0.0, "go_wait_ms": go[0]["ms"] if go else None})
         failed_rounds = max(failed_rounds, d.get("failed_rounds", 0))
         tf = min(d.get("t_fault", {}).values(), default=None)
         if tf is not None:
@@ -407,6 +414,9 @@ def launcher(a):
                                             if s_ and "admission_round_ms" in s_]
         rec["joiner_admission_stages"] = adm_st
         rec["staged_admission"] = os.environ.get("VCX_ELASTIC_STAGE_JOINS", "1") not in ("0", "false", "no", "off")
+        # per survivor: how long its background communicator build ran, what was left of it to wait
+        # for at the switch, and the line-up wait before the admission round
+        rec["staged_survivors"] = staged
         rec["rejoin_stall_ms"] = round(tl[rj]["sync_ms"] - steady_sync, 3) if rj is not None else None
         rec["ms_per_step_after_rejoin"] = round(mean(back), 3) if back else None
         rec["samples_per_s_after_rejoin"] = round(a.peers * a.batch / mean(back) * 1e3, 2) if back else None

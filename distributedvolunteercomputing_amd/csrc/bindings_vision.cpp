@@ -174,61 +174,6 @@ void gemm_bias_heads(at::Tensor X, at::Tensor Wt, at::Tensor bias, at::Tensor lo
                            S > 1 ? splitk_counters(X) : nullptr, cur_stream());
 }
 
-// SSD tail in one launch (kernels/ssd_tail.hip). Per layer l: meta[8 l .. 8 l + 7] =
-// (kind, relu, split, head_loc_off, head_conf_off, unused...), tensors[3 l .. 3 l + 2] = (x, wt, b);
-// outs[l] = the NHWC output of chain layers (kind 0 / 1). Layers < nchain run per frame (x holds
-// every frame), the rest are wide heads over all frames. Heads write loc_all / conf_all at the
-// given per-image element offsets.
-void ssd_tail(int64_t nchain, std::vector<int64_t> meta, std::vector<at::Tensor> tensors, std::vector<at::Tensor> outs,
-              at::Tensor loc_all, at::Tensor conf_all) {
-  const int64_t L = (int64_t)outs.size();
-  TORCH_CHECK(L > 0 && L <= 16 && nchain >= 0 && nchain <= L && (int64_t)meta.size() == 8 * L &&
-                  (int64_t)tensors.size() == 3 * L, "ssd_tail: plan sizes");
-  CHK(loc_all, at::kBFloat16);
-  CHK(conf_all, at::kBFloat16);
-  std::vector<long long> ints(13 * L, 0);
-  std::vector<const void*> ptrs(5 * L, nullptr);
-  int64_t frames = -1;
-  for (int64_t l = 0; l < L; ++l) {
-    const int64_t kind = meta[8 * l], relu = meta[8 * l + 1], split = meta[8 * l + 2];
-    const at::Tensor &x = tensors[3 * l], &w = tensors[3 * l + 1], &b = tensors[3 * l + 2];
-    CHK(x, at::kBFloat16);
-    CHK(w, at::kBFloat16);
-    CHK(b, at::kFloat);
-    TORCH_CHECK(kind >= 0 && kind <= 2 && x.dim() == 4 && w.dim() == 2 && b.numel() == w.size(0), "ssd_tail: layer ", l);
-    const int64_t H = x.size(1), W = x.size(2), C = x.size(3), N = w.size(0), K = w.size(1);
-    const int64_t Ho = kind == 1 ? (H - 1) / 2 + 1 : H, Wo = kind == 1 ? (W - 1) / 2 + 1 : W;
-    TORCH_CHECK(K % 32 == 0 && C % 8 == 0 && (C & (C - 1)) == 0 && K == (kind == 1 ? 9 * C : C), "ssd_tail: layer ", l,
-                " K/C (C a power of two)");
-    if (frames < 0) frames = x.size(0);
-    TORCH_CHECK(x.size(0) == frames, "ssd_tail: every layer sees the same frames");
-    const at::Tensor& y = outs[l];
-    if (kind == 2) {
-      const int64_t loff = meta[8 * l + 3], coff = meta[8 * l + 4];
-      TORCH_CHECK(split > 0 && split < N && loc_all.size(0) == frames && conf_all.size(0) == frames &&
-                      loff >= 0 && coff >= 0 && loff + Ho * Wo * split <= loc_all.size(1) &&
-                      coff + Ho * Wo * (N - split) <= conf_all.size(1), "ssd_tail: head ", l, " out of the concat buffers");
-      ptrs[5 * l + 3] = (const uint16_t*)loc_all.data_ptr() + loff;
-      ptrs[5 * l + 4] = (const uint16_t*)conf_all.data_ptr() + coff;
-      ints[13 * l + 10] = loc_all.size(1);
-      ints[13 * l + 11] = conf_all.size(1);
-    } else {
-      CHK(y, at::kBFloat16);
-      TORCH_CHECK(y.dim() == 4 && y.size(0) == frames && y.size(1) == Ho && y.size(2) == Wo && y.size(3) == N,
-                  "ssd_tail: output ", l);
-      TORCH_CHECK(l < nchain, "ssd_tail: wide layers are heads");
-      ptrs[5 * l + 3] = y.data_ptr();
-    }
-    long long* q = ints.data() + 13 * l;
-    q[0] = kind; q[1] = H; q[2] = W; q[3] = C; q[4] = Ho; q[5] = Wo; q[6] = N; q[7] = K; q[8] = relu; q[9] = split;
-    ptrs[5 * l + 0] = x.data_ptr();
-    ptrs[5 * l + 1] = w.data_ptr();
-    ptrs[5 * l + 2] = b.data_ptr();
-  }
-  TORCH_CHECK(vcx_ssd_tail((int)nchain, (int)L, (int)frames, ints.data(), ptrs.data(), cur_stream()),
-              "ssd_tail: plan rejected by the kernel");
-}
-
 // KxK convolution as an implicit GEMM (no im2col matrix): x NHWC bf16 [imgs, H, W, Cs] using
 // its first C channels (C % 8 == 0, or C == 4 == Cs), Wt [N, Kp] columns (ky, kx, c)
 at::Tensor conv_implicit(at::Tensor x, at::Tensor Wt, at::Tensor bias, int64_t C, int64_t KH, int64_t KW,
@@ -310,7 +255,6 @@ void vcx_register_vision(pybind11::module& m) {
   m.def("gemm_bias_heads", &gemm_bias_heads);
   m.def("dw_pw", &dw_pw);
   m.def("conv_implicit", &conv_implicit);
-  m.def("ssd_tail", &ssd_tail);
   m.def("ssd_detect", &ssd_detect);
   m.def("annotate", &annotate);
 }

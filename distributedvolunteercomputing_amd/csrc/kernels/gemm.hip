@@ -578,6 +578,30 @@ __global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16* __restr
   }
 }
 
+// the same with 16-B global loads and stores (R, Cc multiples of 8): each thread moves two 8-element
+// row pieces into a padded LDS tile, then gathers two 8-element column pieces of it
+__global__ void __launch_bounds__(256) transpose_bf16_v8_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
+                                                                int R, int Cc) {
+  __shared__ __attribute__((aligned(16))) bf16 t[64][72];  // 144-B rows: 16-B aligned, reads spread over banks
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = threadIdx.x + 256 * i, rr = e >> 3, cc = (e & 7) * 8;
+    if (r0 + rr < R && c0 + cc < Cc) *(bf16x8*)&t[rr][cc] = *(const bf16x8*)(src + (int64_t)(r0 + rr) * Cc + c0 + cc);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = threadIdx.x + 256 * i, cc = e >> 3, rr = (e & 7) * 8;
+    if (c0 + cc < Cc && r0 + rr < R) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = t[rr + j][cc];
+      *(bf16x8*)(dst + (int64_t)(c0 + cc) * R + r0 + rr) = v;
+    }
+  }
+}
+
 // out_bf16[i] += (bf16) in_f32[i] (the epilogue's fp32 column sums into a flat .grad slot)
 __global__ void __launch_bounds__(256) add_f32_into_bf16_kernel(const float* __restrict__ in, bf16* __restrict__ out,
                                                                 int n, int accumulate) {
@@ -657,6 +681,11 @@ void vcx_gemm_tn(const void* A, const void* B, float* Cpart, void* out, int M, i
 }
 
 void vcx_transpose_bf16(const void* src, void* dst, int R, int Cc, hipStream_t s) {
+  if (R % 8 == 0 && Cc % 8 == 0 && ((uintptr_t)src | (uintptr_t)dst) % 16 == 0) {
+    hipLaunchKernelGGL(gemm::transpose_bf16_v8_kernel, dim3((Cc + 63) / 64, (R + 63) / 64), dim3(256), 0, s,
+                       (const bf16*)src, (bf16*)dst, R, Cc);
+    return;
+  }
   hipLaunchKernelGGL(gemm::transpose_bf16_kernel, dim3((Cc + 63) / 64, (R + 63) / 64), dim3(256), 0, s,
                      (const bf16*)src, (bf16*)dst, R, Cc);
 }

@@ -29,5 +29,3 @@ void vcx_annotate(uint8_t* frames, int N, int h, int w, const float* dets, const
                   float thresh, uint32_t box_bgr, const uint8_t* name_mask, int nm_h, int nm_w, int nm_x, int nm_y,
                   uint32_t name_bgr, const uint8_t* lab_masks, int lm_n, int lm_h, int lm_w, int lm_x, int lm_y,
                   uint32_t lab_bgr, int* counts_out, hipStream_t s);
-// ssd_tail.hip: SSD extras + multibox heads in one launch (13 ints + 5 pointers per layer)
-bool vcx_ssd_tail(int nchain, int nlayers, int frames, const long long* ints, const void* const* ptrs, hipStream_t s);

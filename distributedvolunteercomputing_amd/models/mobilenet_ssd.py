@@ -279,7 +279,7 @@ class SSDExecutor:
             hs["concats"] = (a["concat"], c["concat"])
             hs["offs"] = (offs[(a["concat"], a["pos"])], offs[(c["concat"], c["pos"])])
             hs["rows"] = a["rows"]
-        return self._fuse_tail(self._heads_after_sources(self._fuse_dw_pw(plan)))
+        return self._heads_after_sources(self._fuse_dw_pw(plan))
 
     @staticmethod
     def _heads_after_sources(plan):
@@ -300,66 +300,6 @@ class SSDExecutor:
         if placed != len(heads):  # a source produced outside the plan's steps: keep the original order
             return plan
         return out
-
-    def _fuse_tail(self, plan):
-        """The SSD extras chain (prototxt 891-1146: 1x1 and 3x3 stride-2 convolutions after the last
-        backbone layer) and every multibox head become ONE `tail` step: csrc/kernels/ssd_tail.hip runs
-        each frame's chain in one workgroup and the two wide heads (conv11, conv13 sources) as tiles
-        of one launch. Applies when the run of pw / conv / head steps at the end of the plan has the
-        MobileNet-SSD shape (1x1, or 3x3 stride 2 pad 1, ReLU, K % 64 == 0); VCX_SSD_TAIL=0 keeps the
-        per-layer steps."""
-        mode = os.environ.get("VCX_SSD_TAIL", "1")
-        if mode == "0":
-            return plan
-        kinds = [st[0] for st in plan]
-        j = max((i for i, k in enumerate(kinds) if k in ("pw", "conv", "head")), default=-1)
-        if j < 0:
-            return plan
-        i = j
-        while i > 0 and kinds[i - 1] in ("pw", "conv", "head"):
-            i -= 1
-        run = plan[i:j + 1]
-        if not run or run[0][0] != "pw":
-            return plan
-        t0 = run[0][1].tops[0]  # the tail's input: the last backbone layer's output
-        chain, chain_tops, heads = [], set(), []
-        for st in run[1:]:
-            kind, l, p = st
-            if kind == "head":
-                heads.append(st)
-                continue
-            src = l.bottoms[0]
-            if src != t0 and src not in chain_tops:
-                return plan
-            w = p["w"]
-            if kind == "pw":
-                ok = w.shape[1] % 64 == 0 and p["relu"]
-            else:
-                ok = (p["k"] == 3 and p["stride"] == 2 and p["pad"] == 1 and p["relu"] and p["C"] == p["cin"]
-                      and p["cin"] % 8 == 0 and p["Kp"] == 9 * p["cin"] and p["Kp"] % 64 == 0)
-            if not ok:
-                return plan
-            chain.append(st)
-            chain_tops.add(l.tops[0])
-        if not chain:
-            return plan
-        # every head: its source inside the chain (per-frame) or before it (wide, all frames at once);
-        # mode "chain": the wide heads stay per-layer steps (side stream, split-K head kernel)
-        wide = [st for st in plan[:i + 1] if st[0] == "head" and mode != "chain"]
-        for st in heads + wide:
-            if st[2]["w"].shape[1] % 64:
-                return plan
-        chain_heads = [st for st in heads if st[2]["src"] in chain_tops]
-        run_wide = [st for st in heads if st[2]["src"] not in chain_tops]  # e.g. the head on the tail's input
-        if mode != "chain":
-            wide += run_wide
-            run_wide = []
-        order = []  # the chain in dependency order, each layer's heads right after it
-        for st in chain:
-            order.append(st)
-            order += [h for h in chain_heads if h[2]["src"] == st[1].tops[0]]
-        keep = [st for st in plan[:i + 1] if st[0] != "head" or mode == "chain"] + run_wide
-        return keep + [("tail", chain[0][1], dict(order=order, wide=wide))] + plan[j + 1:]
 
     def _fuse_dw_pw(self, plan):
         """Depthwise -> pointwise pairs (every MobileNet block, prototxt 42-106 and after) become one
@@ -473,30 +413,6 @@ class SSDExecutor:
                 with torch.cuda.stream(side) if side is not None else _nullctx():
                     ops.native().gemm_bias_heads(x.reshape(N * H * W, x.shape[-1]), p["w"], p["b"], la,
                                                  p["offs"][0], ca, p["offs"][1], p["split"], H * W)
-            elif kind == "tail":
-                # extras chain + all multibox heads in one launch (csrc/kernels/ssd_tail.hip)
-                metas, tens, outs = [], [], []
-                la_, ca_ = None, None
-                steps = p["order"] + p["wide"]
-                for k2, l2, p2 in steps:
-                    if k2 == "head":
-                        xs = t[p2["src"]]
-                        la_, ca_ = (concat_bufs[c] for c in p2["concats"])
-                        metas += [2, 0, p2["split"], p2["offs"][0], p2["offs"][1], 0, 0, 0]
-                        tens += [xs, p2["w"], p2["b"]]
-                        outs.append(torch.empty(0, device=blob.device, dtype=torch.bfloat16))
-                        continue
-                    xs = t[l2.bottoms[0]]
-                    Hs, Ws = hw[l2.bottoms[0]]
-                    Ho, Wo = (Hs, Ws) if k2 == "pw" else ((Hs - 1) // 2 + 1, (Ws - 1) // 2 + 1)
-                    Co = p2["w"].shape[0]
-                    y = torch.empty(N, Ho, Wo, Co, device=blob.device, dtype=torch.bfloat16)
-                    metas += [0 if k2 == "pw" else 1, 1, 0, 0, 0, 0, 0, 0]
-                    tens += [xs, p2["w"], p2["b"]]
-                    outs.append(y)
-                    top2 = l2.tops[0]
-                    t[top2], layout[top2], hw[top2], chans[top2] = y, "nhwc", (Ho, Wo), Co
-                ops.native().ssd_tail(len(p["order"]), metas, tens, outs, la_, ca_)
             elif kind == "concat_buf":
                 t[top], layout[top] = concat_bufs[p["index"]], "plain"
             elif kind == "conv":

@@ -298,6 +298,7 @@ class ElasticMembership:
         # wait that runs out falls back to the polling scan, which owns lease/EOF detection
         self.bell_s = min(2.0, max(0.25, lease_s / 4))
         self.stage_joins = config.get().elastic_stage_joins
+        self.last_go_wait_ms = 0.0
         self._staged = None  # (gen, members, newcomers, njoin, group) agreed, built in the background
         if backend == "nccl":
             # abortable (non-blocking) RCCL communicator init for every generation's group
@@ -490,6 +491,7 @@ class ElasticMembership:
                 members, newcomers, njoin = _parse_gen(_s(self.store.get(key)))
                 if self.pid in members and njoin >= seq:
                     self._adopt(g + 1, members, newcomers, njoin)
+                    self.group.needs_go = True  # line up with the continuing members (guard)
                     self.events.append({"event": "joined", "gen": self.gen, "members": members})
                     return self.group
                 g += 1
@@ -570,7 +572,11 @@ class ElasticMembership:
             grp.connect()
             if fresh:  # communicator build of a new generation (RCCL init / gloo full mesh)
                 self.events.append({"event": "connect", "gen": self.gen, "ms": (time.time() - t0) * 1e3,
-                                    "t": time.time()})
+                                    "t": time.time(), "bg_build_ms": getattr(grp, "bg_build_ms", None)})
+            if getattr(grp, "needs_go", False):
+                self.wait_round_start()
+                grp.needs_go = False
+                self.events.append({"event": "go", "gen": self.gen, "ms": self.last_go_wait_ms, "t": time.time()})
             _dbg(self.pid, f"guard {self.gen}/{tag}: body")
             yield
             _dbg(self.pid, f"guard {self.gen}/{tag}: commit")
@@ -756,6 +762,7 @@ class ElasticMembership:
         grp = PeerGroup(st, members.index(self.pid), len(members), self.backend, generation=g, members=members,
                         timeout_s=self.pg_timeout_s, device=self.device, watch=self)
         grp.fault_hook = self.fault_hook
+        grp.needs_go = True  # its first collective is not lined up by a communicator init (guard)
         grp.start_connect()
         self._staged = (g, list(members), list(newcomers), int(njoin), grp)
         self.joins_seen = max(self.joins_seen, int(njoin))
@@ -783,19 +790,26 @@ class ElasticMembership:
             st[4].abort()
 
     def wait_round_start(self, timeout_s: float | None = None):
-        """A newcomer, inside its admission guard: block until the continuing members have entered
-        this generation (they post ``go/<gen>`` when they adopt it). Lets the joiner time its
-        admission from the round's start; aborts like a collective if a member dies meanwhile."""
-        if not any(m not in self.newcomers for m in self.members):
-            return  # nobody holds a model: no admission transfer to wait for
-        key = f"{_P}go/{self.gen}"
+        """Inside the admission guard: block until EVERY continuing member has entered this
+        generation (each adds 1 to ``go/<gen>`` when it adopts it). A staged generation's
+        communicator was built rounds ago, so nothing else lines its members up before the first
+        collective -- and RCCL opens that collective's connections lazily: a peer that enters it
+        while another is still in its local steps has its connects refused until it gives up
+        (seen at 8 ranks). Aborts like a collective if a member dies meanwhile. Records the wait
+        in ``last_go_wait_ms``."""
+        n_cont = sum(1 for m in self.members if m not in self.newcomers)
         t0 = time.time()
-        while not self.store.check([key]):
+        self.last_go_wait_ms = 0.0
+        if n_cont == 0:
+            return  # nobody holds a model: no admission transfer to line up
+        key = f"{_P}go/{self.gen}"
+        while int(self.store.add(key, 0)) < n_cont:
             if self._abort.is_set():
                 raise PeerFailure(f"gen {self.gen}: aborted before the admission round ({self._abort_reason})")
             if timeout_s is not None and time.time() - t0 > timeout_s:
-                raise PeerFailure(f"gen {self.gen}: no member entered the admission round in {timeout_s}s")
+                raise PeerFailure(f"gen {self.gen}: the members did not all enter the admission round in {timeout_s}s")
             time.sleep(self.poll_s)
+        self.last_go_wait_ms = (time.time() - t0) * 1e3
 
     def _drop_group(self):
         with self._lock:
@@ -831,8 +845,8 @@ class ElasticMembership:
         if self._live is not None:
             self._live.watch(members)
         if self.has_model:
-            try:  # a newcomer times its admission from here (wait_round_start)
-                self.store.set(f"{_P}go/{g}", "1")
+            try:  # counted by wait_round_start
+                self.store.add(f"{_P}go/{g}", 1)
             except Exception:  # noqa: BLE001
                 pass
 

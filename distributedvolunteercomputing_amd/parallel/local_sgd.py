@@ -272,11 +272,10 @@ class LocalSGDTrainer:
                 # finish their local steps first), then the round itself -- model broadcast,
                 # reduction, verdict + apply
                 t0 = time.perf_counter()
-                with mem.guard():
+                with mem.guard():  # connect, then line up with the continuing members (wait_round_start)
                     dev_sync()
-                    t1 = time.perf_counter()
-                    mem.wait_round_start()
                     t2 = time.perf_counter()
+                    t1 = t2 - mem.last_go_wait_ms * 1e-3
                     adopted = self._admit_newcomers(newcomers)
                     dev_sync()
                     t3 = time.perf_counter()

@@ -83,6 +83,7 @@ class PeerGroup:
         self._connected = False
         self._bg = None  # (thread, result box) of a communicator build started by start_connect()
         self.bg_build_ms = None  # how long that build ran (staged admission)
+        self.needs_go = False  # first guarded collective waits for every continuing member (elastic)
         timeout = _dt.timedelta(seconds=timeout_s)
         prefixed = dist.PrefixStore(f"vcx/pg/{generation}", store)
         self.pg = None
@@ -105,6 +106,7 @@ class PeerGroup:
         self._pending = None
         self._bg = None
         self.bg_build_ms = None
+        self.needs_go = False
         self._connected = True  # the default group is connected by init_process_group
         self.generation = 0
         self.size = dist.get_world_size()

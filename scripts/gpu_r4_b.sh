@@ -14,7 +14,6 @@ PT="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
 step gemm_ps_tests 200 $PT tests/test_gemm_ps_gpu.py
 step gemm_ps_bench 200 python -u scripts/gemm_ps_bench.py
 step vision_tests 300 $PT tests/test_vision_gpu.py
-step ssd_tail_ab 120 python -u scripts/ssd_tail_ab.py
 step det_rel_err 120 python -u scripts/detector_rel_err.py
 step detprof 200 bash scripts/gpu_det_prof.sh
 step rn50_tests 240 $PT tests/test_models_gpu.py -k "resnet or batchnorm"

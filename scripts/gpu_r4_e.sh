@@ -11,6 +11,5 @@ step() {  # name, seconds, command...
 }
 PT="python -u -m pytest -q --timeout 120 --timeout-method thread"
 step vision_tests 300 $PT -x tests/test_vision_gpu.py
-step ssd_tail_ab 120 python -u scripts/ssd_tail_ab.py
 step detprof 200 bash scripts/gpu_det_prof.sh
 step rn50_tests 300 $PT -v tests/test_models_gpu.py -k "resnet or batchnorm"

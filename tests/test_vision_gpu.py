@@ -277,25 +277,3 @@ def test_conv_implicit_vs_fp32(gpu, N, H, C, cout, k, stride, pad):
     assert y.shape == r.shape
     rel = float((y.float() - r).norm() / r.norm())
     assert rel < 1e-2, rel
-
-
-def test_ssd_tail_fused_matches_per_layer(gpu, monkeypatch):
-    """The one-launch SSD tail (extras chain + every multibox head, csrc/kernels/ssd_tail.hip) against
-    the per-layer steps it replaces: every extras output and both concat buffers."""
-    monkeypatch.setenv("VCX_SSD_TAIL", "0")
-    ref_ex = SSDExecutor(device=gpu)
-    monkeypatch.setenv("VCX_SSD_TAIL", "1")
-    ex = SSDExecutor(device=gpu)
-    assert any(k == "tail" for k, _, _ in ex._plan) and not any(k == "tail" for k, _, _ in ref_ex._plan)
-    assert not any(k == "head" for k, _, _ in ex._plan)
-    torch.manual_seed(11)
-    for n in (3, 100):
-        frames = torch.randint(0, 256, (n, 225, 400, 3), dtype=torch.uint8, device=gpu)
-        blob = V.blob_from_frames(frames, 300)
-        a, r = ex.forward_blob(blob), ref_ex.forward_blob(blob)
-        for name in ["conv14_1", "conv14_2", "conv15_1", "conv15_2", "conv16_1", "conv16_2", "conv17_1", "conv17_2",
-                     "mbox_loc", "mbox_conf"]:
-            x, y = a[name].float(), r[name].float()
-            rel = float((x - y).norm() / (y.norm() + 1e-6))
-            assert rel < 5e-3, (n, name, rel)
-        assert torch.equal(a["detection_out"][1], r["detection_out"][1]) or n == 100
