@@ -65,6 +65,23 @@ def _is_placeholder(buf) -> bool:
     return flat.numel() >= n and torch.equal(flat[:n].cpu(), _PLACEHOLDER_TAG)
 
 
+class _Landing:
+    """A resized chunk still in flight on the requester's resize stream; ``wait()`` returns it."""
+
+    __slots__ = ("t", "ev", "host")
+
+    def __init__(self, t, ev, host=False):
+        self.t, self.ev, self.host = t, ev, host
+
+    @property
+    def shape(self):
+        return tuple(self.t.shape)
+
+    def wait(self):
+        self.ev.synchronize()
+        return self.t.numpy() if self.host else self.t
+
+
 def _host_tensor(a: np.ndarray) -> torch.Tensor:
     """A tensor view of a host chunk; read-only arrays (memory-mapped sources) are only ever read
     by the transfers, so torch's non-writable warning does not apply."""
@@ -133,15 +150,22 @@ class client:  # noqa: N801 (reference class name)
         self.job_times: list[float] = []
 
         self._pins: dict = {}  # pinned staging of the requester's pre-resize (by role)
-        self._h2d_done = None
+        self._in_done = [None, None]  # per pinned input buffer: the upload that last read it
+        self._in_ring = 0
+        self._rs_stream = None  # the requester's resize stream (its own: not the workers' engines')
         self.send_q: queue.Queue = queue.Queue(maxsize=self.max_buffer)
+        # relay plane: packed chunks wait here for the wire thread, so packing / resizing chunk k+1
+        # overlaps the uplink send of chunk k (measured serial: 9.6 + 5.2 ms per 100-frame 720p chunk,
+        # the requester's send thread was the whole job's bound, profiles/r4_video_job_spans.txt)
+        self.wire_q: queue.Queue = queue.Queue(maxsize=2)
+        self._out_ring = 0  # pinned result buffers rotate: a packed chunk may still be queued or on the wire
         self.work_q: queue.Queue = queue.Queue(maxsize=4)
         self.continue_requesting = False
         self.continue_procesing = True
         self.continue_sending = True
         self.continue_receiving = True
         self._threads = []
-        for fn, nm in ((self.worker, "worker"), (self.send_image_thread, "send"),
+        for fn, nm in ((self.worker, "worker"), (self.send_image_thread, "send"), (self._wire_thread, "wire"),
                        (self.recv_image_thread, "recv"), (self._heartbeat, "hb")):
             t = threading.Thread(target=fn, name=f"vcx-client-{nm}", daemon=True)
             t.start()
@@ -267,16 +291,7 @@ class client:  # noqa: N801 (reference class name)
                 else:
                     chunk = np.stack(frames) if block is None else np.ascontiguousarray(block)
             info = f"{self.my_ip}||request||{'-'.join(map(str, nums))}||{chunk.shape[1]}||{chunk.shape[2]}"
-            if self.plane is not None:  # p2p: the chunk stays here; the coordinator gets its metadata
-                key = next(self._keys)
-                with self._p2p_lock:
-                    self._outgoing[key] = chunk if isinstance(chunk, torch.Tensor) else _host_tensor(chunk)
-                ok = self.sender.send_image(info, _EMPTY, p2p=1, key=key, cshape=list(chunk.shape))
-            else:
-                with self.hspans.span("req_send"):
-                    ok = self.sender.send_image(info, chunk)
-            if not ok:
-                self.log("uplink send failed")
+            self.wire_q.put((info, chunk))  # in order: one wire thread
             self.metrics.incr("chunks_sent")
             frames.clear()
             nums.clear()
@@ -303,6 +318,33 @@ class client:  # noqa: N801 (reference class name)
             if len(frames) >= C:
                 flush()
 
+    def _wire_thread(self):
+        """Second stage of the requester's uplink, in chunk order: waits for a chunk's resize to land
+        (the send thread is already copying the next chunk into the other pinned buffer), then sends
+        it (relay plane) or parks it and sends its metadata (p2p plane)."""
+        while self.continue_sending:
+            try:
+                info, chunk = self.wire_q.get(timeout=0.2)
+            except queue.Empty:
+                continue
+            if isinstance(chunk, _Landing):
+                with self.hspans.span("req_wait_resize"):
+                    chunk = chunk.wait()
+            if self.plane is not None:  # p2p: the chunk stays here; the coordinator gets its metadata
+                key = next(self._keys)
+                held = chunk if isinstance(chunk, torch.Tensor) else _host_tensor(chunk)
+                if held.device.type == "cpu" and self._pins and any(
+                        held.data_ptr() == b.data_ptr() for b in self._pins.values()):
+                    held = held.clone()  # a pinned ring buffer: the next chunks reuse it
+                with self._p2p_lock:
+                    self._outgoing[key] = held
+                ok = self.sender.send_image(info, _EMPTY, p2p=1, key=key, cshape=list(held.shape))
+            else:
+                with self.hspans.span("req_send"):
+                    ok = self.sender.send_image(info, chunk)
+            if not ok:
+                self.log("uplink send failed")
+
     def _pinned(self, name, shape):
         b = self._pins.get(name)
         n = int(np.prod(shape))
@@ -316,25 +358,35 @@ class client:  # noqa: N801 (reference class name)
         pageable 276 MB 720p chunk went through a staged copy); the result comes back through
         pinned memory too, or stays on the GPU for an RCCL pair plane."""
         dev = self.resize_device
-        if self._h2d_done is not None:
-            self._h2d_done.synchronize()  # the previous chunk's upload has left the pinned buffer
-        pin = self._pinned("in", (len(frames),) + tuple(frames[0].shape))
+        if self._rs_stream is None:
+            self._rs_stream = torch.cuda.Stream(dev)
+        # two pinned input buffers: this chunk's copy overlaps the previous chunk's upload + resize
+        i = self._in_ring = (self._in_ring + 1) % 2
+        if self._in_done[i] is not None:
+            self._in_done[i].synchronize()  # the upload that last read this buffer has finished
+        pin = self._pinned(f"in{i}", (len(frames),) + tuple(frames[0].shape))
         if isinstance(frames, np.ndarray):  # one block (e.g. a memory-mapped chunk): one threaded copy
             pin.copy_(_host_tensor(frames))
         else:
-            for i, f in enumerate(frames):
-                pin[i].copy_(torch.from_numpy(f))
-        x = pin.to(dev, non_blocking=True)
-        self._h2d_done = torch.cuda.Event()
-        self._h2d_done.record(torch.cuda.current_stream(dev))
-        small = V.resize_width(x, 400)
-        if self.plane is not None:
-            # the p2p plane holds the chunk until its result is back: its own memory
-            return small if self.plane.device.type == "cuda" else small.cpu()
-        po = self._pinned("out", tuple(small.shape))
-        po.copy_(small, non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
-        return po.numpy()  # sent (copied onto the wire) before the next chunk reuses it
+            for j, f in enumerate(frames):
+                pin[j].copy_(torch.from_numpy(f))
+        with torch.cuda.stream(self._rs_stream):
+            x = pin.to(dev, non_blocking=True)
+            up = torch.cuda.Event()
+            up.record(self._rs_stream)
+            self._in_done[i] = up
+            small = V.resize_width(x, 400)
+            if self.plane is not None and self.plane.device.type == "cuda":
+                done = torch.cuda.Event()
+                done.record(self._rs_stream)
+                return _Landing(small, done)  # an RCCL pair plane sends it from device memory
+            # 4 result buffers: one being sent, two queued for the wire (wire_q), one being filled
+            self._out_ring = (self._out_ring + 1) % 4
+            po = self._pinned(f"out{self._out_ring}", tuple(small.shape))
+            po.copy_(small, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(self._rs_stream)
+        return _Landing(po, done, host=True)
 
     # ------------------------------------------------------------------ receive
     def recv_image_thread(self):
