@@ -183,6 +183,9 @@ def main():
                          "(a steady-state job without an --frames-sized file in RAM)")
     ap.add_argument("--job-repeats", type=int, default=3, help="job runs per plane (median reported)")
     ap.add_argument("--no-job", action="store_true")
+    ap.add_argument("--uplink-ab", action="store_true",
+                    help="each plane also runs with the requester's two-stage uplink off (VCX_UPLINK_PIPELINE=0), "
+                         "interleaved: keys job[_p2p]_nopipe_*")
     ap.add_argument("--data-plane", default="both", choices=["relay", "p2p", "both"])
     ap.add_argument("--y4m-frames", type=int, default=0, help="also run the job on a Y4M file of this many frames")
     ap.add_argument("--source", default="npy", choices=["npy", "synthetic"],
@@ -199,13 +202,21 @@ def main():
         try:
             # each plane's job runs --job-repeats times, interleaved (run-to-run spread of a
             # sub-second job on a shared host is +-15 %): the median is reported, every run listed
+            from distributedvolunteercomputing_amd import config as vcx_config
+
             planes = ("relay", "p2p") if a.data_plane == "both" else (a.data_plane,)
-            runs = {pl: [] for pl in planes}
+            variants = [(pl, pipe) for pl in planes for pipe in ((True, False) if a.uplink_ab else (True,))]
+            runs = {v: [] for v in variants}
             for _ in range(max(1, a.job_repeats)):
-                for plane in planes:
-                    runs[plane].append(bench_job(a, dev, plane, source=src))
-            for plane, rs in runs.items():
-                pre = "job" if plane == "relay" else f"job_{plane}"
+                for plane, pipe in variants:
+                    with vcx_config.override(uplink_pipeline=pipe):
+                        r = bench_job(a, dev, plane, source=src)
+                    if not pipe:  # job[_p2p]_* -> job[_p2p]_nopipe_*
+                        pre = "job" if plane == "relay" else f"job_{plane}"
+                        r = {(pre + "_nopipe" + k[len(pre):] if k.startswith(pre + "_") else k): v for k, v in r.items()}
+                    runs[(plane, pipe)].append(r)
+            for (plane, pipe), rs in runs.items():
+                pre = ("job" if plane == "relay" else f"job_{plane}") + ("" if pipe else "_nopipe")
                 ok = [r for r in rs if r.get(f"{pre}_frames_per_s")]
                 if not ok:
                     rec.update(rs[-1])

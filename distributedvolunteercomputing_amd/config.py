@@ -55,6 +55,8 @@ class RuntimeConfig:
     # VCX_ELASTIC_STAGE_JOINS: a joiner's generation is agreed one round early and its communicator
     # built during the local steps (the admission round pays no communicator init)
     elastic_stage_joins: bool = True
+    # VCX_UPLINK_PIPELINE: the requester packs / resizes chunk k+1 while a wire thread ships chunk k
+    uplink_pipeline: bool = True
     store_port_train: int = 29611  # VCX_STORE_PORT (train CLI): rendezvous store port
     store_port_video: int = 29612  # VCX_STORE_PORT (video CLI): job-control store port
     # ---- observability
@@ -84,6 +86,7 @@ _ENV = {
     "elastic_debug": ("VCX_ELASTIC_DEBUG", _bool),
     "elastic_liveness": ("VCX_ELASTIC_LIVENESS", _bool),
     "elastic_stage_joins": ("VCX_ELASTIC_STAGE_JOINS", _bool),
+    "uplink_pipeline": ("VCX_UPLINK_PIPELINE", _bool),
     "store_port_train": ("VCX_STORE_PORT", int),
     "store_port_video": ("VCX_STORE_PORT", int),
     "trace_dir": ("VCX_TRACE_DIR", str),

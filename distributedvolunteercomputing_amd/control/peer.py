@@ -291,7 +291,10 @@ class client:  # noqa: N801 (reference class name)
                 else:
                     chunk = np.stack(frames) if block is None else np.ascontiguousarray(block)
             info = f"{self.my_ip}||request||{'-'.join(map(str, nums))}||{chunk.shape[1]}||{chunk.shape[2]}"
-            self.wire_q.put((info, chunk))  # in order: one wire thread
+            if config.get().uplink_pipeline:
+                self.wire_q.put((info, chunk))  # in order: one wire thread
+            else:
+                self._ship(info, chunk)
             self.metrics.incr("chunks_sent")
             frames.clear()
             nums.clear()
@@ -327,23 +330,27 @@ class client:  # noqa: N801 (reference class name)
                 info, chunk = self.wire_q.get(timeout=0.2)
             except queue.Empty:
                 continue
-            if isinstance(chunk, _Landing):
-                with self.hspans.span("req_wait_resize"):
-                    chunk = chunk.wait()
-            if self.plane is not None:  # p2p: the chunk stays here; the coordinator gets its metadata
-                key = next(self._keys)
-                held = chunk if isinstance(chunk, torch.Tensor) else _host_tensor(chunk)
-                if held.device.type == "cpu" and self._pins and any(
-                        held.data_ptr() == b.data_ptr() for b in self._pins.values()):
-                    held = held.clone()  # a pinned ring buffer: the next chunks reuse it
-                with self._p2p_lock:
-                    self._outgoing[key] = held
-                ok = self.sender.send_image(info, _EMPTY, p2p=1, key=key, cshape=list(held.shape))
-            else:
-                with self.hspans.span("req_send"):
-                    ok = self.sender.send_image(info, chunk)
-            if not ok:
-                self.log("uplink send failed")
+            self._ship(info, chunk)
+
+    def _ship(self, info, chunk):
+        """Send one packed chunk (relay) or park it and send its metadata (p2p)."""
+        if isinstance(chunk, _Landing):
+            with self.hspans.span("req_wait_resize"):
+                chunk = chunk.wait()
+        if self.plane is not None:  # p2p: the chunk stays here; the coordinator gets its metadata
+            key = next(self._keys)
+            held = chunk if isinstance(chunk, torch.Tensor) else _host_tensor(chunk)
+            if held.device.type == "cpu" and self._pins and any(
+                    held.data_ptr() == b.data_ptr() for b in self._pins.values()):
+                held = held.clone()  # a pinned ring buffer: the next chunks reuse it
+            with self._p2p_lock:
+                self._outgoing[key] = held
+            ok = self.sender.send_image(info, _EMPTY, p2p=1, key=key, cshape=list(held.shape))
+        else:
+            with self.hspans.span("req_send"):
+                ok = self.sender.send_image(info, chunk)
+        if not ok:
+            self.log("uplink send failed")
 
     def _pinned(self, name, shape):
         b = self._pins.get(name)
@@ -414,8 +421,7 @@ class client:  # noqa: N801 (reference class name)
         is logged and counted instead of killing the receive thread."""
         try:
             with self.hspans.span("req_sink"):
-                for i, n in enumerate(nums):
-                    self.sink.push(n, frames[i])
+                self.sink.push_many(nums, frames)
         except Exception as e:  # noqa: BLE001
             self.metrics.incr("sink_errors")
             print(f"output sink failed: {type(e).__name__}: {e}", flush=True)

@@ -192,194 +192,6 @@ attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
 #undef sV_
 }
 
-// Forward, software-pipelined across key tiles (one wave's own MFMAs overlap its own softmax):
-// iteration k issues the score MFMAs of tile k+1, the exp / row-sum / bf16 pack of tile k (whose
-// max is already known), the P.V MFMAs of tile k and the row max of tile k+1 -- one basic block,
-// so the scheduler interleaves the VALU of one tile into the MFMA gaps of the other instead of
-// running QK -> max -> exp -> PV as a serial chain per wave (profiles/r4_attention_pmc.txt: every
-// wave of the tile-serial kernel waits 37 % of its cycles). The deferred rescale (T13) is the only
-// branch, at the end of the iteration. K tiles are prefetched two ahead, V tiles one ahead, through
-// the same two [K | V] LDS-DMA buffers; the (at most two) diagonal tiles run the masked tile-serial
-// step of attn_fwd_d64_kernel. One extra score tile in registers: 2 waves per SIMD.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-attn_fwd_d64_pipe_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int B,
-                         int T, int H, float scale_log2, int staged_epi) {
-  __shared__ __attribute__((aligned(16))) bf16 sKV0[2][A_BK * AD];  // [K | V], swizzled (swz)
-  __shared__ __attribute__((aligned(16))) bf16 sKV1[2][A_BK * AD];
-#define sK_(b) ((b) ? &sKV1[0][0] : &sKV0[0][0])
-#define sV_(b) ((b) ? &sKV1[1][0] : &sKV0[1][0])
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
-  const int nqt = (T + A_BQ - 1) / A_BQ;
-  const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int qt = nqt - 1 - (lb % nqt);
-  const int bh = lb / nqt;
-  const int b = bh / H, hh = bh % H;
-  const int64_t tok = 3ll * H * AD;
-  const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
-  const bf16* Kg = base + H * AD;
-  const bf16* Vg = base + 2 * H * AD;
-  const int q0 = qt * A_BQ;
-  const int qw = q0 + w * 32;
-  const int q = qw + col;
-  const int qc = min(q, T - 1);
-  sx8 qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = *(const sx8*)(base + (int64_t)qc * tok + 16 * s + 8 * h2);
-  f32x16 o0 = {}, o1 = {};
-  float m = -INFINITY, l = 0.f;
-  const int kend = min(T, q0 + A_BQ);
-  const int nkt = (kend + A_BK - 1) / A_BK;
-  const int kdiag = q0 / A_BK;  // tiles [0, kdiag) are unmasked for every wave of the block
-  auto dma_k = [&](int kt, auto buf_c) { dma_tile_swz(Kg, tok, kt * A_BK, T - 1, sK_(decltype(buf_c)::value), w, lane); };
-  auto dma_v = [&](int kt, auto buf_c) { dma_tile_swz(Vg, tok, kt * A_BK, T - 1, sV_(decltype(buf_c)::value), w, lane); };
-  auto qk = [&](auto buf_c, f32x16& s0, f32x16& s1) {
-    constexpr int cur = decltype(buf_c)::value;
-    s0 = f32x16{};
-    s1 = f32x16{};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      s0 = mfma32(row_frag_swz(sK_(cur), col, s, h2), qf[s], s0);
-      s1 = mfma32(row_frag_swz(sK_(cur), 32 + col, s, h2), qf[s], s1);
-    }
-  };
-  // row max of a raw score tile; deferred rescale of O / l (threshold 2^8)
-  auto rowmax = [&](f32x16& s0, f32x16& s1) {
-    mfma_read_fence(s0, s1);
-    float mx0 = max3(s0[0], s0[1], s1[0]), mx1 = max3(s1[1], s0[2], s1[2]);
-#pragma unroll
-    for (int r = 3; r < 15; r += 2) {
-      mx0 = max3(mx0, s0[r], s1[r]);
-      mx1 = max3(mx1, s0[r + 1], s1[r + 1]);
-    }
-    return xhalf_max(max3(mx0, mx1, fmaxf(s0[15], s1[15]))) * scale_log2;
-  };
-  auto rescale = [&](float mx) {
-    if (!__all(mx - m <= 8.f)) {
-      const float mnew = fmaxf(m, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-      l *= alpha;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        o0[r] *= alpha;
-        o1[r] *= alpha;
-      }
-      m = mnew;
-    }
-  };
-  // P = exp2(S c - m), row sums, O += V^T P^T for one score tile whose max is already folded into m
-  auto pv = [&](f32x16& s0, f32x16& s1, auto buf_c) {
-    constexpr int cur = decltype(buf_c)::value;
-    const float mneg = -m;
-    float ps0 = 0.f, ps1 = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p0 = __builtin_amdgcn_exp2f(fmaf(s0[r], scale_log2, mneg));
-      const float p1 = __builtin_amdgcn_exp2f(fmaf(s1[r], scale_log2, mneg));
-      s0[r] = p0;
-      s1[r] = p1;
-      ps0 += p0;
-      ps1 += p1;
-    }
-    l += xhalf_sum(ps0 + ps1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const f32x16& sp = (s < 2) ? s0 : s1;
-      sx8 pb;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pb[j] = bf16_bits(sp[8 * (s & 1) + j]);
-      o0 = mfma32(vt_frag_swz(sV_(cur), (s >> 1) * 32, 0, s & 1, lane), pb, o0);
-      o1 = mfma32(vt_frag_swz(sV_(cur), (s >> 1) * 32, 1, s & 1, lane), pb, o1);
-    }
-  };
-  // the masked tile-serial step of the diagonal tiles (as attn_fwd_d64_kernel)
-  auto tile_masked = [&](int kt, auto cur_c) {
-    constexpr int cur = decltype(cur_c)::value;
-    const int kb = kt * A_BK;
-    if (kb > qw + 31) return;
-    f32x16 s0, s1;
-    qk(cur_c, s0, s1);
-    mfma_read_fence(s0, s1);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
-      s0[r] = key > q ? -INFINITY : s0[r];
-      s1[r] = key + 32 > q ? -INFINITY : s1[r];
-    }
-    rescale(rowmax(s0, s1));
-    pv(s0, s1, cur_c);
-  };
-  f32x16 sa, sb, ta, tb;  // score tiles: (sa, sb) = tile k, (ta, tb) = tile k + 1
-  int kt = 0;
-  if (kdiag >= 2) {
-    // prologue: K0 -> buffer 0, V0 -> buffer 0, K1 -> buffer 1; S0 and its max
-    dma_k(0, I0{});
-    dma_v(0, I0{});
-    dma_k(1, I1{});
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every staged piece (and the Q fragments) landed
-    __syncthreads();
-    qk(I0{}, sa, sb);
-    rescale(rowmax(sa, sb));
-    __syncthreads();  // every wave has read K0: buffer 0's K slot is free for K2
-    // iteration k (buffer parity p = k & 1): K_{k+2} -> K slot p, V_{k+1} -> V slot p^1,
-    // S_{k+1} from K slot p^1, softmax + PV of S_k on V slot p, max of S_{k+1}
-    auto body = [&](int k, auto p_c) {
-      constexpr int p = decltype(p_c)::value;
-      using Q = std::integral_constant<int, p ^ 1>;
-      if (k + 2 < kdiag) dma_k(k + 2, p_c);
-      dma_v(k + 1, Q{});
-      qk(Q{}, ta, tb);
-      pv(sa, sb, p_c);
-      const float mx = rowmax(ta, tb);
-      rescale(mx);
-      sa = ta;
-      sb = tb;
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-      __syncthreads();
-    };
-    for (; kt + 2 < kdiag; kt += 2) {  // iterations kt, kt + 1 (both with a next unmasked tile)
-      body(kt, I0{});
-      body(kt + 1, I1{});
-    }
-    if (kt + 1 < kdiag) body(kt++, I0{});
-    // kt == kdiag - 1 (odd: kdiag is even): finish S_{kdiag-1} on V slot 1 while V_{kdiag} streams
-    // into V slot 0; K_{kdiag} already sits in K slot 0 (prefetched two ahead)
-    if (kdiag < nkt) dma_v(kdiag, I0{});
-    pv(sa, sb, I1{});
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __syncthreads();
-    kt = kdiag;
-  } else {
-    dma_k(0, I0{});
-    dma_v(0, I0{});
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __syncthreads();
-  }
-  // diagonal tiles: tile kt sits in buffer (kt - kdiag) & 1 == 0 first
-  for (int i = 0; kt < nkt; ++kt, ++i) {
-    if (i & 1) {
-      if (kt + 1 < nkt) {
-        dma_k(kt + 1, I0{});
-        dma_v(kt + 1, I0{});
-      }
-      tile_masked(kt, I1{});
-    } else {
-      if (kt + 1 < nkt) {
-        dma_k(kt + 1, I1{});
-        dma_v(kt + 1, I1{});
-      }
-      tile_masked(kt, I0{});
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __syncthreads();
-  }
-  const float inv = 1.f / l;
-  store_acc_tile(o0, o1, inv, out + ((int64_t)b * T + qw) * H * AD + hh * AD, (int64_t)H * AD, T - qw,
-                 &sKV0[0][0] + w * 32 * AD, staged_epi, lane);
-  if (q < T && h2 == 0) lse[((int64_t)b * H + hh) * T + q] = m + __log2f(l);
-#undef sK_
-#undef sV_
-}
-
 // ============================================================================ backward
 // dQ (query-parallel; same tiling as the forward): per 32-key sub-tile
 //   S^T = K Q^T, P^T = exp2(S^T c - lse), dP^T = V dO^T, dS^T = P^T (dP^T - delta),
@@ -752,19 +564,14 @@ using namespace vcx;
 // Backward kernels: 2 waves per SIMD (at 3-4 they spill: dq 0.87-1.25 ms vs 0.64 for the pair);
 // dQ with LDS-DMA staging (264 vs 275 us), dK/dV with register staging (381 vs 383 us: the DMA
 // build of that kernel hits the 256-VGPR cap and spills).
-static int g_fwd_wpe = 3, g_fwd_dma = 1, g_bwd_dma = 1;
-static int g_fwd_pipe = 0;  // 1: attn_fwd_d64_pipe_kernel (software-pipelined across key tiles)  // g_bwd_dma bit 0: dQ kernel, bit 1: dK/dV kernel
+static int g_fwd_wpe = 3, g_fwd_dma = 1, g_bwd_dma = 1;  // g_bwd_dma bit 0: dQ kernel, bit 1: dK/dV kernel
 // output tiles (O, dQ, dK, dV): 1 = staged through LDS, whole-row 16-B stores; 0 = per-lane half-row
 // stores. Bench shape, same box (profiles/r1_attn_variants.log): backward 0.589 vs 0.614 ms, forward
 // within noise (0.201-0.212 vs 0.206-0.208)
 static int g_stage_epi = 1;
 
 void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma, int stage_epi) {
-  if (fwd_wpe == 2 || fwd_wpe == 3) {
-    g_fwd_wpe = fwd_wpe;
-    g_fwd_pipe = 0;
-  }
-  if (fwd_wpe == 4) g_fwd_pipe = 1;  // (variant id, not a wave count: the pipelined forward)
+  if (fwd_wpe == 2 || fwd_wpe == 3) g_fwd_wpe = fwd_wpe;
   if (fwd_dma == 0 || fwd_dma == 1) g_fwd_dma = fwd_dma;
   if (bwd_dma >= 0 && bwd_dma <= 3) g_bwd_dma = bwd_dma;
   if (stage_epi == 0 || stage_epi == 1) g_stage_epi = stage_epi;
@@ -801,10 +608,7 @@ void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int 
 #define VCX_FWD(W, D)                                                                                      \
   hipLaunchKernelGGL((attn_fwd_d64_kernel<W, D>), g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H, \
                      scale * LOG2E, g_stage_epi)
-  if (g_fwd_pipe) {
-    hipLaunchKernelGGL(attn_fwd_d64_pipe_kernel, g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H,
-                       scale * LOG2E, g_stage_epi);
-  } else if (g_fwd_dma) {
+  if (g_fwd_dma) {
     if (g_fwd_wpe == 2) VCX_FWD(2, true); else VCX_FWD(3, true);
   } else {
     if (g_fwd_wpe == 2) VCX_FWD(2, false); else VCX_FWD(3, false);

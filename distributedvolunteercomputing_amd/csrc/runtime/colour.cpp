@@ -48,6 +48,41 @@ void bgr_to_yuv444(const uint8_t* bgr, uint8_t* yuv, int64_t w, int64_t h) {
   });
 }
 
+void bgr_to_yuv444_frames(const uint8_t* bgr, uint8_t* yuv, int64_t k, int64_t w, int64_t h) {
+  // frames [k, h, w, 3] -> [k, 3, h, w]: whole frames per thread (a 400 x 225 output frame is below
+  // the per-frame banding threshold, so one call per frame ran on one core)
+  const int64_t n = w * h;
+  const int64_t hw = (int64_t)std::max(1u, std::thread::hardware_concurrency());
+  const int64_t nt = std::min<int64_t>({8, hw, std::max<int64_t>(1, k * n / 65536), k});
+  auto run = [&](int64_t f0, int64_t f1) {
+    for (int64_t f = f0; f < f1; ++f) {
+      const uint8_t* src = bgr + f * 3 * n;
+      uint8_t* Y = yuv + f * 3 * n;
+      uint8_t* U = Y + n;
+      uint8_t* V = Y + 2 * n;
+      for (int64_t i = 0; i < n; ++i) {
+        const float b = src[3 * i], g = src[3 * i + 1], r = src[3 * i + 2];
+        const float y = 0.299f * r + 0.587f * g + 0.114f * b;
+        Y[i] = sat(y);
+        U[i] = sat((b - y) * 0.564f + 128.0f);
+        V[i] = sat((r - y) * 0.713f + 128.0f);
+      }
+    }
+  };
+  if (nt <= 1) {
+    run(0, k);
+    return;
+  }
+  std::vector<std::thread> th;
+  const int64_t per = (k + nt - 1) / nt;
+  for (int64_t t = 1; t < nt; ++t) {
+    const int64_t f0 = t * per, f1 = std::min(k, f0 + per);
+    if (f0 < f1) th.emplace_back([&run, f0, f1] { run(f0, f1); });
+  }
+  run(0, std::min(k, per));
+  for (auto& x : th) x.join();
+}
+
 void yuv_to_bgr(const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* bgr, int64_t w, int64_t h,
                 int64_t cw) {
   const bool sub = cw != w;  // 4:2:0

@@ -10,6 +10,8 @@ namespace vcxrt {
 
 // bgr [h][w][3] -> yuv planes [3][h][w]
 void bgr_to_yuv444(const uint8_t* bgr, uint8_t* yuv, int64_t w, int64_t h);
+// k frames [k, h, w, 3] -> [k, 3, h, w] planar (one Y4M 4:4:4 frame body each), frames across threads
+void bgr_to_yuv444_frames(const uint8_t* bgr, uint8_t* yuv, int64_t k, int64_t w, int64_t h);
 // planes y [h][w], u/v [ch][cw] with cw = w (4:4:4) or (w + 1) / 2 (4:2:0, 2x2 replication) -> bgr [h][w][3]
 void yuv_to_bgr(const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* bgr, int64_t w, int64_t h, int64_t cw);
 

@@ -170,6 +170,20 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("src"), py::arg("dst"), py::arg("w"), py::arg("h"));
   m.def(
+      "bgr_to_yuv444_frames",
+      [](py::buffer src, py::buffer dst, int64_t k, int64_t w, int64_t h) {
+        py::buffer_info a = src.request(), b = dst.request(true);
+        require_c_contiguous(a, "bgr_to_yuv444_frames src");
+        require_c_contiguous(b, "bgr_to_yuv444_frames dst");
+        if (k < 0 || a.size * a.itemsize < 3 * k * w * h || b.size * b.itemsize < 3 * k * w * h)
+          throw std::invalid_argument("bgr_to_yuv444_frames: buffers smaller than 3 * k * w * h bytes");
+        without_gil([&] {
+          bgr_to_yuv444_frames((const uint8_t*)a.ptr, (uint8_t*)b.ptr, k, w, h);
+          return 0;
+        });
+      },
+      py::arg("src"), py::arg("dst"), py::arg("k"), py::arg("w"), py::arg("h"));
+  m.def(
       "yuv_to_bgr",
       [](py::buffer y, py::buffer u, py::buffer v, py::buffer dst, int64_t w, int64_t h, int64_t cw) {
         py::buffer_info Y = y.request(), U = u.request(), V = v.request(), D = dst.request(true);

@@ -41,6 +41,21 @@ def _rt():
         return None
 
 
+def _as_block(frames) -> np.ndarray:
+    """[k, h, w, 3] contiguous: the frames' own buffer when they are consecutive views of one
+    contiguous array (a received chunk), else one stacked copy."""
+    f0 = frames[0]
+    base = f0.base if isinstance(f0.base, np.ndarray) else None
+    if base is not None and base.ndim == 4 and base.flags.c_contiguous and all(f.base is base for f in frames):
+        step = f0.nbytes
+        o0 = f0.__array_interface__["data"][0] - base.__array_interface__["data"][0]
+        if o0 % step == 0 and all(f.__array_interface__["data"][0] == f0.__array_interface__["data"][0] + i * step
+                                  for i, f in enumerate(frames)) and all(f.flags.c_contiguous for f in frames):
+            j = o0 // step
+            return base[j:j + len(frames)]
+    return np.ascontiguousarray(np.stack(frames))
+
+
 def bgr_to_yuv444(frame: np.ndarray) -> np.ndarray:
     rt = _rt()
     if rt is not None and frame.dtype == np.uint8 and frame.ndim == 3 and frame.shape[2] == 3:
@@ -288,8 +303,24 @@ class Y4MWriter:
         if frame.shape[0] != self.h or frame.shape[1] != self.w:
             raise ValueError(f"frame {frame.shape} does not match writer {self.h}x{self.w}")
         self.f.write(b"FRAME\n")
-        self.f.write(bgr_to_yuv444(frame).tobytes())
+        self.f.write(bgr_to_yuv444(frame))  # the planar buffer itself (no bytes copy)
         self.frames += 1
+
+    def write_many(self, frames):
+        """Several frames in order: one native conversion across threads, then the frame bodies."""
+        rt = _rt()
+        if rt is None or not hasattr(rt, "bgr_to_yuv444_frames") or any(f.shape != (self.h, self.w, 3) or
+                                                                      f.dtype != np.uint8 for f in frames):
+            for f in frames:
+                self.write(f)
+            return
+        block = _as_block(frames)
+        out = np.empty((len(frames), 3, self.h, self.w), np.uint8)
+        rt.bgr_to_yuv444_frames(block, out, len(frames), self.w, self.h)
+        for i in range(len(frames)):
+            self.f.write(b"FRAME\n")
+            self.f.write(out[i])
+        self.frames += len(frames)
 
     def release(self):
         if self.f and not self.f.closed:

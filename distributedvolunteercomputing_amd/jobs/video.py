@@ -282,6 +282,27 @@ class OrderedSink:
                 self.written += 1
             self._check_done()
 
+    def push_many(self, nums, frames):
+        """A received chunk: every frame that becomes writable goes to the writer in one batch
+        (``write_many``: one multi-threaded colour conversion instead of one call per frame)."""
+        with self._lock:
+            ready = []
+            for i, n in enumerate(nums):
+                if n < self.index.next_expected or n in self.stash:
+                    continue
+                self.stash[n] = frames[i]
+                ready.extend(self.stash.pop(k) for k in self.index.push(n))
+            if ready:
+                if self.writer is None:
+                    self.writer = self.writer_factory(ready[0].shape[1], ready[0].shape[0])
+                if hasattr(self.writer, "write_many"):
+                    self.writer.write_many(ready)
+                else:
+                    for f in ready:
+                        self.writer.write(f)
+                self.written += len(ready)
+            self._check_done()
+
     def _check_done(self):
         if self.final is not None and self.index.next_expected > self.final and not self.done.is_set():
             self.t_done = time.time()

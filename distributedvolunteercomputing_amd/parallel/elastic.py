@@ -581,6 +581,9 @@ class ElasticMembership:
             yield
             _dbg(self.pid, f"guard {self.gen}/{tag}: commit")
             self._commit(tag)
+            st = self._staged
+            if st is not None and not st[4]._connected and st[4]._bg is None:
+                st[4].start_connect()  # the staged generation builds during the local steps
         except PeerFailure:
             self._vote(tag, "abort")
             raise
@@ -753,8 +756,9 @@ class ElasticMembership:
         return self.group, True, newcomers
 
     def _stage(self, g, members, newcomers, njoin):
-        """Generation g (the current members + joiners) is agreed: start building its communicator
-        on a helper thread, on a store client of its own; ``sync_round`` switches to it next round."""
+        """Generation g (the current members + joiners) is agreed: its group (on a store client of its
+        own) starts building after this round's collectives commit; ``sync_round`` switches to it
+        next round."""
         try:
             st = self._stores.base.clone()
         except Exception:  # noqa: BLE001
@@ -763,7 +767,9 @@ class ElasticMembership:
                         timeout_s=self.pg_timeout_s, device=self.device, watch=self)
         grp.fault_hook = self.fault_hook
         grp.needs_go = True  # its first collective is not lined up by a communicator init (guard)
-        grp.start_connect()
+        # its build starts once this round's collectives have committed (guard): an RCCL init running
+        # beside another communicator's collectives broke them at 8 ranks (connects refused), and
+        # between the commit and the switch there are only the local steps
         self._staged = (g, list(members), list(newcomers), int(njoin), grp)
         self.joins_seen = max(self.joins_seen, int(njoin))
         self.events.append({"event": "staged", "gen": g, "members": list(members), "joined": list(newcomers),

@@ -51,8 +51,7 @@ g_ref = C.attn_bwd(qkv, o_ref, dO, lse_ref, scale)
 torch.cuda.synchronize()
 res = {}
 for rnd in range(3):
-    # (waves/SIMD, DMA, LDS-staged output stores); waves/SIMD 4 = the software-pipelined forward
-    for fv in ((2, 0, 1), (3, 0, 1), (2, 1, 1), (3, 1, 0), (3, 1, 1), (4, 1, 1)):
+    for fv in ((2, 0, 1), (3, 0, 1), (2, 1, 1), (3, 1, 0), (3, 1, 1)):  # (waves/SIMD, DMA, LDS-staged output stores)
         C.attn_set_variant(fv[0], fv[1], 1, fv[2])
         o, l = C.attn_fwd(qkv, scale)
         if rnd == 0:

@@ -13,7 +13,9 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 from distributedvolunteercomputing_amd import config  # noqa: E402
-from distributedvolunteercomputing_amd.ops import linear as L  # noqa: E402
+import importlib  # noqa: E402
+
+L = importlib.import_module("distributedvolunteercomputing_amd.ops.linear")  # (ops.linear is also a function)
 from distributedvolunteercomputing_amd.ops import native  # noqa: E402
 
 dev = torch.device("cuda", 0)

@@ -73,7 +73,7 @@ def test_attention_matches_sdpa_at_bench_shape(gpu):
     assert rel < 1e-2, float(rel)
 
 
-@pytest.mark.parametrize("variant", [(2, 0, 0, 0), (3, 0, 3, 1), (2, 1, 2, 1), (3, 1, 1, 0), (3, 1, 1, 1), (4, 1, 1, 1)])
+@pytest.mark.parametrize("variant", [(2, 0, 0, 0), (3, 0, 3, 1), (2, 1, 2, 1), (3, 1, 1, 0), (3, 1, 1, 1)])
 def test_attention_deterministic(gpu, variant):
     """Same inputs, same kernel -> bitwise identical outputs (a race on the double-buffered LDS
     tiles would show up here as run-to-run differences)."""
@@ -95,30 +95,6 @@ def test_attention_deterministic(gpu, variant):
             assert torch.equal(g, gs[0])
     finally:
         C.attn_set_variant(3, 1, 1, 1)
-
-
-@pytest.mark.parametrize("T", [64, 200, 384, 1000, 1024])
-def test_attention_pipelined_forward_matches_fp32(gpu, T):
-    """The software-pipelined forward (attn_set_variant fwd_wpe=4: QK of tile k+1 and the max beside
-    softmax + PV of tile k) against fp32 attention, at lengths with 0, 1 and many unmasked tiles per
-    block and a ragged last tile; its log-sum-exp too."""
-    C = ops.native()
-    torch.manual_seed(T)
-    B, H = 3, 4
-    qkv = torch.randn(B, T, 3, H, 64, device=gpu).to(torch.bfloat16)
-    C.attn_set_variant(4, 1, 1, 1)
-    try:
-        o, lse = C.attn_fwd(qkv, 0.125)
-    finally:
-        C.attn_set_variant(3, 1, 1, 1)
-    q, k, v = qkv.float().permute(2, 0, 3, 1, 4).unbind(0)
-    sc = (q @ k.transpose(-1, -2)) * 0.125
-    sc = sc.masked_fill(torch.ones(T, T, device=gpu, dtype=torch.bool).triu(1), float("-inf"))
-    ref = (torch.softmax(sc, -1) @ v).transpose(1, 2)
-    rel = (o.float() - ref).norm() / ref.norm()
-    assert rel < 1e-2, float(rel)
-    l32 = torch.logsumexp(sc, -1) * 1.4426950408889634
-    assert (lse.float() - l32).abs().max().item() < 2e-2
 
 
 def _ref_gqa32(q, k, v, scale):

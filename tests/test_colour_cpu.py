@@ -47,3 +47,21 @@ def test_native_colour_rejects_strided_buffers():
     out = np.zeros((3, 8, 32), np.uint8)[:, :, ::2]  # a strided view: must not be written linearly
     with pytest.raises(ValueError):
         native().bgr_to_yuv444(f, out, 16, 8)
+
+
+@pytest.mark.parametrize("k,h,w", [(100, 225, 400), (3, 7, 9), (1, 1, 1)])
+def test_y4m_write_many_matches_per_frame(tmp_path, k, h, w):
+    """The sink's batched path (one multi-threaded native conversion per received chunk, frames
+    written from the planar buffer) produces the same file as writing frame by frame, whether the
+    frames are consecutive views of one chunk buffer or scattered arrays."""
+    frames = np.random.default_rng(k + h).integers(0, 256, (k, h, w, 3), dtype=np.uint8)
+    a, b, c = (V.Y4MWriter(str(tmp_path / f"{n}.y4m"), w, h, 30) for n in "abc")
+    for f in frames:
+        a.write(f)
+    b.write_many([frames[i] for i in range(k)])  # views of one contiguous block
+    c.write_many([frames[i].copy() for i in range(k)][::-1][::-1])  # separate arrays: stacked copy
+    for x in (a, b, c):
+        x.release()
+    ra, rb, rc = ((tmp_path / f"{n}.y4m").read_bytes() for n in "abc")
+    assert ra == rb == rc
+    assert len(ra) > k * 3 * h * w
