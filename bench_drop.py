@@ -75,7 +75,13 @@ def parse(argv=None):
 
 # ----------------------------------------------------------------------------- peer
 def peer_main(a):
+    import faulthandler
+
     from distributedvolunteercomputing_amd.utils.tuning import enable_tuned_gemms
+
+    # a peer still running shortly before the launcher's kill prints every thread's Python stack
+    # (where a hung peer sits) to its log
+    faulthandler.dump_traceback_later(max(5.0, a.timeout - 15.0), exit=False)
 
     ngpu = int(os.environ.get("VCX_DROP_NGPU", "0"))
     local = a.peer % ngpu if ngpu else 0
