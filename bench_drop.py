@@ -419,7 +419,8 @@ def launcher(a):
         rec["joiner_admission_round_ms"] = [round(s_["admission_round_ms"], 1) for s_ in adm_st
                                             if s_ and "admission_round_ms" in s_]
         rec["joiner_admission_stages"] = adm_st
-        rec["staged_admission"] = os.environ.get("VCX_ELASTIC_STAGE_JOINS", "1") not in ("0", "false", "no", "off")
+        sj = os.environ.get("VCX_ELASTIC_STAGE_JOINS", "gloo")
+        rec["staged_admission"] = sj == "all" or (sj == "gloo" and backend == "gloo")
         # per survivor: how long its background communicator build ran, what was left of it to wait
         # for at the switch, and the line-up wait before the admission round
         rec["staged_survivors"] = staged

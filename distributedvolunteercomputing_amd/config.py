@@ -53,8 +53,10 @@ class RuntimeConfig:
     elastic_debug: bool = False  # VCX_ELASTIC_DEBUG: trace membership decisions to stderr
     elastic_liveness: bool = True  # VCX_ELASTIC_LIVENESS: TCP liveness links (process death seen at once)
     # VCX_ELASTIC_STAGE_JOINS: a joiner's generation is agreed one round early and its communicator
-    # built during the local steps (the admission round pays no communicator init)
-    elastic_stage_joins: bool = True
+    # built during the local steps (the admission round pays no communicator init): "gloo" (default:
+    # gloo groups only -- with RCCL at 8 ranks on one card it broke the members, profiles/
+    # r4_rccl8_rehearsal_1gpu.txt), "all", or "off"
+    elastic_stage_joins: str = "gloo"
     # VCX_UPLINK_PIPELINE: the requester packs / resizes chunk k+1 while a wire thread ships chunk k
     uplink_pipeline: bool = True
     store_port_train: int = 29611  # VCX_STORE_PORT (train CLI): rendezvous store port
@@ -85,14 +87,14 @@ _ENV = {
     "p2p_backend": ("VCX_P2P_BACKEND", str),
     "elastic_debug": ("VCX_ELASTIC_DEBUG", _bool),
     "elastic_liveness": ("VCX_ELASTIC_LIVENESS", _bool),
-    "elastic_stage_joins": ("VCX_ELASTIC_STAGE_JOINS", _bool),
+    "elastic_stage_joins": ("VCX_ELASTIC_STAGE_JOINS", str),
     "uplink_pipeline": ("VCX_UPLINK_PIPELINE", _bool),
     "store_port_train": ("VCX_STORE_PORT", int),
     "store_port_video": ("VCX_STORE_PORT", int),
     "trace_dir": ("VCX_TRACE_DIR", str),
     "metrics_dir": ("VCX_METRICS_DIR", str),
 }
-_CHOICES = {"gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl")}
+_CHOICES = {"gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "all", "off")}
 
 _lock = threading.Lock()
 

@@ -297,7 +297,8 @@ class ElasticMembership:
         # blocking store waits (server-side wake-up) instead of sleep-polling on the fast paths; a
         # wait that runs out falls back to the polling scan, which owns lease/EOF detection
         self.bell_s = min(2.0, max(0.25, lease_s / 4))
-        self.stage_joins = config.get().elastic_stage_joins
+        sj = config.get().elastic_stage_joins
+        self.stage_joins = sj == "all" or (sj == "gloo" and backend == "gloo")
         self.last_go_wait_ms = 0.0
         self._staged = None  # (gen, members, newcomers, njoin, group) agreed, built in the background
         if backend == "nccl":

@@ -14,5 +14,5 @@ step() {  # name, seconds, command...
 step bn_diag 240 python -u scripts/bn_diag.py
 R="python -u bench_drop.py --peers 8 --backend nccl --model gpt2 --batch 2 --seq 256 --steps 16 --warmup 4 --fault collective --drop-peers 6,7 --rejoin --lease 2.0 --timeout 440"
 step rejoin_n8_staged 480 env VCX_ELASTIC_STAGE_JOINS=1 $R --json-out $O/rejoin_n8_staged.json
-step rejoin_n8_unstaged 480 env VCX_ELASTIC_STAGE_JOINS=0 $R --json-out $O/rejoin_n8_unstaged.json
+step rejoin_n8_unstaged 480 env VCX_ELASTIC_STAGE_JOINS=off $R --json-out $O/rejoin_n8_unstaged.json
 step video_30k 900 python -u bench_video.py --frames 30000 --source-frames 3000 --job-repeats 3 --data-plane both

@@ -18,5 +18,5 @@ step detprof 200 bash scripts/gpu_det_prof.sh
 step bench1 300 python -u bench.py
 step bench2 300 python -u bench.py
 R="python -u bench_drop.py --peers 8 --backend nccl --model gpt2 --batch 2 --seq 256 --steps 16 --warmup 4 --fault collective --drop-peers 6,7 --rejoin --lease 2.0 --timeout 150"
-step rejoin_n8_staged 240 env VCX_ELASTIC_STAGE_JOINS=1 VCX_ELASTIC_DEBUG=1 $R --json-out $O/rejoin_n8_staged.json
+step rejoin_n8_staged 240 env VCX_ELASTIC_STAGE_JOINS=all VCX_ELASTIC_DEBUG=1 $R --json-out $O/rejoin_n8_staged.json
 step video_30k 600 python -u bench_video.py --frames 30000 --source-frames 3000 --job-repeats 3 --data-plane both

@@ -13,4 +13,4 @@ step() {  # name, seconds, command...  (rc 1 = failed tests / bench: logged, nex
 step gpu_suite 660 python -u -m pytest -q --timeout 120 --timeout-method thread tests/ -m gpu
 step video_ab 420 python -u bench_video.py --frames 30000 --source-frames 3000 --job-repeats 3 --data-plane both --uplink-ab
 R="python -u bench_drop.py --peers 8 --backend nccl --model gpt2 --batch 2 --seq 256 --steps 16 --warmup 4 --fault collective --drop-peers 6,7 --rejoin --lease 2.0 --timeout 120"
-step rejoin_n8_staged 200 env VCX_ELASTIC_STAGE_JOINS=1 VCX_ELASTIC_DEBUG=1 $R --json-out $O/rejoin_n8_staged.json
+step rejoin_n8_staged 200 env VCX_ELASTIC_STAGE_JOINS=all VCX_ELASTIC_DEBUG=1 $R --json-out $O/rejoin_n8_staged.json
