@@ -721,7 +721,10 @@ __global__ void __launch_bounds__(256) xent_bwd_kernel(const bf16* logits, const
 // (softmax - onehot) / nvalid over the same buffer, versus a read for the loss plus a read and a
 // write for the gradient. The loss backward's incoming scalar is applied afterwards only if it is
 // not 1 (xent_rescale_kernel). Rows with a negative target contribute neither loss nor gradient.
-template <int TPB, int NV, int WPE = 6>
+// KEEP_E: the sum pass keeps e = exp2(x log2e - M) in the row's own registers (as bf16, over the
+// logits it no longer needs) and the gradient pass only scales it by 1 / sum: one exp per element
+// instead of two (the gradient is rounded to bf16 anyway; e's own bf16 rounding adds one more ulp).
+template <int TPB, int NV, int WPE = 6, bool KEEP_E = false>
 __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE))) xent_fused_kernel(
     bf16* __restrict__ logits, const int64_t* __restrict__ tgt, const float* __restrict__ nvalid,
     float* __restrict__ loss_out, int V, int Vp) {
@@ -764,8 +767,13 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE)))
     const int c = tid + k * TPB;
     if (c < Vp8) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (c * 8 + j < V) sum += __builtin_amdgcn_exp2f(fmaf((float)v[k][j], L2E, -M2));
+      for (int j = 0; j < 8; ++j) {
+        if (c * 8 + j < V) {
+          const float e = __builtin_amdgcn_exp2f(fmaf((float)v[k][j], L2E, -M2));
+          sum += e;
+          if constexpr (KEEP_E) v[k][j] = (bf16)e;
+        }
+      }
     }
   }
   sum = wave_sum(sum);
@@ -776,6 +784,7 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE)))
   for (int i = 0; i < NW; ++i) S += red[1][i];
   const float lse2 = M2 + __builtin_amdgcn_logf(S);  // log2-domain lse (v_log_f32 is log2)
   const float sc = (t >= 0) ? 1.f / nvalid[0] : 0.f;
+  const float invS = 1.f / S;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = tid + k * TPB;
@@ -784,7 +793,11 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WPE)))
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int col = c * 8 + j;
-        float p = (col < V) ? __builtin_amdgcn_exp2f(fmaf((float)v[k][j], L2E, -lse2)) : 0.f;
+        float p;
+        if constexpr (KEEP_E)
+          p = (col < V) ? (float)v[k][j] * invS : 0.f;
+        else
+          p = (col < V) ? __builtin_amdgcn_exp2f(fmaf((float)v[k][j], L2E, -lse2)) : 0.f;
         if (col == t) p -= 1.f;
         o[j] = (bf16)(p * sc);
       }
@@ -1029,8 +1042,15 @@ int vcx_xent_fused(void* logits, const int64_t* tgt, const float* nvalid, float*
     hipLaunchKernelGGL((xent_fused_kernel<512, 13, 5>), grid, dim3(512), 0, s, (bf16*)logits, tgt, nvalid, loss, V, Vp);
     return 1;
   }
+  static const bool keep_e = [] {  // VCX_XENT_KEEP_E=1: one exp per element (KEEP_E above)
+    const char* e = getenv("VCX_XENT_KEEP_E");
+    return e && atoi(e) == 1;
+  }();
   if (Vp8 <= 768 * 4)
     hipLaunchKernelGGL((xent_fused_kernel<768, 4>), grid, dim3(768), 0, s, (bf16*)logits, tgt, nvalid, loss, V, Vp);
+  else if (Vp8 <= 768 * 9 && keep_e)
+    hipLaunchKernelGGL((xent_fused_kernel<768, 9, 6, true>), grid, dim3(768), 0, s, (bf16*)logits, tgt, nvalid, loss,
+                       V, Vp);
   else if (Vp8 <= 768 * 9)
     hipLaunchKernelGGL((xent_fused_kernel<768, 9>), grid, dim3(768), 0, s, (bf16*)logits, tgt, nvalid, loss, V, Vp);
   else

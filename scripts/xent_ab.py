@@ -3,6 +3,7 @@
 the logits). Each variant runs in its own process (the TPB choice is read once).
 
     VCX_XENT_TPB=768 python scripts/xent_ab.py
+    VCX_XENT_KEEP_E=1 python scripts/xent_ab.py     (one exp per element, norm_act.hip KEEP_E)
 """
 import os
 import sys
@@ -35,5 +36,5 @@ for _ in range(5):
     ts.append(e0.elapsed_time(e1) / 5)
 t = sorted(ts)[2]
 gb = 2 * R * Vp * 2 / 1e9
-print(f"VCX_XENT_TPB={os.environ.get('VCX_XENT_TPB', '768')}: {t * 1e3:.1f} us/call, {gb / t:.2f} TB/s algorithmic "
+print(f"VCX_XENT_TPB={os.environ.get('VCX_XENT_TPB', '768')} KEEP_E={os.environ.get('VCX_XENT_KEEP_E', '0')}: {t * 1e3:.1f} us/call, {gb / t:.2f} TB/s algorithmic "
       f"(max err {err:.2e})", flush=True)
