@@ -212,8 +212,10 @@ std::vector<at::Tensor> ssd_detect(at::Tensor conf, at::Tensor loc, at::Tensor p
   TORCH_CHECK(C <= 32, "ssd_detect: at most 32 classes");
   auto prob = at::empty({N, C, P}, fo);
   auto cls_out = at::empty({N, C, topk, 5}, fo);
-  auto cls_cnt = at::zeros({N, C}, io);
-  auto out = at::zeros({N, keep, 7}, fo);
+  // every entry is written by the kernels (the background class's count is never read; the merge
+  // zero-pads each image's rows past its count): no fill kernels in front of them
+  auto cls_cnt = at::empty({N, C}, io);
+  auto out = at::empty({N, keep, 7}, fo);
   auto cnt = at::empty({N}, io);
   vcx_ssd_detect(conf.data_ptr(), loc.data_ptr(), pri.data_ptr<float>(), var.data_ptr<float>(), prob.data_ptr<float>(),
                  cls_out.data_ptr<float>(), cls_cnt.data_ptr<int>(), out.data_ptr<float>(), cnt.data_ptr<int>(),

@@ -1278,6 +1278,7 @@ __global__ void __launch_bounds__(256) ssd_merge_kernel(const float* __restrict_
         d[3] = src[1]; d[4] = src[2]; d[5] = src[3]; d[6] = src[4];
       }
     }
+    for (int i = total * 7 + tid; i < keep * 7; i += 256) on[i] = 0.f;  // zero padding (out is not pre-zeroed)
     if (tid == 0) out_cnt[n] = total;
     return;
   }
