@@ -166,6 +166,40 @@ def test_ordered_sink_any_arrival_order(n, data):
     assert sink.done.is_set() and sink.written == n and not sink.stash
 
 
+class _ManyWriter(_ListWriter):
+    def __init__(self):
+        super().__init__()
+        self.batches = 0
+
+    def write_many(self, fs):
+        self.batches += 1
+        for f in fs:
+            self.write(f)
+
+
+@settings(max_examples=80, deadline=None)
+@given(nchunks=st.integers(min_value=1, max_value=12), csize=st.integers(min_value=1, max_value=9), data=st.data())
+def test_ordered_sink_chunks_any_arrival_order(nchunks, csize, data):
+    """push_many (a received chunk at a time, frames handed to the writer in batches): any chunk order
+    with whole-chunk duplicates writes every frame once, in order."""
+    n = nchunks * csize
+    chunks = [list(range(1 + c * csize, 1 + (c + 1) * csize)) for c in range(nchunks)]
+    order = data.draw(st.permutations(range(nchunks)))
+    dups = data.draw(st.lists(st.sampled_from(range(nchunks)), max_size=6))
+    arrivals = list(order)
+    for d in dups:
+        arrivals.insert(data.draw(st.integers(min_value=0, max_value=len(arrivals))), d)
+    w = _ManyWriter()
+    sink = OrderedSink(lambda width, height: w)
+    sink.set_final(n)
+    for c in arrivals:
+        block = np.stack([np.full((2, 2, 3), k % 256, dtype=np.uint8) for k in chunks[c]])
+        sink.push_many(chunks[c], block)
+    assert w.frames == [k % 256 for k in range(1, n + 1)]
+    assert sink.done.is_set() and sink.written == n and not sink.stash
+    assert w.batches <= nchunks
+
+
 @settings(max_examples=200, deadline=None)
 @given(header=st.one_of(st.text(max_size=200), st.dictionaries(
     st.sampled_from(["msg", "dtype", "shape", "chunk", "x"]),
