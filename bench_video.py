@@ -112,7 +112,7 @@ def bench_y4m_job(args, dev):
     return {k.replace("job_", "job_y4m_"): v for k, v in rec.items() if k != "workers"}
 
 
-def bench_job(args, dev, plane="relay", source=None, out_ext=".y4m"):
+def bench_job(args, dev, plane="relay", source=None, out_ext=".npy"):
     """The whole volunteer job on one GPU: a requester and `workers` volunteers in this process.
     ``relay``: chunk bytes through the coordinator (reference topology); ``p2p``: metadata through
     the coordinator, chunk bytes over pair groups (gloo here: the volunteers share one GPU)."""
@@ -189,8 +189,8 @@ def main():
     ap.add_argument("--job-repeats", type=int, default=3, help="job runs per plane (median reported)")
     ap.add_argument("--no-job", action="store_true")
     ap.add_argument("--uplink-ab", action="store_true",
-                    help="each plane also runs with the requester's two-stage uplink off (VCX_UPLINK_PIPELINE=0), "
-                         "interleaved: keys job[_p2p]_nopipe_*")
+                    help="each plane also runs with the requester's two-stage uplink ON (VCX_UPLINK_PIPELINE=1), "
+                         "interleaved: keys job[_p2p]_pipe_*")
     ap.add_argument("--data-plane", default="both", choices=["relay", "p2p", "both"])
     ap.add_argument("--y4m-frames", type=int, default=0, help="also run the job on a Y4M file of this many frames")
     ap.add_argument("--source", default="npy", choices=["npy", "synthetic"],
@@ -210,18 +210,18 @@ def main():
             from distributedvolunteercomputing_amd import config as vcx_config
 
             planes = ("relay", "p2p") if a.data_plane == "both" else (a.data_plane,)
-            variants = [(pl, pipe) for pl in planes for pipe in ((True, False) if a.uplink_ab else (True,))]
+            variants = [(pl, pipe) for pl in planes for pipe in ((False, True) if a.uplink_ab else (False,))]
             runs = {v: [] for v in variants}
             for _ in range(max(1, a.job_repeats)):
                 for plane, pipe in variants:
                     with vcx_config.override(uplink_pipeline=pipe):
                         r = bench_job(a, dev, plane, source=src)
-                    if not pipe:  # job[_p2p]_* -> job[_p2p]_nopipe_*
+                    if pipe:  # job[_p2p]_* -> job[_p2p]_pipe_*
                         pre = "job" if plane == "relay" else f"job_{plane}"
-                        r = {(pre + "_nopipe" + k[len(pre):] if k.startswith(pre + "_") else k): v for k, v in r.items()}
+                        r = {(pre + "_pipe" + k[len(pre):] if k.startswith(pre + "_") else k): v for k, v in r.items()}
                     runs[(plane, pipe)].append(r)
             for (plane, pipe), rs in runs.items():
-                pre = ("job" if plane == "relay" else f"job_{plane}") + ("" if pipe else "_nopipe")
+                pre = ("job" if plane == "relay" else f"job_{plane}") + ("_pipe" if pipe else "")
                 ok = [r for r in rs if r.get(f"{pre}_frames_per_s")]
                 if not ok:
                     rec.update(rs[-1])

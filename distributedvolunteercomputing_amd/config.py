@@ -57,8 +57,10 @@ class RuntimeConfig:
     # gloo groups only -- with RCCL at 8 ranks on one card it broke the members, profiles/
     # r4_rccl8_rehearsal_1gpu.txt), "all", or "off"
     elastic_stage_joins: str = "gloo"
-    # VCX_UPLINK_PIPELINE: the requester packs / resizes chunk k+1 while a wire thread ships chunk k
-    uplink_pipeline: bool = True
+    # VCX_UPLINK_PIPELINE: the requester packs / resizes chunk k+1 while a wire thread ships chunk k.
+    # Off: measured slower on the one-GPU box (relay 4241 vs 5469, p2p 3330 vs 4936 frames/s, same box,
+    # interleaved; profiles/r4_video_job_spans.txt) -- the extra thread's copies contend with the sink's
+    uplink_pipeline: bool = False
     store_port_train: int = 29611  # VCX_STORE_PORT (train CLI): rendezvous store port
     store_port_video: int = 29612  # VCX_STORE_PORT (video CLI): job-control store port
     # ---- observability

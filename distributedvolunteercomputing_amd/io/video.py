@@ -333,12 +333,17 @@ class NpyWriter:
         self.frames = 0
 
     def write(self, frame):
-        self.frames_list.append(np.array(frame, copy=True))
+        self.frames_list.append(np.array(frame, copy=True)[None])
         self.frames += 1
+
+    def write_many(self, frames):
+        """A received chunk's frames: one block copy (consecutive views of the chunk buffer) or a stack."""
+        self.frames_list.append(np.array(_as_block(frames), copy=True))
+        self.frames += len(frames)
 
     def release(self):
         if self.frames_list is not None:
-            np.save(self.path, np.stack(self.frames_list) if self.frames_list else np.zeros((0, 0, 0, 3), np.uint8))
+            np.save(self.path, np.concatenate(self.frames_list) if self.frames_list else np.zeros((0, 0, 0, 3), np.uint8))
             self.frames_list = None
 
 

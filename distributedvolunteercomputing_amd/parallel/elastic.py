@@ -301,6 +301,7 @@ class ElasticMembership:
         self.stage_joins = sj == "all" or (sj == "gloo" and backend == "gloo")
         self.last_go_wait_ms = 0.0
         self._staged = None  # (gen, members, newcomers, njoin, group) agreed, built in the background
+        self._retired: list = []  # groups replaced by a staged generation, shut down after its first commit
         if backend == "nccl":
             # abortable (non-blocking) RCCL communicator init for every generation's group
             os.environ.setdefault("TORCH_NCCL_USE_COMM_NONBLOCKING", "1")
@@ -506,6 +507,7 @@ class ElasticMembership:
         self.stop_heartbeat()
         self._drop_group()
         self._drop_staged()
+        self._release_retired()
 
     # ------------------------------------------------------------------ rounds
     def sync_round(self):
@@ -582,6 +584,7 @@ class ElasticMembership:
             yield
             _dbg(self.pid, f"guard {self.gen}/{tag}: commit")
             self._commit(tag)
+            self._release_retired()
             st = self._staged
             if st is not None and not st[4]._connected and st[4]._bg is None:
                 st[4].start_connect()  # the staged generation builds during the local steps
@@ -818,15 +821,26 @@ class ElasticMembership:
             time.sleep(self.poll_s)
         self.last_go_wait_ms = (time.time() - t0) * 1e3
 
-    def _drop_group(self):
+    def _drop_group(self, defer: bool = False):
         with self._lock:
             grp, self.group = self.group, None
             self._armed = False
-        if grp is not None:
+        if grp is None:
+            return
+        if defer:
+            # switching to a staged generation whose RCCL init may still be running: destroying
+            # the old communicator now blocked inside ncclCommDestroy at 8 ranks (stacks in
+            # gpurun_out/i/rejoin_n8_staged.log); it is released after the next committed round
+            self._retired.append(grp)
+        else:
             grp.shutdown()
 
+    def _release_retired(self):
+        while self._retired:
+            self._retired.pop().shutdown()
+
     def _adopt(self, g, members, newcomers, njoin):
-        self._drop_group()
+        self._drop_group(defer=self._staged is not None and self._staged[0] == g)
         with self._lock:
             self._abort.clear()
             self._abort_reason = ""
