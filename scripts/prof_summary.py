@@ -7,10 +7,13 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 idx = [i for i, r in enumerate(rows) if "adamw_flat" in r["Kernel_Name"]]
 a, b = idx[-2] + 1, idx[-1] + 1
-KEYS = ["attn_fwd", "attn_bwd_dq", "attn_bwd_dkdv", "attn_bwd_delta", "ln_fwd", "ln_bwd", "bias_gelu_fwd",
-        "bias_gelu_bwd", "xent_fwd", "xent_bwd", "embed_fwd", "embed_bwd", "colsum", "adamw", "grad_sumsq",
-        "reduce_kernel", "elementwise", "copyBuffer", "fillBuffer", "adam_prologue", "splitk_reduce", "xent_fused",
-        "gemm_ps_kernel", "gemm_nt_kernel", "transpose_bf16"]
+# first match wins: specific names before the generic ones they contain ("splitk_reduce_kernel" is ours,
+# "reduce_kernel" alone is torch's)
+KEYS = ["attn_hm_fwd", "attn_hm_dq", "attn_hm_dkv", "attn_fwd", "attn_bwd_dq", "attn_bwd_dkdv", "attn_bwd_delta",
+        "ln_fwd", "ln_bwd", "bias_gelu_fwd", "bias_gelu_bwd", "xent_fwd", "xent_bwd", "embed_fwd", "embed_bwd",
+        "colsum", "adamw", "grad_sumsq", "splitk_reduce", "psgd_", "swiglu", "rope_qkv", "FillFunctor",
+        "distribution_elementwise", "reduce_kernel", "elementwise", "copyBuffer", "fillBuffer", "adam_prologue",
+        "xent_fused", "gemm_ps_kernel", "gemm_nt_kernel", "transpose_bf16", "bn_", "stats_kernel", "apply_kernel"]
 
 
 def short(n):
