@@ -15,5 +15,6 @@ step bench1 300 python -u bench.py
 step bench2 300 python -u bench.py
 step detprof 200 bash scripts/gpu_det_prof.sh
 step video_ab 480 python -u bench_video.py --frames 30000 --source-frames 3000 --job-repeats 3 --data-plane both --uplink-ab
+step cfg5_prof 480 bash scripts/gpu_r4_k.sh
 R="python -u bench_drop.py --peers 8 --backend nccl --model gpt2 --batch 2 --seq 256 --steps 16 --warmup 4 --fault collective --drop-peers 6,7 --rejoin --lease 2.0 --timeout 120"
 step rejoin_n8_staged 200 env VCX_ELASTIC_STAGE_JOINS=all VCX_ELASTIC_DEBUG=1 $R --json-out $O/rejoin_n8_staged.json
