@@ -189,8 +189,8 @@ def main():
     ap.add_argument("--job-repeats", type=int, default=3, help="job runs per plane (median reported)")
     ap.add_argument("--no-job", action="store_true")
     ap.add_argument("--uplink-ab", action="store_true",
-                    help="each plane also runs with the requester's two-stage uplink ON (VCX_UPLINK_PIPELINE=1), "
-                         "interleaved: keys job[_p2p]_pipe_*")
+                    help="each plane runs with the requester's two-stage uplink off and on (VCX_UPLINK_PIPELINE=off/all), "
+                         "interleaved: keys job[_p2p]_* (off) and job[_p2p]_pipe_* (on)")
     ap.add_argument("--data-plane", default="both", choices=["relay", "p2p", "both"])
     ap.add_argument("--y4m-frames", type=int, default=0, help="also run the job on a Y4M file of this many frames")
     ap.add_argument("--source", default="npy", choices=["npy", "synthetic"],
@@ -210,11 +210,12 @@ def main():
             from distributedvolunteercomputing_amd import config as vcx_config
 
             planes = ("relay", "p2p") if a.data_plane == "both" else (a.data_plane,)
-            variants = [(pl, pipe) for pl in planes for pipe in ((False, True) if a.uplink_ab else (False,))]
+            variants = [(pl, pipe) for pl in planes for pipe in ((False, True) if a.uplink_ab else (None,))]
             runs = {v: [] for v in variants}
             for _ in range(max(1, a.job_repeats)):
                 for plane, pipe in variants:
-                    with vcx_config.override(uplink_pipeline=pipe):
+                    mode = vcx_config.get().uplink_pipeline if pipe is None else ("all" if pipe else "off")
+                    with vcx_config.override(uplink_pipeline=mode):
                         r = bench_job(a, dev, plane, source=src)
                     if pipe:  # job[_p2p]_* -> job[_p2p]_pipe_*
                         pre = "job" if plane == "relay" else f"job_{plane}"

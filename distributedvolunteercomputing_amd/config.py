@@ -57,10 +57,11 @@ class RuntimeConfig:
     # gloo groups only -- with RCCL at 8 ranks on one card it broke the members, profiles/
     # r4_rccl8_rehearsal_1gpu.txt), "all", or "off"
     elastic_stage_joins: str = "gloo"
-    # VCX_UPLINK_PIPELINE: the requester packs / resizes chunk k+1 while a wire thread ships chunk k.
-    # Off: measured slower on the one-GPU box (relay 4241 vs 5469, p2p 3330 vs 4936 frames/s, same box,
-    # interleaved; profiles/r4_video_job_spans.txt) -- the extra thread's copies contend with the sink's
-    uplink_pipeline: bool = False
+    # VCX_UPLINK_PIPELINE: the requester packs / resizes chunk k+1 while a wire thread ships chunk k:
+    # "relay" (default: the relay plane only -- same-box A/B with the npy sink, relay 6463 vs 5506,
+    # p2p 4650 vs 6101 frames/s: on the p2p plane the wire stage ships only metadata and the extra
+    # thread's host copies just contend; profiles/r4_video_job_spans.txt), "all", or "off"
+    uplink_pipeline: str = "relay"
     store_port_train: int = 29611  # VCX_STORE_PORT (train CLI): rendezvous store port
     store_port_video: int = 29612  # VCX_STORE_PORT (video CLI): job-control store port
     # ---- observability
@@ -90,13 +91,14 @@ _ENV = {
     "elastic_debug": ("VCX_ELASTIC_DEBUG", _bool),
     "elastic_liveness": ("VCX_ELASTIC_LIVENESS", _bool),
     "elastic_stage_joins": ("VCX_ELASTIC_STAGE_JOINS", str),
-    "uplink_pipeline": ("VCX_UPLINK_PIPELINE", _bool),
+    "uplink_pipeline": ("VCX_UPLINK_PIPELINE", str),
     "store_port_train": ("VCX_STORE_PORT", int),
     "store_port_video": ("VCX_STORE_PORT", int),
     "trace_dir": ("VCX_TRACE_DIR", str),
     "metrics_dir": ("VCX_METRICS_DIR", str),
 }
-_CHOICES = {"gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "all", "off")}
+_CHOICES = {"gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "all", "off"),
+            "uplink_pipeline": ("relay", "all", "off")}
 
 _lock = threading.Lock()
 

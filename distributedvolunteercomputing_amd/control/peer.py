@@ -291,7 +291,8 @@ class client:  # noqa: N801 (reference class name)
                 else:
                     chunk = np.stack(frames) if block is None else np.ascontiguousarray(block)
             info = f"{self.my_ip}||request||{'-'.join(map(str, nums))}||{chunk.shape[1]}||{chunk.shape[2]}"
-            if config.get().uplink_pipeline:
+            up = config.get().uplink_pipeline
+            if up == "all" or (up == "relay" and self.plane is None):
                 self.wire_q.put((info, chunk))  # in order: one wire thread
             else:
                 self._ship(info, chunk)
