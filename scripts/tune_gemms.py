@@ -21,7 +21,7 @@ out_csv = sys.argv[1] if len(sys.argv) > 1 else RESULTS
 
 work = tempfile.mkdtemp(prefix="vcx_tune_")
 # start from the committed results: only shapes without an entry are tuned
-shutil.copyfile(RESULTS, os.path.join(work, "results0.csv"))
+shutil.copyfile(RESULTS, os.path.join(work, "results0.csv"))  # read at start: tuned shapes are skipped
 os.environ["PYTORCH_TUNABLEOP_ENABLED"] = "1"
 os.environ["PYTORCH_TUNABLEOP_TUNING"] = "1"
 os.environ["PYTORCH_TUNABLEOP_FILENAME"] = os.path.join(work, "results%d.csv")
@@ -51,10 +51,16 @@ for name, (N, K) in shapes.items():
     print(f"tuned {name}", flush=True)
     del x, w, dy, gw
     torch.cuda.empty_cache()
-torch.cuda.tunable.write_file()
-src = os.path.join(work, "results0.csv")
-old = set(open(RESULTS).read().splitlines()) if os.path.exists(RESULTS) else set()
-new = [ln for ln in open(src).read().splitlines() if ln and ln not in old and not ln.startswith("Validator")]
+# the results file is only written when TunableOp shuts down: take the in-memory results instead
+res = torch.cuda.tunable.get_results()
+lines = open(RESULTS).read().splitlines() if os.path.exists(RESULTS) else []
+have = {tuple(ln.split(",")[:2]) for ln in lines if ln and not ln.startswith("Validator")}
+new = []
+for r in res:
+    op, params, kern, t = r[0], r[1], r[2], r[3]
+    if (op, params) not in have:
+        new.append(f"{op},{params},{kern},{t}")
 print(f"{len(new)} new entries:", *new, sep="\n", flush=True)
-shutil.copyfile(src, out_csv)
+with open(out_csv, "w") as f:
+    f.write("\n".join(lines + new) + "\n")
 print(f"wrote {out_csv}", flush=True)
