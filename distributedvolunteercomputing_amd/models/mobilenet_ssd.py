@@ -253,7 +253,15 @@ class SSDExecutor:
                 plan.append(("nhwc", l, {}))
             elif l.type == "Concat" and i in concat_cols:
                 plan.append(("concat_buf", l, {"index": i}))
-            elif l.type in ("Flatten", "Concat", "PriorBox", "Reshape", "Softmax", "DetectionOutput"):
+            elif l.type == "DetectionOutput":
+                # parameters parsed once here, not on every chunk between the last head and the detect launch
+                dp = lambda k, d: l.p("detection_output_param", k, d)  # noqa: E731
+                nms = lambda k, d: l.sub("detection_output_param", "nms_param", k, d)  # noqa: E731
+                plan.append(("detectionoutput", l, dict(
+                    nc=int(dp("num_classes", 21)), bg=int(dp("background_label_id", 0)),
+                    conf=float(dp("confidence_threshold", 0.01)), nms=float(nms("nms_threshold", 0.45)),
+                    top_k=int(nms("top_k", 100)), keep=int(dp("keep_top_k", 100)))))
+            elif l.type in ("Flatten", "Concat", "PriorBox", "Reshape", "Softmax"):
                 plan.append((l.type.lower(), l, {}))
             else:
                 raise NotImplementedError(f"Caffe layer type {l.type!r} ({l.name})")
@@ -449,18 +457,13 @@ class SSDExecutor:
                     main.wait_stream(side)  # every head has written the concat buffers
                     forked = False
                 loc, conf, pri = (t[b] for b in l.bottoms)
-                dp = lambda k, d: l.p("detection_output_param", k, d)  # noqa: E731
                 P = pri.shape[-1] // 4
-                nc = int(dp("num_classes", 21))
+                nc = p["nc"]
                 cached = next((v for k, v in self._prior_cache.items() if k[0] == "cat" and v[0] is pri), None)
                 boxes, var = (cached[1], cached[2]) if cached is not None else (pri[0, 0], pri[0, 1])
                 dets, cnt = V.ssd_detect(conf.reshape(N, P * nc), loc.reshape(N, P * 4), boxes, var,
-                                         num_classes=nc, background=int(dp("background_label_id", 0)),
-                                         conf_thresh=float(dp("confidence_threshold", 0.01)),
-                                         nms_thresh=float(l.sub("detection_output_param", "nms_param",
-                                                                "nms_threshold", 0.45)),
-                                         top_k=int(l.sub("detection_output_param", "nms_param", "top_k", 100)),
-                                         keep_top_k=int(dp("keep_top_k", 100)))
+                                         num_classes=nc, background=p["bg"], conf_thresh=p["conf"],
+                                         nms_thresh=p["nms"], top_k=p["top_k"], keep_top_k=p["keep"])
                 t[top] = (dets, cnt)
         if forked:
             main.wait_stream(side)
