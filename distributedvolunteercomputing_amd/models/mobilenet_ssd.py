@@ -116,13 +116,6 @@ def _round_up(n, a):
     return (n + a - 1) // a * a
 
 
-def _nt_tail_bound(M: int, N: int, cus: int = 256) -> bool:
-    """gemm_nt's 256 x 256 tiles for [M, N] end in a last wave that occupies at most a quarter of the CUs
-    (and there is more than one wave): the wave-quantisation case of the detector's 19^2 pointwise layers."""
-    tiles = -(-M // 256) * -(-N // 256)
-    return tiles > cus and 0 < tiles % cus <= cus // 4
-
-
 class SSDExecutor:
     def __init__(self, net: NetDef | str | None = None, caffemodel: str | None = None, device="cpu", seed: int = 0):
         if net is None:
@@ -140,9 +133,8 @@ class SSDExecutor:
         # 1.31-1.33 ms per 100-frame chunk: the GPU, not the host, is the bound), and a capture
         # inside the multi-threaded volunteer job was invalidated by the other threads' GPU calls
         self.use_graph = os.environ.get("VCX_VISION_GRAPH", "0") == "1"
-        # nt: gemm_nt (256 x 256 tiles) where it applies | vision: the 128 x 128-tile vision GEMM |
-        # auto: gemm_nt unless its last wave of tiles would leave most of the 256 CUs idle (M = 36100 at
-        # 19^2: 284 tiles = 1.1 waves), where the smaller tiles' 4.4 waves finish sooner
+        # nt: gemm_nt (256 x 256 tiles) where it applies | vision: the 128 x 128-tile vision GEMM (1.197 vs
+        # 1.171 ms per chunk; gemm_nt only where its last tile wave is short: 1.177, profiles/r4_detector_chunk.txt)
         self.pw_gemm = os.environ.get("VCX_VISION_PW", "nt")
         self._graphs = {}
         self._sides = {}
@@ -412,8 +404,7 @@ class SSDExecutor:
                 M = N * H * W
                 K, Co = x.shape[-1], p["w"].shape[0]
                 epi = 4 if p["relu"] else 1
-                use_nt = self.pw_gemm == "nt" or (self.pw_gemm == "auto" and not _nt_tail_bound(M, Co))
-                if use_nt and ops.native().gemm_nt_supported_epi(M, Co, K, epi):
+                if self.pw_gemm == "nt" and ops.native().gemm_nt_supported_epi(M, Co, K, epi):
                     # the wide pointwise layers (K, Cout >= 256) on the training GEMM: 256 x 256
                     # tiles, LDS-DMA ring, bias(+ReLU) epilogue, ragged M
                     y = torch.empty(M, Co, device=x.device, dtype=torch.bfloat16)
