@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
                                                                float* __restrict__ delta, bf16* __restrict__ dqkv,
                                                                float* __restrict__ bpart,
                                                                int B, int T, int H, float scale, float scale_log2,
-                                                               int staged_epi, int order) {
+                                                               int staged_epi) {
   // one shared object per buffer (see the forward): [K | V] tiles, swizzled (swz)
   __shared__ __attribute__((aligned(16))) bf16 sKV0[2][A_BK * AD];
   __shared__ __attribute__((aligned(16))) bf16 sKV1[2][A_BK * AD];
@@ -211,10 +211,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
   const int nqt = (T + A_BQ - 1) / A_BQ;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  // order 0: a (batch, head)'s query tiles side by side, heaviest first; order 1: all heaviest tiles first
-  const int nbh = gridDim.x / nqt;
-  const int qt = nqt - 1 - (order ? lb / nbh : lb % nqt);
-  const int bh = order ? lb % nbh : lb / nqt;
+  const int qt = nqt - 1 - (lb % nqt);
+  const int bh = lb / nqt;
   const int b = bh / H, hh = bh % H;
   const int64_t tok = 3ll * H * AD;
   const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
@@ -383,7 +381,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
                                                                  const float* __restrict__ delta,
                                                                  bf16* __restrict__ dqkv, float* __restrict__ bpart,
                                                                  int B, int T, int H, float scale, float scale_log2,
-                                                                 int staged_epi, int order) {
+                                                                 int staged_epi) {
   // one shared object per buffer (see the forward): [Q | dO] tiles, swizzled (swz)
   __shared__ __attribute__((aligned(16))) bf16 sQD0[2][B_BQ * AD];
   __shared__ __attribute__((aligned(16))) bf16 sQD1[2][B_BQ * AD];
@@ -394,11 +392,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
   const int nkb = (T + 127) / 128;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  // order 0: the key blocks of one (batch, head) side by side (they share its Q / dO rows in L2);
-  // order 1: every (batch, head)'s heaviest key block first, the lightest last (a shorter tail)
-  const int nbh = gridDim.x / nkb;
-  const int kbi = order ? lb / nbh : lb % nkb;
-  const int bh = order ? lb % nbh : lb / nkb;
+  const int kbi = lb % nkb;  // light (late) key blocks last
+  const int bh = lb / nkb;
   const int b = bh / H, hh = bh % H;
   const int64_t tok = 3ll * H * AD;
   const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
@@ -574,11 +569,6 @@ static int g_fwd_wpe = 3, g_fwd_dma = 1, g_bwd_dma = 1;  // g_bwd_dma bit 0: dQ 
 // stores. Bench shape, same box (profiles/r1_attn_variants.log): backward 0.589 vs 0.614 ms, forward
 // within noise (0.201-0.212 vs 0.206-0.208)
 static int g_stage_epi = 1;
-// backward block order (order argument of the dQ / dK-dV kernels); VCX_ATTN_BWD_ORDER
-static int g_bwd_order = [] {
-  const char* e = getenv("VCX_ATTN_BWD_ORDER");
-  return e ? atoi(e) : 0;
-}();
 
 void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma, int stage_epi) {
   if (fwd_wpe == 2 || fwd_wpe == 3) g_fwd_wpe = fwd_wpe;
@@ -597,19 +587,19 @@ void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const 
   if (g_bwd_dma & 1)
     hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, true>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale,
-                       scale * LOG2E, g_stage_epi, g_bwd_order);
+                       scale * LOG2E, g_stage_epi);
   else
     hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, false>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale,
-                       scale * LOG2E, g_stage_epi, g_bwd_order);
+                       scale * LOG2E, g_stage_epi);
   if (g_bwd_dma & 2)
     hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, true>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E,
-                       g_stage_epi, g_bwd_order);
+                       g_stage_epi);
   else
     hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, false>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E,
-                       g_stage_epi, g_bwd_order);
+                       g_stage_epi);
 }
 
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s) {
