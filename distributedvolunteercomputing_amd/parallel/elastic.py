@@ -130,6 +130,10 @@ class _ThreadStores:
         return getattr(self.client(), name)
 
 
+class _NoHello(ConnectionError):
+    """A liveness connect reached something that is not the member's listener (no / wrong hello)."""
+
+
 class _Liveness:
     """Process-death detector (see the module docstring): a listening socket whose accepted
     connections are held open (our death = their EOF) and one outgoing connection per other
@@ -161,8 +165,17 @@ class _Liveness:
                 c, _ = self.srv.accept()
             except OSError:
                 return
+            try:  # the hello that makes the connector's link count as established (see _connect)
+                c.sendall(self._hello(self.pid))
+            except OSError:
+                c.close()
+                continue
             with self._lock:
                 self._held.append(c)
+
+    @staticmethod
+    def _hello(pid: int) -> bytes:
+        return f"vcxlive {pid}\n".encode()
 
     def address_of(self, m: int) -> str | None:
         key = f"{_P}live/{m}"
@@ -195,15 +208,32 @@ class _Liveness:
         host, _, port = addr.rpartition(":")
         try:
             c = socket.create_connection((host, int(port)), timeout=2.0)
-            c.settimeout(None)
+            try:
+                # established = member m's listener answered with its hello: a middlebox that accepts
+                # and closes (or a stranger now on that port) is a failed connect, never a death
+                want, buf = self._hello(m), b""
+                while len(buf) < len(want):
+                    part = c.recv(len(want) - len(buf))
+                    if not part:
+                        raise _NoHello(f"closed before the liveness hello ({buf!r})")
+                    buf += part
+                if buf != want:
+                    raise _NoHello(f"unexpected liveness hello {buf!r}")
+                c.settimeout(None)
+            except OSError:
+                c.close()
+                raise
         except OSError as e:
             with self._lock:
                 self.connect_failures += 1
                 if self._trying.get(m, (None,))[0] == addr:
                     self._trying[m] = (addr, time.time())  # retried after retry_s; not a death
             _dbg(self.pid, f"liveness connect to peer {m} at {addr} failed ({e!r}); lease-only until it succeeds")
-            if isinstance(e, ConnectionRefusedError) and self.on_refused is not None:
-                self.on_refused(m, addr)  # a hint only: the membership also checks its heartbeat
+            # refused, or accepted and then closed / reset without the hello (the member died between
+            # its kernel's accept and its listener's hello -- or a middlebox): a hint only, the
+            # membership declares the death only if the member's heartbeat also stands still
+            if isinstance(e, (ConnectionRefusedError, ConnectionResetError, _NoHello)) and self.on_refused is not None:
+                self.on_refused(m, addr)
             return
         with self._lock:
             if self._stop.is_set():

@@ -111,8 +111,9 @@ def test_sigkilled_peer_dropped_by_liveness_eof_not_lease():
 
 def test_unreachable_liveness_address_is_not_a_death():
     """a member whose published liveness address cannot be reached (wrong route,
-    firewall, nobody listening) must not be declared dead -- only an EOF on an established
-    connection is; the caller (the heartbeat thread) must not block on the connect either."""
+    firewall, nobody listening, or something that accepts and closes) must not be declared dead --
+    only an EOF on an established connection (the member's listener sent its hello) is; the caller
+    (the heartbeat thread) must not block on the connect either."""
     from distributedvolunteercomputing_amd.parallel.elastic import _P, ElasticMembership, _Liveness
 
     port = _mp.free_port()
@@ -132,6 +133,33 @@ def test_unreachable_liveness_address_is_not_a_death():
         live.watch([0, 1, 2])  # a retry inside retry_s is skipped, never an EOF
         time.sleep(0.3)
         assert live.connect_failures >= 1
+        assert eofs == []
+        # something that accepts and closes at once (a middlebox, or a stranger now on that port):
+        # no liveness hello, so a failed connect -- not an established link whose EOF is a death
+        import socket
+        import threading
+
+        box = socket.socket()
+        box.bind(("127.0.0.1", 0))
+        box.listen(8)
+
+        def _accept_close():
+            while True:
+                try:
+                    c, _ = box.accept()
+                except OSError:
+                    return
+                c.close()
+
+        threading.Thread(target=_accept_close, daemon=True).start()
+        store.set(f"{_P}live/4", f"127.0.0.1:{box.getsockname()[1]}")
+        n0 = live.connect_failures
+        live.watch([4])
+        deadline = time.time() + 5
+        while live.connect_failures == n0 and time.time() < deadline:
+            time.sleep(0.02)
+        box.close()
+        assert live.connect_failures > n0 and 4 not in live._conn
         assert eofs == []
         # a reachable member is connected, and its death is still an EOF
         other = _Liveness(store, 3, "127.0.0.1", lambda m, a: None)
