@@ -1,0 +1,17 @@
+# round 4, GPU call U (after the liveness hello change): the whole GPU test suite, smoke(), two 1-GPU bench runs, and the 8-rank
+# RCCL rehearsal of the driver's multi-GPU path (bench direct, drop inside the all-to-all, kill-2-then-rejoin).
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/u || exit 1
+O=gpurun_out/u
+step() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  echo "== $name $(date +%T)" >> $O/summary.txt
+  timeout -k 10 "$secs" "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> $O/summary.txt
+  [ $rc -le 1 ] || exit $rc
+}
+step gpu_suite 600 python -u -m pytest -q --timeout 120 --timeout-method thread tests/ -m gpu
+step smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
+step bench1 240 python -u bench.py
+step bench2 240 python -u bench.py
+ONLY="bench_n8_direct drop_collective_n8 drop_kill2_rejoin_n8" step rccl8 900 bash scripts/gpu_rccl8_rehearsal.sh
