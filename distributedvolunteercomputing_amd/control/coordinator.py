@@ -85,9 +85,9 @@ class coordinator:  # noqa: N801  (reference class name)
         # here so that ANY training peer may die without taking the membership state with it.
         # Access control: torch's TCPStore listens on every interface and has no authentication,
         # so every key the peers use lives under a per-coordinator random prefix (`store_secret`)
-        # that is handed out only to joined volunteers (the `join` reply) and to admitted training
-        # peers (`tjoin`, optionally gated by `train_token`); the `store` verb is refused to anyone
-        # else. A host that can reach the port but never joined cannot name, so cannot forge, the
+        # that is handed out only to admitted training peers (`tjoin`, optionally gated by
+        # `train_token`) and, in a job without a token, to joined volunteers (the `store` verb); the
+        # `store` verb is refused to anyone else. A host that can reach the port but never joined cannot name, so cannot forge, the
         # abort / join / pair-hello records the peers act on (the reference binds every interface
         # with no auth at all: /root/reference/server.py:96).
         # Two prefixes: `store_secret` (the training membership keys) and `p2p_secret` (the chunk
