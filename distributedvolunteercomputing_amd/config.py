@@ -45,6 +45,10 @@ class RuntimeConfig:
     colour_native: bool = True  # VCX_COLOUR_NATIVE: video BGR<->YUV in the C++ runtime (False: numpy)
     resnet_conv1x1: str = "gemm"  # VCX_RESNET_CONV1X1: ResNet 1x1 convolutions as GEMMs on the NHWC view ("gemm")
     # or through the convolution library ("conv")
+    # VCX_CONV_FIND: library (MIOpen) convolutions of the ResNets pick the fastest solver per shape by
+    # timing them on first use (torch.backends.cudnn.benchmark) instead of the immediate-mode heuristic:
+    # ResNet-50 config 3 6886-7011 vs 6593 img/s (profiles/r4_resnet50_ab.txt); costs seconds once per shape
+    conv_find: bool = True
     resnet_bn: str = "fused"  # VCX_RESNET_BN: ResNet train-mode BatchNorm (+ add) + ReLU as fused HIP passes ("fused")
     # or the torch composition ("torch")
     # ---- distributed / control plane
@@ -76,6 +80,7 @@ _ENV = {
     "dgrad_ps": ("VCX_DGRAD_PS", _bool),
     "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
     "resnet_bn": ("VCX_RESNET_BN", str),
+    "conv_find": ("VCX_CONV_FIND", _bool),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),
     "gemm_select": ("VCX_GEMM_SELECT", _bool),
     "wgrad_big_split_min_m": ("VCX_WGRAD_BIG_SPLIT_MIN_M", int),

@@ -4,6 +4,8 @@
 // with torch streams and hipGraph capture.
 #include <torch/extension.h>
 #include <map>
+#include <mutex>
+#include <tuple>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
@@ -206,12 +208,27 @@ void gemm_ps_diag(at::Tensor a, at::Tensor b, at::Tensor c, int64_t epi, int64_t
                    (int)policy, sp, (int)grid_cap, (int)stagger, cur_stream());
 }
 
+// The zero-at-rest workspace of the BN kernels: fp32 [2C] atomic sums, zeroed once here and zeroed again
+// by the finalize kernel of every call. One per (device, stream, C): launches on one stream are
+// ordered, so the layers of a model can share it.
+static float* bn_workspace(const at::Tensor& x, int64_t C) {
+  static std::mutex mu;
+  // never destroyed: no device free during static destruction at interpreter exit
+  static auto* cache = new std::map<std::tuple<int, uintptr_t, int64_t>, at::Tensor>();
+  const auto key = std::make_tuple((int)x.get_device(), (uintptr_t)cur_stream(), C);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache->find(key);
+  if (it == cache->end()) it = cache->emplace(key, at::zeros({2 * C}, x.options().dtype(at::kFloat))).first;
+  return it->second.data_ptr<float>();
+}
+
 // Train-mode BatchNorm (+ residual) (+ ReLU) on NHWC bf16 activations (batchnorm.hip). x / res / y:
 // contiguous [..., C] (the NHWC view of a channels-last tensor); gamma / beta bf16 [C]; running stats
-// bf16 or fp32 [C], updated in place (skipped when undefined). Returns y, mean, rstd, scale (fp32 [C]).
+// bf16 or fp32 [C], updated in place (skipped when undefined); nbt: the layer's num_batches_tracked
+// (int64, incremented on the device) or None. Returns y, mean, rstd, scale (fp32 [C]).
 std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma, at::Tensor beta,
                                      c10::optional<at::Tensor> run_mean, c10::optional<at::Tensor> run_var, double eps,
-                                     double momentum, bool relu) {
+                                     double momentum, bool relu, c10::optional<at::Tensor> nbt) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == at::kBFloat16, "bn: x bf16 contiguous NHWC");
   const int64_t C = x.size(-1), R = x.numel() / C;
   TORCH_CHECK(vcx_bn_supported((int)C) && R > 0, "bn: C must be a power of two in 8..2048");
@@ -228,12 +245,18 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res
     rv = run_var->data_ptr();
     fp32 = run_mean->scalar_type() == at::kFloat;
   }
+  int64_t* nb = nullptr;
+  if (nbt && nbt->defined()) {
+    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1 && nbt->get_device() == x.get_device(),
+                "bn: num_batches_tracked int64 [1] on x's device");
+    nb = nbt->data_ptr<int64_t>();
+  }
   auto f = x.options().dtype(at::kFloat);
-  at::Tensor ws = at::zeros({2 * C}, f), st = at::empty({4, C}, f);
+  at::Tensor st = at::empty({4, C}, f);
   at::Tensor y = at::empty_like(x);
   vcx_bn_fwd_train(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), R, (int)C, gamma.data_ptr(),
-                   beta.data_ptr(), rm, rv, fp32, (float)eps, (float)momentum, ws.data_ptr<float>(), st[0].data_ptr<float>(),
-                   st[1].data_ptr<float>(), st[2].data_ptr<float>(), st[3].data_ptr<float>(), relu ? 1 : 0, cur_stream());
+                   beta.data_ptr(), rm, rv, fp32, (float)eps, (float)momentum, bn_workspace(x, C), st[0].data_ptr<float>(),
+                   st[1].data_ptr<float>(), st[2].data_ptr<float>(), st[3].data_ptr<float>(), nb, relu ? 1 : 0, cur_stream());
   return {y, st[0], st[1], st[2]};
 }
 
@@ -251,8 +274,11 @@ at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor scal
 }
 
 // returns dx, d residual (undefined unless want_dres), dgamma, dbeta (fp32 [C])
+// gw / gb: flat bf16 [C] gradient buffers of gamma / beta that dgamma / dbeta are ADDED into (both or
+// neither); the returned dgamma / dbeta are then for information only
 std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Tensor mean, at::Tensor rstd,
-                               at::Tensor scale, bool relu, bool want_dres) {
+                               at::Tensor scale, bool relu, bool want_dres, c10::optional<at::Tensor> gw,
+                               c10::optional<at::Tensor> gb) {
   TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && x.is_contiguous() && y.is_contiguous() &&
                   dy.sizes() == x.sizes() && y.sizes() == x.sizes() && dy.scalar_type() == at::kBFloat16 &&
                   x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16, "bn_bwd: dy, y, x bf16 NHWC alike");
@@ -260,13 +286,20 @@ std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Te
   TORCH_CHECK(vcx_bn_supported((int)C), "bn: C must be a power of two in 8..2048");
   for (const at::Tensor* t : {&mean, &rstd, &scale})
     TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(), "bn_bwd: stats fp32 [C]");
-  at::Tensor ws = at::zeros({2 * C}, x.options().dtype(at::kFloat));
+  const bool flat = gw && gw->defined();
+  TORCH_CHECK(flat == (gb && gb->defined()), "bn_bwd: gw and gb together");
+  if (flat)
+    for (const at::Tensor* t : {&*gw, &*gb})
+      TORCH_CHECK(t->is_cuda() && t->get_device() == x.get_device() && t->numel() == C && t->is_contiguous() &&
+                      t->scalar_type() == at::kBFloat16, "bn_bwd: gradient buffers bf16 [C]");
+  at::Tensor sums = at::empty({2 * C}, x.options().dtype(at::kFloat));
   at::Tensor dx = at::empty_like(x);
   at::Tensor dres = want_dres ? at::empty_like(x) : at::Tensor();
   vcx_bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-             scale.data_ptr<float>(), R, (int)C, ws.data_ptr<float>(), dx.data_ptr(),
+             scale.data_ptr<float>(), R, (int)C, bn_workspace(x, C), sums.data_ptr<float>(),
+             flat ? gw->data_ptr() : nullptr, flat ? gb->data_ptr() : nullptr, dx.data_ptr(),
              want_dres ? dres.data_ptr() : nullptr, relu ? 1 : 0, cur_stream());
-  return {dx, dres, ws.narrow(0, C, C), ws.narrow(0, 0, C)};
+  return {dx, dres, sums.narrow(0, C, C), sums.narrow(0, 0, C)};
 }
 
 // Weight gradient out[M, N] (+)= a[K, M]^T . b[K, N] (token-major operands) on the hand-written
@@ -748,9 +781,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_ps_supported", &gemm_ps_supported);
   m.def("bn_supported", [](int64_t C) { return vcx_bn_supported((int)C); });
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
-        py::arg("run_mean"), py::arg("run_var"), py::arg("eps"), py::arg("momentum"), py::arg("relu"));
+        py::arg("run_mean"), py::arg("run_var"), py::arg("eps"), py::arg("momentum"), py::arg("relu"),
+        py::arg("nbt") = py::none());
   m.def("bn_apply", &bn_apply);
-  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("mean"), py::arg("rstd"), py::arg("scale"),
+        py::arg("relu"), py::arg("want_dres"), py::arg("gw") = py::none(), py::arg("gb") = py::none());
   m.def("gemm_ps_diag", &gemm_ps_diag, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("epi") = 0,
         py::arg("policy") = 0, py::arg("stamps") = py::none(), py::arg("grid_cap") = 0, py::arg("stagger") = 0);
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),

@@ -2,11 +2,17 @@
 // ResNet-50 of BASELINE config 3 (models/resnet.py). Torch runs each of these as separate passes
 // (batch statistics, normalise, add, ReLU; and in the backward ReLU', statistics of the gradient,
 // input gradient), each reading or writing the whole activation; here:
-//   forward : stats  (read x once: per-channel sum / sum of squares in fp32, block partials + atomics)
-//             finalize (mean, 1/std, the per-channel affine scale/shift, running-stat update)
-//             apply  (read x [+ residual], write y = relu(x * scale + shift [+ residual]))
-//   backward: reduce (read dy, y, x: per-channel sum dz and sum dz * xhat, dz = dy * [y > 0])
-//             dx     (read dy, y, x, write dx [and d residual = dz])
+//   forward : stats    (read x once: per-channel sum / sum of squares in fp32, block partials + atomics)
+//             finalize (mean, 1/std, the per-channel affine scale/shift, running stats, num_batches_tracked)
+//             apply    (read x [+ residual], write y = relu(x * scale + shift [+ residual]))
+//   backward: reduce   (read dy, y, x: per-channel sum dz and sum dz * xhat, dz = dy * [y > 0])
+//             bwd_fin  (the sums for the dx pass; dbeta / dgamma added into the flat bf16 .grad when given)
+//             dx       (read dy, y, x, write dx [and d residual = dz])
+// The atomics accumulate into a zero-at-rest workspace (one per device, stream and C, owned by the
+// binding) that the finalize kernels read and zero again: no fill kernel per call. (A last-block
+// finalize inside the reduction kernels instead -- a ticket counter behind device-scope fences --
+// measured 2x slower reductions, likely the device-scope fence in every block (on the 8-XCD chip it
+// writes back / invalidates the XCD's L2; not profiled further): profiles/r4_resnet50_ab.txt.)
 // Rows R = N * H * W, C channels (a power of two, 8 .. 2048); every lane moves 16 B (8 channels) per
 // access. No reference analog (north-star config 3).
 #include "vcx_common.h"
@@ -74,17 +80,21 @@ __global__ void __launch_bounds__(NT) stats_kernel(const bf16* __restrict__ x, i
 }
 
 // mean, 1/std, scale = gamma/std, shift = beta - mean * scale; running stats (unbiased variance)
-// updated in place in their own dtype (bf16 or fp32)
+// updated in place in their own dtype (bf16 or fp32); num_batches_tracked + 1; ws = [sum | sumsq]
+// zeroed again for the next call
 template <typename RT>
-__global__ void finalize_kernel(const float* __restrict__ sum, const float* __restrict__ sumsq, int64_t R, int C,
-                                const bf16* __restrict__ gamma, const bf16* __restrict__ beta, float eps, float momentum,
-                                RT* __restrict__ run_mean, RT* __restrict__ run_var, float* __restrict__ mean_out,
-                                float* __restrict__ rstd_out, float* __restrict__ scale, float* __restrict__ shift) {
+__global__ void finalize_kernel(float* __restrict__ ws, int64_t R, int C, const bf16* __restrict__ gamma,
+                                const bf16* __restrict__ beta, float eps, float momentum, RT* __restrict__ run_mean,
+                                RT* __restrict__ run_var, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                float* __restrict__ scale, float* __restrict__ shift, int64_t* __restrict__ nbt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) *nbt += 1;
   if (c >= C) return;
   const float inv = 1.f / (float)R;
-  const float m = sum[c] * inv;
-  const float var = fmaxf(sumsq[c] * inv - m * m, 0.f);
+  const float m = ws[c] * inv;
+  const float var = fmaxf(ws[C + c] * inv - m * m, 0.f);
+  ws[c] = 0.f;
+  ws[C + c] = 0.f;
   const float rs = rsqrtf(var + eps);
   const float g = (float)gamma[c], b = (float)beta[c];
   mean_out[c] = m;
@@ -160,6 +170,21 @@ __global__ void __launch_bounds__(NT) bwd_reduce_kernel(const bf16* __restrict__
       sdz, sdzx);
 }
 
+// ws = [sum dz | sum dz xhat] -> sums (for the dx pass and the caller) and, when given, added into the
+// flat bf16 gradients of beta / gamma; ws zeroed again for the next call
+__global__ void bwd_finalize_kernel(float* __restrict__ ws, int C, float* __restrict__ sums, bf16* __restrict__ gw,
+                                    bf16* __restrict__ gb) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float db = ws[c], dg = ws[C + c];
+  ws[c] = 0.f;
+  ws[C + c] = 0.f;
+  sums[c] = db;
+  sums[C + c] = dg;
+  if (gb) gb[c] = (bf16)((float)gb[c] + db);
+  if (gw) gw[c] = (bf16)((float)gw[c] + dg);
+}
+
 // dx = gamma rstd (dz - (sum dz + xhat sum dz xhat) / R); d residual = dz
 template <bool RES, bool RELU>
 __global__ void __launch_bounds__(NT) bwd_dx_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
@@ -217,22 +242,21 @@ using namespace vcx;
 // C a power of two in 8 .. 2048 (the grid-stride loops keep a thread on one channel chunk)
 bool vcx_bn_supported(int C) { return C >= 8 && C <= 2048 && (2048 % C) == 0; }
 
-// forward (train): ws = [sum | sumsq] fp32 [2C] zeroed by the caller; mean/rstd/scale/shift fp32 [C]
+// forward (train): ws = the zero-at-rest workspace, fp32 [2C] (zeroed once by the caller, left zeroed
+// by every call); mean/rstd/scale/shift fp32 [C]; nbt int64 [1] or null
 void vcx_bn_fwd_train(const void* x, const void* res, void* y, int64_t R, int C, const void* gamma, const void* beta,
                       void* run_mean, void* run_var, int run_fp32, float eps, float momentum, float* ws, float* mean,
-                      float* rstd, float* scale, float* shift, int relu, hipStream_t s) {
+                      float* rstd, float* scale, float* shift, int64_t* nbt, int relu, hipStream_t s) {
   using namespace bn;
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
   hipLaunchKernelGGL(stats_kernel, dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
   if (run_fp32)
-    hipLaunchKernelGGL(finalize_kernel<float>, dim3((C + 255) / 256), dim3(256), 0, s, ws, ws + C, R, C,
-                       (const bf16*)gamma, (const bf16*)beta, eps, momentum, (float*)run_mean, (float*)run_var, mean,
-                       rstd, scale, shift);
+    hipLaunchKernelGGL(finalize_kernel<float>, dim3((C + 255) / 256), dim3(256), 0, s, ws, R, C, (const bf16*)gamma,
+                       (const bf16*)beta, eps, momentum, (float*)run_mean, (float*)run_var, mean, rstd, scale, shift, nbt);
   else
-    hipLaunchKernelGGL(finalize_kernel<bf16>, dim3((C + 255) / 256), dim3(256), 0, s, ws, ws + C, R, C,
-                       (const bf16*)gamma, (const bf16*)beta, eps, momentum, (bf16*)run_mean, (bf16*)run_var, mean,
-                       rstd, scale, shift);
+    hipLaunchKernelGGL(finalize_kernel<bf16>, dim3((C + 255) / 256), dim3(256), 0, s, ws, R, C, (const bf16*)gamma,
+                       (const bf16*)beta, eps, momentum, (bf16*)run_mean, (bf16*)run_var, mean, rstd, scale, shift, nbt);
   const int64_t n8 = R * C / 8;
   const int g = grid_for(n8);
   auto go = [&](auto k) {
@@ -259,9 +283,12 @@ void vcx_bn_apply(const void* x, const void* res, void* y, int64_t R, int C, con
     relu ? go(apply_kernel<false, true>) : go(apply_kernel<false, false>);
 }
 
-// backward: ws = [sum dz | sum dz xhat] fp32 [2C] zeroed by the caller (they are also dbeta / dgamma)
+// backward: ws = the zero-at-rest workspace (as in the forward); sums = fp32 [2C] output [sum dz |
+// sum dz xhat] = [dbeta | dgamma]; gw / gb = flat bf16 gradients of gamma / beta that dgamma / dbeta
+// are added into (or null)
 void vcx_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* scale,
-                int64_t R, int C, float* ws, void* dx, void* dres, int relu, hipStream_t s) {
+                int64_t R, int C, float* ws, float* sums, void* gw, void* gb, void* dx, void* dres, int relu,
+                hipStream_t s) {
   using namespace bn;
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
@@ -271,11 +298,12 @@ void vcx_bn_bwd(const void* dy, const void* y, const void* x, const float* mean,
   else
     hipLaunchKernelGGL(bwd_reduce_kernel<false>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const bf16*)y,
                        (const bf16*)x, mean, rstd, R, C, rpb, ws, ws + C);
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, C, sums, (bf16*)gw, (bf16*)gb);
   const int64_t n8 = R * C / 8;
   const int g = grid_for(n8);
   auto go = [&](auto k) {
     hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)dy, (const bf16*)y, (const bf16*)x, mean, rstd, scale,
-                       (const float*)ws, (const float*)(ws + C), (bf16*)dx, (bf16*)dres, n8, C / 8, 1.f / (float)R);
+                       (const float*)sums, (const float*)(sums + C), (bf16*)dx, (bf16*)dres, n8, C / 8, 1.f / (float)R);
   };
   if (dres)
     relu ? go(bwd_dx_kernel<true, true>) : go(bwd_dx_kernel<true, false>);

@@ -102,8 +102,9 @@ void vcx_embed_bwd(const int64_t* idx, const void* dx, float* dwte_scratch, void
 bool vcx_bn_supported(int C);
 void vcx_bn_fwd_train(const void* x, const void* res, void* y, int64_t R, int C, const void* gamma, const void* beta,
                       void* run_mean, void* run_var, int run_fp32, float eps, float momentum, float* ws, float* mean,
-                      float* rstd, float* scale, float* shift, int relu, hipStream_t s);
+                      float* rstd, float* scale, float* shift, int64_t* nbt, int relu, hipStream_t s);
 void vcx_bn_apply(const void* x, const void* res, void* y, int64_t R, int C, const float* scale, const float* shift,
                   int relu, hipStream_t s);
 void vcx_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* scale,
-                int64_t R, int C, float* ws, void* dx, void* dres, int relu, hipStream_t s);
+                int64_t R, int C, float* ws, float* sums, void* gw, void* gb, void* dx, void* dres, int relu,
+                hipStream_t s);

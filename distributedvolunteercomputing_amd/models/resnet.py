@@ -36,7 +36,8 @@ class Conv1x1(nn.Conv2d):
         if self.stride[0] != 1:
             xh = xh[:, ::self.stride[0], ::self.stride[1], :].contiguous()
         N, H, W, C = xh.shape
-        y = linear(xh.reshape(N * H * W, C), self.weight.view(self.out_channels, C))
+        # the [Cout, Cin, 1, 1] parameter itself: its gradient lands in the flat .grad directly
+        y = linear(xh.reshape(N * H * W, C), self.weight)
         return y.view(N, H, W, self.out_channels).permute(0, 3, 1, 2)
 
 
@@ -84,6 +85,8 @@ class ResNet(nn.Module):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
 
     def forward(self, x, y=None):
+        if x.is_cuda and config.get().conv_find and not torch.backends.cudnn.benchmark:
+            torch.backends.cudnn.benchmark = True  # process-wide: MIOpen Find for the 3x3 / 7x7 convolutions
         x = bn_act(self.stem(x), self.bn)
         x = F.max_pool2d(x, 3, 2, 1)
         x = self.blocks(x)

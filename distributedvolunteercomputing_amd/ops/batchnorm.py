@@ -13,7 +13,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import config
-from ._lib import native, use_native
+from ._lib import grad_buffer, native, use_native
 
 
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
@@ -21,26 +21,41 @@ def _nhwc(t: torch.Tensor) -> torch.Tensor:
 
 
 class _BNAct(torch.autograd.Function):
+    """The statistics kernel finalizes in its last block (running stats, num_batches_tracked); with
+    preset flat .grad buffers the backward reduction ADDS dgamma / dbeta into them and autograd gets
+    None for gamma / beta (no cast or accumulation kernels per layer)."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, run_mean, run_var, eps, momentum, relu):
+    def forward(ctx, x, weight, bias, residual, run_mean, run_var, eps, momentum, relu, nbt):
         C = native()
         xh = _nhwc(x)
         rh = _nhwc(residual) if residual is not None else None
-        y, mean, rstd, scale = C.bn_fwd_train(xh, rh, weight, bias, run_mean, run_var, eps, momentum, relu)
+        y, mean, rstd, scale = C.bn_fwd_train(xh, rh, weight, bias, run_mean, run_var, eps, momentum, relu, nbt)
         ctx.save_for_backward(xh, y, mean, rstd, scale)
         ctx.relu, ctx.has_res, ctx.pdtype = relu, residual is not None, weight.dtype
+        ctx.params = (weight, bias)
         return y.permute(0, 3, 1, 2)
 
     @staticmethod
     def backward(ctx, dy):
         xh, y, mean, rstd, scale = ctx.saved_tensors
+        weight, bias = ctx.params
+        ctx.params = None
         dyh = _nhwc(dy)
         if not dyh.is_contiguous():
             dyh = dyh.contiguous()
-        dx, dres, dgamma, dbeta = native().bn_bwd(dyh, y, xh, mean, rstd, scale, ctx.relu, ctx.has_res)
+        gw = grad_buffer(weight) if ctx.needs_input_grad[1] else None
+        gb = grad_buffer(bias) if ctx.needs_input_grad[2] else None
+        flat = gw is not None and gb is not None
+        dx, dres, dgamma, dbeta = native().bn_bwd(dyh, y, xh, mean, rstd, scale, ctx.relu, ctx.has_res,
+                                                  gw if flat else None, gb if flat else None)
         dx = dx.permute(0, 3, 1, 2)
         dres = dres.permute(0, 3, 1, 2) if ctx.has_res else None
-        return dx, dgamma.to(ctx.pdtype), dbeta.to(ctx.pdtype), dres, None, None, None, None, None
+        if flat:  # already added into the flat .grad buffers
+            return dx, None, None, dres, None, None, None, None, None, None
+        dg = dgamma.to(ctx.pdtype) if ctx.needs_input_grad[1] else None
+        db = dbeta.to(ctx.pdtype) if ctx.needs_input_grad[2] else None
+        return dx, dg, db, dres, None, None, None, None, None, None
 
 
 def bn_act_ok(x: torch.Tensor, bn: torch.nn.BatchNorm2d) -> bool:
@@ -54,9 +69,13 @@ def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, residual: torch.Tensor | N
     """relu(bn(x) + residual) with `bn`'s parameters and running statistics (train mode)."""
     if bn_act_ok(x, bn) and (residual is None or (residual.dtype == x.dtype and residual.shape == x.shape
                                                   and residual.is_contiguous(memory_format=torch.channels_last))):
-        bn.num_batches_tracked.add_(1)
+        nbt = bn.num_batches_tracked
+        if nbt is None or nbt.device != x.device or nbt.dtype != torch.long or nbt.numel() != 1:
+            nbt = None  # (then counted here, as torch would)
+            if bn.num_batches_tracked is not None:
+                bn.num_batches_tracked.add_(1)
         return _BNAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, bn.momentum,
-                            relu)
+                            relu, nbt)
     y = bn(x)
     if residual is not None:
         y = y + residual

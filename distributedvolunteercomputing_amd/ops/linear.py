@@ -213,9 +213,10 @@ def _param_grads(dy2, x2, w, bias, want_w, want_b):
     gb = grad_buffer(bias) if want_b else None
     if want_w:
         if gw is not None:
-            wgrad(dy2, x2, out=gw, accumulate=True)  # straight into the (flat) .grad; autograd adds nothing
+            # straight into the (flat) .grad; autograd adds nothing
+            wgrad(dy2, x2, out=gw.view(N, -1), accumulate=True)
         else:
-            dw = wgrad(dy2, x2)
+            dw = wgrad(dy2, x2).view(w.shape)
     if want_b:
         if gb is not None and (N % 8) == 0:
             native().colsum_bf16(dy2, gb)  # HIP column sums added into the flat .grad
@@ -226,22 +227,31 @@ def _param_grads(dy2, x2, w, bias, want_w, want_b):
     return dw, db
 
 
+def _w2(w):
+    """The [N, K] matrix of a weight: w itself, or the [N, K] view of a 1x1 convolution's [N, K, 1, 1]."""
+    return w if w.dim() == 2 else w.view(w.shape[0], -1)
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, bias_grad_elsewhere=False):
+        # w: [N, K], or a 1x1 convolution's [N, K, 1, 1] weight itself (not a view of it: its gradient
+        # then goes straight into the parameter's flat .grad, no view-backward + accumulation pass)
         ctx.save_for_backward(x, w)
         # bias_grad_elsewhere: the sole consumer of y computes the bias gradient itself (column
         # sums it already has at hand) and returns it for the same bias tensor
         ctx.has_bias = b is not None and not bias_grad_elsewhere
         ctx.bias = b
         x2 = x.reshape(-1, x.shape[-1])
+        w = _w2(w)
         if gemm_nt_ok(x2.shape[0], w.shape[0], x2.shape[1], x2):
             return gemm_nt(x2, w, b).view(*x.shape[:-1], w.shape[0])
         return mm(x2, w, trans_b=True, bias=b).view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x, w_param = ctx.saved_tensors
+        w = _w2(w_param)
         N, K = w.shape
         dy2 = dy.reshape(-1, N)
         x2 = x.reshape(-1, K)
@@ -261,6 +271,7 @@ class _Linear(torch.autograd.Function):
         want_w = bool(ctx.needs_input_grad[1])
         want_b = bool(ctx.has_bias and ctx.needs_input_grad[2])
         bias, ctx.bias = ctx.bias, None
+        w = w_param  # gradients are formed for the parameter's own shape
         flat_w = w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == w.dtype
         flat_b = (not want_b) or grad_buffer(bias) is not None
         # config.async_wgrad: measured slower (951 vs 966-971 samples/s)
@@ -286,12 +297,13 @@ def native_linear_ok(w: torch.Tensor) -> bool:
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
            bias_grad_elsewhere: bool = False) -> torch.Tensor:
-    """y = x @ w^T (+ b), x [..., K], w [N, K]. With bias_grad_elsewhere the backward leaves the
-    bias gradient to y's consumer (e.g. ``causal_attention(qkv, bias=b)``), which must then be
-    y's only consumer and return d(loss)/d(b) = column sums of dy for the same tensor."""
+    """y = x @ w^T (+ b), x [..., K], w [N, K] (or a 1x1 convolution's [N, K, 1, 1]). With
+    bias_grad_elsewhere the backward leaves the bias gradient to y's consumer (e.g.
+    ``causal_attention(qkv, bias=b)``), which must then be y's only consumer and return
+    d(loss)/d(b) = column sums of dy for the same tensor."""
     if native_linear_ok(w):
         return _Linear.apply(x, w, b, bias_grad_elsewhere)
-    return F.linear(x, w, b)
+    return F.linear(x, _w2(w), b)
 
 
 # ---------------------------------------------------------------- fused GPT-2 MLP

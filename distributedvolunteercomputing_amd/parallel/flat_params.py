@@ -7,6 +7,10 @@ bucket, trivial sharding (contiguous slices) and trivial re-sharding when peers 
 
 Layout: [decayed params (dim >= 2) | non-decayed params (biases, norm gains)], each segment
 aligned to ``ALIGN`` elements (128 B for bf16) so vectorised 16-B accesses never straddle.
+A 4-D parameter that is channels-last (a ResNet convolution after ``.to(memory_format=
+torch.channels_last)``) keeps that layout in its segment: its parameter and gradient views have
+channels-last strides, so the NHWC convolution kernels take the weight and return its gradient
+without a layout copy each way (ResNet-50: ~48 copies per step, profiles/r4_resnet50_ab.txt).
 """
 from __future__ import annotations
 
@@ -31,6 +35,21 @@ class Segment:
     numel: int
     shape: tuple
     decay: bool
+    channels_last: bool = False
+
+
+def _channels_last(p: torch.Tensor) -> bool:
+    """4-D and stored channels-last (and not also plain-contiguous, as 1x1 kernels are both)."""
+    return p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last) and not p.is_contiguous()
+
+
+def segment_view(buf: torch.Tensor, s: Segment) -> torch.Tensor:
+    """Segment `s` of a flat buffer as a tensor of its parameter's shape (and memory format)."""
+    v = buf[s.offset : s.offset + s.numel]
+    if s.channels_last:
+        n, c, h, w = s.shape
+        return v.view(n, h, w, c).permute(0, 3, 1, 2)
+    return v.view(s.shape)
 
 
 class FlatParams:
@@ -50,7 +69,7 @@ class FlatParams:
         off = 0
         for group, is_decay in ((decay, True), (nodecay, False)):
             for n, p in group:
-                self.segments.append(Segment(n, off, p.numel(), tuple(p.shape), is_decay))
+                self.segments.append(Segment(n, off, p.numel(), tuple(p.shape), is_decay, _channels_last(p)))
                 off = _round_up(off + p.numel())
             if is_decay:
                 self.n_decay = off
@@ -63,10 +82,10 @@ class FlatParams:
         with torch.no_grad():
             for s in self.segments:
                 p = byname[s.name]
-                view = self.param[s.offset : s.offset + s.numel].view(s.shape)
+                view = segment_view(self.param, s)
                 view.copy_(p.detach().to(device=device, dtype=dtype))
                 p.data = view
-                p.grad = self.grad[s.offset : s.offset + s.numel].view(s.shape)
+                p.grad = segment_view(self.grad, s)
                 self._params.append(p)
 
     def zero_grad(self):
@@ -75,11 +94,11 @@ class FlatParams:
     def rebind_grads(self):
         """Re-point .grad at the flat buffer (call if something replaced p.grad)."""
         for s, p in zip(self.segments, self._params):
-            p.grad = self.grad[s.offset : s.offset + s.numel].view(s.shape)
+            p.grad = segment_view(self.grad, s)
 
     def state_dict_views(self, flat: torch.Tensor):
         """Name -> view of an arbitrary flat buffer with this layout (for checkpoints)."""
-        return {s.name: flat[s.offset : s.offset + s.numel].view(s.shape) for s in self.segments}
+        return {s.name: segment_view(flat, s) for s in self.segments}
 
     def shard_bounds(self, rank: int, world: int, align: int = ALIGN):
         """Contiguous [lo, hi) slice of the flat space owned by `rank` (ZeRO-style). For world

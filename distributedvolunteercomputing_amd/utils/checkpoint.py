@@ -39,7 +39,7 @@ def _step_dir(root, step):
 def layout_dict(flat) -> dict:
     return {"numel": flat.numel, "n_decay": flat.n_decay,
             "segments": [{"name": s.name, "offset": s.offset, "numel": s.numel, "shape": list(s.shape),
-                          "decay": s.decay} for s in flat.segments]}
+                          "decay": s.decay, "channels_last": s.channels_last} for s in flat.segments]}
 
 
 def save_checkpoint(trainer, root: str, step: int, *, peer_id: int, is_writer: bool, members=None,
@@ -138,3 +138,7 @@ class ShardReader:
         if have["numel"] != want["numel"] or [s["name"] for s in have["segments"]] != [s["name"] for s in
                                                                                     want["segments"]]:
             raise ValueError("checkpoint flat layout does not match this model")
+        # a segment's element order follows its parameter's memory format (flat_params.segment_view)
+        fmt = [(s["name"], bool(s.get("channels_last", False))) for s in have["segments"]]
+        if fmt != [(s["name"], s["channels_last"]) for s in want["segments"]]:
+            raise ValueError("checkpoint parameter memory formats (channels-last) do not match this model")

@@ -174,6 +174,15 @@ def test_resnet_conv1x1_gemm_matches_conv(gpu, stride):
     y32.backward(g)
     for a, r in ((y.float(), y32), (x.grad.float(), x32.grad), (conv.weight.grad.float(), w32.grad)):
         assert (a - r).norm() / r.norm() < 1e-2, float((a - r).norm() / r.norm())
+    # a preset contiguous .grad of the [Cout, Cin, 1, 1] parameter (the trainer's flat-buffer view) is
+    # accumulated into in place by the weight-gradient GEMM
+    pre = torch.randn_like(conv.weight)
+    conv.weight.grad = pre.clone()
+    buf = conv.weight.grad
+    conv(x).backward(g.to(y.dtype))
+    assert conv.weight.grad.data_ptr() == buf.data_ptr()
+    ref = pre.float() + w32.grad
+    assert (conv.weight.grad.float() - ref).norm() / ref.norm() < 1e-2
 
 
 @pytest.mark.parametrize("C,res,relu", [(64, False, True), (256, True, True), (2048, True, True), (512, False, False)])
@@ -234,3 +243,43 @@ def test_fused_batchnorm_act_vs_fp32(gpu, C, res, relu):
     ok(bn.weight.grad, bnt.weight.grad, bn32.weight.grad, 1e-2)
     ok(bn.bias.grad, bnt.bias.grad, bn32.bias.grad, 1e-2)
     assert rel(bn.running_mean, bn32.running_mean) < 2e-2 and rel(bn.running_var, bn32.running_var) < 2e-2
+    # counted on the device by the statistics kernel's last block
+    assert int(bn.num_batches_tracked) == int(bn32.num_batches_tracked) == 1
+    # the shared workspace was left zeroed: a second pass gives the same output and gradients (up to
+    # the order of the fp32 atomic sums; a workspace left holding the first pass's sums would double them)
+    x.grad = None
+    gw1, gb1 = bn.weight.grad.float(), bn.bias.grad.float()
+    bn.weight.grad = bn.bias.grad = None
+    y2 = bn_act(x, bn, r, relu)
+    y2.backward(g)
+    assert rel(y2, y.float()) < 1e-3 and rel(bn.weight.grad, gw1) < 1e-3 and rel(bn.bias.grad, gb1) < 1e-3
+    assert int(bn.num_batches_tracked) == 2
+
+
+@pytest.mark.parametrize("C", [64, 1024])
+def test_fused_batchnorm_grads_into_flat_buffers(gpu, C):
+    """With preset contiguous .grad buffers (the trainer's flat gradient views) the BN backward ADDS
+    dgamma / dbeta into them in its reduction kernel and hands autograd None; the result equals the
+    returned-gradient path plus the preset values. Only one parameter needing a gradient falls back."""
+    from distributedvolunteercomputing_amd.ops.batchnorm import bn_act
+
+    torch.manual_seed(C + 1)
+    bn = torch.nn.BatchNorm2d(C).to(gpu)
+    torch.nn.init.uniform_(bn.weight, 0.5, 1.5)
+    torch.nn.init.uniform_(bn.bias, -0.5, 0.5)
+    bn = bn.to(torch.bfloat16)
+    x = (torch.randn(8, C, 14, 14, device=gpu)).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    g = torch.randn_like(x)
+    bn_act(x, bn, None, True).backward(g)  # returned-gradient path (no preset .grad)
+    ref_w, ref_b = bn.weight.grad.float(), bn.bias.grad.float()
+    pw = torch.randn(C, device=gpu).to(torch.bfloat16)
+    pb = torch.randn(C, device=gpu).to(torch.bfloat16)
+    bn.weight.grad, bn.bias.grad = pw.clone(), pb.clone()
+    bn_act(x, bn, None, True).backward(g)
+    rel = lambda a, b: float((a.float() - b).norm() / (b.norm() + 1e-6))  # noqa: E731
+    assert rel(bn.weight.grad, pw.float() + ref_w) < 1e-2
+    assert rel(bn.bias.grad, pb.float() + ref_b) < 1e-2
+    bn.bias.requires_grad_(False)
+    bn.weight.grad = None
+    bn_act(x, bn, None, True).backward(g)
+    assert rel(bn.weight.grad, ref_w) < 1e-2
