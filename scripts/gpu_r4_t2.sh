@@ -10,7 +10,7 @@ step() {  # name, seconds, command...
   echo "$name rc=$rc" >> $O/summary.txt
   [ $rc -le 1 ] || exit $rc
 }
-step tune 700 python -u scripts/tune_resnet_gemms.py $O/tunableop_gfx950.csv
+step tune 700 python -u scripts/tune_config_gemms.py $O/tunableop_gfx950.csv
 [ -f $O/tunableop_gfx950.csv ] || exit 1
 for i in 1 2; do
   step old$i 300 python -u bench_configs.py --configs 3 --steps 10
