@@ -260,6 +260,33 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res
   return {y, st[0], st[1], st[2]};
 }
 
+// ResNet stem max-pool 3x3 / stride 2 / pad 1 on the NHWC view [N, H, W, C] (bf16, C % 8 == 0):
+// returns y [N, OH, OW, C] and the uint8 window index of each output element
+std::vector<at::Tensor> maxpool3s2_fwd(at::Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous() && x.scalar_type() == at::kBFloat16 && x.size(3) % 8 == 0 &&
+                  x.size(1) >= 1 && x.size(2) >= 1, "maxpool3s2: x bf16 contiguous NHWC, C % 8 == 0");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(N * H * W * C < (1ll << 40) && H < (1 << 20) && W < (1 << 20), "maxpool3s2: size");
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  at::Tensor y = at::empty({N, OH, OW, C}, x.options());
+  at::Tensor idx = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+  vcx_maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)OH, (int)OW,
+                     cur_stream());
+  return {y, idx};
+}
+
+at::Tensor maxpool3s2_bwd(at::Tensor dy, at::Tensor idx, int64_t H, int64_t W) {
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.is_contiguous() && dy.scalar_type() == at::kBFloat16 &&
+                  idx.sizes() == dy.sizes() && idx.is_contiguous() && idx.scalar_type() == at::kByte &&
+                  idx.get_device() == dy.get_device() && dy.size(3) % 8 == 0, "maxpool3s2_bwd: dy bf16 / idx u8 NHWC alike");
+  const int64_t N = dy.size(0), OH = dy.size(1), OW = dy.size(2), C = dy.size(3);
+  TORCH_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "maxpool3s2_bwd: input size does not match");
+  at::Tensor dx = at::empty({N, H, W, C}, dy.options());
+  vcx_maxpool3s2_bwd(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)OH, (int)OW,
+                     cur_stream());
+  return dx;
+}
+
 at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor scale, at::Tensor shift, bool relu) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == at::kBFloat16, "bn: x bf16 contiguous NHWC");
   const int64_t C = x.size(-1), R = x.numel() / C;
@@ -784,6 +811,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("run_mean"), py::arg("run_var"), py::arg("eps"), py::arg("momentum"), py::arg("relu"),
         py::arg("nbt") = py::none());
   m.def("bn_apply", &bn_apply);
+  m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
+  m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("mean"), py::arg("rstd"), py::arg("scale"),
         py::arg("relu"), py::arg("want_dres"), py::arg("gw") = py::none(), py::arg("gb") = py::none());
   m.def("gemm_ps_diag", &gemm_ps_diag, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("epi") = 0,

@@ -222,6 +222,96 @@ __global__ void __launch_bounds__(NT) bwd_dx_kernel(const bf16* __restrict__ dy,
   }
 }
 
+// ---- the ResNet stem's 3x3 / stride-2 / pad-1 max-pool on NHWC bf16, with a 1-byte window index per
+// output element (kh * 3 + kw) instead of torch's int64 flat index, and a gather backward: each input
+// element sums the gradients of the (at most 2 x 2) windows that picked it, so no zero fill + scatter.
+// One thread per 8 channels of one output (forward) / input (backward) pixel.
+typedef unsigned char u8x8 __attribute__((ext_vector_type(8)));
+
+__global__ void __launch_bounds__(NT) maxpool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                         unsigned char* __restrict__ idx, int N, int H, int W, int C,
+                                                         int OH, int OW) {
+  const int c8 = C / 8;
+  const int64_t total = (int64_t)N * OH * OW * c8;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int cc = (int)(t % c8);
+    int64_t r = t / c8;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int n = (int)(r / OH);
+    float best[8];
+    u8x8 arg;
+    bool first = true;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = oh * 2 - 1 + kh;
+      if (ih < 0 || ih >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = ow * 2 - 1 + kw;
+        if (iw < 0 || iw >= W) continue;
+        float v[8];
+        load8(x + (((int64_t)n * H + ih) * W + iw) * C + cc * 8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          // the first in-window element, then strictly greater or NaN (torch's order and NaN rule)
+          if (first || !(v[e] <= best[e])) {
+            best[e] = v[e];
+            arg[e] = (unsigned char)(kh * 3 + kw);
+          }
+        }
+        first = false;
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)best[e];
+    const int64_t off = (((int64_t)n * OH + oh) * OW + ow) * C + cc * 8;
+    *(bf16x8*)(y + off) = o;
+    *(u8x8*)(idx + off) = arg;
+  }
+}
+
+__global__ void __launch_bounds__(NT) maxpool_bwd_kernel(const bf16* __restrict__ dy, const unsigned char* __restrict__ idx,
+                                                         bf16* __restrict__ dx, int N, int H, int W, int C, int OH,
+                                                         int OW) {
+  const int c8 = C / 8;
+  const int64_t total = (int64_t)N * H * W * c8;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int cc = (int)(t % c8);
+    int64_t r = t / c8;
+    const int iw = (int)(r % W);
+    r /= W;
+    const int ih = (int)(r % H);
+    const int n = (int)(r / H);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    // windows oh with 2 oh - 1 <= ih <= 2 oh + 1
+    const int oh0 = max(0, ih / 2), oh1 = min(OH - 1, (ih + 1) / 2);
+    const int ow0 = max(0, iw / 2), ow1 = min(OW - 1, (iw + 1) / 2);
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      const int kh = ih - (oh * 2 - 1);
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const int kw = iw - (ow * 2 - 1);
+        const int64_t off = (((int64_t)n * OH + oh) * OW + ow) * C + cc * 8;
+        const u8x8 a = *(const u8x8*)(idx + off);
+        float g[8];
+        load8(dy + off, g);
+        const unsigned char k = (unsigned char)(kh * 3 + kw);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (a[e] == k) acc[e] += g[e];
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)acc[e];
+    *(bf16x8*)(dx + (((int64_t)n * H + ih) * W + iw) * C + cc * 8) = o;
+  }
+}
+
 inline int64_t rows_per_block(int64_t R, int C) {
   // at most ~1024 blocks, each at least 32 passes of its row slots (bounds the 2C atomics per block)
   const int64_t rpp = NT / (C / 8);
@@ -309,4 +399,20 @@ void vcx_bn_bwd(const void* dy, const void* y, const void* x, const float* mean,
     relu ? go(bwd_dx_kernel<true, true>) : go(bwd_dx_kernel<true, false>);
   else
     relu ? go(bwd_dx_kernel<false, true>) : go(bwd_dx_kernel<false, false>);
+}
+
+// stem max-pool 3x3 / stride 2 / pad 1, NHWC bf16 (C % 8 == 0): y, idx [N, OH, OW, C]
+void vcx_maxpool3s2_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int OH, int OW, hipStream_t s) {
+  using namespace bn;
+  const int64_t total = (int64_t)N * OH * OW * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, (const bf16*)x, (bf16*)y,
+                     (unsigned char*)idx, N, H, W, C, OH, OW);
+}
+
+void vcx_maxpool3s2_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C, int OH, int OW,
+                        hipStream_t s) {
+  using namespace bn;
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, s, (const bf16*)dy,
+                     (const unsigned char*)idx, (bf16*)dx, N, H, W, C, OH, OW);
 }

@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import config
-from ..ops.batchnorm import bn_act
+from ..ops.batchnorm import bn_act, stem_maxpool
 
 
 class Conv1x1(nn.Conv2d):
@@ -88,7 +88,7 @@ class ResNet(nn.Module):
         if x.is_cuda and config.get().conv_find and not torch.backends.cudnn.benchmark:
             torch.backends.cudnn.benchmark = True  # process-wide: MIOpen Find for the 3x3 / 7x7 convolutions
         x = bn_act(self.stem(x), self.bn)
-        x = F.max_pool2d(x, 3, 2, 1)
+        x = stem_maxpool(x)  # HIP on channels-last bf16 (ops/batchnorm.py)
         x = self.blocks(x)
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         logits = self.fc(x)

@@ -80,3 +80,32 @@ def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, residual: torch.Tensor | N
     if residual is not None:
         y = y + residual
     return F.relu(y) if relu else y
+
+
+class _MaxPool3s2(torch.autograd.Function):
+    """3x3 / stride-2 / pad-1 max-pool (the ResNet stem) on channels-last bf16: a uint8 window index per
+    output element (torch stores int64 flat indices) and a gather backward without fill + scatter."""
+
+    @staticmethod
+    def forward(ctx, x):
+        y, idx = native().maxpool3s2_fwd(_nhwc(x))
+        ctx.save_for_backward(idx)
+        ctx.hw = (x.shape[2], x.shape[3])
+        return y.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        dyh = _nhwc(dy)
+        if not dyh.is_contiguous():
+            dyh = dyh.contiguous()
+        return native().maxpool3s2_bwd(dyh, idx, ctx.hw[0], ctx.hw[1]).permute(0, 3, 1, 2)
+
+
+def stem_maxpool(x: torch.Tensor) -> torch.Tensor:
+    """F.max_pool2d(x, 3, 2, 1): the HIP kernels (csrc/kernels/batchnorm.hip) for channels-last bf16 GPU
+    tensors with C % 8 == 0, torch otherwise."""
+    if (use_native(x) and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        return _MaxPool3s2.apply(x)
+    return F.max_pool2d(x, 3, 2, 1)

@@ -283,3 +283,28 @@ def test_fused_batchnorm_grads_into_flat_buffers(gpu, C):
     bn.weight.grad = None
     bn_act(x, bn, None, True).backward(g)
     assert rel(bn.weight.grad, ref_w) < 1e-2
+
+
+@pytest.mark.parametrize("shape,ties", [((8, 64, 112, 112), False), ((3, 16, 15, 17), False), ((4, 8, 9, 10), True)])
+def test_stem_maxpool_matches_torch(gpu, shape, ties):
+    """The ResNet stem max-pool (3x3 / 2 / pad 1, channels-last bf16, ops/batchnorm.py stem_maxpool) against
+    torch's max_pool2d on the same bf16 input: identical output, and the same input gradient (ties: the
+    first maximum of the window in scan order takes the gradient, as in torch)."""
+    from distributedvolunteercomputing_amd.ops.batchnorm import stem_maxpool
+
+    torch.manual_seed(sum(shape))
+    if ties:
+        x = torch.randint(-2, 3, shape, device=gpu).float()
+    else:
+        x = torch.randn(shape, device=gpu)
+    x = x.to(torch.bfloat16).to(memory_format=torch.channels_last).requires_grad_()
+    y = stem_maxpool(x)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    g = torch.randint(-4, 5, y.shape, device=gpu).to(torch.bfloat16)  # exact fp32 sums in both backwards
+    y.backward(g)
+    xt = x.detach().clone().requires_grad_()
+    with reference_ops():
+        yt = torch.nn.functional.max_pool2d(xt, 3, 2, 1)
+    yt.backward(g)
+    assert torch.equal(y, yt)
+    assert torch.equal(x.grad, xt.grad)
