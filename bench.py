@@ -9,18 +9,52 @@ One "step" = one local AdamW step of every peer (fwd + bwd + fused AdamW on the 
 every H-th step additionally runs the averaging round, which is therefore inside the timed
 region at its real 1/H frequency. Weak scaling: per-peer batch is fixed, global batch = N x B.
 
-Contract (driver): `python bench.py --gpus N --steps K --warmup W` (N>1 under torchrun, one
-rank per GPU). Rank 0 prints ONE JSON line; `value` is the whole-job samples/s.
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`, one rank per GPU. Under
+torchrun (WORLD_SIZE set) this process is one rank. Without a launcher and N > 1, this process
+touches no GPU: it starts `torch.distributed.run` with N ranks as a CHILD process (never an exec)
+and exits with its status, so `--gpus N` always means N ranks. A rank whose formed process group
+is not N ranks exits non-zero. Rank 0 prints ONE JSON line; `value` is the whole-job samples/s,
+`rccl_world` the size of the process group that actually formed, `devices` each rank's device.
+Reference analog: round-robin over every available volunteer, /root/reference/server.py:84-90.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-from distributedvolunteercomputing_amd.utils.tuning import enable_tuned_gemms
+
+def _spawn_ranks(n: int, argv) -> int:
+    """Launch n ranks of this script through torch.distributed.run in a child process (the
+    parent never initialises the GPU: device_count() does not on this ROCm image)."""
+    import torch
+
+    ndev = torch.cuda.device_count()
+    if 0 < ndev < n:
+        print(f"[bench] --gpus {n} but only {ndev} GPUs are visible", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver (RCCL)
+    return subprocess.call(cmd, env=env)
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ:
+    _pre = argparse.ArgumentParser(add_help=False)
+    _pre.add_argument("--gpus", type=int, default=1)
+    _n = _pre.parse_known_args()[0].gpus
+    if _n > 1:
+        sys.exit(_spawn_ranks(_n, sys.argv[1:]))
+
+from distributedvolunteercomputing_amd.utils.tuning import enable_tuned_gemms  # noqa: E402
 
 TUNED_GEMMS = enable_tuned_gemms(int(os.environ.get("LOCAL_RANK", "0")))  # before torch's first GEMM
 
@@ -55,6 +89,9 @@ def parse():
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus != world:
+        print(f"[bench] --gpus {a.gpus} but the launch formed WORLD_SIZE={world}", file=sys.stderr)
+        return 3
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cuda = torch.cuda.is_available()
@@ -66,6 +103,10 @@ def main():
         device = torch.device("cpu")
     if world > 1:
         dist.init_process_group("nccl" if cuda else "gloo", device_id=device if cuda else None)
+        formed = dist.get_world_size()
+        if formed != a.gpus:
+            print(f"[bench] process group formed {formed} ranks, --gpus {a.gpus}", file=sys.stderr)
+            return 3
     group = PeerGroup.from_default(device) if world > 1 else None
 
     cfg = GPT2Config.preset(a.model)
@@ -111,10 +152,24 @@ def main():
     sync_all()
     t0 = time.perf_counter()
     last = None
+    syncs = []
     for i in range(a.steps):
         last = trainer.step(*batch(a.warmup + i))
+        if last.synced:
+            syncs.append(trainer.last_sync_ms)
     sync_all()
     dt = time.perf_counter() - t0
+    # which device each rank ran on, and how many ranks the process group really has
+    dev_desc = f"{device.type}:{device.index if device.index is not None else 0}"
+    if cuda:
+        p = torch.cuda.get_device_properties(device)
+        dev_desc += f" {p.name} pci {getattr(p, 'pci_bus_id', '?')}"
+    devices = [dev_desc]
+    rccl_world = 1
+    if world > 1:
+        rccl_world = dist.get_world_size()
+        devices = [None] * rccl_world
+        dist.all_gather_object(devices, dev_desc)
     loss = float(last.extra["loss_t"]) if last is not None else float("nan")
     if group is not None:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
@@ -150,6 +205,11 @@ def main():
             "mfu_bf16_dense": round(flops / world / BF16_DENSE_PEAK, 4),
             "final_loss": round(loss, 4),
             "sync_ms": round(trainer.last_sync_ms, 3),
+            "sync_ms_timed_mean": round(sum(syncs) / len(syncs), 3) if syncs else None,
+            "sync_rounds_timed": len(syncs),
+            "rccl_world": rccl_world,
+            "backend": dist.get_backend() if world > 1 else None,
+            "devices": devices,
             "tuned_gemms": TUNED_GEMMS,
             "hipgraph": graphed,
             # ranks sharing a card (scripts/rccl_rehearsal_launch.py): a functional run, not a per-GPU number

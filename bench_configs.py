@@ -37,11 +37,12 @@ def _time(step, warmup, steps):
 
 
 def cfg3(a, dev):
-    from distributedvolunteercomputing_amd.models.resnet import resnet50
+    from distributedvolunteercomputing_amd.models.resnet import enable_conv_find, resnet50
     from distributedvolunteercomputing_amd.parallel.compression import TopKCompressor
     from distributedvolunteercomputing_amd.parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer
 
     m = resnet50().to(dev, torch.bfloat16).to(memory_format=torch.channels_last)
+    enable_conv_find()
     tr = LocalSGDTrainer(m, LocalSGDConfig(H=4, lr=1e-3, weight_decay=0.0), device=dev)
     tr.compressor = TopKCompressor(tr.flat.numel, 0.01, dev)
     B = a.resnet_batch

@@ -5,6 +5,7 @@
 #include <torch/extension.h>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <tuple>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
@@ -146,19 +147,16 @@ bool gemm_ps_supported(int64_t M, int64_t N, int64_t K, int64_t epi) {
 }
 
 void gemm_ps(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor> c2, c10::optional<at::Tensor> bias,
-             c10::optional<at::Tensor> colsum, int64_t epi, int64_t grid_cap, int64_t waves, int64_t stagger) {
+             c10::optional<at::Tensor> colsum, int64_t epi, int64_t grid_cap) {
   TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_ps: 2-D cuda tensors");
-  TORCH_CHECK(waves == 8 || waves == 4, "gemm_ps: waves 8 (one workgroup per CU) or 4 (two per CU)");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && c.scalar_type() == at::kBFloat16,
               "gemm_ps: bf16 operands");
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm_ps: K-contiguous rows");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_ps: shape mismatch");
-  TORCH_CHECK(waves == 8 ? vcx_gemm_ps_supported((int)M, (int)N, (int)K, (int)epi)
-                         : vcx_gemm_ps2_supported((int)M, (int)N, (int)K, (int)epi),
-              "gemm_ps: needs M, N % 256 == 0, K % 128 == 0, K >= 256, epilogue 0 (store), 1 (bias), 2 (bias+GELU), "
-              "4 (DGELU + bias grad) or 7 (diagnostic, no stores), N <= 16384 with a bias "
-              "(4 waves: N % 128 == 0, K % 192 == 0, epilogue 0, 1, 2 or 7)");
+  TORCH_CHECK(vcx_gemm_ps_supported((int)M, (int)N, (int)K, (int)epi),
+              "gemm_ps: needs M, N % 256 == 0, K % 128 == 0, K >= 256, epilogue 0 (store), 1 (bias), 2 (bias+GELU) "
+              "or 4 (DGELU + bias grad), N <= 16384 with a bias");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm_ps: 16-B aligned rows");
   for (const at::Tensor* t : {&a, &b, &c})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_ps: 16-B aligned base pointers");
@@ -185,40 +183,31 @@ void gemm_ps(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
     cs = colsum->data_ptr<float>();
   }
   vcx_gemm_ps(a.data_ptr(), b.data_ptr(), c.data_ptr(), c2p, bp, cs, (int)M, (int)N, (int)K, (int)a.stride(0),
-              (int)b.stride(0), (int)c.stride(0), (int)epi, (int)grid_cap, (int)waves, (int)stagger, cur_stream());
-}
-
-// gemm_ps diagnostics (scripts/gemm_ps_diag.py): store cache policy 0 plain / 1 nt / 2 sc1 / 3 sc0 sc1,
-// epi 0 (store) or 7 (no stores), optional per-tile s_memtime stamps int64 [grid, 64, 5]
-void gemm_ps_diag(at::Tensor a, at::Tensor b, at::Tensor c, int64_t epi, int64_t policy,
-                  c10::optional<at::Tensor> stamps, int64_t grid_cap, int64_t stagger) {
-  TORCH_CHECK(a.is_cuda() && a.is_contiguous() && b.is_contiguous() && c.is_contiguous(), "gemm_ps_diag: contiguous");
-  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N && (epi == 0 || epi == 7) && policy >= 0 &&
-                  policy <= 3 && vcx_gemm_ps_supported((int)M, (int)N, (int)K, (int)epi),
-              "gemm_ps_diag: shape / epi / policy");
-  unsigned long long* sp = nullptr;
-  if (stamps) {
-    const int grid = vcx_gemm_ps_grid((int)M, (int)N, (int)grid_cap, 8);
-    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->is_contiguous() && stamps->numel() >= grid * 64 * 5,
-                "gemm_ps_diag: stamps int64 [grid, 64, 5]");
-    sp = reinterpret_cast<unsigned long long*>(stamps->data_ptr());
-  }
-  vcx_gemm_ps_diag(a.data_ptr(), b.data_ptr(), c.data_ptr(), (int)M, (int)N, (int)K, (int)K, (int)K, (int)N, (int)epi,
-                   (int)policy, sp, (int)grid_cap, (int)stagger, cur_stream());
+              (int)b.stride(0), (int)c.stride(0), (int)epi, (int)grid_cap, cur_stream());
 }
 
 // The zero-at-rest workspace of the BN kernels: fp32 [2C] atomic sums, zeroed once here and zeroed again
-// by the finalize kernel of every call. One per (device, stream, C): launches on one stream are
-// ordered, so the layers of a model can share it.
+// by the finalize kernel of every call. Correct only while every stats -> finalize pair that uses one
+// workspace runs back to back on its stream: launches on one stream are ordered, so the layers of a
+// model can share it, but two host threads launching BN of the same width on the same stream could
+// interleave their pairs (one finalize would read both sums). The cache is therefore keyed by the
+// launching host thread as well: one workspace per (device, stream, C, thread). It must exist before a
+// hipGraph capture that uses it (one eager step first, as every trainer here does): created inside a
+// capture, its zero fill would only be a node of the graph, not done by the time eager calls use it.
 static float* bn_workspace(const at::Tensor& x, int64_t C) {
   static std::mutex mu;
   // never destroyed: no device free during static destruction at interpreter exit
-  static auto* cache = new std::map<std::tuple<int, uintptr_t, int64_t>, at::Tensor>();
-  const auto key = std::make_tuple((int)x.get_device(), (uintptr_t)cur_stream(), C);
+  static auto* cache = new std::map<std::tuple<int, uintptr_t, int64_t, size_t>, at::Tensor>();
+  const auto key = std::make_tuple((int)x.get_device(), (uintptr_t)cur_stream(), C,
+                                   std::hash<std::thread::id>{}(std::this_thread::get_id()));
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache->find(key);
-  if (it == cache->end()) it = cache->emplace(key, at::zeros({2 * C}, x.options().dtype(at::kFloat))).first;
+  if (it == cache->end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    TORCH_CHECK(hipStreamIsCapturing(cur_stream(), &cs) == hipSuccess && cs == hipStreamCaptureStatusNone,
+                "bn: first call of this width on this stream/thread inside a graph capture; run one eager step first");
+    it = cache->emplace(key, at::zeros({2 * C}, x.options().dtype(at::kFloat))).first;
+  }
   return it->second.data_ptr<float>();
 }
 
@@ -350,6 +339,33 @@ void gemm_tn(at::Tensor a, at::Tensor b, at::Tensor out, int64_t splits, bool ac
   at::Tensor ws = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
   vcx_gemm_tn(a.data_ptr(), b.data_ptr(), ws.data_ptr<float>(), out.data_ptr(), (int)M, (int)N, (int)K,
               (int)a.stride(0), (int)b.stride(0), (int)splits, accumulate ? 1 : 0, cur_stream());
+}
+
+// Weight gradient out[M, N] (+)= a[K, M]^T . b[K, N] (token-major operands) on the wave-specialised
+// gemm_wg (csrc/kernels/gemm_wg.hip): split-K over the token axis with fp32 partials summed into out.
+// splits <= 0: vcx_gemm_wg_splits; pf: L2 prefetch distance in 32-token slices (0, 4, 6, 8, 12)
+bool gemm_wg_supported(int64_t M, int64_t N, int64_t K, int64_t splits) {
+  return vcx_gemm_wg_supported((int)M, (int)N, (int)K, (int)(splits > 0 ? splits : vcx_gemm_wg_splits((int)M, (int)N, (int)K)));
+}
+
+void gemm_wg(at::Tensor a, at::Tensor b, at::Tensor out, bool accumulate, int64_t splits, int64_t pf) {
+  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_wg: 2-D cuda tensors");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
+              "gemm_wg: bf16 operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.is_contiguous(), "gemm_wg: row-major operands, contiguous out");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "gemm_wg: shape mismatch");
+  if (splits <= 0) splits = vcx_gemm_wg_splits((int)M, (int)N, (int)K);
+  TORCH_CHECK(vcx_gemm_wg_supported((int)M, (int)N, (int)K, (int)splits),
+              "gemm_wg: needs M % 256 == 0, N % 256 == 0, K % 64 == 0, K / 192 >= splits");
+  TORCH_CHECK(pf == 0 || pf == 4 || pf == 6 || pf == 8 || pf == 12, "gemm_wg: pf 0, 4, 6, 8 or 12");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_wg: 16-B aligned rows");
+  TORCH_CHECK(a.stride(0) * K < (int64_t(1) << 40) && b.stride(0) * K < (int64_t(1) << 40), "gemm_wg: size");
+  for (const at::Tensor* t : {&a, &b, &out})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_wg: 16-B aligned base pointers");
+  at::Tensor ws = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
+  vcx_gemm_wg(a.data_ptr(), b.data_ptr(), ws.data_ptr<float>(), out.data_ptr(), (int)M, (int)N, (int)K,
+              (int)a.stride(0), (int)b.stride(0), (int)splits, accumulate ? 1 : 0, (int)pf, cur_stream());
 }
 
 at::Tensor transpose_bf16(at::Tensor src, c10::optional<at::Tensor> dst) {
@@ -815,11 +831,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("mean"), py::arg("rstd"), py::arg("scale"),
         py::arg("relu"), py::arg("want_dres"), py::arg("gw") = py::none(), py::arg("gb") = py::none());
-  m.def("gemm_ps_diag", &gemm_ps_diag, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("epi") = 0,
-        py::arg("policy") = 0, py::arg("stamps") = py::none(), py::arg("grid_cap") = 0, py::arg("stagger") = 0);
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
-        py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0,
-        py::arg("waves") = 8, py::arg("stagger") = 0);
+        py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0);
+  m.def("gemm_wg_supported", &gemm_wg_supported, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits") = 0);
+  m.def("gemm_wg", &gemm_wg, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("accumulate") = false,
+        py::arg("splits") = 0, py::arg("pf") = 8);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("splits"), py::arg("accumulate"));
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),

@@ -62,9 +62,14 @@ __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&
   }
 }
 
+// sums of (x - k) and (x - k)^2 with a per-channel pivot k = x[row 0] (the same for every block):
+// E[x^2] - m^2 on raw fp32 sums cancels catastrophically when |mean| >> std over millions of rows;
+// shifted by a value of the batch, the sums are O(R std^2) and the variance keeps its digits
 __global__ void __launch_bounds__(NT) stats_kernel(const bf16* __restrict__ x, int64_t R, int C, int64_t rows_per_block,
                                                    float* __restrict__ sum, float* __restrict__ sumsq) {
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(R, r0 + rows_per_block);
+  float k[8];
+  load8(x + (threadIdx.x % (C / 8)) * 8, k);
   channel_reduce(
       C, r0, r1,
       [&](int64_t off, float(&s0)[8], float(&s1)[8]) {
@@ -72,18 +77,20 @@ __global__ void __launch_bounds__(NT) stats_kernel(const bf16* __restrict__ x, i
         load8(x + off, v);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          s0[i] += v[i];
-          s1[i] = fmaf(v[i], v[i], s1[i]);
+          const float d = v[i] - k[i];
+          s0[i] += d;
+          s1[i] = fmaf(d, d, s1[i]);
         }
       },
       sum, sumsq);
 }
 
 // mean, 1/std, scale = gamma/std, shift = beta - mean * scale; running stats (unbiased variance)
-// updated in place in their own dtype (bf16 or fp32); num_batches_tracked + 1; ws = [sum | sumsq]
-// zeroed again for the next call
+// updated in place in their own dtype (bf16 or fp32); num_batches_tracked + 1; ws = [sum | sumsq] of
+// the pivot-shifted values (pivot = x[row 0], see stats_kernel), zeroed again for the next call
 template <typename RT>
-__global__ void finalize_kernel(float* __restrict__ ws, int64_t R, int C, const bf16* __restrict__ gamma,
+__global__ void finalize_kernel(float* __restrict__ ws, const bf16* __restrict__ x, int64_t R, int C,
+                                const bf16* __restrict__ gamma,
                                 const bf16* __restrict__ beta, float eps, float momentum, RT* __restrict__ run_mean,
                                 RT* __restrict__ run_var, float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                 float* __restrict__ scale, float* __restrict__ shift, int64_t* __restrict__ nbt) {
@@ -91,8 +98,9 @@ __global__ void finalize_kernel(float* __restrict__ ws, int64_t R, int C, const 
   if (c == 0 && nbt) *nbt += 1;
   if (c >= C) return;
   const float inv = 1.f / (float)R;
-  const float m = ws[c] * inv;
-  const float var = fmaxf(ws[C + c] * inv - m * m, 0.f);
+  const float d = ws[c] * inv;  // mean - pivot
+  const float m = (float)x[c] + d;
+  const float var = fmaxf(ws[C + c] * inv - d * d, 0.f);
   ws[c] = 0.f;
   ws[C + c] = 0.f;
   const float rs = rsqrtf(var + eps);
@@ -255,8 +263,9 @@ __global__ void __launch_bounds__(NT) maxpool_fwd_kernel(const bf16* __restrict_
         load8(x + (((int64_t)n * H + ih) * W + iw) * C + cc * 8, v);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          // the first in-window element, then strictly greater or NaN (torch's order and NaN rule)
-          if (first || !(v[e] <= best[e])) {
+          // the first in-window element, then strictly greater or NaN, and nothing replaces a NaN once
+          // held (torch's order and NaN rule: `val > max || isnan(val)` against the running max)
+          if (first || (best[e] == best[e] && !(v[e] <= best[e]))) {
             best[e] = v[e];
             arg[e] = (unsigned char)(kh * 3 + kw);
           }
@@ -342,10 +351,10 @@ void vcx_bn_fwd_train(const void* x, const void* res, void* y, int64_t R, int C,
   const int nb = (int)((R + rpb - 1) / rpb);
   hipLaunchKernelGGL(stats_kernel, dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
   if (run_fp32)
-    hipLaunchKernelGGL(finalize_kernel<float>, dim3((C + 255) / 256), dim3(256), 0, s, ws, R, C, (const bf16*)gamma,
+    hipLaunchKernelGGL(finalize_kernel<float>, dim3((C + 255) / 256), dim3(256), 0, s, ws, (const bf16*)x, R, C, (const bf16*)gamma,
                        (const bf16*)beta, eps, momentum, (float*)run_mean, (float*)run_var, mean, rstd, scale, shift, nbt);
   else
-    hipLaunchKernelGGL(finalize_kernel<bf16>, dim3((C + 255) / 256), dim3(256), 0, s, ws, R, C, (const bf16*)gamma,
+    hipLaunchKernelGGL(finalize_kernel<bf16>, dim3((C + 255) / 256), dim3(256), 0, s, ws, (const bf16*)x, R, C, (const bf16*)gamma,
                        (const bf16*)beta, eps, momentum, (bf16*)run_mean, (bf16*)run_var, mean, rstd, scale, shift, nbt);
   const int64_t n8 = R * C / 8;
   const int g = grid_for(n8);

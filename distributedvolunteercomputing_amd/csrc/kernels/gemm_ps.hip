@@ -42,9 +42,8 @@ constexpr int SLOT = 2 * SLOT_A;        // 32 KB
 constexpr int RING = 4 * SLOT;          // 128 KB
 constexpr int BIAS_MAX = 16384;         // bias row resident in LDS behind the ring (32 KB)
 
-// (3 is not used: gemm_nt's code 3 is DGELU, so a caller reusing its numbering is refused, not
-// silently given the diagnostic no-store epilogue)
-enum Epi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 4, EPI_NONE = 7 /* diagnostic: no stores */ };
+// (3 is not used: gemm_nt's code 3 is DGELU, so a caller reusing its numbering is refused)
+enum Epi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 4 };
 
 __device__ __forceinline__ int swz(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
 
@@ -71,33 +70,16 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return x * __builtin_amdgcn_rcpf(1.f + __expf(-u2));
 }
 
-// 16-B buffer store as inline asm ending in `s_nop 1`: hipcc let a VALU write overwrite the data
-// VGPRs of a builtin buffer_store_dwordx4 4 instructions after it (lanes 12-15 of each row stored
-// stale dword 1, measured), so the store's read of its data registers is padded by hand
-// (cdna_hip_programming.md §5.7 item 1, stores)
-// SPOL (diagnostic builds only): the store's cache policy -- 0 plain, 1 nt, 2 sc1 (write-through,
-// line dropped from L2), 3 sc0 sc1
-template <int SPOL = 0>
+// 16-B non-temporal buffer store as inline asm ending in `s_nop 1`: hipcc let a VALU write overwrite
+// the data VGPRs of a builtin buffer_store_dwordx4 4 instructions after it (lanes 12-15 of each row
+// stored stale dword 1, measured), so the store's read of its data registers is padded by hand
+// (cdna_hip_programming.md §5.7 item 1, stores). nt: the GPT-2 shapes ran 7-14 % faster than with
+// plain stores (profiles/r4_gemm_ps_diag.txt).
 __device__ __forceinline__ void store16(u32x4 v, u32x4 desc, int voff, int soff) {
-  if constexpr (SPOL == 0)
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(desc), "s"(soff)
-                 : "memory");
-  else if constexpr (SPOL == 1)
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(desc), "s"(soff)
-                 : "memory");
-  else if constexpr (SPOL == 2)
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(desc), "s"(soff)
-                 : "memory");
-  else
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen sc0 sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(desc),
-                 "s"(soff)
-                 : "memory");
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen nt\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(desc), "s"(soff)
+               : "memory");
 }
 
-// Diagnostic stamps (STAMP builds): thread 0 of each workgroup records s_memtime per tile into LDS
-// behind the ring, copied out at the end: [0] tile start, [1] before step 3's wait, [2] after
-// step 3's wait + barrier, [3] epilogue start, [4] epilogue end (every store issued)
-constexpr int NSTAMP = 5, STAMP_TILES = 64;
 // raw buffer descriptor words: 48-bit base, stride 0, num_records bytes, the flags word used by
 // __builtin_amdgcn_make_buffer_rsrc elsewhere in the tree
 __device__ __forceinline__ u32x4 desc_of(const void* base, int bytes) {
@@ -105,13 +87,9 @@ __device__ __forceinline__ u32x4 desc_of(const void* base, int bytes) {
   return u32x4{(unsigned)a, (unsigned)(a >> 32) & 0xffffu, (unsigned)bytes, 0x00020000u};
 }
 
-// Workgroup geometry. NW = 8: one 512-thread workgroup per CU, 256 x 256 tiles, 4-slot ring.
-// NW = 4: two co-resident 256-thread workgroups per CU, 256 x 128 tiles, 3-slot rings (72 KB each):
-// the same 128 x 64 wave tile and main loop, but one workgroup's epilogue stall is the other's
-// compute time (their vmcnt queues are separate).
-template <int NW>
+// Workgroup geometry: one 512-thread workgroup (8 waves) per CU, 256 x 256 tiles, a 4-slot ring
 struct Geo {
-  static constexpr int NTH = NW * 64, BNt = NW == 8 ? 256 : 128, WNC = NW / 2, NSLOT = NW == 8 ? 4 : 3;
+  static constexpr int NW = 8, NTH = NW * 64, BNt = 256, WNC = NW / 2, NSLOT = 4;
   static constexpr int SLOTA = BM * ROWB, SLOTB = SLOTA + BNt * ROWB, RINGB = NSLOT * SLOTB;
   static constexpr int APW = 16 / NW, BPW = BNt / 16 / NW, PPW = APW + BPW;  // LDS-DMA pieces per wave
   static constexpr int VMW = PPW * (NSLOT - 2);  // vmcnt of a step: the slices younger than the awaited one
@@ -122,32 +100,20 @@ struct Frags {
   sx8 w[4];  // B fragments: the wave's 4 column blocks of 16
 };
 
-// (the body is a device function shared by two kernel templates with literal launch bounds: a
-// kernel template on NW lost its host-side stubs)
-// (TAG: the diagnostic kernels instantiate their own specialisations -- a second call site of one
-// already used by gemm_ps_kernel made hipcc's host pass reject both, ROCm 7.2)
-template <int EPI, int NW, int SPOL = 0, bool STAMP = false, int TAG = 0>
-__device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                             bf16* __restrict__ C, bf16* __restrict__ C2,
-                                             const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
-                                             int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger,
-                                             void* stamps_v) {
-  unsigned long long* stamps = (unsigned long long*)stamps_v;
-  using Gm = Geo<NW>;
-  constexpr int BNt = Gm::BNt, SLOTA = Gm::SLOTA, SLOTB = Gm::SLOTB, RINGB = Gm::RINGB, NSLOT = Gm::NSLOT;
+template <int EPI>
+__global__ void __launch_bounds__(512, 1)
+    gemm_ps_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
+                   bf16* __restrict__ C2, const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
+                   int K, int lda, int ldb, int ldc, int tilesN, int tiles) {
+  using Gm = Geo;
+  constexpr int NW = Gm::NW, BNt = Gm::BNt, SLOTA = Gm::SLOTA, SLOTB = Gm::SLOTB, RINGB = Gm::RINGB,
+                NSLOT = Gm::NSLOT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / Gm::WNC, wn = wid % Gm::WNC;
   const int G = gridDim.x, bid = blockIdx.x;
   const int nk = K / BKS;  // multiple of 4, >= 8 (host check)
-  int ti = 0;  // STAMP: this workgroup's tile index
-  auto stamp = [&](int k) {
-    if constexpr (STAMP) {
-      if (tid == 0 && ti < STAMP_TILES)
-        ((unsigned long long*)(smem + RINGB))[ti * NSTAMP + k] = (unsigned long long)clock64();  // s_memtime: shader clock cycles
-    }
-  };
 
   if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {  // the bias row, once per workgroup
     bf16* bl = (bf16*)(smem + RINGB);
@@ -202,17 +168,10 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
           rb, (__attribute__((address_space(3))) void*)(sl + SLOTA + NW * (p - Gm::APW) * 1024), 16,
           b_off0 + (p - Gm::APW) * b_pstep, soff, 0, 0);
   };
-  // the pieces of one slice spread over the step's 4 MFMA groups (NW = 8: one each; NW = 4: 2,1,2,1)
+  // the 4 pieces of one slice, one per MFMA group of the step
   auto stage_group = [&](const Rs& ra, const Rs& rb, int kslice, int slot, auto GR) {
-    constexpr int g = decltype(GR)::value;
-    if constexpr (Gm::PPW == 4) {
-      stage_piece(ra, rb, kslice, slot, std::integral_constant<int, g>{});
-    } else {
-      static_assert(Gm::PPW == 6, "pieces per wave");
-      constexpr int first = g == 0 ? 0 : g == 1 ? 2 : g == 2 ? 3 : 5;
-      stage_piece(ra, rb, kslice, slot, std::integral_constant<int, first>{});
-      if constexpr (g == 0 || g == 2) stage_piece(ra, rb, kslice, slot, std::integral_constant<int, first + 1>{});
-    }
+    static_assert(Gm::PPW == 4, "pieces per wave");
+    stage_piece(ra, rb, kslice, slot, std::integral_constant<int, decltype(GR)::value>{});
   };
   using P0 = std::integral_constant<int, 0>;
   using P1 = std::integral_constant<int, 1>;
@@ -280,13 +239,11 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
   auto step = [&](int s, Frags& fc, Frags& fn, const Rs& sa, const Rs& sb, int ks, bool nowait, auto LD,
                   auto VM, auto ST) {
     constexpr bool ld = decltype(LD)::value, st = decltype(ST)::value;
-    if (STAMP && s == 3) stamp(1);
     if (nowait)
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     else
       wait_vm<decltype(VM)::value>();
     barrier();
-    if (STAMP && s == 3) stamp(2);
     const int slot = s % NSLOT, nslot = (s + 1) % NSLOT;
     if constexpr (st) stage_group(sa, sb, ks, slot, P0{});
     __builtin_amdgcn_sched_barrier(0);
@@ -330,7 +287,6 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
                                                                                       i * 16 * ldc * 2, 0));
   };
   auto epilogue = [&](int m0, int n0, auto DRAIN) {
-    stamp(3);
     float cs[8];  // EPI_DGELU: fp32 column sums of this lane's 8 columns over its 16 rows
 #pragma unroll
     for (int e = 0; e < 8; ++e) cs[e] = 0.f;
@@ -376,10 +332,6 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
         for (int e = 0; e < 8; ++e) h[e] = (bf16)(EPI == EPI_BIAS || EPI == EPI_BIAS_GELU ? o[e] + bv[jp][e] : o[e]);
         v[jp] = __builtin_bit_cast(u32x4, h);
       }
-      if constexpr (EPI == EPI_NONE) {
-        asm volatile("" ::"v"(v[0]), "v"(v[1]));
-        continue;
-      }
       // rows r and r ^ 8 of the 16-row block trade halves (DPP row_ror:8): lanes of rows 0..7 keep
       // their jp = 0 chunk and take row r + 8's; rows 8..15 keep jp = 1 and take row r - 8's. Store
       // A then writes rows 0..7 and store B rows 8..15, each as 8 full 128-B row segments.
@@ -406,8 +358,8 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
           v[q] = __builtin_bit_cast(u32x4, o8);
         }
       }
-      store16<SPOL>(v[0], rc, c_offA, soff);
-      store16<SPOL>(v[1], rc, c_offA + 8 * ldc * 2, soff);
+      store16(v[0], rc, c_offA, soff);
+      store16(v[1], rc, c_offA + 8 * ldc * 2, soff);
       if constexpr (EPI == EPI_BIAS_GELU) {
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -415,7 +367,7 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
           bf16x8 act;
 #pragma unroll
           for (int e = 0; e < 8; ++e) act[e] = (bf16)gelu_tanh((float)pre[e]);
-          store16<SPOL>(__builtin_bit_cast(u32x4, act), rc2, c_offA + q * 8 * ldc * 2, soff);
+          store16(__builtin_bit_cast(u32x4, act), rc2, c_offA + q * 8 * ldc * 2, soff);
         }
       }
     }
@@ -435,18 +387,8 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
         for (int e = 0; e < 8; ++e) atomicAdd(dst + e, cs[e]);
       }
     }
-    stamp(4);
   };
 
-
-  // NW = 4: the second workgroup of each CU pair starts `stagger` x ~8k cycles late, so that the
-  // two co-resident workgroups reach their tile boundaries at different times
-  if (NW == 4 && stagger > 0 && bid >= G / 2)
-    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  // diagnostic (STAMP/SPOL builds): NW = 8 workgroups in 4 start phases inside every XCD, phase p
-  // sleeping p x stagger x ~8k cycles, so that tile boundaries -- and the output bursts -- spread
-  if (NW == 8 && stagger > 0)
-    for (int i = 0; i < ((bid >> 3) & 3) * stagger; ++i) __builtin_amdgcn_s_sleep(127);
 
   // ---- prologue: slices 0..NSLOT-1 of the first tile
   int vb = bid;
@@ -458,7 +400,7 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
   VCX_PS_STAGE_U(0)
   VCX_PS_STAGE_U(1)
   VCX_PS_STAGE_U(2)
-  if constexpr (NSLOT == 4) VCX_PS_STAGE_U(3)
+  VCX_PS_STAGE_U(3)
 #undef VCX_PS_STAGE_U
   wait_vm<0>();  // the first NSLOT slices landed
   barrier();
@@ -471,95 +413,38 @@ __device__ __forceinline__ void gemm_ps_body(const bf16* __restrict__ A, const b
   while (true) {
     int m0, n0;
     coords(vb, m0, n0);
-    stamp(0);
     const int vn = vb + G;
     const bool more = vn < tiles;
     Rs na, nb;  // the next tile's resources (the last tile re-stages its own first slices: never read)
     tile_rs(more ? vn : vb, na, nb);
-    if constexpr (NW == 8) {
-      int s = 0;
-      for (; s + 4 < nk; s += 2) {  // staging this tile's slices s + 4, s + 5
-        step(s, f0, f1, ra, rb, s + 4, s < 3, Tt{}, VM{}, Tt{});
-        step(s + 1, f1, f0, ra, rb, s + 5, s + 1 < 3, Tt{}, VM{}, Tt{});
-      }
-      // last 4 steps: the next tile's slices 0..3 go into the same ring
-      step(s, f0, f1, na, nb, 0, false, Tt{}, VM{}, Tt{});
-      step(s + 1, f1, f0, na, nb, 1, false, Tt{}, VM{}, Tt{});
-      step(s + 2, f0, f1, na, nb, 2, false, Tt{}, VM{}, Tt{});
-      if constexpr (EPI == EPI_DGELU) {
-        load_pre(m0, n0);  // lands behind the last step's MFMAs; its fragments are not read there
-        // the 16 pre loads are younger loads than the awaited slice (loads retire in order)
-        step(s + 3, f1, f0, na, nb, 3, false, Ff{}, std::integral_constant<int, 24>{}, Tt{});
-        epilogue(m0, n0, Tt{});
-        // the next tile's slice 0 (slot 0) landed before the epilogue's vmcnt(0)
-        load_x(0, 0), load_x(0, 2), load_x(0, 4), load_y(f0, 0), load_w(f0, 0, 0), load_w(f0, 0, 2);
-      } else {
-        step(s + 3, f1, f0, na, nb, 3, false, Tt{}, VM{}, Tt{});
-        epilogue(m0, n0, Tt{});  // the fragments of the next tile's slice 0 are in (x, f0) already
-      }
+    int s = 0;
+    for (; s + 4 < nk; s += 2) {  // staging this tile's slices s + 4, s + 5
+      step(s, f0, f1, ra, rb, s + 4, s < 3, Tt{}, VM{}, Tt{});
+      step(s + 1, f1, f0, ra, rb, s + 5, s + 1 < 3, Tt{}, VM{}, Tt{});
+    }
+    // last 4 steps: the next tile's slices 0..3 go into the same ring
+    step(s, f0, f1, na, nb, 0, false, Tt{}, VM{}, Tt{});
+    step(s + 1, f1, f0, na, nb, 1, false, Tt{}, VM{}, Tt{});
+    step(s + 2, f0, f1, na, nb, 2, false, Tt{}, VM{}, Tt{});
+    if constexpr (EPI == EPI_DGELU) {
+      load_pre(m0, n0);  // lands behind the last step's MFMAs; its fragments are not read there
+      // the 16 pre loads are younger loads than the awaited slice (loads retire in order)
+      step(s + 3, f1, f0, na, nb, 3, false, Ff{}, std::integral_constant<int, 24>{}, Tt{});
+      epilogue(m0, n0, Tt{});
+      // the next tile's slice 0 (slot 0) landed before the epilogue's vmcnt(0)
+      load_x(0, 0), load_x(0, 2), load_x(0, 4), load_y(f0, 0), load_w(f0, 0, 0), load_w(f0, 0, 2);
     } else {
-      // 3-slot ring: step s stages slice s + 3 (the next tile's slices 0..2 in the last 3 steps);
-      // steps 0, 1 wait for slices that landed before the previous epilogue's stores
-      for (int s = 0; s < nk; s += 2) {
-        const int k3 = s + 3, k4 = s + 4;
-        const bool n3 = k3 >= nk, n4 = k4 >= nk;
-        step(s, f0, f1, n3 ? na : ra, n3 ? nb : rb, n3 ? k3 - nk : k3, s < 2, Tt{}, VM{}, Tt{});
-        step(s + 1, f1, f0, n4 ? na : ra, n4 ? nb : rb, n4 ? k4 - nk : k4, s + 1 < 2, Tt{}, VM{}, Tt{});
-      }
+      step(s + 3, f1, f0, na, nb, 3, false, Tt{}, VM{}, Tt{});
       epilogue(m0, n0, Tt{});  // the fragments of the next tile's slice 0 are in (x, f0) already
     }
-    ++ti;
     if (!more) break;
     vb = vn;
     ra = na;
     rb = nb;
   }
-  if constexpr (STAMP) {
-    if (tid == 0) {
-      const unsigned long long* src = (const unsigned long long*)(smem + RINGB);
-      for (int i = 0; i < min(ti, STAMP_TILES) * NSTAMP; ++i) stamps[(size_t)bid * STAMP_TILES * NSTAMP + i] = src[i];
-    }
-  }
   // no final drain: the last epilogue's vmcnt(0) retired every LDS-DMA (the last tile re-stages
   // its own first slices as dummies), so only its stores are in flight, and those may outlive the
   // waves
-}
-
-template <int EPI>
-__global__ void __launch_bounds__(512, 1)
-    gemm_ps_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
-                   bf16* __restrict__ C2, const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
-                   int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger) {
-  // nt output stores: the GPT-2 shapes 7-14 % faster than plain ones (profiles/r4_gemm_ps_diag.txt)
-  gemm_ps_body<EPI, 8, 1, false>(A, B, C, C2, bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger, nullptr);
-}
-
-// diagnostic instances: store cache policy x stamps (scripts/gemm_ps_diag.py)
-#define VCX_PS_DIAG(NAME, E, P, S)                                                                              \
-  __global__ void __launch_bounds__(512, 1)                                                                    \
-      NAME(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C, int M, int N, int K,   \
-           int lda, int ldb, int ldc, int tilesN, int tiles, unsigned long long* stamps, int stagger) {         \
-    gemm_ps_body<E, 8, P, S, 1>(A, B, C, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger, \
-                             (void*)stamps);                                                                   \
-  }
-VCX_PS_DIAG(gemm_ps_diag_none, EPI_NONE, 0, false)
-VCX_PS_DIAG(gemm_ps_diag_none_st, EPI_NONE, 0, true)
-VCX_PS_DIAG(gemm_ps_diag_p0, EPI_STORE, 0, false)
-VCX_PS_DIAG(gemm_ps_diag_p0_st, EPI_STORE, 0, true)
-VCX_PS_DIAG(gemm_ps_diag_p1, EPI_STORE, 1, false)
-VCX_PS_DIAG(gemm_ps_diag_p1_st, EPI_STORE, 1, true)
-VCX_PS_DIAG(gemm_ps_diag_p2, EPI_STORE, 2, false)
-VCX_PS_DIAG(gemm_ps_diag_p2_st, EPI_STORE, 2, true)
-VCX_PS_DIAG(gemm_ps_diag_p3, EPI_STORE, 3, false)
-VCX_PS_DIAG(gemm_ps_diag_p3_st, EPI_STORE, 3, true)
-#undef VCX_PS_DIAG
-
-template <int EPI>
-__global__ void __launch_bounds__(256, 2)
-    gemm_ps4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
-                    bf16* __restrict__ C2, const bf16* __restrict__ bias, float* __restrict__ colsum, int M, int N,
-                    int K, int lda, int ldb, int ldc, int tilesN, int tiles, int stagger) {
-  gemm_ps_body<EPI, 4, 1, false>(A, B, C, C2, bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger, nullptr);
 }
 
 }  // namespace gemm_ps
@@ -569,99 +454,45 @@ using namespace vcx;
 
 bool vcx_gemm_ps_supported(int M, int N, int K, int epi) {
   using namespace gemm_ps;
-  const bool known = epi == EPI_STORE || epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_DGELU || epi == EPI_NONE;
+  const bool known = epi == EPI_STORE || epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_DGELU;
   return M > 0 && N > 0 && M % BM == 0 && N % BN == 0 && K % 128 == 0 && K >= 256 && known &&
          ((epi != EPI_BIAS && epi != EPI_BIAS_GELU) || N <= BIAS_MAX);
 }
 
-// the two-workgroups-per-CU geometry (NW = 4): N % 128, no DGELU epilogue. K % 192: the 3-slot ring
-// stages 3 slices ahead and the loop takes 2 steps per iteration, so nk = K / 32 must be a multiple
-// of both (an odd nk ran one step too many into the next tile's slot 0: wrong tiles)
-bool vcx_gemm_ps2_supported(int M, int N, int K, int epi) {
-  using namespace gemm_ps;
-  const bool known = epi == EPI_STORE || epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_NONE;
-  return M > 0 && N > 0 && M % BM == 0 && N % 128 == 0 && K % 192 == 0 && K >= 192 && known &&
-         ((epi != EPI_BIAS && epi != EPI_BIAS_GELU) || N <= BIAS_MAX);
-}
-
-int vcx_gemm_ps_grid(int M, int N, int grid_cap, int nw) {
+int vcx_gemm_ps_grid(int M, int N, int grid_cap) {
   static const int ncu = [] {
     int dev = 0, n = 256;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     return n;
   }();
-  const int tiles = (M / gemm_ps::BM) * (N / (nw == 8 ? 256 : 128));
-  int grid = grid_cap > 0 ? grid_cap : (nw == 8 ? ncu : 2 * ncu);
+  const int tiles = (M / gemm_ps::BM) * (N / gemm_ps::BN);
+  int grid = grid_cap > 0 ? grid_cap : ncu;
   grid = grid < tiles ? grid & ~7 : tiles;  // a multiple of 8 (XCD remap) or one tile each
   return grid <= 0 ? tiles : grid;
 }
 
 void vcx_gemm_ps(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N,
-                 int K, int lda, int ldb, int ldc, int epi, int grid_cap, int nw, int stagger, hipStream_t s) {
+                 int K, int lda, int ldb, int ldc, int epi, int grid_cap, hipStream_t s) {
   using namespace gemm_ps;
   static const bool attrs = [] {
     for (const void* k : {(const void*)gemm_ps_kernel<EPI_STORE>, (const void*)gemm_ps_kernel<EPI_BIAS>,
-                          (const void*)gemm_ps_kernel<EPI_BIAS_GELU>, (const void*)gemm_ps_kernel<EPI_NONE>,
-                          (const void*)gemm_ps_kernel<EPI_DGELU>, (const void*)gemm_ps4_kernel<EPI_STORE>,
-                          (const void*)gemm_ps4_kernel<EPI_BIAS>, (const void*)gemm_ps4_kernel<EPI_BIAS_GELU>,
-                          (const void*)gemm_ps4_kernel<EPI_NONE>})
+                          (const void*)gemm_ps_kernel<EPI_BIAS_GELU>, (const void*)gemm_ps_kernel<EPI_DGELU>})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, RING + 2 * BIAS_MAX);
     return true;
   }();
   (void)attrs;
-  const int bn = nw == 8 ? 256 : 128;
-  const int tilesN = N / bn, tiles = (M / BM) * tilesN;
-  const int grid = vcx_gemm_ps_grid(M, N, grid_cap, nw);
-  const int ring = nw == 8 ? Geo<8>::RINGB : Geo<4>::RINGB;
-  const int lds = ring + (epi == EPI_BIAS || epi == EPI_BIAS_GELU ? (N * 2 + 15) & ~15 : 0);
+  const int tilesN = N / BN, tiles = (M / BM) * tilesN;
+  const int grid = vcx_gemm_ps_grid(M, N, grid_cap);
+  const int lds = Geo::RINGB + (epi == EPI_BIAS || epi == EPI_BIAS_GELU ? (N * 2 + 15) & ~15 : 0);
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(nw * 64), lds, s, (const bf16*)A, (const bf16*)B, (bf16*)C,
-                       (bf16*)C2, (const bf16*)bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles, stagger);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, (const bf16*)A, (const bf16*)B, (bf16*)C, (bf16*)C2,
+                       (const bf16*)bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles);
   };
-  if (nw == 4) {
-    switch (epi) {
-      case EPI_STORE: go(gemm_ps4_kernel<EPI_STORE>); break;
-      case EPI_BIAS: go(gemm_ps4_kernel<EPI_BIAS>); break;
-      case EPI_BIAS_GELU: go(gemm_ps4_kernel<EPI_BIAS_GELU>); break;
-      default: go(gemm_ps4_kernel<EPI_NONE>); break;
-    }
-    return;
-  }
   switch (epi) {
     case EPI_STORE: go(gemm_ps_kernel<EPI_STORE>); break;
     case EPI_BIAS: go(gemm_ps_kernel<EPI_BIAS>); break;
     case EPI_BIAS_GELU: go(gemm_ps_kernel<EPI_BIAS_GELU>); break;
-    case EPI_DGELU: go(gemm_ps_kernel<EPI_DGELU>); break;
-    default: go(gemm_ps_kernel<EPI_NONE>); break;
-  }
-}
-
-// diagnostic launcher: epi 0 (store) or 7 (no stores), policy 0..3, stamps [grid, 64, 5] or null
-void vcx_gemm_ps_diag(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, int epi,
-                      int policy, unsigned long long* stamps, int grid_cap, int stagger, hipStream_t s) {
-  using namespace gemm_ps;
-  const int tilesN = N / 256, tiles = (M / BM) * tilesN;
-  const int grid = vcx_gemm_ps_grid(M, N, grid_cap, 8);
-  const int lds = Geo<8>::RINGB + NSTAMP * STAMP_TILES * 8;
-  auto go = [&](auto kern) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, (const bf16*)A, (const bf16*)B, (bf16*)C, M, N, K, lda,
-                       ldb, ldc, tilesN, tiles, stamps, stagger);
-  };
-  const bool st = stamps != nullptr;
-  if (epi == EPI_NONE) {
-    st ? go(gemm_ps_diag_none_st) : go(gemm_ps_diag_none);
-    return;
-  }
-  switch (policy * 2 + (st ? 1 : 0)) {
-    case 0: go(gemm_ps_diag_p0); break;
-    case 1: go(gemm_ps_diag_p0_st); break;
-    case 2: go(gemm_ps_diag_p1); break;
-    case 3: go(gemm_ps_diag_p1_st); break;
-    case 4: go(gemm_ps_diag_p2); break;
-    case 5: go(gemm_ps_diag_p2_st); break;
-    case 6: go(gemm_ps_diag_p3); break;
-    default: go(gemm_ps_diag_p3_st); break;
+    default: go(gemm_ps_kernel<EPI_DGELU>); break;
   }
 }

@@ -1,0 +1,385 @@
+// Weight-gradient GEMM for gfx950 with wave-specialised operand loads and an XCD-shared L2 prefetch:
+//
+//   Cpart[s][M, N] = sum over tokens k of split s of A[k, M]^T . B[k, N]      (fp32 partials)
+//   out (bf16 [M, N]) (+)= sum_s Cpart[s]                                    (splitk_sum_kernel)
+//
+// The weight gradient of a token-major linear layer, dW[out, in] = dY[tok, out]^T X[tok, in]: both
+// operands are TOKEN-major (the reduction runs over their row index), the output is small (9..36 tiles
+// of 256 x 256 at GPT-2-small), so the token axis is split over the CUs and every split streams its
+// token range of both operands once. Structure, and why:
+//   * main loop of gemm_nt / gemm_tn: 256 x 256 tile per 512-thread workgroup (8 waves as 2 (M) x 4 (N),
+//     128 x 64 each, v_mfma_f32_16x16x32_bf16), 4-slot LDS ring of 32-token slices, counted vmcnt + raw
+//     s_barrier, fragments read TRANSPOSED out of the token-row LDS image by ds_read_b64_tr_b16
+//     (cdna guide T10) and double-buffered in registers.
+//   * the problem of the token-major wgrad (profiles/r2_gemm_tn.txt: waves parked on vmcnt 73 % of the
+//     time): every slice is a fresh HBM/MALL miss, and a wave's vmcnt retires in issue order, so
+//     neither a deeper ring (LDS is full) nor a prefetch issued by the waiting waves (gemm_tn's PF:
+//     the prefetch is older than the DMA the next wait covers) extends the latency a slice may take.
+//   * here the loads are split by WAVE ROLE. Waves 0-3 issue all 32 LDS-DMA pieces of a slice (8
+//     each) and do the counted waits. Waves 4-7 issue NO operand DMA: they touch the lines of slice
+//     t + PF (global_load_dword into a sink register, two per 128-B line) and never wait for them,
+//     so their own in-order vmcnt queue never blocks a barrier. By the time waves 0-3 stage slice
+//     t + PF, it is an L2 hit. All 8 waves run the same MFMAs.
+//   * the prefetch is SHARED across the tiles of a split: a split's tiles run side by side on one XCD
+//     (the XCD-aware order below) and read the same token rows, so tile (tm, tn) touches only its
+//     1/tilesN share of its A panel's slice lines and 1/tilesM of its B panel's: each line once per
+//     XCD, instead of every CU re-requesting its whole 32 KB slice (which would double the L2 request
+//     rate that the DMA itself already runs at about half of).
+// Reference analog: none (the reference trains nothing; SURVEY.md §2.9 north-star trainer).
+#include <type_traits>
+
+#include "vcx_common.h"
+
+namespace vcx {
+namespace gemm_wg {
+
+typedef short sx8 __attribute__((ext_vector_type(8)));
+typedef short sx4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 256, BN = 256, BKS = 32, NT = 512;
+constexpr int TROW = 512;                      // bytes per token row of a 256-wide operand slice
+constexpr int TSLOT_A = BKS * TROW;            // 16 KB
+constexpr int SLOT_BYTES = 2 * TSLOT_A;        // 32 KB: A and B slices
+constexpr int LDS_BYTES = 4 * SLOT_BYTES;      // 128 KB ring
+constexpr int OPS = 8;                         // LDS-DMA ops per slice per loader wave
+
+// 16-B chunk swizzle of a token row: F(r) = 2 (r & 3 | (r >> 3 & 1) << 2); a half-wave's two transposed
+// reads touch 8 rows (q = r & 3 and the group parity r >> 3 & 1) x 2 chunks, spread over all 16 bank
+// slots (conflict-free). LDS-DMA writes lane-linearly, so the swizzle goes on the GLOBAL source address.
+__device__ __forceinline__ int swz(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
+
+__device__ __forceinline__ sx8 tr_frag(const char* p0, const char* p1) {
+  const sx4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sx4*)(p0));
+  const sx4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sx4*)(p1));
+  return sx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// buffer resource words over [base, base + bytes) for inline asm ("s" operand): wave-uniform base and
+// size (SGPRs), 32-bit per-lane offsets
+__device__ __forceinline__ u32x4 desc(const void* base, int bytes) {
+  const uint64_t a = (uint64_t)base;
+  return u32x4{(unsigned)a, (unsigned)(a >> 32) & 0xffffu, (unsigned)bytes, 0x00020000u};
+}
+
+// One 1-KB LDS-DMA piece (16 B per lane to LDS base + 16 lane) as inline asm, M0 = the LDS byte address.
+// Why not __builtin_amdgcn_raw_ptr_buffer_load_lds: hipcc (ROCm 7.2) cannot tell a pending LDS-DMA from
+// the slot a later ds_read_b64_tr_b16 reads, so it drained vmcnt(0) in front of every transposed
+// fragment read of the step -- 8 full drains per step in gemm_tn, the whole pipeline serialised (the
+// "waves parked on vmcnt" of profiles/r2_gemm_tn.txt). Issued as asm, the DMA is invisible to that
+// pass; the kernel's own counted waits (wait_vm) order it. `s_nop 0`: the M0 write -> LDS-DMA hazard.
+__device__ __forceinline__ void dma16(u32x4 d, int voff, int soff, const char* lds) {
+  const unsigned m0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(d), "s"(soff), "{m0}"(m0)
+               : "memory");
+}
+
+// s_waitcnt vmcnt(N) lgkmcnt(0) for N up to 63 (vmcnt bits [3:0] and [15:14])
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  __builtin_amdgcn_s_waitcnt(0x0070 | (N & 15) | ((N >> 4) << 14));
+}
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }  // vmcnt 63: no VM wait
+__device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// L2 touch of one 128-B line (both 64-B halves): the loaded dwords land in `sink`, a register nothing
+// reads (kept allocated by the "+v" constraint of every touch); the prefetch waves drain their queue
+// once, after the main loop
+__device__ __forceinline__ void touch(u32x4 d, int voff, int soff, int& sink) {
+  asm volatile("buffer_load_dword %0, %1, %2, %3 offen\n\tbuffer_load_dword %0, %1, %2, %3 offen offset:64"
+               : "+v"(sink)
+               : "v"(voff), "s"(d), "s"(soff)
+               : "memory");
+}
+
+// A fragments of the wave's row blocks 0..5 are single-buffered (refilled right behind the MFMA group
+// that used them); rows 6, 7 and the B fragments alternate between two named sets, so every read of the
+// next slice is issued before the step's last MFMA group (96 -> 72 fragment VGPRs)
+struct Frags {
+  sx8 y[2];  // A fragments of row blocks 6, 7
+  sx8 w[4];  // B fragments: the wave's 4 column blocks of 16 (output columns)
+};
+
+template <int PF>
+__global__ void __launch_bounds__(NT, 1)
+    gemm_wg_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, float* __restrict__ Cpart, int M, int N,
+                   int K, int lda, int ldb, int tilesN, int tiles, int splits) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const bool loader = wid < 4;
+
+  // ---- XCD-aware bijective order over (split, tile): consecutive logical ids share an XCD, so the
+  // tiles of one split (same token range) run side by side there and share its L2
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int split = wg / tiles, tile = wg - split * tiles;
+  const int tm = tile / tilesN, tn = tile - tm * tilesN;
+  const int tilesM = tiles / tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nb64 = K >> 6;
+  const int kb0 = (int)((int64_t)split * nb64 / splits), kb1 = (int)((int64_t)(split + 1) * nb64 / splits);
+  const int kbeg = kb0 * 64;
+  const int nk = (kb1 - kb0) * 2;  // slices of 32 tokens: even, >= 6 (host: K / 192 >= splits)
+  const int64_t a_slice = (int64_t)BKS * lda, b_slice = (int64_t)BKS * ldb;
+
+  // ---- loader waves (0-3): piece P (0..15) of an operand slice = token rows 2P, 2P + 1 (64 lanes x 16 B);
+  // wave w moves pieces w + 4i (i = 0..3) of A and of B. Lane l: row 2P + (l >> 5), physical chunk l & 31,
+  // holding logical chunk (l & 31) ^ F(row); F depends on the row's bit 3 = i & 1, so even and odd i
+  // have their own per-lane source offsets. Buffer resources over this split's token rows of the tile's
+  // panels (host check: they fit 31 bits); the slice and the 16-row step of i >> 1 go into soffset.
+  const int ntok = (kb1 - kb0) * 64;
+  const int lw = wid & 3;
+  const int row_e = 2 * lw + (lane >> 5), row_o = row_e + 8;
+  const int ch_e = ((lane & 31) ^ swz(row_e)) * 8, ch_o = ((lane & 31) ^ swz(row_o)) * 8;
+  const bf16* a_base = A + (int64_t)kbeg * lda + m0;
+  const bf16* b_base = B + (int64_t)kbeg * ldb + n0;
+  const u32x4 ra = desc(a_base, ntok * lda * 2), rb = desc(b_base, ntok * ldb * 2);
+  const int va_e = (row_e * lda + ch_e) * 2, va_o = (row_o * lda + ch_o) * 2;
+  const int vb_e = (row_e * ldb + ch_e) * 2, vb_o = (row_o * ldb + ch_o) * 2;
+  const int a_sl = BKS * lda * 2, b_sl = BKS * ldb * 2;  // bytes per slice
+  char* const lds_w = smem + lw * 1024;
+
+  // op o (0..7) of slice s: A pieces for o < 4 (i = o), B pieces for o >= 4 (i = o - 4)
+  auto stage_op = [&](int s, int o) {
+    char* slot = lds_w + (s & 3) * SLOT_BYTES;
+    const int i = o & 3;
+    if (o < 4)
+      dma16(ra, (i & 1) ? va_o : va_e, s * a_sl + (i >> 1) * (a_sl >> 1), slot + i * 4096);
+    else
+      dma16(rb, (i & 1) ? vb_o : vb_e, s * b_sl + (i >> 1) * (b_sl >> 1), slot + TSLOT_A + i * 4096);
+  };
+  auto stage = [&](int s) {
+#pragma unroll
+    for (int o = 0; o < OPS; ++o) stage_op(s, o);
+  };
+
+  // ---- prefetch waves (4-7): waves 4, 5 touch this tile's share of its A panel's 128 slice lines (32
+  // rows x 4 lines of 128 B), waves 6, 7 its share of its B panel's; lanes past the share repeat its
+  // first line
+  const bool pfa = (wid & 2) == 0;
+  const int pl = (wid & 1) * 64 + lane;
+  int pf_voff;
+  {
+    const int lo = pfa ? tn * 128 / tilesN : tm * 128 / tilesM;
+    const int hi = pfa ? (tn + 1) * 128 / tilesN : (tm + 1) * 128 / tilesM;
+    const int j = lo + (pl < hi - lo ? pl : 0);
+    pf_voff = ((j >> 2) * (pfa ? lda : ldb) + (j & 3) * 64) * 2;
+  }
+  const u32x4 pf_desc = pfa ? desc(a_base, ntok * lda * 2) : desc(b_base, ntok * ldb * 2);
+  const int pf_sl = pfa ? a_sl : b_sl;
+  int sink = 0;
+  auto prefetch = [&](int t) {
+    if (t < nk) touch(pf_desc, pf_voff, t * pf_sl, sink);
+  };
+
+  // ---- transposed fragment reads: lane l (group g = l >> 4, e = l & 15, q = e >> 2, p = e & 3)
+  // supplies, for read h, the address of token row 8g + 4h + q, columns c0 + 4p .. c0 + 4p + 3 of the
+  // 16-column block; it receives column c0 + e of the 4 rows
+  const int g = lane >> 4, e = lane & 15, qq = e >> 2, pp = e & 3;
+  // rows r0 and r0 + 4 have the same F (F ignores row bit 2), so the read of row r0 + 4 is the read of
+  // row r0 plus the immediate 4 * TROW: one address register per 16-column block, not two
+  const int r0 = 8 * g + qq;
+  const int f0 = swz(r0);
+  const int half8 = (pp & 1) * 8, hchunk = pp >> 1;
+  auto toff = [&](int c) { return r0 * TROW + ((((c >> 3) ^ f0) + hchunk) << 4) + half8; };
+
+  sx8 x[6];
+  auto xfrag = [&](int s, int i) {  // A row block i of slice s
+    const char* so = smem + (s & 3) * SLOT_BYTES;
+    const int c = wm * 128 + 16 * i;
+    return tr_frag(so + toff(c), so + toff(c) + 4 * TROW);
+  };
+  auto wfrag = [&](int s, int j) {  // B column block j of slice s
+    const char* so = smem + (s & 3) * SLOT_BYTES + TSLOT_A;
+    const int c = wn * 64 + 16 * j;
+    return tr_frag(so + toff(c), so + toff(c) + 4 * TROW);
+  };
+  // part 0: x[0, 1], w[0, 1]; part 1: x[2, 3], w[2, 3]; part 2: x[4, 5], y[0, 1]
+  auto load_part = [&](Frags& f, int s, int part) {
+    x[2 * part] = xfrag(s, 2 * part);
+    x[2 * part + 1] = xfrag(s, 2 * part + 1);
+    if (part < 2) {
+      f.w[2 * part] = wfrag(s, 2 * part);
+      f.w[2 * part + 1] = wfrag(s, 2 * part + 1);
+    } else {
+      f.y[0] = xfrag(s, 6);
+      f.y[1] = xfrag(s, 7);
+    }
+  };
+  auto load = [&](Frags& f, int s) {
+#pragma unroll
+    for (int part = 0; part < 3; ++part) load_part(f, s, part);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto mma = [&](const Frags& f, auto I0, auto I1) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = decltype(I0)::value; i < decltype(I1)::value; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const sx8& xf = i < 6 ? x[i < 6 ? i : 0] : f.y[i >= 6 ? i - 6 : 0];
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[j], xf, acc[i][j], 0, 0, 0);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  using I0c = std::integral_constant<int, 0>;
+  using I2c = std::integral_constant<int, 2>;
+  using I4c = std::integral_constant<int, 4>;
+  using I6c = std::integral_constant<int, 6>;
+  using I8c = std::integral_constant<int, 8>;
+
+  // one step of either role: slice s in registers (fc); make slice s + 1 visible, issue [loader: slice
+  // s + 4 into the slot of slice s | prefetch: touch slice s + PF], read slice s + 1 into fn, MFMAs of
+  // slice s. LDS-DMA ops / touches and ds_reads interleave with the 4 MFMA groups.
+  auto step = [&](int s, Frags& fc, Frags& fn, auto ROLE, auto STAGE, auto LOAD, auto PEND) {
+    constexpr bool ld_role = decltype(ROLE)::value;
+    constexpr bool st = decltype(STAGE)::value, ld = decltype(LOAD)::value;
+    if constexpr (ld_role)
+      wait_vm<decltype(PEND)::value>();  // own DMA of slice s + 1 retired; own ds_reads too
+    else
+      wait_lgkm0();  // the prefetch waves wait only for their ds_reads: their touches never block
+    barrier();
+    if constexpr (!ld_role && PF > 0) prefetch(s + PF);
+    if constexpr (ld_role && st) stage_op(s + 4, 0), stage_op(s + 4, 4);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(fc, I0c{}, I2c{});
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (ld) load_part(fn, s + 1, 0);
+    if constexpr (ld_role && st) stage_op(s + 4, 1), stage_op(s + 4, 5);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(fc, I2c{}, I4c{});
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (ld) load_part(fn, s + 1, 1);
+    if constexpr (ld_role && st) stage_op(s + 4, 2), stage_op(s + 4, 6);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(fc, I4c{}, I6c{});
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (ld) load_part(fn, s + 1, 2);
+    if constexpr (ld_role && st) stage_op(s + 4, 3), stage_op(s + 4, 7);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(fc, I6c{}, I8c{});
+  };
+
+  using T = std::true_type;
+  using F = std::false_type;
+  using PS = std::integral_constant<int, 2 * OPS>;  // steady state: two staging steps after slice s + 1
+  using PT1 = std::integral_constant<int, OPS>;
+  using P0 = std::integral_constant<int, 0>;
+  Frags f0r, f1r;
+  // the two roles run the same barrier sequence from two copies of the loop (wave-uniform branch)
+  auto run = [&](auto ROLE) {
+    constexpr bool ld_role = decltype(ROLE)::value;
+    if constexpr (ld_role) {
+      stage(0);
+      stage(1);
+      stage(2);
+      stage(3);
+      wait_vm<3 * OPS>();  // slice 0 landed
+    } else {
+      if constexpr (PF > 4) {
+#pragma unroll 1
+        for (int t = 4; t < PF; ++t) prefetch(t);
+      }
+    }
+    barrier();
+    load(f0r, 0);
+    int s = 0;
+#pragma unroll 1
+    for (; s + 5 < nk; s += 2) {
+      step(s, f0r, f1r, ROLE, T{}, T{}, PS{});
+      step(s + 1, f1r, f0r, ROLE, T{}, T{}, PS{});
+    }
+    step(s, f0r, f1r, ROLE, F{}, T{}, PS{});
+    step(s + 1, f1r, f0r, ROLE, F{}, T{}, PT1{});
+    step(s + 2, f0r, f1r, ROLE, F{}, T{}, P0{});
+    mma(f1r, I0c{}, I8c{});
+  };
+  if (loader)
+    run(T{});
+  else
+    run(F{});
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(sink)::"memory");  // no touch may land in a reused register
+
+  // ---- fp32 partial: acc[i][j] = C[m][n .. n + 3], m = row block i + (lane & 15), n = column block j
+  const int mrow = m0 + wm * 128 + (lane & 15);
+  const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
+  float* cp = Cpart + (int64_t)split * M * N;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *(f32x4*)(cp + (int64_t)(mrow + 16 * i) * N + ncol + 16 * j) = acc[i][j];
+}
+
+// out[i] (bf16) = (accumulate ? out[i] : 0) + sum_s part[s][i], 4 elements per thread
+__global__ void __launch_bounds__(256) splitk_sum_kernel(const float* __restrict__ part, bf16* __restrict__ out,
+                                                         int64_t n, int splits, int accumulate) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  f32x4 a = *(const f32x4*)(part + i);
+  for (int s = 1; s < splits; ++s) a += *(const f32x4*)(part + (int64_t)s * n + i);
+  bf16x4 o = *(bf16x4*)(out + i);
+  bf16x4 r;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) r[t] = (bf16)((accumulate ? (float)o[t] : 0.f) + a[t]);
+  *(bf16x4*)(out + i) = r;
+}
+
+}  // namespace gemm_wg
+}  // namespace vcx
+
+using namespace vcx;
+
+bool vcx_gemm_wg_supported(int M, int N, int K, int splits) {
+  return M > 0 && N > 0 && M % gemm_wg::BM == 0 && N % gemm_wg::BN == 0 && K % 64 == 0 && splits >= 1 &&
+         K / 192 >= splits;  // >= 3 blocks of 64 tokens per split (nk >= 6)
+}
+
+// token-axis splits: about one round of workgroups over the CUs ((M/256)(N/256) tiles x S)
+int vcx_gemm_wg_splits(int M, int N, int K) {
+  const int tiles = (M / gemm_wg::BM) * (N / gemm_wg::BN);
+  int s = 256 / (tiles > 0 ? tiles : 1);
+  if (s < 1) s = 1;
+  if (s > K / 192) s = K / 192;
+  return s < 1 ? 1 : s;
+}
+
+// Cpart[splits, M, N] (fp32 workspace) = per-split A[K, M]^T . B[K, N]; then out (bf16 [M, N], row
+// stride N) = (accumulate ? out : 0) + the sum of the partials. pf: L2 prefetch distance in slices
+// (0, 4, 6, 8 or 12)
+void vcx_gemm_wg(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
+                 int splits, int accumulate, int pf, hipStream_t s) {
+  using namespace gemm_wg;
+  const int tilesN = N / BN, tiles = (M / BM) * tilesN;
+  static const bool attrs = [] {
+    for (const void* k : {(const void*)gemm_wg_kernel<0>, (const void*)gemm_wg_kernel<4>,
+                          (const void*)gemm_wg_kernel<6>, (const void*)gemm_wg_kernel<8>,
+                          (const void*)gemm_wg_kernel<12>})
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    return true;
+  }();
+  (void)attrs;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(tiles * splits), dim3(NT), LDS_BYTES, s, (const bf16*)A, (const bf16*)B, Cpart, M,
+                       N, K, lda, ldb, tilesN, tiles, splits);
+  };
+  switch (pf) {
+    case 0: go(gemm_wg_kernel<0>); break;
+    case 4: go(gemm_wg_kernel<4>); break;
+    case 6: go(gemm_wg_kernel<6>); break;
+    case 12: go(gemm_wg_kernel<12>); break;
+    default: go(gemm_wg_kernel<8>); break;
+  }
+  const int64_t n = (int64_t)M * N;
+  hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, s, Cpart, (bf16*)out, n,
+                     splits, accumulate);
+}

@@ -14,6 +14,11 @@ void vcx_lsgd_apply(const void* avg, float* anchor, float* master, void* param, 
                     float outer_lr, float mu, int nesterov, float avg_scale, hipStream_t s);
 void vcx_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s);
 void vcx_axpy_bf16(const void* src, void* acc, int64_t n, float scale, hipStream_t s);
+// gemm_wg.hip: weight gradient out (+)= A[K, M]^T B[K, N], wave-specialised loads + shared L2 prefetch
+bool vcx_gemm_wg_supported(int M, int N, int K, int splits);
+int vcx_gemm_wg_splits(int M, int N, int K);
+void vcx_gemm_wg(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
+                 int splits, int accumulate, int pf, hipStream_t s);
 bool vcx_gemm_tn_supported(int M, int N, int K, int splits);
 void vcx_gemm_tn(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
                  int splits, int accumulate, hipStream_t s);
@@ -24,15 +29,10 @@ void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bi
 // gemm_ps.hip: persistent store-overlapped GEMM, C = A B^T (B [N, K]); epi 0 store, 1 +bias,
 // 2 +bias -> (C = pre, C2 = gelu(pre)); grid_cap <= 0: one workgroup per CU
 bool vcx_gemm_ps_supported(int M, int N, int K, int epi);
-bool vcx_gemm_ps2_supported(int M, int N, int K, int epi);
-void vcx_gemm_ps_diag(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, int epi,
-                      int policy, unsigned long long* stamps, int grid_cap, int stagger, hipStream_t s);
-int vcx_gemm_ps_grid(int M, int N, int grid_cap, int nw);
+int vcx_gemm_ps_grid(int M, int N, int grid_cap);
 // epi 4: C = (A B^T) * gelu'(C2) with fp32 column sums added into colsum
-// nw = 8: one 512-thread workgroup per CU (256 x 256 tiles); nw = 4: two 256-thread workgroups
-// per CU (256 x 128 tiles), the second half of the grid starting `stagger` x ~8k cycles late
 void vcx_gemm_ps(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N,
-                 int K, int lda, int ldb, int ldc, int epi, int grid_cap, int nw, int stagger, hipStream_t s);
+                 int K, int lda, int ldb, int ldc, int epi, int grid_cap, hipStream_t s);
 void vcx_transpose_bf16(const void* src, void* dst, int R, int Cc, hipStream_t s);
 void vcx_add_f32_into_bf16(const float* in, void* out, int n, int accumulate, hipStream_t s);
 void vcx_reduce_bcast_bf16(const void* in, void* out, void* mine, int P, int64_t n, hipStream_t s);

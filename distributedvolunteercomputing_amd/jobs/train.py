@@ -161,7 +161,11 @@ def main(argv=None):
     dtype = torch.bfloat16 if cuda else torch.float32
     model = model.to(device=device, dtype=dtype)
     if a.model.startswith("resnet"):
+        from ..models.resnet import enable_conv_find
+
         model = model.to(memory_format=torch.channels_last)
+        if device.type == "cuda":
+            enable_conv_find()
     if a.trainer == "localsgd":
         from ..parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer
 

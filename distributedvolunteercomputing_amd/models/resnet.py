@@ -85,8 +85,6 @@ class ResNet(nn.Module):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
 
     def forward(self, x, y=None):
-        if x.is_cuda and config.get().conv_find and not torch.backends.cudnn.benchmark:
-            torch.backends.cudnn.benchmark = True  # process-wide: MIOpen Find for the 3x3 / 7x7 convolutions
         x = bn_act(self.stem(x), self.bn)
         x = stem_maxpool(x)  # HIP on channels-last bf16 (ops/batchnorm.py)
         x = self.blocks(x)
@@ -95,6 +93,15 @@ class ResNet(nn.Module):
         if y is None:
             return logits
         return F.cross_entropy(logits.float(), y)
+
+
+def enable_conv_find():
+    """MIOpen Find per convolution shape (torch.backends.cudnn.benchmark) for the 3x3 / 7x7
+    convolutions, when config.conv_find is on. Process-wide, so the training job / bench that builds
+    the ResNet calls it once at setup -- never the model's forward (a forward that flips a
+    global made every later convolution of the process, other models and tests included, run Find)."""
+    if config.get().conv_find:
+        torch.backends.cudnn.benchmark = True
 
 
 def resnet50(n_classes=1000):

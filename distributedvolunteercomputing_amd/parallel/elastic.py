@@ -315,11 +315,15 @@ class ElasticMembership:
                                                 or os.environ.get("MASTER_ADDR", "127.0.0.1"))
         self._live: _Liveness | None = None
         self._eof: dict[int, str] = {}
-        # member -> (address, heartbeat count, time) of a refused liveness connect: dead only if its
-        # heartbeat has not moved for refuse_grace_s after that (a peer that refuses because of a
-        # routing problem still heartbeats; one that died before we connected does not)
-        self._refused: dict[int, tuple[str, int, float]] = {}
-        self.refuse_grace_s = max(0.3, 3.0 * heartbeat_s)
+        # member -> (address, heartbeat count, time of the first refusal, refusals) of refused liveness
+        # connects: a refusal is only a hint (NAT, overlapping container addresses), so the member is
+        # dead only after refuse_min consecutive refusals of the same address with its heartbeat
+        # standing still for refuse_grace_s since the first one (one refusal plus a 0.6 s
+        # GIL / store stall of its heartbeat evicted live peers). Connects are retried every 2 s, so
+        # a death found this way takes >= 2 s; a peer that dies AFTER we connected is an EOF instead.
+        self._refused: dict[int, tuple[str, int, float, int]] = {}
+        self.refuse_min = 2
+        self.refuse_grace_s = max(2.0, 3.0 * heartbeat_s)
         self.eof_events: list[tuple[int, float]] = []  # (member, time) of every EOF seen
         self._ring_pending = False  # an EOF arrived: the heartbeat thread rings the round's bell
         self._tag = ""  # the armed guard's round tag (its verdict key is posted on a trip)
@@ -414,24 +418,29 @@ class ElasticMembership:
         except Exception:  # noqa: BLE001
             return
         with self._lock:
-            self._refused[m] = (addr, hb, time.time())
+            r = self._refused.get(m)
+            if r is not None and r[0] == addr and r[1] == hb:
+                self._refused[m] = (addr, hb, r[2], r[3] + 1)  # the same standing incarnation again
+            else:
+                self._refused[m] = (addr, hb, time.time(), 1)
 
     def _dead(self, m: int) -> bool:
         """Member m's process is known to be gone: its established liveness link hit EOF, or its
-        published address refused a connect and its heartbeat stood still for refuse_grace_s."""
+        published address refused refuse_min connects in a row while its heartbeat stood still for
+        refuse_grace_s."""
         if m in self._eof and self._gone(m):
             return True
         with self._lock:
             r = self._refused.get(m)
         if r is None or self._live is None:
             return False
-        addr, hb0, t0 = r
+        addr, hb0, t0, n = r
         if self._live.address_of(m) != addr or self._hb(m) != hb0:
             with self._lock:
                 if self._refused.get(m) == r:
                     del self._refused[m]  # restarted, or alive behind a route we cannot use
             return False
-        return time.time() - t0 > self.refuse_grace_s
+        return n >= self.refuse_min and time.time() - t0 > self.refuse_grace_s
 
     def _gone(self, m: int) -> bool:
         """Did the connection to member m's CURRENT incarnation close (a restarted peer publishes

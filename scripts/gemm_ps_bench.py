@@ -82,7 +82,7 @@ def main():
     check()
     if "--check-only" in sys.argv:
         return
-    tl = tn = tp = 0.0
+    tl = tn = 0.0
     shapes = [("qkv", 2304, 768), ("proj", 768, 768), ("fc", 3072, 768), ("fc2", 768, 3072),
               ("dg_qkv", 768, 2304), ("dg_proj", 768, 768), ("dg_fc", 768, 3072), ("dg_fc2", 3072, 768)]
     for name, n, k in shapes:
@@ -95,14 +95,11 @@ def main():
             lib = lambda: torch.mm(a, bt)  # noqa: E731
         else:
             lib = lambda: F.linear(a, b)  # noqa: E731
-        t_lib, t_ps, t_ps2, t_no = timeit([lib, lambda: C.gemm_ps(a, b, c), lambda: C.gemm_ps(a, b, c, grid_cap=512),
-                                           lambda: C.gemm_ps(a, b, c, epi=7)])
-        tl, tn, tp = tl + t_lib, tn + min(t_ps, t_ps2), tp + t_no
+        t_lib, t_ps = timeit([lib, lambda: C.gemm_ps(a, b, c)])
+        tl, tn = tl + t_lib, tn + t_ps
         print(f"{name:7s} N={n:5d} K={k:5d}  library {t_lib:7.1f} us ({fl / t_lib / 1e6:5.0f} TF)  gemm_ps {t_ps:7.1f} "
-              f"({fl / t_ps / 1e6:5.0f})  grid512 {t_ps2:7.1f} ({fl / t_ps2 / 1e6:5.0f})  no-store {t_no:7.1f} "
-              f"({fl / t_no / 1e6:5.0f} TF)", flush=True)
-    print(f"total (8 shapes) library {tl:.0f} us, gemm_ps best {tn:.0f} us, gemm_ps without stores {tp:.0f} us",
-          flush=True)
+              f"({fl / t_ps / 1e6:5.0f} TF)  ratio {t_lib / t_ps:5.3f}", flush=True)
+    print(f"total (8 shapes) library {tl:.0f} us, gemm_ps {tn:.0f} us", flush=True)
     # fc + bias + GELU: library GEMM + the separate bias_gelu pass vs the fused epilogue
     a = torch.randn(M, 768, device=dev, dtype=bf)
     w = torch.randn(3072, 768, device=dev, dtype=bf) * 0.02
@@ -129,10 +126,8 @@ def main():
         b = torch.rand(n, n, device=dev, dtype=bf) * 2 - 1
         c = torch.empty(n, n, device=dev, dtype=bf)
         fl = 2.0 * n ** 3
-        t_lib, t_ps, t_no = timeit([lambda: F.linear(a, b), lambda: C.gemm_ps(a, b, c),
-                                    lambda: C.gemm_ps(a, b, c, epi=7)])
-        print(f"{n}^3  library {fl / t_lib / 1e6:5.0f} TF  gemm_ps {fl / t_ps / 1e6:5.0f} TF  no-store {fl / t_no / 1e6:5.0f} TF",
-              flush=True)
+        t_lib, t_ps = timeit([lambda: F.linear(a, b), lambda: C.gemm_ps(a, b, c)])
+        print(f"{n}^3  library {fl / t_lib / 1e6:5.0f} TF  gemm_ps {fl / t_ps / 1e6:5.0f} TF", flush=True)
     # grid sweep at the qkv shape (persistence: tiles per workgroup)
     a = torch.randn(M, 768, device=dev, dtype=bf)
     b = torch.randn(2304, 768, device=dev, dtype=bf) * 0.02

@@ -38,6 +38,32 @@ def test_bench_single_process():
     _check(_json_line(r.stdout), 1)
 
 
+@pytest.mark.slow
+def test_bench_gpus_flag_spawns_ranks_without_torchrun():
+    """The driver's literal `python bench.py --gpus 4` (no launcher): bench.py starts 4 ranks itself
+    (a child torch.distributed.run, never an exec) and the JSON reports the group that formed."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", *ARGS], cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    _check(rec, 4)
+    assert rec["rccl_world"] == 4 and rec["backend"] == "gloo" and len(rec["devices"]) == 4
+    assert rec["sync_rounds_timed"] == 2 and rec["sync_ms_timed_mean"] > 0  # H = 2, 4 timed steps
+
+
+def test_bench_mismatched_launch_fails_loudly():
+    """--gpus 4 under a 2-rank launch must not report a 2-rank number as a 4-GPU run."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "4", *ARGS]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "WORLD_SIZE=2" in r.stderr
+
+
 def _torchrun(n, extra=()):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -183,3 +183,35 @@ def test_unreachable_liveness_address_is_not_a_death():
     finally:
         if old is not None:
             os.environ["MASTER_ADDR"] = old
+
+
+def test_refused_member_with_briefly_stalled_heartbeat_is_not_evicted():
+    """a live member whose published liveness address refuses connects (NAT,
+    overlapping container addresses) and whose heartbeat then stalls for ~1 s (GIL, store latency)
+    must not be declared dead; a refusing member whose heartbeat stands still across repeated
+    refusals is."""
+    from distributedvolunteercomputing_amd.parallel.elastic import _P, ElasticMembership
+
+    port = _mp.free_port()
+    store = _mp.make_store(0, 1, port)
+    mem = ElasticMembership(store, 0, backend="gloo", lease_s=3.0, heartbeat_s=0.2, liveness=True)
+    mem.start_heartbeat()
+    try:
+        refusing = f"127.0.0.1:{_mp.free_port()}"  # nobody listens: ECONNREFUSED
+        store.set(f"{_P}live/7", refusing)
+        store.add(f"{_P}hb/7", 1)
+        mem._on_refused(7, refusing)
+        time.sleep(1.0)  # member 7's heartbeat stalls 1 s
+        assert not mem._dead(7)
+        mem._on_refused(7, refusing)  # a second refusal, still inside the grace
+        assert not mem._dead(7)
+        store.add(f"{_P}hb/7", 1)  # its heartbeat moves again: the refusals were only a hint
+        assert not mem._dead(7) and 7 not in mem._refused
+        # a member that really died: refused again and again, heartbeat frozen past the grace
+        mem._on_refused(7, refusing)
+        time.sleep(mem.refuse_grace_s + 0.1)
+        assert not mem._dead(7)  # one refusal is never enough
+        mem._on_refused(7, refusing)
+        assert mem._dead(7)
+    finally:
+        mem.stop_heartbeat()

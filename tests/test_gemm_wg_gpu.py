@@ -1,0 +1,72 @@
+"""Weight-gradient GEMM gemm_wg (csrc/kernels/gemm_wg.hip: wave-specialised loads -- waves 0-3 stage
+the LDS ring by inline-asm LDS-DMA, waves 4-7 touch the lines of slice t + PF into L2 -- token-major
+operands read transposed by ds_read_b64_tr_b16, split-K fp32 partials) against an fp32 torch oracle,
+at every prefetch distance, with ragged splits, strided rows and accumulation into a gradient."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(dy, x):
+    return dy.float().t() @ x.float()
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(4096, 768, 3072, 7), (4096, 3072, 768, 7), (8192, 2304, 768, 9),
+                                          (2048, 768, 768, 10), (1024, 256, 512, 1), (8192, 512, 256, 3),
+                                          (65536, 768, 768, 28)])
+def test_gemm_wg_matches_fp32(gpu, M, N, K, splits):
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    g = torch.Generator(device=gpu).manual_seed(M + N + K)
+    dy = torch.randn(M, N, device=gpu, generator=g).to(torch.bfloat16)
+    x = torch.randn(M, K, device=gpu, generator=g).to(torch.bfloat16)
+    ref = _ref(dy, x)
+    scale = ref.abs().max().item()
+    for pf in (0, 4, 6, 8, 12):
+        out = torch.full((N, K), float("nan"), device=gpu, dtype=torch.bfloat16)
+        C.gemm_wg(dy, x, out, False, splits, pf)
+        err = (out.float() - ref).abs().max().item()
+        assert err <= 8e-3 * scale, (pf, err, scale)
+    # accumulate into an existing gradient (the flat .grad path)
+    base = torch.randn(N, K, device=gpu, generator=g).to(torch.bfloat16)
+    acc = base.clone()
+    C.gemm_wg(dy, x, acc, True, splits, 8)
+    err2 = (acc.float() - (ref + base.float())).abs().max().item()
+    assert err2 <= 8e-3 * scale, (err2, scale)
+
+
+def test_gemm_wg_strided_rows_default_splits_and_refusals(gpu):
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    g = torch.Generator(device=gpu).manual_seed(7)
+    big = torch.randn(4096, 1024, device=gpu, generator=g).to(torch.bfloat16)
+    dy = big[:, :768]  # lda = 1024
+    x = torch.randn(4096, 512, device=gpu, generator=g).to(torch.bfloat16)
+    out = torch.empty(768, 512, device=gpu, dtype=torch.bfloat16)
+    C.gemm_wg(dy, x, out)  # default splits and prefetch distance
+    ref = _ref(dy, x)
+    assert (out.float() - ref).abs().max().item() <= 8e-3 * ref.abs().max().item()
+    assert not C.gemm_wg_supported(768, 500, 4096)  # N % 256
+    assert not C.gemm_wg_supported(768, 512, 4000)  # tokens % 64
+    with pytest.raises(RuntimeError):
+        C.gemm_wg(dy, x, out, False, 0, 5)  # no such prefetch distance
+
+
+def test_gemm_wg_repeat_runs_bit_identical(gpu):
+    """No atomics anywhere: repeats must match bit for bit (a slot read before its LDS-DMA landed
+    would show as differing tiles from run to run)."""
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    g = torch.Generator(device=gpu).manual_seed(11)
+    dy = torch.randn(16384, 2304, device=gpu, generator=g).to(torch.bfloat16)
+    x = torch.randn(16384, 768, device=gpu, generator=g).to(torch.bfloat16)
+    out = torch.empty(2304, 768, device=gpu, dtype=torch.bfloat16)
+    C.gemm_wg(dy, x, out)
+    first = out.clone()
+    for _ in range(10):
+        C.gemm_wg(dy, x, out)
+        assert torch.equal(out, first)

@@ -205,6 +205,7 @@ def test_fused_batchnorm_act_vs_fp32(gpu, C, res, relu):
     if r is not None:
         r.requires_grad_()
     y = bn_act(x, bn, r, relu)
+    assert type(y.grad_fn).__name__ == "_BNActBackward"  # the HIP kernels ran, not the torch fallback
     g = torch.randn_like(y)
     y.backward(g)
     x32 = x.detach().float().requires_grad_()
@@ -299,6 +300,7 @@ def test_stem_maxpool_matches_torch(gpu, shape, ties):
         x = torch.randn(shape, device=gpu)
     x = x.to(torch.bfloat16).to(memory_format=torch.channels_last).requires_grad_()
     y = stem_maxpool(x)
+    assert type(y.grad_fn).__name__ == "_MaxPool3s2Backward"  # the HIP kernels ran, not torch's max_pool2d
     assert y.is_contiguous(memory_format=torch.channels_last)
     g = torch.randint(-4, 5, y.shape, device=gpu).to(torch.bfloat16)  # exact fp32 sums in both backwards
     y.backward(g)
@@ -308,3 +310,47 @@ def test_stem_maxpool_matches_torch(gpu, shape, ties):
     yt.backward(g)
     assert torch.equal(y, yt)
     assert torch.equal(x.grad, xt.grad)
+
+
+def test_stem_maxpool_propagates_nan_like_torch(gpu):
+    """a window holding a NaN outputs NaN even when a larger finite value follows the NaN in
+    scan order (torch: `val > max || isnan(val)`; nothing replaces a NaN once held)."""
+    from distributedvolunteercomputing_amd.ops.batchnorm import stem_maxpool
+
+    torch.manual_seed(3)
+    x = torch.randn(2, 8, 9, 9, device=gpu)
+    x[0, :, 2, 2] = float("nan")  # then larger finite values right after it in the same windows
+    x[0, :, 2, 3] = 100.0
+    x[1, 3, 0, 0] = float("nan")
+    x = x.to(torch.bfloat16).to(memory_format=torch.channels_last).requires_grad_()
+    y = stem_maxpool(x)
+    assert type(y.grad_fn).__name__ == "_MaxPool3s2Backward"
+    with reference_ops(), torch.no_grad():
+        yt = torch.nn.functional.max_pool2d(x, 3, 2, 1)
+    y = y.detach()
+    assert torch.equal(torch.isnan(y), torch.isnan(yt)) and bool(torch.isnan(y).any())
+    fin = ~torch.isnan(yt)
+    assert torch.equal(y[fin], yt[fin])
+
+
+def test_fused_batchnorm_large_mean_variance(gpu):
+    """|mean| >> std over many rows. The statistics are summed around a per-channel pivot
+    (a value of the batch), so the variance keeps its digits where E[x^2] - m^2 on raw fp32 sums would
+    cancel; checked against torch in fp32 (output, running variance)."""
+    from distributedvolunteercomputing_amd.ops.batchnorm import bn_act
+
+    torch.manual_seed(11)
+    C = 64
+    bn = torch.nn.BatchNorm2d(C, momentum=1.0).to(gpu)  # running_var = this batch's unbiased variance
+    bn32 = torch.nn.BatchNorm2d(C, momentum=1.0).to(gpu)
+    bn32.load_state_dict(bn.state_dict())
+    bn = bn.to(torch.bfloat16)
+    # mean 200, std 0.5 (bf16 spacing at 200 is 1.0: quantised, but torch sees the same bf16 values)
+    x = (200 + 0.5 * torch.randn(32, C, 56, 56, device=gpu)).to(torch.bfloat16)
+    x = x.to(memory_format=torch.channels_last)
+    y = bn_act(x, bn, None, relu=False)
+    assert type(y.grad_fn).__name__ == "_BNActBackward"
+    y32 = bn32(x.float())
+    var_ref = bn32.running_var
+    assert float(((bn.running_var.float() - var_ref).abs() / var_ref).max()) < 2e-2
+    assert float((y.float() - y32).norm() / y32.norm()) < 2e-2
