@@ -33,7 +33,7 @@ class RuntimeConfig:
     mlp: str = "fused"  # VCX_MLP: GPT-2 MLP fc (+bias+GELU) and fc2-dgrad (*gelu' + bias grad) on the persistent
     # hand-written GEMM's fused epilogues (csrc/kernels/gemm_ps.hip), other GEMMs on `gemm`; "lib": library + passes
     dgrad_ps: bool = True  # VCX_DGRAD_PS: input gradients dX = dY W with K <= 2304 on gemm_ps (measured faster)
-    gemm_wgrad: str = "lib"  # VCX_GEMM_WGRAD: weight gradients on "lib" (split-M batched GEMM) or "vcx" (gemm_tn)
+    gemm_wgrad: str = "vcx"  # VCX_GEMM_WGRAD: weight gradients on "vcx" (gemm_wg, hand-written) or "lib" (split-M batched GEMM)
     gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)
     wgrad_big_split_min_m: int = 16384  # VCX_WGRAD_BIG_SPLIT_MIN_M: rows above which weight grads split over K
     async_wgrad: bool = False  # VCX_ASYNC_WGRAD: weight-grad GEMMs on a side stream (measured slower)

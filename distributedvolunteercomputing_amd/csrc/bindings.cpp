@@ -319,36 +319,14 @@ std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Te
 }
 
 // Weight gradient out[M, N] (+)= a[K, M]^T . b[K, N] (token-major operands) on the hand-written
-// transposed-read MFMA kernel, split-K over the token axis with fp32 partials
-bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t splits) {
-  return vcx_gemm_tn_supported((int)M, (int)N, (int)K, (int)splits);
-}
-
-void gemm_tn(at::Tensor a, at::Tensor b, at::Tensor out, int64_t splits, bool accumulate) {
-  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_tn: 2-D cuda tensors");
-  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
-              "gemm_tn: bf16 operands");
-  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.is_contiguous(), "gemm_tn: row-major operands, contiguous out");
-  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
-  TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "gemm_tn: shape mismatch");
-  TORCH_CHECK(vcx_gemm_tn_supported((int)M, (int)N, (int)K, (int)splits),
-              "gemm_tn: needs M % 256 == 0, N % 256 == 0, K % 64 == 0, K / 128 >= splits");
-  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_tn: 16-B aligned rows");
-  for (const at::Tensor* t : {&a, &b, &out})
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_tn: 16-B aligned base pointers");
-  at::Tensor ws = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
-  vcx_gemm_tn(a.data_ptr(), b.data_ptr(), ws.data_ptr<float>(), out.data_ptr(), (int)M, (int)N, (int)K,
-              (int)a.stride(0), (int)b.stride(0), (int)splits, accumulate ? 1 : 0, cur_stream());
-}
-
-// Weight gradient out[M, N] (+)= a[K, M]^T . b[K, N] (token-major operands) on the wave-specialised
 // gemm_wg (csrc/kernels/gemm_wg.hip): split-K over the token axis with fp32 partials summed into out.
-// splits <= 0: vcx_gemm_wg_splits; pf: L2 prefetch distance in 32-token slices (0, 4, 6, 8, 12)
+// splits <= 0: vcx_gemm_wg_splits; loaders: the waves that stage the LDS ring (8, or 4 with waves 4-7
+// compute-only)
 bool gemm_wg_supported(int64_t M, int64_t N, int64_t K, int64_t splits) {
   return vcx_gemm_wg_supported((int)M, (int)N, (int)K, (int)(splits > 0 ? splits : vcx_gemm_wg_splits((int)M, (int)N, (int)K)));
 }
 
-void gemm_wg(at::Tensor a, at::Tensor b, at::Tensor out, bool accumulate, int64_t splits, int64_t pf) {
+void gemm_wg(at::Tensor a, at::Tensor b, at::Tensor out, bool accumulate, int64_t splits, int64_t loaders) {
   TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_wg: 2-D cuda tensors");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
               "gemm_wg: bf16 operands");
@@ -358,14 +336,14 @@ void gemm_wg(at::Tensor a, at::Tensor b, at::Tensor out, bool accumulate, int64_
   if (splits <= 0) splits = vcx_gemm_wg_splits((int)M, (int)N, (int)K);
   TORCH_CHECK(vcx_gemm_wg_supported((int)M, (int)N, (int)K, (int)splits),
               "gemm_wg: needs M % 256 == 0, N % 256 == 0, K % 64 == 0, K / 192 >= splits");
-  TORCH_CHECK(pf == 0 || pf == 4 || pf == 6 || pf == 8 || pf == 12, "gemm_wg: pf 0, 4, 6, 8 or 12");
+  TORCH_CHECK(loaders == 4 || loaders == 8, "gemm_wg: loaders 4 or 8");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_wg: 16-B aligned rows");
   TORCH_CHECK(a.stride(0) * K < (int64_t(1) << 40) && b.stride(0) * K < (int64_t(1) << 40), "gemm_wg: size");
   for (const at::Tensor* t : {&a, &b, &out})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_wg: 16-B aligned base pointers");
   at::Tensor ws = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
   vcx_gemm_wg(a.data_ptr(), b.data_ptr(), ws.data_ptr<float>(), out.data_ptr(), (int)M, (int)N, (int)K,
-              (int)a.stride(0), (int)b.stride(0), (int)splits, accumulate ? 1 : 0, (int)pf, cur_stream());
+              (int)a.stride(0), (int)b.stride(0), (int)splits, accumulate ? 1 : 0, (int)loaders, cur_stream());
 }
 
 at::Tensor transpose_bf16(at::Tensor src, c10::optional<at::Tensor> dst) {
@@ -835,9 +813,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0);
   m.def("gemm_wg_supported", &gemm_wg_supported, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits") = 0);
   m.def("gemm_wg", &gemm_wg, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("accumulate") = false,
-        py::arg("splits") = 0, py::arg("pf") = 8);
-  m.def("gemm_tn_supported", &gemm_tn_supported);
-  m.def("gemm_tn", &gemm_tn, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("splits"), py::arg("accumulate"));
+        py::arg("splits") = 0, py::arg("loaders") = 8);
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0);
   m.def("transpose_bf16", &transpose_bf16, py::arg("src"), py::arg("dst") = py::none());

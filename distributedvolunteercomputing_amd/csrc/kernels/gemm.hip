@@ -330,238 +330,6 @@ __global__ void __launch_bounds__(NT, 1)
   }
 }
 
-// ============================================================================ weight gradient
-//   Cpart[s][M, N] = sum over tokens k in split s of A[k, M]^T . B[k, N]   (fp32 partials)
-//
-// The weight gradient of a token-major linear layer, dW[out, in] = dY[tok, out]^T X[tok, in]:
-// both operands are TOKEN-major (the reduction index is their row index), so a K-slice of 32
-// tokens is 32 rows x 512 B of each operand, staged HBM -> LDS by LDS-DMA exactly like gemm_nt
-// (4-slot ring, counted vmcnt + raw barrier, 8 waves of 128 x 64), and the MFMA fragments
-// (8 consecutive tokens of one output row) are read TRANSPOSED out of the row-major LDS image by
-// ds_read_b64_tr_b16 (cdna guide T10): two 4-token reads per fragment.
-// LDS image: 512-B rows (one token), 16-B chunks XOR-swizzled by F(r) = 2 * (r & 3 | (r >> 3 & 1) << 2):
-// a half-wave's two transposed reads touch 8 rows (q = r & 3 and the group parity r >> 3 & 1)
-// x 2 chunks, which F spreads over all 16 bank slots (conflict-free). LDS-DMA writes lane-linearly,
-// so the swizzle is applied to the per-lane GLOBAL source address (guide rule 21).
-// Split-K over the token axis: the wgrad outputs hold only 9..36 tiles of 256 x 256, so the
-// grid is tiles x S (S ~ 256 / tiles: one round over the 256 CUs), each split writing an fp32
-// partial; splitk_sum_kernel adds the S partials into the bf16 gradient.
-// Reference analog: none (the reference trains nothing; SURVEY.md §2.9 north-star trainer).
-__device__ __forceinline__ int tn_swz(int r) { return ((r & 3) | (((r >> 3) & 1) << 2)) << 1; }
-
-__device__ __forceinline__ sx8 tr_frag(const char* p0, const char* p1) {
-  typedef short sx4 __attribute__((ext_vector_type(4)));
-#ifdef VCX_TN_DIAG_B128  // timing diagnostic only (WRONG numerics): plain row reads instead of transposed
-  return *(const sx8*)((uintptr_t)p0 & ~(uintptr_t)15);
-#endif
-  const sx4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sx4*)(p0));
-  const sx4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sx4*)(p1));
-  return sx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
-
-constexpr int TROW = 512;                // bytes per token row of a 256-wide operand slice
-constexpr int TSLOT_A = BKS * TROW;      // 16 KB
-
-// s_waitcnt vmcnt(N) lgkmcnt(0) for N up to 63 (vmcnt bits [3:0] and [15:14])
-template <int N>
-__device__ __forceinline__ void waitcnt_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt field");
-  __builtin_amdgcn_s_waitcnt(0x0070 | (N & 15) | ((N >> 4) << 14));
-}
-
-// PF = L2 prefetch distance in slices (0: none). With PF > 0 every step also issues ONE LDS-DMA
-// per lane for slice t + PF into a junk 8 KB LDS region: 512 lanes touch the 256 L2 lines of
-// that slice (each twice), so when its real DMA is issued PF - 4 steps later it hits L2. The
-// operands of a weight gradient stream from HBM / MALL (an XCD's tiles share only a few
-// panels), and the 4-slot ring alone keeps just 3 slices in flight.
-template <int PF>
-__global__ void __launch_bounds__(NT, 1)
-    gemm_tn_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, float* __restrict__ Cpart, int M, int N,
-                   int K, int lda, int ldb, int tilesN, int tiles, int splits) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
-
-  // ---- XCD-aware bijective order over (split, tile): consecutive logical ids share an XCD, and
-  // the tiles of one split (same token range) run side by side there, sharing its L2
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int split = wg / tiles, tile = wg - split * tiles;
-  const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN;
-  const int nb64 = K >> 6;
-  const int kb0 = (int)((int64_t)split * nb64 / splits), kb1 = (int)((int64_t)(split + 1) * nb64 / splits);
-  const int kbeg = kb0 * 64;
-  const int nk = (kb1 - kb0) * 2;  // slices of 32 tokens: even, >= 6 (host: K / 192 >= splits)
-
-  // ---- LDS-DMA staging: piece P (0..15) of an operand slice = token rows 2P, 2P + 1 (64 lanes x
-  // 16 B); wave w moves pieces w and w + 8 of A and of B. Lane l: row 2w + (l >> 5), physical
-  // chunk l & 31, which holds logical chunk (l & 31) ^ F(row) (F(row + 16) = F(row))
-  const int srow = 2 * wid + (lane >> 5);
-  const int schunk = (lane & 31) ^ tn_swz(srow);
-  const bf16* a_src = A + (int64_t)(kbeg + srow) * lda + m0 + schunk * 8;
-  const bf16* b_src = B + (int64_t)(kbeg + srow) * ldb + n0 + schunk * 8;
-  const int64_t a_step16 = (int64_t)16 * lda, b_step16 = (int64_t)16 * ldb;
-  const int64_t a_slice = (int64_t)BKS * lda, b_slice = (int64_t)BKS * ldb;
-  char* const lds_piece = smem + wid * 1024;
-
-  auto stage_piece = [&](int s, int p) {
-    char* slot = lds_piece + (s & 3) * SLOT_BYTES;
-    if (p == 0) glds16(a_src + s * a_slice, slot);
-    if (p == 1) glds16(a_src + s * a_slice + a_step16, slot + 8 * 1024);
-    if (p == 2) glds16(b_src + s * b_slice, slot + TSLOT_A);
-    if (p == 3) glds16(b_src + s * b_slice + b_step16, slot + TSLOT_A + 8 * 1024);
-  };
-  auto stage = [&](int s) {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) stage_piece(s, p);
-  };
-
-  // ---- transposed fragment reads: lane l (group g = l >> 4, e = l & 15, q = e >> 2, p = e & 3)
-  // supplies, for read h, the address of token row 8g + 4h + q, columns c0 + 4p .. c0 + 4p + 3 of
-  // the 16-column block; it receives column c0 + e of the 4 rows
-  const int g = lane >> 4, e = lane & 15, qq = e >> 2, pp = e & 3;
-  const int r0 = 8 * g + qq, r1 = r0 + 4;
-  const int f0 = tn_swz(r0), f1 = tn_swz(r1);
-  const int half8 = (pp & 1) * 8, hchunk = pp >> 1;
-  // byte offset of the 16-column block starting at logical column c (multiple of 16) for read h
-  auto toff = [&](int c, int rr, int ff) { return rr * TROW + ((((c >> 3) ^ ff) + hchunk) << 4) + half8; };
-
-  auto load_part = [&](Frags& f, int s, int part) {  // 0: x[0..3], 1: x[4..7], 2: w[0..3]
-    const char* so = smem + (s & 3) * SLOT_BYTES;
-    if (part < 2) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = wm * 128 + 16 * (4 * part + i);
-        f.x[4 * part + i] = tr_frag(so + toff(c, r0, f0), so + toff(c, r1, f1));
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = wn * 64 + 16 * j;
-        f.w[j] = tr_frag(so + TSLOT_A + toff(c, r0, f0), so + TSLOT_A + toff(c, r1, f1));
-      }
-    }
-  };
-  auto load = [&](Frags& f, int s) {
-#pragma unroll
-    for (int part = 0; part < 3; ++part) load_part(f, s, part);
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto mma = [&](const Frags& f, auto I0, auto I1) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = decltype(I0)::value; i < decltype(I1)::value; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[j], f.x[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  using I0c = std::integral_constant<int, 0>;
-  using I2c = std::integral_constant<int, 2>;
-  using I4c = std::integral_constant<int, 4>;
-  using I6c = std::integral_constant<int, 6>;
-  using I8c = std::integral_constant<int, 8>;
-
-  // L2 prefetch: lane l of wave w touches 16 B of line (w * 64 + l) & 255 of slice t: lines 0..127
-  // are A (32 rows x 4 lines of 128 B), 128..255 B; the DMA lands in the junk region
-  const int pl = (wid * 64 + lane) & 255;
-  const int prow = (pl & 127) >> 2, pseg = (pl & 3) * 64;
-  const bf16* pf_src = (pl < 128 ? A + (int64_t)(kbeg + prow) * lda + m0 : B + (int64_t)(kbeg + prow) * ldb + n0) + pseg;
-  const int64_t pf_slice = pl < 128 ? a_slice : b_slice;
-  char* const pf_lds = smem + LDS_BYTES + wid * 1024;
-  auto prefetch = [&](int t) {
-    const int tt = t < nk ? t : nk - 1;  // always one op per step (uniform vmcnt accounting)
-    glds16(pf_src + tt * pf_slice, pf_lds);
-  };
-  constexpr int OPS = 4 + (PF > 0 ? 1 : 0);  // vm ops per staging step
-
-  // the gemm_nt pipeline (prefetch distance 4 into the LDS ring, counted vmcnt, raw barrier): step
-  // t issues [the L2 prefetch of slice t + PF and] slice t + 4 into the slot of slice t, then waits
-  // for slice t + 1 with the ops of the two steps after its issue still in flight
-  stage(0);
-  stage(1);
-  stage(2);
-  stage(3);
-  if constexpr (PF > 0) {
-#pragma unroll
-    for (int t = 4; t < PF; ++t) prefetch(t);
-  }
-  waitcnt_vm<12 + (PF > 4 ? PF - 4 : 0)>();
-  barrier();
-  Frags f0r, f1r;
-  load(f0r, 0);
-
-  auto step = [&](int s, Frags& fc, Frags& fn, auto STAGE, auto LOAD, auto PEND) {
-    constexpr bool st = decltype(STAGE)::value, ld = decltype(LOAD)::value;
-    waitcnt_vm<decltype(PEND)::value>();  // vm ops allowed in flight
-    barrier();
-    if constexpr (st && PF > 0) prefetch(s + PF);
-    if constexpr (st) stage_piece(s + 4, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(fc, I0c{}, I2c{});
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (ld) load_part(fn, s + 1, 0);
-    if constexpr (st) stage_piece(s + 4, 1);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(fc, I2c{}, I4c{});
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (ld) load_part(fn, s + 1, 1);
-    if constexpr (st) stage_piece(s + 4, 2);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(fc, I4c{}, I6c{});
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (ld) load_part(fn, s + 1, 2);
-    if constexpr (st) stage_piece(s + 4, 3);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(fc, I6c{}, I8c{});
-  };
-  using T = std::true_type;
-  using F = std::false_type;
-  using PS = std::integral_constant<int, 2 * OPS>;  // steady state: two staging steps after slice t + 1
-  using PT1 = std::integral_constant<int, OPS>;
-  using P0 = std::integral_constant<int, 0>;
-  int s = 0;
-  for (; s + 5 < nk; s += 2) {
-    step(s, f0r, f1r, T{}, T{}, PS{});
-    step(s + 1, f1r, f0r, T{}, T{}, PS{});
-  }
-  step(s, f0r, f1r, F{}, T{}, PS{});
-  step(s + 1, f1r, f0r, F{}, T{}, PT1{});
-  step(s + 2, f0r, f1r, F{}, T{}, P0{});
-  mma(f1r, I0c{}, I8c{});
-  if constexpr (PF > 0) waitcnt_vm<0>();  // no prefetch DMA may still target LDS at exit
-
-  // ---- fp32 partial: acc[i][j] = C[m][n .. n + 3], m = row block i + (lane & 15), n = column block j
-  const int mrow = m0 + wm * 128 + (lane & 15);
-  const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
-  float* cp = Cpart + (int64_t)split * M * N;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) *(f32x4*)(cp + (int64_t)(mrow + 16 * i) * N + ncol + 16 * j) = acc[i][j];
-}
-
-// out[i] (bf16) = (accumulate ? out[i] : 0) + sum_s part[s][i], 4 elements per thread
-__global__ void __launch_bounds__(256) splitk_sum_kernel(const float* __restrict__ part, bf16* __restrict__ out,
-                                                         int64_t n, int splits, int accumulate) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= n) return;
-  f32x4 a = *(const f32x4*)(part + i);
-  for (int s = 1; s < splits; ++s) a += *(const f32x4*)(part + (int64_t)s * n + i);
-  bf16x4 o = *(bf16x4*)(out + i);
-  bf16x4 r;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) r[t] = (bf16)((accumulate ? (float)o[t] : 0.f) + a[t]);
-  *(bf16x4*)(out + i) = r;
-}
-
 // dst[r][c] = src[c][r] for a [R, Cc] bf16 matrix (weights: W -> W^T for the input-gradient GEMM)
 __global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
                                                              int R, int Cc) {
@@ -649,35 +417,6 @@ void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bi
     case EPI_BIAS_RELU: args(gemm_nt_kernel<EPI_BIAS_RELU>); break;
     default: args(gemm_nt_kernel<EPI_DGELU>); break;
   }
-}
-
-bool vcx_gemm_tn_supported(int M, int N, int K, int splits) {
-  return M > 0 && N > 0 && M % gemm::BM == 0 && N % gemm::BN == 0 && K % 64 == 0 && splits >= 1 &&
-         K / 192 >= splits;  // >= 3 blocks of 64 tokens per split (ring depth 5: nk >= 8 after rounding)
-}
-
-// Cpart[splits, M, N] (fp32 workspace) = per-split A[K, M]^T . B[K, N]; then out (bf16 [M, N],
-// row stride N) = (accumulate ? out : 0) + sum of the partials
-void vcx_gemm_tn(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
-                 int splits, int accumulate, hipStream_t s) {
-  using namespace gemm;
-  const int tilesN = N / BN, tiles = (M / BM) * tilesN;
-  static const int pf = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_BYTES + 8 * 1024);
-    const char* e = getenv("VCX_TN_PREFETCH");
-    return e && atoi(e) == 0 ? 0 : 8;
-  }();
-  if (pf)
-    hipLaunchKernelGGL(gemm_tn_kernel<8>, dim3(tiles * splits), dim3(NT), LDS_BYTES + 8 * 1024, s, (const bf16*)A,
-                       (const bf16*)B, Cpart, M, N, K, lda, ldb, tilesN, tiles, splits);
-  else
-    hipLaunchKernelGGL(gemm_tn_kernel<0>, dim3(tiles * splits), dim3(NT), LDS_BYTES, s, (const bf16*)A,
-                       (const bf16*)B, Cpart, M, N, K, lda, ldb, tilesN, tiles, splits);
-  const int64_t n = (int64_t)M * N;
-  hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, s, Cpart, (bf16*)out, n,
-                     splits, accumulate);
 }
 
 void vcx_transpose_bf16(const void* src, void* dst, int R, int Cc, hipStream_t s) {

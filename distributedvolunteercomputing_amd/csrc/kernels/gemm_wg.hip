@@ -1,4 +1,4 @@
-// Weight-gradient GEMM for gfx950 with wave-specialised operand loads and an XCD-shared L2 prefetch:
+// Weight-gradient GEMM for gfx950 (the default weight gradient of ops/linear.py):
 //
 //   Cpart[s][M, N] = sum over tokens k of split s of A[k, M]^T . B[k, N]      (fp32 partials)
 //   out (bf16 [M, N]) (+)= sum_s Cpart[s]                                    (splitk_sum_kernel)
@@ -6,25 +6,24 @@
 // The weight gradient of a token-major linear layer, dW[out, in] = dY[tok, out]^T X[tok, in]: both
 // operands are TOKEN-major (the reduction runs over their row index), the output is small (9..36 tiles
 // of 256 x 256 at GPT-2-small), so the token axis is split over the CUs and every split streams its
-// token range of both operands once. Structure, and why:
-//   * main loop of gemm_nt / gemm_tn: 256 x 256 tile per 512-thread workgroup (8 waves as 2 (M) x 4 (N),
-//     128 x 64 each, v_mfma_f32_16x16x32_bf16), 4-slot LDS ring of 32-token slices, counted vmcnt + raw
-//     s_barrier, fragments read TRANSPOSED out of the token-row LDS image by ds_read_b64_tr_b16
-//     (cdna guide T10) and double-buffered in registers.
-//   * the problem of the token-major wgrad (profiles/r2_gemm_tn.txt: waves parked on vmcnt 73 % of the
-//     time): every slice is a fresh HBM/MALL miss, and a wave's vmcnt retires in issue order, so
-//     neither a deeper ring (LDS is full) nor a prefetch issued by the waiting waves (gemm_tn's PF:
-//     the prefetch is older than the DMA the next wait covers) extends the latency a slice may take.
-//   * here the loads are split by WAVE ROLE. Waves 0-3 issue all 32 LDS-DMA pieces of a slice (8
-//     each) and do the counted waits. Waves 4-7 issue NO operand DMA: they touch the lines of slice
-//     t + PF (global_load_dword into a sink register, two per 128-B line) and never wait for them,
-//     so their own in-order vmcnt queue never blocks a barrier. By the time waves 0-3 stage slice
-//     t + PF, it is an L2 hit. All 8 waves run the same MFMAs.
-//   * the prefetch is SHARED across the tiles of a split: a split's tiles run side by side on one XCD
-//     (the XCD-aware order below) and read the same token rows, so tile (tm, tn) touches only its
-//     1/tilesN share of its A panel's slice lines and 1/tilesM of its B panel's: each line once per
-//     XCD, instead of every CU re-requesting its whole 32 KB slice (which would double the L2 request
-//     rate that the DMA itself already runs at about half of).
+// token range of both operands once. Structure:
+//   * 256 x 256 tile per 512-thread workgroup (8 waves as 2 (M) x 4 (N), 128 x 64 each,
+//     v_mfma_f32_16x16x32_bf16), 4-slot LDS ring of 32-token slices staged by LDS-DMA, counted vmcnt +
+//     raw s_barrier (two slices in flight across every barrier), fragments read TRANSPOSED out of the
+//     token-row LDS image by ds_read_b64_tr_b16 (cdna guide T10); A rows 0..5 single-buffered, rows 6, 7
+//     and the B fragments double-buffered in registers.
+//   * the LDS-DMA is issued by inline asm (dma16), not by the buffer/global_load_lds builtins. With the
+//     builtins, hipcc (ROCm 7.2) cannot tell a pending LDS-DMA from the slot a later
+//     ds_read_b64_tr_b16 reads and drains vmcnt(0) in front of the transposed fragment reads -- 8 full
+//     drains per step in the earlier gemm_tn, whose "waves parked on vmcnt 73 % of the time"
+//     (profiles/r2_gemm_tn.txt) were those drains, not memory latency. Invisible to that pass, the
+//     DMA is ordered only by this kernel's own counted waits: 1165-1229 TF/s at the GPT-2 shapes
+//     against the library's 808-978 (profiles/r5_gemm_wg.txt).
+//   * measured and dropped (profiles/r5_gemm_wg.txt): wave-role loads (waves 0-3 staging, 4-7 touching
+//     slice t + PF into L2 without ever waiting, the tiles of a split sharing the touches) -- once the
+//     drains were gone the prefetch only cost (pf 4..12: 0-7 % slower than none).
+//   * XCD-aware order over (split, tile): the tiles of one split (same token rows) run side by side
+//     on one XCD and share its L2.
 // Reference analog: none (the reference trains nothing; SURVEY.md §2.9 north-star trainer).
 #include <type_traits>
 
@@ -42,7 +41,6 @@ constexpr int TROW = 512;                      // bytes per token row of a 256-w
 constexpr int TSLOT_A = BKS * TROW;            // 16 KB
 constexpr int SLOT_BYTES = 2 * TSLOT_A;        // 32 KB: A and B slices
 constexpr int LDS_BYTES = 4 * SLOT_BYTES;      // 128 KB ring
-constexpr int OPS = 8;                         // LDS-DMA ops per slice per loader wave
 
 // 16-B chunk swizzle of a token row: F(r) = 2 (r & 3 | (r >> 3 & 1) << 2); a half-wave's two transposed
 // reads touch 8 rows (q = r & 3 and the group parity r >> 3 & 1) x 2 chunks, spread over all 16 bank
@@ -83,33 +81,25 @@ __device__ __forceinline__ void wait_vm() {
 __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }  // vmcnt 63: no VM wait
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-// L2 touch of one 128-B line (both 64-B halves): the loaded dwords land in `sink`, a register nothing
-// reads (kept allocated by the "+v" constraint of every touch); the prefetch waves drain their queue
-// once, after the main loop
-__device__ __forceinline__ void touch(u32x4 d, int voff, int soff, int& sink) {
-  asm volatile("buffer_load_dword %0, %1, %2, %3 offen\n\tbuffer_load_dword %0, %1, %2, %3 offen offset:64"
-               : "+v"(sink)
-               : "v"(voff), "s"(d), "s"(soff)
-               : "memory");
-}
-
-// A fragments of the wave's row blocks 0..5 are single-buffered (refilled right behind the MFMA group
-// that used them); rows 6, 7 and the B fragments alternate between two named sets, so every read of the
-// next slice is issued before the step's last MFMA group (96 -> 72 fragment VGPRs)
 struct Frags {
   sx8 y[2];  // A fragments of row blocks 6, 7
   sx8 w[4];  // B fragments: the wave's 4 column blocks of 16 (output columns)
 };
 
-template <int PF>
+// NLW = the waves that stage the ring: 8 (every wave moves 4 of a slice's 32 pieces; the default) or 4
+// (waves 0-3 move 8 each, waves 4-7 only compute: 1-3 % slower, profiles/r5_gemm_wg.txt; kept as the
+// tested alternative geometry)
+template <int NLW>
 __global__ void __launch_bounds__(NT, 1)
     gemm_wg_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, float* __restrict__ Cpart, int M, int N,
                    int K, int lda, int ldb, int tilesN, int tiles, int splits) {
+  static_assert(NLW == 4 || NLW == 8, "loader waves");
+  constexpr int PPO = 16 / NLW;   // pieces of one operand per loader wave
+  constexpr int OPS = 2 * PPO;    // LDS-DMA ops per slice per loader wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 2, wn = wid & 3;
-  const bool loader = wid < 4;
 
   // ---- XCD-aware bijective order over (split, tile): consecutive logical ids share an XCD, so the
   // tiles of one split (same token range) run side by side there and share its L2
@@ -118,21 +108,20 @@ __global__ void __launch_bounds__(NT, 1)
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int split = wg / tiles, tile = wg - split * tiles;
   const int tm = tile / tilesN, tn = tile - tm * tilesN;
-  const int tilesM = tiles / tilesN;
   const int m0 = tm * BM, n0 = tn * BN;
   const int nb64 = K >> 6;
   const int kb0 = (int)((int64_t)split * nb64 / splits), kb1 = (int)((int64_t)(split + 1) * nb64 / splits);
   const int kbeg = kb0 * 64;
   const int nk = (kb1 - kb0) * 2;  // slices of 32 tokens: even, >= 6 (host: K / 192 >= splits)
-  const int64_t a_slice = (int64_t)BKS * lda, b_slice = (int64_t)BKS * ldb;
 
-  // ---- loader waves (0-3): piece P (0..15) of an operand slice = token rows 2P, 2P + 1 (64 lanes x 16 B);
-  // wave w moves pieces w + 4i (i = 0..3) of A and of B. Lane l: row 2P + (l >> 5), physical chunk l & 31,
-  // holding logical chunk (l & 31) ^ F(row); F depends on the row's bit 3 = i & 1, so even and odd i
-  // have their own per-lane source offsets. Buffer resources over this split's token rows of the tile's
-  // panels (host check: they fit 31 bits); the slice and the 16-row step of i >> 1 go into soffset.
+  // ---- staging: piece P (0..15) of an operand slice = token rows 2P, 2P + 1 (64 lanes x 16 B); loader
+  // wave w moves pieces w + NLW i (i < PPO) of A and of B. Lane l: row 2P + (l >> 5), physical chunk
+  // l & 31, holding logical chunk (l & 31) ^ F(row). F depends on the row's bit 3: for NLW = 8 the rows
+  // of a wave's pieces are 16 apart (one F), for NLW = 4 8 apart (F alternates with i & 1). Buffer
+  // resources over this split's token rows of the tile's panels (host check: they fit 31 bits); the
+  // slice and the 16-row steps go into soffset.
   const int ntok = (kb1 - kb0) * 64;
-  const int lw = wid & 3;
+  const int lw = wid & (NLW - 1);
   const int row_e = 2 * lw + (lane >> 5), row_o = row_e + 8;
   const int ch_e = ((lane & 31) ^ swz(row_e)) * 8, ch_o = ((lane & 31) ^ swz(row_o)) * 8;
   const bf16* a_base = A + (int64_t)kbeg * lda + m0;
@@ -140,48 +129,35 @@ __global__ void __launch_bounds__(NT, 1)
   const u32x4 ra = desc(a_base, ntok * lda * 2), rb = desc(b_base, ntok * ldb * 2);
   const int va_e = (row_e * lda + ch_e) * 2, va_o = (row_o * lda + ch_o) * 2;
   const int vb_e = (row_e * ldb + ch_e) * 2, vb_o = (row_o * ldb + ch_o) * 2;
-  const int a_sl = BKS * lda * 2, b_sl = BKS * ldb * 2;  // bytes per slice
+  const int a_sl = BKS * lda * 2, b_sl = BKS * ldb * 2;  // bytes per slice (32 rows)
   char* const lds_w = smem + lw * 1024;
 
-  // op o (0..7) of slice s: A pieces for o < 4 (i = o), B pieces for o >= 4 (i = o - 4)
+  // op o (0..OPS-1) of slice s: A pieces for o < PPO (i = o), B pieces after (i = o - PPO)
   auto stage_op = [&](int s, int o) {
     char* slot = lds_w + (s & 3) * SLOT_BYTES;
-    const int i = o & 3;
-    if (o < 4)
-      dma16(ra, (i & 1) ? va_o : va_e, s * a_sl + (i >> 1) * (a_sl >> 1), slot + i * 4096);
+    const int i = o % PPO;
+    const bool odd = NLW == 4 && (i & 1);
+    const int r16 = NLW == 4 ? (i >> 1) : i;  // 16-row steps
+    if (o < PPO)
+      dma16(ra, odd ? va_o : va_e, s * a_sl + r16 * (a_sl >> 1), slot + i * NLW * 1024);
     else
-      dma16(rb, (i & 1) ? vb_o : vb_e, s * b_sl + (i >> 1) * (b_sl >> 1), slot + TSLOT_A + i * 4096);
+      dma16(rb, odd ? vb_o : vb_e, s * b_sl + r16 * (b_sl >> 1), slot + TSLOT_A + i * NLW * 1024);
   };
   auto stage = [&](int s) {
 #pragma unroll
     for (int o = 0; o < OPS; ++o) stage_op(s, o);
   };
-
-  // ---- prefetch waves (4-7): waves 4, 5 touch this tile's share of its A panel's 128 slice lines (32
-  // rows x 4 lines of 128 B), waves 6, 7 its share of its B panel's; lanes past the share repeat its
-  // first line
-  const bool pfa = (wid & 2) == 0;
-  const int pl = (wid & 1) * 64 + lane;
-  int pf_voff;
-  {
-    const int lo = pfa ? tn * 128 / tilesN : tm * 128 / tilesM;
-    const int hi = pfa ? (tn + 1) * 128 / tilesN : (tm + 1) * 128 / tilesM;
-    const int j = lo + (pl < hi - lo ? pl : 0);
-    pf_voff = ((j >> 2) * (pfa ? lda : ldb) + (j & 3) * 64) * 2;
-  }
-  const u32x4 pf_desc = pfa ? desc(a_base, ntok * lda * 2) : desc(b_base, ntok * ldb * 2);
-  const int pf_sl = pfa ? a_sl : b_sl;
-  int sink = 0;
-  auto prefetch = [&](int t) {
-    if (t < nk) touch(pf_desc, pf_voff, t * pf_sl, sink);
+  // the ops of one slice spread over the step's 4 MFMA groups
+  auto stage_group = [&](int s, int grp) {
+#pragma unroll
+    for (int o = grp * OPS / 4; o < (grp + 1) * OPS / 4; ++o) stage_op(s, o);
   };
 
   // ---- transposed fragment reads: lane l (group g = l >> 4, e = l & 15, q = e >> 2, p = e & 3)
   // supplies, for read h, the address of token row 8g + 4h + q, columns c0 + 4p .. c0 + 4p + 3 of the
-  // 16-column block; it receives column c0 + e of the 4 rows
+  // 16-column block; it receives column c0 + e of the 4 rows. Rows r0 and r0 + 4 have the same F (F
+  // ignores row bit 2), so the read of row r0 + 4 is the read of row r0 plus the immediate 4 * TROW.
   const int g = lane >> 4, e = lane & 15, qq = e >> 2, pp = e & 3;
-  // rows r0 and r0 + 4 have the same F (F ignores row bit 2), so the read of row r0 + 4 is the read of
-  // row r0 plus the immediate 4 * TROW: one address register per 16-column block, not two
   const int r0 = 8 * g + qq;
   const int f0 = swz(r0);
   const int half8 = (pp & 1) * 8, hchunk = pp >> 1;
@@ -238,34 +214,32 @@ __global__ void __launch_bounds__(NT, 1)
   using I6c = std::integral_constant<int, 6>;
   using I8c = std::integral_constant<int, 8>;
 
-  // one step of either role: slice s in registers (fc); make slice s + 1 visible, issue [loader: slice
-  // s + 4 into the slot of slice s | prefetch: touch slice s + PF], read slice s + 1 into fn, MFMAs of
-  // slice s. LDS-DMA ops / touches and ds_reads interleave with the 4 MFMA groups.
-  auto step = [&](int s, Frags& fc, Frags& fn, auto ROLE, auto STAGE, auto LOAD, auto PEND) {
-    constexpr bool ld_role = decltype(ROLE)::value;
-    constexpr bool st = decltype(STAGE)::value, ld = decltype(LOAD)::value;
-    if constexpr (ld_role)
+  // one step: slice s in registers; make slice s + 1 visible (a loader's counted vmcnt leaves the two
+  // slices behind it in flight), issue slice s + 4 into the slot of slice s, read slice s + 1 into fn,
+  // MFMAs of slice s; the DMA ops and ds_reads interleave with the 4 MFMA groups
+  auto step = [&](int s, Frags& fc, Frags& fn, auto ROLE, auto STAGE, auto PEND) {
+    constexpr bool loader = decltype(ROLE)::value, st = decltype(STAGE)::value && loader;
+    if constexpr (loader)
       wait_vm<decltype(PEND)::value>();  // own DMA of slice s + 1 retired; own ds_reads too
     else
-      wait_lgkm0();  // the prefetch waves wait only for their ds_reads: their touches never block
+      wait_lgkm0();  // compute-only waves: their ds_reads
     barrier();
-    if constexpr (!ld_role && PF > 0) prefetch(s + PF);
-    if constexpr (ld_role && st) stage_op(s + 4, 0), stage_op(s + 4, 4);
+    if constexpr (st) stage_group(s + 4, 0);
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I0c{}, I2c{});
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (ld) load_part(fn, s + 1, 0);
-    if constexpr (ld_role && st) stage_op(s + 4, 1), stage_op(s + 4, 5);
+    load_part(fn, s + 1, 0);
+    if constexpr (st) stage_group(s + 4, 1);
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I2c{}, I4c{});
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (ld) load_part(fn, s + 1, 1);
-    if constexpr (ld_role && st) stage_op(s + 4, 2), stage_op(s + 4, 6);
+    load_part(fn, s + 1, 1);
+    if constexpr (st) stage_group(s + 4, 2);
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I4c{}, I6c{});
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (ld) load_part(fn, s + 1, 2);
-    if constexpr (ld_role && st) stage_op(s + 4, 3), stage_op(s + 4, 7);
+    load_part(fn, s + 1, 2);
+    if constexpr (st) stage_group(s + 4, 3);
     __builtin_amdgcn_sched_barrier(0);
     mma(fc, I6c{}, I8c{});
   };
@@ -276,39 +250,31 @@ __global__ void __launch_bounds__(NT, 1)
   using PT1 = std::integral_constant<int, OPS>;
   using P0 = std::integral_constant<int, 0>;
   Frags f0r, f1r;
-  // the two roles run the same barrier sequence from two copies of the loop (wave-uniform branch)
   auto run = [&](auto ROLE) {
-    constexpr bool ld_role = decltype(ROLE)::value;
-    if constexpr (ld_role) {
+    if constexpr (decltype(ROLE)::value) {
       stage(0);
       stage(1);
       stage(2);
       stage(3);
       wait_vm<3 * OPS>();  // slice 0 landed
-    } else {
-      if constexpr (PF > 4) {
-#pragma unroll 1
-        for (int t = 4; t < PF; ++t) prefetch(t);
-      }
     }
     barrier();
     load(f0r, 0);
     int s = 0;
 #pragma unroll 1
     for (; s + 5 < nk; s += 2) {
-      step(s, f0r, f1r, ROLE, T{}, T{}, PS{});
-      step(s + 1, f1r, f0r, ROLE, T{}, T{}, PS{});
+      step(s, f0r, f1r, ROLE, T{}, PS{});
+      step(s + 1, f1r, f0r, ROLE, T{}, PS{});
     }
-    step(s, f0r, f1r, ROLE, F{}, T{}, PS{});
-    step(s + 1, f1r, f0r, ROLE, F{}, T{}, PT1{});
-    step(s + 2, f0r, f1r, ROLE, F{}, T{}, P0{});
+    step(s, f0r, f1r, ROLE, F{}, PS{});
+    step(s + 1, f1r, f0r, ROLE, F{}, PT1{});
+    step(s + 2, f0r, f1r, ROLE, F{}, P0{});
     mma(f1r, I0c{}, I8c{});
   };
-  if (loader)
+  if (NLW == 8 || wid < NLW)
     run(T{});
   else
     run(F{});
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(sink)::"memory");  // no touch may land in a reused register
 
   // ---- fp32 partial: acc[i][j] = C[m][n .. n + 3], m = row block i + (lane & 15), n = column block j
   const int mrow = m0 + wm * 128 + (lane & 15);
@@ -354,16 +320,13 @@ int vcx_gemm_wg_splits(int M, int N, int K) {
 }
 
 // Cpart[splits, M, N] (fp32 workspace) = per-split A[K, M]^T . B[K, N]; then out (bf16 [M, N], row
-// stride N) = (accumulate ? out : 0) + the sum of the partials. pf: L2 prefetch distance in slices
-// (0, 4, 6, 8 or 12)
+// stride N) = (accumulate ? out : 0) + the sum of the partials. loaders: 8 (default) or 4 waves stage.
 void vcx_gemm_wg(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
-                 int splits, int accumulate, int pf, hipStream_t s) {
+                 int splits, int accumulate, int loaders, hipStream_t s) {
   using namespace gemm_wg;
   const int tilesN = N / BN, tiles = (M / BM) * tilesN;
   static const bool attrs = [] {
-    for (const void* k : {(const void*)gemm_wg_kernel<0>, (const void*)gemm_wg_kernel<4>,
-                          (const void*)gemm_wg_kernel<6>, (const void*)gemm_wg_kernel<8>,
-                          (const void*)gemm_wg_kernel<12>})
+    for (const void* k : {(const void*)gemm_wg_kernel<4>, (const void*)gemm_wg_kernel<8>})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     return true;
   }();
@@ -372,13 +335,10 @@ void vcx_gemm_wg(const void* A, const void* B, float* Cpart, void* out, int M, i
     hipLaunchKernelGGL(kern, dim3(tiles * splits), dim3(NT), LDS_BYTES, s, (const bf16*)A, (const bf16*)B, Cpart, M,
                        N, K, lda, ldb, tilesN, tiles, splits);
   };
-  switch (pf) {
-    case 0: go(gemm_wg_kernel<0>); break;
-    case 4: go(gemm_wg_kernel<4>); break;
-    case 6: go(gemm_wg_kernel<6>); break;
-    case 12: go(gemm_wg_kernel<12>); break;
-    default: go(gemm_wg_kernel<8>); break;
-  }
+  if (loaders == 4)
+    go(gemm_wg_kernel<4>);
+  else
+    go(gemm_wg_kernel<8>);
   const int64_t n = (int64_t)M * N;
   hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, s, Cpart, (bf16*)out, n,
                      splits, accumulate);

@@ -14,14 +14,11 @@ void vcx_lsgd_apply(const void* avg, float* anchor, float* master, void* param, 
                     float outer_lr, float mu, int nesterov, float avg_scale, hipStream_t s);
 void vcx_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s);
 void vcx_axpy_bf16(const void* src, void* acc, int64_t n, float scale, hipStream_t s);
-// gemm_wg.hip: weight gradient out (+)= A[K, M]^T B[K, N], wave-specialised loads + shared L2 prefetch
+// gemm_wg.hip: weight gradient out (+)= A[K, M]^T B[K, N] (token-major operands), split-K fp32 partials
 bool vcx_gemm_wg_supported(int M, int N, int K, int splits);
 int vcx_gemm_wg_splits(int M, int N, int K);
 void vcx_gemm_wg(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
-                 int splits, int accumulate, int pf, hipStream_t s);
-bool vcx_gemm_tn_supported(int M, int N, int K, int splits);
-void vcx_gemm_tn(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
-                 int splits, int accumulate, hipStream_t s);
+                 int splits, int accumulate, int loaders, hipStream_t s);
 bool vcx_gemm_nt_supported(int M, int N, int K);
 bool vcx_gemm_nt_supported_epi(int M, int N, int K, int epi);
 void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,

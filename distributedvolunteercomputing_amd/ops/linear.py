@@ -1,14 +1,14 @@
-"""Linear layer whose backward computes the weight gradient as a split-M batched GEMM.
+"""Linear layer whose backward computes the weight gradient on a hand-written token-split GEMM.
 
 The weight gradient of a token-major linear layer, dW[N, K] = dY[M, N]^T X[M, K], reduces over
 all M = B*T tokens (65536 at the GPT-2 bench shape) into a small output: a single library GEMM
 has only (N/256)*(K/256) output tiles (9..36 at GPT-2-small sizes) for 256 CUs and runs at
-0.33-0.77 PF/s. Splitting the token axis into S chunks and issuing ONE batched GEMM
-(S x more tiles in flight) measured 1.3-2.3x faster on MI355X (scripts/gemm_probe.py,
-PROBE_SPLITS: qkv 399 -> 243 us, proj 234 -> 100 us, fc 401 -> 301 us, fc2 413 -> 309 us).
-The S partial products are summed in fp32 by a HIP kernel directly INTO the flat gradient
-buffer (``p.grad`` is a view of it, see parallel/flat_params.py), so no separate autograd
-accumulation pass runs either.
+0.33-0.77 PF/s. The default is the hand-written ``gemm_wg`` (csrc/kernels/gemm_wg.hip: the token
+axis split over the CUs, operands read transposed out of LDS, fp32 partials summed by a HIP kernel
+directly INTO the flat gradient buffer -- ``p.grad`` is a view of it, see parallel/flat_params.py):
+1.17-1.23 PF/s at the GPT-2 shapes (profiles/r5_gemm_wg.txt). The library fallback (other shapes,
+``VCX_GEMM_WGRAD=lib``) splits the token axis into S chunks of ONE batched GEMM (S x more tiles in
+flight; 1.3-2.3x a single GEMM, scripts/gemm_probe.py) and sums the partials the same way.
 
 Hand-written GEMMs on the default path (round 4, profiles/r4_gemm_ps_bench.txt): the persistent
 ``gemm_ps`` (csrc/kernels/gemm_ps.hip, nt output stores) runs the GPT-2 MLP's fc + bias + GELU and
@@ -133,28 +133,26 @@ def _splits(M: int, N: int, K: int) -> int:
     return s
 
 
-def tn_splits(M: int, N: int, K: int) -> int:
-    """Token-axis splits of the hand-written weight-gradient GEMM: about one round of
-    workgroups over the 256 CUs ((N/256)(K/256) output tiles x S), at least 192 tokens each."""
-    tiles = (N // 256) * (K // 256)
-    return max(1, min(256 // max(tiles, 1), M // 192))
-
-
-def gemm_tn_ok(M: int, N: int, K: int, t) -> bool:
+def gemm_wg_ok(M: int, N: int, K: int, t) -> bool:
+    """The hand-written weight-gradient GEMM (csrc/kernels/gemm_wg.hip) takes dW[N, K] from M tokens: the
+    default (config.gemm_wgrad == "vcx") wherever the output is a few dozen 256 x 256 tiles that need the
+    token split -- 1.17-1.23 PF/s at the GPT-2 shapes against the library's 0.81-0.98
+    (profiles/r5_gemm_wg.txt). Outputs of more than 128 tiles (Llama-3-8B's projections) fill the GPU
+    without a split and stay on the library."""
     return (config.get().gemm_wgrad == "vcx" and use_native(t) and t.dtype == torch.bfloat16
-            and bool(native().gemm_tn_supported(N, K, M, tn_splits(M, N, K))))
+            and (N // 256) * (K // 256) <= 128 and bool(native().gemm_wg_supported(N, K, M)))
 
 
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False):
     """dW = dy2^T @ x2 ([M, N], [M, K] -> [N, K]); written into / added onto `out` if given."""
     M, N = dy2.shape
     K = x2.shape[1]
-    if gemm_tn_ok(M, N, K, dy2) and dy2.stride(1) == 1 and x2.stride(1) == 1:
-        # hand-written transposed-read MFMA GEMM (csrc/kernels/gemm.hip gemm_tn), fp32 split partials
+    if gemm_wg_ok(M, N, K, dy2) and dy2.stride(1) == 1 and x2.stride(1) == 1 and (out is None or out.is_contiguous()):
+        # hand-written transposed-read MFMA GEMM, token-split fp32 partials summed into `out`
         if out is None:
             out = torch.empty(N, K, device=dy2.device, dtype=dy2.dtype)
             accumulate = False
-        native().gemm_tn(dy2, x2, out, tn_splits(M, N, K), accumulate)
+        native().gemm_wg(dy2, x2, out, accumulate)
         return out
     S = _splits(M, N, K)
     if S == 1 or not use_native(dy2) or (N * K) % 8:

@@ -36,8 +36,12 @@ for name, (N, K) in shapes.items():
         wt = L.transpose_weight(w)
         dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
         cases.append((f"dgrad {name} gemm_ps", fl, lambda dy=dy, wt=wt, dx=dx: C.gemm_ps(dy, wt, dx)))
-    cases.append((f"wgrad {name} default(S={L._splits(M, N, K)})", fl,
-                  lambda dy=dy, x=x, gw=gw: L.wgrad(dy, x, out=gw, accumulate=True)))
+    cases.append((f"wgrad {name} default", fl, lambda dy=dy, x=x, gw=gw: L.wgrad(dy, x, out=gw, accumulate=True)))
+
+    def libw(dy=dy, x=x, gw=gw):
+        with config.override(gemm_wgrad="lib"):
+            L.wgrad(dy, x, out=gw, accumulate=True)
+    cases.append((f"wgrad {name} library(S={L._splits(M, N, K)})", fl, libw))
     cases.append((f"wgrad {name} one GEMM", fl, lambda dy=dy, x=x, gw=gw: gw.addmm_(dy.t(), x)))
     for S in (4, 8, 32):
         if M % S == 0:
@@ -45,9 +49,8 @@ for name, (N, K) in shapes.items():
                 part = torch.bmm(dy.view(S, M // S, N).transpose(1, 2), x.view(S, M // S, K))
                 C.splitk_reduce(part, gw, True)
             cases.append((f"wgrad {name} bmm S={S}", fl, f))
-    if C.gemm_tn_supported(N, K, M, L.tn_splits(M, N, K)):
-        cases.append((f"wgrad {name} gemm_tn", fl,
-                      lambda dy=dy, x=x, gw=gw, N=N, K=K: C.gemm_tn(dy, x, gw, L.tn_splits(M, N, K), True)))
+    if C.gemm_wg_supported(N, K, M):
+        cases.append((f"wgrad {name} gemm_wg", fl, lambda dy=dy, x=x, gw=gw: C.gemm_wg(dy, x, gw, True)))
 
 ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
 for _, _, fn in cases:

@@ -1,7 +1,7 @@
 """Weight-gradient GEMMs at the GPT-2-small bench shapes (65536 tokens), accumulating into a bf16
 gradient as the step does: the library path (split-M batched GEMM + fp32 split reduction, the default
-of ops/linear.py until gemm_wg) against gemm_wg at every L2 prefetch distance (0 = no prefetch: the
-wave-split loads alone). Correctness vs fp32 first, then medians of interleaved rounds."""
+of ops/linear.py until round 5) against gemm_wg with 8 and with 4 loader waves. Correctness vs fp32
+first, then medians of interleaved rounds."""
 import os
 import sys
 
@@ -22,7 +22,7 @@ C = native()
 dev = torch.device("cuda", 0)
 M = int(os.environ.get("TOKENS", "65536"))
 SHAPES = [("qkv", 2304, 768), ("proj", 768, 768), ("fc", 3072, 768), ("fc2", 768, 3072)]
-PFS = [int(p) for p in os.environ.get("PFS", "0,4,6,8,12").split(",")]
+LOADERS = [8, 4]
 ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
 
 cases = []
@@ -32,7 +32,7 @@ for name, N, K in SHAPES:
     x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
     gw = torch.zeros(N, K, device=dev, dtype=torch.bfloat16)
     ref = dy.float().t() @ x.float()
-    C.gemm_wg(dy, x, gw, False, 0, 8)
+    C.gemm_wg(dy, x, gw, False)
     err = ((gw.float() - ref).abs().max() / ref.abs().max()).item()
     print(f"{name}: gemm_wg max rel err vs fp32 {err:.2e}, splits {C.gemm_wg_supported(N, K, M) and 'default'}", flush=True)
     assert err < 8e-3
@@ -42,8 +42,8 @@ for name, N, K in SHAPES:
         with config.override(gemm_wgrad="lib"):
             L.wgrad(dy, x, out=gw, accumulate=True)
     cases.append((name, "library", fl, lib))
-    for pf in PFS:
-        cases.append((name, f"wg pf{pf}", fl, lambda dy=dy, x=x, gw=gw, pf=pf: C.gemm_wg(dy, x, gw, True, 0, pf)))
+    for ld in LOADERS:
+        cases.append((name, f"wg ld{ld}", fl, lambda dy=dy, x=x, gw=gw, ld=ld: C.gemm_wg(dy, x, gw, True, 0, ld)))
 
 for _, _, _, fn in cases:
     fn()

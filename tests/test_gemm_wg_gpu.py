@@ -1,7 +1,7 @@
-"""Weight-gradient GEMM gemm_wg (csrc/kernels/gemm_wg.hip: wave-specialised loads -- waves 0-3 stage
-the LDS ring by inline-asm LDS-DMA, waves 4-7 touch the lines of slice t + PF into L2 -- token-major
-operands read transposed by ds_read_b64_tr_b16, split-K fp32 partials) against an fp32 torch oracle,
-at every prefetch distance, with ragged splits, strided rows and accumulation into a gradient."""
+"""Weight-gradient GEMM gemm_wg (csrc/kernels/gemm_wg.hip: LDS ring staged by inline-asm LDS-DMA,
+token-major operands read transposed by ds_read_b64_tr_b16, split-K fp32 partials) against an fp32
+torch oracle, for both loader geometries (all 8 waves stage, or waves 0-3 only), with ragged splits,
+strided rows, accumulation into a gradient, and the Linear backward routing to it by default."""
 import pytest
 import torch
 
@@ -24,15 +24,15 @@ def test_gemm_wg_matches_fp32(gpu, M, N, K, splits):
     x = torch.randn(M, K, device=gpu, generator=g).to(torch.bfloat16)
     ref = _ref(dy, x)
     scale = ref.abs().max().item()
-    for pf in (0, 4, 6, 8, 12):
+    for loaders in (8, 4):
         out = torch.full((N, K), float("nan"), device=gpu, dtype=torch.bfloat16)
-        C.gemm_wg(dy, x, out, False, splits, pf)
+        C.gemm_wg(dy, x, out, False, splits, loaders)
         err = (out.float() - ref).abs().max().item()
-        assert err <= 8e-3 * scale, (pf, err, scale)
+        assert err <= 8e-3 * scale, (loaders, err, scale)
     # accumulate into an existing gradient (the flat .grad path)
     base = torch.randn(N, K, device=gpu, generator=g).to(torch.bfloat16)
     acc = base.clone()
-    C.gemm_wg(dy, x, acc, True, splits, 8)
+    C.gemm_wg(dy, x, acc, True, splits)
     err2 = (acc.float() - (ref + base.float())).abs().max().item()
     assert err2 <= 8e-3 * scale, (err2, scale)
 
@@ -52,7 +52,20 @@ def test_gemm_wg_strided_rows_default_splits_and_refusals(gpu):
     assert not C.gemm_wg_supported(768, 500, 4096)  # N % 256
     assert not C.gemm_wg_supported(768, 512, 4000)  # tokens % 64
     with pytest.raises(RuntimeError):
-        C.gemm_wg(dy, x, out, False, 0, 5)  # no such prefetch distance
+        C.gemm_wg(dy, x, out, False, 0, 5)  # no such loader geometry
+    # the Linear backward takes gemm_wg by default and agrees with the library path
+    import importlib
+
+    from distributedvolunteercomputing_amd import config
+
+    linear = importlib.import_module("distributedvolunteercomputing_amd.ops.linear")
+    dyc = dy.contiguous()
+    assert linear.gemm_wg_ok(4096, 768, 512, dyc)
+    gv = linear.wgrad(dyc, x)
+    with config.override(gemm_wgrad="lib"):
+        assert not linear.gemm_wg_ok(4096, 768, 512, dyc)
+        gl = linear.wgrad(dyc, x)
+    assert (gv.float() - gl.float()).abs().max().item() <= 1e-2 * ref.abs().max().item()
 
 
 def test_gemm_wg_repeat_runs_bit_identical(gpu):

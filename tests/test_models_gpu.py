@@ -336,21 +336,25 @@ def test_stem_maxpool_propagates_nan_like_torch(gpu):
 def test_fused_batchnorm_large_mean_variance(gpu):
     """|mean| >> std over many rows. The statistics are summed around a per-channel pivot
     (a value of the batch), so the variance keeps its digits where E[x^2] - m^2 on raw fp32 sums would
-    cancel; checked against torch in fp32 (output, running variance)."""
+    cancel. Oracle: float64 statistics of the same bf16 input (torch's fp32 BatchNorm itself scatters
+    by +-2.5 % per channel on this input, so it is not the reference here)."""
     from distributedvolunteercomputing_amd.ops.batchnorm import bn_act
 
     torch.manual_seed(11)
     C = 64
-    bn = torch.nn.BatchNorm2d(C, momentum=1.0).to(gpu)  # running_var = this batch's unbiased variance
-    bn32 = torch.nn.BatchNorm2d(C, momentum=1.0).to(gpu)
-    bn32.load_state_dict(bn.state_dict())
-    bn = bn.to(torch.bfloat16)
-    # mean 200, std 0.5 (bf16 spacing at 200 is 1.0: quantised, but torch sees the same bf16 values)
+    bn = torch.nn.BatchNorm2d(C, momentum=1.0).to(gpu).to(torch.bfloat16)  # running_var = this batch's variance
+    # mean 200, std 0.5 (bf16 spacing at 200 is 1.0: the values are the integers 198..202)
     x = (200 + 0.5 * torch.randn(32, C, 56, 56, device=gpu)).to(torch.bfloat16)
     x = x.to(memory_format=torch.channels_last)
     y = bn_act(x, bn, None, relu=False)
     assert type(y.grad_fn).__name__ == "_BNActBackward"
-    y32 = bn32(x.float())
-    var_ref = bn32.running_var
-    assert float(((bn.running_var.float() - var_ref).abs() / var_ref).max()) < 2e-2
-    assert float((y.float() - y32).norm() / y32.norm()) < 2e-2
+    xd = x.double()
+    mean = xd.mean(dim=(0, 2, 3))
+    var_b = xd.var(dim=(0, 2, 3), unbiased=False)
+    var_u = xd.var(dim=(0, 2, 3), unbiased=True)
+    # running stats are bf16 (spacing 2^-9 at 0.33): within that rounding of the float64 oracle
+    assert float(((bn.running_var.double() - var_u).abs() / var_u).max()) < 4e-3
+    assert float(((bn.running_mean.double() - mean).abs() / mean).max()) < 4e-3
+    yd = (xd - mean[None, :, None, None]) / torch.sqrt(var_b[None, :, None, None] + bn.eps)
+    yd = yd * bn.weight.double()[None, :, None, None] + bn.bias.double()[None, :, None, None]
+    assert float((y.double() - yd).norm() / yd.norm()) < 1e-2
