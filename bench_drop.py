@@ -178,7 +178,8 @@ def peer_main(a):
         sync()
         timeline.append({"step": i, "ms": (time.perf_counter() - t0) * 1e3, "synced": bool(st.synced),
                          "members": st.members, "gen": mem.gen, "sync_ms": st.sync_ms if st.synced else 0.0,
-                         "t_end": time.time(), "t_sync_end": tr.t_sync_end if st.synced else None})
+                         "t_end": time.time(), "t_sync_end": tr.t_sync_end if st.synced else None,
+                         "admit_stages": tr.last_round_stages if st.synced else None})
         i += 1
     store.set("vcx/drop/done", "1")
     with open(os.path.join(a.out, f"peer{a.peer}.json"), "w") as f:
@@ -353,6 +354,10 @@ def launcher(a):
         for e in d["timeline"]:
             cur = tl.setdefault(e["step"], dict(e))
             cur["ms"] = max(cur["ms"], e["ms"])  # a step ends when its slowest survivor is done
+            if e.get("admit_stages"):  # members' admission-round anatomy, max over survivors
+                ms = cur.setdefault("member_stages", {})
+                for k_, v_ in e["admit_stages"].items():
+                    ms[k_] = max(ms.get(k_, v_), v_)
     steps = sorted(tl)
     before = [tl[s]["ms"] for s in steps if s < a.drop_at]
     gen_before = max((tl[s]["gen"] for s in steps if s < a.drop_at), default=0)
@@ -420,11 +425,15 @@ def launcher(a):
                                             if s_ and "admission_round_ms" in s_]
         rec["joiner_admission_stages"] = adm_st
         sj = os.environ.get("VCX_ELASTIC_STAGE_JOINS", "gloo")
-        rec["staged_admission"] = sj == "all" or (sj == "gloo" and backend == "gloo")
+        rec["staged_admission"] = sj == "gloo" and backend == "gloo"
         # per survivor: how long its background communicator build ran, what was left of it to wait
         # for at the switch, and the line-up wait before the admission round
         rec["staged_survivors"] = staged
         rec["rejoin_stall_ms"] = round(tl[rj]["sync_ms"] - steady_sync, 3) if rj is not None else None
+        # the running members' side of that stall (max over survivors): membership agreement, the new
+        # group's communicator init (its first, one-element collective), the model broadcast, the
+        # reduction, guard / verdict / apply -- their sum is the members' admission averaging call
+        rec["rejoin_member_stages_ms"] = tl[rj].get("member_stages") if rj is not None else None
         rec["ms_per_step_after_rejoin"] = round(mean(back), 3) if back else None
         rec["samples_per_s_after_rejoin"] = round(a.peers * a.batch / mean(back) * 1e3, 2) if back else None
     line = json.dumps(rec)

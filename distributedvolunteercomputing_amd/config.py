@@ -102,7 +102,7 @@ _ENV = {
     "trace_dir": ("VCX_TRACE_DIR", str),
     "metrics_dir": ("VCX_METRICS_DIR", str),
 }
-_CHOICES = {"gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "all", "off"),
+_CHOICES = {"gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "off"),
             "uplink_pipeline": ("relay", "all", "off")}
 
 _lock = threading.Lock()

@@ -331,8 +331,13 @@ class ElasticMembership:
         # blocking store waits (server-side wake-up) instead of sleep-polling on the fast paths; a
         # wait that runs out falls back to the polling scan, which owns lease/EOF detection
         self.bell_s = min(2.0, max(0.25, lease_s / 4))
-        sj = config.get().elastic_stage_joins
-        self.stage_joins = sj == "all" or (sj == "gloo" and backend == "gloo")
+        # staged admission (the next generation's communicator built in the background during the local
+        # steps) runs on gloo groups only. On RCCL it was removed in round 5: building the new
+        # communicator on a helper thread while the main thread ran collectives on the current one
+        # SIGSEGVed every member at 8 ranks (gpurun_out/f2/rejoin_n8_staged.log, round 4), and its
+        # members' stall is accounted instead (LocalSGDTrainer.last_round_stages: the new group's
+        # communicator init is its first collective, timed apart from the model broadcast)
+        self.stage_joins = config.get().elastic_stage_joins == "gloo" and backend == "gloo"
         self.last_go_wait_ms = 0.0
         self._staged = None  # (gen, members, newcomers, njoin, group) agreed, built in the background
         self._retired: list = []  # groups replaced by a staged generation, shut down after its first commit

@@ -80,6 +80,8 @@ class LocalSGDTrainer:
         self.last_sync_ms = 0.0
         self.t_sync_end = None
         self.failed_rounds = 0  # elastic rounds aborted mid-collective and redone
+        self.admit_split = None  # the last admission transfer: communicator init vs broadcast (ms, bytes)
+        self.last_round_stages = None  # a continuing member's stages of the last admission round
 
     # ------------------------------------------------------------------ per step
     def set_lr(self, lr: float):
@@ -166,17 +168,41 @@ class LocalSGDTrainer:
         the pseudo-gradient is recomputed, the compressor state is rolled back) and redo the
         round on the next generation."""
         mem = self.membership
+        t0 = time.perf_counter()
         grp, _, newcomers = mem.sync_round()
+        t1 = time.perf_counter()
+        self.last_round_stages = None
         while True:
             self.group = grp
             snap = self.compressor.snapshot() if (self.compressor is not None and grp.size > 1) else None
             try:
                 with mem.guard():
+                    t2 = time.perf_counter()
                     adopted = self._admit_newcomers(newcomers) if newcomers else None
+                    self._dev_sync()
+                    t3 = time.perf_counter()
                     res = self._reduce(newcomers)
                     bufs = self.buffers.averaged(grp)
+                    self._dev_sync()
+                    t4 = time.perf_counter()
                 self._adopt(adopted)  # nothing is applied before the verdict is `commit`
                 self._apply(res, bufs)
+                if newcomers:
+                    # a continuing member's anatomy of an admission round (VERDICT r4 #7: where the
+                    # members' rejoin stall goes): membership agreement, the new group's first
+                    # collective (RCCL communicator init), the model broadcast, the reduction, and
+                    # what is left (guard entry / exit, verdict, apply)
+                    self._dev_sync()
+                    t5 = time.perf_counter()
+                    ad = self.admit_split or {}
+                    self.last_round_stages = {
+                        "sync_round_ms": round((t1 - t0) * 1e3, 3),
+                        "comm_init_ms": round(ad.get("comm_init_ms", 0.0), 3),
+                        "broadcast_ms": round(ad.get("broadcast_ms", 0.0), 3),
+                        "reduce_ms": round((t4 - t3) * 1e3, 3),
+                        "guard_verdict_apply_ms": round(((t5 - t1) - (t4 - t2)) * 1e3, 3),
+                        "broadcast_bytes": ad.get("bytes", 0),
+                    }
                 return
             except PeerFailure:
                 if snap is not None:
@@ -238,8 +264,22 @@ class LocalSGDTrainer:
                              + ([self.buffers.as_fp32().to(bdev)] if nb else []))
         else:
             pack = torch.empty(n, dtype=torch.float32, device=bdev)
+        # a one-element collective first: its time is the new group's communicator set-up (RCCL builds
+        # its communicator lazily, at the first collective) plus one latency, so the broadcast time
+        # below is the model transfer alone
+        t0 = time.perf_counter()
+        g.broadcast_(torch.zeros(1, dtype=torch.float32, device=bdev), root)
+        self._dev_sync()
+        t1 = time.perf_counter()
         g.broadcast_(pack, root)
+        self._dev_sync()
+        t2 = time.perf_counter()
+        self.admit_split = {"comm_init_ms": (t1 - t0) * 1e3, "broadcast_ms": (t2 - t1) * 1e3, "bytes": int(n * 4)}
         return pack if members[g.rank] in newcomers else None
+
+    def _dev_sync(self):
+        if self.anchor.is_cuda:
+            torch.cuda.synchronize(self.anchor.device)
 
     def _adopt(self, pack):
         """A newcomer takes the admitted model (after `commit`)."""
@@ -287,10 +327,12 @@ class LocalSGDTrainer:
                 self._apply(res, bufs)
                 dev_sync()
                 t5 = time.perf_counter()
+                ad = self.admit_split or {}
                 st = {"connect_ms": (t1 - t0) * 1e3, "wait_round_ms": (t2 - t1) * 1e3,
-                      "broadcast_ms": (t3 - t2) * 1e3, "reduce_ms": (t4 - t3) * 1e3,
+                      "comm_init_ms": ad.get("comm_init_ms", 0.0), "broadcast_ms": ad.get("broadcast_ms", (t3 - t2) * 1e3),
+                      "reduce_ms": (t4 - t3) * 1e3,
                       "verdict_apply_ms": (t5 - t4) * 1e3, "admission_round_ms": (t5 - t2) * 1e3,
-                      "broadcast_bytes": int(self.anchor.numel() * 4 * (2 if self.outer_mom is not None else 1))}
+                      "broadcast_bytes": ad.get("bytes", int(self.anchor.numel() * 4 * (2 if self.outer_mom is not None else 1)))}
                 self.admit_stages = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in st.items()}
                 return
             except PeerFailure:

@@ -74,3 +74,10 @@ def test_bench_drop_kill_two_then_rejoin(tmp_path):
     assert rec["staged_admission"] and rec["staged_survivors"], rec
     assert all(s["bg_build_ms"] is not None and s["go_wait_ms"] is not None for s in rec["staged_survivors"])
     assert len(rec["joiner_admission_round_ms"]) == 2
+    # the joiners' communicator init is timed apart from the model broadcast, and the
+    # running members' side of the admission round has its own anatomy
+    for st in rec["joiner_admission_stages"]:
+        assert st["comm_init_ms"] >= 0 and st["broadcast_ms"] >= 0 and st["broadcast_bytes"] > 0, st
+    ms = rec["rejoin_member_stages_ms"]
+    assert ms is not None and {"sync_round_ms", "comm_init_ms", "broadcast_ms", "reduce_ms",
+                               "guard_verdict_apply_ms"} <= set(ms), ms
