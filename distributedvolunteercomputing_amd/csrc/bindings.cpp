@@ -214,7 +214,9 @@ static float* bn_workspace(const at::Tensor& x, int64_t C) {
 // Train-mode BatchNorm (+ residual) (+ ReLU) on NHWC bf16 activations (batchnorm.hip). x / res / y:
 // contiguous [..., C] (the NHWC view of a channels-last tensor); gamma / beta bf16 [C]; running stats
 // bf16 or fp32 [C], updated in place (skipped when undefined); nbt: the layer's num_batches_tracked
-// (int64, incremented on the device) or None. Returns y, mean, rstd, scale (fp32 [C]).
+// (int64, incremented on the device) or None. Returns y, mean, rstd, scale (fp32 [C]) and, with the ReLU,
+// its mask as one bit per element (uint8 [R, C / 8]: bit i of byte e = element 8 e + i is > 0), which
+// the backward reads instead of y; undefined without the ReLU.
 std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma, at::Tensor beta,
                                      c10::optional<at::Tensor> run_mean, c10::optional<at::Tensor> run_var, double eps,
                                      double momentum, bool relu, c10::optional<at::Tensor> nbt) {
@@ -243,10 +245,12 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res
   auto f = x.options().dtype(at::kFloat);
   at::Tensor st = at::empty({4, C}, f);
   at::Tensor y = at::empty_like(x);
-  vcx_bn_fwd_train(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), R, (int)C, gamma.data_ptr(),
-                   beta.data_ptr(), rm, rv, fp32, (float)eps, (float)momentum, bn_workspace(x, C), st[0].data_ptr<float>(),
-                   st[1].data_ptr<float>(), st[2].data_ptr<float>(), st[3].data_ptr<float>(), nb, relu ? 1 : 0, cur_stream());
-  return {y, st[0], st[1], st[2]};
+  at::Tensor mask = relu ? at::empty({R, C / 8}, x.options().dtype(at::kByte)) : at::Tensor();
+  vcx_bn_fwd_train(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), relu ? mask.data_ptr() : nullptr, R,
+                   (int)C, gamma.data_ptr(), beta.data_ptr(), rm, rv, fp32, (float)eps, (float)momentum,
+                   bn_workspace(x, C), st[0].data_ptr<float>(), st[1].data_ptr<float>(), st[2].data_ptr<float>(),
+                   st[3].data_ptr<float>(), nb, relu ? 1 : 0, cur_stream());
+  return {y, st[0], st[1], st[2], mask};
 }
 
 // ResNet stem max-pool 3x3 / stride 2 / pad 1 on the NHWC view [N, H, W, C] (bf16, C % 8 == 0):
@@ -292,13 +296,16 @@ at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor scal
 // returns dx, d residual (undefined unless want_dres), dgamma, dbeta (fp32 [C])
 // gw / gb: flat bf16 [C] gradient buffers of gamma / beta that dgamma / dbeta are ADDED into (both or
 // neither); the returned dgamma / dbeta are then for information only
-std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Tensor mean, at::Tensor rstd,
+std::vector<at::Tensor> bn_bwd(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x, at::Tensor mean, at::Tensor rstd,
                                at::Tensor scale, bool relu, bool want_dres, c10::optional<at::Tensor> gw,
                                c10::optional<at::Tensor> gb) {
-  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && x.is_contiguous() && y.is_contiguous() &&
-                  dy.sizes() == x.sizes() && y.sizes() == x.sizes() && dy.scalar_type() == at::kBFloat16 &&
-                  x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16, "bn_bwd: dy, y, x bf16 NHWC alike");
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes() &&
+                  dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "bn_bwd: dy, x bf16 NHWC alike");
   const int64_t C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(relu == (mask && mask->defined()), "bn_bwd: the ReLU mask with relu (and only then)");
+  if (relu)
+    TORCH_CHECK(mask->is_cuda() && mask->is_contiguous() && mask->scalar_type() == at::kByte &&
+                    mask->numel() * 8 == R * C && mask->get_device() == x.get_device(), "bn_bwd: mask uint8 [R, C / 8]");
   TORCH_CHECK(vcx_bn_supported((int)C), "bn: C must be a power of two in 8..2048");
   for (const at::Tensor* t : {&mean, &rstd, &scale})
     TORCH_CHECK(t->numel() == C && t->scalar_type() == at::kFloat && t->is_contiguous(), "bn_bwd: stats fp32 [C]");
@@ -311,7 +318,7 @@ std::vector<at::Tensor> bn_bwd(at::Tensor dy, at::Tensor y, at::Tensor x, at::Te
   at::Tensor sums = at::empty({2 * C}, x.options().dtype(at::kFloat));
   at::Tensor dx = at::empty_like(x);
   at::Tensor dres = want_dres ? at::empty_like(x) : at::Tensor();
-  vcx_bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+  vcx_bn_bwd(dy.data_ptr(), relu ? mask->data_ptr() : nullptr, x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
              scale.data_ptr<float>(), R, (int)C, bn_workspace(x, C), sums.data_ptr<float>(),
              flat ? gw->data_ptr() : nullptr, flat ? gb->data_ptr() : nullptr, dx.data_ptr(),
              want_dres ? dres.data_ptr() : nullptr, relu ? 1 : 0, cur_stream());
@@ -807,7 +814,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_apply", &bn_apply);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
-  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("mean"), py::arg("rstd"), py::arg("scale"),
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("mean"), py::arg("rstd"), py::arg("scale"),
         py::arg("relu"), py::arg("want_dres"), py::arg("gw") = py::none(), py::arg("gb") = py::none());
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0);

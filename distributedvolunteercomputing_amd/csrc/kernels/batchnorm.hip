@@ -4,10 +4,13 @@
 // input gradient), each reading or writing the whole activation; here:
 //   forward : stats    (read x once: per-channel sum / sum of squares in fp32, block partials + atomics)
 //             finalize (mean, 1/std, the per-channel affine scale/shift, running stats, num_batches_tracked)
-//             apply    (read x [+ residual], write y = relu(x * scale + shift [+ residual]))
-//   backward: reduce   (read dy, y, x: per-channel sum dz and sum dz * xhat, dz = dy * [y > 0])
+//             apply    (read x [+ residual], write y = relu(x * scale + shift [+ residual]) and, with the
+//                       ReLU, its mask as one BIT per element: 1 byte per lane of 8 channels)
+//   backward: reduce   (read dy, mask, x: per-channel sum dz and sum dz * xhat, dz = dy * mask)
 //             bwd_fin  (the sums for the dx pass; dbeta / dgamma added into the flat bf16 .grad when given)
-//             dx       (read dy, y, x, write dx [and d residual = dz])
+//             dx       (read dy, mask, x, write dx [and d residual = dz])
+// The bit mask replaces the bf16 y the backward passes used to read for [y > 0]: 1/16 of its bytes, so
+// each backward pass moves ~2 B per element less (of ~8-10), and y need not be kept for the backward.
 // The atomics accumulate into a zero-at-rest workspace (one per device, stream and C, owned by the
 // binding) that the finalize kernels read and zero again: no fill kernel per call. (A last-block
 // finalize inside the reduction kernels instead -- a ticket counter behind device-scope fences --
@@ -121,7 +124,8 @@ __global__ void finalize_kernel(float* __restrict__ ws, const bf16* __restrict__
 template <bool RES, bool RELU>
 __global__ void __launch_bounds__(NT) apply_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                    const float* __restrict__ scale, const float* __restrict__ shift,
-                                                   bf16* __restrict__ y, int64_t n8, int cpr) {
+                                                   bf16* __restrict__ y, unsigned char* __restrict__ mask, int64_t n8,
+                                                   int cpr) {
   int64_t e = blockIdx.x * (int64_t)NT + threadIdx.x;
   const int c0 = (int)(e % cpr) * 8;
   float sc[8], sh[8];
@@ -135,20 +139,25 @@ __global__ void __launch_bounds__(NT) apply_kernel(const bf16* __restrict__ x, c
     load8(x + e * 8, v);
     if (RES) load8(res + e * 8, r);
     bf16x8 o;
+    unsigned bits = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float z = fmaf(v[i], sc[i], sh[i]);
       if (RES) z += r[i];
-      if (RELU) z = fmaxf(z, 0.f);
+      if (RELU) {
+        bits |= (z > 0.f ? 1u : 0u) << i;
+        z = fmaxf(z, 0.f);
+      }
       o[i] = (bf16)z;
     }
     *(bf16x8*)(y + e * 8) = o;
+    if (RELU && mask) mask[e] = (unsigned char)bits;
   }
 }
 
-// backward reductions: sum dz and sum dz * xhat per channel, dz = dy [* (y > 0)]
+// backward reductions: sum dz and sum dz * xhat per channel, dz = dy [* mask]
 template <bool RELU>
-__global__ void __launch_bounds__(NT) bwd_reduce_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+__global__ void __launch_bounds__(NT) bwd_reduce_kernel(const bf16* __restrict__ dy, const unsigned char* __restrict__ mask,
                                                         const bf16* __restrict__ x, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, int64_t R, int C,
                                                         int64_t rows_per_block, float* __restrict__ sdz,
@@ -164,13 +173,13 @@ __global__ void __launch_bounds__(NT) bwd_reduce_kernel(const bf16* __restrict__
   channel_reduce(
       C, r0, r1,
       [&](int64_t off, float(&s0)[8], float(&s1)[8]) {
-        float g[8], yy[8], xx[8];
+        float g[8], xx[8];
         load8(dy + off, g);
         load8(x + off, xx);
-        if (RELU) load8(y + off, yy);
+        const unsigned mk = RELU ? mask[off >> 3] : 0xffu;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const float dz = RELU ? (yy[i] > 0.f ? g[i] : 0.f) : g[i];
+          const float dz = RELU ? ((mk >> i) & 1u ? g[i] : 0.f) : g[i];
           s0[i] += dz;
           s1[i] = fmaf(dz, (xx[i] - m[i]) * rs[i], s1[i]);
         }
@@ -195,7 +204,7 @@ __global__ void bwd_finalize_kernel(float* __restrict__ ws, int C, float* __rest
 
 // dx = gamma rstd (dz - (sum dz + xhat sum dz xhat) / R); d residual = dz
 template <bool RES, bool RELU>
-__global__ void __launch_bounds__(NT) bwd_dx_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+__global__ void __launch_bounds__(NT) bwd_dx_kernel(const bf16* __restrict__ dy, const unsigned char* __restrict__ mask,
                                                     const bf16* __restrict__ x, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, const float* __restrict__ scale,
                                                     const float* __restrict__ sdz, const float* __restrict__ sdzx,
@@ -213,14 +222,14 @@ __global__ void __launch_bounds__(NT) bwd_dx_kernel(const bf16* __restrict__ dy,
     w[i] = sdzx[c0 + i] * invR;
   }
   for (; e < n8; e += (int64_t)gridDim.x * NT) {
-    float g[8], yy[8], xx[8];
+    float g[8], xx[8];
     load8(dy + e * 8, g);
     load8(x + e * 8, xx);
-    if (RELU) load8(y + e * 8, yy);
+    const unsigned mk = RELU ? mask[e] : 0xffu;
     bf16x8 o, od;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float dz = RELU ? (yy[i] > 0.f ? g[i] : 0.f) : g[i];
+      const float dz = RELU ? ((mk >> i) & 1u ? g[i] : 0.f) : g[i];
       const float xh = (xx[i] - m[i]) * rs[i];
       o[i] = (bf16)(sc[i] * (dz - fmaf(xh, w[i], u[i])));
       od[i] = (bf16)dz;
@@ -343,9 +352,9 @@ bool vcx_bn_supported(int C) { return C >= 8 && C <= 2048 && (2048 % C) == 0; }
 
 // forward (train): ws = the zero-at-rest workspace, fp32 [2C] (zeroed once by the caller, left zeroed
 // by every call); mean/rstd/scale/shift fp32 [C]; nbt int64 [1] or null
-void vcx_bn_fwd_train(const void* x, const void* res, void* y, int64_t R, int C, const void* gamma, const void* beta,
-                      void* run_mean, void* run_var, int run_fp32, float eps, float momentum, float* ws, float* mean,
-                      float* rstd, float* scale, float* shift, int64_t* nbt, int relu, hipStream_t s) {
+void vcx_bn_fwd_train(const void* x, const void* res, void* y, void* mask, int64_t R, int C, const void* gamma,
+                      const void* beta, void* run_mean, void* run_var, int run_fp32, float eps, float momentum, float* ws,
+                      float* mean, float* rstd, float* scale, float* shift, int64_t* nbt, int relu, hipStream_t s) {
   using namespace bn;
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
@@ -359,7 +368,8 @@ void vcx_bn_fwd_train(const void* x, const void* res, void* y, int64_t R, int C,
   const int64_t n8 = R * C / 8;
   const int g = grid_for(n8);
   auto go = [&](auto k) {
-    hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)x, (const bf16*)res, scale, shift, (bf16*)y, n8, C / 8);
+    hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)x, (const bf16*)res, scale, shift, (bf16*)y,
+                       (unsigned char*)mask, n8, C / 8);
   };
   if (res)
     relu ? go(apply_kernel<true, true>) : go(apply_kernel<true, false>);
@@ -374,7 +384,8 @@ void vcx_bn_apply(const void* x, const void* res, void* y, int64_t R, int C, con
   const int64_t n8 = R * C / 8;
   const int g = grid_for(n8);
   auto go = [&](auto k) {
-    hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)x, (const bf16*)res, scale, shift, (bf16*)y, n8, C / 8);
+    hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)x, (const bf16*)res, scale, shift, (bf16*)y,
+                       (unsigned char*)nullptr, n8, C / 8);
   };
   if (res)
     relu ? go(apply_kernel<true, true>) : go(apply_kernel<true, false>);
@@ -385,23 +396,23 @@ void vcx_bn_apply(const void* x, const void* res, void* y, int64_t R, int C, con
 // backward: ws = the zero-at-rest workspace (as in the forward); sums = fp32 [2C] output [sum dz |
 // sum dz xhat] = [dbeta | dgamma]; gw / gb = flat bf16 gradients of gamma / beta that dgamma / dbeta
 // are added into (or null)
-void vcx_bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* rstd, const float* scale,
+void vcx_bn_bwd(const void* dy, const void* mask, const void* x, const float* mean, const float* rstd, const float* scale,
                 int64_t R, int C, float* ws, float* sums, void* gw, void* gb, void* dx, void* dres, int relu,
                 hipStream_t s) {
   using namespace bn;
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
   if (relu)
-    hipLaunchKernelGGL(bwd_reduce_kernel<true>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const bf16*)y,
+    hipLaunchKernelGGL(bwd_reduce_kernel<true>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const unsigned char*)mask,
                        (const bf16*)x, mean, rstd, R, C, rpb, ws, ws + C);
   else
-    hipLaunchKernelGGL(bwd_reduce_kernel<false>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const bf16*)y,
+    hipLaunchKernelGGL(bwd_reduce_kernel<false>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const unsigned char*)mask,
                        (const bf16*)x, mean, rstd, R, C, rpb, ws, ws + C);
   hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, C, sums, (bf16*)gw, (bf16*)gb);
   const int64_t n8 = R * C / 8;
   const int g = grid_for(n8);
   auto go = [&](auto k) {
-    hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)dy, (const bf16*)y, (const bf16*)x, mean, rstd, scale,
+    hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)dy, (const unsigned char*)mask, (const bf16*)x, mean, rstd, scale,
                        (const float*)sums, (const float*)(sums + C), (bf16*)dx, (bf16*)dres, n8, C / 8, 1.f / (float)R);
   };
   if (dres)

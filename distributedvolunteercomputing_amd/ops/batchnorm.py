@@ -3,8 +3,9 @@ channels-last bf16 activations (csrc/kernels/batchnorm.hip): y = relu(bn(x) [+ r
 
 Forward: one statistics pass (read x), a per-channel finalize (running stats updated in place),
 one apply pass (read x [+ residual], write y). Backward: one reduction pass (read dy, y, x) and
-one input-gradient pass (read dy, y, x; write dx [and d residual]): the ReLU mask comes from y, so
-the pre-activation is never stored. On CPU, in fp32 or for unsupported channel counts the
+one input-gradient pass (read dy, mask, x; write dx [and d residual]): the ReLU mask is one bit per
+element written by the forward's apply pass (1/16 of the bytes of y, which the backward used to read),
+so neither the pre-activation nor y is kept for the backward. On CPU, in fp32 or for unsupported channel counts the
 torch composition runs instead (the numerics oracle of tests/test_models_gpu.py).
 """
 from __future__ import annotations
@@ -30,15 +31,15 @@ class _BNAct(torch.autograd.Function):
         C = native()
         xh = _nhwc(x)
         rh = _nhwc(residual) if residual is not None else None
-        y, mean, rstd, scale = C.bn_fwd_train(xh, rh, weight, bias, run_mean, run_var, eps, momentum, relu, nbt)
-        ctx.save_for_backward(xh, y, mean, rstd, scale)
+        y, mean, rstd, scale, mask = C.bn_fwd_train(xh, rh, weight, bias, run_mean, run_var, eps, momentum, relu, nbt)
+        ctx.save_for_backward(xh, mask if relu else None, mean, rstd, scale)
         ctx.relu, ctx.has_res, ctx.pdtype = relu, residual is not None, weight.dtype
         ctx.params = (weight, bias)
         return y.permute(0, 3, 1, 2)
 
     @staticmethod
     def backward(ctx, dy):
-        xh, y, mean, rstd, scale = ctx.saved_tensors
+        xh, mask, mean, rstd, scale = ctx.saved_tensors
         weight, bias = ctx.params
         ctx.params = None
         dyh = _nhwc(dy)
@@ -47,7 +48,7 @@ class _BNAct(torch.autograd.Function):
         gw = grad_buffer(weight) if ctx.needs_input_grad[1] else None
         gb = grad_buffer(bias) if ctx.needs_input_grad[2] else None
         flat = gw is not None and gb is not None
-        dx, dres, dgamma, dbeta = native().bn_bwd(dyh, y, xh, mean, rstd, scale, ctx.relu, ctx.has_res,
+        dx, dres, dgamma, dbeta = native().bn_bwd(dyh, mask, xh, mean, rstd, scale, ctx.relu, ctx.has_res,
                                                   gw if flat else None, gb if flat else None)
         dx = dx.permute(0, 3, 1, 2)
         dres = dres.permute(0, 3, 1, 2) if ctx.has_res else None
