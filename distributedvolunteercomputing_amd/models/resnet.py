@@ -17,6 +17,7 @@ import torch.nn.functional as F
 
 from .. import config
 from ..ops.batchnorm import bn_act, stem_maxpool
+from ..ops.linear import GradJoin, residual_tap
 
 
 class Conv1x1(nn.Conv2d):
@@ -26,18 +27,27 @@ class Conv1x1(nn.Conv2d):
     def __init__(self, cin, cout, stride=1):
         super().__init__(cin, cout, 1, stride=stride, bias=False)
 
-    def forward(self, x):
+    def gemm_path(self, x) -> bool:
+        """This convolution runs as the native GEMM (so a GradJoin on its input is consumed)."""
+        from ..ops.linear import native_linear_ok
+
+        return (x.is_cuda and config.get().resnet_conv1x1 == "gemm" and x.is_contiguous(memory_format=torch.channels_last)
+                and native_linear_ok(self.weight))
+
+    def forward(self, x, join=None):
         if not (x.is_cuda and config.get().resnet_conv1x1 == "gemm"
                 and x.is_contiguous(memory_format=torch.channels_last)):
+            assert join is None
             return super().forward(x)
         from ..ops.linear import linear
 
         xh = x.permute(0, 2, 3, 1)  # [N, H, W, C] view of the channels-last storage
         if self.stride[0] != 1:
+            assert join is None
             xh = xh[:, ::self.stride[0], ::self.stride[1], :].contiguous()
         N, H, W, C = xh.shape
         # the [Cout, Cin, 1, 1] parameter itself: its gradient lands in the flat .grad directly
-        y = linear(xh.reshape(N * H * W, C), self.weight)
+        y = linear(xh.reshape(N * H * W, C), self.weight, join=join)
         return y.view(N, H, W, self.out_channels).permute(0, 3, 1, 2)
 
 
@@ -59,10 +69,16 @@ class Bottleneck(nn.Module):
             self.down = nn.Sequential(Conv1x1(cin, cout, stride=stride), nn.BatchNorm2d(cout))
 
     def forward(self, x):
-        # BatchNorm + ReLU (+ the residual add) as fused HIP passes in train mode (ops/batchnorm.py)
+        # BatchNorm + ReLU (+ the residual add) as fused HIP passes in train mode (ops/batchnorm.py).
+        # Identity shortcut: x feeds conv1 and the residual add, so autograd would sum the two
+        # gradients of x in an elementwise pass; the shortcut's gradient goes to conv1's input-gradient
+        # GEMM instead, which adds it as its C (beta = 1; ops/linear.py GradJoin)
+        join = GradJoin() if (self.down is None and torch.is_grad_enabled() and self.conv1.gemm_path(x)) else None
         idt = x if self.down is None else bn_act(self.down[0](x), self.down[1], relu=False)
-        y = bn_act(self.conv1(x), self.bn1)
+        y = bn_act(self.conv1(x, join=join), self.bn1)
         y = bn_act(self.conv2(y), self.bn2)
+        if join is not None:
+            idt = residual_tap(x, join)  # created after conv1's node: its backward runs first
         return bn_act(self.conv3(y), self.bn3, residual=idt)
 
 

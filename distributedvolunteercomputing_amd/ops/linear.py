@@ -230,9 +230,52 @@ def _w2(w):
     return w if w.dim() == 2 else w.view(w.shape[0], -1)
 
 
+class GradJoin:
+    """Hands one extra gradient of a linear layer's input to that layer's backward, which adds it in
+    its input-gradient GEMM (beta = 1) instead of autograd adding the two gradients in a separate
+    elementwise pass. Made for a residual block whose input x feeds both its first 1x1 convolution
+    and the identity shortcut: ``residual_tap(x, join)`` on the shortcut passes its gradient here,
+    ``linear(x2d, w, join=join)`` adds it (models/resnet.py). Protocol (one backward pass at a
+    time, both sides on the autograd thread): the tap's backward runs first in practice (it becomes
+    ready at the block's last BatchNorm, the convolution only at the end of the branch); whichever
+    side runs second sees the other's state, so the result is right in either order."""
+
+    def __init__(self):
+        self.pending = None  # the shortcut's gradient as the [M, K] matrix of the layer input
+        self.ran = False     # the layer's backward ran without it (the tap then returns its gradient)
+
+    def take(self):
+        g, self.pending = self.pending, None
+        return g
+
+
+class _ResidualTap(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, join):
+        ctx.join = join
+        join.pending, join.ran = None, False
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        join, ctx.join = ctx.join, None
+        if join.ran or g.dim() != 4:
+            return g, None
+        gh = g.permute(0, 2, 3, 1)  # the [N, H, W, C] view the 1x1 convolution's GEMM uses
+        if not gh.is_contiguous():
+            return g, None
+        join.pending = gh.reshape(-1, gh.shape[-1])
+        return None, None
+
+
+def residual_tap(x: torch.Tensor, join: GradJoin) -> torch.Tensor:
+    """x itself (a view), whose gradient goes to ``join`` (channels-last 4-D x) instead of autograd."""
+    return _ResidualTap.apply(x, join)
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, bias_grad_elsewhere=False):
+    def forward(ctx, x, w, b, bias_grad_elsewhere=False, join=None):
         # w: [N, K], or a 1x1 convolution's [N, K, 1, 1] weight itself (not a view of it: its gradient
         # then goes straight into the parameter's flat .grad, no view-backward + accumulation pass)
         ctx.save_for_backward(x, w)
@@ -240,6 +283,7 @@ class _Linear(torch.autograd.Function):
         # sums it already has at hand) and returns it for the same bias tensor
         ctx.has_bias = b is not None and not bias_grad_elsewhere
         ctx.bias = b
+        ctx.join = join
         x2 = x.reshape(-1, x.shape[-1])
         w = _w2(w)
         if gemm_nt_ok(x2.shape[0], w.shape[0], x2.shape[1], x2):
@@ -255,7 +299,16 @@ class _Linear(torch.autograd.Function):
         x2 = x.reshape(-1, K)
         dy2 = dy2.contiguous()
         dx = None
-        if ctx.needs_input_grad[0]:
+        join, ctx.join = ctx.join, None
+        base = join.take() if join is not None else None
+        if join is not None and base is None:
+            join.ran = True
+        if ctx.needs_input_grad[0] and base is not None and base.shape == (dy2.shape[0], K) and base.is_contiguous():
+            # the shortcut's gradient is the C of this GEMM (beta = 1): no separate add pass
+            dx = base.addmm_(dy2, w).view(x.shape)
+        elif base is not None:
+            dx = (mm(dy2, w) + base).view(x.shape) if ctx.needs_input_grad[0] else None
+        elif ctx.needs_input_grad[0]:
             if gemm_nt_ok(dy2.shape[0], K, N, dy2):
                 dx = gemm_nt(dy2, transpose_weight(w)).view(x.shape)
             elif dgrad_ps_ok(dy2.shape[0], K, N, dy2):
@@ -283,9 +336,9 @@ class _Linear(torch.autograd.Function):
             dy2.record_stream(side)  # keep the inputs' memory until the side stream is done with it
             x2.record_stream(side)
             _queue_join(main, side, dy2.device)
-            return dx, None, None, None
+            return dx, None, None, None, None
         dw, db = _param_grads(dy2, x2, w, bias, want_w, want_b)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def native_linear_ok(w: torch.Tensor) -> bool:
@@ -294,13 +347,14 @@ def native_linear_ok(w: torch.Tensor) -> bool:
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
-           bias_grad_elsewhere: bool = False) -> torch.Tensor:
+           bias_grad_elsewhere: bool = False, join: GradJoin | None = None) -> torch.Tensor:
     """y = x @ w^T (+ b), x [..., K], w [N, K] (or a 1x1 convolution's [N, K, 1, 1]). With
     bias_grad_elsewhere the backward leaves the bias gradient to y's consumer (e.g.
     ``causal_attention(qkv, bias=b)``), which must then be y's only consumer and return
     d(loss)/d(b) = column sums of dy for the same tensor."""
     if native_linear_ok(w):
-        return _Linear.apply(x, w, b, bias_grad_elsewhere)
+        return _Linear.apply(x, w, b, bias_grad_elsewhere, join)
+    assert join is None, "a GradJoin needs the native linear path (its backward consumes the joined gradient)"
     return F.linear(x, _w2(w), b)
 
 
