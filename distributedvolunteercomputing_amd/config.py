@@ -51,6 +51,7 @@ class RuntimeConfig:
     conv_find: bool = True
     resnet_bn: str = "fused"  # VCX_RESNET_BN: ResNet train-mode BatchNorm (+ add) + ReLU as fused HIP passes ("fused")
     # or the torch composition ("torch")
+    resnet_join: bool = True  # VCX_RESNET_JOIN: identity-shortcut gradient added in conv1's dgrad GEMM (GradJoin)
     # ---- distributed / control plane
     gloo_host: str = "127.0.0.1"  # VCX_GLOO_HOST: interface gloo peer groups bind to
     p2p_backend: str = ""  # VCX_P2P_BACKEND: pair-group backend of the p2p chunk plane ("" = auto)
@@ -58,8 +59,8 @@ class RuntimeConfig:
     elastic_liveness: bool = True  # VCX_ELASTIC_LIVENESS: TCP liveness links (process death seen at once)
     # VCX_ELASTIC_STAGE_JOINS: a joiner's generation is agreed one round early and its communicator
     # built during the local steps (the admission round pays no communicator init): "gloo" (default:
-    # gloo groups only -- with RCCL at 8 ranks on one card it broke the members, profiles/
-    # r4_rccl8_rehearsal_1gpu.txt), "all", or "off"
+    # gloo groups only; the RCCL form broke the members at 8 ranks on one card, profiles/
+    # r4_rccl8_rehearsal_1gpu.txt, and was removed in round 5), or "off"
     elastic_stage_joins: str = "gloo"
     # VCX_UPLINK_PIPELINE: the requester packs / resizes chunk k+1 while a wire thread ships chunk k:
     # "relay" (default: the relay plane only -- same-box A/B with the npy sink, relay 6463 vs 5506,
@@ -80,6 +81,7 @@ _ENV = {
     "dgrad_ps": ("VCX_DGRAD_PS", _bool),
     "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
     "resnet_bn": ("VCX_RESNET_BN", str),
+    "resnet_join": ("VCX_RESNET_JOIN", _bool),
     "conv_find": ("VCX_CONV_FIND", _bool),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),
     "gemm_select": ("VCX_GEMM_SELECT", _bool),

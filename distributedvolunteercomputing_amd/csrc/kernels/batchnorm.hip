@@ -32,8 +32,16 @@ __device__ __forceinline__ void load8(const bf16* p, float (&v)[8]) {
   for (int i = 0; i < 8; ++i) v[i] = (float)x[i];
 }
 
+template <int U>
+struct Unroll {
+  static constexpr int value = U;
+};
+
 // per-channel partial sums of this block over rows [r0, r1), reduced in LDS over the threads that
-// share a channel chunk, then added to out0 / out1 (fp32 [C]) with one atomic per channel
+// share a channel chunk, then added to out0 / out1 (fp32 [C]) with one atomic per channel.
+// body(off, step, Unroll<U>, s0, s1) handles the U rows off, off + step, ...: the main loop passes
+// U = 4 so every lane keeps 4 row loads per operand in flight (one at a time left these passes at
+// 2-3 TB/s, latency-bound: profiles/r5_cfg3_resnet50_categories.txt)
 template <typename F>
 __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&& body, float* out0, float* out1) {
   __shared__ float red[2][NT][9];  // [quantity][thread][8 channels + pad]
@@ -44,8 +52,12 @@ __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&
   float s0[8], s1[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) s0[i] = s1[i] = 0.f;
-  if (rr < rpp)
-    for (int64_t r = r0 + rr; r < r1; r += rpp) body(r * C + ch * 8, s0, s1);
+  if (rr < rpp) {
+    const int64_t step = (int64_t)rpp * C;
+    int64_t r = r0 + rr;
+    for (; r + 3 * rpp < r1; r += 4 * rpp) body(r * C + ch * 8, step, Unroll<4>{}, s0, s1);
+    for (; r < r1; r += rpp) body(r * C + ch * 8, step, Unroll<1>{}, s0, s1);
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     red[0][tid][i] = s0[i];
@@ -75,15 +87,19 @@ __global__ void __launch_bounds__(NT) stats_kernel(const bf16* __restrict__ x, i
   load8(x + (threadIdx.x % (C / 8)) * 8, k);
   channel_reduce(
       C, r0, r1,
-      [&](int64_t off, float(&s0)[8], float(&s1)[8]) {
-        float v[8];
-        load8(x + off, v);
+      [&](int64_t off, int64_t step, auto u, float(&s0)[8], float(&s1)[8]) {
+        constexpr int U = decltype(u)::value;
+        bf16x8 raw[U];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float d = v[i] - k[i];
-          s0[i] += d;
-          s1[i] = fmaf(d, d, s1[i]);
-        }
+        for (int j = 0; j < U; ++j) raw[j] = *(const bf16x8*)(x + off + j * step);
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float d = (float)raw[j][i] - k[i];
+            s0[i] += d;
+            s1[i] = fmaf(d, d, s1[i]);
+          }
       },
       sum, sumsq);
 }
@@ -172,17 +188,24 @@ __global__ void __launch_bounds__(NT) bwd_reduce_kernel(const bf16* __restrict__
   }
   channel_reduce(
       C, r0, r1,
-      [&](int64_t off, float(&s0)[8], float(&s1)[8]) {
-        float g[8], xx[8];
-        load8(dy + off, g);
-        load8(x + off, xx);
-        const unsigned mk = RELU ? mask[off >> 3] : 0xffu;
+      [&](int64_t off, int64_t step, auto u, float(&s0)[8], float(&s1)[8]) {
+        constexpr int U = decltype(u)::value;
+        bf16x8 g[U], xx[U];
+        unsigned mk[U];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float dz = RELU ? ((mk >> i) & 1u ? g[i] : 0.f) : g[i];
-          s0[i] += dz;
-          s1[i] = fmaf(dz, (xx[i] - m[i]) * rs[i], s1[i]);
+        for (int j = 0; j < U; ++j) {
+          g[j] = *(const bf16x8*)(dy + off + j * step);
+          xx[j] = *(const bf16x8*)(x + off + j * step);
+          mk[j] = RELU ? mask[(off + j * step) >> 3] : 0xffu;
         }
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float dz = RELU ? ((mk[j] >> i) & 1u ? (float)g[j][i] : 0.f) : (float)g[j][i];
+            s0[i] += dz;
+            s1[i] = fmaf(dz, ((float)xx[j][i] - m[i]) * rs[i], s1[i]);
+          }
       },
       sdz, sdzx);
 }

@@ -73,7 +73,8 @@ class Bottleneck(nn.Module):
         # Identity shortcut: x feeds conv1 and the residual add, so autograd would sum the two
         # gradients of x in an elementwise pass; the shortcut's gradient goes to conv1's input-gradient
         # GEMM instead, which adds it as its C (beta = 1; ops/linear.py GradJoin)
-        join = GradJoin() if (self.down is None and torch.is_grad_enabled() and self.conv1.gemm_path(x)) else None
+        join = (GradJoin() if (self.down is None and config.get().resnet_join and torch.is_grad_enabled()
+                               and self.conv1.gemm_path(x)) else None)
         idt = x if self.down is None else bn_act(self.down[0](x), self.down[1], relu=False)
         y = bn_act(self.conv1(x, join=join), self.bn1)
         y = bn_act(self.conv2(y), self.bn2)
