@@ -112,7 +112,7 @@ def bench_y4m_job(args, dev):
     return {k.replace("job_", "job_y4m_"): v for k, v in rec.items() if k != "workers"}
 
 
-def bench_job(args, dev, plane="relay", source=None, out_ext=".npy"):
+def bench_job(args, dev, plane="relay", source=None, out_ext=None):
     """The whole volunteer job on one GPU: a requester and `workers` volunteers in this process.
     ``relay``: chunk bytes through the coordinator (reference topology); ``p2p``: metadata through
     the coordinator, chunk bytes over pair groups (gloo here: the volunteers share one GPU)."""
@@ -120,6 +120,7 @@ def bench_job(args, dev, plane="relay", source=None, out_ext=".npy"):
     from distributedvolunteercomputing_amd.control.peer import client
     from distributedvolunteercomputing_amd.jobs.video import DetectorEngine
 
+    out_ext = out_ext or "." + args.sink
     coord = coordinator("127.0.0.1", 0, ephemeral_ports=True, credits=2, data_plane=plane)
     eng = DetectorEngine(device=dev)  # one GPU: volunteers share one engine (serialised by a lock)
     shm = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
@@ -136,6 +137,10 @@ def bench_job(args, dev, plane="relay", source=None, out_ext=".npy"):
         n = req.sink.written if (t and req.sink is not None) else 0
         # host busy time per stage of each volunteer thread (where the job's wall time goes)
         spans = {"requester": req.hspans.snapshot()}
+        snap = req.metrics.snapshot()
+        reg = snap.get("latency_ms", {}).get("source_register_ms", {}).get("max")
+        if snap["counters"].get("source_register_failed"):
+            reg = "failed"
         for i, w in enumerate(workers):
             spans[f"worker{i}"] = w.hspans.snapshot()
     finally:
@@ -148,7 +153,7 @@ def bench_job(args, dev, plane="relay", source=None, out_ext=".npy"):
     pre = "job" if plane == "relay" else f"job_{plane}"
     return {f"{pre}_time_s": round(t, 3) if t else None, f"{pre}_frames": n,
             f"{pre}_frames_per_s": round(n / t, 1) if t else None, "workers": args.workers,
-            f"{pre}_host_spans": spans}
+            f"{pre}_sink": out_ext, f"{pre}_source_register_ms": reg, f"{pre}_host_spans": spans}
 
 
 def make_npy_source(args) -> str:
@@ -193,6 +198,9 @@ def main():
                          "interleaved: keys job[_p2p]_* (off) and job[_p2p]_pipe_* (on)")
     ap.add_argument("--data-plane", default="both", choices=["relay", "p2p", "both"])
     ap.add_argument("--y4m-frames", type=int, default=0, help="also run the job on a Y4M file of this many frames")
+    ap.add_argument("--sink", default="npy", choices=["npy", "y4m"],
+                    help="the requester's output file, written as the frames arrive and closed inside the "
+                         "job's time: npy (BGR frames) or y4m (4:4:4, converted per chunk)")
     ap.add_argument("--source", default="npy", choices=["npy", "synthetic"],
                     help="npy: frames pre-generated into a memory-mapped file (the job measures the framework); "
                          "synthetic: generated on the fly by the requester (bound by the generator)")

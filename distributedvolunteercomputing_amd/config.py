@@ -43,6 +43,9 @@ class RuntimeConfig:
     tunableop_file: str = ""  # VCX_TUNABLEOP_FILE: alternative TunableOp results file
     offload_arch: str = "gfx950"  # VCX_OFFLOAD_ARCH: target of the in-tree HIP build
     colour_native: bool = True  # VCX_COLOUR_NATIVE: video BGR<->YUV in the C++ runtime (False: numpy)
+    # VCX_REGISTER_SOURCE: a requester page-locks a memory-mapped source (hipHostRegister) and uploads
+    # chunks straight from it (False: each chunk is copied into pinned memory first)
+    register_source: bool = True
     resnet_conv1x1: str = "gemm"  # VCX_RESNET_CONV1X1: ResNet 1x1 convolutions as GEMMs on the NHWC view ("gemm")
     # or through the convolution library ("conv")
     # VCX_CONV_FIND: library (MIOpen) convolutions of the ResNets pick the fastest solver per shape by
@@ -93,6 +96,7 @@ _ENV = {
     "tunableop_file": ("VCX_TUNABLEOP_FILE", str),
     "offload_arch": ("VCX_OFFLOAD_ARCH", str),
     "colour_native": ("VCX_COLOUR_NATIVE", _bool),
+    "register_source": ("VCX_REGISTER_SOURCE", _bool),
     "gloo_host": ("VCX_GLOO_HOST", str),
     "p2p_backend": ("VCX_P2P_BACKEND", str),
     "elastic_debug": ("VCX_ELASTIC_DEBUG", _bool),

@@ -150,6 +150,8 @@ class client:  # noqa: N801 (reference class name)
         self.job_times: list[float] = []
 
         self._pins: dict = {}  # pinned staging of the requester's pre-resize (by role)
+        # memory-mapped sources page-locked in place (hipHostRegister): id -> (array, base address)
+        self._registered: dict = {}
         self._in_done = [None, None]  # per pinned input buffer: the upload that last read it
         self._in_ring = 0
         self._rs_stream = None  # the requester's resize stream (its own: not the workers' engines')
@@ -219,6 +221,7 @@ class client:  # noqa: N801 (reference class name)
         with self._p2p_lock:  # chunks of an earlier job that never came back are not needed any more
             self._outgoing.clear()
         src = open_source(path)
+        self._register_source(src)
         time.sleep(0.0 if path != "live" else 0.5)  # camera warm-up in the reference: 2 s
         out_path = self.path_out
 
@@ -275,6 +278,52 @@ class client:  # noqa: N801 (reference class name)
         if not self.sink.done.wait(timeout):
             return None
         return self.job_times[-1] if self.job_times else None
+
+    def _register_source(self, src):
+        """Page-lock a memory-mapped source where it lies (hipHostRegister, read-only), once per job:
+        each chunk's upload is then one async DMA straight out of the mapping. Without it every
+        100-frame 720p chunk (276 MB) was first copied into pinned memory on the requester's send
+        thread: 9.6-12.5 ms per chunk, the job's bound (profiles/r4_video_job_spans.txt).
+        Mappings of earlier jobs are released first (their uploads have finished: the resize stream
+        is synchronised). A failed registration leaves the copy path in place."""
+        self._unregister_sources()
+        a = getattr(src, "a", None)
+        if (self.resize_device is None or not self.preresize or not isinstance(a, np.memmap) or a.nbytes == 0
+                or not config.get().register_source):
+            return
+        from torch._C import _cudart
+
+        ptr = a.__array_interface__["data"][0]
+        base = ptr & ~4095  # the mapping starts on a page boundary at or before the array data
+        size = ((ptr + a.nbytes - base) + 4095) & ~4095
+        t0 = time.perf_counter()
+        err = int(_cudart.cudaHostRegister(base, size, 0x08))  # hipHostRegisterReadOnly
+        if err != 0:
+            self.metrics.incr("source_register_failed")
+            self.log(f"hipHostRegister of the source mapping failed ({err}): chunks are copied")
+            return
+        self._registered[id(a)] = (a, base)
+        self.metrics.observe("source_register_ms", (time.perf_counter() - t0) * 1e3)
+
+    def _unregister_sources(self):
+        if not self._registered:
+            return
+        from torch._C import _cudart
+
+        if self._rs_stream is not None:
+            self._rs_stream.synchronize()
+        for a, base in self._registered.values():
+            _cudart.cudaHostUnregister(base)
+        self._registered.clear()
+
+    def _registered_block(self, frames):
+        """True when `frames` is a view of a page-locked source mapping."""
+        if not self._registered or not isinstance(frames, np.ndarray):
+            return False
+        b = frames
+        while isinstance(b.base, np.ndarray):
+            b = b.base
+        return any(b is a for a, _ in self._registered.values()) and frames.flags.c_contiguous
 
     # ------------------------------------------------------------------ send (chunk packing)
     def send_image_thread(self):
@@ -343,7 +392,8 @@ class client:  # noqa: N801 (reference class name)
             held = chunk if isinstance(chunk, torch.Tensor) else _host_tensor(chunk)
             if held.device.type == "cpu" and self._pins and any(
                     held.data_ptr() == b.data_ptr() for b in self._pins.values()):
-                held = held.clone()  # a pinned ring buffer: the next chunks reuse it
+                held = held.clone()  # a pinned ring buffer: the next chunks reuse it (the p2p
+                # path of _resize_chunk lands each chunk in a buffer of its own instead)
             with self._p2p_lock:
                 self._outgoing[key] = held
             ok = self.sender.send_image(info, _EMPTY, p2p=1, key=key, cshape=list(held.shape))
@@ -368,29 +418,40 @@ class client:  # noqa: N801 (reference class name)
         dev = self.resize_device
         if self._rs_stream is None:
             self._rs_stream = torch.cuda.Stream(dev)
-        # two pinned input buffers: this chunk's copy overlaps the previous chunk's upload + resize
-        i = self._in_ring = (self._in_ring + 1) % 2
-        if self._in_done[i] is not None:
-            self._in_done[i].synchronize()  # the upload that last read this buffer has finished
-        pin = self._pinned(f"in{i}", (len(frames),) + tuple(frames[0].shape))
-        if isinstance(frames, np.ndarray):  # one block (e.g. a memory-mapped chunk): one threaded copy
-            pin.copy_(_host_tensor(frames))
+        if self._registered_block(frames):  # page-locked mapping: DMA straight from the source
+            with torch.cuda.stream(self._rs_stream):
+                x = torch.empty(frames.shape, dtype=torch.uint8, device=dev)
+                x.copy_(_host_tensor(frames), non_blocking=True)
         else:
-            for j, f in enumerate(frames):
-                pin[j].copy_(torch.from_numpy(f))
+            # two pinned input buffers: this chunk's copy overlaps the previous chunk's upload + resize
+            i = self._in_ring = (self._in_ring + 1) % 2
+            if self._in_done[i] is not None:
+                self._in_done[i].synchronize()  # the upload that last read this buffer has finished
+            pin = self._pinned(f"in{i}", (len(frames),) + tuple(frames[0].shape))
+            if isinstance(frames, np.ndarray):  # one block (e.g. a memory-mapped chunk): one threaded copy
+                pin.copy_(_host_tensor(frames))
+            else:
+                for j, f in enumerate(frames):
+                    pin[j].copy_(torch.from_numpy(f))
+            with torch.cuda.stream(self._rs_stream):
+                x = pin.to(dev, non_blocking=True)
+                up = torch.cuda.Event()
+                up.record(self._rs_stream)
+                self._in_done[i] = up
         with torch.cuda.stream(self._rs_stream):
-            x = pin.to(dev, non_blocking=True)
-            up = torch.cuda.Event()
-            up.record(self._rs_stream)
-            self._in_done[i] = up
             small = V.resize_width(x, 400)
             if self.plane is not None and self.plane.device.type == "cuda":
                 done = torch.cuda.Event()
                 done.record(self._rs_stream)
                 return _Landing(small, done)  # an RCCL pair plane sends it from device memory
-            # 4 result buffers: one being sent, two queued for the wire (wire_q), one being filled
-            self._out_ring = (self._out_ring + 1) % 4
-            po = self._pinned(f"out{self._out_ring}", tuple(small.shape))
+            if self.plane is not None:
+                # a host pair plane holds the chunk until its result is back: a pinned buffer of its
+                # own (torch's caching host allocator recycles them), no clone in _ship
+                po = torch.empty(tuple(small.shape), dtype=torch.uint8, pin_memory=True)
+            else:
+                # 4 result buffers: one being sent, two queued for the wire (wire_q), one being filled
+                self._out_ring = (self._out_ring + 1) % 4
+                po = self._pinned(f"out{self._out_ring}", tuple(small.shape))
             po.copy_(small, non_blocking=True)
             done = torch.cuda.Event()
             done.record(self._rs_stream)
@@ -610,6 +671,7 @@ class client:  # noqa: N801 (reference class name)
             self.plane.close()
         if self.sink is not None:
             self.sink.close()
+        self._unregister_sources()
 
 
 Client = client

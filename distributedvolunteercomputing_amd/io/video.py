@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import functools
 import os
+import struct
 from pathlib import Path
 
 import numpy as np
@@ -328,23 +329,42 @@ class Y4MWriter:
 
 
 class NpyWriter:
+    """uint8 [N, H, W, 3] .npy written as the frames arrive (one write per received chunk, no
+    copy held in memory): the header is written first with room for any frame count and rewritten
+    with the final count by release()."""
+
+    HEADER = 256  # bytes (a multiple of 64, as the format wants)
+
     def __init__(self, path, width, height, fps=30):
-        self.path, self.frames_list = str(path), []
+        self.path, self.w, self.h = str(path), int(width), int(height)
+        self.f = open(self.path, "wb")
         self.frames = 0
+        self.f.write(self._header(0))
+
+    def _header(self, n):
+        d = "{'descr': '|u1', 'fortran_order': False, 'shape': (%d, %d, %d, 3), }" % (n, self.h, self.w)
+        body = d.ljust(self.HEADER - 11) + "\n"
+        return b"\x93NUMPY\x01\x00" + struct.pack("<H", len(body)) + body.encode("latin1")
+
+    def _put(self, block):
+        if block.shape[1:] != (self.h, self.w, 3) or block.dtype != np.uint8:
+            raise ValueError(f"frames {block.dtype} {block.shape[1:]} do not match writer {self.h}x{self.w}")
+        self.f.write(memoryview(np.ascontiguousarray(block)).cast("B"))
+        self.frames += len(block)
 
     def write(self, frame):
-        self.frames_list.append(np.array(frame, copy=True)[None])
-        self.frames += 1
+        self._put(np.asarray(frame)[None])
 
     def write_many(self, frames):
-        """A received chunk's frames: one block copy (consecutive views of the chunk buffer) or a stack."""
-        self.frames_list.append(np.array(_as_block(frames), copy=True))
-        self.frames += len(frames)
+        """A received chunk's frames: written straight from the chunk buffer when they are its
+        consecutive views (else one stacked copy)."""
+        self._put(_as_block(frames))
 
     def release(self):
-        if self.frames_list is not None:
-            np.save(self.path, np.concatenate(self.frames_list) if self.frames_list else np.zeros((0, 0, 0, 3), np.uint8))
-            self.frames_list = None
+        if self.f and not self.f.closed:
+            self.f.seek(0)
+            self.f.write(self._header(self.frames))
+            self.f.close()
 
 
 class PngDirWriter:

@@ -305,9 +305,9 @@ class OrderedSink:
 
     def _check_done(self):
         if self.final is not None and self.index.next_expected > self.final and not self.done.is_set():
-            self.t_done = time.time()
             if self.writer is not None:
-                self.writer.release()
+                self.writer.release()  # the output file is complete inside the job's time
+            self.t_done = time.time()
             self.done.set()
             if self.on_done is not None:
                 self.on_done(self)

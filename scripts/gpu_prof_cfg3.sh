@@ -9,5 +9,5 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$O/trace" -o run -- \
     python3 "$R/bench_configs.py" --configs 3 --steps 3 > "$O/run.log" 2>&1 || exit $?
 f=$(find "$O/trace" -name "*kernel_trace.csv" | head -1)
-python3 "$R/scripts/prof_categories.py" "$f" 30 > "$O/categories.txt" || exit $?
+python3 "$R/scripts/prof_categories.py" "$f" 80 > "$O/categories.txt" || exit $?
 rm -f "$f"
