@@ -54,6 +54,9 @@ class RuntimeConfig:
     conv_find: bool = True
     resnet_bn: str = "fused"  # VCX_RESNET_BN: ResNet train-mode BatchNorm (+ add) + ReLU as fused HIP passes ("fused")
     # or the torch composition ("torch")
+    # VCX_BN_LAYER_WS: each BatchNorm module keeps its own [4C] workspace so the finalize of its
+    # statistics runs inside the apply / dx passes (2 launches per layer and direction instead of 3)
+    bn_layer_ws: bool = True
     resnet_join: bool = True  # VCX_RESNET_JOIN: identity-shortcut gradient added in conv1's dgrad GEMM (GradJoin)
     # ---- distributed / control plane
     gloo_host: str = "127.0.0.1"  # VCX_GLOO_HOST: interface gloo peer groups bind to
@@ -85,6 +88,7 @@ _ENV = {
     "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
     "resnet_bn": ("VCX_RESNET_BN", str),
     "resnet_join": ("VCX_RESNET_JOIN", _bool),
+    "bn_layer_ws": ("VCX_BN_LAYER_WS", _bool),
     "conv_find": ("VCX_CONV_FIND", _bool),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),
     "gemm_select": ("VCX_GEMM_SELECT", _bool),

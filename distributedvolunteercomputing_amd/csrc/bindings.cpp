@@ -217,9 +217,20 @@ static float* bn_workspace(const at::Tensor& x, int64_t C) {
 // (int64, incremented on the device) or None. Returns y, mean, rstd, scale (fp32 [C]) and, with the ReLU,
 // its mask as one bit per element (uint8 [R, C / 8]: bit i of byte e = element 8 e + i is > 0), which
 // the backward reads instead of y; undefined without the ReLU.
+// layer_ws: the layer's own fp32 [4C] workspace [fwd sums | bwd sums] instead of the shared one; its
+// forward half must be zero on entry (the caller's bookkeeping: ops/batchnorm.py) and the backward
+// half is zeroed by this call (finalize inside the apply pass, batchnorm.hip apply_kernel FIN)
+static float* check_layer_ws(const c10::optional<at::Tensor>& lws, const at::Tensor& x, int64_t C) {
+  if (!lws || !lws->defined()) return nullptr;
+  TORCH_CHECK(lws->is_cuda() && lws->get_device() == x.get_device() && lws->scalar_type() == at::kFloat &&
+                  lws->is_contiguous() && lws->numel() == 4 * C, "bn: layer workspace fp32 [4C] on x's device");
+  return lws->data_ptr<float>();
+}
+
 std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma, at::Tensor beta,
                                      c10::optional<at::Tensor> run_mean, c10::optional<at::Tensor> run_var, double eps,
-                                     double momentum, bool relu, c10::optional<at::Tensor> nbt) {
+                                     double momentum, bool relu, c10::optional<at::Tensor> nbt,
+                                     c10::optional<at::Tensor> layer_ws) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == at::kBFloat16, "bn: x bf16 contiguous NHWC");
   const int64_t C = x.size(-1), R = x.numel() / C;
   TORCH_CHECK(vcx_bn_supported((int)C) && R > 0, "bn: C must be a power of two in 8..2048");
@@ -246,10 +257,11 @@ std::vector<at::Tensor> bn_fwd_train(at::Tensor x, c10::optional<at::Tensor> res
   at::Tensor st = at::empty({4, C}, f);
   at::Tensor y = at::empty_like(x);
   at::Tensor mask = relu ? at::empty({R, C / 8}, x.options().dtype(at::kByte)) : at::Tensor();
+  float* lws = check_layer_ws(layer_ws, x, C);
   vcx_bn_fwd_train(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), relu ? mask.data_ptr() : nullptr, R,
                    (int)C, gamma.data_ptr(), beta.data_ptr(), rm, rv, fp32, (float)eps, (float)momentum,
-                   bn_workspace(x, C), st[0].data_ptr<float>(), st[1].data_ptr<float>(), st[2].data_ptr<float>(),
-                   st[3].data_ptr<float>(), nb, relu ? 1 : 0, cur_stream());
+                   lws ? lws : bn_workspace(x, C), st[0].data_ptr<float>(), st[1].data_ptr<float>(),
+                   st[2].data_ptr<float>(), st[3].data_ptr<float>(), nb, relu ? 1 : 0, lws ? 1 : 0, cur_stream());
   return {y, st[0], st[1], st[2], mask};
 }
 
@@ -295,10 +307,11 @@ at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor scal
 
 // returns dx, d residual (undefined unless want_dres), dgamma, dbeta (fp32 [C])
 // gw / gb: flat bf16 [C] gradient buffers of gamma / beta that dgamma / dbeta are ADDED into (both or
-// neither); the returned dgamma / dbeta are then for information only
+// neither); the returned dgamma / dbeta are then for information only. layer_ws: the forward's layer
+// workspace (its backward half zero on entry; its forward half is zeroed by this call)
 std::vector<at::Tensor> bn_bwd(at::Tensor dy, c10::optional<at::Tensor> mask, at::Tensor x, at::Tensor mean, at::Tensor rstd,
                                at::Tensor scale, bool relu, bool want_dres, c10::optional<at::Tensor> gw,
-                               c10::optional<at::Tensor> gb) {
+                               c10::optional<at::Tensor> gb, c10::optional<at::Tensor> layer_ws) {
   TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes() &&
                   dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "bn_bwd: dy, x bf16 NHWC alike");
   const int64_t C = x.size(-1), R = x.numel() / C;
@@ -318,10 +331,11 @@ std::vector<at::Tensor> bn_bwd(at::Tensor dy, c10::optional<at::Tensor> mask, at
   at::Tensor sums = at::empty({2 * C}, x.options().dtype(at::kFloat));
   at::Tensor dx = at::empty_like(x);
   at::Tensor dres = want_dres ? at::empty_like(x) : at::Tensor();
+  float* lws = check_layer_ws(layer_ws, x, C);
   vcx_bn_bwd(dy.data_ptr(), relu ? mask->data_ptr() : nullptr, x.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-             scale.data_ptr<float>(), R, (int)C, bn_workspace(x, C), sums.data_ptr<float>(),
+             scale.data_ptr<float>(), R, (int)C, lws ? lws : bn_workspace(x, C), sums.data_ptr<float>(),
              flat ? gw->data_ptr() : nullptr, flat ? gb->data_ptr() : nullptr, dx.data_ptr(),
-             want_dres ? dres.data_ptr() : nullptr, relu ? 1 : 0, cur_stream());
+             want_dres ? dres.data_ptr() : nullptr, relu ? 1 : 0, lws ? 1 : 0, cur_stream());
   return {dx, dres, sums.narrow(0, C, C), sums.narrow(0, 0, C)};
 }
 
@@ -810,12 +824,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_supported", [](int64_t C) { return vcx_bn_supported((int)C); });
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
         py::arg("run_mean"), py::arg("run_var"), py::arg("eps"), py::arg("momentum"), py::arg("relu"),
-        py::arg("nbt") = py::none());
+        py::arg("nbt") = py::none(), py::arg("layer_ws") = py::none());
   m.def("bn_apply", &bn_apply);
   m.def("maxpool3s2_fwd", &maxpool3s2_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("mean"), py::arg("rstd"), py::arg("scale"),
-        py::arg("relu"), py::arg("want_dres"), py::arg("gw") = py::none(), py::arg("gb") = py::none());
+        py::arg("relu"), py::arg("want_dres"), py::arg("gw") = py::none(), py::arg("gb") = py::none(),
+        py::arg("layer_ws") = py::none());
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0);
   m.def("gemm_wg_supported", &gemm_wg_supported, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits") = 0);

@@ -135,20 +135,82 @@ __global__ void finalize_kernel(float* __restrict__ ws, const bf16* __restrict__
   }
 }
 
+// the finalize of ONE channel from the raw pivot-shifted sums (see finalize_kernel)
+struct ChanStats {
+  float m, var, rs;
+};
+__device__ __forceinline__ ChanStats chan_stats(float s1, float s2, float pivot, float inv, float eps) {
+  const float d = s1 * inv;
+  const float var = fmaxf(s2 * inv - d * d, 0.f);
+  return {pivot + d, var, rsqrtf(var + eps)};
+}
+
+// Per-layer workspace mode (FIN): the finalize runs inside the apply pass. Every thread derives the
+// scale / shift of its 8 channels from the raw sums of the stats pass (ws[0, 2C)); block 0 also writes
+// mean / 1/std / scale for the backward, the running stats and num_batches_tracked, and zeroes the
+// layer's BACKWARD sums ws[2C, 4C) (their last reader, the previous step's dx pass, has finished; their
+// next writer is this step's backward reduction). The forward sums are zeroed by the dx pass. One
+// launch fewer per layer and direction (53 + 53 finalize launches of ~5 us in a ResNet-50 step).
+struct FinArgs {
+  float* ws;  // the layer's [fwd sum | fwd sumsq | bwd sum | bwd sumsq], fp32 [4C]
+  const bf16 *gamma, *beta;
+  void *run_mean, *run_var;
+  int run_fp32;
+  float eps, momentum, inv;
+  int64_t R;
+  float *mean, *rstd, *scale;
+  int64_t* nbt;
+};
+
 // grid-stride loops whose stride (grid x 256 chunks) is a multiple of C / 8 (host check: C divides
 // 2048): every thread keeps the same 8 channels, so their constants load once
-template <bool RES, bool RELU>
+template <bool RES, bool RELU, bool FIN>
 __global__ void __launch_bounds__(NT) apply_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
                                                    const float* __restrict__ scale, const float* __restrict__ shift,
                                                    bf16* __restrict__ y, unsigned char* __restrict__ mask, int64_t n8,
-                                                   int cpr) {
+                                                   int cpr, FinArgs fa) {
   int64_t e = blockIdx.x * (int64_t)NT + threadIdx.x;
   const int c0 = (int)(e % cpr) * 8;
   float sc[8], sh[8];
+  if constexpr (FIN) {
+    const int C = cpr * 8;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    sc[i] = scale[c0 + i];
-    sh[i] = shift[c0 + i];
+    for (int i = 0; i < 8; ++i) {
+      const ChanStats st = chan_stats(fa.ws[c0 + i], fa.ws[C + c0 + i], (float)x[c0 + i], fa.inv, fa.eps);
+      sc[i] = (float)fa.gamma[c0 + i] * st.rs;
+      sh[i] = (float)fa.beta[c0 + i] - st.m * sc[i];
+    }
+    if (blockIdx.x == 0) {
+      if (threadIdx.x == 0 && fa.nbt) *fa.nbt += 1;
+      for (int c = threadIdx.x; c < C; c += NT) {
+        const ChanStats st = chan_stats(fa.ws[c], fa.ws[C + c], (float)x[c], fa.inv, fa.eps);
+        fa.mean[c] = st.m;
+        fa.rstd[c] = st.rs;
+        fa.scale[c] = (float)fa.gamma[c] * st.rs;
+        fa.ws[2 * C + c] = 0.f;
+        fa.ws[3 * C + c] = 0.f;
+        if (fa.run_mean) {
+          const float unb = fa.R > 1 ? st.var * (float)fa.R / (float)(fa.R - 1) : st.var, mo = fa.momentum;
+          if (fa.run_fp32) {
+            float* rm = (float*)fa.run_mean;
+            float* rv = (float*)fa.run_var;
+            rm[c] = (1.f - mo) * rm[c] + mo * st.m;
+            rv[c] = (1.f - mo) * rv[c] + mo * unb;
+          } else {
+            bf16* rm = (bf16*)fa.run_mean;
+            bf16* rv = (bf16*)fa.run_var;
+            rm[c] = (bf16)((1.f - mo) * (float)rm[c] + mo * st.m);
+            rv[c] = (bf16)((1.f - mo) * (float)rv[c] + mo * unb);
+          }
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sc[i] = scale[c0 + i];
+      sh[i] = shift[c0 + i];
+    }
   }
   for (; e < n8; e += (int64_t)gridDim.x * NT) {
     float v[8], r[8];
@@ -225,16 +287,32 @@ __global__ void bwd_finalize_kernel(float* __restrict__ ws, int C, float* __rest
   if (gw) gw[c] = (bf16)((float)gw[c] + dg);
 }
 
-// dx = gamma rstd (dz - (sum dz + xhat sum dz xhat) / R); d residual = dz
-template <bool RES, bool RELU>
+// dx = gamma rstd (dz - (sum dz + xhat sum dz xhat) / R); d residual = dz.
+// FIN (per-layer workspace): sdz / sdzx are the layer's raw backward sums ws[2C, 4C) (no bwd_finalize
+// launch); block 0 writes them to `sums`, adds dbeta / dgamma into gb / gw, and zeroes the layer's
+// FORWARD sums ws[0, 2C) (last read by this step's apply pass; next written by the next forward)
+template <bool RES, bool RELU, bool FIN>
 __global__ void __launch_bounds__(NT) bwd_dx_kernel(const bf16* __restrict__ dy, const unsigned char* __restrict__ mask,
                                                     const bf16* __restrict__ x, const float* __restrict__ mean,
                                                     const float* __restrict__ rstd, const float* __restrict__ scale,
                                                     const float* __restrict__ sdz, const float* __restrict__ sdzx,
                                                     bf16* __restrict__ dx, bf16* __restrict__ dres, int64_t n8, int cpr,
-                                                    float invR) {
+                                                    float invR, float* __restrict__ fin_ws, float* __restrict__ sums,
+                                                    bf16* __restrict__ gw, bf16* __restrict__ gb) {
   int64_t e = blockIdx.x * (int64_t)NT + threadIdx.x;
   const int c0 = (int)(e % cpr) * 8;
+  if (FIN && blockIdx.x == 0) {
+    const int C = cpr * 8;
+    for (int c = threadIdx.x; c < C; c += NT) {
+      const float db = sdz[c], dg = sdzx[c];
+      sums[c] = db;
+      sums[C + c] = dg;
+      if (gb) gb[c] = (bf16)((float)gb[c] + db);
+      if (gw) gw[c] = (bf16)((float)gw[c] + dg);
+      fin_ws[c] = 0.f;
+      fin_ws[C + c] = 0.f;
+    }
+  }
   float sc[8], m[8], rs[8], u[8], w[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -374,30 +452,46 @@ using namespace vcx;
 bool vcx_bn_supported(int C) { return C >= 8 && C <= 2048 && (2048 % C) == 0; }
 
 // forward (train): ws = the zero-at-rest workspace, fp32 [2C] (zeroed once by the caller, left zeroed
-// by every call); mean/rstd/scale/shift fp32 [C]; nbt int64 [1] or null
+// by every call); mean/rstd/scale/shift fp32 [C]; nbt int64 [1] or null.
+// layer_ws: ws is instead the LAYER's own fp32 [4C] workspace (forward sums zero on entry, see
+// apply_kernel FIN): no finalize launch, and the layer's backward sums are zeroed by the apply pass
 void vcx_bn_fwd_train(const void* x, const void* res, void* y, void* mask, int64_t R, int C, const void* gamma,
                       const void* beta, void* run_mean, void* run_var, int run_fp32, float eps, float momentum, float* ws,
-                      float* mean, float* rstd, float* scale, float* shift, int64_t* nbt, int relu, hipStream_t s) {
+                      float* mean, float* rstd, float* scale, float* shift, int64_t* nbt, int relu, int layer_ws,
+                      hipStream_t s) {
   using namespace bn;
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
   hipLaunchKernelGGL(stats_kernel, dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
-  if (run_fp32)
-    hipLaunchKernelGGL(finalize_kernel<float>, dim3((C + 255) / 256), dim3(256), 0, s, ws, (const bf16*)x, R, C, (const bf16*)gamma,
-                       (const bf16*)beta, eps, momentum, (float*)run_mean, (float*)run_var, mean, rstd, scale, shift, nbt);
-  else
-    hipLaunchKernelGGL(finalize_kernel<bf16>, dim3((C + 255) / 256), dim3(256), 0, s, ws, (const bf16*)x, R, C, (const bf16*)gamma,
-                       (const bf16*)beta, eps, momentum, (bf16*)run_mean, (bf16*)run_var, mean, rstd, scale, shift, nbt);
+  FinArgs fa{ws, (const bf16*)gamma, (const bf16*)beta, run_mean, run_var, run_fp32, eps, momentum, 1.f / (float)R, R,
+             mean, rstd, scale, nbt};
+  if (!layer_ws) {
+    if (run_fp32)
+      hipLaunchKernelGGL(finalize_kernel<float>, dim3((C + 255) / 256), dim3(256), 0, s, ws, (const bf16*)x, R, C,
+                         (const bf16*)gamma, (const bf16*)beta, eps, momentum, (float*)run_mean, (float*)run_var, mean,
+                         rstd, scale, shift, nbt);
+    else
+      hipLaunchKernelGGL(finalize_kernel<bf16>, dim3((C + 255) / 256), dim3(256), 0, s, ws, (const bf16*)x, R, C,
+                         (const bf16*)gamma, (const bf16*)beta, eps, momentum, (bf16*)run_mean, (bf16*)run_var, mean,
+                         rstd, scale, shift, nbt);
+  }
   const int64_t n8 = R * C / 8;
   const int g = grid_for(n8);
   auto go = [&](auto k) {
     hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)x, (const bf16*)res, scale, shift, (bf16*)y,
-                       (unsigned char*)mask, n8, C / 8);
+                       (unsigned char*)mask, n8, C / 8, fa);
   };
-  if (res)
-    relu ? go(apply_kernel<true, true>) : go(apply_kernel<true, false>);
-  else
-    relu ? go(apply_kernel<false, true>) : go(apply_kernel<false, false>);
+  if (layer_ws) {
+    if (res)
+      relu ? go(apply_kernel<true, true, true>) : go(apply_kernel<true, false, true>);
+    else
+      relu ? go(apply_kernel<false, true, true>) : go(apply_kernel<false, false, true>);
+  } else {
+    if (res)
+      relu ? go(apply_kernel<true, true, false>) : go(apply_kernel<true, false, false>);
+    else
+      relu ? go(apply_kernel<false, true, false>) : go(apply_kernel<false, false, false>);
+  }
 }
 
 // y = act(x * scale + shift [+ res]) with given per-channel scale/shift (eval mode)
@@ -406,42 +500,54 @@ void vcx_bn_apply(const void* x, const void* res, void* y, int64_t R, int C, con
   using namespace bn;
   const int64_t n8 = R * C / 8;
   const int g = grid_for(n8);
+  const FinArgs fa{};
   auto go = [&](auto k) {
     hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)x, (const bf16*)res, scale, shift, (bf16*)y,
-                       (unsigned char*)nullptr, n8, C / 8);
+                       (unsigned char*)nullptr, n8, C / 8, fa);
   };
   if (res)
-    relu ? go(apply_kernel<true, true>) : go(apply_kernel<true, false>);
+    relu ? go(apply_kernel<true, true, false>) : go(apply_kernel<true, false, false>);
   else
-    relu ? go(apply_kernel<false, true>) : go(apply_kernel<false, false>);
+    relu ? go(apply_kernel<false, true, false>) : go(apply_kernel<false, false, false>);
 }
 
 // backward: ws = the zero-at-rest workspace (as in the forward); sums = fp32 [2C] output [sum dz |
 // sum dz xhat] = [dbeta | dgamma]; gw / gb = flat bf16 gradients of gamma / beta that dgamma / dbeta
-// are added into (or null)
+// are added into (or null). layer_ws: ws is the layer's fp32 [4C] workspace (backward sums zero on
+// entry): the reduction accumulates into ws[2C, 4C), the dx pass finalizes them and zeroes ws[0, 2C)
 void vcx_bn_bwd(const void* dy, const void* mask, const void* x, const float* mean, const float* rstd, const float* scale,
-                int64_t R, int C, float* ws, float* sums, void* gw, void* gb, void* dx, void* dres, int relu,
+                int64_t R, int C, float* ws, float* sums, void* gw, void* gb, void* dx, void* dres, int relu, int layer_ws,
                 hipStream_t s) {
   using namespace bn;
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
+  float* bws = layer_ws ? ws + 2 * C : ws;
   if (relu)
     hipLaunchKernelGGL(bwd_reduce_kernel<true>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const unsigned char*)mask,
-                       (const bf16*)x, mean, rstd, R, C, rpb, ws, ws + C);
+                       (const bf16*)x, mean, rstd, R, C, rpb, bws, bws + C);
   else
     hipLaunchKernelGGL(bwd_reduce_kernel<false>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const unsigned char*)mask,
-                       (const bf16*)x, mean, rstd, R, C, rpb, ws, ws + C);
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, C, sums, (bf16*)gw, (bf16*)gb);
+                       (const bf16*)x, mean, rstd, R, C, rpb, bws, bws + C);
+  if (!layer_ws)
+    hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, C, sums, (bf16*)gw, (bf16*)gb);
+  const float* sdz = layer_ws ? bws : sums;
   const int64_t n8 = R * C / 8;
   const int g = grid_for(n8);
   auto go = [&](auto k) {
     hipLaunchKernelGGL(k, dim3(g), dim3(NT), 0, s, (const bf16*)dy, (const unsigned char*)mask, (const bf16*)x, mean, rstd, scale,
-                       (const float*)sums, (const float*)(sums + C), (bf16*)dx, (bf16*)dres, n8, C / 8, 1.f / (float)R);
+                       sdz, sdz + C, (bf16*)dx, (bf16*)dres, n8, C / 8, 1.f / (float)R, ws, sums, (bf16*)gw, (bf16*)gb);
   };
-  if (dres)
-    relu ? go(bwd_dx_kernel<true, true>) : go(bwd_dx_kernel<true, false>);
-  else
-    relu ? go(bwd_dx_kernel<false, true>) : go(bwd_dx_kernel<false, false>);
+  if (layer_ws) {
+    if (dres)
+      relu ? go(bwd_dx_kernel<true, true, true>) : go(bwd_dx_kernel<true, false, true>);
+    else
+      relu ? go(bwd_dx_kernel<false, true, true>) : go(bwd_dx_kernel<false, false, true>);
+  } else {
+    if (dres)
+      relu ? go(bwd_dx_kernel<true, true, false>) : go(bwd_dx_kernel<true, false, false>);
+    else
+      relu ? go(bwd_dx_kernel<false, true, false>) : go(bwd_dx_kernel<false, false, false>);
+  }
 }
 
 // stem max-pool 3x3 / stride 2 / pad 1, NHWC bf16 (C % 8 == 0): y, idx [N, OH, OW, C]

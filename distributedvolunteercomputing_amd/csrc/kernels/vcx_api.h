@@ -99,7 +99,8 @@ void vcx_embed_bwd(const int64_t* idx, const void* dx, float* dwte_scratch, void
 bool vcx_bn_supported(int C);
 void vcx_bn_fwd_train(const void* x, const void* res, void* y, void* mask, int64_t R, int C, const void* gamma,
                       const void* beta, void* run_mean, void* run_var, int run_fp32, float eps, float momentum, float* ws,
-                      float* mean, float* rstd, float* scale, float* shift, int64_t* nbt, int relu, hipStream_t s);
+                      float* mean, float* rstd, float* scale, float* shift, int64_t* nbt, int relu, int layer_ws,
+                      hipStream_t s);
 void vcx_maxpool3s2_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int OH, int OW, hipStream_t s);
 void vcx_maxpool3s2_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C, int OH, int OW,
                         hipStream_t s);
@@ -107,4 +108,4 @@ void vcx_bn_apply(const void* x, const void* res, void* y, int64_t R, int C, con
                   int relu, hipStream_t s);
 void vcx_bn_bwd(const void* dy, const void* mask, const void* x, const float* mean, const float* rstd, const float* scale,
                 int64_t R, int C, float* ws, float* sums, void* gw, void* gb, void* dx, void* dres, int relu,
-                hipStream_t s);
+                int layer_ws, hipStream_t s);

@@ -2,7 +2,9 @@
 channels-last bf16 activations (csrc/kernels/batchnorm.hip): y = relu(bn(x) [+ residual]).
 
 Forward: one statistics pass (read x), a per-channel finalize (running stats updated in place),
-one apply pass (read x [+ residual], write y). Backward: one reduction pass (read dy, y, x) and
+one apply pass (read x [+ residual], write y). With a per-layer workspace (_LayerWS, the default for
+modules) the finalize runs inside the apply pass and the backward's inside its dx pass: two launches
+per layer and direction instead of three. Backward: one reduction pass (read dy, y, x) and
 one input-gradient pass (read dy, mask, x; write dx [and d residual]): the ReLU mask is one bit per
 element written by the forward's apply pass (1/16 of the bytes of y, which the backward used to read),
 so neither the pre-activation nor y is kept for the backward. On CPU, in fp32 or for unsupported channel counts the
@@ -21,17 +23,56 @@ def _nhwc(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1)  # a contiguous [N, H, W, C] view of channels-last storage
 
 
+class _LayerWS:
+    """A BatchNorm module's own fp32 [4C] workspace [forward sums | backward sums] and which halves are
+    known to be zero on the device. The kernels keep them zero in steady state: the forward's apply pass
+    zeroes the backward half and the backward's dx pass the forward half (batchnorm.hip, FIN). Calls out
+    of that order -- a forward whose backward never ran, two forwards before their backwards, a second
+    backward through a retained graph -- find a half not known to be zero and clear it first (one fill).
+    The halves' states follow the launch order on one stream, which a hipGraph capture of a whole
+    forward + backward step preserves (the same state before and after the captured step)."""
+
+    __slots__ = ("t", "f_clean", "b_clean")
+
+    def __init__(self, C, device):
+        self.t = torch.zeros(4 * C, dtype=torch.float32, device=device)
+        self.f_clean = True
+        self.b_clean = True
+
+    def before_forward(self):
+        if not self.f_clean:
+            self.t[: self.t.numel() // 2].zero_()
+        self.f_clean, self.b_clean = False, True  # the apply pass zeroes the backward half
+
+    def before_backward(self):
+        if not self.b_clean:
+            self.t[self.t.numel() // 2:].zero_()
+        self.b_clean, self.f_clean = False, True  # the dx pass zeroes the forward half
+
+
+def _layer_ws(bn: torch.nn.Module, x: torch.Tensor) -> _LayerWS:
+    ws = getattr(bn, "_vcx_ws", None)
+    if ws is None or ws.t.device != x.device or ws.t.numel() != 4 * x.shape[1]:
+        ws = _LayerWS(x.shape[1], x.device)
+        object.__setattr__(bn, "_vcx_ws", ws)  # not a parameter / buffer: no state_dict entry
+    return ws
+
+
 class _BNAct(torch.autograd.Function):
     """The statistics kernel finalizes in its last block (running stats, num_batches_tracked); with
     preset flat .grad buffers the backward reduction ADDS dgamma / dbeta into them and autograd gets
     None for gamma / beta (no cast or accumulation kernels per layer)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, run_mean, run_var, eps, momentum, relu, nbt):
+    def forward(ctx, x, weight, bias, residual, run_mean, run_var, eps, momentum, relu, nbt, lws=None):
         C = native()
         xh = _nhwc(x)
         rh = _nhwc(residual) if residual is not None else None
-        y, mean, rstd, scale, mask = C.bn_fwd_train(xh, rh, weight, bias, run_mean, run_var, eps, momentum, relu, nbt)
+        if lws is not None:
+            lws.before_forward()
+        y, mean, rstd, scale, mask = C.bn_fwd_train(xh, rh, weight, bias, run_mean, run_var, eps, momentum, relu, nbt,
+                                                    lws.t if lws is not None else None)
+        ctx.lws = lws
         ctx.save_for_backward(xh, mask if relu else None, mean, rstd, scale)
         ctx.relu, ctx.has_res, ctx.pdtype = relu, residual is not None, weight.dtype
         ctx.params = (weight, bias)
@@ -48,15 +89,19 @@ class _BNAct(torch.autograd.Function):
         gw = grad_buffer(weight) if ctx.needs_input_grad[1] else None
         gb = grad_buffer(bias) if ctx.needs_input_grad[2] else None
         flat = gw is not None and gb is not None
+        lws = ctx.lws
+        if lws is not None:
+            lws.before_backward()
         dx, dres, dgamma, dbeta = native().bn_bwd(dyh, mask, xh, mean, rstd, scale, ctx.relu, ctx.has_res,
-                                                  gw if flat else None, gb if flat else None)
+                                                  gw if flat else None, gb if flat else None,
+                                                  lws.t if lws is not None else None)
         dx = dx.permute(0, 3, 1, 2)
         dres = dres.permute(0, 3, 1, 2) if ctx.has_res else None
         if flat:  # already added into the flat .grad buffers
-            return dx, None, None, dres, None, None, None, None, None, None
+            return dx, None, None, dres, None, None, None, None, None, None, None
         dg = dgamma.to(ctx.pdtype) if ctx.needs_input_grad[1] else None
         db = dbeta.to(ctx.pdtype) if ctx.needs_input_grad[2] else None
-        return dx, dg, db, dres, None, None, None, None, None, None
+        return dx, dg, db, dres, None, None, None, None, None, None, None
 
 
 def bn_act_ok(x: torch.Tensor, bn: torch.nn.BatchNorm2d) -> bool:
@@ -75,8 +120,9 @@ def bn_act(x: torch.Tensor, bn: torch.nn.BatchNorm2d, residual: torch.Tensor | N
             nbt = None  # (then counted here, as torch would)
             if bn.num_batches_tracked is not None:
                 bn.num_batches_tracked.add_(1)
+        lws = _layer_ws(bn, x) if config.get().bn_layer_ws else None
         return _BNAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, bn.eps, bn.momentum,
-                            relu, nbt)
+                            relu, nbt, lws)
     y = bn(x)
     if residual is not None:
         y = y + residual

@@ -302,6 +302,53 @@ def test_fused_batchnorm_act_vs_fp32(gpu, C, res, relu):
     assert int(bn.num_batches_tracked) == 2
 
 
+def test_fused_batchnorm_layer_workspace_out_of_order_calls(gpu):
+    """The per-layer workspace (finalize inside the apply / dx passes, ops/batchnorm.py _LayerWS) against the
+    shared-workspace path (separate finalize kernels, self-contained per call) for call orders that break
+    the steady state: a no-grad train-mode forward, two forwards before their backwards (in reverse
+    order), and a second backward through a retained graph. Outputs, gradients and running stats match."""
+    from distributedvolunteercomputing_amd import config
+    from distributedvolunteercomputing_amd.ops.batchnorm import bn_act
+
+    torch.manual_seed(5)
+    C = 128
+    xs = [(torch.randn(8, C, 14, 14, device=gpu) * (1 + i) + i).to(torch.bfloat16).to(memory_format=torch.channels_last)
+          for i in range(3)]
+    gs = [torch.randn_like(x) for x in xs]
+
+    def run(layer_ws):
+        bn = torch.nn.BatchNorm2d(C).to(gpu)
+        torch.nn.init.uniform_(bn.weight, 0.5, 1.5)
+        bn = bn.to(torch.bfloat16)
+        outs, grads = [], []
+        with config.override(bn_layer_ws=layer_ws):
+            with torch.no_grad():
+                outs.append(bn_act(xs[0], bn, None, True))  # forward without a backward
+            a = xs[1].clone().requires_grad_()
+            b = xs[2].clone().requires_grad_()
+            ya = bn_act(a, bn, None, True)
+            yb = bn_act(b, bn, None, True)  # two forwards pending
+            assert type(yb.grad_fn).__name__ == "_BNActBackward"
+            yb.backward(gs[2], retain_graph=True)
+            ya.backward(gs[1])
+            grads += [a.grad.clone(), b.grad.clone(), bn.weight.grad.clone(), bn.bias.grad.clone()]
+            b.grad = None
+            yb.backward(gs[2])  # second backward through the retained graph
+            grads.append(b.grad.clone())
+            ya2 = bn_act(a, bn, None, True)  # back in steady state
+            a.grad = None
+            ya2.backward(gs[1])
+            grads.append(a.grad.clone())
+            outs += [ya, yb, ya2]
+        return outs, grads, (bn.running_mean.float(), bn.running_var.float())
+
+    o1, g1, r1 = run(True)
+    o0, g0, r0 = run(False)
+    rel = lambda a, b: float((a.float() - b.float()).norm() / (b.float().norm() + 1e-6))  # noqa: E731
+    for a, b in zip(o1 + g1 + list(r1), o0 + g0 + list(r0)):
+        assert rel(a, b) < 2e-3, rel(a, b)
+
+
 @pytest.mark.parametrize("C", [64, 1024])
 def test_fused_batchnorm_grads_into_flat_buffers(gpu, C):
     """With preset contiguous .grad buffers (the trainer's flat gradient views) the BN backward ADDS
