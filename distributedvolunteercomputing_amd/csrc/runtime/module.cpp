@@ -184,6 +184,16 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("src"), py::arg("dst"), py::arg("k"), py::arg("w"), py::arg("h"));
   m.def(
+      "write_frames",
+      [](int fd, int64_t off, py::buffer src, int64_t k, int64_t w, int64_t h, bool y4m) {
+        py::buffer_info a = src.request();
+        require_c_contiguous(a, "write_frames src");
+        if (k < 0 || w <= 0 || h <= 0 || off < 0 || a.size * a.itemsize < 3 * k * w * h)
+          throw std::invalid_argument("write_frames: buffer smaller than 3 * k * w * h bytes");
+        return without_gil([&] { return write_frames(fd, off, (const uint8_t*)a.ptr, k, w, h, y4m); });
+      },
+      py::arg("fd"), py::arg("off"), py::arg("src"), py::arg("k"), py::arg("w"), py::arg("h"), py::arg("y4m"));
+  m.def(
       "yuv_to_bgr",
       [](py::buffer y, py::buffer u, py::buffer v, py::buffer dst, int64_t w, int64_t h, int64_t cw) {
         py::buffer_info Y = y.request(), U = u.request(), V = v.request(), D = dst.request(true);

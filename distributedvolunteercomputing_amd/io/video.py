@@ -291,36 +291,44 @@ def open_source(spec: str) -> FrameSource:
 
 
 # ----------------------------------------------------------------------------- sinks
+def _frame_writer():
+    """The C++ runtime's threaded positional frame writer (csrc/runtime/colour.cpp write_frames), or None."""
+    rt = _rt()
+    return rt if rt is not None and hasattr(rt, "write_frames") else None
+
+
 class Y4MWriter:
-    """YUV4MPEG2 4:4:4 writer (cv2.VideoWriter replacement)."""
+    """YUV4MPEG2 4:4:4 writer (cv2.VideoWriter replacement). Every write is positional (os.pwrite at the
+    writer's running offset); a received chunk's frames go through ONE native call that converts and
+    writes frame ranges on several threads with the GIL released."""
 
     def __init__(self, path, width, height, fps=30):
         self.path, self.w, self.h = str(path), int(width), int(height)
         self.f = open(self.path, "wb")
-        self.f.write(f"YUV4MPEG2 W{self.w} H{self.h} F{int(fps)}:1 Ip A1:1 C444\n".encode())
+        hdr = f"YUV4MPEG2 W{self.w} H{self.h} F{int(fps)}:1 Ip A1:1 C444\n".encode()
+        os.pwrite(self.f.fileno(), hdr, 0)
+        self.off = len(hdr)
         self.frames = 0
 
     def write(self, frame: np.ndarray):
         if frame.shape[0] != self.h or frame.shape[1] != self.w:
             raise ValueError(f"frame {frame.shape} does not match writer {self.h}x{self.w}")
-        self.f.write(b"FRAME\n")
-        self.f.write(bgr_to_yuv444(frame))  # the planar buffer itself (no bytes copy)
+        fd = self.f.fileno()
+        os.pwrite(fd, b"FRAME\n", self.off)
+        body = bgr_to_yuv444(frame)  # the planar buffer itself (no bytes copy)
+        os.pwrite(fd, memoryview(body).cast("B"), self.off + 6)
+        self.off += 6 + body.nbytes
         self.frames += 1
 
     def write_many(self, frames):
-        """Several frames in order: one native conversion across threads, then the frame bodies."""
-        rt = _rt()
-        if rt is None or not hasattr(rt, "bgr_to_yuv444_frames") or any(f.shape != (self.h, self.w, 3) or
-                                                                      f.dtype != np.uint8 for f in frames):
+        """Several frames in order: one native conversion + write across threads."""
+        rt = _frame_writer()
+        if rt is None or any(f.shape != (self.h, self.w, 3) or f.dtype != np.uint8 for f in frames):
             for f in frames:
                 self.write(f)
             return
         block = _as_block(frames)
-        out = np.empty((len(frames), 3, self.h, self.w), np.uint8)
-        rt.bgr_to_yuv444_frames(block, out, len(frames), self.w, self.h)
-        for i in range(len(frames)):
-            self.f.write(b"FRAME\n")
-            self.f.write(out[i])
+        self.off += rt.write_frames(self.f.fileno(), self.off, block, len(block), self.w, self.h, True)
         self.frames += len(frames)
 
     def release(self):
@@ -329,9 +337,9 @@ class Y4MWriter:
 
 
 class NpyWriter:
-    """uint8 [N, H, W, 3] .npy written as the frames arrive (one write per received chunk, no
-    copy held in memory): the header is written first with room for any frame count and rewritten
-    with the final count by release()."""
+    """uint8 [N, H, W, 3] .npy written as the frames arrive (positional writes of each received chunk,
+    threaded in the C++ runtime; no copy held in memory): the header is written first with room for any
+    frame count and rewritten with the final count by release()."""
 
     HEADER = 256  # bytes (a multiple of 64, as the format wants)
 
@@ -339,7 +347,7 @@ class NpyWriter:
         self.path, self.w, self.h = str(path), int(width), int(height)
         self.f = open(self.path, "wb")
         self.frames = 0
-        self.f.write(self._header(0))
+        os.pwrite(self.f.fileno(), self._header(0), 0)
 
     def _header(self, n):
         d = "{'descr': '|u1', 'fortran_order': False, 'shape': (%d, %d, %d, 3), }" % (n, self.h, self.w)
@@ -349,7 +357,13 @@ class NpyWriter:
     def _put(self, block):
         if block.shape[1:] != (self.h, self.w, 3) or block.dtype != np.uint8:
             raise ValueError(f"frames {block.dtype} {block.shape[1:]} do not match writer {self.h}x{self.w}")
-        self.f.write(memoryview(np.ascontiguousarray(block)).cast("B"))
+        block = np.ascontiguousarray(block)
+        off = self.HEADER + self.frames * 3 * self.w * self.h
+        rt = _frame_writer()
+        if rt is not None:
+            rt.write_frames(self.f.fileno(), off, block, len(block), self.w, self.h, False)
+        else:
+            os.pwrite(self.f.fileno(), memoryview(block).cast("B"), off)
         self.frames += len(block)
 
     def write(self, frame):
@@ -362,8 +376,7 @@ class NpyWriter:
 
     def release(self):
         if self.f and not self.f.closed:
-            self.f.seek(0)
-            self.f.write(self._header(self.frames))
+            os.pwrite(self.f.fileno(), self._header(self.frames), 0)
             self.f.close()
 
 
