@@ -262,7 +262,11 @@ def launcher(a):
     survivors = [r for r in range(a.peers) if r not in victims]
     joiners = {}
     t_dead = {}
+    t_beat = time.time()
     while not all(r in rc for r in survivors) and time.time() < t_end:
+        if time.time() - t_beat > 30:  # progress for a supervisor that kills silent runs
+            t_beat = time.time()
+            print(f"[bench_drop] waiting: exited {rc}, joiners {sorted(joiners)}", file=sys.stderr, flush=True)
         for r, p in enumerate(procs):
             if r not in rc and p.poll() is not None:
                 rc[r] = p.returncode
@@ -273,9 +277,13 @@ def launcher(a):
                     joiners[v] = subprocess.Popen(common + ["--peer", str(v), "--join"], env=peer_env(v))
         time.sleep(0.2)
     for v, p in joiners.items():
-        try:
-            p.wait(timeout=max(5.0, t_end - time.time()))
-        except subprocess.TimeoutExpired:
+        deadline = max(t_end, time.time() + 5.0)
+        while p.poll() is None and time.time() < deadline:
+            try:
+                p.wait(timeout=min(30.0, max(1.0, deadline - time.time())))
+            except subprocess.TimeoutExpired:
+                print(f"[bench_drop] waiting for joiner {v}", file=sys.stderr, flush=True)
+        if p.poll() is None:
             p.kill()
             p.wait()
         if p.returncode != 0:

@@ -323,11 +323,31 @@ class PeerGroup:
         _GRAVEYARD.append(pg)
 
     # ------------------------------------------------------------------ collectives
+    def _issue(self, op: str, fn):
+        """Issue one collective on this generation's communicator. The watchdog can abort the
+        communicator between ``_check()`` and the issue (a member's lease expired meanwhile): the
+        issue then raises (RCCL: "communicator was aborted") or finds it torn down. Under a watch that
+        is the round's failure -- a PeerFailure the trainer redoes the round on -- not a crash of the
+        survivor (8-rank rehearsal, round 5: survivors died of a DistBackendError raised by
+        alltoall_base itself)."""
+        pg = self.pg
+        try:
+            if pg is None:
+                raise RuntimeError("communicator torn down")
+            return fn(pg)
+        except Exception as e:  # noqa: BLE001
+            w = self.watch
+            if w is None:
+                raise
+            w.declare_abort(f"{op} issue failed on peer {w.pid}: {type(e).__name__}: {str(e)[:120]}")
+            self.abort()
+            raise PeerFailure(f"gen {self.generation}: {op} issue failed: {e}") from e
+
     def allreduce_(self, t: torch.Tensor):
         if self.size == 1:
             return t
         self._check()
-        self._wait(self.pg.allreduce([t]), "allreduce")
+        self._wait(self._issue("allreduce", lambda pg: pg.allreduce([t])), "allreduce")
         return t
 
     def broadcast_(self, t: torch.Tensor, root: int = 0):
@@ -337,7 +357,7 @@ class PeerGroup:
         opts = dist.BroadcastOptions()
         opts.rootRank = root
         opts.rootTensor = 0
-        self._wait(self.pg.broadcast([t], opts), "broadcast")
+        self._wait(self._issue("broadcast", lambda pg: pg.broadcast([t], opts)), "broadcast")
         return t
 
     def reduce_scatter_(self, out: torch.Tensor, inp: torch.Tensor):
@@ -348,11 +368,11 @@ class PeerGroup:
         self._check()
         if self.backend == "gloo":  # gloo lacks reduce_scatter_base: all-reduce then slice
             tmp = inp.clone()
-            self._wait(self.pg.allreduce([tmp]), "reduce_scatter")
+            self._wait(self._issue("reduce_scatter", lambda pg: pg.allreduce([tmp])), "reduce_scatter")
             n = out.numel()
             out.copy_(tmp[self.rank * n : (self.rank + 1) * n])
             return out
-        self._wait(self.pg._reduce_scatter_base(out, inp), "reduce_scatter")
+        self._wait(self._issue("reduce_scatter", lambda pg: pg._reduce_scatter_base(out, inp)), "reduce_scatter")
         return out
 
     def all_gather_(self, out: torch.Tensor, inp: torch.Tensor):
@@ -360,7 +380,7 @@ class PeerGroup:
             out.copy_(inp)
             return out
         self._check()
-        self._wait(self.pg._allgather_base(out, inp), "all_gather")
+        self._wait(self._issue("all_gather", lambda pg: pg._allgather_base(out, inp)), "all_gather")
         return out
 
     def all_gather_object_sizes(self, n: int):
@@ -377,16 +397,16 @@ class PeerGroup:
         self._check()
         if self.backend == "gloo" and t.device.type != "cpu":
             t = t.to("cpu")  # gloo point-to-point moves host memory only (its collectives stage GPU tensors)
-        self._wait(self.pg.send([t], dst, tag), "send")
+        self._wait(self._issue("send", lambda pg: pg.send([t], dst, tag)), "send")
 
     def recv(self, t: torch.Tensor, src: int, tag: int = 0):
         self._check()
         if self.backend == "gloo" and t.device.type != "cpu":
             host = torch.empty(t.shape, dtype=t.dtype)  # a fresh buffer: abandoned if the wait aborts
-            self._wait(self.pg.recv([host], src, tag), "recv")
+            self._wait(self._issue("recv", lambda pg: pg.recv([host], src, tag)), "recv")
             t.copy_(host)
             return
-        self._wait(self.pg.recv([t], src, tag), "recv")
+        self._wait(self._issue("recv", lambda pg: pg.recv([t], src, tag)), "recv")
 
     def exchange(self, send_t: torch.Tensor, recv_t: torch.Tensor, peer: int, tag: int = 0):
         """Pairwise swap with `peer`. The lower rank sends first, the higher receives first,
@@ -402,8 +422,9 @@ class PeerGroup:
         """Generic variable-split all-to-all over flat buffers (RCCL: one grouped send/recv
         launch that drives every xGMI link of this GPU at once)."""
         self._check()
-        self._wait(self.pg.alltoall_base(recv_t.view(-1), send_t.view(-1), list(recv_splits), list(send_splits),
-                                         dist.AllToAllOptions()), "alltoall")
+        self._wait(self._issue("alltoall", lambda pg: pg.alltoall_base(recv_t.view(-1), send_t.view(-1), list(recv_splits),
+                                                                        list(send_splits), dist.AllToAllOptions())),
+                   "alltoall")
 
     def exchange_all(self, send_t: torch.Tensor, recv_t: torch.Tensor, send_to: int, recv_from: int | None = None):
         """One round in which EVERY rank of the group sends `send_t` to `send_to` and receives
