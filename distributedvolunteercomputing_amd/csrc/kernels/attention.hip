@@ -374,14 +374,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
 //   B operands = the bf16-converted accumulators; the keys stay on the lanes throughout)
 constexpr int B_BQ = 64;  // queries per LDS tile
 
-// AUG: the row constants enter through the MFMAs instead of the VALU. One more 32x32x16 MFMA per S and per
-// dP adds -lse[q] / c (resp. -delta[q]) to every element of its query row: A operand = the query's
-// constant as a bf16 pair (hi, lo = the rounding rest; k = 0, 1 of an extra 16-deep chunk), B = (1, 1)
-// on every key. A lane reads its OWN query's pair (one ds_read_b32) instead of the 16 queries of its
-// accumulator rows (four ds_read_b128 per constant), and P = exp2(c S'), dS = P dP' need no fma /
-// subtraction. (hi + lo carries the constant to ~2^-17 relative: |lse / c| ~ 10^2 -> 1e-3 absolute
-// in S', ~2e-4 in the exponent.)
-template <int WPE, bool DMA, bool AUG>
+template <int WPE, bool DMA>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) attn_bwd_dkdv_d64_kernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ lse,
@@ -394,8 +387,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
   __shared__ __attribute__((aligned(16))) bf16 sQD1[2][B_BQ * AD];
 #define sQ_(b) ((b) ? &sQD1[0][0] : &sQD0[0][0])
 #define sD_(b) ((b) ? &sQD1[1][0] : &sQD0[1][0])
-  __shared__ __attribute__((aligned(16))) float sL[2][B_BQ];    // AUG: bf16 pairs (hi, lo) of -lse / c
-  __shared__ __attribute__((aligned(16))) float sDel[2][B_BQ];  // AUG: bf16 pairs of -delta
+  __shared__ __attribute__((aligned(16))) float sL[2][B_BQ];
+  __shared__ __attribute__((aligned(16))) float sDel[2][B_BQ];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h2 = lane >> 5, col = lane & 31;
   const int nkb = (T + 127) / 128;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -438,16 +431,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
       const int qq = qt * B_BQ + tid;
       rl = qq < T ? -lrow[qq] : -INFINITY;
       rdl = drow[min(qq, T - 1)];
-      if constexpr (AUG) {
-        auto pair = [](float v) {  // v as bf16 hi + lo, packed (hi in the low half: k = 0)
-          const bf16 hi = (bf16)v;
-          const bf16 lo = (bf16)(__builtin_isinf(v) ? 0.f : v - (float)hi);  // -inf rows: (-inf, 0)
-          return __uint_as_float((unsigned)(unsigned short)__builtin_bit_cast(short, hi) |
-                                 ((unsigned)(unsigned short)__builtin_bit_cast(short, lo) << 16));
-        };
-        rl = pair(rl / scale_log2);
-        rdl = pair(-rdl);
-      }
     }
   };
   auto sstore = [&](int buf) {
@@ -480,28 +463,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
         dp = mfma32(row_frag_swz(sD_(cur), sub * 32 + col, s, h2), vf[s], dp);
       }
       f32x16 pp;
-      if constexpr (AUG) {
-        // k = 0, 1 of the extra chunk live in the h2 = 0 half; the h2 = 1 half contributes zeros
-        const unsigned al = __float_as_uint(sL[cur][sub * 32 + col]), ad = __float_as_uint(sDel[cur][sub * 32 + col]);
-        const short one = (short)0x3F80;  // bf16 1.0
-        const sx8 ones = h2 ? sx8{0, 0, 0, 0, 0, 0, 0, 0} : sx8{one, one, 0, 0, 0, 0, 0, 0};
-        const sx8 ca = h2 ? sx8{0, 0, 0, 0, 0, 0, 0, 0}
-                          : sx8{(short)(al & 0xffff), (short)(al >> 16), 0, 0, 0, 0, 0, 0};
-        const sx8 cd = h2 ? sx8{0, 0, 0, 0, 0, 0, 0, 0}
-                          : sx8{(short)(ad & 0xffff), (short)(ad >> 16), 0, 0, 0, 0, 0, 0};
-        st = mfma32(ca, ones, st);  // S' = S - lse / c
-        dp = mfma32(cd, ones, dp);  // dP' = dP - delta
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float p = __builtin_amdgcn_exp2f(st[r] * scale_log2);
-          if (MASK) {
-            const int qq = qb + 8 * (r >> 2) + 4 * h2 + (r & 3);
-            p = key > qq ? 0.f : p;
-          }
-          pp[r] = p;
-          st[r] = p * dp[r];  // dS
-        }
-      } else {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         // rows 8g + 4h + (0..3) of S are 4 consecutive queries: one 16-B LDS read each
@@ -518,7 +479,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
           pp[r] = p;
           st[r] = p * (dp[r] - dv[i]);  // dS
         }
-      }
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -604,9 +564,7 @@ using namespace vcx;
 // Backward kernels: 2 waves per SIMD (at 3-4 they spill: dq 0.87-1.25 ms vs 0.64 for the pair);
 // dQ with LDS-DMA staging (264 vs 275 us), dK/dV with register staging (381 vs 383 us: the DMA
 // build of that kernel hits the 256-VGPR cap and spills).
-// g_bwd_dma bit 0: dQ kernel with LDS-DMA, bit 1: dK/dV kernel with LDS-DMA, bit 2: dK/dV with the row
-// constants through the MFMAs (AUG)
-static int g_fwd_wpe = 3, g_fwd_dma = 1, g_bwd_dma = 1;
+static int g_fwd_wpe = 3, g_fwd_dma = 1, g_bwd_dma = 1;  // g_bwd_dma bit 0: dQ kernel, bit 1: dK/dV kernel
 // output tiles (O, dQ, dK, dV): 1 = staged through LDS, whole-row 16-B stores; 0 = per-lane half-row
 // stores. Bench shape, same box (profiles/r1_attn_variants.log): backward 0.589 vs 0.614 ms, forward
 // within noise (0.201-0.212 vs 0.206-0.208)
@@ -615,7 +573,7 @@ static int g_stage_epi = 1;
 void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma, int stage_epi) {
   if (fwd_wpe == 2 || fwd_wpe == 3) g_fwd_wpe = fwd_wpe;
   if (fwd_dma == 0 || fwd_dma == 1) g_fwd_dma = fwd_dma;
-  if (bwd_dma >= 0 && bwd_dma <= 7) g_bwd_dma = bwd_dma;
+  if (bwd_dma >= 0 && bwd_dma <= 3) g_bwd_dma = bwd_dma;
   if (stage_epi == 0 || stage_epi == 1) g_stage_epi = stage_epi;
 }
 
@@ -634,16 +592,14 @@ void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const 
     hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, false>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale,
                        scale * LOG2E, g_stage_epi);
-#define VCX_DKDV(D, A)                                                                                       \
-  hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, D, A>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,     \
-                     (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E, g_stage_epi)
-  switch (g_bwd_dma & 6) {
-    case 0: VCX_DKDV(false, false); break;
-    case 2: VCX_DKDV(true, false); break;
-    case 4: VCX_DKDV(false, true); break;
-    default: VCX_DKDV(true, true); break;
-  }
-#undef VCX_DKDV
+  if (g_bwd_dma & 2)
+    hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, true>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E,
+                       g_stage_epi);
+  else
+    hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, false>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E,
+                       g_stage_epi);
 }
 
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s) {

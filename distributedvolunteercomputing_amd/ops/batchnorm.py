@@ -81,8 +81,7 @@ class _BNAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         xh, mask, mean, rstd, scale = ctx.saved_tensors
-        weight, bias = ctx.params
-        ctx.params = None
+        weight, bias = ctx.params  # (kept: a retained graph may run this backward again)
         dyh = _nhwc(dy)
         if not dyh.is_contiguous():
             dyh = dyh.contiguous()
