@@ -3,7 +3,6 @@
 #include <unistd.h>
 
 #include <algorithm>
-#include <atomic>
 #include <cerrno>
 #include <cstring>
 #include <stdexcept>
@@ -128,38 +127,31 @@ static int pwrite_all(int fd, const uint8_t* p, int64_t n, int64_t off) {
 
 int64_t write_frames(int fd, int64_t off, const uint8_t* bgr, int64_t k, int64_t w, int64_t h, bool y4m) {
   // k BGR frames [k, h, w, 3] at byte offset `off` of fd, as raw frames (npy body) or as Y4M 4:4:4
-  // records ("FRAME\n" + Y, U, V planes), frame ranges on up to 8 threads with positional writes: the
-  // output sink of a video job wrote ~27 MB per 100-frame chunk on one thread (8.7-23 ms, the job's
-  // bound once the uplink stopped copying, profiles/r5_video_job.txt)
+  // records ("FRAME\n" + Y, U, V planes). The Y4M records are converted on up to 8 threads into one
+  // buffer; the bytes go out in ONE positional write: several threads writing one file serialise on
+  // its inode lock (threaded pwrite measured slower than a single write, profiles/r5_video_job.txt)
   const int64_t n = w * h, fb = 3 * n, rec = y4m ? fb + 6 : fb;
+  if (!y4m) {
+    const int e = pwrite_all(fd, bgr, k * fb, off);
+    if (e) throw std::runtime_error(std::string("write_frames: ") + std::strerror(e));
+    return k * fb;
+  }
+  std::vector<uint8_t> buf((size_t)(k * rec));
   const int64_t hw = (int64_t)std::max(1u, std::thread::hardware_concurrency());
   const int64_t nt = std::max<int64_t>(1, std::min<int64_t>({8, hw, k}));
-  std::atomic<int> err{0};
   auto run = [&](int64_t f0, int64_t f1) {
-    if (!y4m) {
-      const int e = pwrite_all(fd, bgr + f0 * fb, (f1 - f0) * fb, off + f0 * fb);
-      if (e) err = e;
-      return;
-    }
-    const int64_t per = std::max<int64_t>(1, std::min<int64_t>(f1 - f0, (4 << 20) / rec));  // <= ~4 MB a write
-    std::vector<uint8_t> buf((size_t)(per * rec));
-    for (int64_t f = f0; f < f1 && !err; f += per) {
-      const int64_t m = std::min(per, f1 - f);
-      for (int64_t j = 0; j < m; ++j) {
-        uint8_t* r = buf.data() + j * rec;
-        std::memcpy(r, "FRAME\n", 6);
-        const uint8_t* src = bgr + (f + j) * fb;
-        uint8_t *Y = r + 6, *U = Y + n, *V = Y + 2 * n;
-        for (int64_t i = 0; i < n; ++i) {
-          const float b = src[3 * i], g = src[3 * i + 1], rr = src[3 * i + 2];
-          const float y = 0.299f * rr + 0.587f * g + 0.114f * b;
-          Y[i] = sat(y);
-          U[i] = sat((b - y) * 0.564f + 128.0f);
-          V[i] = sat((rr - y) * 0.713f + 128.0f);
-        }
+    for (int64_t f = f0; f < f1; ++f) {
+      uint8_t* r = buf.data() + f * rec;
+      std::memcpy(r, "FRAME\n", 6);
+      const uint8_t* src = bgr + f * fb;
+      uint8_t *Y = r + 6, *U = Y + n, *V = Y + 2 * n;
+      for (int64_t i = 0; i < n; ++i) {
+        const float b = src[3 * i], g = src[3 * i + 1], rr = src[3 * i + 2];
+        const float y = 0.299f * rr + 0.587f * g + 0.114f * b;
+        Y[i] = sat(y);
+        U[i] = sat((b - y) * 0.564f + 128.0f);
+        V[i] = sat((rr - y) * 0.713f + 128.0f);
       }
-      const int e = pwrite_all(fd, buf.data(), m * rec, off + f * rec);
-      if (e) err = e;
     }
   };
   if (nt <= 1) {
@@ -174,7 +166,8 @@ int64_t write_frames(int fd, int64_t off, const uint8_t* bgr, int64_t k, int64_t
     run(0, std::min(k, per));
     for (auto& x : th) x.join();
   }
-  if (err) throw std::runtime_error(std::string("write_frames: ") + std::strerror(err.load()));
+  const int e = pwrite_all(fd, buf.data(), k * rec, off);
+  if (e) throw std::runtime_error(std::string("write_frames: ") + std::strerror(e));
   return k * rec;
 }
 

@@ -162,8 +162,9 @@ def test_ordered_sink_any_arrival_order(n, data):
         sink.push(k, np.full((2, 2, 3), k % 256, dtype=np.uint8))
     if final_at >= len(arrivals):
         sink.set_final(n)
+    assert sink.done.wait(10)  # the writes run on the sink's writer thread
     assert w.frames == [k % 256 for k in frames]
-    assert sink.done.is_set() and sink.written == n and not sink.stash
+    assert sink.written == n and not sink.stash
 
 
 class _ManyWriter(_ListWriter):
@@ -195,8 +196,9 @@ def test_ordered_sink_chunks_any_arrival_order(nchunks, csize, data):
     for c in arrivals:
         block = np.stack([np.full((2, 2, 3), k % 256, dtype=np.uint8) for k in chunks[c]])
         sink.push_many(chunks[c], block)
+    assert sink.done.wait(10)
     assert w.frames == [k % 256 for k in range(1, n + 1)]
-    assert sink.done.is_set() and sink.written == n and not sink.stash
+    assert sink.written == n and not sink.stash
     assert w.batches <= nchunks
 
 
