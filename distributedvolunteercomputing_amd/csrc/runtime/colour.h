@@ -15,8 +15,8 @@ void bgr_to_yuv444_frames(const uint8_t* bgr, uint8_t* yuv, int64_t k, int64_t w
 // planes y [h][w], u/v [ch][cw] with cw = w (4:4:4) or (w + 1) / 2 (4:2:0, 2x2 replication) -> bgr [h][w][3]
 void yuv_to_bgr(const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* bgr, int64_t w, int64_t h, int64_t cw);
 
-// k BGR frames written at byte `off` of fd in one positional write (raw, or as Y4M 4:4:4 records converted
-// on several threads);
+// k BGR frames written at byte `off` of fd (raw, or as Y4M 4:4:4 records): a regular file is grown and the
+// range mapped and filled on several threads, anything else gets one positional write;
 // returns the bytes written (throws std::runtime_error on a write error)
 int64_t write_frames(int fd, int64_t off, const uint8_t* bgr, int64_t k, int64_t w, int64_t h, bool y4m);
 
