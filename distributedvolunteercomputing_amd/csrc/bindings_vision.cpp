@@ -174,6 +174,37 @@ void gemm_bias_heads(at::Tensor X, at::Tensor Wt, at::Tensor bias, at::Tensor lo
                            S > 1 ? splitk_counters(X) : nullptr, cur_stream());
 }
 
+// Two MobileNet blocks in one kernel (conv1: dw s1 + pw K1 -> N1, conv2: dw s2 + pw N1 -> N2; the first
+// block's output never leaves LDS). Returns an undefined tensor when no instance covers the shapes.
+at::Tensor dw_pw2(at::Tensor x, at::Tensor dw1_w, at::Tensor dw1_b, bool dw1_relu, at::Tensor W1, at::Tensor b1,
+                  bool relu1, at::Tensor dw2_w, at::Tensor dw2_b, bool dw2_relu, at::Tensor W2, at::Tensor b2, bool relu2) {
+  CHK(x, at::kBFloat16);
+  CHK(dw1_w, at::kBFloat16);
+  CHK(W1, at::kBFloat16);
+  CHK(dw2_w, at::kBFloat16);
+  CHK(W2, at::kBFloat16);
+  CHK(dw1_b, at::kFloat);
+  CHK(b1, at::kFloat);
+  CHK(dw2_b, at::kFloat);
+  CHK(b2, at::kFloat);
+  TORCH_CHECK(x.dim() == 4 && W1.dim() == 2 && W2.dim() == 2, "x NHWC, W1 [N1, K1], W2 [N2, N1]");
+  const int64_t imgs = x.size(0), H = x.size(1), W = x.size(2), K1 = x.size(3), N1 = W1.size(0), N2 = W2.size(0);
+  TORCH_CHECK(W1.size(1) == K1 && W2.size(1) == N1 && dw1_w.numel() == 10 * K1 && dw1_b.numel() == K1 &&
+                  dw2_w.numel() == 10 * N1 && dw2_b.numel() == N1 && b1.numel() == N1 && b2.numel() == N2,
+              "dw_pw2: paired dw weights [5, C, 2], biases [C], W1 [N1, K1], W2 [N2, N1]");
+  for (const at::Tensor* t : {&x, &dw1_w, &dw1_b, &W1, &dw2_w, &dw2_b, &W2})
+    TORCH_CHECK(((uintptr_t)t->data_ptr() & 15) == 0, "dw_pw2: 16-B aligned operands");
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  TORCH_CHECK(imgs * Ho * Wo < INT32_MAX && imgs * H * W * K1 < ((int64_t)1 << 40));
+  auto Y = at::empty({imgs, Ho, Wo, N2}, x.options());
+  if (!vcx_dw_pw2(x.data_ptr(), dw1_w.data_ptr(), dw1_b.data_ptr<float>(), dw1_relu ? 1 : 0, W1.data_ptr(),
+                  b1.data_ptr<float>(), relu1 ? 1 : 0, dw2_w.data_ptr(), dw2_b.data_ptr<float>(), dw2_relu ? 1 : 0,
+                  W2.data_ptr(), b2.data_ptr<float>(), relu2 ? 1 : 0, Y.data_ptr(), (int)imgs, (int)H, (int)W,
+                  (int)K1, (int)N1, (int)N2, cur_stream()))
+    return at::Tensor();
+  return Y;
+}
+
 // KxK convolution as an implicit GEMM (no im2col matrix): x NHWC bf16 [imgs, H, W, Cs] using
 // its first C channels (C % 8 == 0, or C == 4 == Cs), Wt [N, Kp] columns (ky, kx, c)
 at::Tensor conv_implicit(at::Tensor x, at::Tensor Wt, at::Tensor bias, int64_t C, int64_t KH, int64_t KW,
@@ -256,6 +287,7 @@ void vcx_register_vision(pybind11::module& m) {
   m.def("gemm_bias_act", &gemm_bias_act);
   m.def("gemm_bias_heads", &gemm_bias_heads);
   m.def("dw_pw", &dw_pw);
+  m.def("dw_pw2", &dw_pw2);
   m.def("conv_implicit", &conv_implicit);
   m.def("ssd_detect", &ssd_detect);
   m.def("annotate", &annotate);

@@ -20,6 +20,9 @@ void vcx_conv_implicit(const void* x, const void* Wt, const float* bias, void* Y
                        int* cnt, hipStream_t s);
 void vcx_dw_pw(const void* x, const void* dw_w, const float* dw_b, int dw_relu, const void* Wt, const float* bias,
                void* Y, int imgs, int H, int W, int K, int stride, int N, int relu, hipStream_t s);
+bool vcx_dw_pw2(const void* x, const void* dw1_w, const float* dw1_b, int dw1_relu, const void* W1, const float* b1,
+                int relu1, const void* dw2_w, const float* dw2_b, int dw2_relu, const void* W2, const float* b2,
+                int relu2, void* Y, int imgs, int H, int W, int K1, int N1, int N2, hipStream_t s);
 void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,
                        int relu, float* ws, int S, int* cnt, hipStream_t s);
 void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* prob,

@@ -1031,6 +1031,229 @@ __global__ void __launch_bounds__(256) dwpw_persist_kernel(const bf16* __restric
 }
 
 // =====================================================================================
+// Two MobileNet blocks in one persistent kernel: conv1 (depthwise 3x3 s1 + pointwise K1 -> N1) and
+// conv2 (depthwise 3x3 s2 + pointwise N1 -> N2), prototxt conv1/dw .. conv2 (MobileNetSSD_deploy:42-106).
+// Unfused, conv1's output (150^2 x 64 bf16 = 288 MB per 100-frame chunk) is written by one kernel and
+// read back by the next: 2 x 288 MB of the 864 MB the two blocks moved (216 us of the 1.19 ms chunk,
+// profiles/r3_detector_chunk_final.txt). Here a workgroup owns a TH x TW tile of conv2's OUTPUT and
+// recomputes the conv1 region it needs, (2 TH + 1) x (2 TW + 1) pixels, from a (2 TH + 3) x (2 TW + 3)
+// halo of conv0's output: conv1's output lives only in LDS.
+//   R0: the conv0 halo [HH*HW][K1] -> (after dw1) conv1's output P1 [PH*PW][N1] -> (after dw2) the
+//       output staging [TH*TW][N2];  R1: dw1's output (pw1's A tile) -> (after pw1) dw2's output
+//       (pw2's A tile);  W1, W2: the pointwise weights, loaded once per workgroup.
+// P1 pixels outside the image are written as ZERO (conv2's depthwise padding), not as pw1 of zeros.
+// Every intermediate is rounded to bf16 where the unfused kernels store it, and the reductions run in
+// the same order (dw9_accum_w, one MFMA chain per K slice), so the result equals the two-kernel path.
+// The next tile's halo is loaded into registers while this tile's GEMMs and stores run.
+template <int K1, int N1, int N2, int TH, int TW>
+struct Dwpw2 {
+  static constexpr int PH = 2 * TH + 1, PW = 2 * TW + 1, MP = PH * PW, MP16 = (MP + 15) / 16 * 16;
+  static constexpr int HH = PH + 2, HW = PW + 2, MT = TH * TW;
+  static constexpr int HALO_B = HH * HW * K1 * 2, P1_B = MP * N1 * 2, OUT_B = MT * N2 * 2;
+  static constexpr int R0 = (HALO_B > P1_B ? (HALO_B > OUT_B ? HALO_B : OUT_B) : (P1_B > OUT_B ? P1_B : OUT_B));
+  static constexpr int A1_B = MP16 * K1 * 2, A2_B = MT * N1 * 2, R1 = A1_B > A2_B ? A1_B : A2_B;
+  static constexpr int W1_B = N1 * K1 * 2, W2_B = N2 * N1 * 2;
+  static constexpr int LDS = R0 + R1 + W1_B + W2_B;
+  static constexpr int NE = HH * HW * (K1 / 8), NH = (NE + 255) / 256;  // halo 16-B pieces (per thread)
+};
+
+template <int K1, int N1, int N2, int TH, int TW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+dwpw2_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dwp1, const float* __restrict__ dwb1,
+                     int dw1_relu, const bf16* __restrict__ Wt1, const float* __restrict__ pb1, int relu1,
+                     const uint32_t* __restrict__ dwp2, const float* __restrict__ dwb2, int dw2_relu,
+                     const bf16* __restrict__ Wt2, const float* __restrict__ pb2, int relu2, bf16* __restrict__ y,
+                     int H, int W, int Ho, int Wo, int imgs) {
+  using G = Dwpw2<K1, N1, N2, TH, TW>;
+  constexpr int PW = G::PW, MP = G::MP, MP16 = G::MP16, HW = G::HW, MT = G::MT, NE = G::NE, NH = G::NH;
+  constexpr int K18 = K1 / 8, N18 = N1 / 8, KS1 = K1 / 32, KS2 = N1 / 32;
+  static_assert(256 % K18 == 0 && 256 % N18 == 0 && K1 % 32 == 0 && N1 % 64 == 0 && N2 % 64 == 0 && MT % 16 == 0,
+                "tile shape");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const r0 = smem;
+  bf16* const sP1 = (bf16*)smem;                                  // R0 after dw1
+  bf16* const sO = (bf16*)smem;                                   // R0 after dw2
+  bf16* const sA = (bf16*)(smem + G::R0);                         // R1: A1, later A2
+  bf16* const sW1 = (bf16*)(smem + G::R0 + G::R1);
+  bf16* const sW2 = (bf16*)(smem + G::R0 + G::R1 + G::W1_B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntx = (Wo + TW - 1) / TW, nty = (Ho + TH - 1) / TH, per = ntx * nty, ntiles = per * imgs;
+  for (int e = tid; e < N1 * K18; e += 256) {
+    const int row = e / K18, c = e % K18;
+    *(u32x4*)(sW1 + (c >> 2) * N1 * 32 + gidx(row, c & 3)) = *(const u32x4*)(Wt1 + (int64_t)row * K1 + c * 8);
+  }
+  for (int e = tid; e < N2 * N18; e += 256) {
+    const int row = e / N18, c = e % N18;
+    *(u32x4*)(sW2 + (c >> 2) * N2 * 32 + gidx(row, c & 3)) = *(const u32x4*)(Wt2 + (int64_t)row * N1 + c * 8);
+  }
+  const int c8a = tid % K18, c8b = tid % N18;  // this thread's channel groups in dw1 / dw2
+  // dw1's paired weights stay in registers; dw2's (and both biases) are re-read per tile (L1 hits):
+  // holding both sets spilled at the 2-workgroups-per-CU register budget
+  uint32_t wr1[5][8];
+  load_dw_weights(dwp1 + c8a * 8, K1, wr1);
+  u32x4 hr[NH];
+  // halo of tile t: conv0 rows 2 Y0 - 2 .. 2 Y0 + 2 TH, columns 2 X0 - 2 .. 2 X0 + 2 TW (zero outside)
+  auto gload = [&](int t) {
+    const int n = t / per, r = t - n * per;
+    const int iy0 = (r / ntx) * TH * 2 - 2, ix0 = (r % ntx) * TW * 2 - 2;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(x + (int64_t)n * H * W * K1), (short)0, H * W * K1 * 2,
+                                                      0x00020000);
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+      const int e = tid + i * 256;
+      if (e < NE) {
+        const int c = e % K18, px = e / K18, hx = px % HW, hy = px / HW;
+        const int iy = iy0 + hy, ix = ix0 + hx;
+        const int off = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? ((iy * W + ix) * K1 + c * 8) * 2 : (int)0x80000000;
+        hr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      }
+    }
+  };
+  if ((int)blockIdx.x < ntiles) gload(blockIdx.x);
+  const int fr = lane & 15, fc = lane >> 4;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int n = t / per, r = t - n * per, oy0 = (r / ntx) * TH, ox0 = (r % ntx) * TW;
+    // 1. halo (registers) -> R0
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+      const int e = tid + i * 256;
+      if (e < NE) *(u32x4*)(r0 + e * 16) = hr[i];
+    }
+    __syncthreads();
+    // 2. dw1 over the conv1 region (PH x PW pixels) -> A1 (KS1 slices of [MP16][32])
+#pragma unroll 1
+    for (int p = tid / K18; p < MP; p += 256 / K18) {
+      const int py = p / PW, px = p % PW;
+      u32x4 t9[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) t9[q] = *(const u32x4*)(r0 + (((py + q / 3) * HW + px + q % 3) * K1 + c8a * 8) * 2);
+      const f32x4 d1a = *(const f32x4*)(dwb1 + c8a * 8), d1b = *(const f32x4*)(dwb1 + c8a * 8 + 4);
+      float a[8] = {d1a[0], d1a[1], d1a[2], d1a[3], d1b[0], d1b[1], d1b[2], d1b[3]};
+      dw9_accum_w(t9, wr1, a);
+      *(u32x4*)(sA + (c8a >> 2) * MP16 * 32 + gidx(p, c8a & 3)) = dw_out8(a, dw1_relu);
+    }
+    __syncthreads();
+    // 3. pw1: wave w takes columns [w N1/4, (w+1) N1/4) of all MP16 rows, in two row passes (fewer live
+    //    accumulators: the kernel runs at 2 workgroups per CU); results -> P1 in R0 as [MP][N1] bf16
+    //    (+ bias, ReLU), pixels outside the image as 0
+    {
+      constexpr int NB = N1 / 64, MB = MP16 / 16, MBH = (MB + 1) / 2;
+      const int r1 = oy0 * 2 - 1, c1 = ox0 * 2 - 1;  // conv1 coordinates of P1's pixel (0, 0)
+#pragma unroll 1
+      for (int half = 0; half < 2; ++half) {
+        f32x4 acc[MBH][NB];
+#pragma unroll
+        for (int i = 0; i < MBH; ++i)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS1; ++ks) {
+          bf16x8s bw[NB];
+#pragma unroll
+          for (int j = 0; j < NB; ++j) bw[j] = *(const bf16x8s*)(sW1 + ks * N1 * 32 + gidx(wid * (N1 / 4) + j * 16 + fr, fc));
+#pragma unroll
+          for (int i = 0; i < MBH; ++i) {
+            const int ib = half * MBH + i;
+            if (ib >= MB) continue;
+            const bf16x8s af = *(const bf16x8s*)(sA + ks * MP16 * 32 + gidx(ib * 16 + fr, fc));
+#pragma unroll
+            for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af, acc[i][j], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int col = wid * (N1 / 4) + j * 16 + 4 * fc;
+          float bv[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bv[q] = pb1[col + q];
+#pragma unroll
+          for (int i = 0; i < MBH; ++i) {
+            const int px = (half * MBH + i) * 16 + fr;
+            if (px >= MP) continue;
+            const int yy = r1 + px / PW, xx = c1 + px % PW;
+            const bool in = yy >= 0 && yy < H && xx >= 0 && xx < W;
+            bf16x4 o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float v = acc[i][j][q] + bv[q];
+              o[q] = (bf16)(in ? (relu1 ? fmaxf(v, 0.f) : v) : 0.f);
+            }
+            *(bf16x4*)(sP1 + px * N1 + col) = o;
+          }
+        }
+      }
+    }
+    // 4. the next tile's halo loads go out now (R0's halo is dead since dw1) and land during the rest
+    if (t + (int)gridDim.x < ntiles) gload(t + gridDim.x);
+    __syncthreads();
+    // 5. dw2 (stride 2) from P1 -> A2 (KS2 slices of [MT][32]) in R1 (A1 is dead)
+    uint32_t wr2[5][8];
+    load_dw_weights(dwp2 + c8b * 8, N1, wr2);
+    const f32x4 d2a = *(const f32x4*)(dwb2 + c8b * 8), d2b = *(const f32x4*)(dwb2 + c8b * 8 + 4);
+#pragma unroll 1
+    for (int q = tid / N18; q < MT; q += 256 / N18) {
+      const int ty = q / TW, tx = q % TW;
+      u32x4 t9[9];
+#pragma unroll
+      for (int u = 0; u < 9; ++u)
+        t9[u] = *(const u32x4*)(sP1 + ((2 * ty + u / 3) * PW + 2 * tx + u % 3) * N1 + c8b * 8);
+      float a[8] = {d2a[0], d2a[1], d2a[2], d2a[3], d2b[0], d2b[1], d2b[2], d2b[3]};
+      dw9_accum_w(t9, wr2, a);
+      *(u32x4*)(sA + (c8b >> 2) * MT * 32 + gidx(q, c8b & 3)) = dw_out8(a, dw2_relu);
+    }
+    __syncthreads();
+    // 6. pw2: wave w takes columns [w N2/4, (w+1) N2/4); output staged in R0 (P1 is dead)
+    {
+      constexpr int NB = N2 / 64, MB = MT / 16, CH = N2 / 8;
+      f32x4 acc[MB][NB];
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS2; ++ks) {
+        bf16x8s bw[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) bw[j] = *(const bf16x8s*)(sW2 + ks * N2 * 32 + gidx(wid * (N2 / 4) + j * 16 + fr, fc));
+#pragma unroll
+        for (int i = 0; i < MB; ++i) {
+          const bf16x8s af = *(const bf16x8s*)(sA + ks * MT * 32 + gidx(i * 16 + fr, fc));
+#pragma unroll
+          for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af, acc[i][j], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int col = wid * (N2 / 4) + j * 16 + 4 * fc;
+        float bv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[q] = pb2[col + q];
+#pragma unroll
+        for (int i = 0; i < MB; ++i) {
+          const int px = i * 16 + fr;
+          bf16x4 o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v = acc[i][j][q] + bv[q];
+            o[q] = (bf16)(relu2 ? fmaxf(v, 0.f) : v);
+          }
+          *(bf16x4*)(sO + px * N2 + (((col >> 3) ^ (px & (CH - 1))) << 3) + (col & 4)) = o;
+        }
+      }
+      __syncthreads();
+      // 7. coalesced NHWC row segments
+      for (int e = tid; e < MT * CH; e += 256) {
+        const int px = e / CH, ch = e % CH, oy = oy0 + px / TW, ox = ox0 + px % TW;
+        if (oy >= Ho || ox >= Wo) continue;
+        *(u32x4*)(y + (((int64_t)n * Ho + oy) * Wo + ox) * N2 + ch * 8) =
+            *(const u32x4*)(sO + px * N2 + ((ch ^ (px & (CH - 1))) << 3));
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// =====================================================================================
 // K4: the stem, conv0 3x3 (stride 2, pad 1) over the 4-channel padded blob, as MFMA fed straight
 // from global memory: with K = 9 taps x 4 channels the v_mfma_f32_16x16x32_bf16 operand a lane
 // holds (8 consecutive k = two whole taps of one pixel) is exactly two 8-B loads, so neither an
@@ -1570,6 +1793,30 @@ void vcx_dw_pw(const void* x, const void* dw_w, const float* dw_b, int dw_relu, 
   OutMap om{nullptr, N, 0, M, 0, 0, nullptr, 0, nullptr};
   ConvGeom cg{H, W, K, K, Ho, Wo, 3, stride, 1, 9 * K, (const uint32_t*)dw_w, dw_b, dw_relu};
   launch_gba<AM_DW>((const bf16*)x, (const bf16*)Wt, bias, (bf16*)Y, M, N, K, N, relu, om, cg, nullptr, 1, nullptr, s);
+}
+
+// conv1 (dw s1 + pw K1 -> N1) and conv2 (dw s2 + pw N1 -> N2) of MobileNet as ONE kernel
+// (dwpw2_persist_kernel): x NHWC [imgs, H, W, K1] -> Y [imgs, Ho, Wo, N2], Ho = (H - 1) / 2 + 1.
+// Returns false (nothing launched) for shapes without an instance.
+bool vcx_dw_pw2(const void* x, const void* dw1_w, const float* dw1_b, int dw1_relu, const void* W1, const float* b1,
+                int relu1, const void* dw2_w, const float* dw2_b, int dw2_relu, const void* W2, const float* b2,
+                int relu2, void* Y, int imgs, int H, int W, int K1, int N1, int N2, hipStream_t s) {
+  if (!(K1 == 32 && N1 == 64 && N2 == 128) || (int64_t)H * W * K1 * 2 >= INT32_MAX) return false;
+  constexpr int TH = 8, TW = 8;
+  using G = Dwpw2<32, 64, 128, TH, TW>;
+  auto kern = dwpw2_persist_kernel<32, 64, 128, TH, TW>;
+  static const bool attr = [&] {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    return true;
+  }();
+  (void)attr;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int64_t tiles = (int64_t)((Wo + TW - 1) / TW) * ((Ho + TH - 1) / TH) * imgs;
+  const int grid = (int)std::min<int64_t>(tiles, (int64_t)2 * vision_cus());
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), G::LDS, s, (const bf16*)x, (const uint32_t*)dw1_w, dw1_b, dw1_relu,
+                     (const bf16*)W1, b1, relu1, (const uint32_t*)dw2_w, dw2_b, dw2_relu, (const bf16*)W2, b2, relu2,
+                     (bf16*)Y, H, W, Ho, Wo, imgs);
+  return true;
 }
 
 void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y, int M, int N, int K, int ldy,

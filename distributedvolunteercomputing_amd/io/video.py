@@ -21,7 +21,6 @@ from __future__ import annotations
 import functools
 import os
 import struct
-import threading
 from pathlib import Path
 
 import numpy as np
@@ -292,57 +291,6 @@ def open_source(spec: str) -> FrameSource:
 
 
 # ----------------------------------------------------------------------------- sinks
-class _Prealloc:
-    """Allocates a growing output file's blocks AHEAD of the writer on a thread of its own
-    (posix_fallocate, GIL released): the kernel's page allocation + zeroing of the next chunks' range
-    (~6 ms per 27 MB chunk on tmpfs, as long as the copy itself) then overlaps the writer's copy instead
-    of running inside it (profiles/r5_video_job.txt). The file is cut back to its data by ``finish``."""
-
-    def __init__(self, fd: int, ahead: int = 128 << 20, step: int = 32 << 20):
-        self.fd, self.ahead, self.step = fd, ahead, step
-        self.end = self.want = 0
-        self.ok = True
-        self._cv = threading.Condition()
-        self._stop = False
-        self._t = threading.Thread(target=self._run, name="vcx-sink-prealloc", daemon=True)
-        self._t.start()
-
-    def need(self, upto: int):
-        with self._cv:
-            if upto + self.ahead > self.want:
-                self.want = upto + self.ahead
-                self._cv.notify()
-
-    def _run(self):
-        while True:
-            with self._cv:
-                while not self._stop and self.want <= self.end:
-                    self._cv.wait()
-                if self._stop:
-                    return
-                lo, hi = self.end, min(self.want, self.end + self.step)
-            try:
-                os.posix_fallocate(self.fd, lo, hi - lo)
-            except OSError:  # e.g. a filesystem without fallocate: the writes allocate as they go
-                self.ok = False
-                return
-            with self._cv:
-                self.end = hi
-
-    def finish(self, size: int):
-        with self._cv:
-            self._stop = True
-            self._cv.notify()
-        self._t.join()
-        os.ftruncate(self.fd, size)  # drop the blocks allocated past the data
-
-
-def _prealloc(f, path):
-    from .. import config
-
-    return _Prealloc(f.fileno()) if config.get().sink_prealloc and os.path.isfile(path) else None
-
-
 def _frame_writer():
     """The C++ runtime's threaded positional frame writer (csrc/runtime/colour.cpp write_frames), or None."""
     rt = _rt()
@@ -361,7 +309,6 @@ class Y4MWriter:
         os.pwrite(self.f.fileno(), hdr, 0)
         self.off = len(hdr)
         self.frames = 0
-        self._pre = _prealloc(self.f, self.path)
 
     def write(self, frame: np.ndarray):
         if frame.shape[0] != self.h or frame.shape[1] != self.w:
@@ -381,15 +328,11 @@ class Y4MWriter:
                 self.write(f)
             return
         block = _as_block(frames)
-        if self._pre is not None:
-            self._pre.need(self.off + len(block) * (6 + 3 * self.w * self.h))
         self.off += rt.write_frames(self.f.fileno(), self.off, block, len(block), self.w, self.h, True)
         self.frames += len(frames)
 
     def release(self):
         if self.f and not self.f.closed:
-            if self._pre is not None:
-                self._pre.finish(self.off)
             self.f.close()
 
 
@@ -405,7 +348,6 @@ class NpyWriter:
         self.f = open(self.path, "wb")
         self.frames = 0
         os.pwrite(self.f.fileno(), self._header(0), 0)
-        self._pre = _prealloc(self.f, self.path)
 
     def _header(self, n):
         d = "{'descr': '|u1', 'fortran_order': False, 'shape': (%d, %d, %d, 3), }" % (n, self.h, self.w)
@@ -417,8 +359,6 @@ class NpyWriter:
             raise ValueError(f"frames {block.dtype} {block.shape[1:]} do not match writer {self.h}x{self.w}")
         block = np.ascontiguousarray(block)
         off = self.HEADER + self.frames * 3 * self.w * self.h
-        if self._pre is not None:
-            self._pre.need(off + block.nbytes)
         rt = _frame_writer()
         if rt is not None:
             rt.write_frames(self.f.fileno(), off, block, len(block), self.w, self.h, False)
@@ -437,8 +377,6 @@ class NpyWriter:
     def release(self):
         if self.f and not self.f.closed:
             os.pwrite(self.f.fileno(), self._header(self.frames), 0)
-            if self._pre is not None:
-                self._pre.finish(self.HEADER + self.frames * 3 * self.w * self.h)
             self.f.close()
 
 

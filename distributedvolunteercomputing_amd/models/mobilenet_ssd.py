@@ -341,6 +341,27 @@ class SSDExecutor:
                     continue
             out.append(plan[i])
             i += 1
+        return self._fuse_block_pairs(out, uses) if mode != "tile1" and os.environ.get("VCX_DWPW2", "1") != "0" else out
+
+    @staticmethod
+    def _fuse_block_pairs(plan, uses):
+        """conv1 -> conv2 (a stride-1 block 32 -> 64 followed by a stride-2 block 64 -> 128, the 150^2 ->
+        75^2 step of MobileNet, prototxt 42-106) as ONE `dwpw2` step whose kernel keeps conv1's output
+        in LDS (ops.vision.dw_pw2); VCX_DWPW2=0 keeps two steps."""
+        out, i = [], 0
+        while i < len(plan):
+            st = plan[i]
+            if st[0] == "dwpw" and i + 1 < len(plan) and plan[i + 1][0] == "dwpw":
+                a, b = st[2], plan[i + 1][2]
+                shapes = (a["dw"]["w"].shape[1], a["pw"]["w"].shape[0], a["dw"]["stride"],
+                          b["dw"]["w"].shape[1], b["pw"]["w"].shape[0], b["dw"]["stride"])
+                if (shapes == (32, 64, 1, 64, 128, 2) and b["src"] == st[1].tops[0]
+                        and uses.get(st[1].tops[0], 0) == 1):
+                    out.append(("dwpw2", plan[i + 1][1], dict(b1=a, b2=b, src=a["src"])))
+                    i += 2
+                    continue
+            out.append(st)
+            i += 1
         return out
 
     # ------------------------------------------------------------------ helpers
@@ -398,6 +419,11 @@ class SSDExecutor:
             elif kind == "dwpw":
                 d, q = p["dw"], p["pw"]
                 y = V.dw_pw(t[p["src"]], d["w"], d["b"], d["relu"], d["stride"], q["w"], q["b"], q["relu"])
+                t[top], layout[top], hw[top], chans[top] = y, "nhwc", (y.shape[1], y.shape[2]), y.shape[3]
+            elif kind == "dwpw2":
+                blk = [dict(dw_w=p[k]["dw"]["w"], dw_b=p[k]["dw"]["b"], dw_relu=p[k]["dw"]["relu"], w=p[k]["pw"]["w"],
+                            b=p[k]["pw"]["b"], relu=p[k]["pw"]["relu"]) for k in ("b1", "b2")]
+                y = V.dw_pw2(t[p["src"]], blk[0], blk[1])
                 t[top], layout[top], hw[top], chans[top] = y, "nhwc", (y.shape[1], y.shape[2]), y.shape[3]
             elif kind == "pw":
                 H, W = hw[src]

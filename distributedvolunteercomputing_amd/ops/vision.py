@@ -156,6 +156,20 @@ def dw_pw(x, wp, db, dw_relu, stride, Wt, bias, relu=True):
     return gemm_bias_act(d.reshape(-1, K), Wt, bias, relu).view(N, Ho, Wo, -1)
 
 
+def dw_pw2(x, b1, b2):
+    """Two MobileNet blocks (conv1: depthwise s1 + pointwise, conv2: depthwise s2 + pointwise) as ONE
+    kernel where an instance exists (csrc/kernels/vision.hip dwpw2_persist_kernel: the first block's
+    output stays in LDS), else the two fused-block kernels. b1 / b2: dicts with the depthwise paired
+    weights / bias / relu ("dw_w", "dw_b", "dw_relu") and the pointwise "w", "b", "relu" of each block."""
+    if use_native(x):
+        y = native().dw_pw2(x, b1["dw_w"], b1["dw_b"], b1["dw_relu"], b1["w"], b1["b"], b1["relu"],
+                            b2["dw_w"], b2["dw_b"], b2["dw_relu"], b2["w"], b2["b"], b2["relu"])
+        if y is not None and y.numel() > 0:
+            return y
+    h = dw_pw(x, b1["dw_w"], b1["dw_b"], b1["dw_relu"], 1, b1["w"], b1["b"], b1["relu"])
+    return dw_pw(h, b2["dw_w"], b2["dw_b"], b2["dw_relu"], 2, b2["w"], b2["b"], b2["relu"])
+
+
 def gemm_bias_act(X, Wt, bias=None, relu=False):
     """Y = act(X . Wt^T + bias): X [M,K], Wt [N,K] bf16, bias [N] fp32 -> [M,N] bf16."""
     if use_native(X):
