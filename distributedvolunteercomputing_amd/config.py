@@ -46,6 +46,7 @@ class RuntimeConfig:
     # VCX_REGISTER_SOURCE: a requester page-locks a memory-mapped source (hipHostRegister) and uploads
     # chunks straight from it (False: each chunk is copied into pinned memory first)
     register_source: bool = True
+    sink_gpu: bool = True  # VCX_SINK_GPU: a GPU requester converts its Y4M output on the GPU (False: on the host)
     resnet_conv1x1: str = "gemm"  # VCX_RESNET_CONV1X1: ResNet 1x1 convolutions as GEMMs on the NHWC view ("gemm")
     # or through the convolution library ("conv")
     # VCX_CONV_FIND: library (MIOpen) convolutions of the ResNets pick the fastest solver per shape by
@@ -101,6 +102,7 @@ _ENV = {
     "offload_arch": ("VCX_OFFLOAD_ARCH", str),
     "colour_native": ("VCX_COLOUR_NATIVE", _bool),
     "register_source": ("VCX_REGISTER_SOURCE", _bool),
+    "sink_gpu": ("VCX_SINK_GPU", _bool),
     "gloo_host": ("VCX_GLOO_HOST", str),
     "p2p_backend": ("VCX_P2P_BACKEND", str),
     "elastic_debug": ("VCX_ELASTIC_DEBUG", _bool),

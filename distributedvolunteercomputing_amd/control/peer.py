@@ -231,7 +231,8 @@ class client:  # noqa: N801 (reference class name)
             self.metrics.observe("job_s", dt)
             print(f"final frame time taken for the job = {dt}", flush=True)
 
-        self.sink = OrderedSink(lambda w, h: open_sink(out_path, w, h, 30), on_done=done)
+        sink_dev = self.resize_device if config.get().sink_gpu else None
+        self.sink = OrderedSink(lambda w, h: open_sink(out_path, w, h, 30, device=sink_dev), on_done=done)
         self.start_time = time.time()
         n = 0
         C = self.number_of_frames_in_chunk

@@ -205,6 +205,16 @@ at::Tensor dw_pw2(at::Tensor x, at::Tensor dw1_w, at::Tensor dw1_b, bool dw1_rel
   return Y;
 }
 
+// k BGR frames [k, h, w, 3] uint8 -> their Y4M 4:4:4 records (FRAME header + planes), uint8 [k * (6 + 3 h w)]
+at::Tensor bgr_to_y4m(at::Tensor frames) {
+  CHK(frames, at::kByte);
+  TORCH_CHECK(frames.dim() == 4 && frames.size(3) == 3 && frames.numel() < ((int64_t)1 << 40), "frames [k, h, w, 3] uint8");
+  const int64_t k = frames.size(0), h = frames.size(1), w = frames.size(2);
+  auto out = at::empty({k * (6 + 3 * h * w)}, frames.options());
+  if (k > 0) vcx_bgr_to_y4m(frames.data_ptr<uint8_t>(), out.data_ptr<uint8_t>(), (int)k, (int)w, (int)h, cur_stream());
+  return out;
+}
+
 // KxK convolution as an implicit GEMM (no im2col matrix): x NHWC bf16 [imgs, H, W, Cs] using
 // its first C channels (C % 8 == 0, or C == 4 == Cs), Wt [N, Kp] columns (ky, kx, c)
 at::Tensor conv_implicit(at::Tensor x, at::Tensor Wt, at::Tensor bias, int64_t C, int64_t KH, int64_t KW,
@@ -288,6 +298,7 @@ void vcx_register_vision(pybind11::module& m) {
   m.def("gemm_bias_heads", &gemm_bias_heads);
   m.def("dw_pw", &dw_pw);
   m.def("dw_pw2", &dw_pw2);
+  m.def("bgr_to_y4m", &bgr_to_y4m);
   m.def("conv_implicit", &conv_implicit);
   m.def("ssd_detect", &ssd_detect);
   m.def("annotate", &annotate);

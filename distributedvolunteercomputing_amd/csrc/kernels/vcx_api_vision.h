@@ -28,6 +28,7 @@ void vcx_gemm_bias_act(const void* X, const void* Wt, const float* bias, void* Y
 void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const float* var, float* prob,
                     float* cls_out, int* cls_cnt, float* out, int* out_cnt, int N, int P, int C, int bg, float thresh,
                     float nms_thresh, int topk, int keep, hipStream_t s);
+void vcx_bgr_to_y4m(const uint8_t* bgr, uint8_t* out, int k, int w, int h, hipStream_t s);
 void vcx_annotate(uint8_t* frames, int N, int h, int w, const float* dets, const int* det_cnt, int keep, int label,
                   float thresh, uint32_t box_bgr, const uint8_t* name_mask, int nm_h, int nm_w, int nm_x, int nm_y,
                   uint32_t name_bgr, const uint8_t* lab_masks, int lm_n, int lm_h, int lm_w, int lm_x, int lm_y,

@@ -1834,6 +1834,38 @@ void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const f
   hipLaunchKernelGGL(ssd_merge_kernel, dim3(N), dim3(256), 0, s, cls_out, cls_cnt, out, out_cnt, C, bg, topk, keep);
 }
 
+// Y4M 4:4:4 records of k annotated BGR frames [k, h, w, 3] on the GPU: per frame "FRAME\n" + the Y, U and
+// V planes, laid out exactly as the file bytes (the requester's sink then only writes them). BT.601 full
+// range with the host formulas' float operations in the same order and IEEE rounding at each step
+// (__fmul_rn / __fadd_rn: no contraction), so the bytes equal csrc/runtime/colour.cpp and io/video.py.
+// One thread per pixel; the host conversion of a 100-frame chunk held the sink 16-25 ms per chunk
+// (profiles/r5_video_job.txt).
+__device__ __forceinline__ uint8_t sat_u8(float x) {
+  x = __fadd_rn(x, 0.5f);
+  x = x < 0.f ? 0.f : (x > 255.f ? 255.f : x);
+  return (uint8_t)x;
+}
+__global__ void __launch_bounds__(256) bgr_to_y4m_kernel(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ out,
+                                                         int64_t n, int64_t total) {
+  const int64_t rec = 6 + 3 * n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t f = i / n, px = i - f * n;
+    const uint8_t* src = bgr + 3 * i;
+    const float b = src[0], g = src[1], r = src[2];
+    const float y = __fadd_rn(__fadd_rn(__fmul_rn(0.299f, r), __fmul_rn(0.587f, g)), __fmul_rn(0.114f, b));
+    uint8_t* o = out + f * rec + 6;
+    o[px] = sat_u8(y);
+    o[n + px] = sat_u8(__fadd_rn(__fmul_rn(__fsub_rn(b, y), 0.564f), 128.0f));
+    o[2 * n + px] = sat_u8(__fadd_rn(__fmul_rn(__fsub_rn(r, y), 0.713f), 128.0f));
+    if (px < 6) out[f * rec + px] = (uint8_t)("FRAME\n"[px]);
+  }
+}
+
+void vcx_bgr_to_y4m(const uint8_t* bgr, uint8_t* out, int k, int w, int h, hipStream_t s) {
+  const int64_t n = (int64_t)w * h, total = n * k;
+  hipLaunchKernelGGL(bgr_to_y4m_kernel, dim3(stream_grid(total, 256)), dim3(256), 0, s, bgr, out, n, total);
+}
+
 void vcx_annotate(uint8_t* frames, int N, int h, int w, const float* dets, const int* det_cnt, int keep, int label,
                   float thresh, uint32_t box_bgr, const uint8_t* name_mask, int nm_h, int nm_w, int nm_x, int nm_y,
                   uint32_t name_bgr, const uint8_t* lab_masks, int lm_n, int lm_h, int lm_w, int lm_x, int lm_y,

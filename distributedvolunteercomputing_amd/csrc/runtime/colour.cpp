@@ -158,6 +158,33 @@ static void y4m_record(const uint8_t* src, uint8_t* r, int64_t n) {
   }
 }
 
+// `n` bytes at `off` of fd: a regular file grown and the range mapped and filled on up to 8 threads
+// (the Y4M records converted on the GPU arrive as bytes), else one positional write
+int64_t write_bytes(int fd, int64_t off, const uint8_t* src, int64_t n) {
+  if (n <= 0) return 0;
+  struct stat st{};
+  if (::fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
+    if (st.st_size < off + n && ::ftruncate(fd, (off_t)(off + n)) != 0)
+      throw std::runtime_error(std::string("write_bytes: ftruncate: ") + std::strerror(errno));
+    const int64_t pg = ::sysconf(_SC_PAGESIZE), base = off - off % pg, len = off + n - base;
+    void* m = ::mmap(nullptr, (size_t)len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, (off_t)base);
+    if (m != MAP_FAILED) {
+      uint8_t* dst = (uint8_t*)m + (off - base);
+      const int64_t parts = std::max<int64_t>(1, std::min<int64_t>(8, n >> 20));  // >= 1 MB per thread
+      const int64_t per = (n + parts - 1) / parts;
+      parallel_frames(parts, [&](int64_t p0, int64_t p1) {
+        const int64_t a = p0 * per, b = std::min(n, p1 * per);
+        if (a < b) std::memcpy(dst + a, src + a, (size_t)(b - a));
+      });
+      ::munmap(m, (size_t)len);
+      return n;
+    }
+  }
+  const int e = pwrite_all(fd, src, n, off);
+  if (e) throw std::runtime_error(std::string("write_bytes: ") + std::strerror(e));
+  return n;
+}
+
 int64_t write_frames(int fd, int64_t off, const uint8_t* bgr, int64_t k, int64_t w, int64_t h, bool y4m) {
   // k BGR frames [k, h, w, 3] at byte offset `off` of fd, as raw frames (npy body) or as Y4M 4:4:4
   // records ("FRAME\n" + Y, U, V planes). A regular file is grown to cover the range and the range is

@@ -19,5 +19,7 @@ void yuv_to_bgr(const uint8_t* y, const uint8_t* u, const uint8_t* v, uint8_t* b
 // range mapped and filled on several threads, anything else gets one positional write;
 // returns the bytes written (throws std::runtime_error on a write error)
 int64_t write_frames(int fd, int64_t off, const uint8_t* bgr, int64_t k, int64_t w, int64_t h, bool y4m);
+// n bytes at `off` of fd (a regular file through a shared mapping filled on several threads); returns n
+int64_t write_bytes(int fd, int64_t off, const uint8_t* src, int64_t n);
 
 }  // namespace vcxrt

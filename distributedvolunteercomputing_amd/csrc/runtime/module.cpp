@@ -184,6 +184,16 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("src"), py::arg("dst"), py::arg("k"), py::arg("w"), py::arg("h"));
   m.def(
+      "write_bytes",
+      [](int fd, int64_t off, py::buffer src) {
+        py::buffer_info a = src.request();
+        require_c_contiguous(a, "write_bytes src");
+        if (off < 0) throw std::invalid_argument("write_bytes: negative offset");
+        const int64_t n = a.size * a.itemsize;
+        return without_gil([&] { return write_bytes(fd, off, (const uint8_t*)a.ptr, n); });
+      },
+      py::arg("fd"), py::arg("off"), py::arg("src"));
+  m.def(
       "write_frames",
       [](int fd, int64_t off, py::buffer src, int64_t k, int64_t w, int64_t h, bool y4m) {
         py::buffer_info a = src.request();

@@ -300,9 +300,13 @@ def _frame_writer():
 class Y4MWriter:
     """YUV4MPEG2 4:4:4 writer (cv2.VideoWriter replacement). Every write is positional (os.pwrite at the
     writer's running offset); a received chunk's frames go through ONE native call that converts and
-    writes frame ranges on several threads with the GIL released."""
+    writes frame ranges on several threads with the GIL released. With `device` (a GPU requester) the
+    chunk's records are converted there (csrc/kernels/vision.hip bgr_to_y4m: the same bytes) and come
+    back through pinned memory, so the host only copies them into the file."""
 
-    def __init__(self, path, width, height, fps=30):
+    def __init__(self, path, width, height, fps=30, device=None):
+        self.device = device
+        self._pin = None
         self.path, self.w, self.h = str(path), int(width), int(height)
         self.f = open(self.path, "wb")
         hdr = f"YUV4MPEG2 W{self.w} H{self.h} F{int(fps)}:1 Ip A1:1 C444\n".encode()
@@ -328,8 +332,25 @@ class Y4MWriter:
                 self.write(f)
             return
         block = _as_block(frames)
-        self.off += rt.write_frames(self.f.fileno(), self.off, block, len(block), self.w, self.h, True)
+        if self.device is not None and hasattr(rt, "write_bytes"):
+            self.off += rt.write_bytes(self.f.fileno(), self.off, self._gpu_records(block))
+        else:
+            self.off += rt.write_frames(self.f.fileno(), self.off, block, len(block), self.w, self.h, True)
         self.frames += len(frames)
+
+    def _gpu_records(self, block: np.ndarray) -> np.ndarray:
+        import torch
+
+        from ..ops._lib import native
+
+        with torch.cuda.device(self.device):
+            d = torch.from_numpy(np.ascontiguousarray(block)).to(self.device)
+            rec = native().bgr_to_y4m(d)
+            if self._pin is None or self._pin.numel() < rec.numel():
+                self._pin = torch.empty(rec.numel(), dtype=torch.uint8, pin_memory=True)
+            h = self._pin[: rec.numel()]
+            h.copy_(rec)
+        return h.numpy()
 
     def release(self):
         if self.f and not self.f.closed:
@@ -396,12 +417,13 @@ class PngDirWriter:
         pass
 
 
-def open_sink(path, width, height, fps=30):
+def open_sink(path, width, height, fps=30, device=None):
+    """device: a GPU on which a Y4M sink converts its frames (None: on the host)."""
     s = str(path)
     if s.endswith(".npy"):
         return NpyWriter(path, width, height, fps)
     if s.endswith(".y4m"):
-        return Y4MWriter(path, width, height, fps)
+        return Y4MWriter(path, width, height, fps, device=device)
     if os.path.splitext(s)[1] == "":
         return PngDirWriter(path, width, height, fps)
-    return Y4MWriter(s + ".y4m", width, height, fps)
+    return Y4MWriter(s + ".y4m", width, height, fps, device=device)

@@ -4,6 +4,7 @@ chunk data planes. Checks the in-order 400-px output and that every frame went t
 worker; on the p2p plane that no chunk byte crossed the coordinator."""
 import numpy as np
 import pytest
+import torch
 
 from distributedvolunteercomputing_amd.control.coordinator import coordinator
 from distributedvolunteercomputing_amd.control.peer import client
@@ -46,3 +47,24 @@ def test_video_job_detector_engine(gpu, tmp_path, plane):
         for c in (req, w1, w2):
             c.exit_threads()
         coord.exit_threads()
+
+
+def test_y4m_sink_gpu_records_equal_host(tmp_path):
+    """The Y4M sink's GPU conversion (csrc/kernels/vision.hip bgr_to_y4m) writes the same bytes as the host
+    conversion (csrc/runtime/colour.cpp), odd sizes and a partial last write included."""
+    import numpy as np
+
+    from distributedvolunteercomputing_amd.io.video import Y4MWriter
+
+    rng = np.random.default_rng(7)
+    frames = rng.integers(0, 256, (23, 37, 53, 3), dtype=np.uint8)
+    paths = []
+    for dev in (None, torch.device("cuda", 0)):
+        p = tmp_path / f"{'gpu' if dev is not None else 'host'}.y4m"
+        w = Y4MWriter(p, 53, 37, device=dev)
+        w.write_many(list(frames[:10]))
+        w.write(frames[10])
+        w.write_many(list(frames[11:]))
+        w.release()
+        paths.append(p)
+    assert paths[0].read_bytes() == paths[1].read_bytes()
