@@ -36,10 +36,23 @@ import time  # noqa: E402
 _t0 = time.time()
 
 
+def _merged_lines():
+    lines = open(RESULTS).read().splitlines()
+    have = {tuple(ln.split(",")[:2]) for ln in lines if ln and not ln.startswith("Validator")}
+    new = [f"{r[0]},{r[1]},{r[2]},{r[3]}" for r in torch.cuda.tunable.get_results() if (r[0], r[1]) not in have]
+    return lines, new
+
+
 def _heartbeat():  # tuning a big GEMM shape takes tens of seconds with no output of its own
     while True:
         time.sleep(30)
-        print(f"[tune] {time.time() - _t0:.0f} s", flush=True)
+        try:  # the winners so far, so a run stopped at its time limit keeps what it tuned
+            lines, new = _merged_lines()
+            with open(out_csv + ".partial", "w") as f:
+                f.write("\n".join(lines + new) + "\n")
+        except Exception as e:  # noqa: BLE001
+            new = [f"(partial write failed: {e})"]
+        print(f"[tune] {time.time() - _t0:.0f} s, {len(new)} new entries so far", flush=True)
 
 
 threading.Thread(target=_heartbeat, daemon=True).start()
@@ -87,10 +100,7 @@ if "5" in configs:
     _steps(tr, t[:, :-1], t[:, 1:], 5)
     del m, tr, t
     torch.cuda.empty_cache()
-res = torch.cuda.tunable.get_results()
-lines = open(RESULTS).read().splitlines()
-have = {tuple(ln.split(",")[:2]) for ln in lines if ln and not ln.startswith("Validator")}
-new = [f"{r[0]},{r[1]},{r[2]},{r[3]}" for r in res if (r[0], r[1]) not in have]
+lines, new = _merged_lines()
 print(f"{len(new)} new entries:", *new, sep="\n", flush=True)
 with open(out_csv, "w") as f:
     f.write("\n".join(lines + new) + "\n")
