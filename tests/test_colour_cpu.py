@@ -65,3 +65,40 @@ def test_y4m_write_many_matches_per_frame(tmp_path, k, h, w):
     ra, rb, rc = ((tmp_path / f"{n}.y4m").read_bytes() for n in "abc")
     assert ra == rb == rc
     assert len(ra) > k * 3 * h * w
+
+
+@pytest.mark.parametrize("chunks", [[5], [3, 1, 7], [1, 1, 1, 1]])
+def test_npy_sink_streams_and_finalises_header(tmp_path, chunks):
+    """The npy sink writes each chunk at its offset as it arrives (threaded positional writes into the
+    page cache) and rewrites the header with the final frame count on release: np.load reads it back."""
+    rng = np.random.default_rng(len(chunks))
+    n = sum(chunks)
+    frames = rng.integers(0, 256, (n, 19, 23, 3), dtype=np.uint8)
+    w = V.NpyWriter(tmp_path / "o.npy", 23, 19)
+    i = 0
+    for c in chunks:
+        if c == 1:
+            w.write(frames[i])
+        else:
+            w.write_many(list(frames[i:i + c]))
+        i += c
+    w.release()
+    out = np.load(tmp_path / "o.npy")
+    assert out.shape == frames.shape and np.array_equal(out, frames)
+    assert (tmp_path / "o.npy").stat().st_size == V.NpyWriter.HEADER + frames.nbytes
+
+
+def test_native_write_bytes_positional(tmp_path):
+    """write_bytes: a regular file grows to cover the range and keeps the bytes before it."""
+    from distributedvolunteercomputing_amd._native_loader import native
+
+    rt = native()
+    p = tmp_path / "b.bin"
+    data = np.random.default_rng(1).integers(0, 256, 3 << 20, dtype=np.uint8)
+    with open(p, "wb") as f:
+        f.write(b"head")
+        assert rt.write_bytes(f.fileno(), 100, data) == data.nbytes
+        assert rt.write_bytes(f.fileno(), 100 + data.nbytes, data[:7]) == 7
+    b = p.read_bytes()
+    assert b[:4] == b"head" and b[4:100] == bytes(96)
+    assert b[100:100 + data.nbytes] == data.tobytes() and b[100 + data.nbytes:] == data[:7].tobytes()
