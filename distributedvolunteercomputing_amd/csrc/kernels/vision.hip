@@ -1053,7 +1053,9 @@ struct Dwpw2 {
   static constexpr int R0 = (HALO_B > P1_B ? (HALO_B > OUT_B ? HALO_B : OUT_B) : (P1_B > OUT_B ? P1_B : OUT_B));
   static constexpr int A1_B = MP16 * K1 * 2, A2_B = MT * N1 * 2, R1 = A1_B > A2_B ? A1_B : A2_B;
   static constexpr int W1_B = N1 * K1 * 2, W2_B = N2 * N1 * 2;
-  static constexpr int LDS = R0 + R1 + W1_B + W2_B;
+  // dw2's paired weights [5][N1] dwords, then the fp32 biases dw2 [N1], pw1 [N1], pw2 [N2]
+  static constexpr int C_B = 5 * N1 * 4 + (2 * N1 + N2) * 4;
+  static constexpr int LDS = R0 + R1 + W1_B + W2_B + C_B;
   static constexpr int NE = HH * HW * (K1 / 8), NH = (NE + 255) / 256;  // halo 16-B pieces (per thread)
 };
 
@@ -1076,7 +1078,11 @@ dwpw2_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dw
   bf16* const sA = (bf16*)(smem + G::R0);                         // R1: A1, later A2
   bf16* const sW1 = (bf16*)(smem + G::R0 + G::R1);
   bf16* const sW2 = (bf16*)(smem + G::R0 + G::R1 + G::W1_B);
+  uint32_t* const sDw2 = (uint32_t*)(smem + G::R0 + G::R1 + G::W1_B + G::W2_B);  // [5][N1] paired dw2 weights
+  float* const sB = (float*)(sDw2 + 5 * N1);  // dw2 bias [N1] | pw1 bias [N1] | pw2 bias [N2]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int e = tid; e < 5 * N1; e += 256) sDw2[e] = dwp2[e];
+  for (int e = tid; e < 2 * N1 + N2; e += 256) sB[e] = e < N1 ? dwb2[e] : (e < 2 * N1 ? pb1[e - N1] : pb2[e - 2 * N1]);
   const int ntx = (Wo + TW - 1) / TW, nty = (Ho + TH - 1) / TH, per = ntx * nty, ntiles = per * imgs;
   for (int e = tid; e < N1 * K18; e += 256) {
     const int row = e / K18, c = e % K18;
@@ -1165,7 +1171,7 @@ dwpw2_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dw
           const int col = wid * (N1 / 4) + j * 16 + 4 * fc;
           float bv[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) bv[q] = pb1[col + q];
+          for (int q = 0; q < 4; ++q) bv[q] = sB[N1 + col + q];
 #pragma unroll
           for (int i = 0; i < MBH; ++i) {
             const int px = (half * MBH + i) * 16 + fr;
@@ -1178,7 +1184,9 @@ dwpw2_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dw
               const float v = acc[i][j][q] + bv[q];
               o[q] = (bf16)(in ? (relu1 ? fmaxf(v, 0.f) : v) : 0.f);
             }
-            *(bf16x4*)(sP1 + px * N1 + col) = o;
+            // P1 rows are 128 B: the 16-B chunk index is XOR-swizzled by the pixel (else the 16 rows of an
+            // MFMA block land on the same banks)
+            *(bf16x4*)(sP1 + px * N1 + (((col >> 3) ^ (px & 7)) << 3) + (col & 4)) = o;
           }
         }
       }
@@ -1188,15 +1196,17 @@ dwpw2_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dw
     __syncthreads();
     // 5. dw2 (stride 2) from P1 -> A2 (KS2 slices of [MT][32]) in R1 (A1 is dead)
     uint32_t wr2[5][8];
-    load_dw_weights(dwp2 + c8b * 8, N1, wr2);
-    const f32x4 d2a = *(const f32x4*)(dwb2 + c8b * 8), d2b = *(const f32x4*)(dwb2 + c8b * 8 + 4);
+    load_dw_weights(sDw2 + c8b * 8, N1, wr2);
+    const f32x4 d2a = *(const f32x4*)(sB + c8b * 8), d2b = *(const f32x4*)(sB + c8b * 8 + 4);
 #pragma unroll 1
     for (int q = tid / N18; q < MT; q += 256 / N18) {
       const int ty = q / TW, tx = q % TW;
       u32x4 t9[9];
 #pragma unroll
-      for (int u = 0; u < 9; ++u)
-        t9[u] = *(const u32x4*)(sP1 + ((2 * ty + u / 3) * PW + 2 * tx + u % 3) * N1 + c8b * 8);
+      for (int u = 0; u < 9; ++u) {
+        const int pp = (2 * ty + u / 3) * PW + 2 * tx + u % 3;
+        t9[u] = *(const u32x4*)(sP1 + pp * N1 + ((c8b ^ (pp & 7)) << 3));
+      }
       float a[8] = {d2a[0], d2a[1], d2a[2], d2a[3], d2b[0], d2b[1], d2b[2], d2b[3]};
       dw9_accum_w(t9, wr2, a);
       *(u32x4*)(sA + (c8b >> 2) * MT * 32 + gidx(q, c8b & 3)) = dw_out8(a, dw2_relu);
@@ -1227,7 +1237,7 @@ dwpw2_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dw
         const int col = wid * (N2 / 4) + j * 16 + 4 * fc;
         float bv[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) bv[q] = pb2[col + q];
+        for (int q = 0; q < 4; ++q) bv[q] = sB[2 * N1 + col + q];
 #pragma unroll
         for (int i = 0; i < MB; ++i) {
           const int px = i * 16 + fr;
@@ -1836,27 +1846,30 @@ void vcx_ssd_detect(const void* conf, const void* loc, const float* pri, const f
 
 // Y4M 4:4:4 records of k annotated BGR frames [k, h, w, 3] on the GPU: per frame "FRAME\n" + the Y, U and
 // V planes, laid out exactly as the file bytes (the requester's sink then only writes them). BT.601 full
-// range with the host formulas' float operations in the same order and IEEE rounding at each step
-// (__fmul_rn / __fadd_rn: no contraction), so the bytes equal csrc/runtime/colour.cpp and io/video.py.
+// range with the host formulas' float operations in the same order and IEEE rounding at each step (plain
+// operators under `fp contract(off)`: an fma would round once and move some bytes by one), so the bytes
+// equal csrc/runtime/colour.cpp and io/video.py.
 // One thread per pixel; the host conversion of a 100-frame chunk held the sink 16-25 ms per chunk
 // (profiles/r5_video_job.txt).
 __device__ __forceinline__ uint8_t sat_u8(float x) {
-  x = __fadd_rn(x, 0.5f);
+#pragma clang fp contract(off)
+  x = x + 0.5f;
   x = x < 0.f ? 0.f : (x > 255.f ? 255.f : x);
   return (uint8_t)x;
 }
 __global__ void __launch_bounds__(256) bgr_to_y4m_kernel(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ out,
                                                          int64_t n, int64_t total) {
+#pragma clang fp contract(off)
   const int64_t rec = 6 + 3 * n;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t f = i / n, px = i - f * n;
     const uint8_t* src = bgr + 3 * i;
     const float b = src[0], g = src[1], r = src[2];
-    const float y = __fadd_rn(__fadd_rn(__fmul_rn(0.299f, r), __fmul_rn(0.587f, g)), __fmul_rn(0.114f, b));
+    const float y = 0.299f * r + 0.587f * g + 0.114f * b;
     uint8_t* o = out + f * rec + 6;
     o[px] = sat_u8(y);
-    o[n + px] = sat_u8(__fadd_rn(__fmul_rn(__fsub_rn(b, y), 0.564f), 128.0f));
-    o[2 * n + px] = sat_u8(__fadd_rn(__fmul_rn(__fsub_rn(r, y), 0.713f), 128.0f));
+    o[n + px] = sat_u8((b - y) * 0.564f + 128.0f);
+    o[2 * n + px] = sat_u8((r - y) * 0.713f + 128.0f);
     if (px < 6) out[f * rec + px] = (uint8_t)("FRAME\n"[px]);
   }
 }
