@@ -185,7 +185,11 @@ class _Pair:
                         res = None
                     else:
                         shape, dtype = payload
-                        res = torch.empty(shape, dtype=dtype, device=self.plane.device)
+                        # a host pair plane on a GPU volunteer receives into pinned memory: the chunk's
+                        # next hop (the worker's upload, the requester's GPU Y4M conversion) is then a DMA
+                        # instead of a staged copy (torch's caching host allocator recycles the buffers)
+                        pin = self.plane.device.type == "cpu" and self.plane.pin_host
+                        res = torch.empty(shape, dtype=dtype, device=self.plane.device, pin_memory=pin)
                         g.recv(res, 0, tag)
                 except Exception as e:  # noqa: BLE001 — PeerFailure or a transport error: this pair only
                     self.plane.metrics_incr("p2p_failed")
@@ -220,6 +224,7 @@ class PairPlane:
         self.device_key = _device_key(self.device)
         self._dead: set[int] = set()  # volunteers the coordinator declared dead
         self.inject_failures = 0  # tests: make this many receives fail like a broken transport
+        self.pin_host = torch.cuda.is_available()  # host receives land in pinned memory on a GPU volunteer
 
     def is_dead_peer(self, src: int, dst: int) -> bool:
         return src in self._dead or dst in self._dead

@@ -79,6 +79,7 @@ class _Slot:
         self.pin_out = None
         self.h2d_done = None  # event: the pinned input may be refilled
         self.out_done = None  # event: the annotated chunk is in pin_out
+        self.src_ref = None  # a caller's pinned chunk uploaded directly (kept alive until h2d_done)
 
     def buf(self, name, nbytes):
         b = getattr(self, name)
@@ -145,16 +146,24 @@ class DetectorEngine(Engine):
         with self._lock:
             slot = self._slots[self._next]
             self._next = (self._next + 1) % len(self._slots)
-            a = frames if isinstance(frames, np.ndarray) else frames.numpy()
-            a = np.ascontiguousarray(a)
             if slot.h2d_done is not None:
                 slot.h2d_done.synchronize()  # this slot's previous upload finished
             if slot.out_done is not None:
                 slot.out_done.synchronize()  # ... and its previous output was read back
-            pin = slot.buf("pin_in", a.nbytes)
-            pin.copy_(torch.from_numpy(a).view(-1).view(torch.uint8))  # threaded host copy
+            if isinstance(frames, torch.Tensor) and frames.is_contiguous() and frames.is_pinned():
+                # already page-locked (a pinned pair-plane receive): uploaded from where it lies; the slot
+                # holds the reference until the upload is known to be done
+                src = frames
+                slot.src_ref = frames
+            else:
+                a = frames if isinstance(frames, np.ndarray) else frames.numpy()
+                a = np.ascontiguousarray(a)
+                pin = slot.buf("pin_in", a.nbytes)
+                pin.copy_(torch.from_numpy(a).view(-1).view(torch.uint8))  # threaded host copy
+                src = pin.view(a.shape)
+                slot.src_ref = None
             with torch.cuda.stream(self.copy_stream):
-                x = pin.view(a.shape).to(self.device, non_blocking=True)
+                x = src.to(self.device, non_blocking=True)
                 slot.h2d_done = torch.cuda.Event()
                 slot.h2d_done.record(self.copy_stream)
             with torch.cuda.stream(self.stream):
