@@ -98,7 +98,7 @@ def build_C(nproc: int = 8, force: bool = False) -> Path:
     inc, libdir, abi = _torch_flags()
     BUILD.mkdir(parents=True, exist_ok=True)
     headers = list((CSRC / "kernels").glob("*.h"))
-    kern_flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
+    kern_flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast-honor-pragmas",
                   "-munsafe-fp-atomics", f"-I{CSRC}", f"-I{CSRC / 'kernels'}"]
     bind_flags = ["-O2", "-fPIC", "-std=c++17", f"-I{CSRC}", "-D__HIP_PLATFORM_AMD__=1",
                   "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
