@@ -307,6 +307,7 @@ class Y4MWriter:
     def __init__(self, path, width, height, fps=30, device=None):
         self.device = device
         self._pin = None
+        self._stream = None
         self.path, self.w, self.h = str(path), int(width), int(height)
         self.f = open(self.path, "wb")
         hdr = f"YUV4MPEG2 W{self.w} H{self.h} F{int(fps)}:1 Ip A1:1 C444\n".encode()
@@ -343,13 +344,16 @@ class Y4MWriter:
 
         from ..ops._lib import native
 
-        with torch.cuda.device(self.device):
-            d = torch.from_numpy(np.ascontiguousarray(block)).to(self.device)
+        if self._stream is None:  # a stream of its own: the legacy default stream would wait for the engines
+            self._stream = torch.cuda.Stream(self.device)
+        with torch.cuda.device(self.device), torch.cuda.stream(self._stream):
+            d = torch.from_numpy(np.ascontiguousarray(block)).to(self.device, non_blocking=True)
             rec = native().bgr_to_y4m(d)
             if self._pin is None or self._pin.numel() < rec.numel():
                 self._pin = torch.empty(rec.numel(), dtype=torch.uint8, pin_memory=True)
             h = self._pin[: rec.numel()]
-            h.copy_(rec)
+            h.copy_(rec, non_blocking=True)
+        self._stream.synchronize()
         return h.numpy()
 
     def release(self):
