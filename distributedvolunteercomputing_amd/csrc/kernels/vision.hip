@@ -1053,14 +1053,14 @@ struct Dwpw2 {
   static constexpr int R0 = (HALO_B > P1_B ? (HALO_B > OUT_B ? HALO_B : OUT_B) : (P1_B > OUT_B ? P1_B : OUT_B));
   static constexpr int A1_B = MP16 * K1 * 2, A2_B = MT * N1 * 2, R1 = A1_B > A2_B ? A1_B : A2_B;
   static constexpr int W1_B = N1 * K1 * 2, W2_B = N2 * N1 * 2;
-  // dw2's paired weights [5][N1] dwords, then the fp32 biases dw2 [N1], pw1 [N1], pw2 [N2]
-  static constexpr int C_B = 5 * N1 * 4 + (2 * N1 + N2) * 4;
+  // dw2's paired weights [5][N1] dwords, the fp32 biases dw2 [N1], pw1 [N1], pw2 [N2], dw1's weights [5][K1]
+  static constexpr int C_B = 5 * N1 * 4 + (2 * N1 + N2) * 4 + 5 * K1 * 4;
   static constexpr int LDS = R0 + R1 + W1_B + W2_B + C_B;
   static constexpr int NE = HH * HW * (K1 / 8), NH = (NE + 255) / 256;  // halo 16-B pieces (per thread)
 };
 
-template <int K1, int N1, int N2, int TH, int TW>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+template <int K1, int N1, int N2, int TH, int TW, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 dwpw2_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dwp1, const float* __restrict__ dwb1,
                      int dw1_relu, const bf16* __restrict__ Wt1, const float* __restrict__ pb1, int relu1,
                      const uint32_t* __restrict__ dwp2, const float* __restrict__ dwb2, int dw2_relu,
@@ -1080,8 +1080,10 @@ dwpw2_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dw
   bf16* const sW2 = (bf16*)(smem + G::R0 + G::R1 + G::W1_B);
   uint32_t* const sDw2 = (uint32_t*)(smem + G::R0 + G::R1 + G::W1_B + G::W2_B);  // [5][N1] paired dw2 weights
   float* const sB = (float*)(sDw2 + 5 * N1);  // dw2 bias [N1] | pw1 bias [N1] | pw2 bias [N2]
+  uint32_t* const sDw1 = (uint32_t*)(sB + 2 * N1 + N2);  // [5][K1] paired dw1 weights
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int e = tid; e < 5 * N1; e += 256) sDw2[e] = dwp2[e];
+  for (int e = tid; e < 5 * K1; e += 256) sDw1[e] = dwp1[e];
   for (int e = tid; e < 2 * N1 + N2; e += 256) sB[e] = e < N1 ? dwb2[e] : (e < 2 * N1 ? pb1[e - N1] : pb2[e - 2 * N1]);
   const int ntx = (Wo + TW - 1) / TW, nty = (Ho + TH - 1) / TH, per = ntx * nty, ntiles = per * imgs;
   for (int e = tid; e < N1 * K18; e += 256) {
@@ -1093,10 +1095,8 @@ dwpw2_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dw
     *(u32x4*)(sW2 + (c >> 2) * N2 * 32 + gidx(row, c & 3)) = *(const u32x4*)(Wt2 + (int64_t)row * N1 + c * 8);
   }
   const int c8a = tid % K18, c8b = tid % N18;  // this thread's channel groups in dw1 / dw2
-  // dw1's paired weights stay in registers; dw2's (and both biases) are re-read per tile (L1 hits):
-  // holding both sets spilled at the 2-workgroups-per-CU register budget
-  uint32_t wr1[5][8];
-  load_dw_weights(dwp1 + c8a * 8, K1, wr1);
+  // both depthwise weight sets and the biases live in LDS and are read per tile phase (holding them in
+  // registers spilled at 2-3 workgroups per CU)
   u32x4 hr[NH];
   // halo of tile t: conv0 rows 2 Y0 - 2 .. 2 Y0 + 2 TH, columns 2 X0 - 2 .. 2 X0 + 2 TW (zero outside)
   auto gload = [&](int t) {
@@ -1127,13 +1127,15 @@ dwpw2_persist_kernel(const bf16* __restrict__ x, const uint32_t* __restrict__ dw
     }
     __syncthreads();
     // 2. dw1 over the conv1 region (PH x PW pixels) -> A1 (KS1 slices of [MP16][32])
+    uint32_t wr1[5][8];
+    load_dw_weights(sDw1 + c8a * 8, K1, wr1);
 #pragma unroll 1
     for (int p = tid / K18; p < MP; p += 256 / K18) {
       const int py = p / PW, px = p % PW;
       u32x4 t9[9];
 #pragma unroll
       for (int q = 0; q < 9; ++q) t9[q] = *(const u32x4*)(r0 + (((py + q / 3) * HW + px + q % 3) * K1 + c8a * 8) * 2);
-      const f32x4 d1a = *(const f32x4*)(dwb1 + c8a * 8), d1b = *(const f32x4*)(dwb1 + c8a * 8 + 4);
+      const f32x4 d1a = *(const f32x4*)(dwb1 + c8a * 8), d1b = *(const f32x4*)(dwb1 + c8a * 8 + 4);  // L1 hits
       float a[8] = {d1a[0], d1a[1], d1a[2], d1a[3], d1b[0], d1b[1], d1b[2], d1b[3]};
       dw9_accum_w(t9, wr1, a);
       *(u32x4*)(sA + (c8a >> 2) * MP16 * 32 + gidx(p, c8a & 3)) = dw_out8(a, dw1_relu);
@@ -1812,20 +1814,29 @@ bool vcx_dw_pw2(const void* x, const void* dw1_w, const float* dw1_b, int dw1_re
                 int relu1, const void* dw2_w, const float* dw2_b, int dw2_relu, const void* W2, const float* b2,
                 int relu2, void* Y, int imgs, int H, int W, int K1, int N1, int N2, hipStream_t s) {
   if (!(K1 == 32 && N1 == 64 && N2 == 128) || (int64_t)H * W * K1 * 2 >= INT32_MAX) return false;
-  constexpr int TH = 8, TW = 8;
-  using G = Dwpw2<32, 64, 128, TH, TW>;
-  auto kern = dwpw2_persist_kernel<32, 64, 128, TH, TW>;
-  static const bool attr = [&] {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
-    return true;
+  // tile geometry: VCX_DWPW2_TILE=8x8 (2 workgroups per CU, 79 KB LDS) or 4x8 (3 per CU, 52 KB: more
+  // halo and conv1 recompute per output pixel, more workgroups to overlap the phases)
+  static const int geo = [] {
+    const char* e = std::getenv("VCX_DWPW2_TILE");
+    return (e && std::string(e) == "4x8") ? 1 : 0;
   }();
-  (void)attr;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  const int64_t tiles = (int64_t)((Wo + TW - 1) / TW) * ((Ho + TH - 1) / TH) * imgs;
-  const int grid = (int)std::min<int64_t>(tiles, (int64_t)2 * vision_cus());
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), G::LDS, s, (const bf16*)x, (const uint32_t*)dw1_w, dw1_b, dw1_relu,
-                     (const bf16*)W1, b1, relu1, (const uint32_t*)dw2_w, dw2_b, dw2_relu, (const bf16*)W2, b2, relu2,
-                     (bf16*)Y, H, W, Ho, Wo, imgs);
+  auto go = [&](auto kern, int lds, int th, int tw, int per_cu) {
+    static bool attr_done = false;  // one attribute call per instance (the lambda is instantiated per kernel)
+    if (!attr_done) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      attr_done = true;
+    }
+    const int64_t tiles = (int64_t)((Wo + tw - 1) / tw) * ((Ho + th - 1) / th) * imgs;
+    const int grid = (int)std::min<int64_t>(tiles, (int64_t)per_cu * vision_cus());
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, (const bf16*)x, (const uint32_t*)dw1_w, dw1_b, dw1_relu,
+                       (const bf16*)W1, b1, relu1, (const uint32_t*)dw2_w, dw2_b, dw2_relu, (const bf16*)W2, b2, relu2,
+                       (bf16*)Y, H, W, Ho, Wo, imgs);
+  };
+  if (geo == 1)
+    go(dwpw2_persist_kernel<32, 64, 128, 4, 8, 3>, Dwpw2<32, 64, 128, 4, 8>::LDS, 4, 8, 3);
+  else
+    go(dwpw2_persist_kernel<32, 64, 128, 8, 8, 2>, Dwpw2<32, 64, 128, 8, 8>::LDS, 8, 8, 2);
   return true;
 }
 
