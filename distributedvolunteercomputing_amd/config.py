@@ -32,6 +32,9 @@ class RuntimeConfig:
     gemm: str = "lib"  # VCX_GEMM: "lib" (hipBLASLt/rocBLAS) or "vcx" (csrc/kernels/gemm.hip, opt-in: 0.74-0.84x lib)
     mlp: str = "fused"  # VCX_MLP: GPT-2 MLP fc (+bias+GELU) and fc2-dgrad (*gelu' + bias grad) on the persistent
     # hand-written GEMM's fused epilogues (csrc/kernels/gemm_ps.hip), other GEMMs on `gemm`; "lib": library + passes
+    # VCX_NARROW_GEMM: GEMMs with <= 128 output columns and >= 32k rows (ResNet 1x1 convolutions) on
+    # the vision GEMM ("vision") or the library ("lib")
+    narrow_gemm: str = "lib"
     dgrad_ps: bool = True  # VCX_DGRAD_PS: input gradients dX = dY W with K <= 2304 on gemm_ps (measured faster)
     gemm_wgrad: str = "vcx"  # VCX_GEMM_WGRAD: weight gradients on "vcx" (gemm_wg, hand-written) or "lib" (split-M batched GEMM)
     gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)
@@ -86,6 +89,7 @@ _ENV = {
     "gemm": ("VCX_GEMM", str),
     "mlp": ("VCX_MLP", str),
     "dgrad_ps": ("VCX_DGRAD_PS", _bool),
+    "narrow_gemm": ("VCX_NARROW_GEMM", str),
     "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
     "resnet_bn": ("VCX_RESNET_BN", str),
     "resnet_join": ("VCX_RESNET_JOIN", _bool),
@@ -114,7 +118,7 @@ _ENV = {
     "trace_dir": ("VCX_TRACE_DIR", str),
     "metrics_dir": ("VCX_METRICS_DIR", str),
 }
-_CHOICES = {"gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "off"),
+_CHOICES = {"narrow_gemm": ("lib", "vision"), "gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "off"),
             "uplink_pipeline": ("relay", "all", "off")}
 
 _lock = threading.Lock()

@@ -54,6 +54,28 @@ def gemm_nt(a, b, bias=None, out=None):
     return out
 
 
+_ZERO_BIAS: dict = {}
+
+
+def narrow_gemm_ok(M: int, N: int, K: int, t) -> bool:
+    """Y[M, N] = X[M, K] W[N, K]^T with a narrow output (N <= 128, the ResNet-50 1x1 convolutions with
+    64 / 128 output channels at 56^2 / 28^2) on the vision GEMM (csrc/kernels/vision.hip
+    gemm_bias_act_kernel, 128 x 64/128 tiles) instead of the library, whose picks for these shapes tile
+    the long M side 16 rows at a time (config.narrow_gemm; scripts/resnet_1x1_probe.py)."""
+    return (config.get().narrow_gemm == "vision" and N <= 128 and M >= 32768 and K % 32 == 0 and use_native(t)
+            and t.dtype == torch.bfloat16 and t.is_contiguous())
+
+
+def narrow_gemm(a, w):
+    """a [M, K] @ w[N, K]^T on the vision GEMM (caller checked narrow_gemm_ok)."""
+    from . import vision as V
+
+    zb = _ZERO_BIAS.get((w.shape[0], w.device))
+    if zb is None:
+        zb = _ZERO_BIAS[(w.shape[0], w.device)] = torch.zeros(w.shape[0], device=w.device)
+    return V.gemm_bias_act(a, w.contiguous(), zb, False)
+
+
 def transpose_weight(w):
     """W^T as a contiguous bf16 matrix (HIP transpose; weights only — a few MB)."""
     return native().transpose_bf16(w.contiguous())
@@ -288,6 +310,8 @@ class _Linear(torch.autograd.Function):
         w = _w2(w)
         if gemm_nt_ok(x2.shape[0], w.shape[0], x2.shape[1], x2):
             return gemm_nt(x2, w, b).view(*x.shape[:-1], w.shape[0])
+        if b is None and narrow_gemm_ok(x2.shape[0], w.shape[0], x2.shape[1], x2):
+            return narrow_gemm(x2, w).view(*x.shape[:-1], w.shape[0])
         return mm(x2, w, trans_b=True, bias=b).view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
@@ -311,6 +335,8 @@ class _Linear(torch.autograd.Function):
         elif ctx.needs_input_grad[0]:
             if gemm_nt_ok(dy2.shape[0], K, N, dy2):
                 dx = gemm_nt(dy2, transpose_weight(w)).view(x.shape)
+            elif narrow_gemm_ok(dy2.shape[0], K, N, dy2):
+                dx = narrow_gemm(dy2, transpose_weight(w)).view(x.shape)
             elif dgrad_ps_ok(dy2.shape[0], K, N, dy2):
                 # dX = dY W on the persistent hand-written GEMM (B = W^T, a few MB): faster than the
                 # library at the GPT-2 attention shapes (profiles/r4_gemm_ps_bench.txt: dg_qkv, dg_proj)
