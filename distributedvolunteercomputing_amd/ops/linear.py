@@ -58,12 +58,13 @@ _ZERO_BIAS: dict = {}
 
 
 def narrow_gemm_ok(M: int, N: int, K: int, t) -> bool:
-    """Y[M, N] = X[M, K] W[N, K]^T with a narrow output (N <= 128, the ResNet-50 1x1 convolutions with
-    64 / 128 output channels at 56^2 / 28^2) on the vision GEMM (csrc/kernels/vision.hip
-    gemm_bias_act_kernel, 128 x 64/128 tiles) instead of the library, whose picks for these shapes tile
-    the long M side 16 rows at a time (config.narrow_gemm; scripts/resnet_1x1_probe.py)."""
-    return (config.get().narrow_gemm == "vision" and N <= 128 and M >= 32768 and K % 32 == 0 and use_native(t)
-            and t.dtype == torch.bfloat16 and t.is_contiguous())
+    """Y[M, N] = X[M, K] W[N, K]^T with a narrow output on the vision GEMM (csrc/kernels/vision.hip
+    gemm_bias_act_kernel, 128 x 64/128 tiles) instead of the library: the ResNet-50 1x1 convolutions
+    with 64 output channels at 56^2 (M = 401k: 21.6 vs 34.5 us, 41.8 vs 55.7, 44.1 vs 57.6) and 128 at
+    the 401k-row shape (71.4 vs 75.0); at 100k rows or 256+ columns the library is faster
+    (profiles/r5_resnet_1x1_probe.txt; config.narrow_gemm)."""
+    return (config.get().narrow_gemm == "vision" and ((N <= 64 and M >= 131072) or (N <= 128 and M >= 393216))
+            and K % 32 == 0 and use_native(t) and t.dtype == torch.bfloat16 and t.is_contiguous())
 
 
 def narrow_gemm(a, w):
