@@ -34,7 +34,7 @@ class RuntimeConfig:
     # hand-written GEMM's fused epilogues (csrc/kernels/gemm_ps.hip), other GEMMs on `gemm`; "lib": library + passes
     # VCX_NARROW_GEMM: GEMMs with <= 128 output columns and >= 32k rows (ResNet 1x1 convolutions) on
     # the vision GEMM ("vision") or the library ("lib")
-    narrow_gemm: str = "vision"
+    narrow_gemm: str = "lib"
     dgrad_ps: bool = True  # VCX_DGRAD_PS: input gradients dX = dY W with K <= 2304 on gemm_ps (measured faster)
     gemm_wgrad: str = "vcx"  # VCX_GEMM_WGRAD: weight gradients on "vcx" (gemm_wg, hand-written) or "lib" (split-M batched GEMM)
     gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)

@@ -62,7 +62,8 @@ def narrow_gemm_ok(M: int, N: int, K: int, t) -> bool:
     gemm_bias_act_kernel, 128 x 64/128 tiles) instead of the library: the ResNet-50 1x1 convolutions
     with 64 output channels at 56^2 (M = 401k: 21.6 vs 34.5 us, 41.8 vs 55.7, 44.1 vs 57.6) and 128 at
     the 401k-row shape (71.4 vs 75.0); at 100k rows or 256+ columns the library is faster
-    (profiles/r5_resnet_1x1_probe.txt; config.narrow_gemm)."""
+    (profiles/r5_resnet_1x1_probe.txt). Opt-in (config.narrow_gemm = "vision"): inside the config-3 step
+    it measured even (8309 / 8293 vs 8321 / 8292 img/s), the probe's gain did not carry over."""
     return (config.get().narrow_gemm == "vision" and ((N <= 64 and M >= 131072) or (N <= 128 and M >= 393216))
             and K % 32 == 0 and use_native(t) and t.dtype == torch.bfloat16 and t.is_contiguous())
 
@@ -149,6 +150,11 @@ def _splits(M: int, N: int, K: int) -> int:
         if M < config.get().wgrad_big_split_min_m:
             return 1
         s = 4
+    elif M >= 262144:
+        # the ResNet-50 1x1 convolutions at 56^2 (M = 401k, 64..256 x 64..256 outputs): ~6k rows per
+        # split; 16 splits left 25k-row GEMMs on 64 x 16 library tiles (66-125 vs 37-82 us,
+        # profiles/r5_resnet_wgrad_probe.txt)
+        s = 64
     else:
         s = 16
     while s > 1 and (M % s or M // s < MIN_ROWS_PER_SPLIT):
