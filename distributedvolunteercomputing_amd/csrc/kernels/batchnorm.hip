@@ -18,6 +18,8 @@
 // writes back / invalidates the XCD's L2; not profiled further): profiles/r4_resnet50_ab.txt.)
 // Rows R = N * H * W, C channels (a power of two, 8 .. 2048); every lane moves 16 B (8 channels) per
 // access. No reference analog (north-star config 3).
+#include <cstdlib>
+
 #include "vcx_common.h"
 
 namespace vcx {
@@ -42,7 +44,7 @@ struct Unroll {
 // body(off, step, Unroll<U>, s0, s1) handles the U rows off, off + step, ...: the main loop passes
 // U = 4 so every lane keeps 4 row loads per operand in flight (one at a time left these passes at
 // 2-3 TB/s, latency-bound: profiles/r5_cfg3_resnet50_categories.txt)
-template <typename F>
+template <int UR, typename F>
 __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&& body, float* out0, float* out1) {
   __shared__ float red[2][NT][9];  // [quantity][thread][8 channels + pad]
   const int tid = threadIdx.x;
@@ -55,7 +57,7 @@ __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&
   if (rr < rpp) {
     const int64_t step = (int64_t)rpp * C;
     int64_t r = r0 + rr;
-    for (; r + 3 * rpp < r1; r += 4 * rpp) body(r * C + ch * 8, step, Unroll<4>{}, s0, s1);
+    for (; r + (UR - 1) * rpp < r1; r += UR * rpp) body(r * C + ch * 8, step, Unroll<UR>{}, s0, s1);
     for (; r < r1; r += rpp) body(r * C + ch * 8, step, Unroll<1>{}, s0, s1);
   }
 #pragma unroll
@@ -80,12 +82,13 @@ __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&
 // sums of (x - k) and (x - k)^2 with a per-channel pivot k = x[row 0] (the same for every block):
 // E[x^2] - m^2 on raw fp32 sums cancels catastrophically when |mean| >> std over millions of rows;
 // shifted by a value of the batch, the sums are O(R std^2) and the variance keeps its digits
+template <int UR>
 __global__ void __launch_bounds__(NT) stats_kernel(const bf16* __restrict__ x, int64_t R, int C, int64_t rows_per_block,
                                                    float* __restrict__ sum, float* __restrict__ sumsq) {
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(R, r0 + rows_per_block);
   float k[8];
   load8(x + (threadIdx.x % (C / 8)) * 8, k);
-  channel_reduce(
+  channel_reduce<UR>(
       C, r0, r1,
       [&](int64_t off, int64_t step, auto u, float(&s0)[8], float(&s1)[8]) {
         constexpr int U = decltype(u)::value;
@@ -241,7 +244,7 @@ __global__ void __launch_bounds__(NT) apply_kernel(const bf16* __restrict__ x, c
 }
 
 // backward reductions: sum dz and sum dz * xhat per channel, dz = dy [* mask]
-template <bool RELU>
+template <bool RELU, int UR>
 __global__ void __launch_bounds__(NT) bwd_reduce_kernel(const bf16* __restrict__ dy, const unsigned char* __restrict__ mask,
                                                         const bf16* __restrict__ x, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, int64_t R, int C,
@@ -255,7 +258,7 @@ __global__ void __launch_bounds__(NT) bwd_reduce_kernel(const bf16* __restrict__
     m[i] = mean[ch + i];
     rs[i] = rstd[ch + i];
   }
-  channel_reduce(
+  channel_reduce<UR>(
       C, r0, r1,
       [&](int64_t off, int64_t step, auto u, float(&s0)[8], float(&s1)[8]) {
         constexpr int U = decltype(u)::value;
@@ -438,12 +441,22 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_kernel(const bf16* __restrict_
   }
 }
 
+// reduction geometry: VCX_BN_REDUCE=4 (round-5 first form: 4 rows in flight per lane, ~1024 blocks of at
+// least 32 passes) or 8 (default: 8 rows in flight, ~2048 blocks of at least 16 passes -- the small late
+// layers, C = 1024 / 2048 over 25k / 6k rows, got only ~200 blocks)
+inline int reduce_unroll() {
+  static const int u = [] {
+    const char* e = std::getenv("VCX_BN_REDUCE");
+    return (e && e[0] == '4') ? 4 : 8;
+  }();
+  return u;
+}
 inline int64_t rows_per_block(int64_t R, int C) {
-  // at most ~1024 blocks, each at least 32 passes of its row slots (bounds the 2C atomics per block)
-  const int64_t rpp = NT / (C / 8);
-  int64_t rpb = (R + 1023) / 1024;
+  const bool deep = reduce_unroll() == 8;
+  const int64_t rpp = NT / (C / 8), target = deep ? 2048 : 1024, min_passes = deep ? 16 : 32;
+  int64_t rpb = (R + target - 1) / target;
   rpb = ((rpb + rpp - 1) / rpp) * rpp;
-  return rpb < 32 * rpp ? 32 * rpp : rpb;
+  return rpb < min_passes * rpp ? min_passes * rpp : rpb;
 }
 inline int grid_for(int64_t n8) {
   int64_t g = (n8 + NT - 1) / NT;
@@ -469,7 +482,10 @@ void vcx_bn_fwd_train(const void* x, const void* res, void* y, void* mask, int64
   using namespace bn;
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
-  hipLaunchKernelGGL(stats_kernel, dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
+  if (reduce_unroll() == 8)
+    hipLaunchKernelGGL(stats_kernel<8>, dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
+  else
+    hipLaunchKernelGGL(stats_kernel<4>, dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
   FinArgs fa{ws, (const bf16*)gamma, (const bf16*)beta, run_mean, run_var, run_fp32, eps, momentum, 1.f / (float)R, R,
              mean, rstd, scale, nbt};
   if (!layer_ws) {
@@ -529,12 +545,14 @@ void vcx_bn_bwd(const void* dy, const void* mask, const void* x, const float* me
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
   float* bws = layer_ws ? ws + 2 * C : ws;
-  if (relu)
-    hipLaunchKernelGGL(bwd_reduce_kernel<true>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const unsigned char*)mask,
-                       (const bf16*)x, mean, rstd, R, C, rpb, bws, bws + C);
+  auto red = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const unsigned char*)mask, (const bf16*)x, mean,
+                       rstd, R, C, rpb, bws, bws + C);
+  };
+  if (reduce_unroll() == 8)
+    relu ? red(bwd_reduce_kernel<true, 8>) : red(bwd_reduce_kernel<false, 8>);
   else
-    hipLaunchKernelGGL(bwd_reduce_kernel<false>, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const unsigned char*)mask,
-                       (const bf16*)x, mean, rstd, R, C, rpb, bws, bws + C);
+    relu ? red(bwd_reduce_kernel<true, 4>) : red(bwd_reduce_kernel<false, 4>);
   if (!layer_ws)
     hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, C, sums, (bf16*)gw, (bf16*)gb);
   const float* sdz = layer_ws ? bws : sums;
