@@ -62,6 +62,8 @@ class RuntimeConfig:
     # statistics runs inside the apply / dx passes (2 launches per layer and direction instead of 3)
     bn_layer_ws: bool = True
     resnet_join: bool = True  # VCX_RESNET_JOIN: identity-shortcut gradient added in conv1's dgrad GEMM (GradJoin)
+    # VCX_RESNET_PROJ_JOIN: projection shortcuts add their input gradient into the one conv1 left (GradJoin)
+    resnet_proj_join: bool = True
     # ---- distributed / control plane
     gloo_host: str = "127.0.0.1"  # VCX_GLOO_HOST: interface gloo peer groups bind to
     p2p_backend: str = ""  # VCX_P2P_BACKEND: pair-group backend of the p2p chunk plane ("" = auto)
@@ -93,6 +95,7 @@ _ENV = {
     "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
     "resnet_bn": ("VCX_RESNET_BN", str),
     "resnet_join": ("VCX_RESNET_JOIN", _bool),
+    "resnet_proj_join": ("VCX_RESNET_PROJ_JOIN", _bool),
     "bn_layer_ws": ("VCX_BN_LAYER_WS", _bool),
     "conv_find": ("VCX_CONV_FIND", _bool),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),

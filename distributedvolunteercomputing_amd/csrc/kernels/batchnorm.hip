@@ -19,6 +19,7 @@
 // Rows R = N * H * W, C channels (a power of two, 8 .. 2048); every lane moves 16 B (8 channels) per
 // access. No reference analog (north-star config 3).
 #include <cstdlib>
+#include <string>
 
 #include "vcx_common.h"
 
@@ -441,19 +442,28 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_kernel(const bf16* __restrict_
   }
 }
 
-// reduction geometry: VCX_BN_REDUCE=4 (round-5 first form: 4 rows in flight per lane, ~1024 blocks of at
-// least 32 passes) or 8 (default: 8 rows in flight, ~2048 blocks of at least 16 passes -- the small late
-// layers, C = 1024 / 2048 over 25k / 6k rows, got only ~200 blocks)
-inline int reduce_unroll() {
-  static const int u = [] {
+// reduction geometry (rows in flight per lane, target block count, minimum passes per block):
+// VCX_BN_REDUCE = "4" (default: 4 deep, ~1024 blocks of >= 32 passes), "8" (8 deep, ~2048 blocks of >= 16:
+// 2 % slower over config 3, gpurun_out/c16 -- the late layers' ~200 blocks were not the bound), or "4w" /
+// "8n" (4 deep x ~2048 blocks, 8 deep x ~1024) to separate the two
+struct ReduceGeo {
+  int unroll, target, min_passes;
+};
+inline const ReduceGeo& reduce_geo() {
+  static const ReduceGeo g = [] {
     const char* e = std::getenv("VCX_BN_REDUCE");
-    return (e && e[0] == '4') ? 4 : 8;
+    const std::string v = e ? e : "4";
+    if (v == "8") return ReduceGeo{8, 2048, 16};
+    if (v == "8n") return ReduceGeo{8, 1024, 32};
+    if (v == "4w") return ReduceGeo{4, 2048, 16};
+    return ReduceGeo{4, 1024, 32};
   }();
-  return u;
+  return g;
 }
+inline int reduce_unroll() { return reduce_geo().unroll; }
 inline int64_t rows_per_block(int64_t R, int C) {
-  const bool deep = reduce_unroll() == 8;
-  const int64_t rpp = NT / (C / 8), target = deep ? 2048 : 1024, min_passes = deep ? 16 : 32;
+  const ReduceGeo& geo = reduce_geo();
+  const int64_t rpp = NT / (C / 8), target = geo.target, min_passes = geo.min_passes;
   int64_t rpb = (R + target - 1) / target;
   rpb = ((rpb + rpp - 1) / rpp) * rpp;
   return rpb < min_passes * rpp ? min_passes * rpp : rpb;

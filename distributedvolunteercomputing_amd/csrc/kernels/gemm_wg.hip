@@ -27,6 +27,8 @@
 // Reference analog: none (the reference trains nothing; SURVEY.md §2.9 north-star trainer).
 #include <type_traits>
 
+#include <cstdlib>
+
 #include "vcx_common.h"
 
 namespace vcx {
@@ -310,10 +312,22 @@ bool vcx_gemm_wg_supported(int M, int N, int K, int splits) {
          K / 192 >= splits;  // >= 3 blocks of 64 tokens per split (nk >= 6)
 }
 
-// token-axis splits: about one round of workgroups over the CUs ((M/256)(N/256) tiles x S)
+// token-axis splits: about one round of workgroups over the CUs ((M/256)(N/256) tiles x S).
+// VCX_WG_TARGET (workgroups aimed at, default 256): fewer splits trade parallelism for fewer fp32
+// partials (each split writes a 256 KB partial per tile that splitk_sum reads back -- at the ResNet-50
+// shapes, 25k tokens and 4 tiles, 64 splits write as many partial bytes as the operands hold)
+static int wg_target() {
+  static const int t = [] {
+    const char* e = std::getenv("VCX_WG_TARGET");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 256;
+  }();
+  return t;
+}
+
 int vcx_gemm_wg_splits(int M, int N, int K) {
   const int tiles = (M / gemm_wg::BM) * (N / gemm_wg::BN);
-  int s = 256 / (tiles > 0 ? tiles : 1);
+  int s = wg_target() / (tiles > 0 ? tiles : 1);
   if (s < 1) s = 1;
   if (s > K / 192) s = K / 192;
   return s < 1 ? 1 : s;

@@ -34,20 +34,24 @@ class Conv1x1(nn.Conv2d):
         return (x.is_cuda and config.get().resnet_conv1x1 == "gemm" and x.is_contiguous(memory_format=torch.channels_last)
                 and native_linear_ok(self.weight))
 
-    def forward(self, x, join=None):
+    def forward(self, x, join=None, deposit=False):
         if not (x.is_cuda and config.get().resnet_conv1x1 == "gemm"
                 and x.is_contiguous(memory_format=torch.channels_last)):
             assert join is None
             return super().forward(x)
-        from ..ops.linear import linear
+        from ..ops.linear import linear, subsample_tap
 
-        xh = x.permute(0, 2, 3, 1)  # [N, H, W, C] view of the channels-last storage
         if self.stride[0] != 1:
-            assert join is None
-            xh = xh[:, ::self.stride[0], ::self.stride[1], :].contiguous()
+            assert not deposit
+            if join is not None:  # the input gradient lands in the one conv1 deposited (ops/linear.py GradJoin)
+                xh, join = subsample_tap(x, join, self.stride[0]), None
+            else:
+                xh = x.permute(0, 2, 3, 1)[:, ::self.stride[0], ::self.stride[1], :].contiguous()
+        else:
+            xh = x.permute(0, 2, 3, 1)  # [N, H, W, C] view of the channels-last storage
         N, H, W, C = xh.shape
         # the [Cout, Cin, 1, 1] parameter itself: its gradient lands in the flat .grad directly
-        y = linear(xh.reshape(N * H * W, C), self.weight, join=join)
+        y = linear(xh.reshape(N * H * W, C), self.weight, join=join, deposit=deposit)
         return y.view(N, H, W, self.out_channels).permute(0, 3, 1, 2)
 
 
@@ -73,12 +77,19 @@ class Bottleneck(nn.Module):
         # Identity shortcut: x feeds conv1 and the residual add, so autograd would sum the two
         # gradients of x in an elementwise pass; the shortcut's gradient goes to conv1's input-gradient
         # GEMM instead, which adds it as its C (beta = 1; ops/linear.py GradJoin)
-        join = (GradJoin() if (self.down is None and config.get().resnet_join and torch.is_grad_enabled()
-                               and self.conv1.gemm_path(x)) else None)
-        idt = x if self.down is None else bn_act(self.down[0](x), self.down[1], relu=False)
-        y = bn_act(self.conv1(x, join=join), self.bn1)
+        # Projection shortcut: conv1's input gradient is left in the join and the shortcut convolution
+        # (older node, so its backward runs later) adds its own into it -- beta = 1 at stride 1, a
+        # strided in-place add at stride 2 -- instead of autograd's full-size zero fill + slice copy + add
+        join = (GradJoin() if (config.get().resnet_join and torch.is_grad_enabled() and self.conv1.gemm_path(x)
+                               and (self.down is None or (config.get().resnet_proj_join and self.down[0].gemm_path(x))))
+                else None)
+        if self.down is None:
+            idt = x
+        else:
+            idt = bn_act(self.down[0](x, join=join), self.down[1], relu=False)
+        y = bn_act(self.conv1(x, join=join, deposit=self.down is not None and join is not None), self.bn1)
         y = bn_act(self.conv2(y), self.bn2)
-        if join is not None:
+        if join is not None and self.down is None:
             idt = residual_tap(x, join)  # created after conv1's node: its backward runs first
         return bn_act(self.conv3(y), self.bn3, residual=idt)
 

@@ -267,7 +267,13 @@ class GradJoin:
     ``linear(x2d, w, join=join)`` adds it (models/resnet.py). Protocol (one backward pass at a
     time, both sides on the autograd thread): the tap's backward runs first in practice (it becomes
     ready at the block's last BatchNorm, the convolution only at the end of the branch); whichever
-    side runs second sees the other's state, so the result is right in either order."""
+    side runs second sees the other's state, so the result is right in either order.
+
+    Projection shortcuts run the other way round: the shortcut's nodes are older than conv1's, so
+    conv1's backward runs first and DEPOSITS its input gradient (``linear(..., join=j, deposit=True)``
+    returns None for x); the shortcut convolution then adds its own into that buffer -- with beta = 1
+    at stride 1, or as a strided in-place add at stride 2 (``subsample_tap``) instead of autograd's
+    zero-filled full-size slice gradient plus a full-size add."""
 
     def __init__(self):
         self.pending = None  # the shortcut's gradient as the [M, K] matrix of the layer input
@@ -302,9 +308,38 @@ def residual_tap(x: torch.Tensor, join: GradJoin) -> torch.Tensor:
     return _ResidualTap.apply(x, join)
 
 
+class _SubsampleTap(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, join, s):
+        ctx.join, ctx.s = join, s
+        ctx.full = (x.shape[0], x.shape[2], x.shape[3], x.shape[1])  # N, H, W, C
+        join.ran = False
+        return x.permute(0, 2, 3, 1)[:, ::s, ::s, :].contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        join, ctx.join = ctx.join, None
+        s, (N, H, W, C) = ctx.s, ctx.full
+        base = join.take()
+        if base is not None and base.is_contiguous() and base.numel() == N * H * W * C:
+            full = base.view(N, H, W, C)
+            full[:, ::s, ::s, :].add_(g)  # conv1's deposited input gradient: only the strided quarter moves
+        else:
+            join.ran = True
+            full = g.new_zeros(N, H, W, C)
+            full[:, ::s, ::s, :] = g
+        return full.permute(0, 3, 1, 2), None, None
+
+
+def subsample_tap(x: torch.Tensor, join: GradJoin, stride: int) -> torch.Tensor:
+    """The contiguous [N, H/s, W/s, C] subsample of channels-last 4-D x (a stride-s 1x1 convolution's
+    input); its backward adds the gradient into the input gradient conv1 deposited in ``join``."""
+    return _SubsampleTap.apply(x, join, stride)
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, bias_grad_elsewhere=False, join=None):
+    def forward(ctx, x, w, b, bias_grad_elsewhere=False, join=None, deposit=False):
         # w: [N, K], or a 1x1 convolution's [N, K, 1, 1] weight itself (not a view of it: its gradient
         # then goes straight into the parameter's flat .grad, no view-backward + accumulation pass)
         ctx.save_for_backward(x, w)
@@ -312,7 +347,9 @@ class _Linear(torch.autograd.Function):
         # sums it already has at hand) and returns it for the same bias tensor
         ctx.has_bias = b is not None and not bias_grad_elsewhere
         ctx.bias = b
-        ctx.join = join
+        ctx.join, ctx.deposit = join, deposit
+        if deposit:
+            join.pending, join.ran = None, False
         x2 = x.reshape(-1, x.shape[-1])
         w = _w2(w)
         if gemm_nt_ok(x2.shape[0], w.shape[0], x2.shape[1], x2):
@@ -331,6 +368,9 @@ class _Linear(torch.autograd.Function):
         dy2 = dy2.contiguous()
         dx = None
         join, ctx.join = ctx.join, None
+        deposit = ctx.deposit
+        if deposit:  # conv1 of a projection-shortcut block: runs first, leaves dx for the shortcut
+            join, depo = None, join
         base = join.take() if join is not None else None
         if join is not None and base is None:
             join.ran = True
@@ -352,6 +392,8 @@ class _Linear(torch.autograd.Function):
                 dx = dx.view(x.shape)
             else:
                 dx = mm(dy2, w).view(x.shape)
+        if deposit and dx is not None and not depo.ran and dx.is_contiguous():
+            depo.pending, dx = dx.view(-1, K), None
         want_w = bool(ctx.needs_input_grad[1])
         want_b = bool(ctx.has_bias and ctx.needs_input_grad[2])
         bias, ctx.bias = ctx.bias, None
@@ -369,9 +411,9 @@ class _Linear(torch.autograd.Function):
             dy2.record_stream(side)  # keep the inputs' memory until the side stream is done with it
             x2.record_stream(side)
             _queue_join(main, side, dy2.device)
-            return dx, None, None, None, None
+            return dx, None, None, None, None, None
         dw, db = _param_grads(dy2, x2, w, bias, want_w, want_b)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 def native_linear_ok(w: torch.Tensor) -> bool:
@@ -380,13 +422,14 @@ def native_linear_ok(w: torch.Tensor) -> bool:
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
-           bias_grad_elsewhere: bool = False, join: GradJoin | None = None) -> torch.Tensor:
+           bias_grad_elsewhere: bool = False, join: GradJoin | None = None, deposit: bool = False) -> torch.Tensor:
     """y = x @ w^T (+ b), x [..., K], w [N, K] (or a 1x1 convolution's [N, K, 1, 1]). With
     bias_grad_elsewhere the backward leaves the bias gradient to y's consumer (e.g.
     ``causal_attention(qkv, bias=b)``), which must then be y's only consumer and return
-    d(loss)/d(b) = column sums of dy for the same tensor."""
+    d(loss)/d(b) = column sums of dy for the same tensor. ``join``: see GradJoin (deposit = this
+    layer's backward leaves its input gradient in the join for a later consumer)."""
     if native_linear_ok(w):
-        return _Linear.apply(x, w, b, bias_grad_elsewhere, join)
+        return _Linear.apply(x, w, b, bias_grad_elsewhere, join, deposit)
     assert join is None, "a GradJoin needs the native linear path (its backward consumes the joined gradient)"
     return F.linear(x, _w2(w), b)
 

@@ -104,8 +104,9 @@ def test_resnet_bottlenecks_vs_fp32_oracle(gpu):
 def test_resnet_identity_shortcut_gradient_join(gpu):
     """Identity-shortcut bottlenecks (ResNet with 2 blocks per stage) take the shortcut's gradient into
     conv1's input-gradient GEMM (ops/linear.py GradJoin, beta = 1: one rounding) instead of autograd's
-    bf16 add. Against an fp32 oracle of the same model, the joined gradients (input and every
-    parameter) are no worse than the unjoined ones."""
+    bf16 add; projection-shortcut blocks (stride 1 and 2) add the shortcut convolution's input gradient
+    into the one conv1 deposited. Against an fp32 oracle of the same model, the joined gradients (input
+    and every parameter) are no worse than the unjoined ones."""
     import copy
 
     from distributedvolunteercomputing_amd.models import resnet as R
@@ -119,9 +120,10 @@ def test_resnet_identity_shortcut_gradient_join(gpu):
     m = m.to(torch.bfloat16).to(memory_format=torch.channels_last)
     x = torch.randn(16, 3, 32, 32, device=gpu)
     y = torch.randint(0, 10, (16,), device=gpu)
-    joined = [b for b in m.blocks if b.down is None]
     probe = lambda c: torch.empty(1, c, 4, 4, device=gpu, dtype=torch.bfloat16).to(memory_format=torch.channels_last)  # noqa: E731
-    assert joined and all(b.conv1.gemm_path(probe(b.conv1.in_channels)) for b in joined)
+    assert sorted(b.down[0].stride[0] for b in m.blocks if b.down is not None) == [1, 2]
+    assert all(b.conv1.gemm_path(probe(b.conv1.in_channels)) for b in m.blocks)
+    assert all(b.down[0].gemm_path(probe(b.conv1.in_channels)) for b in m.blocks if b.down is not None)
 
     def grads(model, join_on, dt):
         orig = R.GradJoin
@@ -135,7 +137,20 @@ def test_resnet_identity_shortcut_gradient_join(gpu):
         finally:
             R.GradJoin = orig
 
-    gj, gn = grads(m, True, torch.bfloat16), grads(m, False, torch.bfloat16)
+    takes, orig_take = [], R.GradJoin.take
+
+    def take(self):
+        g = orig_take(self)
+        takes.append(g is not None)
+        return g
+
+    R.GradJoin.take = take
+    try:
+        gj = grads(m, True, torch.bfloat16)
+    finally:
+        R.GradJoin.take = orig_take
+    assert takes.count(True) == len(m.blocks), takes  # every block's second side found the first's gradient
+    gn = grads(m, False, torch.bfloat16)
     with reference_ops():
         go = grads(oracle, True, torch.float32)
     for i, (a_, b_, o_) in enumerate(zip(gj, gn, go)):
