@@ -442,21 +442,23 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_kernel(const bf16* __restrict_
   }
 }
 
-// reduction geometry (rows in flight per lane, target block count, minimum passes per block):
-// VCX_BN_REDUCE = "4" (default: 4 deep, ~1024 blocks of >= 32 passes), "8" (8 deep, ~2048 blocks of >= 16:
-// 2 % slower over config 3, gpurun_out/c16 -- the late layers' ~200 blocks were not the bound), or "4w" /
-// "8n" (4 deep x ~2048 blocks, 8 deep x ~1024) to separate the two
+// reduction geometry (rows in flight per lane, target block count, minimum passes per block), config 3
+// same box (gpurun_out/c16, c17): VCX_BN_REDUCE = "8n" (default: 8 deep, ~1024 blocks of >= 32 passes;
+// 8629-8722 img/s), "4" (4 deep, ~1024 blocks: 8556-8562), "8" (8 deep, ~2048 blocks of >= 16: 2 % under
+// "4"), "4w" (4 deep, ~2048 blocks: 8380-8386) -- more blocks cost more than the small late layers gain
+// (every block adds its partial sums into the workspace) -- and "8h" (8 deep, ~512 blocks)
 struct ReduceGeo {
   int unroll, target, min_passes;
 };
 inline const ReduceGeo& reduce_geo() {
   static const ReduceGeo g = [] {
     const char* e = std::getenv("VCX_BN_REDUCE");
-    const std::string v = e ? e : "4";
+    const std::string v = e ? e : "8n";
     if (v == "8") return ReduceGeo{8, 2048, 16};
-    if (v == "8n") return ReduceGeo{8, 1024, 32};
+    if (v == "4") return ReduceGeo{4, 1024, 32};
     if (v == "4w") return ReduceGeo{4, 2048, 16};
-    return ReduceGeo{4, 1024, 32};
+    if (v == "8h") return ReduceGeo{8, 512, 32};
+    return ReduceGeo{8, 1024, 32};
   }();
   return g;
 }

@@ -312,10 +312,11 @@ bool vcx_gemm_wg_supported(int M, int N, int K, int splits) {
          K / 192 >= splits;  // >= 3 blocks of 64 tokens per split (nk >= 6)
 }
 
-// token-axis splits: about one round of workgroups over the CUs ((M/256)(N/256) tiles x S).
-// VCX_WG_TARGET (workgroups aimed at, default 256): fewer splits trade parallelism for fewer fp32
-// partials (each split writes a 256 KB partial per tile that splitk_sum reads back -- at the ResNet-50
-// shapes, 25k tokens and 4 tiles, 64 splits write as many partial bytes as the operands hold)
+// token-axis splits: about one round of workgroups over the CUs ((M/256)(N/256) tiles x S), with at least
+// 768 tokens per split: each split writes a 256 KB fp32 partial per tile that splitk_sum reads back, so
+// short splits move more partial bytes than operand bytes (ResNet-50 at 25k / 6k tokens: 64 / 16 splits of
+// 392 tokens -> 32 / 8 of 784: config 3 8635-8656 vs 8556-8562 img/s, gpurun_out/c17; the GPT-2 shapes,
+// 65536 tokens, keep their split counts). VCX_WG_TARGET: the workgroup count aimed at (default 256).
 static int wg_target() {
   static const int t = [] {
     const char* e = std::getenv("VCX_WG_TARGET");
@@ -329,7 +330,7 @@ int vcx_gemm_wg_splits(int M, int N, int K) {
   const int tiles = (M / gemm_wg::BM) * (N / gemm_wg::BN);
   int s = wg_target() / (tiles > 0 ? tiles : 1);
   if (s < 1) s = 1;
-  if (s > K / 192) s = K / 192;
+  if (s > K / 768) s = K / 768;
   return s < 1 ? 1 : s;
 }
 
