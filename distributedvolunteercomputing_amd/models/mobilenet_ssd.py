@@ -136,9 +136,6 @@ class SSDExecutor:
         # nt: gemm_nt (256 x 256 tiles) where it applies | vision: the 128 x 128-tile vision GEMM (1.197 vs
         # 1.171 ms per chunk; gemm_nt only where its last tile wave is short: 1.177, profiles/r4_detector_chunk.txt)
         self.pw_gemm = os.environ.get("VCX_VISION_PW", "nt")
-        # ... but not where gemm_nt has fewer 256 x 256 tiles than this: conv14_1 (M = 10000, N = 256) made 40
-        # tiles on 256 CUs (27.5 us); the vision GEMM splits K over ~300 workgroups there
-        self.pw_nt_min_tiles = int(os.environ.get("VCX_VISION_PW_NT_MIN_TILES", "128"))
         self._graphs = {}
         self._sides = {}
         self.graph_error = None
@@ -433,8 +430,7 @@ class SSDExecutor:
                 M = N * H * W
                 K, Co = x.shape[-1], p["w"].shape[0]
                 epi = 4 if p["relu"] else 1
-                if (self.pw_gemm == "nt" and ops.native().gemm_nt_supported_epi(M, Co, K, epi)
-                        and ((M + 255) // 256) * (Co // 256) >= self.pw_nt_min_tiles):
+                if self.pw_gemm == "nt" and ops.native().gemm_nt_supported_epi(M, Co, K, epi):
                     # the wide pointwise layers (K, Cout >= 256) on the training GEMM: 256 x 256
                     # tiles, LDS-DMA ring, bias(+ReLU) epilogue, ragged M
                     y = torch.empty(M, Co, device=x.device, dtype=torch.bfloat16)
