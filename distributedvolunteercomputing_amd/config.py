@@ -61,6 +61,9 @@ class RuntimeConfig:
     # VCX_BN_LAYER_WS: each BatchNorm module keeps its own [4C] workspace so the finalize of its
     # statistics runs inside the apply / dx passes (2 launches per layer and direction instead of 3)
     bn_layer_ws: bool = True
+    # VCX_CONV3X3_WGRAD: weight gradients of the ResNet 3x3 convolutions with Cin, Cout % 256 == 0 on gemm_wg with
+    # the patch matrix gathered while staging ("vcx"), or MIOpen's ("lib")
+    conv3x3_wgrad: str = "vcx"
     resnet_join: bool = True  # VCX_RESNET_JOIN: identity-shortcut gradient added in conv1's dgrad GEMM (GradJoin)
     # VCX_RESNET_PROJ_JOIN: projection shortcuts add their input gradient into the one conv1 left (GradJoin)
     resnet_proj_join: bool = True
@@ -95,6 +98,7 @@ _ENV = {
     "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
     "resnet_bn": ("VCX_RESNET_BN", str),
     "resnet_join": ("VCX_RESNET_JOIN", _bool),
+    "conv3x3_wgrad": ("VCX_CONV3X3_WGRAD", str),
     "resnet_proj_join": ("VCX_RESNET_PROJ_JOIN", _bool),
     "bn_layer_ws": ("VCX_BN_LAYER_WS", _bool),
     "conv_find": ("VCX_CONV_FIND", _bool),
@@ -121,7 +125,7 @@ _ENV = {
     "trace_dir": ("VCX_TRACE_DIR", str),
     "metrics_dir": ("VCX_METRICS_DIR", str),
 }
-_CHOICES = {"narrow_gemm": ("lib", "vision"), "gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "off"),
+_CHOICES = {"narrow_gemm": ("lib", "vision"), "conv3x3_wgrad": ("lib", "vcx"), "gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "off"),
             "uplink_pipeline": ("relay", "all", "off")}
 
 _lock = threading.Lock()

@@ -367,6 +367,41 @@ void gemm_wg(at::Tensor a, at::Tensor b, at::Tensor out, bool accumulate, int64_
               (int)a.stride(0), (int)b.stride(0), (int)splits, accumulate ? 1 : 0, (int)loaders, cur_stream());
 }
 
+// 3x3 convolution (pad 1, stride 1|2) weight gradient on gemm_wg with the patch matrix of x gathered while
+// staging: out [Cout, 9 Cin] (+)= dY^T P(x) -- the [Cout][ky][kx][Cin] (channels-last) weight layout.
+// dy: NHWC [imgs, Ho, Wo, Cout], x: NHWC [imgs, H, W, Cin], both contiguous bf16
+bool gemm_wg_conv3x3_supported(int64_t Cout, int64_t Cin, int64_t imgs, int64_t H, int64_t W, int64_t stride) {
+  if (stride != 1 && stride != 2) return false;
+  const int64_t tokens = imgs * ((H - 1) / stride + 1) * ((W - 1) / stride + 1);
+  if (tokens >= (int64_t(1) << 31)) return false;
+  const int splits = vcx_gemm_wg_splits((int)Cout, (int)(9 * Cin), (int)tokens);
+  return vcx_gemm_wg_conv3x3_supported((int)Cout, (int)Cin, (int)tokens, imgs * H * W * Cin * 2, splits);
+}
+
+void gemm_wg_conv3x3(at::Tensor dy, at::Tensor x, at::Tensor out, bool accumulate, int64_t stride, int64_t splits) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && out.is_cuda() && dy.dim() == 4 && x.dim() == 4 && out.dim() == 2,
+              "gemm_wg_conv3x3: dy [N, Ho, Wo, Cout], x [N, H, W, Cin], out [Cout, 9 Cin] on the GPU");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
+              "gemm_wg_conv3x3: bf16");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && out.is_contiguous(), "gemm_wg_conv3x3: contiguous NHWC");
+  const int64_t imgs = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = dy.size(3);
+  TORCH_CHECK(stride == 1 || stride == 2, "gemm_wg_conv3x3: stride 1 or 2");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  TORCH_CHECK(dy.size(0) == imgs && dy.size(1) == Ho && dy.size(2) == Wo, "gemm_wg_conv3x3: dy / x shapes");
+  TORCH_CHECK(out.size(0) == Cout && out.size(1) == 9 * Cin, "gemm_wg_conv3x3: out [Cout, 9 Cin]");
+  const int64_t tokens = imgs * Ho * Wo;
+  TORCH_CHECK(tokens < (int64_t(1) << 31), "gemm_wg_conv3x3: size");
+  if (splits <= 0) splits = vcx_gemm_wg_splits((int)Cout, (int)(9 * Cin), (int)tokens);
+  TORCH_CHECK(vcx_gemm_wg_conv3x3_supported((int)Cout, (int)Cin, (int)tokens, imgs * H * W * Cin * 2, (int)splits),
+              "gemm_wg_conv3x3: needs Cout % 256 == 0, Cin % 256 == 0, N Ho Wo % 64 == 0, N Ho Wo / 192 >= splits, "
+              "x under 2 GB");
+  for (const at::Tensor* t : {&dy, &x, &out})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_wg_conv3x3: 16-B aligned base pointers");
+  at::Tensor ws = at::empty({splits, Cout, 9 * Cin}, dy.options().dtype(at::kFloat));
+  vcx_gemm_wg_conv3x3(dy.data_ptr(), x.data_ptr(), ws.data_ptr<float>(), out.data_ptr(), (int)Cout, (int)Cin, (int)imgs,
+                      (int)H, (int)W, (int)stride, (int)splits, accumulate ? 1 : 0, cur_stream());
+}
+
 at::Tensor transpose_bf16(at::Tensor src, c10::optional<at::Tensor> dst) {
   TORCH_CHECK(src.is_cuda() && src.dim() == 2 && src.is_contiguous() && src.scalar_type() == at::kBFloat16,
               "transpose_bf16: contiguous 2-D bf16");
@@ -834,6 +869,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0);
   m.def("gemm_wg_supported", &gemm_wg_supported, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits") = 0);
+  m.def("gemm_wg_conv3x3_supported", &gemm_wg_conv3x3_supported, py::arg("Cout"), py::arg("Cin"), py::arg("imgs"),
+        py::arg("H"), py::arg("W"), py::arg("stride"));
+  m.def("gemm_wg_conv3x3", &gemm_wg_conv3x3, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = false,
+        py::arg("stride") = 1, py::arg("splits") = 0);
   m.def("gemm_wg", &gemm_wg, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("accumulate") = false,
         py::arg("splits") = 0, py::arg("loaders") = 8);
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),

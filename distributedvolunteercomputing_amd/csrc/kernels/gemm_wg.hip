@@ -88,14 +88,24 @@ struct Frags {
   sx8 w[4];  // B fragments: the wave's 4 column blocks of 16 (output columns)
 };
 
+// Implicit 3x3 convolution operand (IMPL): B is the NHWC input x [imgs, H, W, Cin] of a 3x3 convolution
+// (pad 1, stride st) and the kernel's B matrix is its patch matrix P[token, (ky, kx, c)] -- token = output
+// pixel (img, oy, ox), P = x[img, oy st + ky - 1, ox st + kx - 1, c] (0 outside the image) -- so
+// out[Cout, 9 Cin] = dY^T P is the convolution's weight gradient in the channels-last weight layout
+// [Cout][ky][kx][Cin], without an im2col matrix. Cin % 256 == 0: a 256-column block of P is one tap.
+struct ConvG {
+  int H, W, Ho, Wo, Cin, st, xbytes;
+};
+
 // NLW = the waves that stage the ring: 8 (every wave moves 4 of a slice's 32 pieces; the default) or 4
 // (waves 0-3 move 8 each, waves 4-7 only compute: 1-3 % slower, profiles/r5_gemm_wg.txt; kept as the
 // tested alternative geometry)
-template <int NLW>
+template <int NLW, bool IMPL>
 __global__ void __launch_bounds__(NT, 1)
     gemm_wg_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, float* __restrict__ Cpart, int M, int N,
-                   int K, int lda, int ldb, int tilesN, int tiles, int splits) {
+                   int K, int lda, int ldb, int tilesN, int tiles, int splits, ConvG cg) {
   static_assert(NLW == 4 || NLW == 8, "loader waves");
+  static_assert(!IMPL || NLW == 8, "the implicit operand is staged by all 8 waves");
   constexpr int PPO = 16 / NLW;   // pieces of one operand per loader wave
   constexpr int OPS = 2 * PPO;    // LDS-DMA ops per slice per loader wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -127,12 +137,31 @@ __global__ void __launch_bounds__(NT, 1)
   const int row_e = 2 * lw + (lane >> 5), row_o = row_e + 8;
   const int ch_e = ((lane & 31) ^ swz(row_e)) * 8, ch_o = ((lane & 31) ^ swz(row_o)) * 8;
   const bf16* a_base = A + (int64_t)kbeg * lda + m0;
-  const bf16* b_base = B + (int64_t)kbeg * ldb + n0;
-  const u32x4 ra = desc(a_base, ntok * lda * 2), rb = desc(b_base, ntok * ldb * 2);
+  const bf16* b_base = IMPL ? B : B + (int64_t)kbeg * ldb + n0;
+  const u32x4 ra = desc(a_base, ntok * lda * 2), rb = IMPL ? desc(B, cg.xbytes) : desc(b_base, ntok * ldb * 2);
   const int va_e = (row_e * lda + ch_e) * 2, va_o = (row_o * lda + ch_o) * 2;
   const int vb_e = (row_e * ldb + ch_e) * 2, vb_o = (row_o * ldb + ch_o) * 2;
   const int a_sl = BKS * lda * 2, b_sl = BKS * ldb * 2;  // bytes per slice (32 rows)
   char* const lds_w = smem + lw * 1024;
+
+  // IMPL: the output pixel of each of this lane's B rows (row_e + 16 i of the NEXT slice to stage), advanced
+  // by 32 tokens after every op that stages it (the ops of one piece are issued in slice order); a row
+  // whose tap falls outside the image gets an offset past the resource, which the buffer load returns as 0
+  int timg[PPO], toy[PPO], tox[PPO], tdy = 0, tdx = 0, tc0 = 0;
+  if constexpr (IMPL) {
+    const int tap = n0 / cg.Cin;
+    tc0 = n0 - tap * cg.Cin;
+    tdy = tap / 3 - 1;
+    tdx = tap - 3 * (tap / 3) - 1;
+    const int hw = cg.Ho * cg.Wo;
+#pragma unroll
+    for (int i = 0; i < PPO; ++i) {
+      const int t = kbeg + row_e + 16 * i, img = t / hw, rem = t - img * hw, oy = rem / cg.Wo;
+      timg[i] = img;
+      toy[i] = oy;
+      tox[i] = rem - oy * cg.Wo;
+    }
+  }
 
   // op o (0..OPS-1) of slice s: A pieces for o < PPO (i = o), B pieces after (i = o - PPO)
   auto stage_op = [&](int s, int o) {
@@ -140,10 +169,24 @@ __global__ void __launch_bounds__(NT, 1)
     const int i = o % PPO;
     const bool odd = NLW == 4 && (i & 1);
     const int r16 = NLW == 4 ? (i >> 1) : i;  // 16-row steps
-    if (o < PPO)
+    if (o < PPO) {
       dma16(ra, odd ? va_o : va_e, s * a_sl + r16 * (a_sl >> 1), slot + i * NLW * 1024);
-    else
+    } else if constexpr (IMPL) {
+      const int iy = toy[i] * cg.st + tdy, ix = tox[i] * cg.st + tdx;
+      const bool in = (unsigned)iy < (unsigned)cg.H && (unsigned)ix < (unsigned)cg.W;
+      const int voff = in ? (((timg[i] * cg.H + iy) * cg.W + ix) * cg.Cin + tc0 + ch_e) * 2 : cg.xbytes;
+      dma16(rb, voff, 0, slot + TSLOT_A + i * NLW * 1024);
+      tox[i] += BKS;
+      while (tox[i] >= cg.Wo) {
+        tox[i] -= cg.Wo;
+        if (++toy[i] == cg.Ho) {
+          toy[i] = 0;
+          ++timg[i];
+        }
+      }
+    } else {
       dma16(rb, odd ? vb_o : vb_e, s * b_sl + r16 * (b_sl >> 1), slot + TSLOT_A + i * NLW * 1024);
+    }
   };
   auto stage = [&](int s) {
 #pragma unroll
@@ -307,6 +350,8 @@ __global__ void __launch_bounds__(256) splitk_sum_kernel(const float* __restrict
 
 using namespace vcx;
 
+using gemm_wg::ConvG;
+
 bool vcx_gemm_wg_supported(int M, int N, int K, int splits) {
   return M > 0 && N > 0 && M % gemm_wg::BM == 0 && N % gemm_wg::BN == 0 && K % 64 == 0 && splits >= 1 &&
          K / 192 >= splits;  // >= 3 blocks of 64 tokens per split (nk >= 6)
@@ -336,25 +381,48 @@ int vcx_gemm_wg_splits(int M, int N, int K) {
 
 // Cpart[splits, M, N] (fp32 workspace) = per-split A[K, M]^T . B[K, N]; then out (bf16 [M, N], row
 // stride N) = (accumulate ? out : 0) + the sum of the partials. loaders: 8 (default) or 4 waves stage.
-void vcx_gemm_wg(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
-                 int splits, int accumulate, int loaders, hipStream_t s) {
+static void launch_wg(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
+                      int splits, int accumulate, int loaders, ConvG cg, hipStream_t s) {
   using namespace gemm_wg;
   const int tilesN = N / BN, tiles = (M / BM) * tilesN;
   static const bool attrs = [] {
-    for (const void* k : {(const void*)gemm_wg_kernel<4>, (const void*)gemm_wg_kernel<8>})
+    for (const void* k : {(const void*)gemm_wg_kernel<4, false>, (const void*)gemm_wg_kernel<8, false>,
+                          (const void*)gemm_wg_kernel<8, true>})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     return true;
   }();
   (void)attrs;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(tiles * splits), dim3(NT), LDS_BYTES, s, (const bf16*)A, (const bf16*)B, Cpart, M,
-                       N, K, lda, ldb, tilesN, tiles, splits);
+                       N, K, lda, ldb, tilesN, tiles, splits, cg);
   };
-  if (loaders == 4)
-    go(gemm_wg_kernel<4>);
+  if (cg.Cin > 0)
+    go(gemm_wg_kernel<8, true>);
+  else if (loaders == 4)
+    go(gemm_wg_kernel<4, false>);
   else
-    go(gemm_wg_kernel<8>);
+    go(gemm_wg_kernel<8, false>);
   const int64_t n = (int64_t)M * N;
   hipLaunchKernelGGL(splitk_sum_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, s, Cpart, (bf16*)out, n,
                      splits, accumulate);
+}
+
+void vcx_gemm_wg(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
+                 int splits, int accumulate, int loaders, hipStream_t s) {
+  launch_wg(A, B, Cpart, out, M, N, K, lda, ldb, splits, accumulate, loaders, ConvG{0, 0, 0, 0, 0, 0, 0}, s);
+}
+
+// 3x3 convolution (pad 1) weight gradient: out[Cout, 9 Cin] (+)= dY[tokens, Cout]^T P(x), the channels-last
+// weight layout; dy NHWC [imgs, Ho, Wo, Cout], x NHWC [imgs, H, W, Cin]; splits <= 0: vcx_gemm_wg_splits
+bool vcx_gemm_wg_conv3x3_supported(int Cout, int Cin, int tokens, int64_t xbytes, int splits) {
+  return Cout > 0 && Cin > 0 && Cout % gemm_wg::BM == 0 && Cin % gemm_wg::BN == 0 && tokens > 0 && tokens % 64 == 0 &&
+         splits >= 1 && tokens / 192 >= splits && xbytes + 64 < (int64_t(1) << 31);
+}
+
+void vcx_gemm_wg_conv3x3(const void* dy, const void* x, float* Cpart, void* out, int Cout, int Cin, int imgs, int H,
+                         int W, int stride, int splits, int accumulate, hipStream_t s) {
+  const int Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  const int64_t xbytes = (int64_t)imgs * H * W * Cin * 2;
+  launch_wg(dy, x, Cpart, out, Cout, 9 * Cin, imgs * Ho * Wo, Cout, 0, splits, accumulate, 8,
+            ConvG{H, W, Ho, Wo, Cin, stride, (int)xbytes}, s);
 }

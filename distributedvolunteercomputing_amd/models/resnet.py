@@ -55,6 +55,67 @@ class Conv1x1(nn.Conv2d):
         return y.view(N, H, W, self.out_channels).permute(0, 3, 1, 2)
 
 
+class _Conv3x3(torch.autograd.Function):
+    """3x3 convolution (pad 1) with MIOpen's forward and input gradient and the weight gradient on the
+    hand-written gemm_wg (csrc/kernels/gemm_wg.hip, the patch matrix of x gathered while staging): written
+    straight into the parameter's flat .grad when it has one (channels-last [Cout][ky][kx][Cin] storage)."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride):
+        ctx.save_for_backward(x, w)
+        ctx.stride = stride
+        return F.conv2d(x, w, None, stride, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops._lib import native
+
+        x, w = ctx.saved_tensors
+        s = ctx.stride
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        dw = None
+        if ctx.needs_input_grad[1]:
+            cout = w.shape[0]
+            g = w.grad
+            dyh, xh = dy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1)  # contiguous NHWC views
+            if (g is not None and g.dtype == w.dtype and g.shape == w.shape
+                    and g.is_contiguous(memory_format=torch.channels_last)):
+                native().gemm_wg_conv3x3(dyh, xh, g.permute(0, 2, 3, 1).view(cout, -1), True, s)
+            else:
+                d2 = torch.empty(cout, 3, 3, w.shape[1], device=w.device, dtype=w.dtype)
+                native().gemm_wg_conv3x3(dyh, xh, d2.view(cout, -1), False, s)
+                dw = d2.permute(0, 3, 1, 2)
+        return dx, dw, None
+
+
+class Conv3x3(nn.Conv2d):
+    """3x3 convolution, pad 1 (the bottleneck's conv2): nn.Conv2d, whose weight gradient runs on gemm_wg where
+    the shape tiles (config.conv3x3_wgrad; ResNet-50 stages 3 and 4 at B=128)."""
+
+    def __init__(self, cin, cout, stride=1):
+        super().__init__(cin, cout, 3, stride=stride, padding=1, bias=False)
+
+    def vcx_wgrad(self, x) -> bool:
+        from ..ops._lib import native, use_native
+
+        if not (x.is_cuda and config.get().conv3x3_wgrad == "vcx" and torch.is_grad_enabled()
+                and self.weight.requires_grad and self.weight.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+                and use_native(x) and x.is_contiguous(memory_format=torch.channels_last)
+                and self.weight.is_contiguous(memory_format=torch.channels_last)):
+            return False
+        N, C, H, W = x.shape
+        return bool(native().gemm_wg_conv3x3_supported(self.out_channels, C, N, H, W, self.stride[0]))
+
+    def forward(self, x):
+        if self.vcx_wgrad(x):
+            return _Conv3x3.apply(x, self.weight, self.stride[0])
+        return super().forward(x)
+
+
 class Bottleneck(nn.Module):
     expansion = 4
 
@@ -63,7 +124,7 @@ class Bottleneck(nn.Module):
         cout = width * self.expansion
         self.conv1 = Conv1x1(cin, width)
         self.bn1 = nn.BatchNorm2d(width)
-        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.conv2 = Conv3x3(width, width, stride=stride)
         self.bn2 = nn.BatchNorm2d(width)
         self.conv3 = Conv1x1(width, cout)
         self.bn3 = nn.BatchNorm2d(cout)

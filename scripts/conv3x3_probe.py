@@ -77,4 +77,27 @@ for H, Cin, Cout, s in SHAPES:
 
         tl = bench(lib_wgrad)
         print(f"wgrad {H:3d}^2 {Cin:4d}->{Cout:4d} s{s}: library {tl:7.1f} us {flops / tl / 1e6:6.0f} TF", flush=True)
+# weight gradients: MIOpen vs gemm_wg with the implicit patch operand (csrc/kernels/gemm_wg.hip IMPL) where it tiles
+for H, Cin, Cout, s in SHAPES:
+    if not C.gemm_wg_conv3x3_supported(Cout, Cin, B, H, H, s):
+        continue
+    x = torch.randn(B, Cin, H, H, device=dev, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, Cin, 3, 3, device=dev) / (3 * Cin ** 0.5)).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    Ho = (H - 1) // s + 1
+    flops = 2.0 * B * Ho * Ho * Cout * 9 * Cin
+    dy = torch.randn(B, Cout, Ho, Ho, device=dev, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+
+    def lib_wgrad():
+        return torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                   [False, True, False])[1]
+
+    out = torch.empty(Cout, 9 * Cin, device=dev, dtype=torch.bfloat16)
+    dyh, xh = dy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1)
+    ref = lib_wgrad().float().permute(0, 2, 3, 1).reshape(Cout, -1)
+    C.gemm_wg_conv3x3(dyh, xh, out, False, s)
+    err = float((out.float() - ref).norm() / ref.norm())
+    tl = bench(lib_wgrad)
+    tv = bench(lambda: C.gemm_wg_conv3x3(dyh, xh, out, False, s))
+    print(f"wgrad {H:3d}^2 {Cin:4d}->{Cout:4d} s{s}: library {tl:7.1f} us {flops / tl / 1e6:6.0f} TF | "
+          f"vcx gemm_wg {tv:7.1f} us {flops / tv / 1e6:6.0f} TF | rel err vs library {err:.2e}", flush=True)
 print(f"done in {time.time() - t0:.0f} s", flush=True)
