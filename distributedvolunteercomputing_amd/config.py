@@ -37,6 +37,9 @@ class RuntimeConfig:
     narrow_gemm: str = "lib"
     dgrad_ps: bool = True  # VCX_DGRAD_PS: input gradients dX = dY W with K <= 2304 on gemm_ps (measured faster)
     gemm_wgrad: str = "vcx"  # VCX_GEMM_WGRAD: weight gradients on "vcx" (gemm_wg, hand-written) or "lib" (split-M batched GEMM)
+    # VCX_WGRAD_WIDE: also outputs of more than 128 256x256 tiles with <= 1024 input columns on gemm_wg (the
+    # GPT-2 LM heads, [50304, 768 | 1024]: 1..4 token splits, ragged last row panel)
+    wgrad_wide: bool = True
     gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)
     wgrad_big_split_min_m: int = 16384  # VCX_WGRAD_BIG_SPLIT_MIN_M: rows above which weight grads split over K
     async_wgrad: bool = False  # VCX_ASYNC_WGRAD: weight-grad GEMMs on a side stream (measured slower)
@@ -103,6 +106,7 @@ _ENV = {
     "bn_layer_ws": ("VCX_BN_LAYER_WS", _bool),
     "conv_find": ("VCX_CONV_FIND", _bool),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),
+    "wgrad_wide": ("VCX_WGRAD_WIDE", _bool),
     "gemm_select": ("VCX_GEMM_SELECT", _bool),
     "wgrad_big_split_min_m": ("VCX_WGRAD_BIG_SPLIT_MIN_M", int),
     "async_wgrad": ("VCX_ASYNC_WGRAD", _bool),

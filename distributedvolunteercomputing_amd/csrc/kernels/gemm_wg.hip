@@ -27,6 +27,7 @@
 // Reference analog: none (the reference trains nothing; SURVEY.md §2.9 north-star trainer).
 #include <type_traits>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "vcx_common.h"
@@ -57,7 +58,7 @@ __device__ __forceinline__ sx8 tr_frag(const char* p0, const char* p1) {
 
 // buffer resource words over [base, base + bytes) for inline asm ("s" operand): wave-uniform base and
 // size (SGPRs), 32-bit per-lane offsets
-__device__ __forceinline__ u32x4 desc(const void* base, int bytes) {
+__device__ __forceinline__ u32x4 desc(const void* base, unsigned bytes) {
   const uint64_t a = (uint64_t)base;
   return u32x4{(unsigned)a, (unsigned)(a >> 32) & 0xffffu, (unsigned)bytes, 0x00020000u};
 }
@@ -138,10 +139,13 @@ __global__ void __launch_bounds__(NT, 1)
   const int ch_e = ((lane & 31) ^ swz(row_e)) * 8, ch_o = ((lane & 31) ^ swz(row_o)) * 8;
   const bf16* a_base = A + (int64_t)kbeg * lda + m0;
   const bf16* b_base = IMPL ? B : B + (int64_t)kbeg * ldb + n0;
-  const u32x4 ra = desc(a_base, ntok * lda * 2), rb = IMPL ? desc(B, cg.xbytes) : desc(b_base, ntok * ldb * 2);
+  // (a split's panel of a wide operand -- the GPT-2 LM head's [tokens, 50304] logit gradient -- passes 2 GB:
+  // byte counts and slice offsets are unsigned 32-bit, host check < 4 GB)
+  const u32x4 ra = desc(a_base, (unsigned)ntok * (unsigned)lda * 2u),
+              rb = IMPL ? desc(B, (unsigned)cg.xbytes) : desc(b_base, (unsigned)ntok * (unsigned)ldb * 2u);
   const int va_e = (row_e * lda + ch_e) * 2, va_o = (row_o * lda + ch_o) * 2;
   const int vb_e = (row_e * ldb + ch_e) * 2, vb_o = (row_o * ldb + ch_o) * 2;
-  const int a_sl = BKS * lda * 2, b_sl = BKS * ldb * 2;  // bytes per slice (32 rows)
+  const unsigned a_sl = BKS * lda * 2, b_sl = BKS * ldb * 2;  // bytes per slice (32 rows)
   char* const lds_w = smem + lw * 1024;
 
   // IMPL: the output pixel of each of this lane's B rows (row_e + 16 i of the NEXT slice to stage), advanced
@@ -170,7 +174,7 @@ __global__ void __launch_bounds__(NT, 1)
     const bool odd = NLW == 4 && (i & 1);
     const int r16 = NLW == 4 ? (i >> 1) : i;  // 16-row steps
     if (o < PPO) {
-      dma16(ra, odd ? va_o : va_e, s * a_sl + r16 * (a_sl >> 1), slot + i * NLW * 1024);
+      dma16(ra, odd ? va_o : va_e, (int)((unsigned)s * a_sl + (unsigned)r16 * (a_sl >> 1)), slot + i * NLW * 1024);
     } else if constexpr (IMPL) {
       const int iy = toy[i] * cg.st + tdy, ix = tox[i] * cg.st + tdx;
       const bool in = (unsigned)iy < (unsigned)cg.H && (unsigned)ix < (unsigned)cg.W;
@@ -185,7 +189,8 @@ __global__ void __launch_bounds__(NT, 1)
         }
       }
     } else {
-      dma16(rb, odd ? vb_o : vb_e, s * b_sl + r16 * (b_sl >> 1), slot + TSLOT_A + i * NLW * 1024);
+      dma16(rb, odd ? vb_o : vb_e, (int)((unsigned)s * b_sl + (unsigned)r16 * (b_sl >> 1)),
+            slot + TSLOT_A + i * NLW * 1024);
     }
   };
   auto stage = [&](int s) {
@@ -321,14 +326,18 @@ __global__ void __launch_bounds__(NT, 1)
   else
     run(F{});
 
-  // ---- fp32 partial: acc[i][j] = C[m][n .. n + 3], m = row block i + (lane & 15), n = column block j
+  // ---- fp32 partial: acc[i][j] = C[m][n .. n + 3], m = row block i + (lane & 15), n = column block j.
+  // Ragged M (M % 256 = 128: the LM head's 50304 rows): the last row panel's A columns past M read the next
+  // token row's values (or 0 past the resource), and their output rows are not stored
   const int mrow = m0 + wm * 128 + (lane & 15);
   const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
   float* cp = Cpart + (int64_t)split * M * N;
 #pragma unroll
   for (int i = 0; i < 8; ++i)
+    if (mrow + 16 * i < M) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *(f32x4*)(cp + (int64_t)(mrow + 16 * i) * N + ncol + 16 * j) = acc[i][j];
+      for (int j = 0; j < 4; ++j) *(f32x4*)(cp + (int64_t)(mrow + 16 * i) * N + ncol + 16 * j) = acc[i][j];
+    }
 }
 
 // out[i] (bf16) = (accumulate ? out[i] : 0) + sum_s part[s][i], 4 elements per thread
@@ -353,8 +362,12 @@ using namespace vcx;
 using gemm_wg::ConvG;
 
 bool vcx_gemm_wg_supported(int M, int N, int K, int splits) {
-  return M > 0 && N > 0 && M % gemm_wg::BM == 0 && N % gemm_wg::BN == 0 && K % 64 == 0 && splits >= 1 &&
-         K / 192 >= splits;  // >= 3 blocks of 64 tokens per split (nk >= 6)
+  if (!(M > 0 && N > 0 && M % 128 == 0 && N % gemm_wg::BN == 0 && K % 64 == 0 && splits >= 1 &&
+        K / 192 >= splits))  // >= 3 blocks of 64 tokens per split (nk >= 6)
+    return false;
+  // a split's operand panels stay under 4 GB (unsigned 32-bit buffer offsets)
+  const int64_t tok = ((int64_t)(K / 64 + splits - 1) / splits) * 64;
+  return tok * std::max(M, N) * 2 < (int64_t(1) << 32) - (int64_t(1) << 20);
 }
 
 // token-axis splits: about one round of workgroups over the CUs ((M/256)(N/256) tiles x S), with at least
@@ -372,7 +385,20 @@ static int wg_target() {
 }
 
 int vcx_gemm_wg_splits(int M, int N, int K) {
-  const int tiles = (M / gemm_wg::BM) * (N / gemm_wg::BN);
+  const int tiles = ((M + gemm_wg::BM - 1) / gemm_wg::BM) * (N / gemm_wg::BN);
+  if (tiles > wg_target()) {
+    // more tiles than one round (the LM head: 591): 1..4 splits, the fewest rounds of workgroups per unit of
+    // work -- ceil(tiles S / 256) / S -- among the counts whose split panels stay under 4 GB
+    int best = 0;
+    double best_cost = 1e30;
+    for (int s = 1; s <= 4 && s <= K / 768; ++s) {
+      const int64_t tok = ((int64_t)(K / 64 + s - 1) / s) * 64;
+      if (tok * std::max(M, N) * 2 >= (int64_t(1) << 32) - (int64_t(1) << 20)) continue;
+      const double cost = (double)((tiles * s + wg_target() - 1) / wg_target()) / s;
+      if (cost < best_cost - 1e-9) best_cost = cost, best = s;
+    }
+    return best > 0 ? best : 4;
+  }
   int s = wg_target() / (tiles > 0 ? tiles : 1);
   if (s < 1) s = 1;
   if (s > K / 768) s = K / 768;
@@ -384,7 +410,7 @@ int vcx_gemm_wg_splits(int M, int N, int K) {
 static void launch_wg(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
                       int splits, int accumulate, int loaders, ConvG cg, hipStream_t s) {
   using namespace gemm_wg;
-  const int tilesN = N / BN, tiles = (M / BM) * tilesN;
+  const int tilesN = N / BN, tiles = ((M + BM - 1) / BM) * tilesN;
   static const bool attrs = [] {
     for (const void* k : {(const void*)gemm_wg_kernel<4, false>, (const void*)gemm_wg_kernel<8, false>,
                           (const void*)gemm_wg_kernel<8, true>})

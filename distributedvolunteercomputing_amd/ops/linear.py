@@ -166,10 +166,14 @@ def gemm_wg_ok(M: int, N: int, K: int, t) -> bool:
     """The hand-written weight-gradient GEMM (csrc/kernels/gemm_wg.hip) takes dW[N, K] from M tokens: the
     default (config.gemm_wgrad == "vcx") wherever the output is a few dozen 256 x 256 tiles that need the
     token split -- 1.17-1.23 PF/s at the GPT-2 shapes against the library's 0.81-0.98
-    (profiles/r5_gemm_wg.txt). Outputs of more than 128 tiles (Llama-3-8B's projections) fill the GPU
-    without a split and stay on the library."""
-    return (config.get().gemm_wgrad == "vcx" and use_native(t) and t.dtype == torch.bfloat16
-            and (N // 256) * (K // 256) <= 128 and bool(native().gemm_wg_supported(N, K, M)))
+    (profiles/r5_gemm_wg.txt). Outputs of more than 128 tiles fill the GPU without a split: Llama-3-8B's
+    projections stay on the library; the GPT-2 LM heads ([50304, 768 | 1024], K <= 1024) take gemm_wg with
+    1..4 splits (config.wgrad_wide)."""
+    cfg = config.get()
+    tiles = ((N + 255) // 256) * (K // 256)
+    return (cfg.gemm_wgrad == "vcx" and use_native(t) and t.dtype == torch.bfloat16
+            and (tiles <= 128 or (cfg.wgrad_wide and K <= 1024 and M >= 32768))
+            and bool(native().gemm_wg_supported(N, K, M)))
 
 
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False):

@@ -14,7 +14,7 @@ def _ref(dy, x):
 
 @pytest.mark.parametrize("M,N,K,splits", [(4096, 768, 3072, 7), (4096, 3072, 768, 7), (8192, 2304, 768, 9),
                                           (2048, 768, 768, 10), (1024, 256, 512, 1), (8192, 512, 256, 3),
-                                          (65536, 768, 768, 28)])
+                                          (65536, 768, 768, 28), (4096, 1152, 768, 3), (8192, 640, 512, 2)])
 def test_gemm_wg_matches_fp32(gpu, M, N, K, splits):
     from distributedvolunteercomputing_amd.ops import native
 
@@ -83,3 +83,28 @@ def test_gemm_wg_repeat_runs_bit_identical(gpu):
     for _ in range(10):
         C.gemm_wg(dy, x, out)
         assert torch.equal(out, first)
+
+
+def test_gemm_wg_lm_head_shape_default_splits(gpu):
+    """The GPT-2 LM head's weight gradient [50304, 768] over 65536 tokens (ops/linear.py gemm_wg_ok,
+    config.wgrad_wide): 591 tiles with a ragged last row panel (50304 = 196.5 x 256), the default 3 token
+    splits, each split's [21888, 50304] logit-gradient panel past 2 GB (unsigned buffer offsets)."""
+    from distributedvolunteercomputing_amd.ops import native
+    from distributedvolunteercomputing_amd.ops.linear import gemm_wg_ok
+
+    C = native()
+    T, V, D = 65536, 50304, 768
+    assert C.gemm_wg_supported(V, D, T) and gemm_wg_ok(T, V, D, torch.empty(1, device=gpu, dtype=torch.bfloat16))
+    g = torch.Generator(device=gpu).manual_seed(11)
+    dy = (torch.randn(T, V, device=gpu, generator=g, dtype=torch.bfloat16) * 0.01)
+    x = torch.randn(T, D, device=gpu, generator=g).to(torch.bfloat16)
+    ref = torch.zeros(V, D, device=gpu)
+    for i in range(0, T, 8192):
+        ref += dy[i:i + 8192].float().t() @ x[i:i + 8192].float()
+    out = torch.full((V, D), float("nan"), device=gpu, dtype=torch.bfloat16)
+    C.gemm_wg(dy, x, out)
+    scale = ref.abs().max().item()
+    assert torch.isfinite(out.float()).all()
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 8e-3 * scale, (err, scale)
+
