@@ -64,7 +64,7 @@ class RuntimeConfig:
     # VCX_BN_LAYER_WS: each BatchNorm module keeps its own [4C] workspace so the finalize of its
     # statistics runs inside the apply / dx passes (2 launches per layer and direction instead of 3)
     bn_layer_ws: bool = True
-    # VCX_CONV3X3_WGRAD: weight gradients of the ResNet 3x3 convolutions with Cin, Cout % 256 == 0 on gemm_wg with
+    # VCX_CONV3X3_WGRAD: weight gradients of the ResNet 3x3 convolutions with Cin, Cout % 128 == 0 on gemm_wg with
     # the patch matrix gathered while staging ("vcx"), or MIOpen's ("lib")
     conv3x3_wgrad: str = "vcx"
     resnet_join: bool = True  # VCX_RESNET_JOIN: identity-shortcut gradient added in conv1's dgrad GEMM (GradJoin)

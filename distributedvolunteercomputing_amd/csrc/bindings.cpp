@@ -395,7 +395,7 @@ void gemm_wg_conv3x3(at::Tensor dy, at::Tensor x, at::Tensor out, bool accumulat
   TORCH_CHECK(tokens < (int64_t(1) << 31), "gemm_wg_conv3x3: size");
   if (splits <= 0) splits = vcx_gemm_wg_splits((int)Cout, (int)(9 * Cin), (int)tokens);
   TORCH_CHECK(vcx_gemm_wg_conv3x3_supported((int)Cout, (int)Cin, (int)tokens, imgs * H * W * Cin * 2, (int)splits),
-              "gemm_wg_conv3x3: needs Cout % 256 == 0, Cin % 256 == 0, N Ho Wo % 64 == 0, N Ho Wo / 192 >= splits, "
+              "gemm_wg_conv3x3: needs Cout % 128 == 0, Cin % 128 == 0, N Ho Wo % 64 == 0, N Ho Wo / 192 >= splits, "
               "x under 2 GB");
   for (const at::Tensor* t : {&dy, &x, &out})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_wg_conv3x3: 16-B aligned base pointers");

@@ -93,7 +93,9 @@ struct Frags {
 // (pad 1, stride st) and the kernel's B matrix is its patch matrix P[token, (ky, kx, c)] -- token = output
 // pixel (img, oy, ox), P = x[img, oy st + ky - 1, ox st + kx - 1, c] (0 outside the image) -- so
 // out[Cout, 9 Cin] = dY^T P is the convolution's weight gradient in the channels-last weight layout
-// [Cout][ky][kx][Cin], without an im2col matrix. Cin % 256 == 0: a 256-column block of P is one tap.
+// [Cout][ky][kx][Cin], without an im2col matrix. Each lane's 8 columns lie in one tap (Cin % 8 == 0; a
+// 256-column block of P spans 2 taps at Cin = 128); past the last tap (9 Cin % 256 != 0: the ragged last
+// column block) the lane stages zeros and those output columns are not stored.
 struct ConvG {
   int H, W, Ho, Wo, Cin, st, xbytes;
 };
@@ -150,12 +152,13 @@ __global__ void __launch_bounds__(NT, 1)
 
   // IMPL: the output pixel of each of this lane's B rows (row_e + 16 i of the NEXT slice to stage), advanced
   // by 32 tokens after every op that stages it (the ops of one piece are issued in slice order); a row
-  // whose tap falls outside the image gets an offset past the resource, which the buffer load returns as 0
+  // whose tap falls outside the image gets an offset past the resource, which the buffer load returns as 0.
+  // The lane's tap and channel come from its own patch column n0 + ch_e (the same in every row it stages)
   int timg[PPO], toy[PPO], tox[PPO], tdy = 0, tdx = 0, tc0 = 0;
   if constexpr (IMPL) {
-    const int tap = n0 / cg.Cin;
-    tc0 = n0 - tap * cg.Cin;
-    tdy = tap / 3 - 1;
+    const int pcol = n0 + ch_e, tap = pcol / cg.Cin;
+    tc0 = pcol - tap * cg.Cin;
+    tdy = tap < 9 ? tap / 3 - 1 : (1 << 24);  // past the last tap: never inside the image
     tdx = tap - 3 * (tap / 3) - 1;
     const int hw = cg.Ho * cg.Wo;
 #pragma unroll
@@ -178,7 +181,7 @@ __global__ void __launch_bounds__(NT, 1)
     } else if constexpr (IMPL) {
       const int iy = toy[i] * cg.st + tdy, ix = tox[i] * cg.st + tdx;
       const bool in = (unsigned)iy < (unsigned)cg.H && (unsigned)ix < (unsigned)cg.W;
-      const int voff = in ? (((timg[i] * cg.H + iy) * cg.W + ix) * cg.Cin + tc0 + ch_e) * 2 : cg.xbytes;
+      const int voff = in ? (((timg[i] * cg.H + iy) * cg.W + ix) * cg.Cin + tc0) * 2 : cg.xbytes;
       dma16(rb, voff, 0, slot + TSLOT_A + i * NLW * 1024);
       tox[i] += BKS;
       while (tox[i] >= cg.Wo) {
@@ -336,7 +339,8 @@ __global__ void __launch_bounds__(NT, 1)
   for (int i = 0; i < 8; ++i)
     if (mrow + 16 * i < M) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) *(f32x4*)(cp + (int64_t)(mrow + 16 * i) * N + ncol + 16 * j) = acc[i][j];
+      for (int j = 0; j < 4; ++j)
+        if (ncol + 16 * j < N) *(f32x4*)(cp + (int64_t)(mrow + 16 * i) * N + ncol + 16 * j) = acc[i][j];
     }
 }
 
@@ -385,7 +389,7 @@ static int wg_target() {
 }
 
 int vcx_gemm_wg_splits(int M, int N, int K) {
-  const int tiles = ((M + gemm_wg::BM - 1) / gemm_wg::BM) * (N / gemm_wg::BN);
+  const int tiles = ((M + gemm_wg::BM - 1) / gemm_wg::BM) * ((N + gemm_wg::BN - 1) / gemm_wg::BN);
   if (tiles > wg_target()) {
     // more tiles than one round (the LM head: 591): 1..4 splits, the fewest rounds of workgroups per unit of
     // work -- ceil(tiles S / 256) / S -- among the counts whose split panels stay under 4 GB
@@ -410,7 +414,7 @@ int vcx_gemm_wg_splits(int M, int N, int K) {
 static void launch_wg(const void* A, const void* B, float* Cpart, void* out, int M, int N, int K, int lda, int ldb,
                       int splits, int accumulate, int loaders, ConvG cg, hipStream_t s) {
   using namespace gemm_wg;
-  const int tilesN = N / BN, tiles = ((M + BM - 1) / BM) * tilesN;
+  const int tilesN = (N + BN - 1) / BN, tiles = ((M + BM - 1) / BM) * tilesN;
   static const bool attrs = [] {
     for (const void* k : {(const void*)gemm_wg_kernel<4, false>, (const void*)gemm_wg_kernel<8, false>,
                           (const void*)gemm_wg_kernel<8, true>})
@@ -441,7 +445,7 @@ void vcx_gemm_wg(const void* A, const void* B, float* Cpart, void* out, int M, i
 // 3x3 convolution (pad 1) weight gradient: out[Cout, 9 Cin] (+)= dY[tokens, Cout]^T P(x), the channels-last
 // weight layout; dy NHWC [imgs, Ho, Wo, Cout], x NHWC [imgs, H, W, Cin]; splits <= 0: vcx_gemm_wg_splits
 bool vcx_gemm_wg_conv3x3_supported(int Cout, int Cin, int tokens, int64_t xbytes, int splits) {
-  return Cout > 0 && Cin > 0 && Cout % gemm_wg::BM == 0 && Cin % gemm_wg::BN == 0 && tokens > 0 && tokens % 64 == 0 &&
+  return Cout > 0 && Cin > 0 && Cout % 128 == 0 && Cin % 128 == 0 && tokens > 0 && tokens % 64 == 0 &&
          splits >= 1 && tokens / 192 >= splits && xbytes + 64 < (int64_t(1) << 31);
 }
 

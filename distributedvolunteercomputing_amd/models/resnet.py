@@ -94,7 +94,7 @@ class _Conv3x3(torch.autograd.Function):
 
 class Conv3x3(nn.Conv2d):
     """3x3 convolution, pad 1 (the bottleneck's conv2): nn.Conv2d, whose weight gradient runs on gemm_wg where
-    the shape tiles (config.conv3x3_wgrad; ResNet-50 stages 3 and 4 at B=128)."""
+    the shape tiles (config.conv3x3_wgrad; ResNet-50 stages 2, 3 and 4 at B=128)."""
 
     def __init__(self, cin, cout, stride=1):
         super().__init__(cin, cout, 3, stride=stride, padding=1, bias=False)

@@ -1,6 +1,6 @@
 """3x3 convolution weight gradient on the hand-written gemm_wg with the patch matrix of x gathered while
 staging (csrc/kernels/gemm_wg.hip IMPL, bindings gemm_wg_conv3x3; models/resnet.py Conv3x3): against the fp32
-torch weight gradient of the same bf16 operands, at the ResNet-50 stage-3/4 channel counts, stride 1 and 2,
+torch weight gradient of the same bf16 operands, at the ResNet-50 stage-2/3/4 channel counts, stride 1 and 2,
 including the zero padding at every image border and accumulation into an existing gradient."""
 import pytest
 import torch
@@ -22,7 +22,10 @@ def _rel(a, b):
 
 # (imgs, H, Cin, Cout, stride): tokens = imgs * Ho * Wo is a multiple of 64
 SHAPES = [(16, 14, 256, 256, 1), (64, 7, 512, 512, 1), (16, 28, 256, 256, 2), (16, 14, 256, 512, 1),
-          (64, 14, 512, 256, 2), (4, 32, 256, 256, 1)]
+          (64, 14, 512, 256, 2), (4, 32, 256, 256, 1),
+          # 128 channels (ResNet-50 stage 2): 2 taps per 256-column block, ragged last block (1152 columns),
+          # ragged output rows (Cout = 128 of a 256-row tile)
+          (16, 28, 128, 128, 1), (16, 56, 128, 128, 2), (8, 28, 128, 256, 1), (8, 28, 256, 128, 1)]
 
 
 @pytest.mark.parametrize("imgs,H,cin,cout,s", SHAPES)
@@ -45,7 +48,7 @@ def test_conv3x3_wgrad_matches_fp32(C, gpu, imgs, H, cin, cout, s):
 
 
 def test_conv3x3_wgrad_refuses_untiled_shapes(C):
-    assert not C.gemm_wg_conv3x3_supported(128, 128, 128, 28, 28, 1)  # Cout, Cin % 256
+    assert not C.gemm_wg_conv3x3_supported(64, 64, 128, 56, 56, 1)    # Cout, Cin % 128
     assert not C.gemm_wg_conv3x3_supported(256, 256, 3, 14, 14, 1)    # 588 tokens: not a multiple of 64
     assert not C.gemm_wg_conv3x3_supported(256, 256, 16, 14, 14, 3)   # stride
 
