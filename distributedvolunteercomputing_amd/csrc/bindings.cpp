@@ -356,12 +356,12 @@ void gemm_wg(at::Tensor a, at::Tensor b, at::Tensor out, bool accumulate, int64_
   TORCH_CHECK(b.size(0) == K && out.size(0) == M && out.size(1) == N, "gemm_wg: shape mismatch");
   if (splits <= 0) splits = vcx_gemm_wg_splits((int)M, (int)N, (int)K);
   TORCH_CHECK(vcx_gemm_wg_supported((int)M, (int)N, (int)K, (int)splits),
-              "gemm_wg: needs M % 128 == 0, N % 256 == 0, K % 64 == 0, K / 192 >= splits, split panels under 4 GB");
+              "gemm_wg: needs M % 128 == 0, N % 256 == 0, K % 64 == 0, K / 192 >= splits, split panels under 2 GB");
   TORCH_CHECK(loaders == 4 || loaders == 8, "gemm_wg: loaders 4 or 8");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_wg: 16-B aligned rows");
   const int64_t tok = ((K / 64 + splits - 1) / splits) * 64;  // the longest split's token rows
-  TORCH_CHECK(tok * std::max(a.stride(0), b.stride(0)) * 2 < (int64_t(1) << 32) - (int64_t(1) << 20),
-              "gemm_wg: a split's operand panel must stay under 4 GB (more splits)");
+  TORCH_CHECK(tok * std::max(a.stride(0), b.stride(0)) * 2 < (int64_t(1) << 31) - (int64_t(1) << 20),
+              "gemm_wg: a split's operand panel must stay under 2 GB (more splits)");
   for (const at::Tensor* t : {&a, &b, &out})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_wg: 16-B aligned base pointers");
   at::Tensor ws = at::empty({splits, M, N}, a.options().dtype(at::kFloat));

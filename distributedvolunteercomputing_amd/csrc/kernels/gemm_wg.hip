@@ -141,11 +141,14 @@ __global__ void __launch_bounds__(NT, 1)
   const int ch_e = ((lane & 31) ^ swz(row_e)) * 8, ch_o = ((lane & 31) ^ swz(row_o)) * 8;
   const bf16* a_base = A + (int64_t)kbeg * lda + m0;
   const bf16* b_base = IMPL ? B : B + (int64_t)kbeg * ldb + n0;
-  // (a split's panel of a wide operand -- the GPT-2 LM head's [tokens, 50304] logit gradient -- passes 2 GB:
-  // byte counts and slice offsets are unsigned 32-bit, host check < 4 GB)
+  // (byte counts and slice offsets computed unsigned; the host keeps a split's panel under 2 GB)
   const u32x4 ra = desc(a_base, (unsigned)ntok * (unsigned)lda * 2u),
               rb = IMPL ? desc(B, (unsigned)cg.xbytes) : desc(b_base, (unsigned)ntok * (unsigned)ldb * 2u);
-  const int va_e = (row_e * lda + ch_e) * 2, va_o = (row_o * lda + ch_o) * 2;
+  // ragged last row panel (M % 256 = 128): the lanes of columns past M re-read the panel's last valid chunk
+  // (their output rows are not stored), so no load leaves the operand -- the LM head's logit gradient ends
+  // exactly at its allocation's end
+  const int cha_e = min(ch_e, M - m0 - 8), cha_o = min(ch_o, M - m0 - 8);
+  const int va_e = (row_e * lda + cha_e) * 2, va_o = (row_o * lda + cha_o) * 2;
   const int vb_e = (row_e * ldb + ch_e) * 2, vb_o = (row_o * ldb + ch_o) * 2;
   const unsigned a_sl = BKS * lda * 2, b_sl = BKS * ldb * 2;  // bytes per slice (32 rows)
   char* const lds_w = smem + lw * 1024;
@@ -369,9 +372,9 @@ bool vcx_gemm_wg_supported(int M, int N, int K, int splits) {
   if (!(M > 0 && N > 0 && M % 128 == 0 && N % gemm_wg::BN == 0 && K % 64 == 0 && splits >= 1 &&
         K / 192 >= splits))  // >= 3 blocks of 64 tokens per split (nk >= 6)
     return false;
-  // a split's operand panels stay under 4 GB (unsigned 32-bit buffer offsets)
+  // a split's operand panels stay under 2 GB (32-bit buffer offsets, slice offsets in soffset)
   const int64_t tok = ((int64_t)(K / 64 + splits - 1) / splits) * 64;
-  return tok * std::max(M, N) * 2 < (int64_t(1) << 32) - (int64_t(1) << 20);
+  return tok * std::max(M, N) * 2 < (int64_t(1) << 31) - (int64_t(1) << 20);
 }
 
 // token-axis splits: about one round of workgroups over the CUs ((M/256)(N/256) tiles x S), with at least
@@ -392,12 +395,12 @@ int vcx_gemm_wg_splits(int M, int N, int K) {
   const int tiles = ((M + gemm_wg::BM - 1) / gemm_wg::BM) * ((N + gemm_wg::BN - 1) / gemm_wg::BN);
   if (tiles > wg_target()) {
     // more tiles than one round (the LM head: 591): 1..4 splits, the fewest rounds of workgroups per unit of
-    // work -- ceil(tiles S / 256) / S -- among the counts whose split panels stay under 4 GB
+    // work -- ceil(tiles S / 256) / S -- among the counts whose split panels stay under 2 GB
     int best = 0;
     double best_cost = 1e30;
     for (int s = 1; s <= 4 && s <= K / 768; ++s) {
       const int64_t tok = ((int64_t)(K / 64 + s - 1) / s) * 64;
-      if (tok * std::max(M, N) * 2 >= (int64_t(1) << 32) - (int64_t(1) << 20)) continue;
+      if (tok * std::max(M, N) * 2 >= (int64_t(1) << 31) - (int64_t(1) << 20)) continue;
       const double cost = (double)((tiles * s + wg_target() - 1) / wg_target()) / s;
       if (cost < best_cost - 1e-9) best_cost = cost, best = s;
     }

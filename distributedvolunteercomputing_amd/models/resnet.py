@@ -94,7 +94,7 @@ class _Conv3x3(torch.autograd.Function):
 
 class Conv3x3(nn.Conv2d):
     """3x3 convolution, pad 1 (the bottleneck's conv2): nn.Conv2d, whose weight gradient runs on gemm_wg where
-    the shape tiles (config.conv3x3_wgrad; ResNet-50 stages 2, 3 and 4 at B=128)."""
+    the shape tiles (config.conv3x3_wgrad; ResNet-50 stages 3 and 4 at B=128)."""
 
     def __init__(self, cin, cout, stride=1):
         super().__init__(cin, cout, 3, stride=stride, padding=1, bias=False)
@@ -108,7 +108,10 @@ class Conv3x3(nn.Conv2d):
                 and self.weight.is_contiguous(memory_format=torch.channels_last)):
             return False
         N, C, H, W = x.shape
-        return bool(native().gemm_wg_conv3x3_supported(self.out_channels, C, N, H, W, self.stride[0]))
+        # 128 output channels (stage 2) tile but run half-empty 256-row tiles: even with MIOpen there
+        # (77-79 vs 78-82 us, config 3 unchanged, profiles/r5_conv3x3_probe.txt) -- 256-multiples only
+        return self.out_channels % 256 == 0 and bool(
+            native().gemm_wg_conv3x3_supported(self.out_channels, C, N, H, W, self.stride[0]))
 
     def forward(self, x):
         if self.vcx_wgrad(x):

@@ -87,8 +87,9 @@ def test_gemm_wg_repeat_runs_bit_identical(gpu):
 
 def test_gemm_wg_lm_head_shape_default_splits(gpu):
     """The GPT-2 LM head's weight gradient [50304, 768] over 65536 tokens (ops/linear.py gemm_wg_ok,
-    config.wgrad_wide): 591 tiles with a ragged last row panel (50304 = 196.5 x 256), the default 3 token
-    splits, each split's [21888, 50304] logit-gradient panel past 2 GB (unsigned buffer offsets)."""
+    config.wgrad_wide): 591 tiles with a ragged last row panel (50304 = 196.5 x 256) whose lanes past the
+    last column re-read valid data (the logit gradient ends at its allocation's end), the default 4 token
+    splits (each split's [16384, 50304] panel 1.65 GB, under the 2 GB offset limit)."""
     from distributedvolunteercomputing_amd.ops import native
     from distributedvolunteercomputing_amd.ops.linear import gemm_wg_ok
 
