@@ -89,7 +89,8 @@ def test_abort_posted_without_the_prefix_is_not_followed(coord):
         assert not peer.tripped()
         assert peer._njoin() == 0 and peer._pending_joiners(1) == []
         # control: the prefixed key is the one the peers act on
-        dist.PrefixStore(coord.store_secret, attacker).set("vcx/el/abort/0", "real abort")
+        # (the key of the generation the peer is in: under a loaded CPU its lease bookkeeping can move on)
+        dist.PrefixStore(coord.store_secret, attacker).set(f"vcx/el/abort/{peer.gen}", "real abort")
         peer._watch()
         assert peer.tripped() and peer.abort_reason() == "real abort"
     finally:
