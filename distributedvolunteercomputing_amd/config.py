@@ -40,6 +40,9 @@ class RuntimeConfig:
     # VCX_WGRAD_WIDE: also outputs of more than 128 256x256 tiles with <= 1024 input columns on gemm_wg (the
     # GPT-2 LM heads, [50304, 768 | 1024]: 1..4 token splits, ragged last row panel)
     wgrad_wide: bool = True
+    # VCX_WGRAD_RAGGED: outputs whose row count is a multiple of 128 but not 256 (half-empty last row panel;
+    # ResNet-50 stage 2's [128, 256 | 512]) on gemm_wg too; the LM heads take it regardless
+    wgrad_ragged: bool = True
     gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)
     wgrad_big_split_min_m: int = 16384  # VCX_WGRAD_BIG_SPLIT_MIN_M: rows above which weight grads split over K
     async_wgrad: bool = False  # VCX_ASYNC_WGRAD: weight-grad GEMMs on a side stream (measured slower)
@@ -107,6 +110,7 @@ _ENV = {
     "conv_find": ("VCX_CONV_FIND", _bool),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),
     "wgrad_wide": ("VCX_WGRAD_WIDE", _bool),
+    "wgrad_ragged": ("VCX_WGRAD_RAGGED", _bool),
     "gemm_select": ("VCX_GEMM_SELECT", _bool),
     "wgrad_big_split_min_m": ("VCX_WGRAD_BIG_SPLIT_MIN_M", int),
     "async_wgrad": ("VCX_ASYNC_WGRAD", _bool),

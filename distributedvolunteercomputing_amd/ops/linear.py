@@ -171,8 +171,9 @@ def gemm_wg_ok(M: int, N: int, K: int, t) -> bool:
     1..4 splits (config.wgrad_wide)."""
     cfg = config.get()
     tiles = ((N + 255) // 256) * (K // 256)
+    wide = cfg.wgrad_wide and K <= 1024 and M >= 32768 and tiles > 128
     return (cfg.gemm_wgrad == "vcx" and use_native(t) and t.dtype == torch.bfloat16
-            and (tiles <= 128 or (cfg.wgrad_wide and K <= 1024 and M >= 32768))
+            and (tiles <= 128 or wide) and (N % 256 == 0 or wide or cfg.wgrad_ragged)
             and bool(native().gemm_wg_supported(N, K, M)))
 
 
