@@ -41,8 +41,9 @@ class RuntimeConfig:
     # GPT-2 LM heads, [50304, 768 | 1024]: 1..4 token splits, ragged last row panel)
     wgrad_wide: bool = True
     # VCX_WGRAD_RAGGED: outputs whose row count is a multiple of 128 but not 256 (half-empty last row panel;
-    # ResNet-50 stage 2's [128, 256 | 512]) on gemm_wg too; the LM heads take it regardless
-    wgrad_ragged: bool = True
+    # ResNet-50 stage 2's [128, 256 | 512]) on gemm_wg too -- config 3 8849-8871 vs 8918-8960 img/s without
+    # (gpurun_out/c26), so off; the LM heads take the ragged panel regardless
+    wgrad_ragged: bool = False
     gemm_select: bool = False  # VCX_GEMM_SELECT: per-shape layout probe of the forward GEMMs (no in-step gain)
     wgrad_big_split_min_m: int = 16384  # VCX_WGRAD_BIG_SPLIT_MIN_M: rows above which weight grads split over K
     async_wgrad: bool = False  # VCX_ASYNC_WGRAD: weight-grad GEMMs on a side stream (measured slower)
