@@ -71,6 +71,9 @@ class RuntimeConfig:
     # VCX_CONV3X3_WGRAD: weight gradients of the ResNet 3x3 convolutions with Cin, Cout % 128 == 0 on gemm_wg with
     # the patch matrix gathered while staging ("vcx"), or MIOpen's ("lib")
     conv3x3_wgrad: str = "vcx"
+    # VCX_ENGINE_BATCH: chunks a volunteer that already holds several runs through the detector as ONE batch
+    # (1 = one chunk per network launch)
+    engine_batch: int = 2
     resnet_join: bool = True  # VCX_RESNET_JOIN: identity-shortcut gradient added in conv1's dgrad GEMM (GradJoin)
     # VCX_RESNET_PROJ_JOIN: projection shortcuts add their input gradient into the one conv1 left (GradJoin)
     resnet_proj_join: bool = True
@@ -105,6 +108,7 @@ _ENV = {
     "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
     "resnet_bn": ("VCX_RESNET_BN", str),
     "resnet_join": ("VCX_RESNET_JOIN", _bool),
+    "engine_batch": ("VCX_ENGINE_BATCH", int),
     "conv3x3_wgrad": ("VCX_CONV3X3_WGRAD", str),
     "resnet_proj_join": ("VCX_RESNET_PROJ_JOIN", _bool),
     "bn_layer_ws": ("VCX_BN_LAYER_WS", _bool),

@@ -581,27 +581,54 @@ class client:  # noqa: N801 (reference class name)
         overlap k's network (DetectorEngine.submit). Device-resident chunks of the RCCL pair
         plane: k+1's compute is enqueued behind its receive while k's result is posted and sent,
         so receive k+1 ∥ infer k ∥ send k-1 (DetectorEngine.submit_tensor)."""
-        pending = None
+        pending = []
+        batch_max = max(1, config.get().engine_batch)
         while self.continue_procesing:
             try:
-                item = self.work_q.get(timeout=0.002 if pending is not None else 0.2)
+                item = self.work_q.get(timeout=0.002 if pending else 0.2)
             except queue.Empty:
                 item = None
+            nxt = []
             if item is not None:
-                hdr, arr, requester, nums = item
-                dev_res = bool(hdr.get("p2p")) and arr.device.type != "cpu"
-                eng = self._get_engine()
-                with self.hspans.span("wk_submit"):
-                    job = eng.submit_tensor(arr, requester) if dev_res else eng.submit(arr, requester)
-                nxt = (job, hdr, requester, nums, time.perf_counter(), dev_res)
+                items = [item]
+                while len(items) < batch_max:  # chunks already waiting run as one network batch
+                    try:
+                        items.append(self.work_q.get_nowait())
+                    except queue.Empty:
+                        break
+                nxt = self._submit(self._get_engine(), items)
+            if pending and (nxt or self.work_q.empty()):
+                for p in pending:
+                    self._finish(*p)
+                pending = []
+            pending = nxt or pending
+        for p in pending:
+            self._finish(*p)
+
+    def _submit(self, eng, items):
+        """Submit received chunks to the engine: consecutive chunks of one kind (host / device-resident) and
+        frame shape as ONE batch where the engine batches (DetectorEngine.submit_many: the network's last
+        tile waves and extras tail paid once, 1.00 vs 1.16 ms per 100 frames for two chunks). Returns the
+        pending (job, hdr, requester, nums, t0, dev_res) entries in arrival order."""
+        groups = []
+        for it in items:
+            hdr, arr, _req, _nums = it
+            dev_res = bool(hdr.get("p2p")) and arr.device.type != "cpu"
+            if groups and groups[-1][0] == dev_res and tuple(groups[-1][1][-1][1].shape[1:]) == tuple(arr.shape[1:]):
+                groups[-1][1].append(it)
             else:
-                nxt = None
-            if pending is not None and (nxt is not None or self.work_q.empty()):
-                self._finish(*pending)
-                pending = None
-            pending = nxt if nxt is not None else pending
-        if pending is not None:
-            self._finish(*pending)
+                groups.append((dev_res, [it]))
+        out = []
+        for dev_res, its in groups:
+            t0 = time.perf_counter()
+            with self.hspans.span("wk_submit"):
+                if len(its) > 1 and hasattr(eng, "submit_many"):
+                    pairs = [(a, r) for _h, a, r, _n in its]
+                    jobs = eng.submit_tensor_many(pairs) if dev_res else eng.submit_many(pairs)
+                else:
+                    jobs = [eng.submit_tensor(a, r) if dev_res else eng.submit(a, r) for _h, a, r, _n in its]
+            out.extend((job, hdr, req, nums, t0, dev_res) for (hdr, _a, req, nums), job in zip(its, jobs))
+        return out
 
     def _finish(self, job, hdr, requester, nums, t0, dev_res=False):
         if dev_res:  # annotated chunk on the device: held for the pair send to the requester

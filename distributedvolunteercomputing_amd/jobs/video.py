@@ -92,13 +92,14 @@ class _Slot:
 class EngineJob:
     """A chunk in flight on the GPU (``DetectorEngine.submit``); ``result()`` waits for it."""
 
-    def __init__(self, engine, slot, out_shape, counts, out_dev):
+    def __init__(self, engine, slot, out_shape, counts, out_dev, off: int = 0):
         self.engine, self.slot, self.out_shape, self.counts, self.out_dev = engine, slot, out_shape, counts, out_dev
+        self.off = off  # byte offset of this chunk in the slot's pinned output (batched chunks share a slot)
 
     def result(self):
         self.slot.out_done.synchronize()
         n = int(np.prod(self.out_shape))
-        out = self.slot.pin_out[:n].numpy().reshape(self.out_shape)
+        out = self.slot.pin_out[self.off:self.off + n].numpy().reshape(self.out_shape)
         return out, self.counts.cpu().tolist()
 
 
@@ -210,6 +211,86 @@ class DetectorEngine(Engine):
                 ev.record(self.stream)
             x.record_stream(self.stream)
             return _TensorJob(out, ev)
+
+    @torch.no_grad()
+    def submit_many(self, items):
+        """Several host chunks [(frames, requester), ...] of one frame shape as ONE network batch: the
+        per-layer kernels' last tile wave and the latency-bound extras tail are paid once per launch (two
+        chunks: 1.00 vs 1.16 ms per 100 frames, profiles/r5_detector_layers.txt). One pinned slot, one
+        upload, one readback; returns one job per chunk (its slice of the slot's output)."""
+        shapes = [tuple(f.shape) for f, _ in items]
+        if len(items) == 1 or self.stream is None or len({sh[1:] for sh in shapes}) != 1:
+            return [self.submit(f, r) for f, r in items]
+        with self._lock:
+            slot = self._slots[self._next]
+            self._next = (self._next + 1) % len(self._slots)
+            if slot.h2d_done is not None:
+                slot.h2d_done.synchronize()
+            if slot.out_done is not None:
+                slot.out_done.synchronize()
+            arrs = [np.ascontiguousarray(f if isinstance(f, np.ndarray) else f.numpy()) for f, _ in items]
+            pin = slot.buf("pin_in", sum(a.nbytes for a in arrs))
+            off = 0
+            for a in arrs:
+                pin[off:off + a.nbytes].copy_(torch.from_numpy(a).view(-1).view(torch.uint8))
+                off += a.nbytes
+            slot.src_ref = None
+            src = pin.view(sum(sh[0] for sh in shapes), *shapes[0][1:])
+            with torch.cuda.stream(self.copy_stream):
+                x = src.to(self.device, non_blocking=True)
+                slot.h2d_done = torch.cuda.Event()
+                slot.h2d_done.record(self.copy_stream)
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(slot.h2d_done)
+                x.record_stream(self.stream)
+                out, counts = self._compute_many(x, [r for _, r in items], [sh[0] for sh in shapes])
+                po = slot.buf("pin_out", out.numel()).view(out.shape)
+                po.copy_(out, non_blocking=True)
+                slot.out_done = torch.cuda.Event()
+                slot.out_done.record(self.stream)
+            jobs, a = [], 0
+            per = out[0].numel()
+            for sh, c in zip(shapes, counts):
+                jobs.append(EngineJob(self, slot, (sh[0],) + tuple(out.shape[1:]), c, out[a:a + sh[0]], off=a * per))
+                a += sh[0]
+            return jobs
+
+    @torch.no_grad()
+    def submit_tensor_many(self, items):
+        """Device-resident variant of ``submit_many``: the chunks are concatenated on the device (one D2D
+        copy) and run as one batch; one job per chunk (a view of the batched output)."""
+        shapes = [tuple(f.shape) for f, _ in items]
+        if len(items) == 1 or self.stream is None or len({sh[1:] for sh in shapes}) != 1:
+            return [self.submit_tensor(f, r) for f, r in items]
+        with self._lock:
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.stream):
+                x = torch.cat([f.to(self.device) for f, _ in items])
+                out, _ = self._compute_many(x, [r for _, r in items], [sh[0] for sh in shapes])
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+            for f, _ in items:
+                if f.device == self.device:
+                    f.record_stream(self.stream)
+            jobs, a = [], 0
+            for sh in shapes:
+                jobs.append(_TensorJob(out[a:a + sh[0]], ev))
+                a += sh[0]
+            return jobs
+
+    def _compute_many(self, x, requesters, sizes):
+        tr = self.tracer
+        with tr.span("resize"):
+            small = V.resize_width(x, self.width).contiguous()
+        with tr.span("detect"):
+            dets, cnt = self.exec.detect(small)
+        counts, a = [], 0
+        with tr.span("annotate"):
+            for req, n in zip(requesters, sizes):
+                counts.append(V.annotate(small[a:a + n], dets[a:a + n], cnt[a:a + n], req, label=self.label,
+                                         cls_name=self.consider, thresh=self.conf_thresh))
+                a += n
+        return small, counts
 
     def _run(self, frames, requester):  # CPU path / reference
         x = frames if isinstance(frames, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frames))
