@@ -19,5 +19,6 @@ for set in "SQ_WAVES SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_IN
   echo "[pmc] pass $i rc=$rc"
   [ $rc -ne 0 ] && { tail -5 "$OUT/p$i.log"; exit $rc; }
 done
-python3 "$R/scripts/pmc_summary.py" "$OUT" > "$OUT/summary.txt"
+python3 "$R/scripts/pmc_summary.py" "$OUT" > "$OUT/summary.txt" || exit $?
+rm -rf "$OUT"/p1 "$OUT"/p2  # the raw counter CSVs exceed what gpurun copies back; the summary keeps the numbers
 exit 0
