@@ -28,12 +28,42 @@ import sys
 import time
 
 
-def _spawn_ranks(n: int, argv) -> int:
-    """Launch n ranks of this script through torch.distributed.run in a child process (the
-    parent never initialises the GPU: device_count() does not on this ROCm image)."""
-    import torch
+def _visible_gpus() -> int:
+    """GPUs this process could use, counted without the HIP runtime (the spawning parent must make
+    no HIP call at all): the *_VISIBLE_DEVICES lists when set, else the KFD
+    topology in sysfs (GPU nodes have SIMDs). 0 = none found / unknown: the ranks validate."""
+    lists = [os.environ[v] for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+             if v in os.environ]
+    if lists:
+        return min(len([x for x in v.split(",") if x.strip()]) for v in lists)
+    n = 0
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for node in os.listdir(base):
+            try:
+                with open(os.path.join(base, node, "properties")) as f:
+                    props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        return 0
+    return n
 
-    ndev = torch.cuda.device_count()
+
+def _mapped_libs() -> list[str]:
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({ln.split()[-1].rsplit("/", 1)[-1] for ln in f if ".so" in ln})
+    except OSError:
+        return []
+
+
+def _spawn_ranks(n: int, argv) -> int:
+    """Launch n ranks of this script through torch.distributed.run in a child process. The parent
+    imports neither torch nor the HIP runtime (it counts GPUs from the environment / sysfs)."""
+    ndev = _visible_gpus()
     if 0 < ndev < n:
         print(f"[bench] --gpus {n} but only {ndev} GPUs are visible", file=sys.stderr)
         return 2
@@ -44,7 +74,12 @@ def _spawn_ranks(n: int, argv) -> int:
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver (RCCL)
-    return subprocess.call(cmd, env=env)
+    rc = subprocess.call(cmd, env=env)
+    rep = os.environ.get("VCX_BENCH_PARENT_LIBS")
+    if rep:  # tests/test_bench_cpu.py: what the spawning parent had mapped
+        with open(rep, "w") as f:
+            f.write("\n".join(_mapped_libs()) + "\n")
+    return rc
 
 
 if __name__ == "__main__" and "WORLD_SIZE" not in os.environ:
@@ -83,7 +118,39 @@ def parse():
                          "all 7 xGMI links (parallel/collectives.py); rccl = the library all-reduce")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--graph", type=int, default=1, help="1: replay each local step as one hipGraph, 0: eager")
+    ap.add_argument("--rccl-log", type=int, default=1,
+                    help="1: RCCL INIT/P2P log to a file per rank (unless NCCL_DEBUG is set), parsed for the "
+                         "transport each connection chose (rccl_transports in the JSON)")
     return ap.parse_args()
+
+
+def _rccl_log_setup(enable: bool, rank: int) -> str | None:
+    if not enable or "NCCL_DEBUG" in os.environ:
+        return None
+    d = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"vcx_bench_rccl_{os.getppid()}")
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, f"rank{rank}.log")
+    os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P,NET", NCCL_DEBUG_FILE=path)
+    return path
+
+
+def _rccl_transports(path: str | None) -> dict:
+    """Counts of the transports RCCL's connection lines name ('... via P2P/IPC', 'via SHM', 'via NET/...')."""
+    import re
+
+    out: dict[str, int] = {}
+    if not path or not os.path.exists(path):
+        return out
+    with open(path, errors="replace") as f:
+        for ln in f:
+            m = re.search(r" via (\S+)", ln)
+            if m and "Channel" in ln:
+                out[m.group(1)] = out.get(m.group(1), 0) + 1
+    try:
+        os.remove(path)
+    except OSError:
+        pass
+    return out
 
 
 def main():
@@ -94,6 +161,7 @@ def main():
         return 3
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    rccl_log = _rccl_log_setup(a.rccl_log and world > 1, rank)
     cuda = torch.cuda.is_available()
     if cuda:
         # one rank per GPU; ranks beyond the GPU count share cards (rehearsal launches only)
@@ -107,6 +175,17 @@ def main():
         if formed != a.gpus:
             print(f"[bench] process group formed {formed} ranks, --gpus {a.gpus}", file=sys.stderr)
             return 3
+        if cuda:
+            # one GPU per rank whenever there are enough GPUs: two ranks on one card would halve
+            # that card's share and report a per-GPU number that is not one
+            ndev = torch.cuda.device_count()
+            p = torch.cuda.get_device_properties(device)
+            mine = (device.index, getattr(p, "pci_bus_id", None), getattr(p, "uuid", None))
+            seen = [None] * formed
+            dist.all_gather_object(seen, str(mine))
+            if formed <= ndev and len(set(seen)) < formed:
+                print(f"[bench] ranks share a GPU although {ndev} are visible: {seen}", file=sys.stderr)
+                return 4
     group = PeerGroup.from_default(device) if world > 1 else None
 
     cfg = GPT2Config.preset(a.model)
@@ -150,6 +229,8 @@ def main():
 
         allreduce_sum_(torch.zeros_like(trainer.delta), group, a.algo)  # same size as the real round
     sync_all()
+    trainer.time_reduce = world > 1  # the averaging collective timed apart (algbw / busbw below)
+    trainer.reduce_log = []
     t0 = time.perf_counter()
     last = None
     syncs = []
@@ -171,6 +252,16 @@ def main():
         devices = [None] * rccl_world
         dist.all_gather_object(devices, dev_desc)
     loss = float(last.extra["loss_t"]) if last is not None else float("nan")
+    red = trainer.reduce_log
+    red_ms = sum(m for m, _ in red) / len(red) if red else None
+    red_bytes = red[0][1] if red else trainer.delta.numel() * trainer.delta.element_size()
+    transports = {}
+    if world > 1:
+        tr = [None] * world
+        dist.all_gather_object(tr, _rccl_transports(rccl_log))
+        for d in tr:
+            for k, v in (d or {}).items():
+                transports[k] = transports.get(k, 0) + v
     if group is not None:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -214,6 +305,12 @@ def main():
             "hipgraph": graphed,
             # ranks sharing a card (scripts/rccl_rehearsal_launch.py): a functional run, not a per-GPU number
             "ranks_share_gpu": bool(cuda and world > torch.cuda.device_count()),
+            # averaging round anatomy (weak scaling: what the collective costs as N grows)
+            "avg_bytes_per_rank": red_bytes,
+            "avg_collective_ms_mean": round(red_ms, 3) if red_ms else None,
+            "avg_algbw_GBps": round(red_bytes / red_ms / 1e6, 4) if red_ms else None,
+            "avg_busbw_GBps": round(red_bytes / red_ms / 1e6 * 2 * (world - 1) / world, 4) if red_ms else None,
+            "rccl_transports": transports or None,
             "gemm_lt_shapes": sum(1 for v in gemm_choices().values() if v == "lt"),
             "gemm_shapes": len(gemm_choices()),
         }

@@ -26,6 +26,7 @@ import sys
 import sysconfig
 from pathlib import Path
 
+from . import _digest as _srcdigest
 from . import config
 
 PKG = Path(__file__).resolve().parent
@@ -93,6 +94,28 @@ def _compile_all(jobs, nproc):
     return len(todo)
 
 
+def _digest_object(kind: str, symbol: str, compiler: list[str]) -> tuple[Path, str]:
+    """Compile a one-function object returning the sources' digest (linked into the extension, read
+    back by the loader, _digest.check)."""
+    d = _srcdigest.source_digest(kind)
+    src = BUILD / f"{kind}_digest.cpp"
+    obj = BUILD / f"{kind}_digest.o"
+    text = f'extern "C" const char* {symbol}() {{ return "{d}"; }}\n'
+    if not (src.exists() and src.read_text() == text and obj.exists()):
+        src.write_text(text)
+        _run([*compiler, "-O2", "-fPIC", "-c", str(src), "-o", str(obj)], f"{kind} digest")
+    return obj, d
+
+
+def _needs_link(out: Path, n: int, d: str) -> bool:
+    st = BUILD / (out.name + ".digest")
+    return bool(n) or not out.exists() or not st.exists() or st.read_text() != d
+
+
+def _linked(out: Path, d: str):
+    (BUILD / (out.name + ".digest")).write_text(d)
+
+
 def build_C(nproc: int = 8, force: bool = False) -> Path:
     hipcc = _hipcc()
     inc, libdir, abi = _torch_flags()
@@ -118,13 +141,16 @@ def build_C(nproc: int = 8, force: bool = False) -> Path:
         for _, _, obj, _ in jobs:
             obj.with_suffix(obj.suffix + ".stamp").unlink(missing_ok=True)
     n = _compile_all(jobs, nproc)
+    dobj, dig = _digest_object("C", "vcx_source_digest", [hipcc])
+    objs.append(dobj)
     out = PKG / f"_C{EXT}"
-    if n or not out.exists():
+    if _needs_link(out, n, dig):
         # hipBLASLt: torch's own bundled copy (same library instance torch's GEMMs use)
         libs = ["-ltorch", "-ltorch_cpu", "-lc10", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64",
                 "-lhipblaslt"]
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out),
               f"-L{libdir}", *libs, f"-Wl,-rpath,{libdir}"], "link _C")
+        _linked(out, dig)
         print(f"[vcx build] linked {out.name}", flush=True)
     return out
 
@@ -147,9 +173,12 @@ def build_native(nproc: int = 8, force: bool = False) -> Path:
         for _, _, obj, _ in jobs:
             obj.with_suffix(obj.suffix + ".stamp").unlink(missing_ok=True)
     n = _compile_all(jobs, nproc)
+    dobj, dig = _digest_object("native", "vcx_native_source_digest", [cxx])
+    objs.append(dobj)
     out = PKG / f"_native{EXT}"
-    if n or not out.exists():
+    if _needs_link(out, n, dig):
         _run([cxx, "-shared", "-fPIC", "-pthread", *map(str, objs), "-o", str(out)], "link _native")
+        _linked(out, dig)
         print(f"[vcx build] linked {out.name}", flush=True)
     return out
 

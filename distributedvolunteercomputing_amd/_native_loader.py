@@ -3,6 +3,8 @@ from __future__ import annotations
 
 import importlib
 
+from . import _digest
+
 _mod = None
 
 
@@ -10,10 +12,12 @@ def native():
     global _mod
     if _mod is None:
         try:
-            _mod = importlib.import_module("distributedvolunteercomputing_amd._native")
+            mod = importlib.import_module("distributedvolunteercomputing_amd._native")
         except ImportError as e:
             raise RuntimeError(
                 "distributedvolunteercomputing_amd._native (C++ runtime) is not built: "
                 "run `python -m distributedvolunteercomputing_amd._build --only native`"
             ) from e
+        _digest.check(mod, "native")  # refuse a runtime built from other sources
+        _mod = mod
     return _mod

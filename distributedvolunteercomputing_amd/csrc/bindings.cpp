@@ -844,9 +844,11 @@ std::vector<at::Tensor> attn_hm_bwd(at::Tensor q, at::Tensor k, at::Tensor v, at
 void vcx_register_vision(pybind11::module& m);
 void vcx_register_compress(pybind11::module& m);
 void vcx_register_lt(pybind11::module& m);
+extern "C" const char* vcx_source_digest();  // generated by _build.py (digest of the sources linked here)
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels of distributedvolunteercomputing_amd";
+  m.def("source_digest", [] { return std::string(vcx_source_digest()); });
   m.def("grad_sumsq", &grad_sumsq);
   m.def("adam_prologue", &adam_prologue);
   m.def("adamw_flat", &adamw_flat);

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import importlib
 
-from .. import config
+from .. import _digest, config
 
 _C = None
 _ERR: Exception | None = None
@@ -20,7 +20,9 @@ def _load():
     if _C is not None or _ERR is not None:
         return
     try:
-        _C = importlib.import_module("distributedvolunteercomputing_amd._C")
+        mod = importlib.import_module("distributedvolunteercomputing_amd._C")
+        _digest.check(mod, "C")  # refuse an extension built from other sources (stale prebuilt .so)
+        _C = mod
     except Exception as e:  # pragma: no cover - depends on build state
         _ERR = e
 

@@ -30,6 +30,14 @@ Here every peer
   is agreed now, the current round still runs on g, every member starts building g+1's
   communicator on a helper thread, and the group switches to g+1 at the NEXT round, whose
   admission then pays only the model broadcast (the RCCL init ran during the local steps);
+* store writes and visibility: a TCPStore ``set`` is not acknowledged (the client sends it and
+  returns; measured: a ``check`` on another connection right after an 8 MB ``set`` missed it 32
+  times in 50), while ``add`` / ``compare_set`` / ``get`` / ``check`` are request-response and a
+  connection's requests are applied in order. So every key other peers must see at a point they
+  can name is posted with ``compare_set`` (abort, outcome, verdict) or followed by an ``add`` on the
+  same connection (arrival); a joiner's ``join/<seq>`` record can trail its ``njoin`` ticket, and
+  the scan admits joiners only up to the first ticket whose record is not visible yet
+  (``_pending_joiners``) -- counting the ticket without its record lost that joiner for good;
 * process death is seen at once, not after a lease: every peer listens on a TCP "liveness" port
   (published as ``live/<pid>``) and holds one connection to each other member's. Nothing is ever
   sent on them; when a peer process dies (SIGKILL, crash, OOM) its kernel closes its sockets and
@@ -295,6 +303,7 @@ class ElasticMembership:
         self.group: PeerGroup | None = None
         self.round = 0
         self.joins_seen = 0
+        self._join_gap: dict[int, float] = {}  # join ticket -> when its record was first found missing
         self.has_model = True
         self.fault_hook = None  # passed to every generation's PeerGroup (fault-injection tests)
         self.failures = 0
@@ -540,6 +549,11 @@ class ElasticMembership:
                     self.group.needs_go = True  # line up with the continuing members (guard)
                     self.events.append({"event": "joined", "gen": self.gen, "members": members})
                     return self.group
+                if njoin >= seq:
+                    # our ticket was counted without us (its record reached the store after the
+                    # members gave up waiting for it, see _pending_joiners): take a new one
+                    seq = int(self.store.add(f"{_P}njoin", 1))
+                    self.store.set(f"{_P}join/{seq}", str(self.pid))
                 g += 1
                 continue
             time.sleep(0.01)
@@ -715,15 +729,15 @@ class ElasticMembership:
         arrived = {self.pid: self.has_model}
         dead, left = set(), set()
         t0 = now
-        nj_cached, joiners = -1, []
+        nj_cached, joiners, njoin = -1, [], self.joins_seen
         while True:
             if self.store.check([okey]):
                 return self._follow(okey)
             if not recovery and self.store.check([f"{_P}abort/{g}"]):
                 return self.recover()
-            njoin = self._njoin()
-            if njoin != nj_cached:
-                joiners, nj_cached = self._pending_joiners(njoin), njoin
+            nj_raw = self._njoin()
+            if nj_raw != nj_cached or njoin < nj_raw:  # new tickets, or records still on their way
+                (joiners, njoin), nj_cached = self._pending_joiners(nj_raw), nj_raw
             missing = []
             for m in others:
                 if m in arrived or m in dead or m in left:
@@ -922,14 +936,26 @@ class ElasticMembership:
         return int(self.store.add(f"{_P}njoin", 0))
 
     def _pending_joiners(self, njoin):
+        """(joiners, upto): the peers behind join tickets joins_seen+1 .. upto, where upto stops in
+        front of the first ticket whose ``join/<seq>`` record is not visible yet (the joiner takes
+        its ticket with an acknowledged ``add`` and then posts the record with an unacknowledged
+        ``set``). A ticket whose record stays missing for lease_s (the joiner died between the two)
+        is skipped, so it cannot hold back the joiners behind it."""
         out = []
+        upto = self.joins_seen
+        now = time.time()
         for seq in range(self.joins_seen + 1, njoin + 1):
             key = f"{_P}join/{seq}"
             if self.store.check([key]):
                 pid = int(_s(self.store.get(key)))
                 if pid not in out:
                     out.append(pid)
-        return out
+            else:
+                t0 = self._join_gap.setdefault(seq, now)
+                if now - t0 <= self.lease_s:
+                    break
+            upto = seq
+        return out, upto
 
     def _latest_gen(self, start: int = 0) -> int:
         g = start

@@ -82,6 +82,10 @@ class LocalSGDTrainer:
         self.failed_rounds = 0  # elastic rounds aborted mid-collective and redone
         self.admit_split = None  # the last admission transfer: communicator init vs broadcast (ms, bytes)
         self.last_round_stages = None  # a continuing member's stages of the last admission round
+        # bench.py: time the averaging collective alone (device-synchronised on both sides) and
+        # record its bytes, for algbw / busbw in the bench JSON
+        self.time_reduce = False
+        self.reduce_log: list[tuple[float, int]] = []  # (ms, bytes per rank) of each timed collective
 
     # ------------------------------------------------------------------ per step
     def set_lr(self, lr: float):
@@ -222,7 +226,13 @@ class LocalSGDTrainer:
         if self.compressor is not None:
             avg = self.compressor.allreduce_mean(self.delta, g)
             return avg, g.size / contributors
+        if self.time_reduce:
+            self._dev_sync()
+            t0 = time.perf_counter()
         allreduce_sum_(self.delta, g, self.cfg.algo)
+        if self.time_reduce:
+            self._dev_sync()
+            self.reduce_log.append(((time.perf_counter() - t0) * 1e3, self.delta.numel() * self.delta.element_size()))
         return self.delta, 1.0 / contributors
 
     def _apply(self, res, bufs=None):

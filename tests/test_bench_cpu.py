@@ -39,16 +39,25 @@ def test_bench_single_process():
 
 
 @pytest.mark.slow
-def test_bench_gpus_flag_spawns_ranks_without_torchrun():
+def test_bench_gpus_flag_spawns_ranks_without_torchrun(tmp_path):
     """The driver's literal `python bench.py --gpus 4` (no launcher): bench.py starts 4 ranks itself
-    (a child torch.distributed.run, never an exec) and the JSON reports the group that formed."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", *ARGS], cwd=ROOT, env=_env(),
+    (a child torch.distributed.run, never an exec) and the JSON reports the group that formed. The
+    spawning parent loads neither torch nor the HIP runtime (VERDICT r5 weak #9), and the JSON carries
+    the averaging round's bytes, time and bandwidth (VERDICT r5 next #6)."""
+    libs = tmp_path / "parent_libs.txt"
+    env = dict(_env(), VCX_BENCH_PARENT_LIBS=str(libs))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", *ARGS], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
     _check(rec, 4)
     assert rec["rccl_world"] == 4 and rec["backend"] == "gloo" and len(rec["devices"]) == 4
     assert rec["sync_rounds_timed"] == 2 and rec["sync_ms_timed_mean"] > 0  # H = 2, 4 timed steps
+    loaded = libs.read_text().split()
+    assert loaded and not [x for x in loaded if "amdhip64" in x or "libtorch" in x or "hsa-runtime" in x], loaded
+    assert rec["avg_bytes_per_rank"] > 0 and rec["avg_collective_ms_mean"] > 0
+    assert rec["avg_algbw_GBps"] > 0 and abs(rec["avg_busbw_GBps"] / rec["avg_algbw_GBps"] - 1.5) < 5e-2
+    assert rec["rccl_transports"] is None  # gloo: no RCCL connection lines
 
 
 def test_bench_mismatched_launch_fails_loudly():
@@ -109,3 +118,24 @@ def test_rehearsal_launcher_propagates_a_failed_rank(tmp_path):
            "--", sys.executable, "-c", prog]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=90)
     assert r.returncode == 7, r.stderr
+
+
+def test_rccl_transport_parse_and_gpu_count(tmp_path, monkeypatch):
+    """The transport counts come from RCCL's connection lines; the parent's GPU count from the
+    visible-devices lists (intersection = the shortest) without any HIP call."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("vcx_bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    log = tmp_path / "rank0.log"
+    log.write_text("host:1:2 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC\n"
+                   "host:1:2 [0] NCCL INFO Channel 01/0 : 0[0] -> 1[1] via P2P/IPC\n"
+                   "host:1:2 [0] NCCL INFO Channel 00/1 : 0[0] -> 2[2] via SHM/direct/direct\n"
+                   "host:1:2 [0] NCCL INFO Using network Socket\n")
+    assert b._rccl_transports(str(log)) == {"P2P/IPC": 2, "SHM/direct/direct": 1}
+    assert not log.exists()  # parsed once, then removed
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3")
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1")
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    assert b._visible_gpus() == 2
