@@ -152,6 +152,9 @@ class client:  # noqa: N801 (reference class name)
         self._pins: dict = {}  # pinned staging of the requester's pre-resize (by role)
         # memory-mapped sources page-locked in place (hipHostRegister): id -> (array, base address)
         self._registered: dict = {}
+        # guards _registered and the enqueue of copies out of a registered mapping: a new job's
+        # requester thread unregisters while the previous job's send thread may still be using it
+        self._reg_lock = threading.Lock()
         self._in_done = [None, None]  # per pinned input buffer: the upload that last read it
         self._in_ring = 0
         self._rs_stream = None  # the requester's resize stream (its own: not the workers' engines')
@@ -221,19 +224,26 @@ class client:  # noqa: N801 (reference class name)
         with self._p2p_lock:  # chunks of an earlier job that never came back are not needed any more
             self._outgoing.clear()
         src = open_source(path)
-        self._register_source(src)
         time.sleep(0.0 if path != "live" else 0.5)  # camera warm-up in the reference: 2 s
+        # the job clock starts before the source is page-locked (reference: before the first read,
+        # worker.py:105-107): that setup grows with the source and is part of the job
+        self.start_time = time.time()
+        self._register_source(src)
         out_path = self.path_out
 
         def done(sink):
             dt = sink.t_done - self.start_time
+            if sink.errors:
+                # the output file is incomplete: not a completed job (no job time for it)
+                self.metrics.incr("jobs_failed")
+                print(f"job failed: {sink.errors} output write error(s); {out_path} is incomplete", flush=True)
+                return
             self.job_times.append(dt)
             self.metrics.observe("job_s", dt)
             print(f"final frame time taken for the job = {dt}", flush=True)
 
         sink_dev = self.resize_device if config.get().sink_gpu else None
         self.sink = OrderedSink(lambda w, h: open_sink(out_path, w, h, 30, device=sink_dev), on_done=done)
-        self.start_time = time.time()
         n = 0
         C = self.number_of_frames_in_chunk
         while self.continue_requesting:
@@ -303,28 +313,32 @@ class client:  # noqa: N801 (reference class name)
             self.metrics.incr("source_register_failed")
             self.log(f"hipHostRegister of the source mapping failed ({err}): chunks are copied")
             return
-        self._registered[id(a)] = (a, base)
+        with self._reg_lock:
+            self._registered[id(a)] = (a, base)
         self.metrics.observe("source_register_ms", (time.perf_counter() - t0) * 1e3)
 
     def _unregister_sources(self):
-        if not self._registered:
-            return
-        from torch._C import _cudart
+        """Under the registration lock: no copy out of a mapping can be enqueued between the stream
+        synchronisation and the unregister (a DMA from unregistered memory can fault the GPU)."""
+        with self._reg_lock:
+            if not self._registered:
+                return
+            from torch._C import _cudart
 
-        if self._rs_stream is not None:
-            self._rs_stream.synchronize()
-        for a, base in self._registered.values():
-            _cudart.cudaHostUnregister(base)
-        self._registered.clear()
+            if self._rs_stream is not None:
+                self._rs_stream.synchronize()
+            for a, base in list(self._registered.values()):
+                _cudart.cudaHostUnregister(base)
+            self._registered.clear()
 
     def _registered_block(self, frames):
-        """True when `frames` is a view of a page-locked source mapping."""
+        """True when `frames` is a view of a page-locked source mapping (call under _reg_lock)."""
         if not self._registered or not isinstance(frames, np.ndarray):
             return False
         b = frames
         while isinstance(b.base, np.ndarray):
             b = b.base
-        return any(b is a for a, _ in self._registered.values()) and frames.flags.c_contiguous
+        return any(b is a for a, _ in list(self._registered.values())) and frames.flags.c_contiguous
 
     # ------------------------------------------------------------------ send (chunk packing)
     def send_image_thread(self):
@@ -419,11 +433,13 @@ class client:  # noqa: N801 (reference class name)
         dev = self.resize_device
         if self._rs_stream is None:
             self._rs_stream = torch.cuda.Stream(dev)
-        if self._registered_block(frames):  # page-locked mapping: DMA straight from the source
-            with torch.cuda.stream(self._rs_stream):
-                x = torch.empty(frames.shape, dtype=torch.uint8, device=dev)
-                x.copy_(_host_tensor(frames), non_blocking=True)
-        else:
+        x = None
+        with self._reg_lock:  # the mapping stays registered until this copy is enqueued
+            if self._registered_block(frames):  # page-locked mapping: DMA straight from the source
+                with torch.cuda.stream(self._rs_stream):
+                    x = torch.empty(frames.shape, dtype=torch.uint8, device=dev)
+                    x.copy_(_host_tensor(frames), non_blocking=True)
+        if x is None:
             # two pinned input buffers: this chunk's copy overlaps the previous chunk's upload + resize
             i = self._in_ring = (self._in_ring + 1) % 2
             if self._in_done[i] is not None:

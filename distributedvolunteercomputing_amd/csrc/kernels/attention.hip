@@ -192,6 +192,203 @@ attn_fwd_d64_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
 #undef sV_
 }
 
+// ---------------------------------------------------------------------------- forward, 3-slot ring
+// The same tile algorithm with the K/V staging of gemm_wg: a 3-slot LDS ring
+// (3 x 16 KB per block; three blocks per CU at 3 waves per SIMD = 144 KB), tile kt + 2 issued while
+// tile kt computes, LDS-DMA as inline asm (invisible to hipcc's waitcnt pass, so it inserts no
+// vmcnt(0) drain of its own), a COUNTED s_waitcnt that leaves the next tile's 4 pieces in flight
+// across the raw s_barrier (the two-buffer kernel above drains every load at every tile: one
+// vmcnt(0) per K/V tile in its ISA).
+namespace ring {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// buffer resource over [base, base + bytes): wave-uniform (SGPRs), 32-bit per-lane offsets
+__device__ __forceinline__ u32x4 desc(const void* base, unsigned bytes) {
+  const uint64_t a = (uint64_t)base;
+  return u32x4{(unsigned)a, (unsigned)(a >> 32) & 0xffffu, bytes, 0x00020000u};
+}
+
+// one 1-KB LDS-DMA piece (16 B per lane to lds + 16 lane); M0 = LDS byte address; `s_nop 0`: M0 -> DMA hazard
+__device__ __forceinline__ void dma16(u32x4 d, int voff, const bf16* lds) {
+  const unsigned m0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) bf16*)lds;
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(d), "{m0}"(m0) : "memory");
+}
+
+// s_waitcnt vmcnt(N) lgkmcnt(0)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 16, "vmcnt field");
+  __builtin_amdgcn_s_waitcnt(0x0070 | N);
+}
+__device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+constexpr int SLOT = 2 * A_BK * AD;  // elements: K tile then V tile (16 KB)
+
+}  // namespace ring
+
+template <int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
+attn_fwd_d64_ring_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int B, int T,
+                         int H, float scale_log2, int staged_epi) {
+  using namespace ring;
+  __shared__ __attribute__((aligned(16))) bf16 sm[3 * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, h2 = lane >> 5, col = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqt = (T + A_BQ - 1) / A_BQ;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = nqt - 1 - (lb % nqt);  // heaviest (last) query tiles first
+  const int bh = lb / nqt;
+  const int b = bh / H, hh = bh % H;
+  const int64_t tok = 3ll * H * AD;
+  const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
+  const int q0 = qt * A_BQ;
+  const int qw = q0 + w * 32;
+  const int q = qw + col;
+  const int qc = min(q, T - 1);
+  sx8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *(const sx8*)(base + (int64_t)qc * tok + 16 * s + 8 * h2);
+  // the Q fragments must not share a vmcnt count with the asm DMA below (hipcc cannot count those)
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  f32x16 o0 = {}, o1 = {};
+  float m = -INFINITY, l = 0.f;
+  const int kend = min(T, q0 + A_BQ);
+  const int nkt = (kend + A_BK - 1) / A_BK;
+  // K and V of this (batch, head): rows of `tok` elements; the resource ends after row T - 1's 64 columns
+  const unsigned kv_bytes = (unsigned)(((int64_t)(T - 1) * tok + AD) * 2);
+  const u32x4 rK = desc(base + H * AD, kv_bytes), rV = desc(base + 2 * H * AD, kv_bytes);
+  // this lane's two pieces (2w, 2w + 1) of a 64 x 64 tile: row r_i, swizzled source chunk ch_i (swz layout)
+  int r_[2], c_[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = (w * 2 + i) * 64 + lane, r = p >> 3, k = (r >> 1) & 7;
+    r_[i] = r;
+    c_[i] = ((p & 7) ^ (((k & 1) << 2) | (k >> 1))) * 8;
+  }
+  auto issue = [&](int kt, int slot) {  // 4 DMA ops per wave: K pieces 2w, 2w+1, then V pieces
+    bf16* sl = sm + slot * SLOT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int voff = (int)(((int64_t)min(kt * A_BK + r_[i], T - 1) * tok + c_[i]) * 2);
+      dma16(rK, voff, sl + (w * 2 + i) * 512);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int voff = (int)(((int64_t)min(kt * A_BK + r_[i], T - 1) * tok + c_[i]) * 2);
+      dma16(rV, voff, sl + A_BK * AD + (w * 2 + i) * 512);
+    }
+  };
+  auto tile = [&](int kt, auto slot_c, auto mask_c) {
+    constexpr int slot = decltype(slot_c)::value;
+    constexpr bool MASK = decltype(mask_c)::value;
+    const bf16* sK = sm + slot * SLOT;
+    const bf16* sV = sK + A_BK * AD;
+    const int kb = kt * A_BK;
+    if (MASK && kb > qw + 31) return;
+    f32x16 s0 = {}, s1 = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s0 = mfma32(row_frag_swz(sK, col, s, h2), qf[s], s0);
+      s1 = mfma32(row_frag_swz(sK, 32 + col, s, h2), qf[s], s1);
+    }
+    mfma_read_fence(s0, s1);
+    if (MASK) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
+        s0[r] = key > q ? -INFINITY : s0[r];
+        s1[r] = key + 32 > q ? -INFINITY : s1[r];
+      }
+    }
+    float mx0 = max3(s0[0], s0[1], s1[0]), mx1 = max3(s1[1], s0[2], s1[2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) {
+      mx0 = max3(mx0, s0[r], s1[r]);
+      mx1 = max3(mx1, s0[r + 1], s1[r + 1]);
+    }
+    const float mx = xhalf_max(max3(mx0, mx1, fmaxf(s0[15], s1[15]))) * scale_log2;
+    if (!__all(mx - m <= 8.f)) {  // deferred rescale (T13), threshold 2^8
+      const float mnew = fmaxf(m, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      l *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        o0[r] *= alpha;
+        o1[r] *= alpha;
+      }
+      m = mnew;
+    }
+    const float mneg = -m;
+    float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p0 = __builtin_amdgcn_exp2f(fmaf(s0[r], scale_log2, mneg));
+      const float p1 = __builtin_amdgcn_exp2f(fmaf(s1[r], scale_log2, mneg));
+      s0[r] = p0;
+      s1[r] = p1;
+      ps0 += p0;
+      ps1 += p1;
+    }
+    l += xhalf_sum(ps0 + ps1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const f32x16& sp = (s < 2) ? s0 : s1;
+      sx8 pb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[j] = bf16_bits(sp[8 * (s & 1) + j]);
+      o0 = mfma32(vt_frag_swz(sV, (s >> 1) * 32, 0, s & 1, lane), pb, o0);
+      o1 = mfma32(vt_frag_swz(sV, (s >> 1) * 32, 1, s & 1, lane), pb, o1);
+    }
+  };
+  // step kt: tile kt is visible in slot kt % 3, tile kt + 1 in flight; issue kt + 2 into the slot
+  // tile kt - 1 left (every wave passed the barrier behind it), compute kt, then wait for this
+  // wave's pieces of kt + 1 (leaving kt + 2's four in flight) and make everyone's visible
+  auto step = [&](int kt, auto slot_c, auto mask_c) {
+    constexpr int slot = decltype(slot_c)::value;
+    const bool more = kt + 2 < nkt;
+    if (more) issue(kt + 2, (slot + 2) % 3);
+    tile(kt, slot_c, mask_c);
+    if (more)
+      wait_vm<4>();
+    else
+      wait_vm<0>();
+    barrier();
+  };
+  issue(0, 0);
+  if (nkt > 1) issue(1, 1);
+  if (nkt > 1)
+    wait_vm<4>();
+  else
+    wait_vm<0>();
+  barrier();
+  using I2 = std::integral_constant<int, 2>;
+  using Fm = std::false_type;
+  using Tm = std::true_type;
+  const int kdiag = q0 / A_BK;
+  int kt = 0;
+  for (; kt + 2 < kdiag; kt += 3) {
+    step(kt, I0{}, Fm{});
+    step(kt + 1, I1{}, Fm{});
+    step(kt + 2, I2{}, Fm{});
+  }
+  if (kt < kdiag) step(kt++, I0{}, Fm{});  // kt % 3 == 0 here
+  if (kt < kdiag) step(kt++, I1{}, Fm{});
+  for (; kt < nkt; ++kt) {  // the (at most two) diagonal tiles
+    const int sl = kt % 3;
+    if (sl == 0)
+      step(kt, I0{}, Tm{});
+    else if (sl == 1)
+      step(kt, I1{}, Tm{});
+    else
+      step(kt, I2{}, Tm{});
+  }
+  const float inv = 1.f / l;
+  store_acc_tile(o0, o1, inv, out + ((int64_t)b * T + qw) * H * AD + hh * AD, (int64_t)H * AD, T - qw,
+                 sm + w * 32 * AD, staged_epi, lane);
+  if (q < T && h2 == 0) lse[((int64_t)b * H + hh) * T + q] = m + __log2f(l);
+}
+
 // ============================================================================ backward
 // dQ (query-parallel; same tiling as the forward): per 32-key sub-tile
 //   S^T = K Q^T, P^T = exp2(S^T c - lse), dP^T = V dO^T, dS^T = P^T (dP^T - delta),
@@ -572,7 +769,7 @@ static int g_stage_epi = 1;
 
 void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma, int stage_epi) {
   if (fwd_wpe == 2 || fwd_wpe == 3) g_fwd_wpe = fwd_wpe;
-  if (fwd_dma == 0 || fwd_dma == 1) g_fwd_dma = fwd_dma;
+  if (fwd_dma >= 0 && fwd_dma <= 2) g_fwd_dma = fwd_dma;  // 2: the 3-slot ring (attn_fwd_d64_ring_kernel)
   if (bwd_dma >= 0 && bwd_dma <= 3) g_bwd_dma = bwd_dma;
   if (stage_epi == 0 || stage_epi == 1) g_stage_epi = stage_epi;
 }
@@ -608,7 +805,14 @@ void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int 
 #define VCX_FWD(W, D)                                                                                      \
   hipLaunchKernelGGL((attn_fwd_d64_kernel<W, D>), g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H, \
                      scale * LOG2E, g_stage_epi)
-  if (g_fwd_dma) {
+  if (g_fwd_dma == 2) {
+    if (g_fwd_wpe == 2)
+      hipLaunchKernelGGL((attn_fwd_d64_ring_kernel<2>), g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H,
+                         scale * LOG2E, g_stage_epi);
+    else
+      hipLaunchKernelGGL((attn_fwd_d64_ring_kernel<3>), g, dim3(256), 0, s, (const bf16*)qkv, (bf16*)out, lse, B, T, H,
+                         scale * LOG2E, g_stage_epi);
+  } else if (g_fwd_dma) {
     if (g_fwd_wpe == 2) VCX_FWD(2, true); else VCX_FWD(3, true);
   } else {
     if (g_fwd_wpe == 2) VCX_FWD(2, false); else VCX_FWD(3, false);

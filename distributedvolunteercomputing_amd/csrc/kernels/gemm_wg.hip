@@ -333,8 +333,9 @@ __global__ void __launch_bounds__(NT, 1)
     run(F{});
 
   // ---- fp32 partial: acc[i][j] = C[m][n .. n + 3], m = row block i + (lane & 15), n = column block j.
-  // Ragged M (M % 256 = 128: the LM head's 50304 rows): the last row panel's A columns past M read the next
-  // token row's values (or 0 past the resource), and their output rows are not stored
+  // Ragged M (M % 256 = 128: the LM head's 50304 rows): the last row panel's lanes for columns past M
+  // re-read the panel's last valid chunk (the clamp of cha_e / cha_o above), and those output rows are
+  // not stored
   const int mrow = m0 + wm * 128 + (lane & 15);
   const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
   float* cp = Cpart + (int64_t)split * M * N;

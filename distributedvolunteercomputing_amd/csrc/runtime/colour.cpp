@@ -2,6 +2,7 @@
 
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/statvfs.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -158,12 +159,25 @@ static void y4m_record(const uint8_t* src, uint8_t* r, int64_t n) {
   }
 }
 
+// The mapped write path grows the file with ftruncate (a sparse range) and fills it through a shared
+// mapping: if the filesystem cannot back those pages (full disk / tmpfs), the page fault raises SIGBUS
+// and kills the process, where a write() would have failed with ENOSPC. So the mapping is
+// used only while the filesystem has the bytes the range still needs, with a 64 MB margin for other
+// writers; otherwise the positional write path runs and reports the error as an exception.
+static bool room_for(int fd, const struct stat& st, int64_t end) {
+  const int64_t need = end - std::min<int64_t>(end, (int64_t)st.st_blocks * 512);
+  if (need <= 0) return true;
+  struct statvfs vs{};
+  if (::fstatvfs(fd, &vs) != 0) return false;
+  return (int64_t)vs.f_bavail * (int64_t)vs.f_frsize > need + (int64_t(64) << 20);
+}
+
 // `n` bytes at `off` of fd: a regular file grown and the range mapped and filled on up to 8 threads
 // (the Y4M records converted on the GPU arrive as bytes), else one positional write
 int64_t write_bytes(int fd, int64_t off, const uint8_t* src, int64_t n) {
   if (n <= 0) return 0;
   struct stat st{};
-  if (::fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
+  if (::fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && room_for(fd, st, off + n)) {
     if (st.st_size < off + n && ::ftruncate(fd, (off_t)(off + n)) != 0)
       throw std::runtime_error(std::string("write_bytes: ftruncate: ") + std::strerror(errno));
     const int64_t pg = ::sysconf(_SC_PAGESIZE), base = off - off % pg, len = off + n - base;
@@ -195,7 +209,7 @@ int64_t write_frames(int fd, int64_t off, const uint8_t* bgr, int64_t k, int64_t
   const int64_t n = w * h, fb = 3 * n, rec = y4m ? fb + 6 : fb, total = k * rec;
   if (k <= 0) return 0;
   struct stat st{};
-  if (::fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
+  if (::fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && room_for(fd, st, off + total)) {
     if (st.st_size < off + total && ::ftruncate(fd, (off_t)(off + total)) != 0)
       throw std::runtime_error(std::string("write_frames: ftruncate: ") + std::strerror(errno));
     const int64_t pg = ::sysconf(_SC_PAGESIZE), base = off - off % pg, len = off + total - base;

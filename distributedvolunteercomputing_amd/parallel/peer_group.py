@@ -337,11 +337,32 @@ class PeerGroup:
             return fn(pg)
         except Exception as e:  # noqa: BLE001
             w = self.watch
-            if w is None:
-                raise
+            if w is None or not self._transport_failure(e):
+                raise  # a caller bug (shape / split mismatch ...) stays a visible crash
             w.declare_abort(f"{op} issue failed on peer {w.pid}: {type(e).__name__}: {str(e)[:120]}")
             self.abort()
             raise PeerFailure(f"gen {self.generation}: {op} issue failed: {e}") from e
+
+    _TRANSPORT_WORDS = ("abort", "torn down", "connection", "timed out", "timeout", "closed", "reset by peer",
+                        "broken pipe", "unhandled system error", "remote process exited")
+
+    def _transport_failure(self, e: Exception) -> bool:
+        """Did the issue fail because of the communicator or a peer (-> the round's PeerFailure), rather
+        than because of the call itself? Programming errors (ValueError, TypeError, IndexError, ...)
+        and RuntimeErrors that name no transport condition are re-raised unchanged."""
+        w = self.watch
+        if self.aborted or self.pg is None or (w is not None and w.tripped()):
+            return True
+        for name in ("DistBackendError", "DistNetworkError", "DistStoreError"):
+            cls = getattr(dist, name, None)
+            if cls is not None and isinstance(e, cls):
+                return True
+        if isinstance(e, (ConnectionError, TimeoutError)):
+            return True
+        if type(e) is RuntimeError:
+            msg = str(e).lower()
+            return any(k in msg for k in self._TRANSPORT_WORDS)
+        return False
 
     def allreduce_(self, t: torch.Tensor):
         if self.size == 1:

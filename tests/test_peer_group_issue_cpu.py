@@ -60,3 +60,25 @@ def test_issue_failure_without_watch_raises_the_error():
     g = _group(None)
     with pytest.raises(RuntimeError, match="aborted"):
         g.allreduce_(torch.zeros(4))
+
+
+class _BuggyPG:
+    def allreduce(self, *a, **k):
+        raise ValueError("split sizes do not match the tensor")
+
+    def alltoall_base(self, *a, **k):
+        raise RuntimeError("Split sizes doesn't match total dim 0 size")
+
+
+def test_caller_bug_under_watch_stays_a_crash():
+    """only transport / abort failures become a PeerFailure (a redone round); a caller's
+    shape or split mistake is re-raised unchanged and declares no abort."""
+    w = _Watch()
+    g = _group(w)
+    g.pg = _BuggyPG()
+    with pytest.raises(ValueError, match="split sizes"):
+        g.allreduce_(torch.zeros(4))
+    t = torch.zeros(8)
+    with pytest.raises(RuntimeError, match="Split sizes"):
+        g.alltoall_(t, t.clone(), [2, 2, 2, 2], [2, 2, 2, 2])
+    assert w.reasons == [] and not g.aborted and g.pg is not None

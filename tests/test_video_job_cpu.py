@@ -295,3 +295,29 @@ def test_memory_mapped_npy_source_sends_whole_chunks(coord, tmp_path):
     finally:
         req.exit_threads()
         w.exit_threads()
+
+
+def test_failed_output_writes_fail_the_job(coord, tmp_path, monkeypatch):
+    """a sink whose writes fail (disk full, I/O error) must not record a completed job
+    time for a truncated output file."""
+    import distributedvolunteercomputing_amd.control.peer as peer_mod
+
+    class Broken:
+        def write(self, f):
+            raise OSError(28, "No space left on device")
+
+        def release(self):
+            pass
+
+    monkeypatch.setattr(peer_mod, "open_sink", lambda *a, **k: Broken())
+    req = _client(coord, tmp_path, PassthroughEngine())
+    w = _client(coord, tmp_path, PassthroughEngine())
+    try:
+        req.preresize = False
+        req.become_requester("synthetic:120:64x48")
+        assert req.wait_job(timeout=60) is None  # done, but not a completed job
+        assert req.sink.done.is_set() and req.sink.errors > 0
+        assert req.job_times == [] and req.metrics.counters.get("jobs_failed", 0) == 1
+    finally:
+        for c in (req, w):
+            c.exit_threads()
