@@ -18,6 +18,9 @@
 // ds_read_b128 row reads and the ds_read_b64_tr_b16 transposed reads conflict-free. K/V (Q/dO)
 // tiles are double-buffered and staged through registers (issue next tile's global loads before
 // the MFMAs, write LDS after).
+#include <cstdio>
+#include <cstdlib>
+
 #include "attn_common.h"
 
 namespace vcx {
@@ -751,6 +754,362 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, W
 #undef sD_
 }
 
+// dK / dV with the forward ring's staging ("start with attn_bwd_dkdv"): the Q and
+// dO tiles of query tile qt + 2 and that tile's row constants (lse, delta) are issued by inline-asm
+// LDS-DMA into a 3-slot ring while tile qt computes; one counted wait (the next tile's 5 ops per wave
+// stay in flight) and one raw barrier per tile. The two-buffer kernel above stages through registers
+// and drains every load before its ds_writes (vmcnt(0) in 3 of its 7 loop blocks). Row constants
+// arrive raw (the -lse and -inf of query rows past T are applied where they are used: every tile that
+// holds rows past T runs the masked body, whose mask also drops those rows).
+namespace ring {
+constexpr int QSLOT = 2 * B_BQ * AD;           // elements: Q tile then dO tile (16 KB)
+constexpr int CSLOT = 4 * 256;                 // floats: 1 KB per wave (lse: wave 0, delta: wave 1, 2/3: spare)
+constexpr int DK_SLOT_BYTES = QSLOT * 2 + CSLOT * 4;
+}  // namespace ring
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+attn_bwd_dkdv_d64_ring_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const float* __restrict__ lse,
+                              const float* __restrict__ delta, bf16* __restrict__ dqkv, float* __restrict__ bpart, int B,
+                              int T, int H, float scale, float scale_log2, int staged_epi) {
+  using namespace ring;
+  __shared__ __attribute__((aligned(16))) char smc[3 * DK_SLOT_BYTES];
+  auto sQ_ = [&](int s) { return (bf16*)(smc + s * DK_SLOT_BYTES); };
+  auto sD_ = [&](int s) { return (bf16*)(smc + s * DK_SLOT_BYTES) + B_BQ * AD; };
+  auto sC_ = [&](int s) { return (float*)(smc + s * DK_SLOT_BYTES + QSLOT * 2); };  // [lse 256 | delta 256 | spare]
+  const int tid = threadIdx.x, lane = tid & 63, h2 = lane >> 5, col = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nkb = (T + 127) / 128;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int kbi = lb % nkb;
+  const int bh = lb / nkb;
+  const int b = bh / H, hh = bh % H;
+  const int64_t tok = 3ll * H * AD;
+  const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
+  const int64_t otok = (int64_t)H * AD;
+  const bf16* dOb = dout + (int64_t)b * T * otok + hh * AD;
+  const float* lrow = lse + ((int64_t)b * H + hh) * T;
+  const float* drow = delta + ((int64_t)b * H + hh) * T;
+  const int k0 = kbi * 128, kw = k0 + w * 32, key = kw + col, kc = min(key, T - 1);
+  sx8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = *(const sx8*)(base + H * AD + (int64_t)kc * tok + 16 * s + 8 * h2);
+    vf[s] = *(const sx8*)(base + 2 * H * AD + (int64_t)kc * tok + 16 * s + 8 * h2);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // the K/V fragments: out of the asm DMA's vmcnt accounting
+  f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
+  const int qstart = k0 / B_BQ;
+  const int nqt = (T + B_BQ - 1) / B_BQ;
+  const unsigned q_bytes = (unsigned)(((int64_t)(T - 1) * tok + AD) * 2);
+  const unsigned d_bytes = (unsigned)(((int64_t)(T - 1) * otok + AD) * 2);
+  const u32x4 rQ = desc(base, q_bytes), rD = desc(dOb, d_bytes);
+  const u32x4 rC = desc(w == 1 ? drow : lrow, (unsigned)T * 4u);  // wave 1: delta, the others: lse
+  int r_[2], c_[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = (w * 2 + i) * 64 + lane, r = p >> 3, k = (r >> 1) & 7;
+    r_[i] = r;
+    c_[i] = ((p & 7) ^ (((k & 1) << 2) | (k >> 1))) * 8;
+  }
+  auto issue = [&](int qt, int slot) {  // 5 DMA ops per wave: Q pieces 2w, 2w+1, dO pieces, row constants
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      dma16(rQ, (int)(((int64_t)min(qt * B_BQ + r_[i], T - 1) * tok + c_[i]) * 2), sQ_(slot) + (w * 2 + i) * 512);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      dma16(rD, (int)(((int64_t)min(qt * B_BQ + r_[i], T - 1) * otok + c_[i]) * 2), sD_(slot) + (w * 2 + i) * 512);
+    // lanes l and l + 16 k read floats qt * 64 + 4 (l & 15) .. + 3 (past T: outside the resource, 0)
+    const unsigned m0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(sC_(slot) + w * 256);
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"((qt * B_BQ + 4 * (lane & 15)) * 4),
+                 "s"(rC), "{m0}"(m0)
+                 : "memory");
+  };
+  // one 64-query tile; MASK: the diagonal tiles and any tile with query rows past T
+  auto tile = [&](int qt, auto slot_c, auto mask_c) {
+    constexpr int slot = decltype(slot_c)::value;
+    constexpr bool MASK = decltype(mask_c)::value;
+    const bf16* sQ = sQ_(slot);
+    const bf16* sD = sD_(slot);
+    const float* sL = sC_(slot);
+    const float* sDel = sC_(slot) + 256;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int qb = qt * B_BQ + sub * 32;
+      if (MASK && qb + 31 < kw) continue;  // every query before this wave's first key
+      f32x16 st = {}, dp = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        st = mfma32(row_frag_swz(sQ, sub * 32 + col, s, h2), kf[s], st);
+        dp = mfma32(row_frag_swz(sD, sub * 32 + col, s, h2), vf[s], dp);
+      }
+      f32x16 pp;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 lv = *(const f32x4*)(&sL[sub * 32 + 8 * g + 4 * h2]);
+        const f32x4 dv = *(const f32x4*)(&sDel[sub * 32 + 8 * g + 4 * h2]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * g + i;
+          float p = __builtin_amdgcn_exp2f(fmaf(st[r], scale_log2, -lv[i]));
+          if (MASK) {
+            const int qq = qb + 8 * g + 4 * h2 + i;
+            p = (key > qq || qq >= T) ? 0.f : p;
+          }
+          pp[r] = p;
+          st[r] = p * (dp[r] - dv[i]);  // dS
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sx8 pb, sb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pb[j] = bf16_bits(pp[8 * s + j]);
+          sb[j] = bf16_bits(st[8 * s + j]);
+        }
+        dv0 = mfma32(vt_frag_swz(sD, sub * 32, 0, s, lane), pb, dv0);
+        dv1 = mfma32(vt_frag_swz(sD, sub * 32, 1, s, lane), pb, dv1);
+        dk0 = mfma32(vt_frag_swz(sQ, sub * 32, 0, s, lane), sb, dk0);
+        dk1 = mfma32(vt_frag_swz(sQ, sub * 32, 1, s, lane), sb, dk1);
+      }
+    }
+  };
+  // tile qt sits in slot (qt - qstart) % 3; issue qt + 2 into the slot qt - 1 left, compute qt, wait for
+  // this wave's 5 ops of qt + 1 (qt + 2's stay in flight), barrier
+  auto step = [&](int qt, auto slot_c, auto mask_c) {
+    constexpr int slot = decltype(slot_c)::value;
+    const bool more = qt + 2 < nqt;
+    if (more) issue(qt + 2, (slot + 2) % 3);
+    tile(qt, slot_c, mask_c);
+    if (more)
+      wait_vm<5>();
+    else
+      wait_vm<0>();
+    barrier();
+  };
+  using I2 = std::integral_constant<int, 2>;
+  using Fm = std::false_type;
+  using Tm = std::true_type;
+  issue(qstart, 0);
+  if (qstart + 1 < nqt) issue(qstart + 1, 1);
+  if (qstart + 1 < nqt)
+    wait_vm<5>();
+  else
+    wait_vm<0>();
+  barrier();
+  // the last tile takes the masked body when it holds query rows past T
+  const int nfull = (T % B_BQ) ? nqt - 1 : nqt;  // tiles [.., nfull) have no rows past T
+  step(qstart, I0{}, Tm{});  // queries k0 .. k0 + 127 cross the diagonal
+  int qt = qstart + 1;
+  if (qt < nqt) step(qt++, I1{}, Tm{});
+  // slot of qt is (qt - qstart) % 3 = 2 here
+  for (; qt + 2 < nfull; qt += 3) {
+    step(qt, I2{}, Fm{});
+    step(qt + 1, I0{}, Fm{});
+    step(qt + 2, I1{}, Fm{});
+  }
+  for (; qt < nqt; ++qt) {
+    const int sl = (qt - qstart) % 3;
+    const bool m = qt >= nfull;
+    if (sl == 0) {
+      if (m) step(qt, I0{}, Tm{}); else step(qt, I0{}, Fm{});
+    } else if (sl == 1) {
+      if (m) step(qt, I1{}, Tm{}); else step(qt, I1{}, Fm{});
+    } else {
+      if (m) step(qt, I2{}, Tm{}); else step(qt, I2{}, Fm{});
+    }
+  }
+  bf16* sm0 = (bf16*)smc;
+  if (bpart) {  // column sums of this block's dK and dV rows: slots 1 and 2 of a QKV-bias partial row
+    float* red = (float*)smc;  // the ring is dead after the loop's last barrier (every DMA retired)
+    float v[32];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      v[r] = key < T ? dk0[r] * scale : 0.f;
+      v[16 + r] = key < T ? dk1[r] * scale : 0.f;
+    }
+    red[w * AD + acc_pair_col(col, h2)] = half_colsum32(v, col);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      v[r] = key < T ? dv0[r] : 0.f;
+      v[16 + r] = key < T ? dv1[r] : 0.f;
+    }
+    red[4 * AD + w * AD + acc_pair_col(col, h2)] = half_colsum32(v, col);
+    __syncthreads();
+    if (tid < 2 * AD) {
+      const int sl = tid >> 6, d = tid & 63;
+      const float* rr = red + sl * 4 * AD;
+      bpart[((int64_t)b * nkb + kbi) * 3 * H * AD + (1 + sl) * H * AD + hh * AD + d] =
+          (rr[d] + rr[AD + d]) + (rr[2 * AD + d] + rr[3 * AD + d]);
+    }
+    __syncthreads();  // red is overwritten by the dK images below
+  }
+  bf16* dk_row0 = dqkv + ((int64_t)b * T + kw) * tok + H * AD + hh * AD;  // slot 1 = dK, slot 2 = dV
+  store_acc_tile(dk0, dk1, scale, dk_row0, tok, T - kw, sm0 + w * 32 * AD, staged_epi, lane);
+  store_acc_tile(dv0, dv1, 1.f, dk_row0 + H * AD, tok, T - kw, sm0 + 4 * 32 * AD + w * 32 * AD, staged_epi, lane);
+}
+
+// dQ with the ring staging of the forward (K / V tiles of key tile kt + 2 in flight while kt computes)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+attn_bwd_dq_d64_ring_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout, const bf16* __restrict__ out,
+                            const float* __restrict__ lse, float* __restrict__ delta, bf16* __restrict__ dqkv,
+                            float* __restrict__ bpart, int B, int T, int H, float scale, float scale_log2,
+                            int staged_epi) {
+  using namespace ring;
+  __shared__ __attribute__((aligned(16))) bf16 sm[3 * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, h2 = lane >> 5, col = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqt = (T + A_BQ - 1) / A_BQ;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int qt = nqt - 1 - (lb % nqt);
+  const int bh = lb / nqt;
+  const int b = bh / H, hh = bh % H;
+  const int64_t tok = 3ll * H * AD;
+  const bf16* base = qkv + (int64_t)b * T * tok + hh * AD;
+  const int64_t otok = (int64_t)H * AD;
+  const bf16* dOb = dout + (int64_t)b * T * otok + hh * AD;
+  const int q0 = qt * A_BQ, qw = q0 + w * 32, q = qw + col, qc = min(q, T - 1);
+  sx8 qf[4], df[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = *(const sx8*)(base + (int64_t)qc * tok + 16 * s + 8 * h2);
+    df[s] = *(const sx8*)(dOb + (int64_t)qc * otok + 16 * s + 8 * h2);
+  }
+  const float nlq = -lse[((int64_t)b * H + hh) * T + qc];
+  const f32x16 lq16 = splat16(nlq);
+  float dq_delta;
+  {
+    const bf16* Ob = out + ((int64_t)b * T + qc) * otok + hh * AD;
+    float acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const sx8 ov = *(const sx8*)(Ob + 16 * s + 8 * h2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const short ob = ov[j], db = df[s][j];
+        acc = fmaf((float)*(const bf16*)&ob, (float)*(const bf16*)&db, acc);
+      }
+    }
+    dq_delta = xhalf_sum(acc);
+    if (h2 == 0 && q < T) delta[((int64_t)b * H + hh) * T + q] = dq_delta;
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // every compiler-issued load / store retired before the asm DMA
+  const f32x16 dl16 = splat16(-dq_delta);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = prescale(qf[s], scale_log2);
+  f32x16 a0 = {}, a1 = {};
+  const int kend = min(T, q0 + A_BQ);
+  const int nkt = (kend + A_BK - 1) / A_BK;
+  const unsigned kv_bytes = (unsigned)(((int64_t)(T - 1) * tok + AD) * 2);
+  const u32x4 rK = desc(base + H * AD, kv_bytes), rV = desc(base + 2 * H * AD, kv_bytes);
+  int r_[2], c_[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = (w * 2 + i) * 64 + lane, r = p >> 3, k = (r >> 1) & 7;
+    r_[i] = r;
+    c_[i] = ((p & 7) ^ (((k & 1) << 2) | (k >> 1))) * 8;
+  }
+  auto issue = [&](int kt, int slot) {
+    bf16* sl = sm + slot * SLOT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      dma16(rK, (int)(((int64_t)min(kt * A_BK + r_[i], T - 1) * tok + c_[i]) * 2), sl + (w * 2 + i) * 512);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      dma16(rV, (int)(((int64_t)min(kt * A_BK + r_[i], T - 1) * tok + c_[i]) * 2), sl + A_BK * AD + (w * 2 + i) * 512);
+  };
+  auto tile = [&](int kt, auto slot_c, auto mask_c) {
+    constexpr int slot = decltype(slot_c)::value;
+    constexpr bool MASK = decltype(mask_c)::value;
+    const bf16* sK = sm + slot * SLOT;
+    const bf16* sV = sK + A_BK * AD;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb = kt * A_BK + sub * 32;
+      if (MASK && kb > qw + 31) continue;
+      f32x16 st = lq16, dp = dl16;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        st = mfma32(row_frag_swz(sK, sub * 32 + col, s, h2), qf[s], st);
+        dp = mfma32(row_frag_swz(sV, sub * 32 + col, s, h2), df[s], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = __builtin_amdgcn_exp2f(st[r]);
+        if (MASK) {
+          const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * h2;
+          p = key > q ? 0.f : p;
+        }
+        st[r] = p * dp[r];  // dS^T
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sx8 db;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) db[j] = bf16_bits(st[8 * s + j]);
+        a0 = mfma32(vt_frag_swz(sK, sub * 32, 0, s, lane), db, a0);
+        a1 = mfma32(vt_frag_swz(sK, sub * 32, 1, s, lane), db, a1);
+      }
+    }
+  };
+  auto step = [&](int kt, auto slot_c, auto mask_c) {
+    constexpr int slot = decltype(slot_c)::value;
+    const bool more = kt + 2 < nkt;
+    if (more) issue(kt + 2, (slot + 2) % 3);
+    tile(kt, slot_c, mask_c);
+    if (more)
+      wait_vm<4>();
+    else
+      wait_vm<0>();
+    barrier();
+  };
+  using I2 = std::integral_constant<int, 2>;
+  using Fm = std::false_type;
+  using Tm = std::true_type;
+  issue(0, 0);
+  if (nkt > 1) issue(1, 1);
+  if (nkt > 1)
+    wait_vm<4>();
+  else
+    wait_vm<0>();
+  barrier();
+  const int kdiag = q0 / A_BK;
+  int kt = 0;
+  for (; kt + 2 < kdiag; kt += 3) {
+    step(kt, I0{}, Fm{});
+    step(kt + 1, I1{}, Fm{});
+    step(kt + 2, I2{}, Fm{});
+  }
+  if (kt < kdiag) step(kt++, I0{}, Fm{});
+  if (kt < kdiag) step(kt++, I1{}, Fm{});
+  for (; kt < nkt; ++kt) {
+    const int sl = kt % 3;
+    if (sl == 0)
+      step(kt, I0{}, Tm{});
+    else if (sl == 1)
+      step(kt, I1{}, Tm{});
+    else
+      step(kt, I2{}, Tm{});
+  }
+  store_acc_tile(a0, a1, scale, dqkv + ((int64_t)b * T + qw) * tok + hh * AD, tok, T - qw,  // slot 0 = dQ
+                 sm + w * 32 * AD, staged_epi, lane);
+  if (bpart) {
+    float v[32];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      v[r] = q < T ? a0[r] * scale : 0.f;
+      v[16 + r] = q < T ? a1[r] * scale : 0.f;
+    }
+    const float cs = half_colsum32(v, col);
+    float* red = (float*)(sm + SLOT);  // past the dQ images (slot 0 holds them)
+    red[w * AD + acc_pair_col(col, h2)] = cs;
+    __syncthreads();
+    if (tid < AD)
+      bpart[((int64_t)b * nqt + qt) * 3 * H * AD + hh * AD + tid] =
+          (red[tid] + red[AD + tid]) + (red[2 * AD + tid] + red[3 * AD + tid]);
+  }
+}
+
 }  // namespace vcx
 
 using namespace vcx;
@@ -761,16 +1120,32 @@ using namespace vcx;
 // Backward kernels: 2 waves per SIMD (at 3-4 they spill: dq 0.87-1.25 ms vs 0.64 for the pair);
 // dQ with LDS-DMA staging (264 vs 275 us), dK/dV with register staging (381 vs 383 us: the DMA
 // build of that kernel hits the 256-VGPR cap and spills).
-static int g_fwd_wpe = 3, g_fwd_dma = 1, g_bwd_dma = 1;  // g_bwd_dma bit 0: dQ kernel, bit 1: dK/dV kernel
+// Round 6 defaults: the forward and dK/dV on the 3-slot inline-asm LDS-DMA ring (fwd_dma = 2, bwd bit 2): same
+// box, interleaved medians (profiles/r6_attention_ring.txt): forward 0.1937 vs 0.2080 ms, backward 0.5571 vs
+// 0.5852 ms, outputs bit-identical at T = 1024 / 200 / 202; bench 1063.2 / 1063.0 vs 1053.6 samples/s. The dQ
+// kernel on the ring (bit 3) measured even (0.5837 ms) and stays on the two-buffer LDS-DMA kernel.
+static int g_fwd_wpe = 3, g_fwd_dma = 2, g_bwd_dma = 5;  // g_bwd_dma bit 0: dQ LDS-DMA, 1: dK/dV LDS-DMA, 2: dK/dV ring, 3: dQ ring
 // output tiles (O, dQ, dK, dV): 1 = staged through LDS, whole-row 16-B stores; 0 = per-lane half-row
 // stores. Bench shape, same box (profiles/r1_attn_variants.log): backward 0.589 vs 0.614 ms, forward
 // within noise (0.201-0.212 vs 0.206-0.208)
 static int g_stage_epi = 1;
 
+void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma, int stage_epi);
+// VCX_ATTN="fwd_wpe,fwd_dma,bwd_dma" overrides the defaults once, at the first launch (bench A/B)
+static void env_variant() {
+  static const bool once = [] {
+    const char* e = std::getenv("VCX_ATTN");
+    int a = -1, b = -1, c = -1;
+    if (e && std::sscanf(e, "%d,%d,%d", &a, &b, &c) == 3) vcx_attn_set_variant(a, b, c, -1);
+    return true;
+  }();
+  (void)once;
+}
+
 void vcx_attn_set_variant(int fwd_wpe, int fwd_dma, int bwd_dma, int stage_epi) {
   if (fwd_wpe == 2 || fwd_wpe == 3) g_fwd_wpe = fwd_wpe;
   if (fwd_dma >= 0 && fwd_dma <= 2) g_fwd_dma = fwd_dma;  // 2: the 3-slot ring (attn_fwd_d64_ring_kernel)
-  if (bwd_dma >= 0 && bwd_dma <= 3) g_bwd_dma = bwd_dma;
+  if (bwd_dma >= 0 && bwd_dma <= 15) g_bwd_dma = bwd_dma;  // bit 2: dK/dV on the 3-slot ring, bit 3: dQ on it
   if (stage_epi == 0 || stage_epi == 1) g_stage_epi = stage_epi;
 }
 
@@ -778,10 +1153,15 @@ int vcx_attn_bias_partials(int B, int T) { return B * ((T + 127) / 128); }
 
 void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const float* lse, float* delta, void* dqkv,
                       float* bias_part, int B, int T, int H, float scale, hipStream_t s) {
+  env_variant();
   // dQ first: it also computes delta = rowsum(dO * O) for the dK/dV kernel
   const int nkb = (T + 127) / 128;
   const int nqt = (T + A_BQ - 1) / A_BQ;
-  if (g_bwd_dma & 1)
+  if (g_bwd_dma & 8)
+    hipLaunchKernelGGL(attn_bwd_dq_d64_ring_kernel, dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale,
+                       scale * LOG2E, g_stage_epi);
+  else if (g_bwd_dma & 1)
     hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, true>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale,
                        scale * LOG2E, g_stage_epi);
@@ -789,7 +1169,11 @@ void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const 
     hipLaunchKernelGGL((attn_bwd_dq_d64_kernel<2, false>), dim3(B * H * nqt), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, (const bf16*)out, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale,
                        scale * LOG2E, g_stage_epi);
-  if (g_bwd_dma & 2)
+  if ((g_bwd_dma & 4) && T % 4 == 0)  // the row-constant DMA reads 16-B groups of lse / delta rows
+    hipLaunchKernelGGL(attn_bwd_dkdv_d64_ring_kernel, dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
+                       (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E,
+                       g_stage_epi);
+  else if (g_bwd_dma & 2)
     hipLaunchKernelGGL((attn_bwd_dkdv_d64_kernel<2, true>), dim3(B * H * nkb), dim3(256), 0, s, (const bf16*)qkv,
                        (const bf16*)dout, lse, delta, (bf16*)dqkv, bias_part, B, T, H, scale, scale * LOG2E,
                        g_stage_epi);
@@ -800,6 +1184,7 @@ void vcx_attn_bwd_d64(const void* qkv, const void* out, const void* dout, const 
 }
 
 void vcx_attn_fwd_d64(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t s) {
+  env_variant();
   const int nqt = (T + A_BQ - 1) / A_BQ;
   const dim3 g(B * H * nqt);
 #define VCX_FWD(W, D)                                                                                      \

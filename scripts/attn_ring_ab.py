@@ -50,4 +50,23 @@ for v, ts in res.items():
     ms = sorted(ts)[len(ts) // 2]
     print(f"fwd (waves/SIMD, staging) {v}: {ms:.4f} ms  {fl / ms / 1e9:7.1f} TF/s  rounds {['%.4f' % x for x in ts]}",
           flush=True)
+
+# backward: bwd_dma bits (1: dQ LDS-DMA two-buffer, 2: dK/dV LDS-DMA two-buffer, 4: dK/dV ring, 8: dQ ring)
+dO = torch.randn(B, T, H, D, device="cuda", dtype=torch.bfloat16)
+C.attn_set_variant(3, 1, 1, 1)
+g_ref = C.attn_bwd(qkv, o_ref, dO, l_ref, scale)
+bvars = [1, 5, 8, 12, 3]
+for v in bvars:
+    C.attn_set_variant(3, 1, v, 1)
+    g = C.attn_bwd(qkv, o_ref, dO, l_ref, scale)
+    torch.cuda.synchronize()
+    print(f"bwd bits {v}: max|dqkv - default| = {(g.float() - g_ref.float()).abs().max().item():.3e}", flush=True)
+bres = {v: [] for v in bvars}
+for rnd in range(5):
+    for v in bvars:
+        C.attn_set_variant(3, 1, v, 1)
+        bres[v].append(tm(lambda: C.attn_bwd(qkv, o_ref, dO, l_ref, scale)))
+for v, ts in bres.items():
+    ms = sorted(ts)[len(ts) // 2]
+    print(f"bwd bits {v}: {ms:.4f} ms  {2.5 * fl / ms / 1e9:7.1f} TF/s  rounds {['%.4f' % x for x in ts]}", flush=True)
 C.attn_set_variant(3, 1, 1, 1)

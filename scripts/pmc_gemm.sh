@@ -10,7 +10,9 @@ shift || true
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 i=0
-for set in "SQ_WAVES SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_INST_LDS" "FETCH_SIZE"; do
+for set in "FETCH_SIZE GRBM_GUI_ACTIVE" "WRITE_SIZE GRBM_GUI_ACTIVE" \
+           "SQ_WAVES SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i + 1))
   echo "[pmc] pass $i: $set"
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $set --output-format csv -d "$OUT/p$i" -o run -- \
@@ -20,5 +22,5 @@ for set in "SQ_WAVES SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_IN
   [ $rc -ne 0 ] && { tail -5 "$OUT/p$i.log"; exit $rc; }
 done
 python3 "$R/scripts/pmc_summary.py" "$OUT" > "$OUT/summary.txt" || exit $?
-rm -rf "$OUT"/p1 "$OUT"/p2  # the raw counter CSVs exceed what gpurun copies back; the summary keeps the numbers
+rm -rf "$OUT"/p1 "$OUT"/p2 "$OUT"/p3 "$OUT"/p4  # the raw counter CSVs exceed what gpurun copies back; the summary keeps the numbers
 exit 0
