@@ -120,8 +120,14 @@ def bench_job(args, dev, plane="relay", source=None, out_ext=None):
     from distributedvolunteercomputing_amd.control.peer import client
     from distributedvolunteercomputing_amd.jobs.video import DetectorEngine
 
+    from distributedvolunteercomputing_amd import config as vcx_config
+
     out_ext = out_ext or "." + args.sink
-    coord = coordinator("127.0.0.1", 0, ephemeral_ports=True, credits=2, data_plane=plane)
+    # p2p_shared: the p2p plane with the source under the shared root (the workers read their chunks'
+    # frames from the file themselves; the requester sends index windows)
+    shared = plane == "p2p_shared"
+    root = os.path.dirname(os.path.realpath(source)) if shared and source else ""
+    coord = coordinator("127.0.0.1", 0, ephemeral_ports=True, credits=2, data_plane="p2p" if shared else plane)
     eng = DetectorEngine(device=dev)  # one GPU: volunteers share one engine (serialised by a lock)
     shm = "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else None
     tmp = tempfile.mkdtemp(prefix="vcx_video_", dir=shm)  # RAM-backed like the source; removed after the job
@@ -132,8 +138,9 @@ def bench_job(args, dev, plane="relay", source=None, out_ext=None):
     try:
         if source and source.endswith(".npy") and args.source_frames and args.source_frames < args.frames:
             source = f"{source}@{args.frames}"  # the pre-generated file played in a loop
-        req.become_requester(source or f"synthetic:{args.frames}:{args.width}x{args.height}")
-        t = req.wait_job(timeout=1800)
+        with vcx_config.override(shared_source_root=root):
+            req.become_requester(source or f"synthetic:{args.frames}:{args.width}x{args.height}")
+            t = req.wait_job(timeout=1800)
         n = req.sink.written if (t and req.sink is not None) else 0
         # host busy time per stage of each volunteer thread (where the job's wall time goes)
         spans = {"requester": req.hspans.snapshot()}
@@ -143,6 +150,11 @@ def bench_job(args, dev, plane="relay", source=None, out_ext=None):
             reg = "failed"
         for i, w in enumerate(workers):
             spans[f"worker{i}"] = w.hspans.snapshot()
+        # bytes each volunteer moved over its own host -> GPU link (requester: raw chunks it uploaded for its
+        # resize; workers: host chunks they uploaded to their engine), and the chunks sent as index windows
+        h2d = {"requester": int(req.metrics.counters.get("h2d_bytes", 0))}
+        h2d.update({f"worker{i}": int(w.metrics.counters.get("h2d_bytes", 0)) for i, w in enumerate(workers)})
+        windows = int(req.metrics.counters.get("window_chunks_sent", 0))
     finally:
         for c in [req] + workers:
             c.exit_threads()
@@ -153,7 +165,8 @@ def bench_job(args, dev, plane="relay", source=None, out_ext=None):
     pre = "job" if plane == "relay" else f"job_{plane}"
     return {f"{pre}_time_s": round(t, 3) if t else None, f"{pre}_frames": n,
             f"{pre}_frames_per_s": round(n / t, 1) if t else None, "workers": args.workers,
-            f"{pre}_sink": out_ext, f"{pre}_source_register_ms": reg, f"{pre}_host_spans": spans}
+            f"{pre}_sink": out_ext, f"{pre}_source_register_ms": reg, f"{pre}_host_spans": spans,
+            f"{pre}_h2d_bytes": h2d, f"{pre}_window_chunks": windows}
 
 
 def make_npy_source(args) -> str:
@@ -196,7 +209,9 @@ def main():
     ap.add_argument("--uplink-ab", action="store_true",
                     help="each plane runs with the requester's two-stage uplink off and on (VCX_UPLINK_PIPELINE=off/all), "
                          "interleaved: keys job[_p2p]_* (off) and job[_p2p]_pipe_* (on)")
-    ap.add_argument("--data-plane", default="both", choices=["relay", "p2p", "both"])
+    ap.add_argument("--data-plane", default="both", choices=["relay", "p2p", "p2p_shared", "both", "all"],
+                    help="both = relay + p2p; all = relay + p2p + p2p_shared (workers read their chunks from the "
+                         "memory-mapped source themselves: one host link per GPU instead of the requester's)")
     ap.add_argument("--y4m-frames", type=int, default=0, help="also run the job on a Y4M file of this many frames")
     ap.add_argument("--sink", default="npy", choices=["npy", "y4m"],
                     help="the requester's output file, written as the frames arrive and closed inside the "
@@ -217,7 +232,7 @@ def main():
             # sub-second job on a shared host is +-15 %): the median is reported, every run listed
             from distributedvolunteercomputing_amd import config as vcx_config
 
-            planes = ("relay", "p2p") if a.data_plane == "both" else (a.data_plane,)
+            planes = {"both": ("relay", "p2p"), "all": ("relay", "p2p", "p2p_shared")}.get(a.data_plane, (a.data_plane,))
             variants = [(pl, pipe) for pl in planes for pipe in ((False, True) if a.uplink_ab else (None,))]
             runs = {v: [] for v in variants}
             for _ in range(max(1, a.job_repeats)):
@@ -243,7 +258,8 @@ def main():
                 os.unlink(src)
         if a.y4m_frames:
             rec.update(bench_y4m_job(a, dev))
-    rec["value"] = max([rec.get(k) or 0 for k in ("job_frames_per_s", "job_p2p_frames_per_s")]) or \
+    rec["value"] = max([rec.get(k) or 0 for k in ("job_frames_per_s", "job_p2p_frames_per_s",
+                                                    "job_p2p_shared_frames_per_s")]) or \
         rec["engine_frames_per_s"]
     print(json.dumps(rec), flush=True)
 

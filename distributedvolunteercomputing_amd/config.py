@@ -35,6 +35,9 @@ class RuntimeConfig:
     # VCX_NARROW_GEMM: GEMMs with <= 128 output columns and >= 32k rows (ResNet 1x1 convolutions) on
     # the vision GEMM ("vision") or the library ("lib")
     narrow_gemm: str = "lib"
+    # VCX_MLP_GRAD_FWD: the fused fc forward stores gelu'(pre) instead of pre, so the fc2 input gradient's
+    # epilogue is one multiply (gemm_ps epilogues 5 / 6) instead of gelu'(pre) per element (4)
+    mlp_grad_fwd: bool = True
     dgrad_ps: bool = True  # VCX_DGRAD_PS: input gradients dX = dY W with K <= 2304 on gemm_ps (measured faster)
     gemm_wgrad: str = "vcx"  # VCX_GEMM_WGRAD: weight gradients on "vcx" (gemm_wg, hand-written) or "lib" (split-M batched GEMM)
     # VCX_WGRAD_WIDE: also outputs of more than 128 256x256 tiles with <= 1024 input columns on gemm_wg (the
@@ -92,6 +95,12 @@ class RuntimeConfig:
     # p2p 4650 vs 6101 frames/s: on the p2p plane the wire stage ships only metadata and the extra
     # thread's host copies just contend; profiles/r4_video_job_spans.txt), "all", or "off"
     uplink_pipeline: str = "relay"
+    # VCX_SHARED_SOURCE_ROOT: on the p2p chunk plane, a requester whose source is a memory-mapped .npy file
+    # under this directory sends each chunk as an index window (file, first frame, count) and every worker
+    # reads its window from the file and uploads it over its OWN host link (8 GPUs: 8 links instead of the
+    # requester's one); a worker reads only windows of .npy files under its own value. "" = off (the
+    # requester uploads, resizes and sends the frames). node_job sets it to the source's directory.
+    shared_source_root: str = ""
     store_port_train: int = 29611  # VCX_STORE_PORT (train CLI): rendezvous store port
     store_port_video: int = 29612  # VCX_STORE_PORT (video CLI): job-control store port
     # ---- observability
@@ -104,6 +113,7 @@ _ENV = {
     "gemm": ("VCX_GEMM", str),
     "mlp": ("VCX_MLP", str),
     "dgrad_ps": ("VCX_DGRAD_PS", _bool),
+    "mlp_grad_fwd": ("VCX_MLP_GRAD_FWD", _bool),
     "narrow_gemm": ("VCX_NARROW_GEMM", str),
     "resnet_conv1x1": ("VCX_RESNET_CONV1X1", str),
     "resnet_bn": ("VCX_RESNET_BN", str),
@@ -133,6 +143,7 @@ _ENV = {
     "elastic_liveness": ("VCX_ELASTIC_LIVENESS", _bool),
     "elastic_stage_joins": ("VCX_ELASTIC_STAGE_JOINS", str),
     "uplink_pipeline": ("VCX_UPLINK_PIPELINE", str),
+    "shared_source_root": ("VCX_SHARED_SOURCE_ROOT", str),
     "store_port_train": ("VCX_STORE_PORT", int),
     "store_port_video": ("VCX_STORE_PORT", int),
     "trace_dir": ("VCX_TRACE_DIR", str),

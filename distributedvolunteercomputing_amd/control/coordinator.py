@@ -47,6 +47,20 @@ from .transport import BadFrame, FrameHub, FrameSender
 _EMPTY = np.zeros(0, dtype=np.uint8)  # payload of a metadata-only frame
 
 
+def _window(w):
+    """A well-formed shared-source window {path: str, first: int >= 0, n: int > 0}, else None (the chunk
+    then travels as frames). Only the shape is checked here; each worker checks the path against its own
+    shared_source_root before it reads anything (peer._read_window)."""
+    if not isinstance(w, dict):
+        return None
+    path, first, n = w.get("path"), w.get("first"), w.get("n")
+    if not isinstance(path, str) or not path or len(path) > 4096:
+        return None
+    if not all(isinstance(x, int) and not isinstance(x, bool) for x in (first, n)) or first < 0 or n <= 0:
+        return None
+    return {"path": path, "first": first, "n": n}
+
+
 class _Volunteer:
     def __init__(self, addr, port, hub, sender, vid=0):
         self.vid = vid
@@ -344,6 +358,12 @@ class coordinator:  # noqa: N801  (reference class name)
                 continue
             if command == "failed" and p2p:  # a pair transfer of this chunk to v failed
                 cid = int(hdr.get("chunk", -1))
+                if hdr.get("nowin"):  # v cannot read the chunk's shared-source window: the requester sends it
+                    with self._lock:
+                        rec = self.chunks.get(cid)
+                        if rec is not None and rec[2] is not None:
+                            rec[2]["win"] = None
+                    self.metrics.incr("window_fallbacks")
                 if self.sched.fail(cid, v.addr):
                     self.metrics.incr("p2p_failed_requeued")
                     self._kick()
@@ -354,8 +374,10 @@ class coordinator:  # noqa: N801  (reference class name)
                 cid = next(self._ids)
                 with self._lock:
                     # p2p: metadata only — the frames stay in the requester's (GPU) memory
+                    # shared-source mode: `win` = the chunk's index window in a file the workers read themselves
                     self.chunks[cid] = (info, None, {"key": hdr.get("key"), "cshape": hdr.get("cshape"),
-                                                     "src": v.vid}) if p2p else (info, arr, None)
+                                                     "src": v.vid, "win": _window(hdr.get("win"))}) if p2p \
+                        else (info, arr, None)
                 self.sched.submit(cid, requester)
                 self.metrics.incr("chunks_in")
                 self._kick()
@@ -425,6 +447,10 @@ class coordinator:  # noqa: N801  (reference class name)
                 with self._lock:
                     self.chunks.pop(a.chunk, None)
                 continue
+            elif meta.get("win") is not None:  # shared source: the worker reads the window itself
+                v.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "work", "chunk": a.chunk, "src": meta["src"],
+                                             "cshape": meta["cshape"], "key": meta["key"], "win": meta["win"]}))
+                self.metrics.incr("window_dispatched")
             else:  # p2p: the worker posts the receive, the requester the send, of the same chunk
                 v.outbox.put((info, _EMPTY, {"p2p": 1, "cmd": "work", "chunk": a.chunk, "src": meta["src"],
                                              "cshape": meta["cshape"], "key": meta["key"]}))

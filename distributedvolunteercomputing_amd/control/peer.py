@@ -92,6 +92,36 @@ def _host_tensor(a: np.ndarray) -> torch.Tensor:
         return torch.from_numpy(a)
 
 
+class _Window:
+    """A chunk that stays in its source file (shared-source mode): frames [first, first + n) of a
+    memory-mapped uint8 [N, H, W, 3] .npy that every volunteer can read. The requester sends this
+    index window instead of the frames; a worker reads and uploads the frames itself, over its own
+    host link (the requester's single link is the ingest bound)."""
+
+    __slots__ = ("path", "first", "n", "shape")
+
+    def __init__(self, path: str, first: int, n: int, shape):
+        self.path, self.first, self.n, self.shape = path, int(first), int(n), tuple(shape)
+
+    def meta(self) -> dict:
+        return {"path": self.path, "first": self.first, "n": self.n}
+
+    def read(self) -> np.ndarray:
+        return np.load(self.path, mmap_mode="r", allow_pickle=False)[self.first:self.first + self.n]
+
+
+def _shared_path(path) -> str | None:
+    """`path` resolved, if it is a .npy file under this volunteer's shared_source_root (else None):
+    a worker reads windows of such files only, so a requester cannot make it read anything else."""
+    root = config.get().shared_source_root
+    if not root or not path:
+        return None
+    p, r = os.path.realpath(str(path)), os.path.realpath(root)
+    if not p.endswith(".npy") or os.path.commonpath([p, r]) != r or not os.path.isfile(p):
+        return None
+    return p
+
+
 class client:  # noqa: N801 (reference class name)
     verbose = False
     req_rep = True
@@ -152,6 +182,7 @@ class client:  # noqa: N801 (reference class name)
         self._pins: dict = {}  # pinned staging of the requester's pre-resize (by role)
         # memory-mapped sources page-locked in place (hipHostRegister): id -> (array, base address)
         self._registered: dict = {}
+        self._win_maps: dict[str, np.ndarray] = {}  # shared-source mode: this worker's mappings by path
         # guards _registered and the enqueue of copies out of a registered mapping: a new job's
         # requester thread unregisters while the previous job's send thread may still be using it
         self._reg_lock = threading.Lock()
@@ -225,10 +256,14 @@ class client:  # noqa: N801 (reference class name)
             self._outgoing.clear()
         src = open_source(path)
         time.sleep(0.0 if path != "live" else 0.5)  # camera warm-up in the reference: 2 s
+        # shared-source mode: on the p2p plane, chunks of a memory-mapped file under the shared root
+        # go out as index windows; the workers read and upload the frames themselves
+        win_path = _shared_path(getattr(src, "path", None)) if self.plane is not None else None
         # the job clock starts before the source is page-locked (reference: before the first read,
         # worker.py:105-107): that setup grows with the source and is part of the job
         self.start_time = time.time()
-        self._register_source(src)
+        if win_path is None:
+            self._register_source(src)
         out_path = self.path_out
 
         def done(sink):
@@ -247,6 +282,14 @@ class client:  # noqa: N801 (reference class name)
         n = 0
         C = self.number_of_frames_in_chunk
         while self.continue_requesting:
+            if win_path is not None:  # an index window: no frame byte is read or moved here
+                j = src.i % len(src.a)
+                arr = src.read_chunk(C)  # a view of the mapping (its pages are never touched)
+                if len(arr) == 0:
+                    break
+                self.send_q.put(("window", (n + 1, _Window(win_path, j, len(arr), arr.shape))))
+                n += len(arr)
+                continue
             if src.chunked:  # whole chunks straight from the source (memory-mapped file: no copy here)
                 with self.hspans.span("req_read"):
                     arr = src.read_chunk(C)
@@ -302,6 +345,13 @@ class client:  # noqa: N801 (reference class name)
         if (self.resize_device is None or not self.preresize or not isinstance(a, np.memmap) or a.nbytes == 0
                 or not config.get().register_source):
             return
+        self._register_mapping(a)
+
+    def _register_mapping(self, a):
+        """hipHostRegister (read-only) of the pages under a memory-mapped array; kept until
+        _unregister_sources (next job of this requester, or exit)."""
+        if not isinstance(a, np.memmap) or a.nbytes == 0:
+            return
         from torch._C import _cudart
 
         ptr = a.__array_interface__["data"][0]
@@ -327,9 +377,12 @@ class client:  # noqa: N801 (reference class name)
 
             if self._rs_stream is not None:
                 self._rs_stream.synchronize()
+            if self._win_maps and torch.cuda.is_available():
+                torch.cuda.synchronize()  # a worker's uploads out of a registered window mapping
             for a, base in list(self._registered.values()):
                 _cudart.cudaHostUnregister(base)
             self._registered.clear()
+            self._win_maps.clear()
 
     def _registered_block(self, frames):
         """True when `frames` is a view of a page-locked source mapping (call under _reg_lock)."""
@@ -339,6 +392,38 @@ class client:  # noqa: N801 (reference class name)
         while isinstance(b.base, np.ndarray):
             b = b.base
         return any(b is a for a, _ in list(self._registered.values())) and frames.flags.c_contiguous
+
+    def _read_window(self, win, cshape):
+        """The frames of a shared-source window as a view of this worker's mapping of the file (None when
+        the window is malformed, outside this volunteer's shared_source_root, or not what was announced).
+        On a GPU worker the whole mapping is page-locked once (as the requester does, _register_source),
+        so each chunk's upload is one DMA out of the page cache over this worker's own link."""
+        try:
+            path, first, n = str(win["path"]), int(win["first"]), int(win["n"])
+        except (KeyError, TypeError, ValueError):
+            return None
+        p = _shared_path(path)
+        if p is None or first < 0 or n <= 0:
+            return None
+        a = self._win_maps.get(p)
+        if a is None:
+            try:
+                a = np.load(p, mmap_mode="r", allow_pickle=False)
+            except (OSError, ValueError):
+                return None
+            if a.ndim != 4 or a.dtype != np.uint8 or a.shape[-1] != 3:
+                return None
+            self._win_maps[p] = a
+            eng = self.engine
+            if (eng is not None and getattr(eng, "device", None) is not None and torch.device(eng.device).type == "cuda"
+                    and config.get().register_source):
+                self._register_mapping(a)
+        if first + n > len(a):
+            return None
+        v = a[first:first + n]
+        if cshape is not None and list(v.shape) != list(cshape):
+            return None
+        return v
 
     # ------------------------------------------------------------------ send (chunk packing)
     def send_image_thread(self):
@@ -372,6 +457,20 @@ class client:  # noqa: N801 (reference class name)
             n, f = item
             if n == "flush":
                 flush()
+                continue
+            if n == "window":  # shared-source mode: only the chunk's index window leaves this volunteer
+                flush()
+                first, win = f
+                info = (f"{self.my_ip}||request||{'-'.join(map(str, range(first, first + win.n)))}"
+                        f"||{win.shape[1]}||{win.shape[2]}")
+                key = next(self._keys)
+                with self._p2p_lock:
+                    self._outgoing[key] = win
+                ok = self.sender.send_image(info, _EMPTY, p2p=1, key=key, cshape=list(win.shape), win=win.meta())
+                if not ok:
+                    self.log("uplink send failed")
+                self.metrics.incr("chunks_sent")
+                self.metrics.incr("window_chunks_sent")
                 continue
             if n == "chunk":  # a whole chunk from a chunked source: frames first..first+k-1
                 flush()
@@ -431,6 +530,8 @@ class client:  # noqa: N801 (reference class name)
         pageable 276 MB 720p chunk went through a staged copy); the result comes back through
         pinned memory too, or stays on the GPU for an RCCL pair plane."""
         dev = self.resize_device
+        self.metrics.incr("h2d_bytes", sum(int(f.nbytes) for f in frames) if isinstance(frames, list)
+                          else int(frames.nbytes))
         if self._rs_stream is None:
             self._rs_stream = torch.cuda.Stream(dev)
         x = None
@@ -519,6 +620,9 @@ class client:  # noqa: N801 (reference class name)
         elif cmd == "send":  # requester: chunk `key` -> worker `dst`
             with self._p2p_lock:
                 t = self._outgoing.get(int(hdr["key"]))
+            if isinstance(t, _Window):  # a worker could not read the window: send its frames after all
+                self.metrics.incr("window_fallback_sends")
+                t = _host_tensor(np.ascontiguousarray(t.read()))
             if t is None:
                 # a chunk this requester no longer holds (an earlier job's): the worker has posted
                 # the matching receive, so send a placeholder to keep the pair's FIFO in step; its
@@ -528,6 +632,17 @@ class client:  # noqa: N801 (reference class name)
             plane.send(int(hdr["dst"]), t, cid)
         elif cmd == "work":  # worker: receive the chunk, then infer it
             msg = hdr["msg"]
+            if hdr.get("win") is not None:  # shared-source mode: read the window from the file here
+                arr = self._read_window(hdr["win"], hdr.get("cshape"))
+                if arr is None:  # not readable here: the requester sends the frames instead
+                    self.metrics.incr("window_refused")
+                    self.sender.send_image(f"{msg.split('||')[0]}||failed", _EMPTY, p2p=1, chunk=cid, nowin=1)
+                    return
+                parts = msg.split("||")
+                nums = [int(x) for x in parts[2].split("-")] if parts[2] else []
+                self.metrics.incr("window_chunks")
+                self.work_q.put(({"chunk": cid, "p2p": 1, "win": 1}, arr, parts[0], nums))
+                return
 
             def got(buf, hdr=hdr, msg=msg):
                 if isinstance(buf, BaseException):
@@ -588,7 +703,8 @@ class client:  # noqa: N801 (reference class name)
         parts = msg.split("||")
         info = f"{self.my_ip}||request||{parts[2]}||{t.shape[1]}||{t.shape[2]}"
         self.metrics.incr("p2p_resubmitted")
-        self.sender.send_image(info, _EMPTY, p2p=1, key=int(key), cshape=list(t.shape))
+        extra = {"win": t.meta()} if isinstance(t, _Window) else {}
+        self.sender.send_image(info, _EMPTY, p2p=1, key=int(key), cshape=list(t.shape), **extra)
 
     # ------------------------------------------------------------------ worker role
     def worker(self):
@@ -629,7 +745,9 @@ class client:  # noqa: N801 (reference class name)
         groups = []
         for it in items:
             hdr, arr, _req, _nums = it
-            dev_res = bool(hdr.get("p2p")) and arr.device.type != "cpu"
+            dev_res = bool(hdr.get("p2p")) and isinstance(arr, torch.Tensor) and arr.device.type != "cpu"
+            if not dev_res and getattr(eng, "device", None) is not None and torch.device(eng.device).type == "cuda":
+                self.metrics.incr("h2d_bytes", int(arr.nbytes))  # this volunteer's own host -> GPU link
             if groups and groups[-1][0] == dev_res and tuple(groups[-1][1][-1][1].shape[1:]) == tuple(arr.shape[1:]):
                 groups[-1][1].append(it)
             else:
@@ -638,7 +756,14 @@ class client:  # noqa: N801 (reference class name)
         for dev_res, its in groups:
             t0 = time.perf_counter()
             with self.hspans.span("wk_submit"):
-                if len(its) > 1 and hasattr(eng, "submit_many"):
+                if not dev_res and all(h.get("win") for h, _a, _r, _n in its):
+                    # shared-source windows: page-locked mapping -> upload straight from it (under the
+                    # registration lock, so the mapping cannot be unregistered before the copy is enqueued)
+                    jobs = []
+                    for _h, a, r, _n in its:
+                        with self._reg_lock:
+                            jobs.append(eng.submit(a, r, pinned=self._registered_block(a)))
+                elif len(its) > 1 and hasattr(eng, "submit_many"):
                     pairs = [(a, r) for _h, a, r, _n in its]
                     jobs = eng.submit_tensor_many(pairs) if dev_res else eng.submit_many(pairs)
                 else:

@@ -155,29 +155,30 @@ void gemm_ps(at::Tensor a, at::Tensor b, at::Tensor c, c10::optional<at::Tensor>
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_ps: shape mismatch");
   TORCH_CHECK(vcx_gemm_ps_supported((int)M, (int)N, (int)K, (int)epi),
-              "gemm_ps: needs M, N % 256 == 0, K % 128 == 0, K >= 256, epilogue 0 (store), 1 (bias), 2 (bias+GELU) "
-              "or 4 (DGELU + bias grad), N <= 16384 with a bias");
+              "gemm_ps: needs M, N % 256 == 0, K % 128 == 0, K >= 256, epilogue 0 (store), 1 (bias), 2 (bias+GELU), "
+              "4 (DGELU + bias grad), 5 (bias+GELU, c = gelu'(pre)) or 6 (c = acc * c2 + bias grad), N <= 16384 with "
+              "a bias");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "gemm_ps: 16-B aligned rows");
   for (const at::Tensor* t : {&a, &b, &c})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_ps: 16-B aligned base pointers");
   // buffer resources cover one 256-row panel each: 32-bit byte offsets
   TORCH_CHECK(256 * std::max({a.stride(0), b.stride(0), c.stride(0)}) * 2 < (int64_t(1) << 31), "gemm_ps: rows too long");
   void* c2p = nullptr;
-  if (epi == 2 || epi == 4) {
+  if (epi == 2 || epi == 4 || epi == 5 || epi == 6) {
     TORCH_CHECK(c2 && c2->sizes() == c.sizes() && c2->strides() == c.strides() && c2->scalar_type() == at::kBFloat16,
-                "gemm_ps: epilogue 2/4 needs c2 like c");
+                "gemm_ps: epilogues 2/4/5/6 need c2 like c");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(c2->data_ptr()) % 16 == 0, "gemm_ps: 16-B aligned c2");
     c2p = c2->data_ptr();
   }
   const void* bp = nullptr;
-  if (epi == 1 || epi == 2) {
+  if (epi == 1 || epi == 2 || epi == 5) {
     TORCH_CHECK(bias && bias->numel() == N && bias->is_contiguous() && bias->scalar_type() == at::kBFloat16,
                 "gemm_ps: bias [N] bf16");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0, "gemm_ps: 16-B aligned bias");
     bp = bias->data_ptr();
   }
   float* cs = nullptr;
-  if (epi == 4) {
+  if (epi == 4 || epi == 6) {
     TORCH_CHECK(colsum && colsum->numel() == N && colsum->scalar_type() == at::kFloat && colsum->is_contiguous(),
                 "gemm_ps: colsum [N] fp32");
     cs = colsum->data_ptr<float>();

@@ -43,7 +43,16 @@ constexpr int RING = 4 * SLOT;          // 128 KB
 constexpr int BIAS_MAX = 16384;         // bias row resident in LDS behind the ring (32 KB)
 
 // (3 is not used: gemm_nt's code 3 is DGELU, so a caller reusing its numbering is refused)
-enum Epi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 4 };
+// EPI_BIAS_GELU_D (round 6): the fc forward writes gelu'(pre) to C instead of pre (and gelu(pre) to C2):
+// pre is read by nothing but the backward's gelu', so the forward, which already has sigmoid(2u) for gelu,
+// finishes gelu' in 4 more VALU ops per element, and the fc2 input gradient's epilogue (EPI_DMUL) is one
+// multiply instead of the ~16 VALU ops + 2 transcendentals of gelu'(pre) (EPI_DGELU ran at 29 % MFMA busy,
+// 473 vs 286 us for the same GEMM without an epilogue, profiles/r6_gpt2_step_pmc.txt).
+enum Epi { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_DGELU = 4, EPI_BIAS_GELU_D = 5, EPI_DMUL = 6 };
+template <int E>
+constexpr bool has_bias() { return E == EPI_BIAS || E == EPI_BIAS_GELU || E == EPI_BIAS_GELU_D; }
+template <int E>
+constexpr bool reads_c2() { return E == EPI_DGELU || E == EPI_DMUL; }
 
 __device__ __forceinline__ int swz(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
 
@@ -61,6 +70,15 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-u2));  // sigmoid(2u) = (1 + tanh u) / 2
   // d/dx [x sigmoid(2u)] = s + x s (1 - s) 2u',  2u' = sqrt(8/pi) (1 + 3 * 0.044715 x^2)
   return fmaf(x * sg * (1.f - sg), 1.5957691216057308f * fmaf(0.134145f, x2, 1.f), sg);
+}
+
+// gelu(x) and gelu'(x) sharing sigmoid(2u), u = sqrt(2/pi) (x + 0.044715 x^3)
+__device__ __forceinline__ void gelu_and_grad(float x, float& act, float& grad) {
+  const float x2 = x * x;
+  const float u2 = x * fmaf(1.5957691216057308f * 0.044715f, x2, 1.5957691216057308f);
+  const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-u2));
+  act = x * sg;
+  grad = fmaf(act * (1.f - sg), fmaf(1.5957691216057308f * 0.134145f, x2, 1.5957691216057308f), sg);
 }
 
 __device__ __forceinline__ float gelu_tanh(float x) {
@@ -115,7 +133,7 @@ __global__ void __launch_bounds__(512, 1)
   const int G = gridDim.x, bid = blockIdx.x;
   const int nk = K / BKS;  // multiple of 4, >= 8 (host check)
 
-  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {  // the bias row, once per workgroup
+  if constexpr (has_bias<EPI>()) {  // the bias row, once per workgroup
     bf16* bl = (bf16*)(smem + RINGB);
     for (int c = tid * 8; c < N; c += Gm::NTH * 8) *(bf16x8*)(bl + c) = *(const bf16x8*)(bias + c);
     __syncthreads();
@@ -300,9 +318,9 @@ __global__ void __launch_bounds__(512, 1)
     __builtin_amdgcn_sched_barrier(0);
     const u32x4 rc = desc_of(C + (int64_t)m0 * ldc + n0, BM * ldc * 2);
     u32x4 rc2;
-    if constexpr (EPI == EPI_BIAS_GELU) rc2 = desc_of(C2 + (int64_t)m0 * ldc + n0, BM * ldc * 2);
+    if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_D) rc2 = desc_of(C2 + (int64_t)m0 * ldc + n0, BM * ldc * 2);
     float bv[2][8];
-    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+    if constexpr (has_bias<EPI>()) {
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
         const bf16x8 b8 = *(const bf16x8*)(bl + n0 + ccol + 32 * jp);
@@ -329,7 +347,7 @@ __global__ void __launch_bounds__(512, 1)
         acc[i][2 * jp + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
         bf16x8 h;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) h[e] = (bf16)(EPI == EPI_BIAS || EPI == EPI_BIAS_GELU ? o[e] + bv[jp][e] : o[e]);
+        for (int e = 0; e < 8; ++e) h[e] = (bf16)(has_bias<EPI>() ? o[e] + bv[jp][e] : o[e]);
         v[jp] = __builtin_bit_cast(u32x4, h);
       }
       // rows r and r ^ 8 of the 16-row block trade halves (DPP row_ror:8): lanes of rows 0..7 keep
@@ -343,6 +361,42 @@ __global__ void __launch_bounds__(512, 1)
           v[1][d] = y;
         else
           v[0][d] = y;
+      }
+      if constexpr (EPI == EPI_DMUL) {  // v = dY W (the gradient w.r.t. gelu(pre)), gelu'(pre) from registers
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const bf16x8 g8 = __builtin_bit_cast(bf16x8, v[q]), p8 = __builtin_bit_cast(bf16x8, pre[i][q]);
+          bf16x8 o8;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = (float)g8[e] * (float)p8[e];
+            cs[e] += d;
+            o8[e] = (bf16)d;
+          }
+          v[q] = __builtin_bit_cast(u32x4, o8);
+        }
+      }
+      if constexpr (EPI == EPI_BIAS_GELU_D) {  // v = pre (bf16): C gets gelu'(pre), C2 gelu(pre)
+        u32x4 av[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const bf16x8 p8 = __builtin_bit_cast(bf16x8, v[q]);
+          bf16x8 a8, g8;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float a, g;
+            gelu_and_grad((float)p8[e], a, g);
+            a8[e] = (bf16)a;
+            g8[e] = (bf16)g;
+          }
+          v[q] = __builtin_bit_cast(u32x4, g8);
+          av[q] = __builtin_bit_cast(u32x4, a8);
+        }
+        store16(v[0], rc, c_offA, soff);
+        store16(v[1], rc, c_offA + 8 * ldc * 2, soff);
+        store16(av[0], rc2, c_offA, soff);
+        store16(av[1], rc2, c_offA + 8 * ldc * 2, soff);
+        continue;
       }
       if constexpr (EPI == EPI_DGELU) {  // v = dY W (the gradient w.r.t. gelu(pre)), pre from registers
 #pragma unroll
@@ -371,7 +425,7 @@ __global__ void __launch_bounds__(512, 1)
         }
       }
     }
-    if constexpr (EPI == EPI_DGELU) {
+    if constexpr (reads_c2<EPI>()) {
       // bias gradient: the 8 lanes of rows 0..7 (lane bits 0..2) share the same 8 columns
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -426,7 +480,7 @@ __global__ void __launch_bounds__(512, 1)
     step(s, f0, f1, na, nb, 0, false, Tt{}, VM{}, Tt{});
     step(s + 1, f1, f0, na, nb, 1, false, Tt{}, VM{}, Tt{});
     step(s + 2, f0, f1, na, nb, 2, false, Tt{}, VM{}, Tt{});
-    if constexpr (EPI == EPI_DGELU) {
+    if constexpr (reads_c2<EPI>()) {
       load_pre(m0, n0);  // lands behind the last step's MFMAs; its fragments are not read there
       // the 16 pre loads are younger loads than the awaited slice (loads retire in order)
       step(s + 3, f1, f0, na, nb, 3, false, Ff{}, std::integral_constant<int, 24>{}, Tt{});
@@ -454,9 +508,10 @@ using namespace vcx;
 
 bool vcx_gemm_ps_supported(int M, int N, int K, int epi) {
   using namespace gemm_ps;
-  const bool known = epi == EPI_STORE || epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_DGELU;
-  return M > 0 && N > 0 && M % BM == 0 && N % BN == 0 && K % 128 == 0 && K >= 256 && known &&
-         ((epi != EPI_BIAS && epi != EPI_BIAS_GELU) || N <= BIAS_MAX);
+  const bool known = epi == EPI_STORE || epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_DGELU ||
+                     epi == EPI_BIAS_GELU_D || epi == EPI_DMUL;
+  const bool bias = epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_GELU_D;
+  return M > 0 && N > 0 && M % BM == 0 && N % BN == 0 && K % 128 == 0 && K >= 256 && known && (!bias || N <= BIAS_MAX);
 }
 
 int vcx_gemm_ps_grid(int M, int N, int grid_cap) {
@@ -477,14 +532,16 @@ void vcx_gemm_ps(const void* A, const void* B, void* C, void* C2, const void* bi
   using namespace gemm_ps;
   static const bool attrs = [] {
     for (const void* k : {(const void*)gemm_ps_kernel<EPI_STORE>, (const void*)gemm_ps_kernel<EPI_BIAS>,
-                          (const void*)gemm_ps_kernel<EPI_BIAS_GELU>, (const void*)gemm_ps_kernel<EPI_DGELU>})
+                          (const void*)gemm_ps_kernel<EPI_BIAS_GELU>, (const void*)gemm_ps_kernel<EPI_DGELU>,
+                          (const void*)gemm_ps_kernel<EPI_BIAS_GELU_D>, (const void*)gemm_ps_kernel<EPI_DMUL>})
       (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, RING + 2 * BIAS_MAX);
     return true;
   }();
   (void)attrs;
   const int tilesN = N / BN, tiles = (M / BM) * tilesN;
   const int grid = vcx_gemm_ps_grid(M, N, grid_cap);
-  const int lds = Geo::RINGB + (epi == EPI_BIAS || epi == EPI_BIAS_GELU ? (N * 2 + 15) & ~15 : 0);
+  const int lds =
+      Geo::RINGB + (epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_GELU_D ? (N * 2 + 15) & ~15 : 0);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, (const bf16*)A, (const bf16*)B, (bf16*)C, (bf16*)C2,
                        (const bf16*)bias, colsum, M, N, K, lda, ldb, ldc, tilesN, tiles);
@@ -493,6 +550,8 @@ void vcx_gemm_ps(const void* A, const void* B, void* C, void* C2, const void* bi
     case EPI_STORE: go(gemm_ps_kernel<EPI_STORE>); break;
     case EPI_BIAS: go(gemm_ps_kernel<EPI_BIAS>); break;
     case EPI_BIAS_GELU: go(gemm_ps_kernel<EPI_BIAS_GELU>); break;
+    case EPI_BIAS_GELU_D: go(gemm_ps_kernel<EPI_BIAS_GELU_D>); break;
+    case EPI_DMUL: go(gemm_ps_kernel<EPI_DMUL>); break;
     default: go(gemm_ps_kernel<EPI_DGELU>); break;
   }
 }

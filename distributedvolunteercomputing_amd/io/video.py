@@ -186,6 +186,7 @@ class NpySource(FrameSource):
     chunked = True
 
     def __init__(self, path, total: int | None = None):
+        self.path = str(path)
         self.a = np.load(path, mmap_mode="r", allow_pickle=False)
         if self.a.ndim != 4 or self.a.shape[-1] != 3 or self.a.dtype != np.uint8:
             raise ValueError(f"{path}: expected uint8 [N,H,W,3], got {self.a.dtype} {self.a.shape}")

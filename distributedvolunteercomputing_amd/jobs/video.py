@@ -37,9 +37,10 @@ class Engine:
         out, _ = self.process(frames.cpu().numpy(), requester)
         return torch.from_numpy(np.ascontiguousarray(out)).to(frames.device)
 
-    def submit(self, frames, requester):
+    def submit(self, frames, requester, pinned: bool = False):
         """Start a chunk; the returned job's ``result()`` gives ``process``'s return value.
-        Engines without an asynchronous pipeline compute here."""
+        Engines without an asynchronous pipeline compute here. ``pinned``: the host frames lie in
+        page-locked memory (a registered source mapping) and may be uploaded from where they are."""
         res = self.process(frames, requester)
         job = EngineJob(self, None, None, None, None)
         job.result = lambda: res
@@ -136,8 +137,10 @@ class DetectorEngine(Engine):
         self.tracer = NULL_TRACER  # set a utils.trace.SpanTracer for per-stage device times
 
     @torch.no_grad()
-    def submit(self, frames, requester) -> "EngineJob":
-        """Start a chunk ([n, H, W, 3] uint8 numpy or host tensor); returns an EngineJob."""
+    def submit(self, frames, requester, pinned: bool = False) -> "EngineJob":
+        """Start a chunk ([n, H, W, 3] uint8 numpy or host tensor); returns an EngineJob. ``pinned``:
+        contiguous numpy frames in page-locked memory (a hipHostRegister'ed source mapping of a shared-source
+        worker) are uploaded straight from there instead of through the pinned staging slot."""
         if self.stream is None:
             out, counts = self._run(frames, requester)
             res = (out.cpu().numpy(), counts.cpu().tolist())
@@ -151,7 +154,14 @@ class DetectorEngine(Engine):
                 slot.h2d_done.synchronize()  # this slot's previous upload finished
             if slot.out_done is not None:
                 slot.out_done.synchronize()  # ... and its previous output was read back
-            if isinstance(frames, torch.Tensor) and frames.is_contiguous() and frames.is_pinned():
+            if pinned and isinstance(frames, np.ndarray) and frames.flags.c_contiguous:
+                import warnings
+
+                with warnings.catch_warnings():  # a read-only mapping: only ever read by the upload
+                    warnings.simplefilter("ignore", UserWarning)
+                    src = torch.from_numpy(frames)
+                slot.src_ref = src
+            elif isinstance(frames, torch.Tensor) and frames.is_contiguous() and frames.is_pinned():
                 # already page-locked (a pinned pair-plane receive): uploaded from where it lies; the slot
                 # holds the reference until the upload is known to be done
                 src = frames

@@ -470,7 +470,9 @@ class _MlpGelu(torch.autograd.Function):
         pre = torch.empty(M, F_, device=x.device, dtype=x.dtype)
         act = torch.empty_like(pre)
         if ps:
-            C.gemm_ps(x2, w1, pre, act, b1, None, 2)
+            # `pre` holds gelu'(pre) (epilogue 5): the backward needs pre only for gelu', and the forward
+            # already has sigmoid(2u) (VCX_MLP_GRAD_FWD=0: store pre, gelu' in the backward's epilogue 4)
+            C.gemm_ps(x2, w1, pre, act, b1, None, 5 if config.get().mlp_grad_fwd else 2)
             y = mm(act, w2, trans_b=True)
         else:
             C.gemm_nt(x2, w1, pre, act, b1, None, 2)
@@ -478,6 +480,7 @@ class _MlpGelu(torch.autograd.Function):
         ctx.save_for_backward(x2, w1, b1, w2, pre, act)
         ctx.xshape = x.shape
         ctx.ps = ps
+        ctx.grad_fwd = bool(ps and config.get().mlp_grad_fwd)
         return y.view(*x.shape[:-1], w2.shape[0])
 
     @staticmethod
@@ -489,7 +492,7 @@ class _MlpGelu(torch.autograd.Function):
         cs = torch.zeros(F_, device=dy.device, dtype=torch.float32)
         dpre = torch.empty_like(pre)
         if ctx.ps:
-            C.gemm_ps(dy2, transpose_weight(w2), dpre, pre, None, cs, 4)
+            C.gemm_ps(dy2, transpose_weight(w2), dpre, pre, None, cs, 6 if ctx.grad_fwd else 4)
         else:
             C.gemm_nt(dy2, transpose_weight(w2), dpre, pre, None, cs, 3)
         dw2, _ = _param_grads(dy2, act, w2, None, ctx.needs_input_grad[3], False)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Per-kernel trace of the GPT-2-small bench step on the default tree (eager: every kernel its own dispatch),
+# summarised by scripts/prof_summary.py into gpurun_out/$OUT/step.txt (OUT defaults to profstep1).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O="$R/gpurun_out/${OUT:-profstep1}"
+mkdir -p "$O"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/trace" -o run -- \
+    python3 "$R/bench.py" --steps 3 --warmup 2 --graph 0 > "$O/step.log" 2>&1 || exit $?
+f=$(find "$O/trace" -name "*kernel_trace.csv" | head -1)
+python3 "$R/scripts/prof_summary.py" "$f" > "$O/step.txt" || exit $?
+rm -rf "$O/trace"

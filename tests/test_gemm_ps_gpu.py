@@ -42,6 +42,25 @@ def test_gemm_ps_matches_fp32(gpu, M, N, K, cap):
     assert (c.float() - x.grad).abs().max().item() < 2e-2 * x.grad.abs().max().item()
     s = x.grad.sum(0)
     assert (cs - s).abs().max().item() < 1e-2 * s.abs().max().item() + 1e-2
+    # round 6 pair: epilogue 5 (c = gelu'(pre), c2 = gelu(pre), pre = a b^T + bias) and epilogue 6
+    # (c = (a b^T) * c2 with fp32 column sums): the fused MLP's forward and fc2 input gradient
+    gp = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+    act = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+    C.gemm_ps(a, b, gp, act, bias, None, 5, cap)
+    torch.cuda.synchronize()
+    pre32 = (ref + bias.float()).to(torch.bfloat16).float().requires_grad_()  # the kernel rounds pre to bf16
+    g = F.gelu(pre32, approximate="tanh")
+    assert (act.float() - g.detach()).abs().max().item() < 3e-2 * g.abs().max().item()
+    g.backward(torch.ones_like(g))
+    assert (gp.float() - pre32.grad).abs().max().item() < 1e-2  # gelu' lies in [-0.17, 1.13]
+    c = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+    cs = torch.zeros(N, device=dev, dtype=torch.float32)
+    C.gemm_ps(a, b, c, gp, None, cs, 6, cap)
+    torch.cuda.synchronize()
+    want = ref.to(torch.bfloat16).float() * pre32.grad
+    assert (c.float() - want).abs().max().item() < 2e-2 * want.abs().max().item()
+    s = want.sum(0)
+    assert (cs - s).abs().max().item() < 1e-2 * s.abs().max().item() + 1e-2
 
 
 def test_gemm_ps_strided_rows_and_refusals(gpu):
@@ -65,13 +84,15 @@ def test_gemm_ps_strided_rows_and_refusals(gpu):
 
 
 def test_gemm_ps_refuses_unknown_epilogues(gpu):
-    """Only the four real epilogues are accepted: 3 (gemm_nt's DGELU code) and the removed
-    no-store diagnostic 7 are refused."""
+    """Only the real epilogues are accepted: 3 (gemm_nt's DGELU code) and the removed no-store
+    diagnostic 7 are refused (5 and 6 are the round-6 gelu'-in-the-forward pair)."""
     from distributedvolunteercomputing_amd.ops import native
 
     C = native()
-    for epi in (3, 5, 6, 7):
+    for epi in (3, 7, 8):
         assert not C.gemm_ps_supported(512, 256, 768, epi)
+    for epi in (5, 6):
+        assert C.gemm_ps_supported(512, 256, 768, epi)
     a = torch.randn(512, 768, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(256, 768, device="cuda", dtype=torch.bfloat16)
     c = torch.empty(512, 256, device="cuda", dtype=torch.bfloat16)

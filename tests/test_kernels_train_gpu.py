@@ -386,3 +386,29 @@ def test_transpose_bf16(gpu, R, Cc):
     w = torch.randn(R, Cc, device=gpu).to(torch.bfloat16)
     t = ops.native().transpose_bf16(w)
     assert torch.equal(t, w.t().contiguous())
+
+
+@pytest.mark.parametrize("grad_fwd", [True, False])
+def test_mlp_gelu_persistent_matches_unfused(gpu, grad_fwd):
+    """ops.mlp_gelu on gemm_ps (the default fused MLP) vs the library + bias_gelu path, with gelu'(pre)
+    stored by the forward (epilogues 5 / 6, the round-6 default) and with pre stored (epilogues 2 / 4);
+    gradients of every input compared as a whole."""
+    from distributedvolunteercomputing_amd import config
+
+    torch.manual_seed(1)
+    x = _bf(torch.randn(1024, 768, device=gpu))
+    w1 = _bf(torch.randn(3072, 768, device=gpu) * 0.02).requires_grad_()
+    b1 = _bf(torch.randn(3072, device=gpu) * 0.02).requires_grad_()
+    w2 = _bf(torch.randn(768, 3072, device=gpu) * 0.02).requires_grad_()
+    dy = _bf(torch.randn(1024, 768, device=gpu))
+    outs = {}
+    for mode in ("lib", "fused"):
+        with config.override(mlp=mode, mlp_grad_fwd=grad_fwd):
+            xi = x.clone().requires_grad_()
+            for p in (w1, b1, w2):
+                p.grad = None
+            y = ops.mlp_gelu(xi, w1, b1, w2)
+            y.backward(dy)
+            outs[mode] = [t.float().clone() for t in (y, xi.grad, w1.grad, b1.grad, w2.grad)]
+    for a, b in zip(outs["lib"], outs["fused"]):
+        assert (a - b).norm() / b.norm() < 2e-2

@@ -47,3 +47,35 @@ def test_video_cli_three_processes_exit_cleanly(tmp_path):
     errs = "".join((tmp_path / f"rank{i}.err").read_text()[-1500:] for i in range(3))
     assert r.returncode == 0, r.stderr + errs
     assert "terminate called" not in errs
+
+
+def _rank_npy(rank, world, port, out_dir, ctrl_port, src):
+    import os
+
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1")
+    from distributedvolunteercomputing_amd.control.node_job import run_node_job
+    from distributedvolunteercomputing_amd.jobs.video import PassthroughEngine
+
+    st = run_node_job(src, out_dir, engine_factory=PassthroughEngine, chunk=50, control_port=ctrl_port,
+                      store_port=port, lease_s=5.0, out_ext=".npy", preresize=False)
+    return st
+
+
+def test_node_job_npy_source_is_read_by_the_workers(tmp_path):
+    """VERDICT r5 next #4 (8-GPU-shaped ingest): with an .npy source, node_job puts every volunteer in
+    shared-source mode; the requester (rank 0) sends index windows only, each worker reads its chunks
+    from the file, and the output is complete and in order."""
+    from distributedvolunteercomputing_amd.io.video import decode_frame_index, synthetic_frame
+
+    src = tmp_path / "src" / "in.npy"
+    src.parent.mkdir()
+    np.save(src, np.stack([synthetic_frame(i, 64, 48) for i in range(230)]))
+    out = tmp_path / "out"
+    out.mkdir()
+    res = _mp.run(_rank_npy, 3, str(out), _mp.free_port(), str(src), timeout=180)
+    st = res[0]
+    assert st["frames"] == 230 and st["chunks"] == 5
+    assert st["requester"].get("window_chunks_sent") == 5 and st["requester"].get("h2d_bytes", 0) == 0
+    assert st["coordinator"].get("window_dispatched") == 5 and not st["coordinator"].get("window_fallbacks")
+    frames = np.load(st["out"])
+    assert [decode_frame_index(f) for f in frames] == list(range(230))

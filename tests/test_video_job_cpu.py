@@ -321,3 +321,88 @@ def test_failed_output_writes_fail_the_job(coord, tmp_path, monkeypatch):
     finally:
         for c in (req, w):
             c.exit_threads()
+
+
+def _p2p_coord():
+    return coordinator("127.0.0.1", 0, ephemeral_ports=True, lease_s=2.0, data_plane="p2p")
+
+
+def test_shared_source_windows_leave_the_requester_without_frames(tmp_path):
+    """with the source under the shared root, the requester sends only index windows;
+    each worker reads its chunks' frames from the file itself. Three volunteers; the requester reads and
+    moves no frame byte, the output is complete and in order. Reference: every chunk went through the
+    requester and the coordinator (/root/reference/worker.py:131-159, server.py:84-90)."""
+    from distributedvolunteercomputing_amd import config
+    from distributedvolunteercomputing_amd.io.video import synthetic_frame
+
+    src = tmp_path / "shared" / "in.npy"
+    src.parent.mkdir()
+    np.save(src, np.stack([synthetic_frame(i, 64, 48) for i in range(230)]))
+    c = _p2p_coord()
+    req = _client(c, tmp_path, PassthroughEngine())
+    w1 = _client(c, tmp_path, PassthroughEngine())
+    w2 = _client(c, tmp_path, PassthroughEngine(delay_s=0.02))
+    try:
+        with config.override(shared_source_root=str(src.parent)):
+            req.preresize = False
+            req.become_requester(str(src))
+            assert req.wait_job(timeout=60) is not None
+        out = np.load(req.path_out)
+        assert [decode_frame_index(f) for f in out] == list(range(230))
+        rc = req.metrics.counters
+        assert rc.get("window_chunks_sent", 0) == 3 and rc.get("chunks_returned", 0) == 3
+        assert rc.get("h2d_bytes", 0) == 0 and rc.get("window_fallback_sends", 0) == 0
+        assert c.metrics.counters.get("window_dispatched", 0) == 3
+        assert sum(w.metrics.counters.get("window_chunks", 0) for w in (w1, w2)) == 3
+        assert sum(w.metrics.counters.get("frames_processed", 0) for w in (w1, w2)) == 230
+        assert not req._outgoing  # every window released once its result was in
+    finally:
+        for v in (req, w1, w2):
+            v.exit_threads()
+        c.exit_threads()
+
+
+def test_worker_that_cannot_read_the_window_gets_the_frames_from_the_requester(tmp_path):
+    """A worker outside the shared root (or without the file) refuses the window; the coordinator turns
+    that chunk into an ordinary pair transfer and the requester reads and sends its frames."""
+    from distributedvolunteercomputing_amd import config
+    from distributedvolunteercomputing_amd.io.video import synthetic_frame
+
+    src = tmp_path / "shared" / "in.npy"
+    src.parent.mkdir()
+    np.save(src, np.stack([synthetic_frame(i, 32, 24) for i in range(200)]))
+    c = _p2p_coord()
+    req = _client(c, tmp_path, PassthroughEngine(), chunk=40)
+    w = _client(c, tmp_path, PassthroughEngine(), chunk=40)
+    w._read_window = lambda *a, **k: None  # this worker cannot see the file
+    try:
+        with config.override(shared_source_root=str(src.parent)):
+            req.preresize = False
+            req.become_requester(str(src))
+            assert req.wait_job(timeout=60) is not None
+        out = np.load(req.path_out)
+        assert [decode_frame_index(f) for f in out] == list(range(200))
+        assert w.metrics.counters.get("window_refused", 0) == 5
+        assert req.metrics.counters.get("window_fallback_sends", 0) == 5
+        assert c.metrics.counters.get("window_fallbacks", 0) == 5
+    finally:
+        req.exit_threads()
+        w.exit_threads()
+        c.exit_threads()
+
+
+def test_window_outside_the_shared_root_is_refused(tmp_path):
+    from distributedvolunteercomputing_amd import config
+    from distributedvolunteercomputing_amd.control.peer import _shared_path
+
+    inside = tmp_path / "root" / "a.npy"
+    inside.parent.mkdir()
+    np.save(inside, np.zeros((2, 4, 4, 3), np.uint8))
+    outside = tmp_path / "b.npy"
+    np.save(outside, np.zeros((2, 4, 4, 3), np.uint8))
+    with config.override(shared_source_root=str(inside.parent)):
+        assert _shared_path(str(inside)) == str(inside.resolve())
+        assert _shared_path(str(outside)) is None
+        assert _shared_path(str(inside.parent / ".." / "b.npy")) is None  # no escape through ..
+    with config.override(shared_source_root=""):
+        assert _shared_path(str(inside)) is None  # off unless a root is configured
