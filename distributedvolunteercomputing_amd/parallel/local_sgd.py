@@ -201,6 +201,7 @@ class LocalSGDTrainer:
                     ad = self.admit_split or {}
                     self.last_round_stages = {
                         "sync_round_ms": round((t1 - t0) * 1e3, 3),
+                        "peer_wait_ms": round(ad.get("peer_wait_ms", 0.0), 3),
                         "comm_init_ms": round(ad.get("comm_init_ms", 0.0), 3),
                         "broadcast_ms": round(ad.get("broadcast_ms", 0.0), 3),
                         "reduce_ms": round((t4 - t3) * 1e3, 3),
@@ -274,6 +275,12 @@ class LocalSGDTrainer:
                              + ([self.buffers.as_fp32().to(bdev)] if nb else []))
         else:
             pack = torch.empty(n, dtype=torch.float32, device=bdev)
+        # every member of the new group checks in at the rendezvous store first, so the communicator
+        # set-up below is timed from the moment the LAST rank arrived: a member that enters the admission
+        # round while a joiner is still starting up waits here (peer_wait_ms), not inside the init
+        # (the members' 2.56 s vs the joiners' 1.34 s of "communicator init")
+        tw = time.perf_counter()
+        self._admission_checkin(g)
         # a one-element collective first: its time is the new group's communicator set-up (RCCL builds
         # its communicator lazily, at the first collective) plus one latency, so the broadcast time
         # below is the model transfer alone
@@ -284,8 +291,23 @@ class LocalSGDTrainer:
         g.broadcast_(pack, root)
         self._dev_sync()
         t2 = time.perf_counter()
-        self.admit_split = {"comm_init_ms": (t1 - t0) * 1e3, "broadcast_ms": (t2 - t1) * 1e3, "bytes": int(n * 4)}
+        self.admit_split = {"peer_wait_ms": (t0 - tw) * 1e3, "comm_init_ms": (t1 - t0) * 1e3,
+                            "broadcast_ms": (t2 - t1) * 1e3, "bytes": int(n * 4)}
         return pack if members[g.rank] in newcomers else None
+
+    def _admission_checkin(self, g):
+        """Store barrier of the admission round's group (elastic runs only): add one to the generation's
+        check-in counter and wait until every member has; a trip of the watchdog (a member died) ends
+        the wait as a PeerFailure like any guarded collective."""
+        mem = self.membership
+        if mem is None or g.size <= 1:
+            return
+        key = f"vcx/el/admit_in/{mem.gen}"
+        mem.store.add(key, 1)
+        while int(mem.store.add(key, 0)) < g.size:
+            if mem.tripped():
+                raise PeerFailure(f"gen {mem.gen}: aborted during the admission check-in ({mem.abort_reason()})")
+            time.sleep(0.001)
 
     def _dev_sync(self):
         if self.anchor.is_cuda:
@@ -339,7 +361,7 @@ class LocalSGDTrainer:
                 t5 = time.perf_counter()
                 ad = self.admit_split or {}
                 st = {"connect_ms": (t1 - t0) * 1e3, "wait_round_ms": (t2 - t1) * 1e3,
-                      "comm_init_ms": ad.get("comm_init_ms", 0.0), "broadcast_ms": ad.get("broadcast_ms", (t3 - t2) * 1e3),
+                      "peer_wait_ms": ad.get("peer_wait_ms", 0.0), "comm_init_ms": ad.get("comm_init_ms", 0.0), "broadcast_ms": ad.get("broadcast_ms", (t3 - t2) * 1e3),
                       "reduce_ms": (t4 - t3) * 1e3,
                       "verdict_apply_ms": (t5 - t4) * 1e3, "admission_round_ms": (t5 - t2) * 1e3,
                       "broadcast_bytes": ad.get("bytes", int(self.anchor.numel() * 4 * (2 if self.outer_mom is not None else 1)))}

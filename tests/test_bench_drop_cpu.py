@@ -78,6 +78,7 @@ def test_bench_drop_kill_two_then_rejoin(tmp_path):
     # running members' side of the admission round has its own anatomy
     for st in rec["joiner_admission_stages"]:
         assert st["comm_init_ms"] >= 0 and st["broadcast_ms"] >= 0 and st["broadcast_bytes"] > 0, st
+        assert st["peer_wait_ms"] >= 0, st  # waiting for the other ranks, apart from the init
     ms = rec["rejoin_member_stages_ms"]
-    assert ms is not None and {"sync_round_ms", "comm_init_ms", "broadcast_ms", "reduce_ms",
+    assert ms is not None and {"sync_round_ms", "peer_wait_ms", "comm_init_ms", "broadcast_ms", "reduce_ms",
                                "guard_verdict_apply_ms"} <= set(ms), ms
