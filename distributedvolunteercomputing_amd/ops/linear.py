@@ -166,14 +166,16 @@ def gemm_wg_ok(M: int, N: int, K: int, t) -> bool:
     """The hand-written weight-gradient GEMM (csrc/kernels/gemm_wg.hip) takes dW[N, K] from M tokens: the
     default (config.gemm_wgrad == "vcx") wherever the output is a few dozen 256 x 256 tiles that need the
     token split -- 1.17-1.23 PF/s at the GPT-2 shapes against the library's 0.81-0.98
-    (profiles/r5_gemm_wg.txt). Outputs of more than 128 tiles fill the GPU without a split: Llama-3-8B's
-    projections stay on the library; the GPT-2 LM heads ([50304, 768 | 1024], K <= 1024) take gemm_wg with
-    1..4 splits (config.wgrad_wide)."""
+    (profiles/r5_gemm_wg.txt). An output of one round of tiles (129..256) runs unsplit: Llama-3-8B's q / o
+    projections ([4096, 4096] from 4096 tokens) 129.7 vs 146.5 us on the library; its k / v (4 splits) and
+    gate / up / down (896 tiles) lost 5-11 % and stay on the library (profiles/r6_llama_wgrad.txt). The GPT-2
+    LM heads ([50304, 768 | 1024], K <= 1024) take gemm_wg with 1..4 splits (config.wgrad_wide)."""
     cfg = config.get()
     tiles = ((N + 255) // 256) * (K // 256)
     wide = cfg.wgrad_wide and K <= 1024 and M >= 32768 and tiles > 128
+    one_round = 128 < tiles <= 256 and M >= 4096
     return (cfg.gemm_wgrad == "vcx" and use_native(t) and t.dtype == torch.bfloat16
-            and (tiles <= 128 or wide) and (N % 256 == 0 or wide or cfg.wgrad_ragged)
+            and (tiles <= 128 or one_round or wide) and (N % 256 == 0 or wide or cfg.wgrad_ragged)
             and bool(native().gemm_wg_supported(N, K, M)))
 
 
