@@ -38,6 +38,9 @@ class RuntimeConfig:
     # VCX_MLP_GRAD_FWD: the fused fc forward stores gelu'(pre) instead of pre, so the fc2 input gradient's
     # epilogue is one multiply (gemm_ps epilogues 5 / 6) instead of gelu'(pre) per element (4)
     mlp_grad_fwd: bool = True
+    # VCX_GEMM_FWD: forward GEMMs x W^T (+ b) and input gradients dY W of the linear layers on "lib" or "vcx"
+    # (csrc/kernels/gemm_f.hip, opt-in: 0.85-0.93x the library at the GPT-2 shapes, profiles/r6_gemm_f.txt)
+    gemm_fwd: str = "lib"
     dgrad_ps: bool = True  # VCX_DGRAD_PS: input gradients dX = dY W with K <= 2304 on gemm_ps (measured faster)
     gemm_wgrad: str = "vcx"  # VCX_GEMM_WGRAD: weight gradients on "vcx" (gemm_wg, hand-written) or "lib" (split-M batched GEMM)
     # VCX_WGRAD_WIDE: also outputs of more than 128 256x256 tiles with <= 1024 input columns on gemm_wg (the
@@ -124,6 +127,7 @@ _ENV = {
     "bn_layer_ws": ("VCX_BN_LAYER_WS", _bool),
     "conv_find": ("VCX_CONV_FIND", _bool),
     "gemm_wgrad": ("VCX_GEMM_WGRAD", str),
+    "gemm_fwd": ("VCX_GEMM_FWD", str),
     "wgrad_wide": ("VCX_WGRAD_WIDE", _bool),
     "wgrad_ragged": ("VCX_WGRAD_RAGGED", _bool),
     "gemm_select": ("VCX_GEMM_SELECT", _bool),
@@ -149,7 +153,7 @@ _ENV = {
     "trace_dir": ("VCX_TRACE_DIR", str),
     "metrics_dir": ("VCX_METRICS_DIR", str),
 }
-_CHOICES = {"narrow_gemm": ("lib", "vision"), "conv3x3_wgrad": ("lib", "vcx"), "gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "off"),
+_CHOICES = {"narrow_gemm": ("lib", "vision"), "conv3x3_wgrad": ("lib", "vcx"), "gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "gemm_fwd": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "off"),
             "uplink_pipeline": ("relay", "all", "off")}
 
 _lock = threading.Lock()

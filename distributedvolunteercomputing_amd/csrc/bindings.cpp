@@ -370,6 +370,31 @@ void gemm_wg(at::Tensor a, at::Tensor b, at::Tensor out, bool accumulate, int64_
               (int)a.stride(0), (int)b.stride(0), (int)splits, accumulate ? 1 : 0, (int)loaders, cur_stream());
 }
 
+// out[M, N] = a[M, K] . b[N, K]^T (+ bias[N]) on gemm_f (csrc/kernels/gemm_f.hip): 256 x 256 tiles, 4 waves of 128 x 128
+bool gemm_f_supported(int64_t M, int64_t N, int64_t K) { return vcx_gemm_f_supported((int)M, (int)N, (int)K); }
+
+void gemm_f(at::Tensor a, at::Tensor b, at::Tensor out, c10::optional<at::Tensor> bias, int64_t waves) {
+  TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_f: 2-D cuda tensors");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
+              "gemm_f: bf16 operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.stride(1) == 1, "gemm_f: row-major operands");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm_f: shape mismatch");
+  TORCH_CHECK(vcx_gemm_f_supported((int)M, (int)N, (int)K), "gemm_f: needs N % 128 == 0, K % 64 == 0, K >= 192");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "gemm_f: 16-B aligned rows");
+  for (const at::Tensor* t : {&a, &b, &out})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_f: 16-B aligned base pointers");
+  TORCH_CHECK(a.get_device() == b.get_device() && a.get_device() == out.get_device(), "gemm_f: one device");
+  const bool hb = bias && bias->defined();
+  if (hb)
+    TORCH_CHECK(bias->is_cuda() && bias->get_device() == a.get_device() && bias->numel() == N && bias->is_contiguous() &&
+                    bias->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0,
+                "gemm_f: bias bf16 [N], contiguous, 8-B aligned");
+  TORCH_CHECK(256 * std::max(a.stride(0), b.stride(0)) * 2 < (int64_t(1) << 31), "gemm_f: tile panels under 2 GB");
+  vcx_gemm_f(a.data_ptr(), b.data_ptr(), out.data_ptr(), hb ? bias->data_ptr() : nullptr, (int)M, (int)N, (int)K, (int)a.stride(0), (int)b.stride(0),
+             (int)out.stride(0), (int)waves, cur_stream());
+}
+
 // 3x3 convolution (pad 1, stride 1|2) weight gradient on gemm_wg with the patch matrix of x gathered while
 // staging: out [Cout, 9 Cin] (+)= dY^T P(x) -- the [Cout][ky][kx][Cin] (channels-last) weight layout.
 // dy: NHWC [imgs, Ho, Wo, Cout], x: NHWC [imgs, H, W, Cin], both contiguous bf16
@@ -873,6 +898,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("layer_ws") = py::none());
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0);
+  m.def("gemm_f_supported", &gemm_f_supported, py::arg("M"), py::arg("N"), py::arg("K"));
+  m.def("gemm_f", &gemm_f, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("bias") = py::none(),
+        py::arg("waves") = 0);
   m.def("gemm_wg_supported", &gemm_wg_supported, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits") = 0);
   m.def("gemm_wg_conv3x3_supported", &gemm_wg_conv3x3_supported, py::arg("Cout"), py::arg("Cin"), py::arg("imgs"),
         py::arg("H"), py::arg("W"), py::arg("stride"));

@@ -1,0 +1,297 @@
+// Forward / input-gradient GEMM for gfx950 on gemm_wg's staging pipeline:
+//
+//   C[M, N] = A[M, K] . B[N, K]^T (+ bias[N])     (both operands K-contiguous: x W^T, dY (W^T)^T)
+//
+// the plain forward GEMMs and the LM head's input gradient are the last library GEMMs of the
+// GPT-2 step. Structure:
+//   * 256 x 256 tile per workgroup in one of two wave layouts: 8 waves as 2 (M) x 4 (N) of 128 x 64 (two waves per
+//     SIMD, 128 accumulators in VGPRs; the default) or 4 waves as 2 x 2 of 128 x 128 (hipBLASLt's MT256x256x64
+//     WG32_8_1 / MIWT8_8 geometry: one wave per SIMD, 256 accumulators in AGPRs);
+//   * 4-slot LDS ring of 32-deep K-slices (32 KB each: A 256 x 64 B, B 256 x 64 B), LDS-DMA issued as inline asm
+//     (hipcc's waitcnt pass cannot see it, so it adds no vmcnt drains), a counted vmcnt that keeps two slices in
+//     flight across every raw s_barrier, fragments of slice s + 1 read during slice s into a second register set;
+//   * MFMAs as inline asm on pinned accumulators (the builtin let the register allocator rotate them: 68
+//     v_accvgpr_mov per 128 MFMAs in the 4-wave loop);
+//   * 16-B chunks XOR-swizzled per row F[(row >> 2) & 3] = {0, 2, 3, 1} (gemm.hip), applied to the DMA's per-lane
+//     SOURCE address since the DMA writes each wave's 1-KB piece lane-linearly: conflict-free ds_read_b128;
+//   * optional bias added in the epilogue (F.linear's GemmAndBias);
+//   * the output tile leaves through the (then idle) ring as whole row segments, non-temporal stores;
+//   * XCD-aware tile order: each XCD's concurrent tiles form a block of GROUP_M row panels x column panels.
+// Measured (profiles/r6_gemm_f.txt, GPT-2 shapes at 65536 tokens): 0.85-0.93x the library (8 waves: qkv 227.9 vs
+// 203.6 us, fc2 259.0 vs 218.6, 4096^3 1317 vs 1518 TF/s -- the cdna guide's 8-phase template level); 4 waves
+// 0.78-0.81x. Counters (8 waves, qkv + 4096^3): MFMA busy 48 %, 36 % of wave-cycles parked at waits / barriers,
+// against the library's 57 % / 14 %; a 5-slot ring (memory latency) and staggering the two M halves' DMA issue
+// measured even. Hence opt-in (config.gemm_fwd = "vcx"); the library keeps the forward GEMMs.
+// Reference analog: per-frame net.forward, /root/reference/worker.py:248-249 (the pointwise GEMMs).
+#include <type_traits>
+
+#include "vcx_common.h"
+
+namespace vcx {
+namespace gemm_f {
+
+typedef short sx8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 256, BN = 256, BKS = 32;
+constexpr int ROWB = BKS * 2;           // 64 B per row per slice
+constexpr int SLOT_A = BM * ROWB;       // 16 KB
+constexpr int SLOT = 2 * SLOT_A;        // 32 KB: A and B slices
+constexpr int STG_BYTES = 4 * SLOT;     // 128 KB output staging (the ring's first 4 slots)
+
+__device__ __forceinline__ int swz(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
+
+// buffer resource words over [base, base + bytes): wave-uniform base and size (SGPRs), 32-bit per-lane offsets
+__device__ __forceinline__ u32x4 desc(const void* base, unsigned bytes) {
+  const uint64_t a = (uint64_t)base;
+  return u32x4{(unsigned)a, (unsigned)(a >> 32) & 0xffffu, bytes, 0x00020000u};
+}
+
+// one 1-KB LDS-DMA piece (16 B per lane to LDS base + 16 lane), M0 = the LDS byte address; `s_nop 0`: the
+// M0 write -> LDS-DMA hazard
+__device__ __forceinline__ void dma16(u32x4 d, int voff, int soff, const char* lds) {
+  const unsigned m0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(d), "s"(soff), "{m0}"(m0)
+               : "memory");
+}
+
+// s_waitcnt vmcnt(N) lgkmcnt(0) for N up to 63 (vmcnt bits [3:0] and [15:14])
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  __builtin_amdgcn_s_waitcnt(0x0070 | (N & 15) | ((N >> 4) << 14));
+}
+__device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// WN waves along N, 2 along M: WN = 2 -> 4 waves of 128 x 128 (one wave per SIMD, 256 accumulator registers),
+// WN = 4 -> 8 waves of 128 x 64 (two waves per SIMD, 128)
+template <int WN>
+struct Geo {
+  static constexpr int WAVES = 2 * WN, NT = 64 * WAVES;
+  static constexpr int TN = BN / WN;       // output columns per wave
+  static constexpr int JB = TN / 16;       // B fragments (column blocks) per wave
+  static constexpr int OPS = 32 / WAVES;   // LDS-DMA pieces per wave per slice (16 of A + 16 of B per slice)
+  static constexpr int RB = TN * 2;        // staged output row bytes
+  static constexpr int CPR = RB / 16;      // 16-B chunks per staged row
+};
+
+template <int WN>
+struct Frags {
+  sx8 a[8];                // A fragments: the wave's 8 row blocks of 16 (output rows)
+  sx8 b[Geo<WN>::JB];      // B fragments: the wave's column blocks of 16
+};
+
+// D: ring slots, two slices in flight across each barrier (a 5-slot ring over the whole 160 KB LDS, three in
+// flight, measured even to 4 % slower: 236.3 vs 227.9 us qkv, 105.7 vs 104.4 sq4096)
+template <int WN, int D>
+__global__ void __launch_bounds__(Geo<WN>::NT, 1)
+    gemm_f_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
+                  const bf16* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int tilesN) {
+  using G = Geo<WN>;
+  static_assert(D == 4, "the pipeline tail below is written for a 4-slot ring");
+  constexpr int JB = G::JB, OPS = G::OPS, HOPS = OPS / 2, WAVES = G::WAVES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+
+  // ---- XCD-aware bijective tile order (gemm.hip): consecutive logical tiles share an XCD, walked as blocks of
+  // GROUP_M row panels x all column panels
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GROUP_M = 4;
+  const int tilesM = nwg / tilesN;
+  const int per_group = GROUP_M * tilesN;
+  const int gfirst = (wg / per_group) * GROUP_M;
+  const int gsize = min(tilesM - gfirst, GROUP_M);
+  const int m0 = (gfirst + (wg % per_group) % gsize) * BM, n0 = ((wg % per_group) / gsize) * BN;
+
+  // ---- staging: piece p (0..15) of an operand slice = rows 16 p .. 16 p + 15 (64 lanes x 16 B); wave w moves
+  // pieces w + WAVES q (q < HOPS) of A and of B. Lane l: row 16 p + (l >> 2), physical chunk l & 3 holding
+  // logical chunk (l & 3) ^ F(row) (F depends on row bits 2..3 only: the same for every piece). Rows past the
+  // operand (ragged M, the half column panel of N % 256 == 128) read past the resource: zeros, and their
+  // outputs are never stored.
+  const int prow = lane >> 2, pch = (lane & 3) ^ swz(prow);
+  const int rowsA = min(BM, M - m0), rowsB = min(BN, N - n0);
+  const u32x4 ra = desc(A + (int64_t)m0 * lda, (unsigned)(((int64_t)(rowsA - 1) * lda + K) * 2));
+  const u32x4 rb = desc(B + (int64_t)n0 * ldb, (unsigned)(((int64_t)(rowsB - 1) * ldb + K) * 2));
+  int va[HOPS], vb[HOPS];
+#pragma unroll
+  for (int q = 0; q < HOPS; ++q) {
+    const int r = (wid + WAVES * q) * 16 + prow;
+    va[q] = r < rowsA ? (r * lda + pch * 8) * 2 : 0x7fffff00;  // past the resource: returns 0
+    vb[q] = r < rowsB ? (r * ldb + pch * 8) * 2 : 0x7fffff00;
+  }
+  auto stage_op = [&](int s, int o) {  // op o of slice s: A piece q = o (o < HOPS), B piece q = o - HOPS
+    char* slot = smem + (s % D) * SLOT;
+    const int q = o % HOPS;
+    if (o < HOPS)
+      dma16(ra, va[q], s * ROWB, slot + (wid + WAVES * q) * 1024);
+    else
+      dma16(rb, vb[q], s * ROWB, slot + SLOT_A + (wid + WAVES * q) * 1024);
+  };
+  auto stage = [&](int s) {
+#pragma unroll
+    for (int o = 0; o < OPS; ++o) stage_op(s, o);
+  };
+
+  // ---- fragment reads: lane l -> row (l & 15) of a 16-row block, k chunk (l >> 4)
+  const int frow = lane & 15;
+  const int foff = frow * ROWB + (((lane >> 4) ^ swz(frow)) << 4);
+  auto afrag = [&](int s, int i) {
+    return *(const sx8*)(smem + (s % D) * SLOT + (wm * 128 + 16 * i) * ROWB + foff);
+  };
+  auto bfrag = [&](int s, int j) {
+    return *(const sx8*)(smem + (s % D) * SLOT + SLOT_A + (wn * G::TN + 16 * j) * ROWB + foff);
+  };
+
+  f32x4 acc[8][JB];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < JB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // in-place accumulation, the accumulators pinned by the constraint (with the builtin the register allocator
+  // rotated them through 68 v_accvgpr_mov per 128 MFMAs): AGPRs at one wave per SIMD, VGPRs at two (the
+  // unified file split 128 / 128 would not fit the fragments). An accumulate chain needs no wait states; the
+  // epilogue's first reads are padded by hand (the MFMAs are invisible to hipcc's hazard recognizer).
+  auto mma_row = [&](const Frags<WN>& f, int i) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      if constexpr (WN == 2)
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(f.b[j]), "v"(f.a[i]));
+      else
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[i][j]) : "v"(f.b[j]), "v"(f.a[i]));
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // one step: slice s in fc; make slice s + 1 visible (the counted vmcnt leaves the D - 2 slices behind it in
+  // flight), issue slice s + D into the slot of slice s (read into registers during step s - 1), then 8 MFMA
+  // groups (one output row block each), each followed by the reads of slice s + 1's fragments of that row (and
+  // column) block into fn; the DMA ops ride along the first 4 groups (placing the second M half's in the last 4
+  // measured even, 8 waves: 233.5 vs 234.3 us qkv, 109.2 vs 110.1 sq4096)
+  auto step = [&](int s, Frags<WN>& fc, Frags<WN>& fn, auto STAGE, auto PEND) {
+    wait_vm<decltype(PEND)::value>();
+    barrier();
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      if constexpr (decltype(STAGE)::value) {
+        if (g < 4) {
+#pragma unroll
+          for (int o = 0; o < OPS / 4; ++o) stage_op(s + D, (OPS / 4) * g + o);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mma_row(fc, g);
+      __builtin_amdgcn_sched_barrier(0);
+      fn.a[g] = afrag(s + 1, g);
+      if (g < JB) fn.b[g] = bfrag(s + 1, g);
+    }
+  };
+
+  using T = std::true_type;
+  using F = std::false_type;
+  using PS = std::integral_constant<int, (D - 2) * OPS>;
+  using P2 = std::integral_constant<int, 2 * OPS>;
+  using P1 = std::integral_constant<int, OPS>;
+  using P0 = std::integral_constant<int, 0>;
+  const int nk = K / BKS;  // even, >= 6 (host: K % 64 == 0, K >= 192)
+  Frags<WN> f0, f1;
+#pragma unroll
+  for (int t = 0; t < D; ++t) stage(t);
+  wait_vm<(D - 1) * OPS>();  // slice 0 landed
+  barrier();
+#pragma unroll
+  for (int g = 0; g < 8; ++g) f0.a[g] = afrag(0, g);
+#pragma unroll
+  for (int j = 0; j < JB; ++j) f0.b[j] = bfrag(0, j);
+  int s = 0;
+#pragma unroll 1
+  for (; s + D + 1 < nk; s += 2) {  // both steps stage
+    step(s, f0, f1, T{}, PS{});
+    step(s + 1, f1, f0, T{}, PS{});
+  }
+  // s = nk - 4: three steps, nothing left to stage
+  step(s, f0, f1, F{}, P2{});
+  step(s + 1, f1, f0, F{}, P1{});
+  step(s + 2, f0, f1, F{}, P0{});
+#pragma unroll
+  for (int g = 0; g < 8; ++g) mma_row(f1, g);
+
+  // ---- epilogue: acc[i][j] = C[wm 128 + 16 i + (l & 15)][wn TN + 16 j + 4 (l >> 4) .. + 3]. Each wave stages
+  // its 128 x TN bf16 block in its own part of the ring (RB-byte rows, 16-B chunks XOR-swizzled by the row),
+  // then writes whole RB-byte row segments (CPR lanes per row) with non-temporal stores.
+  // the last MFMAs' results -> their first readers: >= 12 wait states for an 8-pass MFMA
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+  __syncthreads();  // every wave is past its last fragment read; every DMA retired (vmcnt(0) of the last step)
+  if (n0 + wn * G::TN >= N) return;  // the missing half of a 128-column last panel (no barrier follows)
+  constexpr int RB = G::RB, CPR = G::CPR;
+  char* const stg = smem + wid * (128 * RB);
+  float bv[JB][4];  // the bias of the lane's output columns (zeros without one)
+#pragma unroll
+  for (int j = 0; j < JB; ++j) {
+    bf16x4 b4 = {};
+    if (bias) b4 = *(const bf16x4*)(bias + n0 + wn * G::TN + 16 * j + 4 * (lane >> 4));
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bv[j][t] = (float)b4[t];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      const int c = 16 * j + 4 * (lane >> 4);
+      bf16x4 v;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = (bf16)(acc[i][j][t] + bv[j][t]);
+      *(bf16x4*)(stg + r * RB + (((c >> 3) ^ (r & (CPR - 1))) << 4) + ((c >> 2) & 1) * 8) = v;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back only its own block
+  const int k = lane % CPR;
+  const int mrem = M - (m0 + wm * 128);
+  bf16* const base = C + (int64_t)(m0 + wm * 128) * ldc + n0 + wn * G::TN + k * 8;
+#pragma unroll 8
+  for (int it = 0; it < 2 * CPR; ++it) {
+    const int r = it * (64 / CPR) + lane / CPR;
+    const bf16x8 v = *(const bf16x8*)(stg + r * RB + ((k ^ (r & (CPR - 1))) << 4));
+    if (r < mrem) __builtin_nontemporal_store(v, (bf16x8*)(base + (int64_t)r * ldc));
+  }
+}
+
+template <int WN, int D>
+void launch(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda, int ldb, int ldc,
+            hipStream_t s) {
+  constexpr int LDS_BYTES = D * SLOT;
+  static const bool attrs = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_f_kernel<WN, D>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    return true;
+  }();
+  (void)attrs;
+  const int tilesN = (N + BN - 1) / BN, tiles = ((M + BM - 1) / BM) * tilesN;
+  hipLaunchKernelGGL((gemm_f_kernel<WN, D>), dim3(tiles), dim3(Geo<WN>::NT), LDS_BYTES, s, (const bf16*)A,
+                     (const bf16*)B, (bf16*)C, (const bf16*)bias, M, N, K, lda, ldb, ldc, tilesN);
+}
+
+}  // namespace gemm_f
+}  // namespace vcx
+
+using namespace vcx;
+
+bool vcx_gemm_f_supported(int M, int N, int K) {
+  // N a multiple of 128 (a wave's columns are all in or all out), K a multiple of 64 and >= 192 (even slice
+  // count, 3-deep ring), operand panels under 2 GB (32-bit buffer offsets)
+  return M > 0 && N > 0 && N % 128 == 0 && K % 64 == 0 && K >= 192 && (int64_t)256 * K * 2 < (int64_t(1) << 31);
+}
+
+// waves: 4 (128 x 128 per wave) or 8 (128 x 64 per wave); anything else = the default (8)
+void vcx_gemm_f(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda, int ldb,
+                int ldc, int waves, hipStream_t s) {
+  if (waves == 4)
+    gemm_f::launch<2, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, s);
+  else
+    gemm_f::launch<4, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, s);
+}

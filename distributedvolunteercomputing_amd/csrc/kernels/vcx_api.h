@@ -22,6 +22,10 @@ void vcx_gemm_wg(const void* A, const void* B, float* Cpart, void* out, int M, i
 bool vcx_gemm_wg_conv3x3_supported(int Cout, int Cin, int tokens, int64_t xbytes, int splits);
 void vcx_gemm_wg_conv3x3(const void* dy, const void* x, float* Cpart, void* out, int Cout, int Cin, int imgs, int H,
                          int W, int stride, int splits, int accumulate, hipStream_t s);
+// gemm_f.hip: C[M, N] = A[M, K] B[N, K]^T (+ bias[N]), 4 waves of 128 x 128 (the library's forward geometry)
+bool vcx_gemm_f_supported(int M, int N, int K);
+void vcx_gemm_f(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda, int ldb,
+                int ldc, int waves, hipStream_t s);
 bool vcx_gemm_nt_supported(int M, int N, int K);
 bool vcx_gemm_nt_supported_epi(int M, int N, int K, int epi);
 void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,

@@ -78,6 +78,20 @@ def narrow_gemm(a, w):
     return V.gemm_bias_act(a, w.contiguous(), zb, False)
 
 
+def gemm_f_ok(M: int, N: int, K: int, t) -> bool:
+    """Y[M, N] = X[M, K] W[N, K]^T on the hand-written forward GEMM (csrc/kernels/gemm_f.hip) -- opt-in
+    (config.gemm_fwd == "vcx"): 0.85-0.93x the library at the GPT-2 shapes (profiles/r6_gemm_f.txt)."""
+    return (config.get().gemm_fwd == "vcx" and use_native(t) and t.dtype == torch.bfloat16 and t.is_contiguous()
+            and bool(native().gemm_f_supported(M, N, K)))
+
+
+def gemm_f(a, w, bias=None):
+    """a [M, K] @ w[N, K]^T (+ bias) on gemm_f (caller checked gemm_f_ok)."""
+    out = torch.empty(a.shape[0], w.shape[0], device=a.device, dtype=a.dtype)
+    native().gemm_f(a, w.contiguous(), out, bias)
+    return out
+
+
 def transpose_weight(w):
     """W^T as a contiguous bf16 matrix (HIP transpose; weights only — a few MB)."""
     return native().transpose_bf16(w.contiguous())
@@ -361,6 +375,8 @@ class _Linear(torch.autograd.Function):
         w = _w2(w)
         if gemm_nt_ok(x2.shape[0], w.shape[0], x2.shape[1], x2):
             return gemm_nt(x2, w, b).view(*x.shape[:-1], w.shape[0])
+        if gemm_f_ok(x2.shape[0], w.shape[0], x2.shape[1], x2) and (b is None or b.is_contiguous()):
+            return gemm_f(x2, w, b).view(*x.shape[:-1], w.shape[0])
         if b is None and narrow_gemm_ok(x2.shape[0], w.shape[0], x2.shape[1], x2):
             return narrow_gemm(x2, w).view(*x.shape[:-1], w.shape[0])
         return mm(x2, w, trans_b=True, bias=b).view(*x.shape[:-1], w.shape[0])
@@ -389,6 +405,8 @@ class _Linear(torch.autograd.Function):
         elif ctx.needs_input_grad[0]:
             if gemm_nt_ok(dy2.shape[0], K, N, dy2):
                 dx = gemm_nt(dy2, transpose_weight(w)).view(x.shape)
+            elif gemm_f_ok(dy2.shape[0], K, N, dy2):
+                dx = gemm_f(dy2, transpose_weight(w)).view(x.shape)
             elif narrow_gemm_ok(dy2.shape[0], K, N, dy2):
                 dx = narrow_gemm(dy2, transpose_weight(w)).view(x.shape)
             elif dgrad_ps_ok(dy2.shape[0], K, N, dy2):
@@ -475,7 +493,7 @@ class _MlpGelu(torch.autograd.Function):
             # `pre` holds gelu'(pre) (epilogue 5): the backward needs pre only for gelu', and the forward
             # already has sigmoid(2u) (VCX_MLP_GRAD_FWD=0: store pre, gelu' in the backward's epilogue 4)
             C.gemm_ps(x2, w1, pre, act, b1, None, 5 if config.get().mlp_grad_fwd else 2)
-            y = mm(act, w2, trans_b=True)
+            y = gemm_f(act, w2) if gemm_f_ok(M, w2.shape[0], F_, act) else mm(act, w2, trans_b=True)
         else:
             C.gemm_nt(x2, w1, pre, act, b1, None, 2)
             y = gemm_nt(act, w2)
