@@ -77,6 +77,10 @@ class RuntimeConfig:
     # VCX_CONV3X3_WGRAD: weight gradients of the ResNet 3x3 convolutions with Cin, Cout % 128 == 0 on gemm_wg with
     # the patch matrix gathered while staging ("vcx"), or MIOpen's ("lib")
     conv3x3_wgrad: str = "vcx"
+    # VCX_CONV3X3_FWD: forwards (and stride-1 input gradients) of the ResNet 3x3 convolutions with 256+ output
+    # channels on gemm_f's implicit GEMM ("vcx": 1.09-1.38x MIOpen at stages 3 / 4, profiles/r6_conv3x3_fwd.txt),
+    # or MIOpen's ("lib")
+    conv3x3_fwd: str = "vcx"
     # VCX_ENGINE_BATCH: chunks a volunteer that already holds several runs through the detector as ONE batch
     # (1 = one chunk per network launch)
     engine_batch: int = 2
@@ -123,6 +127,7 @@ _ENV = {
     "resnet_join": ("VCX_RESNET_JOIN", _bool),
     "engine_batch": ("VCX_ENGINE_BATCH", int),
     "conv3x3_wgrad": ("VCX_CONV3X3_WGRAD", str),
+    "conv3x3_fwd": ("VCX_CONV3X3_FWD", str),
     "resnet_proj_join": ("VCX_RESNET_PROJ_JOIN", _bool),
     "bn_layer_ws": ("VCX_BN_LAYER_WS", _bool),
     "conv_find": ("VCX_CONV_FIND", _bool),
@@ -153,7 +158,7 @@ _ENV = {
     "trace_dir": ("VCX_TRACE_DIR", str),
     "metrics_dir": ("VCX_METRICS_DIR", str),
 }
-_CHOICES = {"narrow_gemm": ("lib", "vision"), "conv3x3_wgrad": ("lib", "vcx"), "gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "gemm_fwd": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "off"),
+_CHOICES = {"narrow_gemm": ("lib", "vision"), "conv3x3_wgrad": ("lib", "vcx"), "conv3x3_fwd": ("lib", "vcx"), "gemm": ("lib", "vcx"), "mlp": ("fused", "lib"), "gemm_wgrad": ("lib", "vcx"), "gemm_fwd": ("lib", "vcx"), "tunableop": ("on", "off"), "p2p_backend": ("", "gloo", "nccl"), "elastic_stage_joins": ("gloo", "off"),
             "uplink_pipeline": ("relay", "all", "off")}
 
 _lock = threading.Lock()

@@ -373,7 +373,19 @@ void gemm_wg(at::Tensor a, at::Tensor b, at::Tensor out, bool accumulate, int64_
 // out[M, N] = a[M, K] . b[N, K]^T (+ bias[N]) on gemm_f (csrc/kernels/gemm_f.hip): 256 x 256 tiles, 4 waves of 128 x 128
 bool gemm_f_supported(int64_t M, int64_t N, int64_t K) { return vcx_gemm_f_supported((int)M, (int)N, (int)K); }
 
-void gemm_f(at::Tensor a, at::Tensor b, at::Tensor out, c10::optional<at::Tensor> bias, int64_t waves) {
+// splits < 0: vcx_gemm_f_splits (one round of workgroups); the fp32 partials live in a temporary [splits, M, N]
+static std::pair<int, at::Tensor> f_splits(int64_t M, int64_t N, int64_t K, int64_t splits, const at::Tensor& like) {
+  if (splits < 0) splits = vcx_gemm_f_splits((int)M, (int)N, (int)K);
+  if (splits == 0) splits = 1;
+  TORCH_CHECK(vcx_gemm_f_split_ok((int)M, (int)N, (int)K, (int)splits),
+              "gemm_f: the K slices (K / 32) must split into even counts >= 6");
+  at::Tensor ws = splits > 1 ? at::empty({splits, M, N}, like.options().dtype(at::kFloat)) : at::Tensor();
+  return {(int)splits, ws};
+}
+
+int64_t gemm_f_splits(int64_t M, int64_t N, int64_t K) { return vcx_gemm_f_splits((int)M, (int)N, (int)K); }
+
+void gemm_f(at::Tensor a, at::Tensor b, at::Tensor out, c10::optional<at::Tensor> bias, int64_t waves, int64_t splits) {
   TORCH_CHECK(a.is_cuda() && a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_f: 2-D cuda tensors");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16,
               "gemm_f: bf16 operands");
@@ -391,8 +403,43 @@ void gemm_f(at::Tensor a, at::Tensor b, at::Tensor out, c10::optional<at::Tensor
                     bias->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 8 == 0,
                 "gemm_f: bias bf16 [N], contiguous, 8-B aligned");
   TORCH_CHECK(256 * std::max(a.stride(0), b.stride(0)) * 2 < (int64_t(1) << 31), "gemm_f: tile panels under 2 GB");
+  auto [ns, ws] = f_splits(M, N, K, splits, a);
+  TORCH_CHECK(ns == 1 || out.stride(0) % 4 == 0, "gemm_f: split output rows 8-B aligned");
   vcx_gemm_f(a.data_ptr(), b.data_ptr(), out.data_ptr(), hb ? bias->data_ptr() : nullptr, (int)M, (int)N, (int)K, (int)a.stride(0), (int)b.stride(0),
-             (int)out.stride(0), (int)waves, cur_stream());
+             (int)out.stride(0), (int)waves, ns, ns > 1 ? ws.data_ptr<float>() : nullptr, cur_stream());
+}
+
+// 3x3 convolution (pad 1, stride 1|2) forward on gemm_f as an implicit GEMM: y[N, Ho, Wo, Cout] (+ bias) =
+// conv(x[N, H, W, Cin], w[Cout][3][3][Cin]) with the patch matrix of x gathered by the LDS-DMA's per-lane offsets
+bool gemm_f_conv3x3_supported(int64_t imgs, int64_t H, int64_t W, int64_t Cin, int64_t Cout, int64_t stride) {
+  return vcx_gemm_f_conv3x3_supported((int)imgs, (int)H, (int)W, (int)Cin, (int)Cout, (int)stride);
+}
+
+void gemm_f_conv3x3(at::Tensor x, at::Tensor w, at::Tensor out, int64_t stride, c10::optional<at::Tensor> bias,
+                    int64_t waves, int64_t splits) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && w.dim() == 4 && out.dim() == 4, "gemm_f_conv3x3: x [N, H, W, Cin], "
+              "w [Cout, 3, 3, Cin], out [N, Ho, Wo, Cout] on the GPU");
+  for (const at::Tensor* t : {&x, &w, &out}) {
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->get_device() == x.get_device(),
+                "gemm_f_conv3x3: contiguous bf16 tensors on one device");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_f_conv3x3: 16-B aligned base pointers");
+  }
+  const int64_t imgs = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = w.size(0);
+  TORCH_CHECK(w.size(1) == 3 && w.size(2) == 3 && w.size(3) == Cin, "gemm_f_conv3x3: w [Cout, 3, 3, Cin]");
+  TORCH_CHECK(stride == 1 || stride == 2, "gemm_f_conv3x3: stride 1 or 2");
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  TORCH_CHECK(out.size(0) == imgs && out.size(1) == Ho && out.size(2) == Wo && out.size(3) == Cout,
+              "gemm_f_conv3x3: out [N, Ho, Wo, Cout]");
+  TORCH_CHECK(vcx_gemm_f_conv3x3_supported((int)imgs, (int)H, (int)W, (int)Cin, (int)Cout, (int)stride),
+              "gemm_f_conv3x3: needs Cin a power of two >= 64, Cout % 128 == 0, x under 2 GB");
+  const bool hb = bias && bias->defined();
+  if (hb)
+    TORCH_CHECK(bias->is_cuda() && bias->get_device() == x.get_device() && bias->numel() == Cout &&
+                    bias->is_contiguous() && bias->scalar_type() == at::kBFloat16, "gemm_f_conv3x3: bias bf16 [Cout]");
+  auto [ns, ws] = f_splits(imgs * Ho * Wo, Cout, 9 * Cin, splits, x);
+  vcx_gemm_f_conv3x3(x.data_ptr(), w.data_ptr(), out.data_ptr(), hb ? bias->data_ptr() : nullptr, (int)imgs, (int)H,
+                     (int)W, (int)Cin, (int)Cout, (int)stride, (int)waves, ns, ns > 1 ? ws.data_ptr<float>() : nullptr,
+                     cur_stream());
 }
 
 // 3x3 convolution (pad 1, stride 1|2) weight gradient on gemm_wg with the patch matrix of x gathered while
@@ -899,8 +946,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_ps", &gemm_ps, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0, py::arg("grid_cap") = 0);
   m.def("gemm_f_supported", &gemm_f_supported, py::arg("M"), py::arg("N"), py::arg("K"));
+  m.def("gemm_f_conv3x3_supported", &gemm_f_conv3x3_supported, py::arg("imgs"), py::arg("H"), py::arg("W"),
+        py::arg("Cin"), py::arg("Cout"), py::arg("stride"));
+  m.def("gemm_f_conv3x3", &gemm_f_conv3x3, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("stride"),
+        py::arg("bias") = py::none(), py::arg("waves") = 0, py::arg("splits") = -1);
+  m.def("gemm_f_splits", &gemm_f_splits, py::arg("M"), py::arg("N"), py::arg("K"));
   m.def("gemm_f", &gemm_f, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("bias") = py::none(),
-        py::arg("waves") = 0);
+        py::arg("waves") = 0, py::arg("splits") = -1);
   m.def("gemm_wg_supported", &gemm_wg_supported, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits") = 0);
   m.def("gemm_wg_conv3x3_supported", &gemm_wg_conv3x3_supported, py::arg("Cout"), py::arg("Cin"), py::arg("imgs"),
         py::arg("H"), py::arg("W"), py::arg("stride"));

@@ -81,12 +81,21 @@ struct Frags {
   sx8 b[Geo<WN>::JB];      // B fragments: the wave's column blocks of 16
 };
 
+// 3x3 convolution (pad 1) as an implicit GEMM: A = the patch matrix of NHWC x gathered while staging
+struct Conv {
+  int H, W, lc, Ho, Wo, stride;  // lc = log2(Cin)
+  unsigned xbytes;
+};
+
 // D: ring slots, two slices in flight across each barrier (a 5-slot ring over the whole 160 KB LDS, three in
 // flight, measured even to 4 % slower: 236.3 vs 227.9 us qkv, 105.7 vs 104.4 sq4096)
-template <int WN, int D>
+// CONV: A is NHWC x [imgs, H, W, Cin] and row m of the GEMM the output pixel m of [imgs, Ho, Wo]; K = 9 Cin in the
+// [ky][kx][Cin] order of the channels-last weight, each 32-deep slice inside one tap (Cin a power of two >= 64)
+template <int WN, int D, bool CONV>
 __global__ void __launch_bounds__(Geo<WN>::NT, 1)
     gemm_f_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
-                  const bf16* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int tilesN) {
+                  const bf16* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int tilesN,
+                  Conv cv, int splits, float* __restrict__ ws) {
   using G = Geo<WN>;
   static_assert(D == 4, "the pipeline tail below is written for a 4-slot ring");
   constexpr int JB = G::JB, OPS = G::OPS, HOPS = OPS / 2, WAVES = G::WAVES;
@@ -99,9 +108,12 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   // GROUP_M row panels x all column panels
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int wga = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  // split-K: the grid is splits x tiles, split-major (one XCD's neighbours share the split's K range)
+  const int tiles = nwg / splits, split = wga / tiles, wg = wga - split * tiles;
+  const int ks0 = split * (K / BKS / splits);  // the split's first K slice
   constexpr int GROUP_M = 4;
-  const int tilesM = nwg / tilesN;
+  const int tilesM = tiles / tilesN;
   const int per_group = GROUP_M * tilesN;
   const int gfirst = (wg / per_group) * GROUP_M;
   const int gsize = min(tilesM - gfirst, GROUP_M);
@@ -114,22 +126,44 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   // outputs are never stored.
   const int prow = lane >> 2, pch = (lane & 3) ^ swz(prow);
   const int rowsA = min(BM, M - m0), rowsB = min(BN, N - n0);
-  const u32x4 ra = desc(A + (int64_t)m0 * lda, (unsigned)(((int64_t)(rowsA - 1) * lda + K) * 2));
+  const u32x4 ra = CONV ? desc(A, cv.xbytes) : desc(A + (int64_t)m0 * lda, (unsigned)(((int64_t)(rowsA - 1) * lda + K) * 2));
   const u32x4 rb = desc(B + (int64_t)n0 * ldb, (unsigned)(((int64_t)(rowsB - 1) * ldb + K) * 2));
   int va[HOPS], vb[HOPS];
+  // CONV: per A piece the lane's output pixel as the input pixel of tap (0, 0) -- (ih0, iw0) and its index pix0
+  // (rows past M: ih0 = -4, never inside the image)
+  int ih0[HOPS], iw0[HOPS];
 #pragma unroll
   for (int q = 0; q < HOPS; ++q) {
     const int r = (wid + WAVES * q) * 16 + prow;
-    va[q] = r < rowsA ? (r * lda + pch * 8) * 2 : 0x7fffff00;  // past the resource: returns 0
+    if constexpr (CONV) {
+      const int m = m0 + r, hw = cv.Ho * cv.Wo;
+      const int n = m / hw, oh = (m - n * hw) / cv.Wo, ow = m - n * hw - oh * cv.Wo;
+      ih0[q] = m < M ? oh * cv.stride - 1 : -4;
+      iw0[q] = ow * cv.stride - 1;
+      va[q] = (n * cv.H + ih0[q]) * cv.W + iw0[q];
+    } else {
+      va[q] = r < rowsA ? (r * lda + pch * 8) * 2 : 0x7fffff00;  // past the resource: returns 0
+    }
     vb[q] = r < rowsB ? (r * ldb + pch * 8) * 2 : 0x7fffff00;
   }
   auto stage_op = [&](int s, int o) {  // op o of slice s: A piece q = o (o < HOPS), B piece q = o - HOPS
     char* slot = smem + (s % D) * SLOT;
     const int q = o % HOPS;
-    if (o < HOPS)
-      dma16(ra, va[q], s * ROWB, slot + (wid + WAVES * q) * 1024);
-    else
-      dma16(rb, vb[q], s * ROWB, slot + SLOT_A + (wid + WAVES * q) * 1024);
+    if (o < HOPS) {
+      if constexpr (CONV) {  // slice s = channels c0 .. c0 + 31 of tap t = (ky, kx); padding taps read zeros
+        const int sg = ks0 + s;  // the global slice
+        const int t = (sg * BKS) >> cv.lc, c0 = (sg * BKS) & ((1 << cv.lc) - 1);
+        const int ky = (t * 11) >> 5, kx = t - 3 * ky;  // t / 3 for t < 9
+        const int ih = ih0[q] + ky, iw = iw0[q] + kx;
+        const bool ok = (unsigned)ih < (unsigned)cv.H && (unsigned)iw < (unsigned)cv.W;
+        const int voff = ok ? (((va[q] + ky * cv.W + kx) << cv.lc) + c0 + pch * 8) * 2 : 0x7fffff00;
+        dma16(ra, voff, 0, slot + (wid + WAVES * q) * 1024);
+      } else {
+        dma16(ra, va[q], (ks0 + s) * ROWB, slot + (wid + WAVES * q) * 1024);
+      }
+    } else {
+      dma16(rb, vb[q], (ks0 + s) * ROWB, slot + SLOT_A + (wid + WAVES * q) * 1024);
+    }
   };
   auto stage = [&](int s) {
 #pragma unroll
@@ -198,7 +232,7 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   using P2 = std::integral_constant<int, 2 * OPS>;
   using P1 = std::integral_constant<int, OPS>;
   using P0 = std::integral_constant<int, 0>;
-  const int nk = K / BKS;  // even, >= 6 (host: K % 64 == 0, K >= 192)
+  const int nk = K / BKS / splits;  // slices per split: even, >= 6 (host)
   Frags<WN> f0, f1;
 #pragma unroll
   for (int t = 0; t < D; ++t) stage(t);
@@ -228,6 +262,19 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
   __syncthreads();  // every wave is past its last fragment read; every DMA retired (vmcnt(0) of the last step)
   if (n0 + wn * G::TN >= N) return;  // the missing half of a 128-column last panel (no barrier follows)
+  if (splits > 1) {  // fp32 partial straight from the accumulators (splitk_bias_kernel sums them)
+    float* const wb = ws + ((int64_t)split * M + m0 + wm * 128) * N + n0 + wn * G::TN + 4 * (lane >> 4);
+    const int mrem = M - (m0 + wm * 128);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 16 * i + (lane & 15);
+      if (r < mrem) {
+#pragma unroll
+        for (int j = 0; j < JB; ++j) *(f32x4*)(wb + (int64_t)r * N + 16 * j) = acc[i][j];
+      }
+    }
+    return;
+  }
   constexpr int RB = G::RB, CPR = G::CPR;
   char* const stg = smem + wid * (128 * RB);
   float bv[JB][4];  // the bias of the lane's output columns (zeros without one)
@@ -262,18 +309,39 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   }
 }
 
-template <int WN, int D>
+// C[m][n] = bf16(sum over splits of ws[s][m][n] (+ bias[n])), 4 columns per thread
+__global__ void __launch_bounds__(256) splitk_bias_kernel(const float* __restrict__ ws, const bf16* __restrict__ bias,
+                                                        bf16* __restrict__ C, int M, int N, int ldc, int splits) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4, mn = (int64_t)M * N;
+  if (i >= mn) return;
+  const int m = (int)(i / N), n = (int)(i - (int64_t)m * N);
+  f32x4 a = *(const f32x4*)(ws + i);
+  for (int s = 1; s < splits; ++s) a += *(const f32x4*)(ws + (int64_t)s * mn + i);
+  bf16x4 b4 = {};
+  if (bias) b4 = *(const bf16x4*)(bias + n);
+  bf16x4 r;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) r[t] = (bf16)(a[t] + (float)b4[t]);
+  *(bf16x4*)(C + (int64_t)m * ldc + n) = r;
+}
+
+template <int WN, int D, bool CONV = false>
 void launch(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda, int ldb, int ldc,
-            hipStream_t s) {
+            int splits, float* ws, hipStream_t s, Conv cv = {}) {
   constexpr int LDS_BYTES = D * SLOT;
   static const bool attrs = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_f_kernel<WN, D>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_f_kernel<WN, D, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_BYTES);
     return true;
   }();
   (void)attrs;
   const int tilesN = (N + BN - 1) / BN, tiles = ((M + BM - 1) / BM) * tilesN;
-  hipLaunchKernelGGL((gemm_f_kernel<WN, D>), dim3(tiles), dim3(Geo<WN>::NT), LDS_BYTES, s, (const bf16*)A,
-                     (const bf16*)B, (bf16*)C, (const bf16*)bias, M, N, K, lda, ldb, ldc, tilesN);
+  hipLaunchKernelGGL((gemm_f_kernel<WN, D, CONV>), dim3(tiles * splits), dim3(Geo<WN>::NT), LDS_BYTES, s,
+                     (const bf16*)A, (const bf16*)B, (bf16*)C, (const bf16*)bias, M, N, K, lda, ldb, ldc, tilesN, cv,
+                     splits, ws);
+  if (splits > 1)
+    hipLaunchKernelGGL(splitk_bias_kernel, dim3((unsigned)(((int64_t)M * N / 4 + 255) / 256)), dim3(256), 0, s, ws,
+                       (const bf16*)bias, (bf16*)C, M, N, ldc, splits);
 }
 
 }  // namespace gemm_f
@@ -287,11 +355,61 @@ bool vcx_gemm_f_supported(int M, int N, int K) {
   return M > 0 && N > 0 && N % 128 == 0 && K % 64 == 0 && K >= 192 && (int64_t)256 * K * 2 < (int64_t(1) << 31);
 }
 
-// waves: 4 (128 x 128 per wave) or 8 (128 x 64 per wave); anything else = the default (8)
+bool vcx_gemm_f_split_ok(int M, int N, int K, int splits) {
+  const int nk = K / gemm_f::BKS;
+  return splits >= 1 && splits <= 16 && nk % splits == 0 && (nk / splits) % 2 == 0 && nk / splits >= 6;
+}
+
+// K splits for an output of fewer tiles than CUs: the largest count that keeps splits x tiles within one round
+// of 256 workgroups and each split's slice count even and >= 6 (1: no split)
+int vcx_gemm_f_splits(int M, int N, int K) {
+  const int tiles = ((M + gemm_f::BM - 1) / gemm_f::BM) * ((N + gemm_f::BN - 1) / gemm_f::BN);
+  int best = 1;
+  for (int s = 2; s <= 16 && tiles * s <= 256; ++s)
+    if (vcx_gemm_f_split_ok(M, N, K, s)) best = s;
+  return best;
+}
+
+// waves: 4 (128 x 128 per wave) or 8 (128 x 64 per wave); anything else = the default (8). splits > 1: ws holds
+// splits x M x N fp32 partials
 void vcx_gemm_f(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda, int ldb,
-                int ldc, int waves, hipStream_t s) {
+                int ldc, int waves, int splits, float* ws, hipStream_t s) {
   if (waves == 4)
-    gemm_f::launch<2, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, s);
+    gemm_f::launch<2, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, splits, ws, s);
   else
-    gemm_f::launch<4, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, s);
+    gemm_f::launch<4, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, splits, ws, s);
+}
+
+static int log2_exact(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
+}
+
+bool vcx_gemm_f_conv3x3_supported(int imgs, int H, int W, int Cin, int Cout, int stride) {
+  // Cin a power of two >= 64 (a 32-deep slice inside one tap, K = 9 Cin a multiple of 64), Cout a multiple of 128,
+  // x under 2 GB (32-bit offsets), output rows in int
+  const int lc = log2_exact(Cin);
+  const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
+  return imgs > 0 && H > 0 && W > 0 && lc >= 6 && Cout % 128 == 0 && (stride == 1 || stride == 2) &&
+         (int64_t)imgs * H * W * Cin * 2 < (int64_t(1) << 31) - (int64_t(1) << 20) && imgs * Ho * Wo < (int64_t(1) << 31) &&
+         vcx_gemm_f_supported(1, Cout, 9 * Cin);
+}
+
+// y[imgs, Ho, Wo, Cout] (+ bias) = conv3x3(x[imgs, H, W, Cin], w[Cout][3][3][Cin]), pad 1
+void vcx_gemm_f_conv3x3(const void* x, const void* w, void* y, const void* bias, int imgs, int H, int W, int Cin,
+                        int Cout, int stride, int waves, int splits, float* ws, hipStream_t s) {
+  gemm_f::Conv cv;
+  cv.H = H;
+  cv.W = W;
+  cv.lc = log2_exact(Cin);
+  cv.Ho = (H - 1) / stride + 1;
+  cv.Wo = (W - 1) / stride + 1;
+  cv.stride = stride;
+  cv.xbytes = (unsigned)((int64_t)imgs * H * W * Cin * 2);
+  const int M = imgs * cv.Ho * cv.Wo, K = 9 * Cin;
+  if (waves == 4)
+    gemm_f::launch<2, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
+  else
+    gemm_f::launch<4, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
 }

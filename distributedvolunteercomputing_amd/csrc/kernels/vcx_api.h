@@ -24,8 +24,13 @@ void vcx_gemm_wg_conv3x3(const void* dy, const void* x, float* Cpart, void* out,
                          int W, int stride, int splits, int accumulate, hipStream_t s);
 // gemm_f.hip: C[M, N] = A[M, K] B[N, K]^T (+ bias[N]), 4 waves of 128 x 128 (the library's forward geometry)
 bool vcx_gemm_f_supported(int M, int N, int K);
+bool vcx_gemm_f_split_ok(int M, int N, int K, int splits);
+int vcx_gemm_f_splits(int M, int N, int K);
 void vcx_gemm_f(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda, int ldb,
-                int ldc, int waves, hipStream_t s);
+                int ldc, int waves, int splits, float* ws, hipStream_t s);
+bool vcx_gemm_f_conv3x3_supported(int imgs, int H, int W, int Cin, int Cout, int stride);
+void vcx_gemm_f_conv3x3(const void* x, const void* w, void* y, const void* bias, int imgs, int H, int W, int Cin,
+                        int Cout, int stride, int waves, int splits, float* ws, hipStream_t s);
 bool vcx_gemm_nt_supported(int M, int N, int K);
 bool vcx_gemm_nt_supported_epi(int M, int N, int K, int epi);
 void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,

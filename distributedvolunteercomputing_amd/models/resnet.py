@@ -4,8 +4,9 @@ synthetic ImageNet shapes, top-k sparsified gradients + error feedback, 8 peers"
 Channels-last bf16. The 1x1 convolutions (about 70 % of the FLOPs) are plain GEMMs on the NHWC
 view -- [N*H*W, Cin] x [Cout, Cin]^T -- and run through the framework's linear layer (library
 GEMMs picked per shape, split-M weight gradients summed straight into the flat gradient buffer);
-stride-2 ones subsample the NHWC view first. The 3x3 / 7x7 convolutions go through MIOpen's NHWC
-kernels. Train-mode BatchNorm runs fused with its ReLU and the residual add (ops/batchnorm.py,
+stride-2 ones subsample the NHWC view first. The 3x3 convolutions of stages 3 and 4 run forward, input
+gradient (stride 1) and weight gradient on the hand-written gemm_f / gemm_wg kernels, the others and the 7x7 stem
+through MIOpen's NHWC kernels. Train-mode BatchNorm runs fused with its ReLU and the residual add (ops/batchnorm.py,
 csrc/kernels/batchnorm.hip). BatchNorm statistics are buffers that the trainers average at every
 synchronisation.
 """
@@ -55,15 +56,36 @@ class Conv1x1(nn.Conv2d):
         return y.view(N, H, W, self.out_channels).permute(0, 3, 1, 2)
 
 
+def _fwd_vcx(imgs, H, W, cin, cout, stride) -> bool:
+    """gemm_f's implicit-GEMM convolution takes this shape: 256+ output channels (half-empty 256-wide tiles at 128
+    lost to MIOpen: 59.5 vs 47.4 us at 28^2, profiles/r6_conv3x3_fwd.txt)."""
+    from ..ops._lib import native
+
+    return (config.get().conv3x3_fwd == "vcx" and cout % 256 == 0
+            and bool(native().gemm_f_conv3x3_supported(imgs, H, W, cin, cout, stride)))
+
+
 class _Conv3x3(torch.autograd.Function):
-    """3x3 convolution (pad 1) with MIOpen's forward and input gradient and the weight gradient on the
-    hand-written gemm_wg (csrc/kernels/gemm_wg.hip, the patch matrix of x gathered while staging): written
-    straight into the parameter's flat .grad when it has one (channels-last [Cout][ky][kx][Cin] storage)."""
+    """3x3 convolution (pad 1). Forward and stride-1 input gradient on gemm_f's implicit GEMM
+    (csrc/kernels/gemm_f.hip CONV: the patch matrix gathered by the LDS-DMA's per-lane offsets; the input gradient
+    as the forward convolution of dy with the flipped, transposed weights) where it measured faster than MIOpen,
+    MIOpen's otherwise; the weight gradient on gemm_wg (csrc/kernels/gemm_wg.hip, the patch matrix of x gathered
+    while staging), written straight into the parameter's flat .grad when it has one (channels-last
+    [Cout][ky][kx][Cin] storage)."""
 
     @staticmethod
-    def forward(ctx, x, w, stride):
+    def forward(ctx, x, w, stride, wg=True):
+        from ..ops._lib import native
+
         ctx.save_for_backward(x, w)
-        ctx.stride = stride
+        ctx.stride, ctx.wg = stride, wg
+        imgs, cin, H, W = x.shape
+        cout = w.shape[0]
+        if _fwd_vcx(imgs, H, W, cin, cout, stride):
+            Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+            y = torch.empty(imgs, Ho, Wo, cout, device=x.device, dtype=x.dtype)
+            native().gemm_f_conv3x3(x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1), y, stride)
+            return y.permute(0, 3, 1, 2)  # channels-last NCHW view
         return F.conv2d(x, w, None, stride, 1)
 
     @staticmethod
@@ -75,10 +97,20 @@ class _Conv3x3(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
-                                                     [True, False, False])[0]
+            imgs, cin, H, W = x.shape
+            if s == 1 and _fwd_vcx(imgs, H, W, w.shape[0], cin, 1):
+                # dx = conv(dy, W') with W'[ci][ky][kx][co] = W[co][ci][2 - ky][2 - kx] (a weight-sized copy)
+                dxh = torch.empty(imgs, H, W, cin, device=x.device, dtype=x.dtype)
+                native().gemm_f_conv3x3(dy.permute(0, 2, 3, 1), w.flip(2, 3).permute(1, 2, 3, 0).contiguous(), dxh, 1)
+                dx = dxh.permute(0, 3, 1, 2)
+            else:
+                dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                         [True, False, False])[0]
         dw = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and not ctx.wg:
+            dw = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1]
+        elif ctx.needs_input_grad[1]:
             cout = w.shape[0]
             g = w.grad
             dyh, xh = dy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1)  # contiguous NHWC views
@@ -89,12 +121,13 @@ class _Conv3x3(torch.autograd.Function):
                 d2 = torch.empty(cout, 3, 3, w.shape[1], device=w.device, dtype=w.dtype)
                 native().gemm_wg_conv3x3(dyh, xh, d2.view(cout, -1), False, s)
                 dw = d2.permute(0, 3, 1, 2)
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class Conv3x3(nn.Conv2d):
-    """3x3 convolution, pad 1 (the bottleneck's conv2): nn.Conv2d, whose weight gradient runs on gemm_wg where
-    the shape tiles (config.conv3x3_wgrad; ResNet-50 stages 3 and 4 at B=128)."""
+    """3x3 convolution, pad 1 (the bottleneck's conv2): nn.Conv2d whose weight gradient runs on gemm_wg, and forward
+    and stride-1 input gradient on gemm_f, where the shape tiles (config.conv3x3_wgrad / conv3x3_fwd; ResNet-50
+    stages 3 and 4 at B=128)."""
 
     def __init__(self, cin, cout, stride=1):
         super().__init__(cin, cout, 3, stride=stride, padding=1, bias=False)
@@ -116,6 +149,11 @@ class Conv3x3(nn.Conv2d):
     def forward(self, x):
         if self.vcx_wgrad(x):
             return _Conv3x3.apply(x, self.weight, self.stride[0])
+        if (x.is_cuda and x.dtype == torch.bfloat16 and self.weight.dtype == torch.bfloat16
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and self.weight.is_contiguous(memory_format=torch.channels_last)
+                and _fwd_vcx(x.shape[0], x.shape[2], x.shape[3], x.shape[1], self.out_channels, self.stride[0])):
+            return _Conv3x3.apply(x, self.weight, self.stride[0], False)  # MIOpen weight gradient
         return super().forward(x)
 
 

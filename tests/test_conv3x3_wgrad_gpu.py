@@ -77,3 +77,29 @@ def test_resnet_conv3x3_module_grads(gpu, preset_grad):
     want_w = wr.grad + (g0.float() if preset_grad else 0)
     assert _rel(m.weight.grad, want_w) < 1e-2
     assert _rel(x.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("fwd,wgrad,stride", [("vcx", "vcx", 1), ("vcx", "lib", 1), ("lib", "vcx", 1),
+                                              ("vcx", "vcx", 2), ("vcx", "lib", 2)])
+def test_resnet_conv3x3_module_on_gemm_f(gpu, fwd, wgrad, stride):
+    """models/resnet.Conv3x3 with the forward (and, at stride 1, the input gradient) on gemm_f's implicit GEMM
+    in every combination with the weight-gradient path: output, input and weight gradients against fp32."""
+    from distributedvolunteercomputing_amd import config
+    from distributedvolunteercomputing_amd.models.resnet import Conv3x3
+
+    torch.manual_seed(5 + stride)
+    m = Conv3x3(256, 256, stride=stride).to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(8, 256, 14, 14, device=gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x.requires_grad_()
+    Ho = (14 - 1) // stride + 1
+    r = torch.randn(8, 256, Ho, Ho, device=gpu)
+    with config.override(conv3x3_fwd=fwd, conv3x3_wgrad=wgrad):
+        y = m(x)
+        (y.float() * r).sum().backward()
+    xr = x.detach().float().requires_grad_()
+    wr = m.weight.detach().float().requires_grad_()
+    yr = F.conv2d(xr, wr, None, stride, 1)
+    (yr * r).sum().backward()
+    assert _rel(y, yr) < 1e-2
+    assert _rel(m.weight.grad, wr.grad) < 1e-2
+    assert _rel(x.grad, xr.grad) < 1e-2

@@ -90,3 +90,88 @@ def test_linear_on_gemm_f_matches_library(gpu):
         w.grad = b.grad = None
     for a, r in zip(outs["vcx"], outs["lib"]):
         assert (a - r).abs().max().item() < 1e-2 * r.abs().max().item()
+
+
+@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("imgs,H,W,Cin,Cout,stride", [(2, 9, 7, 64, 128, 1), (3, 8, 8, 128, 256, 2),
+                                                      (1, 7, 7, 512, 128, 1), (5, 5, 6, 64, 384, 2),
+                                                      (2, 14, 14, 256, 256, 1)])
+def test_gemm_f_conv3x3_matches_fp32(gpu, imgs, H, W, Cin, Cout, stride, waves):
+    """gemm_f's implicit-GEMM mode (the patch matrix gathered by the LDS-DMA's per-lane offsets, padding taps
+    as zeros) against an fp32 convolution: borders, odd and non-square images, stride 2, a ragged last row
+    tile, with and without bias."""
+    import torch.nn.functional as F
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    assert C.gemm_f_conv3x3_supported(imgs, H, W, Cin, Cout, stride)
+    torch.manual_seed(imgs * H + Cin + stride)
+    x = torch.randn(imgs, H, W, Cin, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(Cout, 3, 3, Cin, device="cuda") / (3 * Cin ** 0.5)).to(torch.bfloat16)
+    bias = torch.randn(Cout, device="cuda", dtype=torch.bfloat16)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), stride=stride, padding=1)
+    ref = ref.permute(0, 2, 3, 1)
+    y = torch.full((imgs, Ho, Wo, Cout), float("nan"), device="cuda", dtype=torch.bfloat16)
+    C.gemm_f_conv3x3(x, w, y, stride, None, waves)
+    torch.cuda.synchronize()
+    assert (y.float() - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
+    C.gemm_f_conv3x3(x, w, y, stride, bias, waves)
+    torch.cuda.synchronize()
+    ref = ref + bias.float()
+    assert (y.float() - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
+
+
+def test_gemm_f_conv3x3_refusals(gpu):
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    assert not C.gemm_f_conv3x3_supported(2, 8, 8, 96, 128, 1)   # Cin not a power of two
+    assert not C.gemm_f_conv3x3_supported(2, 8, 8, 32, 128, 1)   # Cin < 64
+    assert not C.gemm_f_conv3x3_supported(2, 8, 8, 64, 64, 1)    # Cout % 128
+    assert not C.gemm_f_conv3x3_supported(2, 8, 8, 64, 128, 3)   # stride
+    x = torch.randn(2, 8, 8, 64, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(128, 3, 3, 64, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        C.gemm_f_conv3x3(x, w, torch.empty(2, 8, 8, 128, device="cuda", dtype=torch.bfloat16), 2)  # wrong out shape
+
+
+@pytest.mark.parametrize("splits", [2, 4, -1])
+def test_gemm_f_split_k_matches_fp32(gpu, splits):
+    """Split-K (fp32 partials per split, summed with the bias by splitk_bias_kernel): explicit and automatic
+    split counts, ragged M, a 128-column last panel, strided output rows."""
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    torch.manual_seed(11 + splits)
+    M, N, K = 700, 640, 1536
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.03
+    bias = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+    wide = torch.full((M, N + 64), float("nan"), device="cuda", dtype=torch.bfloat16)
+    c = wide[:, :N]
+    C.gemm_f(a, b, c, bias, 8, splits)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().t() + bias.float()
+    assert (c.float() - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
+    assert torch.isnan(wide[:, N:].float()).all()
+    assert C.gemm_f_splits(M, N, K) > 1  # 9 tiles: split to fill the CUs
+    with pytest.raises(RuntimeError):
+        C.gemm_f(a, b, c, bias, 8, 5)  # 48 slices do not split into 5 even parts
+
+
+def test_gemm_f_conv3x3_split_k(gpu):
+    """The deep-K, few-tile convolutions of ResNet-50 stage 4 take the automatic split."""
+    import torch.nn.functional as F
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    torch.manual_seed(2)
+    x = torch.randn(4, 7, 7, 512, device="cuda", dtype=torch.bfloat16)
+    w = (torch.randn(512, 3, 3, 512, device="cuda") / 70).to(torch.bfloat16)
+    y = torch.empty(4, 7, 7, 512, device="cuda", dtype=torch.bfloat16)
+    assert C.gemm_f_splits(4 * 49, 512, 9 * 512) > 1
+    C.gemm_f_conv3x3(x, w, y, 1)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), padding=1).permute(0, 2, 3, 1)
+    assert (y.float() - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
