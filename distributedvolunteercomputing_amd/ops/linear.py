@@ -183,7 +183,10 @@ def gemm_wg_ok(M: int, N: int, K: int, t) -> bool:
     (profiles/r5_gemm_wg.txt). An output of one round of tiles (129..256) runs unsplit: Llama-3-8B's q / o
     projections ([4096, 4096] from 4096 tokens) 129.7 vs 146.5 us on the library; its k / v (4 splits) and
     gate / up / down (896 tiles) lost 5-11 % and stay on the library (profiles/r6_llama_wgrad.txt). The GPT-2
-    LM heads ([50304, 768 | 1024], K <= 1024) take gemm_wg with 1..4 splits (config.wgrad_wide)."""
+    LM heads ([50304, 768 | 1024], K <= 1024) take gemm_wg with 1..4 splits (config.wgrad_wide).
+    Memory: the binding allocates the fp32 split partials [splits, N, K] per call from the caching allocator --
+    a transient 618 MB for the GPT-2-small LM head at 4 splits (824 MB at GPT-2-medium), a few MB elsewhere;
+    under a hipGraph capture it is one fixed pool allocation."""
     cfg = config.get()
     tiles = ((N + 255) // 256) * (K // 256)
     wide = cfg.wgrad_wide and K <= 1024 and M >= 32768 and tiles > 128
