@@ -38,3 +38,29 @@ def test_update_override_and_consumers():
     with pytest.raises(ValueError):
         config.update(p2p_backend="mpi")
     assert "VCX_GEMM" in config.describe()
+
+
+def test_round6_compute_path_flags():
+    """VCX_GEMM_FWD (forward GEMMs on gemm_f, opt-in) and VCX_CONV3X3_FWD (the stage-3/4 3x3 convolutions on
+    gemm_f's implicit GEMM, default): parsed, validated, and refused by the CPU-side gates."""
+    import torch
+
+    import importlib
+
+    from distributedvolunteercomputing_amd.models import resnet
+
+    linear = importlib.import_module("distributedvolunteercomputing_amd.ops.linear")
+    c = config.from_env({"VCX_GEMM_FWD": "vcx", "VCX_CONV3X3_FWD": "lib"})
+    assert c.gemm_fwd == "vcx" and c.conv3x3_fwd == "lib"
+    d = config.RuntimeConfig()
+    assert d.gemm_fwd == "lib" and d.conv3x3_fwd == "vcx"
+    for env in ({"VCX_GEMM_FWD": "hipblaslt"}, {"VCX_CONV3X3_FWD": "miopen"}):
+        with pytest.raises(ValueError):
+            config.from_env(env)
+    with config.override(gemm_fwd="vcx"):
+        assert not linear.gemm_f_ok(65536, 2304, 768, torch.zeros(2, 2, dtype=torch.bfloat16))  # CPU tensor
+    with config.override(conv3x3_fwd="lib"):
+        assert not resnet._fwd_vcx(128, 14, 14, 256, 256, 1)  # off: no native call made
+    m = resnet.Conv3x3(64, 256).to(torch.bfloat16)
+    x = torch.randn(1, 64, 6, 6, dtype=torch.bfloat16)
+    assert m(x).shape == (1, 256, 6, 6)  # CPU: nn.Conv2d
