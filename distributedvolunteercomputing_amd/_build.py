@@ -116,6 +116,16 @@ def _linked(out: Path, d: str):
     (BUILD / (out.name + ".digest")).write_text(d)
 
 
+# Per-file compiler flags. attention.hip: no SLP vectorisation. The SLP vectorizer packs adjacent scalar f32
+# adds / multiplies of the softmax and dS = P (dP - delta) into v_pk_add_f32 / v_pk_mul_f32, which cost ~22-26
+# cycles more than the scalar pair when issued between MFMAs (MI355X_MICROARCH.md, "price of one filler beside
+# MFMAs"); without it the dK/dV tile body issues scalar ops only and the 3-wave forward stops spilling: forward
+# 0.184-0.188 vs 0.192 ms, backward 0.557-0.559 vs 0.573-0.577, bench 1071-1073 vs 1060-1062 samples/s, outputs
+# identical (profiles/r6_attention_noslp.txt). Measured and not applied: attention_hm.hip (Llama GQA backward
+# 0.555 vs 0.541 ms), gemm_ps.hip + gemm.hip (bench 1086-1089 vs 1090-1091).
+FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
+
+
 def build_C(nproc: int = 8, force: bool = False) -> Path:
     hipcc = _hipcc()
     inc, libdir, abi = _torch_flags()
@@ -129,8 +139,9 @@ def build_C(nproc: int = 8, force: bool = False) -> Path:
     jobs, objs = [], []
     for src in sorted((CSRC / "kernels").glob("*.hip")):
         obj = BUILD / (src.stem + ".hip.o")
-        stamp = _digest([src] + headers, " ".join(kern_flags))
-        jobs.append((src.name, [hipcc, *kern_flags, "-c", str(src), "-o", str(obj)], obj, stamp))
+        flags = kern_flags + FILE_FLAGS.get(src.name, [])
+        stamp = _digest([src] + headers, " ".join(flags))
+        jobs.append((src.name, [hipcc, *flags, "-c", str(src), "-o", str(obj)], obj, stamp))
         objs.append(obj)
     for src in sorted(CSRC.glob("bindings*.cpp")):
         obj = BUILD / (src.stem + ".cpp.o")
