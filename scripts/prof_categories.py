@@ -7,6 +7,7 @@ import re
 import sys
 
 CATS = [  # first match wins
+    ("implicit-GEMM conv / forward GEMM (HIP gemm_f)", r"gemm_f::|gemm_f_kernel"),
     ("BN (HIP batchnorm.hip)", r"vcx::bn::|stats_kernel|finalize_kernel|apply_kernel|bwd_reduce_kernel|bwd_dx_kernel"),
     ("max-pool (HIP)", r"maxpool"),
     ("weight-gradient GEMM (HIP gemm_wg)", r"gemm_wg"),
