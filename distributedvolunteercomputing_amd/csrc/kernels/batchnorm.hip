@@ -18,6 +18,7 @@
 // writes back / invalidates the XCD's L2; not profiled further): profiles/r4_resnet50_ab.txt.)
 // Rows R = N * H * W, C channels (a power of two, 8 .. 2048); every lane moves 16 B (8 channels) per
 // access. No reference analog (north-star config 3).
+#include <cstdio>
 #include <cstdlib>
 #include <string>
 
@@ -45,12 +46,12 @@ struct Unroll {
 // body(off, step, Unroll<U>, s0, s1) handles the U rows off, off + step, ...: the main loop passes
 // U = 4 so every lane keeps 4 row loads per operand in flight (one at a time left these passes at
 // 2-3 TB/s, latency-bound: profiles/r5_cfg3_resnet50_categories.txt)
-template <int UR, typename F>
+template <int UR, int BT, typename F>
 __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&& body, float* out0, float* out1) {
-  __shared__ float red[2][NT][9];  // [quantity][thread][8 channels + pad]
+  __shared__ float red[2][BT][9];  // [quantity][thread][8 channels + pad]
   const int tid = threadIdx.x;
   const int cpr = C / 8;                // chunks per row
-  const int rpp = NT / cpr;             // rows per pass (>= 1)
+  const int rpp = BT / cpr;             // rows per pass (>= 1)
   const int ch = tid % cpr, rr = tid / cpr;
   float s0[8], s1[8];
 #pragma unroll
@@ -68,7 +69,7 @@ __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&
   }
   __syncthreads();
   // thread t < C: channel t = chunk t / 8, element t % 8, summed over the rpp row slots
-  for (int c = tid; c < C; c += NT) {
+  for (int c = tid; c < C; c += BT) {
     const int k = c / 8, e = c % 8;
     float a = 0.f, b = 0.f;
     for (int q = 0; q < rpp; ++q) {
@@ -83,13 +84,13 @@ __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&
 // sums of (x - k) and (x - k)^2 with a per-channel pivot k = x[row 0] (the same for every block):
 // E[x^2] - m^2 on raw fp32 sums cancels catastrophically when |mean| >> std over millions of rows;
 // shifted by a value of the batch, the sums are O(R std^2) and the variance keeps its digits
-template <int UR>
-__global__ void __launch_bounds__(NT) stats_kernel(const bf16* __restrict__ x, int64_t R, int C, int64_t rows_per_block,
+template <int UR, int BT>
+__global__ void __launch_bounds__(BT) stats_kernel(const bf16* __restrict__ x, int64_t R, int C, int64_t rows_per_block,
                                                    float* __restrict__ sum, float* __restrict__ sumsq) {
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(R, r0 + rows_per_block);
   float k[8];
   load8(x + (threadIdx.x % (C / 8)) * 8, k);
-  channel_reduce<UR>(
+  channel_reduce<UR, BT>(
       C, r0, r1,
       [&](int64_t off, int64_t step, auto u, float(&s0)[8], float(&s1)[8]) {
         constexpr int U = decltype(u)::value;
@@ -245,8 +246,8 @@ __global__ void __launch_bounds__(NT) apply_kernel(const bf16* __restrict__ x, c
 }
 
 // backward reductions: sum dz and sum dz * xhat per channel, dz = dy [* mask]
-template <bool RELU, int UR>
-__global__ void __launch_bounds__(NT) bwd_reduce_kernel(const bf16* __restrict__ dy, const unsigned char* __restrict__ mask,
+template <bool RELU, int UR, int BT>
+__global__ void __launch_bounds__(BT) bwd_reduce_kernel(const bf16* __restrict__ dy, const unsigned char* __restrict__ mask,
                                                         const bf16* __restrict__ x, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, int64_t R, int C,
                                                         int64_t rows_per_block, float* __restrict__ sdz,
@@ -259,7 +260,7 @@ __global__ void __launch_bounds__(NT) bwd_reduce_kernel(const bf16* __restrict__
     m[i] = mean[ch + i];
     rs[i] = rstd[ch + i];
   }
-  channel_reduce<UR>(
+  channel_reduce<UR, BT>(
       C, r0, r1,
       [&](int64_t off, int64_t step, auto u, float(&s0)[8], float(&s1)[8]) {
         constexpr int U = decltype(u)::value;
@@ -442,30 +443,38 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_kernel(const bf16* __restrict_
   }
 }
 
-// reduction geometry (rows in flight per lane, target block count, minimum passes per block), config 3
-// same box (gpurun_out/c16, c17): VCX_BN_REDUCE = "8n" (default: 8 deep, ~1024 blocks of >= 32 passes;
+// reduction geometry (rows in flight per lane, target block count, minimum passes per block, threads per block).
+// Round 6 default "w512q": 8 deep, ~256 blocks of 512 threads -- a quarter of the blocks, so a quarter of the
+// per-block atomics into the layer's sums, which cost the statistics pass a third of its time at 1024 blocks
+// (profiles/r6_bn_kernels.txt: stats 257.5 -> 200.0 us, reductions 420 -> 392 us per set of ResNet-50 shapes;
+// config 3 9306 / 9318 vs 9222 / 9164 img/s, same box, interleaved). Round 5, config 3
+// same box (gpurun_out/c16, c17): VCX_BN_REDUCE = "8n" (8 deep, ~1024 blocks of >= 32 passes;
 // 8629-8722 img/s), "4" (4 deep, ~1024 blocks: 8556-8562), "8" (8 deep, ~2048 blocks of >= 16: 2 % under
 // "4"), "4w" (4 deep, ~2048 blocks: 8380-8386) -- more blocks cost more than the small late layers gain
 // (every block adds its partial sums into the workspace) -- and "8h" (8 deep, ~512 blocks)
 struct ReduceGeo {
-  int unroll, target, min_passes;
+  int unroll, target, min_passes, threads = 256;
 };
 inline const ReduceGeo& reduce_geo() {
   static const ReduceGeo g = [] {
     const char* e = std::getenv("VCX_BN_REDUCE");
-    const std::string v = e ? e : "8n";
+    const std::string v = e ? e : "w512q";
     if (v == "8") return ReduceGeo{8, 2048, 16};
     if (v == "4") return ReduceGeo{4, 1024, 32};
     if (v == "4w") return ReduceGeo{4, 2048, 16};
     if (v == "8h") return ReduceGeo{8, 512, 32};
-    return ReduceGeo{8, 1024, 32};
+    if (v == "w512") return ReduceGeo{8, 512, 32, 512};
+    if (v == "8n") return ReduceGeo{8, 1024, 32};
+    if (v != "w512q") std::fprintf(stderr, "[vcx] VCX_BN_REDUCE=%s unknown, using w512q\n", v.c_str());
+    return ReduceGeo{8, 256, 32, 512};
   }();
   return g;
 }
 inline int reduce_unroll() { return reduce_geo().unroll; }
+inline int reduce_threads() { return reduce_geo().threads; }
 inline int64_t rows_per_block(int64_t R, int C) {
   const ReduceGeo& geo = reduce_geo();
-  const int64_t rpp = NT / (C / 8), target = geo.target, min_passes = geo.min_passes;
+  const int64_t rpp = geo.threads / (C / 8), target = geo.target, min_passes = geo.min_passes;
   int64_t rpb = (R + target - 1) / target;
   rpb = ((rpb + rpp - 1) / rpp) * rpp;
   return rpb < min_passes * rpp ? min_passes * rpp : rpb;
@@ -494,10 +503,12 @@ void vcx_bn_fwd_train(const void* x, const void* res, void* y, void* mask, int64
   using namespace bn;
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
-  if (reduce_unroll() == 8)
-    hipLaunchKernelGGL(stats_kernel<8>, dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
+  if (reduce_threads() == 512)
+    hipLaunchKernelGGL((stats_kernel<8, 512>), dim3(nb), dim3(512), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
+  else if (reduce_unroll() == 8)
+    hipLaunchKernelGGL((stats_kernel<8, NT>), dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
   else
-    hipLaunchKernelGGL(stats_kernel<4>, dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
+    hipLaunchKernelGGL((stats_kernel<4, NT>), dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
   FinArgs fa{ws, (const bf16*)gamma, (const bf16*)beta, run_mean, run_var, run_fp32, eps, momentum, 1.f / (float)R, R,
              mean, rstd, scale, nbt};
   if (!layer_ws) {
@@ -557,14 +568,17 @@ void vcx_bn_bwd(const void* dy, const void* mask, const void* x, const float* me
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
   float* bws = layer_ws ? ws + 2 * C : ws;
+  const int bt = reduce_threads();
   auto red = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(NT), 0, s, (const bf16*)dy, (const unsigned char*)mask, (const bf16*)x, mean,
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(bt), 0, s, (const bf16*)dy, (const unsigned char*)mask, (const bf16*)x, mean,
                        rstd, R, C, rpb, bws, bws + C);
   };
-  if (reduce_unroll() == 8)
-    relu ? red(bwd_reduce_kernel<true, 8>) : red(bwd_reduce_kernel<false, 8>);
+  if (bt == 512)
+    relu ? red(bwd_reduce_kernel<true, 8, 512>) : red(bwd_reduce_kernel<false, 8, 512>);
+  else if (reduce_unroll() == 8)
+    relu ? red(bwd_reduce_kernel<true, 8, NT>) : red(bwd_reduce_kernel<false, 8, NT>);
   else
-    relu ? red(bwd_reduce_kernel<true, 4>) : red(bwd_reduce_kernel<false, 4>);
+    relu ? red(bwd_reduce_kernel<true, 4, NT>) : red(bwd_reduce_kernel<false, 4, NT>);
   if (!layer_ws)
     hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, C, sums, (bf16*)gw, (bf16*)gb);
   const float* sdz = layer_ws ? bws : sums;
