@@ -392,7 +392,7 @@ void gemm_f(at::Tensor a, at::Tensor b, at::Tensor out, c10::optional<at::Tensor
   TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && out.stride(1) == 1, "gemm_f: row-major operands");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm_f: shape mismatch");
-  TORCH_CHECK(vcx_gemm_f_supported((int)M, (int)N, (int)K), "gemm_f: needs N % 128 == 0, K % 64 == 0, K >= 192");
+  TORCH_CHECK(vcx_gemm_f_supported((int)M, (int)N, (int)K), "gemm_f: needs N % 128 == 0 or N == 64, K % 64 == 0, K >= 192");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "gemm_f: 16-B aligned rows");
   for (const at::Tensor* t : {&a, &b, &out})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_f: 16-B aligned base pointers");
@@ -431,7 +431,7 @@ void gemm_f_conv3x3(at::Tensor x, at::Tensor w, at::Tensor out, int64_t stride, 
   TORCH_CHECK(out.size(0) == imgs && out.size(1) == Ho && out.size(2) == Wo && out.size(3) == Cout,
               "gemm_f_conv3x3: out [N, Ho, Wo, Cout]");
   TORCH_CHECK(vcx_gemm_f_conv3x3_supported((int)imgs, (int)H, (int)W, (int)Cin, (int)Cout, (int)stride),
-              "gemm_f_conv3x3: needs Cin a power of two >= 64, Cout % 128 == 0, x under 2 GB");
+              "gemm_f_conv3x3: needs Cin a power of two >= 64, Cout % 128 == 0 or Cout == 64, x under 2 GB");
   const bool hb = bias && bias->defined();
   if (hb)
     TORCH_CHECK(bias->is_cuda() && bias->get_device() == x.get_device() && bias->numel() == Cout &&

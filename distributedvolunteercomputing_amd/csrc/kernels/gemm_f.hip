@@ -33,11 +33,9 @@ namespace gemm_f {
 typedef short sx8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 256, BN = 256, BKS = 32;
+constexpr int BM = 256, BKS = 32;
 constexpr int ROWB = BKS * 2;           // 64 B per row per slice
-constexpr int SLOT_A = BM * ROWB;       // 16 KB
-constexpr int SLOT = 2 * SLOT_A;        // 32 KB: A and B slices
-constexpr int STG_BYTES = 4 * SLOT;     // 128 KB output staging (the ring's first 4 slots)
+constexpr int SLOT_A = BM * ROWB;       // 16 KB: the A slice
 
 __device__ __forceinline__ int swz(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
 
@@ -63,22 +61,30 @@ __device__ __forceinline__ void wait_vm() {
 }
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-// WN waves along N, 2 along M: WN = 2 -> 4 waves of 128 x 128 (one wave per SIMD, 256 accumulator registers),
-// WN = 4 -> 8 waves of 128 x 64 (two waves per SIMD, 128)
-template <int WN>
+// Tile 256 x BNT, WM waves along M and WN along N: <2, 2, 256> = 4 waves of 128 x 128 (one wave per SIMD, 256
+// accumulator registers), <2, 4, 256> = 8 waves of 128 x 64 (two waves per SIMD, 128; the default),
+// <4, 2, 128> = 8 waves of 64 x 64 for 128 output columns (the 128-channel convolutions)
+template <int WM_, int WN_, int BNT_>
 struct Geo {
-  static constexpr int WAVES = 2 * WN, NT = 64 * WAVES;
-  static constexpr int TN = BN / WN;       // output columns per wave
-  static constexpr int JB = TN / 16;       // B fragments (column blocks) per wave
-  static constexpr int OPS = 32 / WAVES;   // LDS-DMA pieces per wave per slice (16 of A + 16 of B per slice)
-  static constexpr int RB = TN * 2;        // staged output row bytes
-  static constexpr int CPR = RB / 16;      // 16-B chunks per staged row
+  static constexpr int WM = WM_, WN = WN_, BNT = BNT_, WAVES = WM * WN, NT = 64 * WAVES;
+  static constexpr int TM = BM / WM, IB = TM / 16;  // output rows per wave, A fragments (row blocks) per wave
+  static constexpr int TN = BNT / WN, JB = TN / 16;  // output columns per wave, B fragments per wave
+  static constexpr int AOPS = 16 / WAVES, BOPS = BNT / 16 / WAVES;  // LDS-DMA pieces per wave per slice
+  static constexpr int OPS = AOPS + BOPS, OPG = (OPS + 3) / 4;      // ... and per MFMA group (first 4 groups)
+  static constexpr int SLOT = SLOT_A + BNT * ROWB;  // A and B slices
+  static constexpr int RB = TN * 2;                 // staged output row bytes
+  static constexpr int CPR = RB / 16;               // 16-B chunks per staged row
+  static_assert(AOPS * WAVES == 16 && BOPS * WAVES == BNT / 16 && JB <= IB && IB <= 8, "tile geometry");
 };
+using G4 = Geo<2, 2, 256>;
+using G8 = Geo<2, 4, 256>;
+using G8n = Geo<4, 2, 128>;
+using G4n = Geo<4, 1, 64>;  // 4 waves of 64 x 64 on a 256 x 64 tile (64 output channels; 2 workgroups per CU)
 
-template <int WN>
+template <class G>
 struct Frags {
-  sx8 a[8];                // A fragments: the wave's 8 row blocks of 16 (output rows)
-  sx8 b[Geo<WN>::JB];      // B fragments: the wave's column blocks of 16
+  sx8 a[G::IB];  // A fragments: the wave's row blocks of 16 (output rows)
+  sx8 b[G::JB];  // B fragments: the wave's column blocks of 16
 };
 
 // 3x3 convolution (pad 1) as an implicit GEMM: A = the patch matrix of NHWC x gathered while staging
@@ -91,14 +97,14 @@ struct Conv {
 // flight, measured even to 4 % slower: 236.3 vs 227.9 us qkv, 105.7 vs 104.4 sq4096)
 // CONV: A is NHWC x [imgs, H, W, Cin] and row m of the GEMM the output pixel m of [imgs, Ho, Wo]; K = 9 Cin in the
 // [ky][kx][Cin] order of the channels-last weight, each 32-deep slice inside one tap (Cin a power of two >= 64)
-template <int WN, int D, bool CONV>
-__global__ void __launch_bounds__(Geo<WN>::NT, 1)
+template <class G, int D, bool CONV>
+__global__ void __launch_bounds__(G::NT, 1)
     gemm_f_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, bf16* __restrict__ C,
                   const bf16* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int tilesN,
                   Conv cv, int splits, float* __restrict__ ws) {
-  using G = Geo<WN>;
   static_assert(D == 4, "the pipeline tail below is written for a 4-slot ring");
-  constexpr int JB = G::JB, OPS = G::OPS, HOPS = OPS / 2, WAVES = G::WAVES;
+  constexpr int IB = G::IB, JB = G::JB, OPS = G::OPS, AOPS = G::AOPS, WAVES = G::WAVES, WN = G::WN, TM = G::TM;
+  constexpr int BN = G::BNT, SLOT = G::SLOT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -128,12 +134,12 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   const int rowsA = min(BM, M - m0), rowsB = min(BN, N - n0);
   const u32x4 ra = CONV ? desc(A, cv.xbytes) : desc(A + (int64_t)m0 * lda, (unsigned)(((int64_t)(rowsA - 1) * lda + K) * 2));
   const u32x4 rb = desc(B + (int64_t)n0 * ldb, (unsigned)(((int64_t)(rowsB - 1) * ldb + K) * 2));
-  int va[HOPS], vb[HOPS];
+  int va[AOPS], vb[G::BOPS];
   // CONV: per A piece the lane's output pixel as the input pixel of tap (0, 0) -- (ih0, iw0) and its index pix0
   // (rows past M: ih0 = -4, never inside the image)
-  int ih0[HOPS], iw0[HOPS];
+  int ih0[AOPS], iw0[AOPS];
 #pragma unroll
-  for (int q = 0; q < HOPS; ++q) {
+  for (int q = 0; q < AOPS; ++q) {
     const int r = (wid + WAVES * q) * 16 + prow;
     if constexpr (CONV) {
       const int m = m0 + r, hw = cv.Ho * cv.Wo;
@@ -144,12 +150,16 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
     } else {
       va[q] = r < rowsA ? (r * lda + pch * 8) * 2 : 0x7fffff00;  // past the resource: returns 0
     }
+  }
+#pragma unroll
+  for (int q = 0; q < G::BOPS; ++q) {
+    const int r = (wid + WAVES * q) * 16 + prow;
     vb[q] = r < rowsB ? (r * ldb + pch * 8) * 2 : 0x7fffff00;
   }
-  auto stage_op = [&](int s, int o) {  // op o of slice s: A piece q = o (o < HOPS), B piece q = o - HOPS
+  auto stage_op = [&](int s, int o) {  // op o of slice s: A piece q = o (o < AOPS), B piece q = o - AOPS
     char* slot = smem + (s % D) * SLOT;
-    const int q = o % HOPS;
-    if (o < HOPS) {
+    const int q = o < AOPS ? o : o - AOPS;
+    if (o < AOPS) {
       if constexpr (CONV) {  // slice s = channels c0 .. c0 + 31 of tap t = (ky, kx); padding taps read zeros
         const int sg = ks0 + s;  // the global slice
         const int t = (sg * BKS) >> cv.lc, c0 = (sg * BKS) & ((1 << cv.lc) - 1);
@@ -174,15 +184,15 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   const int frow = lane & 15;
   const int foff = frow * ROWB + (((lane >> 4) ^ swz(frow)) << 4);
   auto afrag = [&](int s, int i) {
-    return *(const sx8*)(smem + (s % D) * SLOT + (wm * 128 + 16 * i) * ROWB + foff);
+    return *(const sx8*)(smem + (s % D) * SLOT + (wm * TM + 16 * i) * ROWB + foff);
   };
   auto bfrag = [&](int s, int j) {
     return *(const sx8*)(smem + (s % D) * SLOT + SLOT_A + (wn * G::TN + 16 * j) * ROWB + foff);
   };
 
-  f32x4 acc[8][JB];
+  f32x4 acc[IB][JB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < IB; ++i)
 #pragma unroll
     for (int j = 0; j < JB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -190,11 +200,11 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   // rotated them through 68 v_accvgpr_mov per 128 MFMAs): AGPRs at one wave per SIMD, VGPRs at two (the
   // unified file split 128 / 128 would not fit the fragments). An accumulate chain needs no wait states; the
   // epilogue's first reads are padded by hand (the MFMAs are invisible to hipcc's hazard recognizer).
-  auto mma_row = [&](const Frags<WN>& f, int i) {
+  auto mma_row = [&](const Frags<G>& f, int i) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int j = 0; j < JB; ++j) {
-      if constexpr (WN == 2)
+      if constexpr (G::WAVES == 4)
         asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(f.b[j]), "v"(f.a[i]));
       else
         asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[i][j]) : "v"(f.b[j]), "v"(f.a[i]));
@@ -207,16 +217,15 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   // groups (one output row block each), each followed by the reads of slice s + 1's fragments of that row (and
   // column) block into fn; the DMA ops ride along the first 4 groups (placing the second M half's in the last 4
   // measured even, 8 waves: 233.5 vs 234.3 us qkv, 109.2 vs 110.1 sq4096)
-  auto step = [&](int s, Frags<WN>& fc, Frags<WN>& fn, auto STAGE, auto PEND) {
+  auto step = [&](int s, Frags<G>& fc, Frags<G>& fn, auto STAGE, auto PEND) {
     wait_vm<decltype(PEND)::value>();
     barrier();
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
+    for (int g = 0; g < IB; ++g) {
       if constexpr (decltype(STAGE)::value) {
-        if (g < 4) {
 #pragma unroll
-          for (int o = 0; o < OPS / 4; ++o) stage_op(s + D, (OPS / 4) * g + o);
-        }
+        for (int o = G::OPG * g; o < G::OPG * (g + 1); ++o)
+          if (o < OPS) stage_op(s + D, o);
       }
       __builtin_amdgcn_sched_barrier(0);
       mma_row(fc, g);
@@ -233,13 +242,13 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   using P1 = std::integral_constant<int, OPS>;
   using P0 = std::integral_constant<int, 0>;
   const int nk = K / BKS / splits;  // slices per split: even, >= 6 (host)
-  Frags<WN> f0, f1;
+  Frags<G> f0, f1;
 #pragma unroll
   for (int t = 0; t < D; ++t) stage(t);
   wait_vm<(D - 1) * OPS>();  // slice 0 landed
   barrier();
 #pragma unroll
-  for (int g = 0; g < 8; ++g) f0.a[g] = afrag(0, g);
+  for (int g = 0; g < IB; ++g) f0.a[g] = afrag(0, g);
 #pragma unroll
   for (int j = 0; j < JB; ++j) f0.b[j] = bfrag(0, j);
   int s = 0;
@@ -253,7 +262,7 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   step(s + 1, f1, f0, F{}, P1{});
   step(s + 2, f0, f1, F{}, P0{});
 #pragma unroll
-  for (int g = 0; g < 8; ++g) mma_row(f1, g);
+  for (int g = 0; g < IB; ++g) mma_row(f1, g);
 
   // ---- epilogue: acc[i][j] = C[wm 128 + 16 i + (l & 15)][wn TN + 16 j + 4 (l >> 4) .. + 3]. Each wave stages
   // its 128 x TN bf16 block in its own part of the ring (RB-byte rows, 16-B chunks XOR-swizzled by the row),
@@ -263,10 +272,10 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   __syncthreads();  // every wave is past its last fragment read; every DMA retired (vmcnt(0) of the last step)
   if (n0 + wn * G::TN >= N) return;  // the missing half of a 128-column last panel (no barrier follows)
   if (splits > 1) {  // fp32 partial straight from the accumulators (splitk_bias_kernel sums them)
-    float* const wb = ws + ((int64_t)split * M + m0 + wm * 128) * N + n0 + wn * G::TN + 4 * (lane >> 4);
-    const int mrem = M - (m0 + wm * 128);
+    float* const wb = ws + ((int64_t)split * M + m0 + wm * TM) * N + n0 + wn * G::TN + 4 * (lane >> 4);
+    const int mrem = M - (m0 + wm * TM);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < IB; ++i) {
       const int r = 16 * i + (lane & 15);
       if (r < mrem) {
 #pragma unroll
@@ -276,7 +285,7 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
     return;
   }
   constexpr int RB = G::RB, CPR = G::CPR;
-  char* const stg = smem + wid * (128 * RB);
+  char* const stg = smem + wid * (TM * RB);
   float bv[JB][4];  // the bias of the lane's output columns (zeros without one)
 #pragma unroll
   for (int j = 0; j < JB; ++j) {
@@ -286,7 +295,7 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
     for (int t = 0; t < 4; ++t) bv[j][t] = (float)b4[t];
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < IB; ++i) {
     const int r = 16 * i + (lane & 15);
 #pragma unroll
     for (int j = 0; j < JB; ++j) {
@@ -299,10 +308,10 @@ __global__ void __launch_bounds__(Geo<WN>::NT, 1)
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads back only its own block
   const int k = lane % CPR;
-  const int mrem = M - (m0 + wm * 128);
-  bf16* const base = C + (int64_t)(m0 + wm * 128) * ldc + n0 + wn * G::TN + k * 8;
+  const int mrem = M - (m0 + wm * TM);
+  bf16* const base = C + (int64_t)(m0 + wm * TM) * ldc + n0 + wn * G::TN + k * 8;
 #pragma unroll 8
-  for (int it = 0; it < 2 * CPR; ++it) {
+  for (int it = 0; it < TM / (64 / CPR); ++it) {
     const int r = it * (64 / CPR) + lane / CPR;
     const bf16x8 v = *(const bf16x8*)(stg + r * RB + ((k ^ (r & (CPR - 1))) << 4));
     if (r < mrem) __builtin_nontemporal_store(v, (bf16x8*)(base + (int64_t)r * ldc));
@@ -325,18 +334,19 @@ __global__ void __launch_bounds__(256) splitk_bias_kernel(const float* __restric
   *(bf16x4*)(C + (int64_t)m * ldc + n) = r;
 }
 
-template <int WN, int D, bool CONV = false>
+template <class G, int D, bool CONV = false>
 void launch(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda, int ldb, int ldc,
             int splits, float* ws, hipStream_t s, Conv cv = {}) {
-  constexpr int LDS_BYTES = D * SLOT;
+  // the ring, and the output staging (a TM x TN block per wave) inside it
+  constexpr int LDS_BYTES = D * G::SLOT > G::WAVES * G::TM * G::RB ? D * G::SLOT : G::WAVES * G::TM * G::RB;
   static const bool attrs = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_f_kernel<WN, D, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm_f_kernel<G, D, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_BYTES);
     return true;
   }();
   (void)attrs;
-  const int tilesN = (N + BN - 1) / BN, tiles = ((M + BM - 1) / BM) * tilesN;
-  hipLaunchKernelGGL((gemm_f_kernel<WN, D, CONV>), dim3(tiles * splits), dim3(Geo<WN>::NT), LDS_BYTES, s,
+  const int tilesN = (N + G::BNT - 1) / G::BNT, tiles = ((M + BM - 1) / BM) * tilesN;
+  hipLaunchKernelGGL((gemm_f_kernel<G, D, CONV>), dim3(tiles * splits), dim3(G::NT), LDS_BYTES, s,
                      (const bf16*)A, (const bf16*)B, (bf16*)C, (const bf16*)bias, M, N, K, lda, ldb, ldc, tilesN, cv,
                      splits, ws);
   if (splits > 1)
@@ -352,7 +362,8 @@ using namespace vcx;
 bool vcx_gemm_f_supported(int M, int N, int K) {
   // N a multiple of 128 (a wave's columns are all in or all out), K a multiple of 64 and >= 192 (even slice
   // count, 3-deep ring), operand panels under 2 GB (32-bit buffer offsets)
-  return M > 0 && N > 0 && N % 128 == 0 && K % 64 == 0 && K >= 192 && (int64_t)256 * K * 2 < (int64_t(1) << 31);
+  return M > 0 && N > 0 && (N % 128 == 0 || N == 64) && K % 64 == 0 && K >= 192 &&
+         (int64_t)256 * K * 2 < (int64_t(1) << 31);
 }
 
 bool vcx_gemm_f_split_ok(int M, int N, int K, int splits) {
@@ -363,21 +374,26 @@ bool vcx_gemm_f_split_ok(int M, int N, int K, int splits) {
 // K splits for an output of fewer tiles than CUs: the largest count that keeps splits x tiles within one round
 // of 256 workgroups and each split's slice count even and >= 6 (1: no split)
 int vcx_gemm_f_splits(int M, int N, int K) {
-  const int tiles = ((M + gemm_f::BM - 1) / gemm_f::BM) * ((N + gemm_f::BN - 1) / gemm_f::BN);
+  const int bn = N <= 64 ? 64 : N <= 128 ? 128 : 256;  // the tile width vcx_gemm_f launches
+  const int tiles = ((M + gemm_f::BM - 1) / gemm_f::BM) * ((N + bn - 1) / bn);
   int best = 1;
   for (int s = 2; s <= 16 && tiles * s <= 256; ++s)
     if (vcx_gemm_f_split_ok(M, N, K, s)) best = s;
   return best;
 }
 
-// waves: 4 (128 x 128 per wave) or 8 (128 x 64 per wave); anything else = the default (8). splits > 1: ws holds
-// splits x M x N fp32 partials
+// waves: 4 (128 x 128 per wave) or 8 (128 x 64 per wave); anything else = the default (8); N = 128: 8 waves of
+// 64 x 64 on a 256 x 128 tile; N = 64: 4 waves of 64 x 64 on a 256 x 64 tile. splits > 1: ws holds splits x M x N fp32 partials
 void vcx_gemm_f(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda, int ldb,
                 int ldc, int waves, int splits, float* ws, hipStream_t s) {
-  if (waves == 4)
-    gemm_f::launch<2, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, splits, ws, s);
+  if (N <= 64)  // the narrow tiles first: a 256-wide tile's waves store whole 64 / 128-column blocks
+    gemm_f::launch<gemm_f::G4n, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, splits, ws, s);
+  else if (N <= 128)
+    gemm_f::launch<gemm_f::G8n, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, splits, ws, s);
+  else if (waves == 4)
+    gemm_f::launch<gemm_f::G4, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, splits, ws, s);
   else
-    gemm_f::launch<4, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, splits, ws, s);
+    gemm_f::launch<gemm_f::G8, 4>(A, B, C, bias, M, N, K, lda, ldb, ldc, splits, ws, s);
 }
 
 static int log2_exact(int v) {
@@ -391,7 +407,7 @@ bool vcx_gemm_f_conv3x3_supported(int imgs, int H, int W, int Cin, int Cout, int
   // x under 2 GB (32-bit offsets), output rows in int
   const int lc = log2_exact(Cin);
   const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
-  return imgs > 0 && H > 0 && W > 0 && lc >= 6 && Cout % 128 == 0 && (stride == 1 || stride == 2) &&
+  return imgs > 0 && H > 0 && W > 0 && lc >= 6 && (Cout % 128 == 0 || Cout == 64) && (stride == 1 || stride == 2) &&
          (int64_t)imgs * H * W * Cin * 2 < (int64_t(1) << 31) - (int64_t(1) << 20) && imgs * Ho * Wo < (int64_t(1) << 31) &&
          vcx_gemm_f_supported(1, Cout, 9 * Cin);
 }
@@ -408,8 +424,12 @@ void vcx_gemm_f_conv3x3(const void* x, const void* w, void* y, const void* bias,
   cv.stride = stride;
   cv.xbytes = (unsigned)((int64_t)imgs * H * W * Cin * 2);
   const int M = imgs * cv.Ho * cv.Wo, K = 9 * Cin;
-  if (waves == 4)
-    gemm_f::launch<2, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
+  if (Cout <= 64)
+    gemm_f::launch<gemm_f::G4n, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
+  else if (Cout <= 128)
+    gemm_f::launch<gemm_f::G8n, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
+  else if (waves == 4)
+    gemm_f::launch<gemm_f::G4, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
   else
-    gemm_f::launch<4, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
+    gemm_f::launch<gemm_f::G8, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
 }

@@ -5,8 +5,9 @@ Channels-last bf16. The 1x1 convolutions (about 70 % of the FLOPs) are plain GEM
 view -- [N*H*W, Cin] x [Cout, Cin]^T -- and run through the framework's linear layer (library
 GEMMs picked per shape, split-M weight gradients summed straight into the flat gradient buffer);
 stride-2 ones subsample the NHWC view first. The 3x3 convolutions of stages 3 and 4 run forward, input
-gradient (stride 1) and weight gradient on the hand-written gemm_f / gemm_wg kernels, the others and the 7x7 stem
-through MIOpen's NHWC kernels. Train-mode BatchNorm runs fused with its ReLU and the residual add (ops/batchnorm.py,
+gradient (stride 1) on the hand-written gemm_f implicit GEMM (every stage) and, at stages 3 / 4, their weight
+gradients on gemm_wg; the stride-2 input gradients, the stage-1/2 weight gradients and the 7x7 stem run MIOpen's
+NHWC kernels. Train-mode BatchNorm runs fused with its ReLU and the residual add (ops/batchnorm.py,
 csrc/kernels/batchnorm.hip). BatchNorm statistics are buffers that the trainers average at every
 synchronisation.
 """
@@ -57,12 +58,15 @@ class Conv1x1(nn.Conv2d):
 
 
 def _fwd_vcx(imgs, H, W, cin, cout, stride) -> bool:
-    """gemm_f's implicit-GEMM convolution takes this shape: 256+ output channels (half-empty 256-wide tiles at 128
-    lost to MIOpen: 59.5 vs 47.4 us at 28^2, profiles/r6_conv3x3_fwd.txt)."""
+    """gemm_f's implicit-GEMM convolution takes this shape: every ResNet-50 3x3 convolution (64 / 128 channels on its
+    256 x 64 / 256 x 128 tiles, 256+ on 256 x 256 with split-K where few tiles; 1.09-1.38x MIOpen forward and
+    stride-1 input gradient at every stage, profiles/r6_conv3x3_fwd.txt)."""
     from ..ops._lib import native
 
-    return (config.get().conv3x3_fwd == "vcx" and cout % 256 == 0
-            and bool(native().gemm_f_conv3x3_supported(imgs, H, W, cin, cout, stride)))
+    import os
+    if cout < int(os.environ.get("VCX_CONV3X3_FWD_MINC", "0")):  # TEMP A/B
+        return False
+    return config.get().conv3x3_fwd == "vcx" and bool(native().gemm_f_conv3x3_supported(imgs, H, W, cin, cout, stride))
 
 
 class _Conv3x3(torch.autograd.Function):

@@ -1,4 +1,5 @@
-"""Forward GEMM in the library's geometry (csrc/kernels/gemm_f.hip: 256 x 256 tiles, 4 waves of 128 x 128 or 8 of 128 x 64)
+"""Forward GEMM in the library's geometry (csrc/kernels/gemm_f.hip: 256 x 256 tiles, 4 waves of 128 x 128 or 8 of 128 x 64;
+256 x 128 (8 waves of 64 x 64) for N = 128 and 256 x 64 (4 waves of 64 x 64) for N = 64)
 against an fp32 PyTorch reference: one tile, many tiles, a 128-column last panel, the shortest K (3 slices ahead of 6), ragged M (rows past
 the operand read as zeros and are never stored), strided rows, refusals, and bit-identical repeats."""
 import pytest
@@ -10,7 +11,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (4096, 2304, 768), (8192, 768, 3072), (300, 512, 192),
                                    (1000, 256, 1024), (256 * 33, 768, 768),
-                                   (700, 640, 384), (512, 128, 256)])
+                                   (700, 640, 384), (512, 128, 256), (1000, 64, 576), (300, 128, 192)])
 def test_gemm_f_matches_fp32(gpu, M, N, K, waves):
     from distributedvolunteercomputing_amd.ops import native
 
@@ -48,7 +49,8 @@ def test_gemm_f_strided_rows_and_refusals(gpu):
     assert wide[:, 512:].abs().max().item() == 0
     assert not C.gemm_f_supported(512, 768, 128)  # K < 192
     assert not C.gemm_f_supported(512, 768, 800)  # K % 64
-    assert not C.gemm_f_supported(512, 704, 768)  # N % 128
+    assert not C.gemm_f_supported(512, 704, 768)  # N % 128 (and not 64)
+    assert not C.gemm_f_supported(512, 32, 768)
     with pytest.raises(RuntimeError):
         C.gemm_f(a, b[:, :512].contiguous(), torch.empty(512, 512, device="cuda", dtype=torch.bfloat16))
 
@@ -95,7 +97,8 @@ def test_linear_on_gemm_f_matches_library(gpu):
 @pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("imgs,H,W,Cin,Cout,stride", [(2, 9, 7, 64, 128, 1), (3, 8, 8, 128, 256, 2),
                                                       (1, 7, 7, 512, 128, 1), (5, 5, 6, 64, 384, 2),
-                                                      (2, 14, 14, 256, 256, 1)])
+                                                      (2, 14, 14, 256, 256, 1), (3, 11, 13, 64, 64, 1),
+                                                      (2, 12, 12, 64, 64, 2), (1, 9, 9, 128, 64, 1)])
 def test_gemm_f_conv3x3_matches_fp32(gpu, imgs, H, W, Cin, Cout, stride, waves):
     """gemm_f's implicit-GEMM mode (the patch matrix gathered by the LDS-DMA's per-lane offsets, padding taps
     as zeros) against an fp32 convolution: borders, odd and non-square images, stride 2, a ragged last row
@@ -128,7 +131,7 @@ def test_gemm_f_conv3x3_refusals(gpu):
     C = native()
     assert not C.gemm_f_conv3x3_supported(2, 8, 8, 96, 128, 1)   # Cin not a power of two
     assert not C.gemm_f_conv3x3_supported(2, 8, 8, 32, 128, 1)   # Cin < 64
-    assert not C.gemm_f_conv3x3_supported(2, 8, 8, 64, 64, 1)    # Cout % 128
+    assert not C.gemm_f_conv3x3_supported(2, 8, 8, 64, 96, 1)    # Cout % 128 (and not 64)
     assert not C.gemm_f_conv3x3_supported(2, 8, 8, 64, 128, 3)   # stride
     x = torch.randn(2, 8, 8, 64, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(128, 3, 3, 64, device="cuda", dtype=torch.bfloat16)
