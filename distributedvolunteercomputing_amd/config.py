@@ -77,9 +77,8 @@ class RuntimeConfig:
     # VCX_CONV3X3_WGRAD: weight gradients of the ResNet 3x3 convolutions with Cin, Cout % 128 == 0 on gemm_wg with
     # the patch matrix gathered while staging ("vcx"), or MIOpen's ("lib")
     conv3x3_wgrad: str = "vcx"
-    # VCX_CONV3X3_FWD: forwards (and stride-1 input gradients) of the ResNet 3x3 convolutions with 256+ output
-    # channels on gemm_f's implicit GEMM ("vcx": 1.09-1.38x MIOpen at stages 3 / 4, profiles/r6_conv3x3_fwd.txt),
-    # or MIOpen's ("lib")
+    # VCX_CONV3X3_FWD: forwards (and stride-1 input gradients) of the ResNet 3x3 convolutions on gemm_f's implicit
+    # GEMM ("vcx": 1.09-1.38x MIOpen at every stage, profiles/r6_conv3x3_fwd.txt), or MIOpen's ("lib")
     conv3x3_fwd: str = "vcx"
     # VCX_ENGINE_BATCH: chunks a volunteer that already holds several runs through the detector as ONE batch
     # (1 = one chunk per network launch)

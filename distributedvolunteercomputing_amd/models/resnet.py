@@ -4,10 +4,9 @@ synthetic ImageNet shapes, top-k sparsified gradients + error feedback, 8 peers"
 Channels-last bf16. The 1x1 convolutions (about 70 % of the FLOPs) are plain GEMMs on the NHWC
 view -- [N*H*W, Cin] x [Cout, Cin]^T -- and run through the framework's linear layer (library
 GEMMs picked per shape, split-M weight gradients summed straight into the flat gradient buffer);
-stride-2 ones subsample the NHWC view first. The 3x3 convolutions of stages 3 and 4 run forward, input
-gradient (stride 1) on the hand-written gemm_f implicit GEMM (every stage) and, at stages 3 / 4, their weight
-gradients on gemm_wg; the stride-2 input gradients, the stage-1/2 weight gradients and the 7x7 stem run MIOpen's
-NHWC kernels. Train-mode BatchNorm runs fused with its ReLU and the residual add (ops/batchnorm.py,
+stride-2 ones subsample the NHWC view first. The 3x3 convolutions run forward and stride-1 input gradient on
+the hand-written gemm_f implicit GEMM (every stage) and, at stages 3 / 4, their weight gradients on gemm_wg; the
+stride-2 input gradients, the stage-1/2 weight gradients and the 7x7 stem run MIOpen's NHWC kernels. Train-mode BatchNorm runs fused with its ReLU and the residual add (ops/batchnorm.py,
 csrc/kernels/batchnorm.hip). BatchNorm statistics are buffers that the trainers average at every
 synchronisation.
 """
@@ -63,9 +62,6 @@ def _fwd_vcx(imgs, H, W, cin, cout, stride) -> bool:
     stride-1 input gradient at every stage, profiles/r6_conv3x3_fwd.txt)."""
     from ..ops._lib import native
 
-    import os
-    if cout < int(os.environ.get("VCX_CONV3X3_FWD_MINC", "0")):  # TEMP A/B
-        return False
     return config.get().conv3x3_fwd == "vcx" and bool(native().gemm_f_conv3x3_supported(imgs, H, W, cin, cout, stride))
 
 
@@ -129,9 +125,9 @@ class _Conv3x3(torch.autograd.Function):
 
 
 class Conv3x3(nn.Conv2d):
-    """3x3 convolution, pad 1 (the bottleneck's conv2): nn.Conv2d whose weight gradient runs on gemm_wg, and forward
-    and stride-1 input gradient on gemm_f, where the shape tiles (config.conv3x3_wgrad / conv3x3_fwd; ResNet-50
-    stages 3 and 4 at B=128)."""
+    """3x3 convolution, pad 1 (the bottleneck's conv2): nn.Conv2d whose forward and stride-1 input gradient run on
+    gemm_f (config.conv3x3_fwd; every ResNet-50 stage) and whose weight gradient runs on gemm_wg where the shape
+    tiles (config.conv3x3_wgrad; stages 3 and 4 at B=128)."""
 
     def __init__(self, cin, cout, stride=1):
         super().__init__(cin, cout, 3, stride=stride, padding=1, bias=False)
