@@ -122,7 +122,8 @@ def _linked(out: Path, d: str):
 # MFMAs"); without it the dK/dV tile body issues scalar ops only and the 3-wave forward stops spilling: forward
 # 0.184-0.188 vs 0.192 ms, backward 0.557-0.559 vs 0.573-0.577, bench 1071-1073 vs 1060-1062 samples/s, outputs
 # identical (profiles/r6_attention_noslp.txt). Measured and not applied: attention_hm.hip (Llama GQA backward
-# 0.555 vs 0.541 ms), gemm_ps.hip + gemm.hip (bench 1086-1089 vs 1090-1091).
+# 0.555 vs 0.541 ms), gemm_ps.hip + gemm.hip (bench 1086-1089 vs 1090-1091), vision.hip (detector chunk 1.179 vs
+# 1.185 ms eager: even).
 FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
 
 
