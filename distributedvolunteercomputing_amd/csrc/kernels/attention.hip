@@ -1123,8 +1123,10 @@ using namespace vcx;
 // Round 6 defaults: the forward and dK/dV on the 3-slot inline-asm LDS-DMA ring (fwd_dma = 2, bwd bit 2): same
 // box, interleaved medians (profiles/r6_attention_ring.txt): forward 0.1937 vs 0.2080 ms, backward 0.5571 vs
 // 0.5852 ms, outputs bit-identical at T = 1024 / 200 / 202; bench 1063.2 / 1063.0 vs 1053.6 samples/s. The dQ
-// kernel on the ring (bit 3) measured even (0.5837 ms) and stays on the two-buffer LDS-DMA kernel.
-static int g_fwd_wpe = 3, g_fwd_dma = 2, g_bwd_dma = 5;  // g_bwd_dma bit 0: dQ LDS-DMA, 1: dK/dV LDS-DMA, 2: dK/dV ring, 3: dQ ring
+// kernel on the ring (bit 3) measured even (0.5837 ms) then; built without SLP vectorisation (_build.py FILE_FLAGS)
+// it is ahead: backward 0.5278 (both rings, bits 12) vs 0.5337 ms (bits 5), outputs bit-identical
+// (gpurun_out/attab, scripts/attn_ring_ab.py) -- now the default.
+static int g_fwd_wpe = 3, g_fwd_dma = 2, g_bwd_dma = 12;  // g_bwd_dma bit 0: dQ LDS-DMA, 1: dK/dV LDS-DMA, 2: dK/dV ring, 3: dQ ring
 // output tiles (O, dQ, dK, dV): 1 = staged through LDS, whole-row 16-B stores; 0 = per-lane half-row
 // stores. Bench shape, same box (profiles/r1_attn_variants.log): backward 0.589 vs 0.614 ms, forward
 // within noise (0.201-0.212 vs 0.206-0.208)

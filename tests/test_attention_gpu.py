@@ -73,7 +73,11 @@ def test_attention_matches_sdpa_at_bench_shape(gpu):
     assert rel < 1e-2, float(rel)
 
 
-@pytest.mark.parametrize("variant", [(2, 0, 0, 0), (3, 0, 3, 1), (2, 1, 2, 1), (3, 1, 1, 0), (3, 1, 1, 1)])
+DEFAULT_VARIANT = (3, 2, 12, 1)  # csrc/kernels/attention.hip g_fwd_wpe, g_fwd_dma, g_bwd_dma, g_stage_epi
+
+
+@pytest.mark.parametrize("variant", [(2, 0, 0, 0), (3, 0, 3, 1), (2, 1, 2, 1), (3, 1, 1, 0), (3, 1, 1, 1),
+                                     (2, 2, 4, 1), (3, 2, 8, 1), DEFAULT_VARIANT])
 def test_attention_deterministic(gpu, variant):
     """Same inputs, same kernel -> bitwise identical outputs (a race on the double-buffered LDS
     tiles would show up here as run-to-run differences)."""
@@ -94,7 +98,7 @@ def test_attention_deterministic(gpu, variant):
         for g in gs[1:]:
             assert torch.equal(g, gs[0])
     finally:
-        C.attn_set_variant(3, 1, 1, 1)
+        C.attn_set_variant(*DEFAULT_VARIANT)  # the defaults, for the tests that run after this one
 
 
 def _ref_gqa32(q, k, v, scale):
