@@ -79,21 +79,26 @@ def test_resnet_conv3x3_module_grads(gpu, preset_grad):
     assert _rel(x.grad, xr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("fwd,wgrad,stride", [("vcx", "vcx", 1), ("vcx", "lib", 1), ("lib", "vcx", 1),
-                                              ("vcx", "vcx", 2), ("vcx", "lib", 2)])
-def test_resnet_conv3x3_module_on_gemm_f(gpu, fwd, wgrad, stride):
+@pytest.mark.parametrize("fwd,wgrad,stride,ch", [("vcx", "vcx", 1, 256), ("vcx", "lib", 1, 256), ("lib", "vcx", 1, 256),
+                                                 ("vcx", "vcx", 2, 256), ("vcx", "lib", 2, 256), ("vcx", "vcx", 1, 128),
+                                                 ("vcx", "vcx", 2, 128), ("vcx", "vcx", 1, 64)])
+def test_resnet_conv3x3_module_on_gemm_f(gpu, fwd, wgrad, stride, ch):
     """models/resnet.Conv3x3 with the forward (and, at stride 1, the input gradient) on gemm_f's implicit GEMM
-    in every combination with the weight-gradient path: output, input and weight gradients against fp32."""
+    in every combination with the weight-gradient path: output, input and weight gradients against fp32; the
+    128- and 64-channel stages on its 256 x 128 / 256 x 64 tiles (weight gradient on MIOpen there)."""
     from distributedvolunteercomputing_amd import config
     from distributedvolunteercomputing_amd.models.resnet import Conv3x3
 
     torch.manual_seed(5 + stride)
-    m = Conv3x3(256, 256, stride=stride).to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
-    x = torch.randn(8, 256, 14, 14, device=gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    m = Conv3x3(ch, ch, stride=stride).to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(8, ch, 14, 14, device=gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
     x.requires_grad_()
     Ho = (14 - 1) // stride + 1
-    r = torch.randn(8, 256, Ho, Ho, device=gpu)
+    r = torch.randn(8, ch, Ho, Ho, device=gpu)
     with config.override(conv3x3_fwd=fwd, conv3x3_wgrad=wgrad):
+        from distributedvolunteercomputing_amd.models import resnet
+
+        assert resnet._fwd_vcx(8, 14, 14, ch, ch, stride) == (fwd == "vcx")  # the path under test is taken
         y = m(x)
         (y.float() * r).sum().backward()
     xr = x.detach().float().requires_grad_()
