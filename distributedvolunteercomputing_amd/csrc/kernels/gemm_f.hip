@@ -6,7 +6,14 @@
 // GPT-2 step. Structure:
 //   * 256 x 256 tile per workgroup in one of two wave layouts: 8 waves as 2 (M) x 4 (N) of 128 x 64 (two waves per
 //     SIMD, 128 accumulators in VGPRs; the default) or 4 waves as 2 x 2 of 128 x 128 (hipBLASLt's MT256x256x64
-//     WG32_8_1 / MIWT8_8 geometry: one wave per SIMD, 256 accumulators in AGPRs);
+//     WG32_8_1 / MIWT8_8 geometry: one wave per SIMD, 256 accumulators in AGPRs); for N = 128 / 64 a 256 x 128
+//     tile (8 waves of 64 x 64) / 256 x 64 tile (4 waves of 64 x 64, two workgroups per CU);
+//   * CONV: a 3x3 convolution (pad 1, stride 1 | 2) as an implicit GEMM -- the patch matrix of NHWC x gathered by
+//     the LDS-DMA's per-lane source offsets, padding taps as offsets past the buffer resource (the load returns 0);
+//     the ResNet-50 3x3 forwards and stride-1 input gradients (models/resnet.py, 1.09-1.38x MIOpen at every
+//     stage, profiles/r6_conv3x3_fwd.txt);
+//   * split-K over one round of workgroups for deep-K / few-tile shapes: fp32 partials straight from the
+//     accumulators, summed with the bias by splitk_bias_kernel;
 //   * 4-slot LDS ring of 32-deep K-slices (32 KB each: A 256 x 64 B, B 256 x 64 B), LDS-DMA issued as inline asm
 //     (hipcc's waitcnt pass cannot see it, so it adds no vmcnt drains), a counted vmcnt that keeps two slices in
 //     flight across every raw s_barrier, fragments of slice s + 1 read during slice s into a second register set;
@@ -21,7 +28,8 @@
 // 203.6 us, fc2 259.0 vs 218.6, 4096^3 1317 vs 1518 TF/s -- the cdna guide's 8-phase template level); 4 waves
 // 0.78-0.81x. Counters (8 waves, qkv + 4096^3): MFMA busy 48 %, 36 % of wave-cycles parked at waits / barriers,
 // against the library's 57 % / 14 %; a 5-slot ring (memory latency) and staggering the two M halves' DMA issue
-// measured even. Hence opt-in (config.gemm_fwd = "vcx"); the library keeps the forward GEMMs.
+// measured even. Hence opt-in for the linear layers (config.gemm_fwd = "vcx"); the library keeps the GPT-2 forward
+// GEMMs, while the convolutions -- where MIOpen's kernels run at 300-600 TF/s -- default to this kernel.
 // Reference analog: per-frame net.forward, /root/reference/worker.py:248-249 (the pointwise GEMMs).
 #include <type_traits>
 
