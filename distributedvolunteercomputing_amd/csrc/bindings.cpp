@@ -416,7 +416,7 @@ bool gemm_f_conv3x3_supported(int64_t imgs, int64_t H, int64_t W, int64_t Cin, i
 }
 
 void gemm_f_conv3x3(at::Tensor x, at::Tensor w, at::Tensor out, int64_t stride, c10::optional<at::Tensor> bias,
-                    int64_t waves, int64_t splits) {
+                    int64_t waves, int64_t splits, bool flip_taps) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4 && w.dim() == 4 && out.dim() == 4, "gemm_f_conv3x3: x [N, H, W, Cin], "
               "w [Cout, 3, 3, Cin], out [N, Ho, Wo, Cout] on the GPU");
   for (const at::Tensor* t : {&x, &w, &out}) {
@@ -439,7 +439,7 @@ void gemm_f_conv3x3(at::Tensor x, at::Tensor w, at::Tensor out, int64_t stride, 
   auto [ns, ws] = f_splits(imgs * Ho * Wo, Cout, 9 * Cin, splits, x);
   vcx_gemm_f_conv3x3(x.data_ptr(), w.data_ptr(), out.data_ptr(), hb ? bias->data_ptr() : nullptr, (int)imgs, (int)H,
                      (int)W, (int)Cin, (int)Cout, (int)stride, (int)waves, ns, ns > 1 ? ws.data_ptr<float>() : nullptr,
-                     cur_stream());
+                     flip_taps ? 1 : 0, cur_stream());
 }
 
 // 3x3 convolution (pad 1, stride 1|2) weight gradient on gemm_wg with the patch matrix of x gathered while
@@ -949,7 +949,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_f_conv3x3_supported", &gemm_f_conv3x3_supported, py::arg("imgs"), py::arg("H"), py::arg("W"),
         py::arg("Cin"), py::arg("Cout"), py::arg("stride"));
   m.def("gemm_f_conv3x3", &gemm_f_conv3x3, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("stride"),
-        py::arg("bias") = py::none(), py::arg("waves") = 0, py::arg("splits") = -1);
+        py::arg("bias") = py::none(), py::arg("waves") = 0, py::arg("splits") = -1, py::arg("flip_taps") = false);
   m.def("gemm_f_splits", &gemm_f_splits, py::arg("M"), py::arg("N"), py::arg("K"));
   m.def("gemm_f", &gemm_f, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("bias") = py::none(),
         py::arg("waves") = 0, py::arg("splits") = -1);

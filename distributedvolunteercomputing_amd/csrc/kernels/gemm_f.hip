@@ -98,6 +98,7 @@ struct Frags {
 // 3x3 convolution (pad 1) as an implicit GEMM: A = the patch matrix of NHWC x gathered while staging
 struct Conv {
   int H, W, lc, Ho, Wo, stride;  // lc = log2(Cin)
+  int flip;                       // gather tap (2 - ky, 2 - kx) for weight tap (ky, kx): w[Cin][ky][kx][Cout] unflipped
   unsigned xbytes;
 };
 
@@ -171,7 +172,8 @@ __global__ void __launch_bounds__(G::NT, 1)
       if constexpr (CONV) {  // slice s = channels c0 .. c0 + 31 of tap t = (ky, kx); padding taps read zeros
         const int sg = ks0 + s;  // the global slice
         const int t = (sg * BKS) >> cv.lc, c0 = (sg * BKS) & ((1 << cv.lc) - 1);
-        const int ky = (t * 11) >> 5, kx = t - 3 * ky;  // t / 3 for t < 9
+        int ky = (t * 11) >> 5, kx = t - 3 * ky;  // t / 3 for t < 9
+        if (cv.flip) ky = 2 - ky, kx = 2 - kx;     // an input gradient against the unflipped transposed weight
         const int ih = ih0[q] + ky, iw = iw0[q] + kx;
         const bool ok = (unsigned)ih < (unsigned)cv.H && (unsigned)iw < (unsigned)cv.W;
         const int voff = ok ? (((va[q] + ky * cv.W + kx) << cv.lc) + c0 + pch * 8) * 2 : 0x7fffff00;
@@ -420,10 +422,13 @@ bool vcx_gemm_f_conv3x3_supported(int imgs, int H, int W, int Cin, int Cout, int
          vcx_gemm_f_supported(1, Cout, 9 * Cin);
 }
 
-// y[imgs, Ho, Wo, Cout] (+ bias) = conv3x3(x[imgs, H, W, Cin], w[Cout][3][3][Cin]), pad 1
+// y[imgs, Ho, Wo, Cout] (+ bias) = conv3x3(x[imgs, H, W, Cin], w[Cout][3][3][Cin]), pad 1; flip: the kernel's taps
+// mirrored (w holds tap (ky, kx) where the convolution wants (2 - ky, 2 - kx): a stride-1 input gradient from the
+// transposed weight without a flip copy)
 void vcx_gemm_f_conv3x3(const void* x, const void* w, void* y, const void* bias, int imgs, int H, int W, int Cin,
-                        int Cout, int stride, int waves, int splits, float* ws, hipStream_t s) {
+                        int Cout, int stride, int waves, int splits, float* ws, int flip, hipStream_t s) {
   gemm_f::Conv cv;
+  cv.flip = flip;
   cv.H = H;
   cv.W = W;
   cv.lc = log2_exact(Cin);

@@ -178,3 +178,25 @@ def test_gemm_f_conv3x3_split_k(gpu):
     torch.cuda.synchronize()
     ref = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), padding=1).permute(0, 2, 3, 1)
     assert (y.float() - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 64), (128, 256), (256, 128)])
+def test_gemm_f_conv3x3_flip_taps_is_the_input_gradient(gpu, cin, cout):
+    """flip_taps: gemm_f_conv3x3(dy, W^T, flip_taps=True) with the UNFLIPPED transposed weight [Cin][ky][kx][Cout]
+    equals the stride-1 input gradient of the convolution (fp32 oracle: torch's convolution_backward)."""
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    torch.manual_seed(cin + cout)
+    imgs, H, W = 3, 9, 11
+    x = torch.randn(imgs, cin, H, W, device="cuda")
+    w = torch.randn(cout, cin, 3, 3, device="cuda") / (3 * cin ** 0.5)
+    dy = torch.randn(imgs, cout, H, W, device="cuda")
+    ref = torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                              [True, False, False])[0].permute(0, 2, 3, 1)
+    dyh = dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    wt = w.permute(1, 2, 3, 0).contiguous().to(torch.bfloat16)  # [Cin][ky][kx][Cout], taps unflipped
+    dx = torch.empty(imgs, H, W, cin, device="cuda", dtype=torch.bfloat16)
+    C.gemm_f_conv3x3(dyh, wt, dx, 1, flip_taps=True)
+    torch.cuda.synchronize()
+    assert (dx.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
