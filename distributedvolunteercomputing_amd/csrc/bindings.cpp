@@ -417,15 +417,18 @@ bool gemm_f_conv3x3_supported(int64_t imgs, int64_t H, int64_t W, int64_t Cin, i
 
 void gemm_f_conv3x3(at::Tensor x, at::Tensor w, at::Tensor out, int64_t stride, c10::optional<at::Tensor> bias,
                     int64_t waves, int64_t splits, bool flip_taps) {
-  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && w.dim() == 4 && out.dim() == 4, "gemm_f_conv3x3: x [N, H, W, Cin], "
-              "w [Cout, 3, 3, Cin], out [N, Ho, Wo, Cout] on the GPU");
+  // w: [Cout, 3, 3, Cin], or tap-major [9, Cout, Cin] (the transpose of a channels-last weight matrix)
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && (w.dim() == 4 || w.dim() == 3) && out.dim() == 4,
+              "gemm_f_conv3x3: x [N, H, W, Cin], w [Cout, 3, 3, Cin] or [9, Cout, Cin], out [N, Ho, Wo, Cout] on the GPU");
   for (const at::Tensor* t : {&x, &w, &out}) {
     TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->get_device() == x.get_device(),
                 "gemm_f_conv3x3: contiguous bf16 tensors on one device");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "gemm_f_conv3x3: 16-B aligned base pointers");
   }
-  const int64_t imgs = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = w.size(0);
-  TORCH_CHECK(w.size(1) == 3 && w.size(2) == 3 && w.size(3) == Cin, "gemm_f_conv3x3: w [Cout, 3, 3, Cin]");
+  const bool tap_major = w.dim() == 3;
+  const int64_t imgs = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = tap_major ? w.size(1) : w.size(0);
+  TORCH_CHECK(tap_major ? (w.size(0) == 9 && w.size(2) == Cin) : (w.size(1) == 3 && w.size(2) == 3 && w.size(3) == Cin),
+              "gemm_f_conv3x3: w [Cout, 3, 3, Cin] or tap-major [9, Cout, Cin]");
   TORCH_CHECK(stride == 1 || stride == 2, "gemm_f_conv3x3: stride 1 or 2");
   const int64_t Ho = (H - 1) / stride + 1, Wo = (W - 1) / stride + 1;
   TORCH_CHECK(out.size(0) == imgs && out.size(1) == Ho && out.size(2) == Wo && out.size(3) == Cout,
@@ -439,7 +442,7 @@ void gemm_f_conv3x3(at::Tensor x, at::Tensor w, at::Tensor out, int64_t stride, 
   auto [ns, ws] = f_splits(imgs * Ho * Wo, Cout, 9 * Cin, splits, x);
   vcx_gemm_f_conv3x3(x.data_ptr(), w.data_ptr(), out.data_ptr(), hb ? bias->data_ptr() : nullptr, (int)imgs, (int)H,
                      (int)W, (int)Cin, (int)Cout, (int)stride, (int)waves, ns, ns > 1 ? ws.data_ptr<float>() : nullptr,
-                     flip_taps ? 1 : 0, cur_stream());
+                     flip_taps ? 1 : 0, tap_major ? 1 : 0, cur_stream());
 }
 
 // 3x3 convolution (pad 1, stride 1|2) weight gradient on gemm_wg with the patch matrix of x gathered while

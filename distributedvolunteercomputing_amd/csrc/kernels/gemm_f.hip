@@ -99,6 +99,7 @@ struct Frags {
 struct Conv {
   int H, W, lc, Ho, Wo, stride;  // lc = log2(Cin)
   int flip;                       // gather tap (2 - ky, 2 - kx) for weight tap (ky, kx): w[Cin][ky][kx][Cout] unflipped
+  int btap;                       // > 0: B is tap-major, [9][N][Cin] (ldb = Cin), tap t's rows at t * btap elements
   unsigned xbytes;
 };
 
@@ -142,7 +143,9 @@ __global__ void __launch_bounds__(G::NT, 1)
   const int prow = lane >> 2, pch = (lane & 3) ^ swz(prow);
   const int rowsA = min(BM, M - m0), rowsB = min(BN, N - n0);
   const u32x4 ra = CONV ? desc(A, cv.xbytes) : desc(A + (int64_t)m0 * lda, (unsigned)(((int64_t)(rowsA - 1) * lda + K) * 2));
-  const u32x4 rb = desc(B + (int64_t)n0 * ldb, (unsigned)(((int64_t)(rowsB - 1) * ldb + K) * 2));
+  const u32x4 rb = desc(B + (int64_t)n0 * ldb, (unsigned)(((CONV && cv.btap ? 8 * (int64_t)cv.btap + (1 << cv.lc)
+                                                                            : (int64_t)K) +
+                                                             (int64_t)(rowsB - 1) * ldb) * 2));
   int va[AOPS], vb[G::BOPS];
   // CONV: per A piece the lane's output pixel as the input pixel of tap (0, 0) -- (ih0, iw0) and its index pix0
   // (rows past M: ih0 = -4, never inside the image)
@@ -182,7 +185,15 @@ __global__ void __launch_bounds__(G::NT, 1)
         dma16(ra, va[q], (ks0 + s) * ROWB, slot + (wid + WAVES * q) * 1024);
       }
     } else {
-      dma16(rb, vb[q], (ks0 + s) * ROWB, slot + SLOT_A + (wid + WAVES * q) * 1024);
+      int soff = (ks0 + s) * ROWB;
+      if constexpr (CONV) {
+        if (cv.btap) {  // tap-major B (the transposed weight of an input gradient): tap t's rows at t * btap
+          const int sg = ks0 + s;
+          const int t = (sg * BKS) >> cv.lc, c0 = (sg * BKS) & ((1 << cv.lc) - 1);
+          soff = (t * cv.btap + c0) * 2;
+        }
+      }
+      dma16(rb, vb[q], soff, slot + SLOT_A + (wid + WAVES * q) * 1024);
     }
   };
   auto stage = [&](int s) {
@@ -424,11 +435,14 @@ bool vcx_gemm_f_conv3x3_supported(int imgs, int H, int W, int Cin, int Cout, int
 
 // y[imgs, Ho, Wo, Cout] (+ bias) = conv3x3(x[imgs, H, W, Cin], w[Cout][3][3][Cin]), pad 1; flip: the kernel's taps
 // mirrored (w holds tap (ky, kx) where the convolution wants (2 - ky, 2 - kx): a stride-1 input gradient from the
-// transposed weight without a flip copy)
+// transposed weight without a flip copy); tap_major: w is [9][Cout][Cin] (each tap's [Cout][Cin] block in turn: the
+// transpose of the channels-last weight matrix [Cin_conv, 9 Cout_conv], one transpose kernel)
 void vcx_gemm_f_conv3x3(const void* x, const void* w, void* y, const void* bias, int imgs, int H, int W, int Cin,
-                        int Cout, int stride, int waves, int splits, float* ws, int flip, hipStream_t s) {
+                        int Cout, int stride, int waves, int splits, float* ws, int flip, int tap_major,
+                        hipStream_t s) {
   gemm_f::Conv cv;
   cv.flip = flip;
+  cv.btap = tap_major ? Cout * Cin : 0;
   cv.H = H;
   cv.W = W;
   cv.lc = log2_exact(Cin);
@@ -436,13 +450,13 @@ void vcx_gemm_f_conv3x3(const void* x, const void* w, void* y, const void* bias,
   cv.Wo = (W - 1) / stride + 1;
   cv.stride = stride;
   cv.xbytes = (unsigned)((int64_t)imgs * H * W * Cin * 2);
-  const int M = imgs * cv.Ho * cv.Wo, K = 9 * Cin;
+  const int M = imgs * cv.Ho * cv.Wo, K = 9 * Cin, ldb = tap_major ? Cin : K;
   if (Cout <= 64)
-    gemm_f::launch<gemm_f::G4n, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
+    gemm_f::launch<gemm_f::G4n, 4, true>(x, w, y, bias, M, Cout, K, 0, ldb, Cout, splits, ws, s, cv);
   else if (Cout <= 128)
-    gemm_f::launch<gemm_f::G8n, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
+    gemm_f::launch<gemm_f::G8n, 4, true>(x, w, y, bias, M, Cout, K, 0, ldb, Cout, splits, ws, s, cv);
   else if (waves == 4)
-    gemm_f::launch<gemm_f::G4, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
+    gemm_f::launch<gemm_f::G4, 4, true>(x, w, y, bias, M, Cout, K, 0, ldb, Cout, splits, ws, s, cv);
   else
-    gemm_f::launch<gemm_f::G8, 4, true>(x, w, y, bias, M, Cout, K, 0, K, Cout, splits, ws, s, cv);
+    gemm_f::launch<gemm_f::G8, 4, true>(x, w, y, bias, M, Cout, K, 0, ldb, Cout, splits, ws, s, cv);
 }

@@ -30,7 +30,8 @@ void vcx_gemm_f(const void* A, const void* B, void* C, const void* bias, int M, 
                 int ldc, int waves, int splits, float* ws, hipStream_t s);
 bool vcx_gemm_f_conv3x3_supported(int imgs, int H, int W, int Cin, int Cout, int stride);
 void vcx_gemm_f_conv3x3(const void* x, const void* w, void* y, const void* bias, int imgs, int H, int W, int Cin,
-                        int Cout, int stride, int waves, int splits, float* ws, int flip, hipStream_t s);
+                        int Cout, int stride, int waves, int splits, float* ws, int flip, int tap_major,
+                        hipStream_t s);
 bool vcx_gemm_nt_supported(int M, int N, int K);
 bool vcx_gemm_nt_supported_epi(int M, int N, int K, int epi);
 void vcx_gemm_nt(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N, int K,

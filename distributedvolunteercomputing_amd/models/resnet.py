@@ -100,10 +100,12 @@ class _Conv3x3(torch.autograd.Function):
             imgs, cin, H, W = x.shape
             if s == 1 and _fwd_vcx(imgs, H, W, w.shape[0], cin, 1):
                 # dx = conv(dy, W') with W'[ci][ky][kx][co] = W[co][ci][2 - ky][2 - kx]: the kernel mirrors its taps
-                # (flip_taps), so W' is the transposed weight alone (one weight-sized copy, no flip pass)
+                # (flip_taps), so W' is the transposed weight alone: the [Cout, 9 Cin] channels-last weight matrix
+                # transposed by one tiled kernel into tap-major [9][Cin][Cout] (no permute copy, no flip pass)
                 dxh = torch.empty(imgs, H, W, cin, device=x.device, dtype=x.dtype)
-                native().gemm_f_conv3x3(dy.permute(0, 2, 3, 1), w.permute(1, 2, 3, 0).contiguous(), dxh, 1,
-                                        flip_taps=True)
+                cout = w.shape[0]
+                wt = native().transpose_bf16(w.permute(0, 2, 3, 1).reshape(cout, 9 * cin)).view(9, cin, cout)
+                native().gemm_f_conv3x3(dy.permute(0, 2, 3, 1), wt, dxh, 1, flip_taps=True)
                 dx = dxh.permute(0, 3, 1, 2)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,

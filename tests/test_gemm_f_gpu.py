@@ -200,3 +200,34 @@ def test_gemm_f_conv3x3_flip_taps_is_the_input_gradient(gpu, cin, cout):
     C.gemm_f_conv3x3(dyh, wt, dx, 1, flip_taps=True)
     torch.cuda.synchronize()
     assert (dx.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("cin,cout,imgs,hw", [(64, 64, 3, 9), (128, 256, 3, 9), (256, 128, 3, 9), (512, 512, 4, 7)])
+def test_gemm_f_conv3x3_tap_major_weight(gpu, cin, cout, imgs, hw):
+    """Tap-major B ([9][Cout_call][Cin_call], a 3-D w): the input gradient from the transposed channels-last weight
+    matrix (transpose_bf16 of [Cout, 9 Cin] viewed [9, Cin, Cout]) with flip_taps, and a forward convolution from
+    the same layout; the 512-channel case runs split-K. fp32 oracle: torch's convolution / convolution_backward."""
+    import torch.nn.functional as F
+
+    from distributedvolunteercomputing_amd.ops import native
+
+    C = native()
+    torch.manual_seed(cin * 3 + cout)
+    x = torch.randn(imgs, cin, hw, hw + 2, device="cuda")
+    w = torch.randn(cout, cin, 3, 3, device="cuda") / (3 * cin ** 0.5)
+    dy = torch.randn(imgs, cout, hw, hw + 2, device="cuda")
+    ref = torch.ops.aten.convolution_backward(dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                              [True, False, False])[0].permute(0, 2, 3, 1)
+    wb = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = C.transpose_bf16(wb.permute(0, 2, 3, 1).reshape(cout, 9 * cin)).view(9, cin, cout)
+    dx = torch.empty(imgs, hw, hw + 2, cin, device="cuda", dtype=torch.bfloat16)
+    C.gemm_f_conv3x3(dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16), wt, dx, 1, flip_taps=True)
+    torch.cuda.synchronize()
+    assert (dx.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    # forward from a tap-major weight: w9[t][co][ci] = w[co][ci][t]
+    w9 = w.permute(2, 3, 0, 1).reshape(9, cout, cin).contiguous().to(torch.bfloat16)
+    y = torch.empty(imgs, hw, hw + 2, cout, device="cuda", dtype=torch.bfloat16)
+    C.gemm_f_conv3x3(x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16), w9, y, 1)
+    torch.cuda.synchronize()
+    yref = F.conv2d(x, w, padding=1).permute(0, 2, 3, 1)
+    assert (y.float() - yref).abs().max().item() < 2e-2 * yref.abs().max().item()
