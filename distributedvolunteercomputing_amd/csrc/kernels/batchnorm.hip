@@ -45,9 +45,13 @@ struct Unroll {
 // share a channel chunk, then added to out0 / out1 (fp32 [C]) with one atomic per channel.
 // body(off, step, Unroll<U>, s0, s1) handles the U rows off, off + step, ...: the main loop passes
 // U = 4 so every lane keeps 4 row loads per operand in flight (one at a time left these passes at
-// 2-3 TB/s, latency-bound: profiles/r5_cfg3_resnet50_categories.txt)
-template <int UR, int BT, typename F>
-__device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&& body, float* out0, float* out1) {
+// 2-3 TB/s, latency-bound: profiles/r5_cfg3_resnet50_categories.txt).
+// channel_reduce_tail is the frame: main(r, step, rpp, ch, s0, s1) sums the full groups of rows from r and returns
+// the first row it left; single rows finish with body(off, step, Unroll<1>, s0, s1); then the LDS reduction and
+// the atomics
+template <int BT, typename M, typename F>
+__device__ __forceinline__ void channel_reduce_tail(int C, int64_t r0, int64_t r1, M&& main, F&& body, float* out0,
+                                                    float* out1) {
   __shared__ float red[2][BT][9];  // [quantity][thread][8 channels + pad]
   const int tid = threadIdx.x;
   const int cpr = C / 8;                // chunks per row
@@ -58,8 +62,7 @@ __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&
   for (int i = 0; i < 8; ++i) s0[i] = s1[i] = 0.f;
   if (rr < rpp) {
     const int64_t step = (int64_t)rpp * C;
-    int64_t r = r0 + rr;
-    for (; r + (UR - 1) * rpp < r1; r += UR * rpp) body(r * C + ch * 8, step, Unroll<UR>{}, s0, s1);
+    int64_t r = main(r0 + rr, step, rpp, ch, s0, s1);
     for (; r < r1; r += rpp) body(r * C + ch * 8, step, Unroll<1>{}, s0, s1);
   }
 #pragma unroll
@@ -81,32 +84,91 @@ __device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&
   }
 }
 
+// PIPE (R registers of U rows, ld(off, step, regs) / acc(regs, s0, s1) instead of body): two register sets
+// of U rows, the next set's loads issued before the current one is summed, so the memory queue never drains
+// between rounds of loads (the unpipelined loop issues U rows, waits for all of them, sums, then issues again)
+template <int UR, int BT, typename F>
+__device__ __forceinline__ void channel_reduce(int C, int64_t r0, int64_t r1, F&& body, float* out0, float* out1) {
+  channel_reduce_tail<BT>(C, r0, r1, [&](int64_t r, int64_t step, int rpp, int ch, float(&s0)[8], float(&s1)[8]) {
+    for (; r + (UR - 1) * rpp < r1; r += UR * rpp) body(r * C + ch * 8, step, Unroll<UR>{}, s0, s1);
+    return r;
+  }, body, out0, out1);
+}
+
+template <int U, int BT, typename R, typename LD, typename ACC, typename F>
+__device__ __forceinline__ void channel_reduce_pipe(int C, int64_t r0, int64_t r1, LD&& ld, ACC&& acc, F&& body,
+                                                    float* out0, float* out1) {
+  channel_reduce_tail<BT>(C, r0, r1, [&](int64_t r, int64_t step, int rpp, int ch, float(&s0)[8], float(&s1)[8]) {
+    const int64_t span = (int64_t)U * rpp;
+    R a, b;
+    if (r + (U - 1) * rpp < r1) {
+      ld(r * C + ch * 8, step, a);
+      for (;;) {
+        r += span;
+        if (r + (U - 1) * rpp >= r1) {
+          acc(a, s0, s1);
+          break;
+        }
+        ld(r * C + ch * 8, step, b);
+        acc(a, s0, s1);
+        r += span;
+        if (r + (U - 1) * rpp >= r1) {
+          acc(b, s0, s1);
+          break;
+        }
+        ld(r * C + ch * 8, step, a);
+        acc(b, s0, s1);
+      }
+    }
+    return r;
+  }, body, out0, out1);
+}
+
 // sums of (x - k) and (x - k)^2 with a per-channel pivot k = x[row 0] (the same for every block):
 // E[x^2] - m^2 on raw fp32 sums cancels catastrophically when |mean| >> std over millions of rows;
 // shifted by a value of the batch, the sums are O(R std^2) and the variance keeps its digits
-template <int UR, int BT>
+template <int U>
+struct XRows {
+  static constexpr int n = U;
+  bf16x8 v[U];
+};
+template <int U>
+struct DyXRows {
+  static constexpr int n = U;
+  bf16x8 g[U], x[U];
+  unsigned mk[U];
+};
+
+// PIPE: channel_reduce_pipe with two sets of UR / 2 rows (the same rows in flight per lane)
+template <int UR, int BT, bool PIPE = false>
 __global__ void __launch_bounds__(BT) stats_kernel(const bf16* __restrict__ x, int64_t R, int C, int64_t rows_per_block,
                                                    float* __restrict__ sum, float* __restrict__ sumsq) {
   const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(R, r0 + rows_per_block);
   float k[8];
   load8(x + (threadIdx.x % (C / 8)) * 8, k);
-  channel_reduce<UR, BT>(
-      C, r0, r1,
-      [&](int64_t off, int64_t step, auto u, float(&s0)[8], float(&s1)[8]) {
-        constexpr int U = decltype(u)::value;
-        bf16x8 raw[U];
+  auto ld = [&](int64_t off, int64_t step, auto& g) {
 #pragma unroll
-        for (int j = 0; j < U; ++j) raw[j] = *(const bf16x8*)(x + off + j * step);
+    for (int j = 0; j < g.n; ++j) g.v[j] = *(const bf16x8*)(x + off + j * step);
+  };
+  auto acc = [&](const auto& g, float(&s0)[8], float(&s1)[8]) {
 #pragma unroll
-        for (int j = 0; j < U; ++j)
+    for (int j = 0; j < g.n; ++j)
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float d = (float)raw[j][i] - k[i];
-            s0[i] += d;
-            s1[i] = fmaf(d, d, s1[i]);
-          }
-      },
-      sum, sumsq);
+      for (int i = 0; i < 8; ++i) {
+        const float d = (float)g.v[j][i] - k[i];
+        s0[i] += d;
+        s1[i] = fmaf(d, d, s1[i]);
+      }
+  };
+  auto body = [&](int64_t off, int64_t step, auto u, float(&s0)[8], float(&s1)[8]) {
+    XRows<decltype(u)::value> g;
+    ld(off, step, g);
+    acc(g, s0, s1);
+  };
+  if constexpr (PIPE)
+    channel_reduce_pipe<UR / 2, BT, XRows<UR / 2>>(C, r0, r1, ld, acc, body, sum, sumsq);
+  else
+    channel_reduce<UR, BT>(C, r0, r1, body, sum, sumsq);
 }
 
 // mean, 1/std, scale = gamma/std, shift = beta - mean * scale; running stats (unbiased variance)
@@ -246,7 +308,7 @@ __global__ void __launch_bounds__(NT) apply_kernel(const bf16* __restrict__ x, c
 }
 
 // backward reductions: sum dz and sum dz * xhat per channel, dz = dy [* mask]
-template <bool RELU, int UR, int BT>
+template <bool RELU, int UR, int BT, bool PIPE = false>
 __global__ void __launch_bounds__(BT) bwd_reduce_kernel(const bf16* __restrict__ dy, const unsigned char* __restrict__ mask,
                                                         const bf16* __restrict__ x, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, int64_t R, int C,
@@ -260,28 +322,33 @@ __global__ void __launch_bounds__(BT) bwd_reduce_kernel(const bf16* __restrict__
     m[i] = mean[ch + i];
     rs[i] = rstd[ch + i];
   }
-  channel_reduce<UR, BT>(
-      C, r0, r1,
-      [&](int64_t off, int64_t step, auto u, float(&s0)[8], float(&s1)[8]) {
-        constexpr int U = decltype(u)::value;
-        bf16x8 g[U], xx[U];
-        unsigned mk[U];
+  auto ld = [&](int64_t off, int64_t step, auto& g) {
 #pragma unroll
-        for (int j = 0; j < U; ++j) {
-          g[j] = *(const bf16x8*)(dy + off + j * step);
-          xx[j] = *(const bf16x8*)(x + off + j * step);
-          mk[j] = RELU ? mask[(off + j * step) >> 3] : 0xffu;
-        }
+    for (int j = 0; j < g.n; ++j) {
+      g.g[j] = *(const bf16x8*)(dy + off + j * step);
+      g.x[j] = *(const bf16x8*)(x + off + j * step);
+      g.mk[j] = RELU ? mask[(off + j * step) >> 3] : 0xffu;
+    }
+  };
+  auto acc = [&](const auto& g, float(&s0)[8], float(&s1)[8]) {
 #pragma unroll
-        for (int j = 0; j < U; ++j)
+    for (int j = 0; j < g.n; ++j)
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float dz = RELU ? ((mk[j] >> i) & 1u ? (float)g[j][i] : 0.f) : (float)g[j][i];
-            s0[i] += dz;
-            s1[i] = fmaf(dz, ((float)xx[j][i] - m[i]) * rs[i], s1[i]);
-          }
-      },
-      sdz, sdzx);
+      for (int i = 0; i < 8; ++i) {
+        const float dz = RELU ? ((g.mk[j] >> i) & 1u ? (float)g.g[j][i] : 0.f) : (float)g.g[j][i];
+        s0[i] += dz;
+        s1[i] = fmaf(dz, ((float)g.x[j][i] - m[i]) * rs[i], s1[i]);
+      }
+  };
+  auto body = [&](int64_t off, int64_t step, auto u, float(&s0)[8], float(&s1)[8]) {
+    DyXRows<decltype(u)::value> g;
+    ld(off, step, g);
+    acc(g, s0, s1);
+  };
+  if constexpr (PIPE)
+    channel_reduce_pipe<UR / 2, BT, DyXRows<UR / 2>>(C, r0, r1, ld, acc, body, sdz, sdzx);
+  else
+    channel_reduce<UR, BT>(C, r0, r1, body, sdz, sdzx);
 }
 
 // ws = [sum dz | sum dz xhat] -> sums (for the dx pass and the caller) and, when given, added into the
@@ -444,7 +511,12 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_kernel(const bf16* __restrict_
 }
 
 // reduction geometry (rows in flight per lane, target block count, minimum passes per block, threads per block).
-// Round 6 default "w512q": 8 deep, ~256 blocks of 512 threads -- a quarter of the blocks, so a quarter of the
+// Round 6 default "w512p": w512q's geometry on channel_reduce_pipe (the next 4 rows' loads issued before the current
+// 4 are summed): bwd_reduce 398.1 -> 383.6 us per set of shapes, the small late layers gaining, the 205 MB ones
+// (dy and x together likely past the 256 MB last-level cache) at ~4.5 TB/s either way; config 3 ahead in 6 of 6
+// interleaved pairs, +0.1..2.1 % (profiles/r6_bn_kernels.txt). "w512i" (the blocks sweeping the rows together,
+// grid-stride, instead of a contiguous range each) measured 4-8 % slower on the large shapes: not kept.
+// Before it, "w512q": 8 deep, ~256 blocks of 512 threads -- a quarter of the blocks, so a quarter of the
 // per-block atomics into the layer's sums, which cost the statistics pass a third of its time at 1024 blocks
 // (profiles/r6_bn_kernels.txt: stats 257.5 -> 200.0 us, reductions 420 -> 392 us per set of ResNet-50 shapes;
 // config 3 9306 / 9318 vs 9222 / 9164 img/s, same box, interleaved). Round 5, config 3
@@ -454,24 +526,27 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_kernel(const bf16* __restrict_
 // (every block adds its partial sums into the workspace) -- and "8h" (8 deep, ~512 blocks)
 struct ReduceGeo {
   int unroll, target, min_passes, threads = 256;
+  bool pipe = false;  // channel_reduce_pipe
 };
 inline const ReduceGeo& reduce_geo() {
   static const ReduceGeo g = [] {
     const char* e = std::getenv("VCX_BN_REDUCE");
-    const std::string v = e ? e : "w512q";
+    const std::string v = e ? e : "w512p";
     if (v == "8") return ReduceGeo{8, 2048, 16};
     if (v == "4") return ReduceGeo{4, 1024, 32};
     if (v == "4w") return ReduceGeo{4, 2048, 16};
     if (v == "8h") return ReduceGeo{8, 512, 32};
     if (v == "w512") return ReduceGeo{8, 512, 32, 512};
     if (v == "8n") return ReduceGeo{8, 1024, 32};
-    if (v != "w512q") std::fprintf(stderr, "[vcx] VCX_BN_REDUCE=%s unknown, using w512q\n", v.c_str());
-    return ReduceGeo{8, 256, 32, 512};
+    if (v == "w512q") return ReduceGeo{8, 256, 32, 512};
+    if (v != "w512p") std::fprintf(stderr, "[vcx] VCX_BN_REDUCE=%s unknown, using w512p\n", v.c_str());
+    return ReduceGeo{8, 256, 32, 512, true};
   }();
   return g;
 }
 inline int reduce_unroll() { return reduce_geo().unroll; }
 inline int reduce_threads() { return reduce_geo().threads; }
+inline bool reduce_pipe() { return reduce_geo().pipe; }
 inline int64_t rows_per_block(int64_t R, int C) {
   const ReduceGeo& geo = reduce_geo();
   const int64_t rpp = geo.threads / (C / 8), target = geo.target, min_passes = geo.min_passes;
@@ -503,7 +578,9 @@ void vcx_bn_fwd_train(const void* x, const void* res, void* y, void* mask, int64
   using namespace bn;
   const int64_t rpb = rows_per_block(R, C);
   const int nb = (int)((R + rpb - 1) / rpb);
-  if (reduce_threads() == 512)
+  if (reduce_pipe())
+    hipLaunchKernelGGL((stats_kernel<8, 512, true>), dim3(nb), dim3(512), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
+  else if (reduce_threads() == 512)
     hipLaunchKernelGGL((stats_kernel<8, 512>), dim3(nb), dim3(512), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
   else if (reduce_unroll() == 8)
     hipLaunchKernelGGL((stats_kernel<8, NT>), dim3(nb), dim3(NT), 0, s, (const bf16*)x, R, C, rpb, ws, ws + C);
@@ -573,7 +650,9 @@ void vcx_bn_bwd(const void* dy, const void* mask, const void* x, const float* me
     hipLaunchKernelGGL(kern, dim3(nb), dim3(bt), 0, s, (const bf16*)dy, (const unsigned char*)mask, (const bf16*)x, mean,
                        rstd, R, C, rpb, bws, bws + C);
   };
-  if (bt == 512)
+  if (reduce_pipe())
+    relu ? red(bwd_reduce_kernel<true, 8, 512, true>) : red(bwd_reduce_kernel<false, 8, 512, true>);
+  else if (bt == 512)
     relu ? red(bwd_reduce_kernel<true, 8, 512>) : red(bwd_reduce_kernel<false, 8, 512>);
   else if (reduce_unroll() == 8)
     relu ? red(bwd_reduce_kernel<true, 8, NT>) : red(bwd_reduce_kernel<false, 8, NT>);
