@@ -9,12 +9,18 @@ fused AdamW — runs in full):
   5: Llama-3-8B sharded-optimizer trainer + PowerSGD rank 4 (HBM sizing check on 288 GB)
 Prints one JSON line per config. Under a torchrun-style env (WORLD_SIZE > 1) config 5 runs one
 sharded peer per rank (ZeRO-1 over the group, PowerSGD-averaged gradients, parameter all-gather).
+On one process (no WORLD_SIZE > 1) several configs run one child process each, started before this
+parent touches the GPU: run in one process after config 3, config 4 measured 323-357 samples/s
+against 400-401 on its own (gpurun_out/c4ord*, profiles/r6_final_validation.txt), whatever config 3's
+convolution path -- a process-state interaction (allocator / library state left by the ResNet), not
+a property of config 4's step.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -128,12 +134,27 @@ def main():
     ap.add_argument("--llama-seq", type=int, default=2048)
     ap.add_argument("--llama-replicas", type=int, default=2, help="config 5 with several peers: shard replicas")
     a = ap.parse_args()
+    configs = a.configs.split(",")
+    if len(configs) > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        # one child per config; this parent never initialises the GPU (argv minus --configs)
+        rest, skip = [], False
+        for arg in sys.argv[1:]:
+            if skip:
+                skip = False
+            elif arg == "--configs":
+                skip = True
+            elif not arg.startswith("--configs="):
+                rest.append(arg)
+        rc = 0
+        for c in configs:
+            rc = max(rc, subprocess.run([sys.executable, os.path.abspath(__file__), "--configs", c] + rest).returncode)
+        return rc
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     fns = {"3": cfg3, "4": cfg4, "5": cfg5}
     rc = 0
-    for c in a.configs.split(","):
+    for c in configs:
         try:
             rec = fns[c](a, dev)
         except Exception as e:  # report and continue with the next config
