@@ -13,7 +13,7 @@ On one process (no WORLD_SIZE > 1) several configs run one child process each, s
 parent touches the GPU: run in one process after config 3, config 4 measured 323-357 samples/s
 against 400-401 on its own (gpurun_out/c4ord*, profiles/r6_final_validation.txt), whatever config 3's
 convolution path -- a process-state interaction (allocator / library state left by the ResNet), not
-a property of config 4's step.
+a property of config 4's step. BENCH_CONFIGS_INPROC=1 keeps them in one process.
 """
 from __future__ import annotations
 
@@ -42,6 +42,20 @@ def _time(step, warmup, steps):
     return (time.perf_counter() - t0) / steps, out
 
 
+def _graph(tr, x, y, a):
+    """hipGraph capture of the local step (bench.py's path: zero-grad + forward + backward + fused AdamW replayed
+    as one graph launch; the averaging round stays outside); eager steps if capture is refused."""
+    if a.no_graph:
+        return False
+    try:
+        tr.capture(x, y, warmup=3)
+        return True
+    except Exception as e:  # stay correct: eager steps instead
+        print(f"[bench_configs] hipGraph capture failed ({type(e).__name__}: {e}); running eager", file=sys.stderr)
+        tr.graph = None
+        return False
+
+
 def cfg3(a, dev):
     from distributedvolunteercomputing_amd.models.resnet import enable_conv_find, resnet50
     from distributedvolunteercomputing_amd.parallel.compression import TopKCompressor
@@ -54,6 +68,7 @@ def cfg3(a, dev):
     B = a.resnet_batch
     x = torch.randn(B, 3, 224, 224, device=dev).to(torch.bfloat16).to(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (B,), device=dev)
+    graphed = _graph(tr, x, y, a)
     dt, st = _time(lambda: tr.step(x, y), 4, a.steps)
     # cost of one compressed averaging round on its own (warmed up: the first call loads the
     # compression kernels' code objects; mean of 10 rounds)
@@ -66,7 +81,7 @@ def cfg3(a, dev):
     torch.cuda.synchronize()
     return {"config": 3, "model": "resnet50", "images_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 2),
             "batch": B, "topk_ratio": 0.01, "topk_round_ms": round((time.perf_counter() - t0) * 1e3 / 10, 3),
-            "params": tr.flat.numel}
+            "params": tr.flat.numel, "hipgraph": graphed}
 
 
 def cfg4(a, dev):
@@ -78,10 +93,12 @@ def cfg4(a, dev):
     tr = LocalSGDTrainer(m, LocalSGDConfig(H=4), device=dev)
     B, T = a.medium_batch, 1024
     x = torch.randint(0, cfg.vocab_size, (B, T + 1), device=dev)
-    dt, _ = _time(lambda: tr.step(x[:, :-1], x[:, 1:]), 4, a.steps)
+    xi, yi = x[:, :-1].contiguous(), x[:, 1:].contiguous()
+    graphed = _graph(tr, xi, yi, a)
+    dt, _ = _time(lambda: tr.step(xi, yi), 4, a.steps)
     return {"config": 4, "model": "gpt2-medium", "samples_per_s": round(B / dt, 2), "tokens_per_s": round(B * T / dt),
             "ms_per_step": round(dt * 1e3, 2), "batch": B, "mfu_bf16_dense": round(m.flops_per_token(T) * B * T / dt /
-                                                                                    2.5e15, 4)}
+                                                                                    2.5e15, 4), "hipgraph": graphed}
 
 
 def cfg5(a, dev):
@@ -123,6 +140,19 @@ def cfg5(a, dev):
             "mfu_bf16_dense": round(m.flops_per_token(T) * B * T / dt / 2.5e15, 4)}
 
 
+def child_argv(argv, config):
+    """argv for the child process of one config: the parent's arguments with --configs replaced."""
+    rest, skip = [], False
+    for arg in argv:
+        if skip:
+            skip = False
+        elif arg == "--configs":
+            skip = True
+        elif not arg.startswith("--configs="):
+            rest.append(arg)
+    return ["--configs", config] + rest
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="3,4,5")
@@ -132,22 +162,15 @@ def main():
     ap.add_argument("--llama", default="llama3-8b")
     ap.add_argument("--llama-batch", type=int, default=2)
     ap.add_argument("--llama-seq", type=int, default=2048)
+    ap.add_argument("--no-graph", action="store_true", help="configs 3 / 4: eager steps (no hipGraph capture)")
     ap.add_argument("--llama-replicas", type=int, default=2, help="config 5 with several peers: shard replicas")
     a = ap.parse_args()
     configs = a.configs.split(",")
-    if len(configs) > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
-        # one child per config; this parent never initialises the GPU (argv minus --configs)
-        rest, skip = [], False
-        for arg in sys.argv[1:]:
-            if skip:
-                skip = False
-            elif arg == "--configs":
-                skip = True
-            elif not arg.startswith("--configs="):
-                rest.append(arg)
+    if len(configs) > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1 and os.environ.get("BENCH_CONFIGS_INPROC") != "1":
+        # one child per config; this parent never initialises the GPU
         rc = 0
         for c in configs:
-            rc = max(rc, subprocess.run([sys.executable, os.path.abspath(__file__), "--configs", c] + rest).returncode)
+            rc = max(rc, subprocess.run([sys.executable, os.path.abspath(__file__)] + child_argv(sys.argv[1:], c)).returncode)
         return rc
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % torch.cuda.device_count())
