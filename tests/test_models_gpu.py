@@ -476,3 +476,47 @@ def test_fused_batchnorm_large_mean_variance(gpu):
     yd = (xd - mean[None, :, None, None]) / torch.sqrt(var_b[None, :, None, None] + bn.eps)
     yd = yd * bn.weight.double()[None, :, None, None] + bn.bias.double()[None, :, None, None]
     assert float((y.double() - yd).norm() / yd.norm()) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C", [(2, 3, 64), (3, 9, 128), (5, 11, 256), (7, 13, 64)])
+def test_fused_batchnorm_ragged_row_counts(gpu, N, H, C):
+    """The reductions' pipelined row loop (csrc/kernels/batchnorm.hip channel_reduce_pipe) at row counts that leave
+    no full group of rows, an odd number of groups, lanes diverging between a full group and the single-row
+    tail: output and gradients against torch's BatchNorm + ReLU in fp32."""
+    from distributedvolunteercomputing_amd.ops.batchnorm import bn_act
+
+    torch.manual_seed(N * H + C)
+    bn = torch.nn.BatchNorm2d(C).to(gpu)
+    torch.nn.init.uniform_(bn.weight, 0.5, 1.5)
+    torch.nn.init.uniform_(bn.bias, -0.5, 0.5)
+    bn32 = torch.nn.BatchNorm2d(C).to(gpu)
+    bn32.load_state_dict(bn.state_dict())
+    bn = bn.to(torch.bfloat16)
+    x = (torch.randn(N, C, H, H, device=gpu) + 0.3).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x.requires_grad_()
+    y = bn_act(x, bn, None, True)
+    assert type(y.grad_fn).__name__ == "_BNActBackward"
+    g = torch.randn_like(y)
+    y.backward(g)
+    x32 = x.detach().float().requires_grad_()
+    y32 = torch.relu(bn32(x32))
+    y32.backward(g.float())
+    # torch's own bf16 BatchNorm + ReLU sets the bar (a ReLU output's gradients: elements near 0 round to the
+    # other side of the mask, as in test_fused_batchnorm_act_vs_fp32)
+    bnt = torch.nn.BatchNorm2d(C).to(gpu)
+    bnt.load_state_dict(bn32.state_dict())
+    bnt = bnt.to(torch.bfloat16)
+    xt = x.detach().clone().requires_grad_()
+    with reference_ops():
+        yt = torch.relu(bnt(xt))
+        yt.backward(g)
+    rel = lambda a, b: float((a.float() - b).norm() / (b.norm() + 1e-6))  # noqa: E731
+
+    def ok(a, t, ref, tol):
+        e, et = rel(a, ref), rel(t, ref)
+        assert e < max(tol, 1.1 * et), (e, et)
+
+    ok(y, yt, y32, 1e-2)
+    ok(x.grad, xt.grad, x32.grad, 1e-2)
+    ok(bn.weight.grad, bnt.weight.grad, bn32.weight.grad, 1e-2)
+    ok(bn.bias.grad, bnt.bias.grad, bn32.bias.grad, 1e-2)
