@@ -293,6 +293,45 @@ at::Tensor maxpool3s2_bwd(at::Tensor dy, at::Tensor idx, int64_t H, int64_t W) {
   return dx;
 }
 
+static void nhwc_check(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.is_contiguous() && t.scalar_type() == at::kBFloat16 && t.size(3) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && t.numel() < (1ll << 40),
+              what, ": bf16 contiguous NHWC [N, H, W, C], C % 8 == 0, 16-B aligned");
+}
+
+// x [N, H, W, C] -> x[:, ::s, ::s, :] contiguous
+at::Tensor subsample_nhwc(at::Tensor x, int64_t s) {
+  nhwc_check(x, "subsample_nhwc");
+  TORCH_CHECK(s >= 1 && s <= 8, "subsample_nhwc: stride 1..8");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  at::Tensor y = at::empty({N, (H - 1) / s + 1, (W - 1) / s + 1, C}, x.options());
+  if (y.numel()) vcx_subsample_nhwc(x.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)s, cur_stream());
+  return y;
+}
+
+// full[:, ::s, ::s, :] += g, in place
+void subsample_add_nhwc(at::Tensor full, at::Tensor g, int64_t s) {
+  nhwc_check(full, "subsample_add_nhwc");
+  nhwc_check(g, "subsample_add_nhwc");
+  TORCH_CHECK(s >= 1 && s <= 8 && full.get_device() == g.get_device(), "subsample_add_nhwc: stride 1..8, one device");
+  const int64_t N = full.size(0), H = full.size(1), W = full.size(2), C = full.size(3);
+  TORCH_CHECK(g.size(0) == N && g.size(1) == (H - 1) / s + 1 && g.size(2) == (W - 1) / s + 1 && g.size(3) == C,
+              "subsample_add_nhwc: g must be [N, ceil(H / s), ceil(W / s), C]");
+  if (g.numel()) vcx_subsample_add_nhwc(full.data_ptr(), g.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)s, cur_stream());
+}
+
+// g [N, C] -> out [N, H, W, C] = g[:, None, None, :] * scale
+at::Tensor bcast_hw_nhwc(at::Tensor g, int64_t H, int64_t W, double scale) {
+  TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && g.scalar_type() == at::kBFloat16 && g.size(1) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0 && H >= 1 && W >= 1,
+              "bcast_hw_nhwc: g bf16 contiguous [N, C], C % 8 == 0");
+  const int64_t N = g.size(0), C = g.size(1);
+  TORCH_CHECK(N * H * W * C < (1ll << 40), "bcast_hw_nhwc: size");
+  at::Tensor out = at::empty({N, H, W, C}, g.options());
+  if (out.numel()) vcx_bcast_hw_nhwc(g.data_ptr(), out.data_ptr(), (int)N, (int)(H * W), (int)C, (float)scale, cur_stream());
+  return out;
+}
+
 at::Tensor bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor scale, at::Tensor shift, bool relu) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == at::kBFloat16, "bn: x bf16 contiguous NHWC");
   const int64_t C = x.size(-1), R = x.numel() / C;
@@ -966,6 +1005,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("c"), py::arg("c2") = py::none(),
         py::arg("bias") = py::none(), py::arg("colsum") = py::none(), py::arg("epi") = 0);
   m.def("transpose_bf16", &transpose_bf16, py::arg("src"), py::arg("dst") = py::none());
+  m.def("subsample_nhwc", &subsample_nhwc, py::arg("x"), py::arg("stride"));
+  m.def("subsample_add_nhwc", &subsample_add_nhwc, py::arg("full"), py::arg("g"), py::arg("stride"));
+  m.def("bcast_hw_nhwc", &bcast_hw_nhwc, py::arg("g"), py::arg("H"), py::arg("W"), py::arg("scale"));
   m.def("add_f32_into_bf16", &add_f32_into_bf16);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("ln_fwd", &ln_fwd);

@@ -512,6 +512,60 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_kernel(const bf16* __restrict_
   }
 }
 
+// ---- ResNet strided-shortcut and pooling helpers on NHWC bf16 (C % 8 == 0), one lane per 8 channels of one
+// pixel, 16-B accesses (torch's strided copy / add / broadcast for these ran at 1.4-2.3 TB/s in the config-3 step:
+// scripts/cfg3_copy_sources.py)
+// y[n, i, j] = x[n, i s, j s] (a stride-s 1x1 convolution's input)
+__global__ void __launch_bounds__(NT) subsample_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N, int H,
+                                                       int W, int C, int s, int OH, int OW) {
+  const int c8 = C / 8;
+  const int64_t total = (int64_t)N * OH * OW * c8;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int cc = (int)(t % c8);
+    const int64_t p = t / c8;  // output pixel
+    const int j = (int)(p % OW);
+    const int64_t q = p / OW;
+    const int i = (int)(q % OH), n = (int)(q / OH);
+    *(bf16x8*)(y + p * C + cc * 8) = *(const bf16x8*)(x + (((int64_t)n * H + i * s) * W + j * s) * C + cc * 8);
+  }
+}
+
+// full[n, i s, j s] += g[n, i, j] (the stride-s shortcut's input gradient into the block input's)
+__global__ void __launch_bounds__(NT) subsample_add_kernel(bf16* __restrict__ full, const bf16* __restrict__ g, int N,
+                                                           int H, int W, int C, int s, int OH, int OW) {
+  const int c8 = C / 8;
+  const int64_t total = (int64_t)N * OH * OW * c8;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int cc = (int)(t % c8);
+    const int64_t p = t / c8;
+    const int j = (int)(p % OW);
+    const int64_t q = p / OW;
+    const int i = (int)(q % OH), n = (int)(q / OH);
+    bf16* f = full + (((int64_t)n * H + i * s) * W + j * s) * C + cc * 8;
+    const bf16x8 a = *(const bf16x8*)f, b = *(const bf16x8*)(g + p * C + cc * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)a[e] + (float)b[e]);
+    *(bf16x8*)f = o;
+  }
+}
+
+// out[n, h, w, c] = g[n, c] * scale (the global average pool's backward)
+__global__ void __launch_bounds__(NT) bcast_hw_kernel(const bf16* __restrict__ g, bf16* __restrict__ out, int N, int HW,
+                                                      int C, float scale) {
+  const int c8 = C / 8;
+  const int64_t total = (int64_t)N * HW * c8;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int cc = (int)(t % c8);
+    const int n = (int)(t / ((int64_t)HW * c8));
+    const bf16x8 v = *(const bf16x8*)(g + (int64_t)n * C + cc * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)v[e] * scale);
+    *(bf16x8*)(out + t * 8) = o;
+  }
+}
+
 // reduction geometry (rows in flight per lane, target block count, minimum passes per block, threads per block).
 // Round 6 default "w512p": w512q's geometry on channel_reduce_pipe (the next 4 rows' loads issued before the current
 // 4 are summed): bwd_reduce 398.1 -> 383.6 us per set of shapes, the small late layers gaining, the 205 MB ones
@@ -680,6 +734,27 @@ void vcx_bn_bwd(const void* dy, const void* mask, const void* x, const float* me
     else
       relu ? go(bwd_dx_kernel<false, true, false>) : go(bwd_dx_kernel<false, false, false>);
   }
+}
+
+// y [N, OH, OW, C] = x[:, ::s, ::s, :]; full[:, ::s, ::s, :] += g; out [N, HW, C] = g [N, C] * scale (NHWC bf16)
+void vcx_subsample_nhwc(const void* x, void* y, int N, int H, int W, int C, int s, hipStream_t st) {
+  using namespace bn;
+  const int OH = (H - 1) / s + 1, OW = (W - 1) / s + 1;
+  hipLaunchKernelGGL(subsample_kernel, dim3(grid_for((int64_t)N * OH * OW * (C / 8))), dim3(NT), 0, st, (const bf16*)x,
+                     (bf16*)y, N, H, W, C, s, OH, OW);
+}
+
+void vcx_subsample_add_nhwc(void* full, const void* g, int N, int H, int W, int C, int s, hipStream_t st) {
+  using namespace bn;
+  const int OH = (H - 1) / s + 1, OW = (W - 1) / s + 1;
+  hipLaunchKernelGGL(subsample_add_kernel, dim3(grid_for((int64_t)N * OH * OW * (C / 8))), dim3(NT), 0, st, (bf16*)full,
+                     (const bf16*)g, N, H, W, C, s, OH, OW);
+}
+
+void vcx_bcast_hw_nhwc(const void* g, void* out, int N, int HW, int C, float scale, hipStream_t st) {
+  using namespace bn;
+  hipLaunchKernelGGL(bcast_hw_kernel, dim3(grid_for((int64_t)N * HW * (C / 8))), dim3(NT), 0, st, (const bf16*)g,
+                     (bf16*)out, N, HW, C, scale);
 }
 
 // stem max-pool 3x3 / stride 2 / pad 1, NHWC bf16 (C % 8 == 0): y, idx [N, OH, OW, C]

@@ -114,6 +114,9 @@ void vcx_bn_fwd_train(const void* x, const void* res, void* y, void* mask, int64
                       const void* beta, void* run_mean, void* run_var, int run_fp32, float eps, float momentum, float* ws,
                       float* mean, float* rstd, float* scale, float* shift, int64_t* nbt, int relu, int layer_ws,
                       hipStream_t s);
+void vcx_subsample_nhwc(const void* x, void* y, int N, int H, int W, int C, int s, hipStream_t st);
+void vcx_subsample_add_nhwc(void* full, const void* g, int N, int H, int W, int C, int s, hipStream_t st);
+void vcx_bcast_hw_nhwc(const void* g, void* out, int N, int HW, int C, float scale, hipStream_t st);
 void vcx_maxpool3s2_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int OH, int OW, hipStream_t s);
 void vcx_maxpool3s2_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C, int OH, int OW,
                         hipStream_t s);

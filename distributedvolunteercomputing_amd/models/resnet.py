@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import config
-from ..ops.batchnorm import bn_act, stem_maxpool
+from ..ops.batchnorm import bn_act, global_avgpool, stem_maxpool
 from ..ops.linear import GradJoin, residual_tap
 
 
@@ -222,7 +222,7 @@ class ResNet(nn.Module):
         x = bn_act(self.stem(x), self.bn)
         x = stem_maxpool(x)  # HIP on channels-last bf16 (ops/batchnorm.py)
         x = self.blocks(x)
-        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        x = global_avgpool(x)
         logits = self.fc(x)
         if y is None:
             return logits

@@ -338,7 +338,11 @@ class _SubsampleTap(torch.autograd.Function):
         ctx.join, ctx.s = join, s
         ctx.full = (x.shape[0], x.shape[2], x.shape[3], x.shape[1])  # N, H, W, C
         join.ran = False
-        return x.permute(0, 2, 3, 1)[:, ::s, ::s, :].contiguous()
+        xh = x.permute(0, 2, 3, 1)
+        ctx.hip = _nhwc_hip_ok(xh)
+        if ctx.hip:  # csrc/kernels/batchnorm.hip subsample_kernel: 16-B lanes (torch's strided copy: ~1.4 TB/s)
+            return native().subsample_nhwc(xh, s)
+        return xh[:, ::s, ::s, :].contiguous()
 
     @staticmethod
     def backward(ctx, g):
@@ -347,12 +351,22 @@ class _SubsampleTap(torch.autograd.Function):
         base = join.take()
         if base is not None and base.is_contiguous() and base.numel() == N * H * W * C:
             full = base.view(N, H, W, C)
-            full[:, ::s, ::s, :].add_(g)  # conv1's deposited input gradient: only the strided quarter moves
+            # conv1's deposited input gradient: only the strided quarter moves
+            if ctx.hip and g.is_contiguous() and _nhwc_hip_ok(g) and full.dtype == g.dtype:
+                native().subsample_add_nhwc(full, g, s)
+            else:
+                full[:, ::s, ::s, :].add_(g)
         else:
             join.ran = True
             full = g.new_zeros(N, H, W, C)
             full[:, ::s, ::s, :] = g
         return full.permute(0, 3, 1, 2), None, None
+
+
+def _nhwc_hip_ok(t: torch.Tensor) -> bool:
+    """A contiguous NHWC bf16 GPU tensor the strided-shortcut kernels take (C % 8 == 0, 16-B aligned)."""
+    return (use_native(t) and t.dtype == torch.bfloat16 and t.dim() == 4 and t.is_contiguous() and t.shape[3] % 8 == 0
+            and t.data_ptr() % 16 == 0)
 
 
 def subsample_tap(x: torch.Tensor, join: GradJoin, stride: int) -> torch.Tensor:

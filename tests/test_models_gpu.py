@@ -520,3 +520,56 @@ def test_fused_batchnorm_ragged_row_counts(gpu, N, H, C):
     ok(x.grad, xt.grad, x32.grad, 1e-2)
     ok(bn.weight.grad, bnt.weight.grad, bn32.weight.grad, 1e-2)
     ok(bn.bias.grad, bnt.bias.grad, bn32.bias.grad, 1e-2)
+
+
+@pytest.mark.parametrize("N,H,W,C,s", [(3, 56, 56, 256, 2), (2, 14, 14, 1024, 2), (2, 7, 9, 64, 2), (1, 5, 5, 8, 3)])
+def test_nhwc_subsample_kernels_vs_torch(gpu, N, H, W, C, s):
+    """The strided-shortcut helpers (csrc/kernels/batchnorm.hip): subsample_nhwc = x[:, ::s, ::s, :],
+    subsample_add_nhwc = full[:, ::s, ::s, :] += g (bit-exact: one bf16 add per element, as torch's), and
+    bcast_hw_nhwc = g[:, None, None, :] * scale."""
+    from distributedvolunteercomputing_amd.ops import native
+
+    C_ = native()
+    torch.manual_seed(N * H + C)
+    x = torch.randn(N, H, W, C, device=gpu).to(torch.bfloat16)
+    y = C_.subsample_nhwc(x, s)
+    assert torch.equal(y, x[:, ::s, ::s, :])
+    g = torch.randn_like(y)
+    full = x.clone()
+    ref = x.clone()
+    ref[:, ::s, ::s, :].add_(g)
+    C_.subsample_add_nhwc(full, g, s)
+    assert torch.equal(full, ref)
+    gg = torch.randn(N, C, device=gpu).to(torch.bfloat16)
+    out = C_.bcast_hw_nhwc(gg, H, W, 1.0 / (H * W))
+    refb = (gg.float() / (H * W))[:, None, None, :].expand(N, H, W, C)
+    assert (out.float() - refb).abs().max().item() <= 1e-2 * refb.abs().max().item()
+
+
+def test_global_avgpool_and_subsample_tap_grads(gpu):
+    """global_avgpool (HIP broadcast backward) and subsample_tap (HIP subsample forward, strided add backward into
+    the deposited conv1 gradient) against torch autograd on the same bf16 inputs."""
+    from distributedvolunteercomputing_amd.ops.batchnorm import global_avgpool
+    from distributedvolunteercomputing_amd.ops.linear import GradJoin, subsample_tap
+
+    torch.manual_seed(5)
+    x = torch.randn(4, 64, 7, 7, device=gpu).to(torch.bfloat16).to(memory_format=torch.channels_last).requires_grad_()
+    g = torch.randn(4, 64, device=gpu).to(torch.bfloat16)
+    global_avgpool(x).backward(g)
+    x2 = x.detach().clone().requires_grad_()
+    torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x2, 1), 1).backward(g)
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
+    assert (x.grad.float() - x2.grad.float()).abs().max().item() < 1e-3
+    # subsample_tap: the stride-2 shortcut's input gradient lands in the buffer conv1 deposited
+    xs = torch.randn(2, 32, 9, 11, device=gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    xs.requires_grad_()
+    join = GradJoin()
+    sub = subsample_tap(xs, join, 2)
+    assert torch.equal(sub, xs.detach().permute(0, 2, 3, 1)[:, ::2, ::2, :])
+    dep = torch.randn(2, 9, 11, 32, device=gpu).to(torch.bfloat16)
+    join.pending = dep.reshape(-1, 32).clone()
+    gs = torch.randn_like(sub)
+    sub.backward(gs)
+    ref = dep.clone()
+    ref[:, ::2, ::2, :] += gs
+    assert torch.equal(xs.grad.permute(0, 2, 3, 1), ref)
