@@ -528,11 +528,14 @@ at::Tensor transpose_bf16(at::Tensor src, c10::optional<at::Tensor> dst) {
   return out;
 }
 
-void add_f32_into_bf16(at::Tensor in, at::Tensor out, bool accumulate) {
+// out (bf16) (+)= in (fp32); zero_in: in is zeroed after the read (a zero-at-rest accumulation buffer)
+void add_f32_into_bf16(at::Tensor in, at::Tensor out, bool accumulate, bool zero_in) {
   TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kFloat && out.scalar_type() == at::kBFloat16 &&
-                  in.numel() == out.numel() && in.is_contiguous() && out.is_contiguous(),
-              "add_f32_into_bf16: fp32 in, bf16 out of equal size");
-  vcx_add_f32_into_bf16(in.data_ptr<float>(), out.data_ptr(), (int)in.numel(), accumulate ? 1 : 0, cur_stream());
+                  in.numel() == out.numel() && in.is_contiguous() && out.is_contiguous() &&
+                  in.get_device() == out.get_device() && in.numel() < (int64_t(1) << 31),
+              "add_f32_into_bf16: fp32 in, bf16 out of equal size on one device");
+  vcx_add_f32_into_bf16(in.data_ptr<float>(), out.data_ptr(), (int)in.numel(), accumulate ? 1 : 0, zero_in ? 1 : 0,
+                        cur_stream());
 }
 
 void reduce_bcast_bf16(at::Tensor in, c10::optional<at::Tensor> out, c10::optional<at::Tensor> mine, int64_t P) {
@@ -1008,7 +1011,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("subsample_nhwc", &subsample_nhwc, py::arg("x"), py::arg("stride"));
   m.def("subsample_add_nhwc", &subsample_add_nhwc, py::arg("full"), py::arg("g"), py::arg("stride"));
   m.def("bcast_hw_nhwc", &bcast_hw_nhwc, py::arg("g"), py::arg("H"), py::arg("W"), py::arg("scale"));
-  m.def("add_f32_into_bf16", &add_f32_into_bf16);
+  m.def("add_f32_into_bf16", &add_f32_into_bf16, py::arg("src"), py::arg("out"), py::arg("accumulate"),
+        py::arg("zero_src") = false);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("mean"),

@@ -370,11 +370,15 @@ __global__ void __launch_bounds__(256) transpose_bf16_v8_kernel(const bf16* __re
   }
 }
 
-// out_bf16[i] += (bf16) in_f32[i] (the epilogue's fp32 column sums into a flat .grad slot)
-__global__ void __launch_bounds__(256) add_f32_into_bf16_kernel(const float* __restrict__ in, bf16* __restrict__ out,
-                                                                int n, int accumulate) {
+// out_bf16[i] += (bf16) in_f32[i] (the epilogue's fp32 column sums into a flat .grad slot); zero_in: in[i] = 0
+// afterwards (a zero-at-rest column-sum buffer: no fill launch before the next GEMM adds into it)
+__global__ void __launch_bounds__(256) add_f32_into_bf16_kernel(float* __restrict__ in, bf16* __restrict__ out, int n,
+                                                                int accumulate, int zero_in) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) out[i] = (bf16)((accumulate ? (float)out[i] : 0.f) + in[i]);
+  if (i < n) {
+    out[i] = (bf16)((accumulate ? (float)out[i] : 0.f) + in[i]);
+    if (zero_in) in[i] = 0.f;
+  }
 }
 
 }  // namespace gemm
@@ -429,7 +433,7 @@ void vcx_transpose_bf16(const void* src, void* dst, int R, int Cc, hipStream_t s
                      (const bf16*)src, (bf16*)dst, R, Cc);
 }
 
-void vcx_add_f32_into_bf16(const float* in, void* out, int n, int accumulate, hipStream_t s) {
+void vcx_add_f32_into_bf16(float* in, void* out, int n, int accumulate, int zero_in, hipStream_t s) {
   hipLaunchKernelGGL(gemm::add_f32_into_bf16_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, (bf16*)out, n,
-                     accumulate);
+                     accumulate, zero_in);
 }

@@ -44,7 +44,7 @@ int vcx_gemm_ps_grid(int M, int N, int grid_cap);
 void vcx_gemm_ps(const void* A, const void* B, void* C, void* C2, const void* bias, float* colsum, int M, int N,
                  int K, int lda, int ldb, int ldc, int epi, int grid_cap, hipStream_t s);
 void vcx_transpose_bf16(const void* src, void* dst, int R, int Cc, hipStream_t s);
-void vcx_add_f32_into_bf16(const float* in, void* out, int n, int accumulate, hipStream_t s);
+void vcx_add_f32_into_bf16(float* in, void* out, int n, int accumulate, int zero_in, hipStream_t s);
 void vcx_reduce_bcast_bf16(const void* in, void* out, void* mine, int P, int64_t n, hipStream_t s);
 void vcx_splitk_reduce(const void* part, void* acc, int S, int64_t n, int accumulate, hipStream_t s);
 

@@ -526,7 +526,10 @@ class _MlpGelu(torch.autograd.Function):
         x2, w1, b1, w2, pre, act = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         M, F_ = pre.shape
-        cs = torch.zeros(F_, device=dy.device, dtype=torch.float32)
+        gb = grad_buffer(b1) if ctx.needs_input_grad[2] else None
+        # the bias gradient's fp32 column sums: a zero-at-rest buffer per (size, device, stream) that the add into
+        # the flat .grad zeroes again (no fill launch per layer), a fresh zero tensor when the sums are returned
+        cs = _colsum_buffer(F_, dy.device) if gb is not None else torch.zeros(F_, device=dy.device, dtype=torch.float32)
         dpre = torch.empty_like(pre)
         if ctx.ps:
             C.gemm_ps(dy2, transpose_weight(w2), dpre, pre, None, cs, 6 if ctx.grad_fwd else 4)
@@ -536,15 +539,27 @@ class _MlpGelu(torch.autograd.Function):
         dw1, _ = _param_grads(dpre, x2, w1, None, ctx.needs_input_grad[1], False)
         db1 = None
         if ctx.needs_input_grad[2]:
-            gb = grad_buffer(b1)
             if gb is not None:
-                C.add_f32_into_bf16(cs, gb, True)
+                C.add_f32_into_bf16(cs, gb, True, True)
             else:
                 db1 = cs.to(b1.dtype)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = (mm(dpre, w1) if ctx.ps else gemm_nt(dpre, transpose_weight(w1))).view(ctx.xshape)
         return dx, dw1, db1, dw2, None
+
+
+_COLSUM = {}
+
+
+def _colsum_buffer(n: int, device) -> torch.Tensor:
+    """Zero-at-rest fp32 [n] on `device` for the current stream: the GEMM epilogue adds column sums into it and
+    add_f32_into_bf16(..., zero_src=True) leaves it zeroed again (uses on one stream are ordered)."""
+    key = (n, device, torch.cuda.current_stream(device).cuda_stream)
+    buf = _COLSUM.get(key)
+    if buf is None:
+        buf = _COLSUM[key] = torch.zeros(n, device=device, dtype=torch.float32)
+    return buf
 
 
 def mlp_gelu_ok(x, w1, w2) -> bool:

@@ -1,4 +1,4 @@
-"""Where the config-3 step (ResNet-50 local-SGD + top-k EF, B=128) launches torch copies and elementwise kernels:
+"""Where the config-3 step (or, with argument gpt2, the bench.py GPT-2 step) (ResNet-50 local-SGD + top-k EF, B=128) launches torch copies and elementwise kernels:
 torch.profiler over one step, every aten copy / elementwise op with its input shapes, device time and the deepest
 stack frame inside this package. Diagnostic (prints a table)."""
 import collections
@@ -17,17 +17,26 @@ from distributedvolunteercomputing_amd.parallel.compression import TopKCompresso
 from distributedvolunteercomputing_amd.parallel.local_sgd import LocalSGDConfig, LocalSGDTrainer  # noqa: E402
 
 dev = torch.device("cuda", 0)
-m = resnet50().to(dev, torch.bfloat16).to(memory_format=torch.channels_last)
-enable_conv_find()
-tr = LocalSGDTrainer(m, LocalSGDConfig(H=4, lr=1e-3, weight_decay=0.0), device=dev)
-tr.compressor = TopKCompressor(tr.flat.numel, 0.01, dev)
-B = 128
-x = torch.randn(B, 3, 224, 224, device=dev).to(torch.bfloat16).to(memory_format=torch.channels_last)
-y = torch.randint(0, 1000, (B,), device=dev)
+if len(sys.argv) > 1 and sys.argv[1] == "gpt2":  # the bench.py step instead (GPT-2-small, 64 x 1024)
+    from distributedvolunteercomputing_amd.models.gpt2 import GPT2, GPT2Config
+
+    cfg = GPT2Config.preset("gpt2")
+    m = GPT2(cfg).to(dev, torch.bfloat16)
+    tr = LocalSGDTrainer(m, LocalSGDConfig(H=4), device=dev)
+    tok = torch.randint(0, cfg.vocab_size, (64, 1025), device=dev)
+    x, y = tok[:, :-1].contiguous(), tok[:, 1:].contiguous()
+else:
+    m = resnet50().to(dev, torch.bfloat16).to(memory_format=torch.channels_last)
+    enable_conv_find()
+    tr = LocalSGDTrainer(m, LocalSGDConfig(H=4, lr=1e-3, weight_decay=0.0), device=dev)
+    tr.compressor = TopKCompressor(tr.flat.numel, 0.01, dev)
+    B = 128
+    x = torch.randn(B, 3, 224, 224, device=dev).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (B,), device=dev)
 for _ in range(3):
     tr.step(x, y)
 torch.cuda.synchronize()
-WATCH = ("copy_", "contiguous", "clone", "add", "mul", "sub", "fill_", "zero_", "to", "cat", "div")
+WATCH = ("copy_", "contiguous", "clone", "add", "mul", "sub", "fill_", "zero", "to", "cat", "div", "empty", "full")
 with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True, with_stack=True) as prof:
     tr.step(x, y)
     torch.cuda.synchronize()

@@ -412,3 +412,27 @@ def test_mlp_gelu_persistent_matches_unfused(gpu, grad_fwd):
             outs[mode] = [t.float().clone() for t in (y, xi.grad, w1.grad, b1.grad, w2.grad)]
     for a, b in zip(outs["lib"], outs["fused"]):
         assert (a - b).norm() / b.norm() < 2e-2
+
+
+def test_mlp_gelu_bias_grad_into_flat_buffer_repeats(gpu):
+    """The fused MLP's fc bias gradient added into a preset .grad buffer (the flat-parameter path) through the
+    zero-at-rest column-sum buffer (ops/linear.py _colsum_buffer): three backwards accumulate 3x the gradient the
+    returned-tensor path gives once, and the buffer is left zeroed."""
+    import importlib
+
+    L = importlib.import_module("distributedvolunteercomputing_amd.ops.linear")  # the module, not ops.linear()
+    torch.manual_seed(3)
+    x = _bf(torch.randn(512, 768, device=gpu))
+    w1 = _bf(torch.randn(3072, 768, device=gpu) * 0.02).requires_grad_()
+    b1 = _bf(torch.randn(3072, device=gpu) * 0.02).requires_grad_()
+    w2 = _bf(torch.randn(768, 3072, device=gpu) * 0.02).requires_grad_()
+    dy = _bf(torch.randn(512, 768, device=gpu))
+    ops.mlp_gelu(x, w1, b1, w2).backward(dy)  # b1.grad None: the sums come back as a tensor
+    ref = b1.grad.float().clone()
+    b1.grad = torch.zeros_like(b1)  # a preset buffer: grad_buffer() path
+    for _ in range(3):
+        ops.mlp_gelu(x, w1, b1, w2).backward(dy)
+    torch.cuda.synchronize()
+    assert (b1.grad.float() - 3 * ref).norm() / (3 * ref).norm() < 2e-2
+    bufs = [v for k, v in L._COLSUM.items() if k[0] == 3072]
+    assert bufs and all(int(torch.count_nonzero(v)) == 0 for v in bufs)
