@@ -40,12 +40,21 @@ class _AddLN(torch.autograd.Function):
         ctx.has_bias = bias is not None
         ctx.has_bb = bb is not None
         ctx.rms = rms
+        # an unused residual output (the last block's) gets no zero-filled gradient: dx_res None -> no residual add
+        ctx.set_materialize_grads(False)
         if b is None:
             x = x.view_as(x)  # output aliases the input: hand autograd a view, not the input itself
         return y, x
 
     @staticmethod
     def backward(ctx, dy, dx_res):
+        if dy is None:  # only the residual output was used: it is a + b (+ bb)
+            if dx_res is None:
+                return None, None, None, None, None, None, None
+            dbb = None
+            if ctx.has_bb:
+                dbb = dx_res.reshape(-1, dx_res.shape[-1]).float().sum(0).to(dx_res.dtype)
+            return dx_res, (dx_res if ctx.has_b else None), None, None, None, None, dbb
         x, w, mean, rstd = ctx.saved_tensors
         C = native()
         dres = None if dx_res is None else dx_res.contiguous()

@@ -436,3 +436,30 @@ def test_mlp_gelu_bias_grad_into_flat_buffer_repeats(gpu):
     assert (b1.grad.float() - 3 * ref).norm() / (3 * ref).norm() < 2e-2
     bufs = [v for k, v in L._COLSUM.items() if k[0] == 3072]
     assert bufs and all(int(torch.count_nonzero(v)) == 0 for v in bufs)
+
+
+@pytest.mark.parametrize("use", ["y", "x"])
+def test_add_layernorm_one_output_unused(gpu, use):
+    """add_layernorm with only one of its outputs used (GPT-2's last block leaves the residual stream unused): no
+    zero-filled gradient is materialised for the other, and the gradients match fp32 (branch bias included)."""
+    torch.manual_seed(4)
+    R, C = 513, 768
+    a = _bf(torch.randn(R, C, device=gpu)).requires_grad_()
+    b = _bf(torch.randn(R, C, device=gpu)).requires_grad_()
+    w = _bf(torch.rand(C, device=gpu) + 0.5).requires_grad_()
+    bias = _bf(torch.randn(C, device=gpu) * 0.1).requires_grad_()
+    bb = _bf(torch.randn(C, device=gpu) * 0.1).requires_grad_()
+    y, x = ops.add_layernorm(a, b, w, bias, branch_bias=bb)
+    g = _bf(torch.randn(R, C, device=gpu)).float()
+    ((y if use == "y" else x).float() * g).sum().backward()
+    a32, b32, w32, bias32, bb32 = (t.detach().float().requires_grad_() for t in (a, b, w, bias, bb))
+    xr = a32 + b32 + bb32
+    yr = F.layer_norm(xr, (C,), w32, bias32, 1e-5)
+    ((yr if use == "y" else xr) * g).sum().backward()
+    assert torch.allclose(a.grad.float(), a32.grad, atol=5e-2, rtol=3e-2)
+    assert torch.allclose(b.grad.float(), b32.grad, atol=5e-2, rtol=3e-2)
+    assert (bb.grad.float() - bb32.grad).norm() / bb32.grad.norm() < 2e-2
+    if use == "y":
+        assert (w.grad.float() - w32.grad).norm() / w32.grad.norm() < 2e-2
+    else:
+        assert w.grad is None or float(w.grad.float().abs().max()) == 0.0
